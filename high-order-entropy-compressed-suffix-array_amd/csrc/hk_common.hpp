@@ -1,0 +1,172 @@
+// hk_common.hpp — shared definitions for the hkcsa HIP library (gfx950 only).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+namespace hk {
+
+constexpr int kWave = 64;  // CDNA wavefront width (hard-coded, see cdna_hip_programming.md §1)
+
+// ---------------------------------------------------------------- errors
+void set_error(const std::string& msg);
+
+struct HipError {
+  hipError_t code;
+  std::string where;
+};
+
+#define HK_HIP(call)                                                                        \
+  do {                                                                                      \
+    hipError_t e_ = (call);                                                                 \
+    if (e_ != hipSuccess) throw ::hk::HipError{e_, std::string(#call) + " @" __FILE__ ":" + \
+                                                      std::to_string(__LINE__)};            \
+  } while (0)
+
+struct ApiError {
+  int code;
+  std::string msg;
+};
+
+// ------------------------------------------------------- device helpers
+__device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
+
+// popcount of `m` restricted to lanes below the calling lane
+__device__ __forceinline__ uint32_t mbcnt(uint64_t m) {
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+__device__ __forceinline__ uint64_t ballot64(bool p) { return __ballot(p); }
+
+template <typename T>
+__device__ __forceinline__ T wave_incl_sum(T v) {
+  const uint32_t l = lane_id();
+#pragma unroll
+  for (int o = 1; o < kWave; o <<= 1) {
+    T t = __shfl_up(v, o, kWave);
+    if (l >= (uint32_t)o) v += t;
+  }
+  return v;
+}
+
+template <typename T>
+__device__ __forceinline__ T wave_incl_max(T v) {
+  const uint32_t l = lane_id();
+#pragma unroll
+  for (int o = 1; o < kWave; o <<= 1) {
+    T t = __shfl_up(v, o, kWave);
+    if (l >= (uint32_t)o) v = v > t ? v : t;
+  }
+  return v;
+}
+
+template <typename T>
+__device__ __forceinline__ T wave_sum(T v) {
+#pragma unroll
+  for (int o = kWave / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
+  return v;
+}
+
+// Relaxed agent-scope 8-byte accesses (sc1; L1 bypass) for lookback granules.
+__device__ __forceinline__ uint64_t ld_agent(const uint64_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_agent(uint64_t* p, uint64_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+inline uint64_t ceil_div(uint64_t a, uint64_t b) { return (a + b - 1) / b; }
+
+// ------------------------------------------------------ device buffers
+struct DevBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+  DevBuf() = default;
+  DevBuf(const DevBuf&) = delete;
+  DevBuf& operator=(const DevBuf&) = delete;
+  DevBuf(DevBuf&& o) noexcept : p(o.p), bytes(o.bytes) { o.p = nullptr; o.bytes = 0; }
+  DevBuf& operator=(DevBuf&& o) noexcept {
+    if (this != &o) { release(); p = o.p; bytes = o.bytes; o.p = nullptr; o.bytes = 0; }
+    return *this;
+  }
+  ~DevBuf() { release(); }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    bytes = 0;
+  }
+  // grow-only allocation (contents not preserved)
+  void ensure(size_t nbytes) {
+    if (nbytes <= bytes && p) return;
+    release();
+    size_t b = nbytes ? nbytes : 16;
+    hipError_t e = hipMalloc(&p, b);
+    if (e != hipSuccess) {
+      p = nullptr;
+      (void)hipGetLastError();
+      throw ApiError{-5, "hipMalloc of " + std::to_string(b) + " bytes failed"};
+    }
+    bytes = b;
+  }
+  template <typename T> T* as() const { return static_cast<T*>(p); }
+};
+
+// ----------------------------------------------------- timing registry
+struct KernelTimer {
+  struct Pending { std::string name; hipEvent_t a, b; double bytes; };
+  struct Stat { uint64_t launches = 0; double ms = 0, bytes = 0; };
+  bool enabled = false;
+  std::vector<Pending> pending;
+  std::vector<std::pair<std::string, Stat>> stats;
+  hipStream_t stream = nullptr;
+
+  Stat& stat(const std::string& n) {
+    for (auto& s : stats) if (s.first == n) return s.second;
+    stats.emplace_back(n, Stat{});
+    return stats.back().second;
+  }
+  // returns the event to record after the launch (or nullptr when disabled)
+  hipEvent_t begin(const std::string& name, double bytes) {
+    if (!enabled) return nullptr;
+    Pending pd{name, nullptr, nullptr, bytes};
+    HK_HIP(hipEventCreate(&pd.a));
+    HK_HIP(hipEventCreate(&pd.b));
+    HK_HIP(hipEventRecord(pd.a, stream));
+    pending.push_back(pd);
+    return pd.b;
+  }
+  void end(hipEvent_t ev) {
+    if (ev) HK_HIP(hipEventRecord(ev, stream));
+  }
+  void resolve() {
+    for (auto& pd : pending) {
+      HK_HIP(hipEventSynchronize(pd.b));
+      float ms = 0;
+      HK_HIP(hipEventElapsedTime(&ms, pd.a, pd.b));
+      Stat& s = stat(pd.name);
+      s.launches++;
+      s.ms += ms;
+      s.bytes += pd.bytes;
+      (void)hipEventDestroy(pd.a);
+      (void)hipEventDestroy(pd.b);
+    }
+    pending.clear();
+  }
+  void reset() { resolve(); stats.clear(); }
+  ~KernelTimer() {
+    for (auto& pd : pending) { (void)hipEventDestroy(pd.a); (void)hipEventDestroy(pd.b); }
+  }
+};
+
+// RAII scope that brackets one launch with timing events
+struct TimedLaunch {
+  KernelTimer& t;
+  hipEvent_t ev;
+  TimedLaunch(KernelTimer& tm, const char* name, double bytes) : t(tm), ev(tm.begin(name, bytes)) {}
+  ~TimedLaunch() { if (ev) (void)hipEventRecord(ev, t.stream); }
+};
+
+}  // namespace hk

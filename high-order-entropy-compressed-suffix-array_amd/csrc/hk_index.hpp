@@ -1,0 +1,108 @@
+// hk_index.hpp — the opaque hkcsa_index handle and the per-module drivers.
+#pragma once
+
+#include <cstring>
+
+#include "hk_sort.hpp"
+
+namespace hk {
+
+constexpr int kMaxLevels = 8;
+constexpr int kLineBits = 448;   // 7 data words per 64-B rank line (word 0 = ones before the line)
+
+struct WtTables {                // per level, per dense code (host mirror of the device tables)
+  uint8_t bit[kMaxLevels][256];
+  uint64_t start[kMaxLevels][256];
+  uint64_t zeros[kMaxLevels][256];
+  uint8_t depth[256];
+};
+
+// kernel argument bundle for rank walks
+struct WtView {
+  const uint64_t* lines[kMaxLevels];
+  const uint64_t* obn;     // [L][256]  ones before the code's node at level d
+  const uint64_t* rbase;   // [L][256]  right-child base: start + zeros - obn
+  const uint8_t* bit;      // [L][256]
+  const uint8_t* depth;    // [256]
+  const int16_t* code;     // [256] byte -> dense code, -1 when absent
+  const uint64_t* Ccode;   // [257]
+  int levels;
+  int sigma;
+  uint64_t n;
+};
+
+struct Index {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  uint64_t n = 0;
+  DevBuf text;                 // T' (n bytes + 64 pad)
+
+  // alphabet
+  bool have_alpha = false;
+  uint64_t byte_hist[256] = {0};
+  int sigma = 0;
+  uint8_t syms[256] = {0};
+  int16_t code_of[256];
+  uint64_t Cbyte[257] = {0};
+  uint64_t Ccode[257] = {0};
+
+  // products
+  bool have_sa = false, have_bwt = false, have_wt = false;
+  DevBuf sa;                   // u32[n]
+  DevBuf bwt;                  // u8[n]
+  int wt_levels = 0;
+  DevBuf wt_lines[kMaxLevels];
+  uint64_t wt_nlines = 0;
+  DevBuf wt_obn, wt_rbase, wt_bit, wt_depth, wt_code, wt_C;
+  WtTables tabs;
+
+  // construction workspace (kept across builds so repeated builds do not allocate)
+  SortWork sw;
+  DevBuf keys[2], vals[2];
+  DevBuf isa;
+  DevBuf act[2][3];            // P, J, G of the active list (double-buffered)
+  DevBuf tile_a, tile_b, tile_c, tile_d;
+  DevBuf small;                // scratch for totals etc.
+  DevBuf seq[2];               // WT level code sequences
+
+  // sharded construction
+  bool sharded = false;
+  bool sa_pos64 = false;       // sharded slices of texts with n >= 2^32 hold u64 positions
+  uint64_t shard_lo = 0, shard_hi = 0;
+
+  KernelTimer timer;
+  std::vector<uint64_t> info;  // build counters (see hkcsa_build_info)
+
+  WtView view() const;
+};
+
+void compute_alphabet(Index& ix);
+void build_sa(Index& ix);
+void build_bwt(Index& ix);
+void bwt_gather64(Index& ix, const uint64_t* d_sa);   // BWT over a caller SA (u64)
+void build_wt(Index& ix);
+void release_workspace(Index& ix);
+void synth_text(uint8_t* d_text, uint64_t n, const uint8_t* alphabet, int sigma, uint64_t seed,
+                uint8_t terminator, hipStream_t s);
+
+// queries (device-resident inputs and outputs)
+void query_count(Index& ix, const uint8_t* d_pats, const uint64_t* d_offs, uint64_t P,
+                 int64_t* d_lr, uint64_t* d_cnt);
+void query_locate_gather(Index& ix, const int64_t* d_lr, const uint64_t* d_occ_offs, uint64_t P,
+                         uint64_t* d_pos);
+void query_rank(Index& ix, const uint8_t* d_c, const uint64_t* d_i, uint64_t k, uint64_t* d_out);
+void wt_level_words(Index& ix, int depth, uint64_t* d_words);
+
+// sharded SA (RCCL)
+int shard_buckets();
+void shard_histogram(Index& ix, int nranks, int rank, uint64_t* d_hist);
+void shard_build(Index& ix, const uint64_t* h_global_hist, int nranks, int rank);
+void shard_get_sa(Index& ix, uint64_t a, uint64_t b, uint64_t* out);
+void build_sa_sharded(Index& ix, const uint8_t id[128], int nranks, int rank);
+void comm_unique_id(uint8_t id[128]);
+
+// shared with the SA code: pack q symbols of b bits each into a key
+void pack_keys(const uint8_t* d_text, uint64_t n, uint64_t lo, uint64_t count, const uint8_t* d_lut,
+               int b, int q, uint64_t* d_keys, hipStream_t s);
+
+}  // namespace hk

@@ -1,0 +1,489 @@
+// hk_sort.hip — scans and the onesweep LSD radix sort (gfx950).
+//
+// The radix pass is the roofline kernel of the suffix-array build (SURVEY.md §8d:
+// algorithmic bytes 2*N*(K+V) per 8-bit pass).  One launch per digit:
+//   * every workgroup takes a tile id from an atomic counter (so all lower tiles have
+//     started: the lookback below always makes progress),
+//   * ranks its 8192 keys with wave64 ballot multisplit (8 ballots per item, a per-wave
+//     LDS histogram carries counts across the wave's 16 items, stable order),
+//   * publishes its 256 digit counts as 8-byte {epoch|flag|count} granules written and
+//     polled with relaxed agent-scope (sc1) accesses — the granule IS the flag, so no
+//     fences are needed (MI355X_MICROARCH.md §visibility, R2 granules),
+//   * looks back over predecessor tiles for its exclusive digit prefix (decoupled lookback),
+//   * stages keys then values through LDS in sorted order and writes them out so that
+//     consecutive lanes write consecutive addresses of one digit run.
+// Digit offsets come from one upfront histogram kernel over all digit positions.
+
+#include "hk_sort.hpp"
+
+namespace hk {
+
+// =============================================================== scans
+namespace {
+
+constexpr int SC_T = 256;
+constexpr int SC_I = 16;
+constexpr int SC_TILE = SC_T * SC_I;
+
+struct OpSum {
+  static __device__ __forceinline__ uint64_t id() { return 0; }
+  static __device__ __forceinline__ uint64_t f(uint64_t a, uint64_t b) { return a + b; }
+};
+struct OpMax {
+  static __device__ __forceinline__ uint64_t id() { return 0; }
+  static __device__ __forceinline__ uint64_t f(uint64_t a, uint64_t b) { return a > b ? a : b; }
+};
+
+template <typename Op>
+__device__ __forceinline__ uint64_t block_reduce(uint64_t v, uint64_t* red) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = Op::f(v, __shfl_xor(v, o, 64));
+  if (lane == 0) red[w] = v;
+  __syncthreads();
+  uint64_t r = Op::id();
+  for (int i = 0; i < SC_T / 64; ++i) r = Op::f(r, red[i]);
+  return r;
+}
+
+// exclusive block scan of one value per thread; returns exclusive prefix, *total = block total
+template <typename Op>
+__device__ __forceinline__ uint64_t block_excl_scan(uint64_t v, uint64_t* red, uint64_t* total) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint64_t inc = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    uint64_t t = __shfl_up(inc, o, 64);
+    if (lane >= o) inc = Op::f(inc, t);
+  }
+  if (lane == 63) red[w] = inc;
+  __syncthreads();
+  uint64_t carry = Op::id(), tot = Op::id();
+  for (int i = 0; i < SC_T / 64; ++i) {
+    if (i < w) carry = Op::f(carry, red[i]);
+    tot = Op::f(tot, red[i]);
+  }
+  uint64_t exc = __shfl_up(inc, 1, 64);
+  if (lane == 0) exc = Op::id();
+  *total = tot;
+  return Op::f(carry, exc);
+}
+
+template <typename Tin, typename Op>
+__global__ __launch_bounds__(SC_T) void k_scan_reduce(const Tin* __restrict__ in, uint64_t n,
+                                                      uint64_t* __restrict__ part) {
+  __shared__ uint64_t red[SC_T / 64];
+  const uint64_t base = (uint64_t)blockIdx.x * SC_TILE;
+  uint64_t acc = Op::id();
+#pragma unroll
+  for (int i = 0; i < SC_I; ++i) {
+    uint64_t j = base + (uint64_t)i * SC_T + threadIdx.x;
+    if (j < n) acc = Op::f(acc, (uint64_t)in[j]);
+  }
+  uint64_t r = block_reduce<Op>(acc, red);
+  if (threadIdx.x == 0) part[blockIdx.x] = r;
+}
+
+template <typename Tin, typename Op>
+__global__ __launch_bounds__(SC_T) void k_scan_down(const Tin* in, uint64_t* out, uint64_t n,
+                                                    const uint64_t* __restrict__ part_excl,
+                                                    int write_total) {
+  __shared__ uint64_t tile[SC_TILE];
+  __shared__ uint64_t red[SC_T / 64];
+  const uint64_t base = (uint64_t)blockIdx.x * SC_TILE;
+  const uint64_t carry_in = part_excl ? part_excl[blockIdx.x] : Op::id();
+#pragma unroll
+  for (int i = 0; i < SC_I; ++i) {
+    uint64_t j = base + (uint64_t)i * SC_T + threadIdx.x;
+    tile[i * SC_T + threadIdx.x] = j < n ? (uint64_t)in[j] : Op::id();
+  }
+  __syncthreads();
+  uint64_t loc[SC_I];
+  uint64_t run = Op::id();
+#pragma unroll
+  for (int i = 0; i < SC_I; ++i) {
+    loc[i] = run;
+    run = Op::f(run, tile[threadIdx.x * SC_I + i]);
+  }
+  uint64_t total;
+  uint64_t pre = block_excl_scan<Op>(run, red, &total);
+  pre = Op::f(carry_in, pre);
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < SC_I; ++i) tile[threadIdx.x * SC_I + i] = Op::f(pre, loc[i]);
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < SC_I; ++i) {
+    uint64_t j = base + (uint64_t)i * SC_T + threadIdx.x;
+    if (j < n) out[j] = tile[i * SC_T + threadIdx.x];
+  }
+  if (write_total && blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) out[n] = Op::f(carry_in, total);
+}
+
+template <typename Tin, typename Op>
+void scan_impl(uint64_t* scratch, const Tin* in, uint64_t* out, uint64_t n, bool write_total,
+               hipStream_t s) {
+  if (n == 0) {
+    if (write_total) HK_HIP(hipMemsetAsync(out, 0, sizeof(uint64_t), s));
+    return;
+  }
+  const uint64_t nb = ceil_div(n, SC_TILE);
+  uint64_t* part = nullptr;
+  if (nb > 1) {
+    part = scratch;
+    k_scan_reduce<Tin, Op><<<(unsigned)nb, SC_T, 0, s>>>(in, n, part);
+    HK_HIP(hipGetLastError());
+    scan_impl<uint64_t, Op>(scratch + nb + 1, part, part, nb, false, s);
+  }
+  k_scan_down<Tin, Op><<<(unsigned)nb, SC_T, 0, s>>>(in, out, n, part, write_total ? 1 : 0);
+  HK_HIP(hipGetLastError());
+}
+
+uint64_t scan_scratch_words(uint64_t n) {
+  uint64_t w = 16;
+  while (n > SC_TILE) {
+    n = ceil_div(n, SC_TILE);
+    w += n + 1;
+  }
+  return w;
+}
+
+}  // namespace
+
+void scan_exclusive_u64(SortWork& w, const uint64_t* in, uint64_t* out, uint64_t count,
+                        bool write_total, hipStream_t s) {
+  w.scan_tmp.ensure(scan_scratch_words(count) * 8);
+  scan_impl<uint64_t, OpSum>(w.scan_tmp.as<uint64_t>(), in, out, count, write_total, s);
+}
+void scan_exclusive_u32_to_u64(SortWork& w, const uint32_t* in, uint64_t* out, uint64_t count,
+                               bool write_total, hipStream_t s) {
+  w.scan_tmp.ensure(scan_scratch_words(count) * 8);
+  scan_impl<uint32_t, OpSum>(w.scan_tmp.as<uint64_t>(), in, out, count, write_total, s);
+}
+void scan_exclusive_max_u64(SortWork& w, const uint64_t* in, uint64_t* out, uint64_t count,
+                            hipStream_t s) {
+  w.scan_tmp.ensure(scan_scratch_words(count) * 8);
+  scan_impl<uint64_t, OpMax>(w.scan_tmp.as<uint64_t>(), in, out, count, false, s);
+}
+
+// ========================================================== radix sort
+namespace {
+
+constexpr int HG_T = 512;
+constexpr int HG_PER_BLOCK = HG_T * 16;
+
+// digit histograms for `np` consecutive 8-bit digits starting at bit `lo`
+__global__ __launch_bounds__(HG_T) void k_digit_hist(const uint64_t* __restrict__ keys, uint64_t n,
+                                                     int lo, int np,
+                                                     unsigned long long* __restrict__ hist) {
+  __shared__ uint32_t h[8][256];
+  for (int i = threadIdx.x; i < 8 * 256; i += HG_T) (&h[0][0])[i] = 0;
+  __syncthreads();
+  const uint64_t stride = (uint64_t)gridDim.x * HG_T * 2;
+  for (uint64_t j = ((uint64_t)blockIdx.x * HG_T + threadIdx.x) * 2; j < n; j += stride) {
+    uint64_t a, b;
+    bool two = j + 1 < n;
+    if (two) {
+      const ulonglong2 kk = *reinterpret_cast<const ulonglong2*>(keys + j);
+      a = kk.x;
+      b = kk.y;
+    } else {
+      a = keys[j];
+      b = 0;
+    }
+    for (int p = 0; p < np; ++p) {
+      const int sh = lo + 8 * p;
+      atomicAdd(&h[p][(a >> sh) & 255], 1u);
+      if (two) atomicAdd(&h[p][(b >> sh) & 255], 1u);
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < np * 256; i += HG_T) {
+    uint32_t c = (&h[0][0])[i];
+    if (c) atomicAdd(&hist[i], (unsigned long long)c);
+  }
+}
+
+// exclusive scan of each 256-bin histogram: one wave... one block of 256 threads per digit
+__global__ __launch_bounds__(256) void k_hist_offsets(const uint64_t* __restrict__ hist,
+                                                      uint64_t* __restrict__ offs) {
+  __shared__ uint64_t red[4];
+  const int p = blockIdx.x, d = threadIdx.x;
+  const uint64_t v = hist[p * 256 + d];
+  const int lane = d & 63, w = d >> 6;
+  uint64_t inc = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    uint64_t t = __shfl_up(inc, o, 64);
+    if (lane >= o) inc += t;
+  }
+  if (lane == 63) red[w] = inc;
+  __syncthreads();
+  uint64_t carry = 0;
+  for (int i = 0; i < w; ++i) carry += red[i];
+  offs[p * 256 + d] = carry + inc - v;
+}
+
+constexpr int OS_T = 512;
+constexpr int OS_I = 16;
+constexpr int OS_W = OS_T / 64;
+constexpr int OS_TILE = OS_T * OS_I;   // 8192 pairs per tile
+constexpr int OS_WSPAN = OS_I * 64;    // 1024 consecutive pairs per wave
+constexpr uint64_t ST_VAL_MASK = (1ull << 46) - 1;
+constexpr uint64_t ST_AGG = 1, ST_INC = 2;
+constexpr uint32_t SPIN_LIMIT = 1u << 22;
+
+__device__ __forceinline__ uint64_t st_pack(uint32_t epoch, uint64_t flag, uint64_t v) {
+  return ((uint64_t)epoch << 48) | (flag << 46) | v;
+}
+
+template <typename V>
+struct OsShared {
+  union {
+    uint64_t keys[OS_TILE];
+    V vals[OS_TILE];
+  } stage;
+  uint32_t whist[OS_W][256];   // per-wave digit counts, then per-wave exclusive prefix
+  uint32_t tstart[256];        // tile-local exclusive digit start
+  uint64_t gbase[256];         // global destination base minus tstart
+  uint32_t wsum[4];
+  uint32_t tile;
+};
+
+template <typename V>
+__global__ __launch_bounds__(OS_T, 4) void k_onesweep(
+    const uint64_t* __restrict__ kin, const V* __restrict__ vin, uint64_t* __restrict__ kout,
+    V* __restrict__ vout, uint64_t n, uint32_t shift, const uint64_t* __restrict__ goff,
+    uint64_t* status, uint32_t* tile_counter, uint32_t epoch, uint32_t* err, int iota) {
+  __shared__ OsShared<V> sh;
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+
+  for (uint32_t i = tid; i < OS_W * 256; i += OS_T) (&sh.whist[0][0])[i] = 0;
+  if (tid == 0) sh.tile = atomicAdd(tile_counter, 1u);
+  __syncthreads();
+  const uint32_t tile = sh.tile;
+  const uint64_t tbase = (uint64_t)tile * OS_TILE;
+  const uint64_t wbase = tbase + (uint64_t)wv * OS_WSPAN;
+
+  uint64_t key[OS_I];
+#pragma unroll
+  for (int k = 0; k < OS_I; ++k) {
+    const uint64_t j = wbase + (uint64_t)k * 64 + lane;
+    key[k] = j < n ? kin[j] : ~0ull;
+  }
+
+  // ---- rank within the wave (stable: item-major, then lane)
+  uint32_t rk[OS_I];
+#pragma unroll
+  for (int k = 0; k < OS_I; ++k) {
+    const uint64_t j = wbase + (uint64_t)k * 64 + lane;
+    const bool valid = j < n;
+    const uint32_t d = (uint32_t)(key[k] >> shift) & 255u;
+    uint64_t m = ballot64(valid);
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+      const bool bit = (d >> b) & 1u;
+      const uint64_t bb = ballot64(bit);
+      m &= bit ? bb : ~bb;
+    }
+    const uint32_t below = mbcnt(m);
+    const uint32_t prior = sh.whist[wv][d];
+    if (valid && below == 0) sh.whist[wv][d] = prior + (uint32_t)__popcll(m);
+    rk[k] = ((prior + below) & 0xFFFFu) | (d << 16);
+  }
+  __syncthreads();
+
+  // ---- per-digit tile count, per-wave exclusive prefix, tile-local digit starts
+  uint32_t tcount = 0;
+  if (tid < 256) {
+    uint32_t run = 0;
+#pragma unroll
+    for (int w = 0; w < OS_W; ++w) {
+      const uint32_t c = sh.whist[w][tid];
+      sh.whist[w][tid] = run;
+      run += c;
+    }
+    tcount = run;
+    uint32_t inc = run;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      uint32_t t = __shfl_up(inc, o, 64);
+      if (lane >= (uint32_t)o) inc += t;
+    }
+    if (lane == 63) sh.wsum[wv] = inc;
+    sh.tstart[tid] = inc - run;  // wave-local exclusive, fixed below
+  }
+  __syncthreads();
+  if (tid < 256) {
+    uint32_t carry = 0;
+    for (uint32_t w = 0; w < wv; ++w) carry += sh.wsum[w];
+    sh.tstart[tid] += carry;
+
+    // ---- publish and look back
+    const uint32_t d = tid;
+    uint64_t* my = status + (uint64_t)tile * 256 + d;
+    uint64_t excl = 0;
+    if (tile == 0) {
+      st_agent(my, st_pack(epoch, ST_INC, tcount));
+    } else {
+      st_agent(my, st_pack(epoch, ST_AGG, tcount));
+      int64_t t = (int64_t)tile - 1;
+      uint32_t spins = 0;
+      while (t >= 0) {
+        const uint64_t s = ld_agent(status + (uint64_t)t * 256 + d);
+        const uint64_t flag = (s >> 46) & 3u;
+        if ((uint32_t)(s >> 48) != epoch || flag == 0) {
+          if (++spins > SPIN_LIMIT) {
+            atomicOr(err, 1u);
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+          continue;
+        }
+        excl += s & ST_VAL_MASK;
+        if (flag == ST_INC) break;
+        --t;
+      }
+      st_agent(my, st_pack(epoch, ST_INC, excl + tcount));
+    }
+    sh.gbase[d] = goff[d] + excl - sh.tstart[d];
+  }
+  __syncthreads();
+
+  // ---- keys: stage in sorted order, write out in runs (rk becomes the tile-local rank)
+#pragma unroll
+  for (int k = 0; k < OS_I; ++k) {
+    const uint64_t j = wbase + (uint64_t)k * 64 + lane;
+    const uint32_t d = rk[k] >> 16;
+    rk[k] = sh.tstart[d] + sh.whist[wv][d] + (rk[k] & 0xFFFFu);
+    if (j < n) sh.stage.keys[rk[k]] = key[k];
+  }
+  __syncthreads();
+  const uint32_t tile_n = (uint32_t)((n - tbase) < (uint64_t)OS_TILE ? (n - tbase) : OS_TILE);
+  uint32_t dg[OS_I / 4] = {0, 0, 0, 0};   // digits of the staged slots, 4 per register
+#pragma unroll
+  for (int i = 0; i < OS_I; ++i) {
+    const uint32_t s = (uint32_t)i * OS_T + tid;
+    if (s < tile_n) {
+      const uint64_t kk = sh.stage.keys[s];
+      const uint32_t d = (uint32_t)(kk >> shift) & 255u;
+      dg[i >> 2] |= d << (8 * (i & 3));
+      kout[sh.gbase[d] + s] = kk;
+    }
+  }
+  __syncthreads();
+  // ---- values: loaded only now (keeps the ranking phase under 128 VGPRs: 2 blocks/CU)
+#pragma unroll
+  for (int k = 0; k < OS_I; ++k) {
+    const uint64_t j = wbase + (uint64_t)k * 64 + lane;
+    if (j < n) sh.stage.vals[rk[k]] = iota ? (V)j : vin[j];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < OS_I; ++i) {
+    const uint32_t s = (uint32_t)i * OS_T + tid;
+    if (s < tile_n) vout[sh.gbase[(dg[i >> 2] >> (8 * (i & 3))) & 255u] + s] = sh.stage.vals[s];
+  }
+}
+
+template <typename V>
+__global__ void k_iota(V* v, uint64_t n) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (uint64_t)gridDim.x * blockDim.x)
+    v[i] = (V)i;
+}
+
+}  // namespace
+
+template <typename V>
+void fill_iota(V* v, uint64_t n, hipStream_t s) {
+  if (!n) return;
+  unsigned g = (unsigned)std::min<uint64_t>(ceil_div(n, 256), 8192);
+  k_iota<V><<<g, 256, 0, s>>>(v, n);
+  HK_HIP(hipGetLastError());
+}
+
+template <typename V>
+int radix_sort_pairs(SortWork& w, KernelTimer& tm, uint64_t* k[2], V* v[2], int in_slot,
+                     uint64_t n, int bit_lo, int bit_hi, bool vals_iota, hipStream_t s) {
+  w.passes_run = 0;
+  w.passes_skipped = 0;
+  int cur = in_slot;
+  if (n == 0 || bit_hi <= bit_lo) {
+    if (vals_iota) fill_iota<V>(v[cur], n, s);
+    return cur;
+  }
+  const int np = (bit_hi - bit_lo + 7) / 8;
+  if (np > 8) throw ApiError{-1, "radix_sort_pairs: more than 64 key bits"};
+  const uint64_t tiles = ceil_div(n, OS_TILE);
+  if (tiles > 0xFFFFFFFFull) throw ApiError{-6, "radix_sort_pairs: too many tiles"};
+
+  w.hist.ensure(8 * 256 * 8);
+  w.offs.ensure(8 * 256 * 8);
+  w.counters.ensure(64 * 4);
+  w.err.ensure(16);
+  if (tiles > w.status_tiles || !w.status.p) {
+    w.status.ensure(tiles * 256 * 8);
+    HK_HIP(hipMemsetAsync(w.status.p, 0, tiles * 256 * 8, s));
+    w.status_tiles = tiles;
+    w.epoch = 0;
+  }
+
+  // 1. histograms of every digit (one read of the keys)
+  HK_HIP(hipMemsetAsync(w.hist.p, 0, 8 * 256 * 8, s));
+  {
+    TimedLaunch t(tm, "radix_hist", (double)n * 8);
+    unsigned g = (unsigned)std::min<uint64_t>(ceil_div(n, HG_PER_BLOCK), 2048);
+    k_digit_hist<<<g, HG_T, 0, s>>>(k[cur], n, bit_lo, np, w.hist.as<unsigned long long>());
+    HK_HIP(hipGetLastError());
+  }
+  k_hist_offsets<<<np, 256, 0, s>>>(w.hist.as<uint64_t>(), w.offs.as<uint64_t>());
+  HK_HIP(hipGetLastError());
+  HK_HIP(hipMemcpyAsync(w.h_hist, w.hist.p, np * 256 * 8, hipMemcpyDeviceToHost, s));
+  HK_HIP(hipMemsetAsync(w.counters.p, 0, 64 * 4, s));
+  HK_HIP(hipMemsetAsync(w.err.p, 0, 4, s));
+  HK_HIP(hipStreamSynchronize(s));
+
+  bool iota_pending = vals_iota;
+  for (int p = 0; p < np; ++p) {
+    bool trivial = false;
+    for (int d = 0; d < 256; ++d)
+      if (w.h_hist[p * 256 + d] == n) trivial = true;
+    if (trivial) {
+      w.passes_skipped++;
+      continue;
+    }
+    if (w.epoch >= 0xFFFF) {
+      HK_HIP(hipMemsetAsync(w.status.p, 0, w.status_tiles * 256 * 8, s));
+      w.epoch = 0;
+    }
+    w.epoch++;
+    const int nxt = cur ^ 1;
+    {
+      TimedLaunch t(tm, "radix_onesweep", (double)n * 2.0 * (8 + sizeof(V)));
+      k_onesweep<V><<<(unsigned)tiles, OS_T, 0, s>>>(
+          k[cur], iota_pending ? nullptr : v[cur], k[nxt], v[nxt], n, (uint32_t)(bit_lo + 8 * p),
+          w.offs.as<uint64_t>() + p * 256, w.status.as<uint64_t>(), w.counters.as<uint32_t>() + p,
+          w.epoch, w.err.as<uint32_t>(), iota_pending ? 1 : 0);
+      HK_HIP(hipGetLastError());
+    }
+    iota_pending = false;
+    cur = nxt;
+    w.passes_run++;
+  }
+  if (iota_pending) fill_iota<V>(v[cur], n, s);
+  uint32_t herr = 0;
+  HK_HIP(hipMemcpyAsync(&herr, w.err.p, 4, hipMemcpyDeviceToHost, s));
+  HK_HIP(hipStreamSynchronize(s));
+  if (herr) throw ApiError{-7, "radix sort lookback exceeded its spin bound"};
+  return cur;
+}
+
+template int radix_sort_pairs<uint32_t>(SortWork&, KernelTimer&, uint64_t* k[2], uint32_t* v[2],
+                                        int, uint64_t, int, int, bool, hipStream_t);
+template int radix_sort_pairs<uint64_t>(SortWork&, KernelTimer&, uint64_t* k[2], uint64_t* v[2],
+                                        int, uint64_t, int, int, bool, hipStream_t);
+template void fill_iota<uint32_t>(uint32_t*, uint64_t, hipStream_t);
+template void fill_iota<uint64_t>(uint64_t*, uint64_t, hipStream_t);
+
+}  // namespace hk

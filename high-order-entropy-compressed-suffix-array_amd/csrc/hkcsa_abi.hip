@@ -1,0 +1,524 @@
+// hkcsa_abi.hip — extern "C" boundary of libhkcsa.so (declared in include/hkcsa.h).
+// Each entry point catches every C++ exception and maps it to a negative error code plus a
+// thread-local message; nothing ever throws across the ABI.
+
+#include <cstring>
+#include <new>
+#include <string>
+
+#include "../../include/hkcsa.h"
+#include "hk_index.hpp"
+
+struct hkcsa_index {
+  hk::Index ix;
+};
+
+struct hkcsa_queries {
+  uint64_t P = 0;
+  hk::DevBuf pats, offs, lr, cnt, occ_offs, pos;
+  uint64_t total = 0;
+  bool have_lr = false, have_pos = false;
+};
+
+namespace hk {
+static thread_local std::string g_err;
+void set_error(const std::string& m) { g_err = m; }
+}  // namespace hk
+
+namespace {
+
+template <typename F>
+int guarded(F&& f) {
+  try {
+    f();
+    return HKCSA_OK;
+  } catch (const hk::HipError& e) {
+    hk::set_error(std::string("HIP error ") + hipGetErrorString(e.code) + " in " + e.where);
+    (void)hipGetLastError();
+    return HKCSA_E_HIP;
+  } catch (const hk::ApiError& e) {
+    hk::set_error(e.msg);
+    return e.code;
+  } catch (const std::bad_alloc&) {
+    hk::set_error("host allocation failed");
+    return HKCSA_E_NOMEM;
+  } catch (const std::exception& e) {
+    hk::set_error(e.what());
+    return HKCSA_E_INVALID;
+  }
+}
+
+void need(bool c, int code, const char* msg) {
+  if (!c) throw hk::ApiError{code, msg};
+}
+
+void activate(const hkcsa_index* h) {
+  need(h != nullptr, HKCSA_E_INVALID, "null index handle");
+  HK_HIP(hipSetDevice(h->ix.device));
+}
+
+void init_index(hk::Index& ix, const hkcsa_opts* o, uint64_t n) {
+  int dev = (o && o->device >= 0) ? o->device : -1;
+  if (dev < 0) HK_HIP(hipGetDevice(&dev));
+  int cnt = 0;
+  HK_HIP(hipGetDeviceCount(&cnt));
+  need(dev < cnt, HKCSA_E_INVALID, "device ordinal out of range");
+  HK_HIP(hipSetDevice(dev));
+  ix.device = dev;
+  HK_HIP(hipStreamCreateWithFlags(&ix.stream, hipStreamNonBlocking));
+  ix.timer.stream = ix.stream;
+  ix.n = n;
+  ix.text.ensure(n + 64);
+  HK_HIP(hipMemsetAsync(ix.text.p, 0, n + 64, ix.stream));
+}
+
+}  // namespace
+
+extern "C" {
+
+int hkcsa_abi_version(void) { return HKCSA_ABI_VERSION; }
+
+const char* hkcsa_last_error(void) { return hk::g_err.c_str(); }
+
+int hkcsa_device_count(int* n) {
+  return guarded([&] {
+    need(n != nullptr, HKCSA_E_INVALID, "null output");
+    HK_HIP(hipGetDeviceCount(n));
+  });
+}
+
+int hkcsa_create(const uint8_t* text, uint64_t n, const hkcsa_opts* o, hkcsa_index** out) {
+  return guarded([&] {
+    need(out != nullptr, HKCSA_E_INVALID, "null output handle");
+    need(n == 0 || text != nullptr, HKCSA_E_INVALID, "null text");
+    need(n > 0, HKCSA_E_INVALID, "text must hold at least the sentinel");
+    auto* h = new hkcsa_index();
+    try {
+      init_index(h->ix, o, n);
+      HK_HIP(hipMemcpyAsync(h->ix.text.p, text, n, hipMemcpyHostToDevice, h->ix.stream));
+      HK_HIP(hipStreamSynchronize(h->ix.stream));
+    } catch (...) {
+      delete h;
+      throw;
+    }
+    *out = h;
+  });
+}
+
+int hkcsa_create_synthetic(uint64_t n, const uint8_t* alphabet, int sigma, uint64_t seed,
+                           uint8_t terminator, const hkcsa_opts* o, hkcsa_index** out) {
+  return guarded([&] {
+    need(out != nullptr, HKCSA_E_INVALID, "null output handle");
+    need(n > 0, HKCSA_E_INVALID, "n must be > 0");
+    need(alphabet != nullptr && sigma >= 1 && sigma <= 256, HKCSA_E_INVALID, "bad alphabet");
+    auto* h = new hkcsa_index();
+    try {
+      init_index(h->ix, o, n);
+      hk::synth_text(h->ix.text.as<uint8_t>(), n, alphabet, sigma, seed, terminator, h->ix.stream);
+      HK_HIP(hipStreamSynchronize(h->ix.stream));
+    } catch (...) {
+      delete h;
+      throw;
+    }
+    *out = h;
+  });
+}
+
+int hkcsa_build_sa(hkcsa_index* h) {
+  return guarded([&] {
+    activate(h);
+    h->ix.have_bwt = h->ix.have_wt = false;
+    hk::build_sa(h->ix);
+  });
+}
+int hkcsa_build_bwt(hkcsa_index* h) {
+  return guarded([&] {
+    activate(h);
+    h->ix.have_wt = false;
+    hk::build_bwt(h->ix);
+  });
+}
+int hkcsa_build_wt(hkcsa_index* h) {
+  return guarded([&] {
+    activate(h);
+    hk::build_wt(h->ix);
+  });
+}
+int hkcsa_build_all(hkcsa_index* h) {
+  return guarded([&] {
+    activate(h);
+    hk::build_sa(h->ix);
+    hk::build_bwt(h->ix);
+    hk::build_wt(h->ix);
+  });
+}
+int hkcsa_release_workspace(hkcsa_index* h) {
+  return guarded([&] {
+    activate(h);
+    HK_HIP(hipStreamSynchronize(h->ix.stream));
+    hk::release_workspace(h->ix);
+  });
+}
+int hkcsa_synchronize(hkcsa_index* h) {
+  return guarded([&] {
+    activate(h);
+    HK_HIP(hipStreamSynchronize(h->ix.stream));
+  });
+}
+void hkcsa_free(hkcsa_index* h) {
+  if (!h) return;
+  (void)hipSetDevice(h->ix.device);
+  (void)hipStreamSynchronize(h->ix.stream);
+  hipStream_t s = h->ix.stream;
+  delete h;
+  if (s) (void)hipStreamDestroy(s);
+}
+
+int hkcsa_bwt_gather(const uint8_t* text, uint64_t n, const uint64_t* sa, uint8_t* out) {
+  return guarded([&] {
+    need(n == 0 || (text && sa && out), HKCSA_E_INVALID, "null argument");
+    if (!n) return;
+    for (uint64_t i = 0; i < n; ++i) need(sa[i] < n, HKCSA_E_RANGE, "suffix array entry out of range");
+    hk::Index ix;
+    init_index(ix, nullptr, n);
+    hipStream_t s = ix.stream;
+    try {
+      HK_HIP(hipMemcpyAsync(ix.text.p, text, n, hipMemcpyHostToDevice, s));
+      hk::DevBuf dsa;
+      dsa.ensure(n * 8);
+      HK_HIP(hipMemcpyAsync(dsa.p, sa, n * 8, hipMemcpyHostToDevice, s));
+      hk::bwt_gather64(ix, dsa.as<uint64_t>());
+      HK_HIP(hipMemcpyAsync(out, ix.bwt.p, n, hipMemcpyDeviceToHost, s));
+      HK_HIP(hipStreamSynchronize(s));
+    } catch (...) {
+      (void)hipStreamSynchronize(s);
+      (void)hipStreamDestroy(s);
+      throw;
+    }
+    (void)hipStreamDestroy(s);
+  });
+}
+
+int hkcsa_use_text_as_bwt(hkcsa_index* h) {
+  return guarded([&] {
+    activate(h);
+    h->ix.bwt.ensure(h->ix.n + 64);
+    HK_HIP(hipMemcpyAsync(h->ix.bwt.p, h->ix.text.p, h->ix.n, hipMemcpyDeviceToDevice, h->ix.stream));
+    HK_HIP(hipStreamSynchronize(h->ix.stream));
+    h->ix.have_bwt = true;
+    h->ix.have_wt = false;
+  });
+}
+
+int hkcsa_get_n(const hkcsa_index* h, uint64_t* n) {
+  return guarded([&] {
+    need(h && n, HKCSA_E_INVALID, "null argument");
+    *n = h->ix.n;
+  });
+}
+
+int hkcsa_get_sa(hkcsa_index* h, uint64_t lo, uint64_t hi, uint64_t* out) {
+  return guarded([&] {
+    activate(h);
+    need(h->ix.have_sa && !h->ix.sharded, HKCSA_E_STATE, "suffix array not built");
+    need(lo <= hi && hi <= h->ix.n, HKCSA_E_RANGE, "SA range out of bounds");
+    need(hi == lo || out, HKCSA_E_INVALID, "null output");
+    const uint64_t c = hi - lo;
+    if (!c) return;
+    std::vector<uint32_t> tmp(c);
+    HK_HIP(hipMemcpyAsync(tmp.data(), h->ix.sa.as<uint32_t>() + lo, c * 4, hipMemcpyDeviceToHost, h->ix.stream));
+    HK_HIP(hipStreamSynchronize(h->ix.stream));
+    for (uint64_t i = 0; i < c; ++i) out[i] = tmp[i];
+  });
+}
+
+int hkcsa_get_bwt(hkcsa_index* h, uint64_t lo, uint64_t hi, uint8_t* out) {
+  return guarded([&] {
+    activate(h);
+    need(h->ix.have_bwt, HKCSA_E_STATE, "BWT not built");
+    need(lo <= hi && hi <= h->ix.n, HKCSA_E_RANGE, "BWT range out of bounds");
+    if (hi == lo) return;
+    need(out != nullptr, HKCSA_E_INVALID, "null output");
+    HK_HIP(hipMemcpyAsync(out, h->ix.bwt.as<uint8_t>() + lo, hi - lo, hipMemcpyDeviceToHost, h->ix.stream));
+    HK_HIP(hipStreamSynchronize(h->ix.stream));
+  });
+}
+
+int hkcsa_get_text(hkcsa_index* h, uint64_t lo, uint64_t hi, uint8_t* out) {
+  return guarded([&] {
+    activate(h);
+    need(lo <= hi && hi <= h->ix.n, HKCSA_E_RANGE, "text range out of bounds");
+    if (hi == lo) return;
+    need(out != nullptr, HKCSA_E_INVALID, "null output");
+    HK_HIP(hipMemcpyAsync(out, h->ix.text.as<uint8_t>() + lo, hi - lo, hipMemcpyDeviceToHost, h->ix.stream));
+    HK_HIP(hipStreamSynchronize(h->ix.stream));
+  });
+}
+
+int hkcsa_extract(hkcsa_index* h, uint64_t i, uint64_t j, uint8_t* out) { return hkcsa_get_text(h, i, j, out); }
+
+int hkcsa_get_C(hkcsa_index* h, uint64_t C[257]) {
+  return guarded([&] {
+    activate(h);
+    need(C != nullptr, HKCSA_E_INVALID, "null output");
+    hk::compute_alphabet(h->ix);
+    memcpy(C, h->ix.Cbyte, 257 * 8);
+  });
+}
+
+int hkcsa_get_alphabet(hkcsa_index* h, uint8_t syms[256], int* sigma) {
+  return guarded([&] {
+    activate(h);
+    need(syms && sigma, HKCSA_E_INVALID, "null output");
+    hk::compute_alphabet(h->ix);
+    memcpy(syms, h->ix.syms, 256);
+    *sigma = h->ix.sigma;
+  });
+}
+
+int hkcsa_wt_levels(hkcsa_index* h, int* levels) {
+  return guarded([&] {
+    activate(h);
+    need(levels != nullptr, HKCSA_E_INVALID, "null output");
+    need(h->ix.have_wt, HKCSA_E_STATE, "wavelet tree not built");
+    *levels = h->ix.wt_levels;
+  });
+}
+
+int hkcsa_wt_level(hkcsa_index* h, int depth, uint64_t* nbits, uint64_t* words_out) {
+  return guarded([&] {
+    activate(h);
+    need(h->ix.have_wt, HKCSA_E_STATE, "wavelet tree not built");
+    need(depth >= 0 && depth < h->ix.wt_levels, HKCSA_E_RANGE, "level out of range");
+    if (nbits) *nbits = h->ix.n;
+    if (!words_out) return;
+    const uint64_t nw = hk::ceil_div(h->ix.n, 64);
+    hk::DevBuf tmp;
+    tmp.ensure(nw * 8 + 8);
+    hk::wt_level_words(h->ix, depth, tmp.as<uint64_t>());
+    HK_HIP(hipMemcpyAsync(words_out, tmp.p, nw * 8, hipMemcpyDeviceToHost, h->ix.stream));
+    HK_HIP(hipStreamSynchronize(h->ix.stream));
+  });
+}
+
+int hkcsa_rank(hkcsa_index* h, const uint8_t* c, const uint64_t* i, uint64_t count, uint64_t* out) {
+  return guarded([&] {
+    activate(h);
+    need(h->ix.have_wt, HKCSA_E_STATE, "wavelet tree not built");
+    if (!count) return;
+    need(c && i && out, HKCSA_E_INVALID, "null argument");
+    hk::DevBuf dc, di, dout;
+    dc.ensure(count);
+    di.ensure(count * 8);
+    dout.ensure(count * 8);
+    hipStream_t s = h->ix.stream;
+    HK_HIP(hipMemcpyAsync(dc.p, c, count, hipMemcpyHostToDevice, s));
+    HK_HIP(hipMemcpyAsync(di.p, i, count * 8, hipMemcpyHostToDevice, s));
+    hk::query_rank(h->ix, dc.as<uint8_t>(), di.as<uint64_t>(), count, dout.as<uint64_t>());
+    HK_HIP(hipMemcpyAsync(out, dout.p, count * 8, hipMemcpyDeviceToHost, s));
+    HK_HIP(hipStreamSynchronize(s));
+  });
+}
+
+// ------------------------------------------------------------ query sets
+int hkcsa_queries_upload(hkcsa_index* h, const uint8_t* pats, const uint64_t* offs, uint64_t P,
+                         hkcsa_queries** out) {
+  return guarded([&] {
+    activate(h);
+    need(out != nullptr, HKCSA_E_INVALID, "null output");
+    need(offs != nullptr, HKCSA_E_INVALID, "null offsets");
+    need(offs[0] == 0, HKCSA_E_INVALID, "offs[0] must be 0");
+    for (uint64_t p = 0; p < P; ++p) need(offs[p + 1] >= offs[p], HKCSA_E_INVALID, "offsets not monotone");
+    const uint64_t bytes = offs[P];
+    need(bytes == 0 || pats != nullptr, HKCSA_E_INVALID, "null patterns");
+    auto* q = new hkcsa_queries();
+    try {
+      hipStream_t s = h->ix.stream;
+      q->P = P;
+      q->pats.ensure(bytes + 16);
+      q->offs.ensure((P + 1) * 8);
+      if (bytes) HK_HIP(hipMemcpyAsync(q->pats.p, pats, bytes, hipMemcpyHostToDevice, s));
+      HK_HIP(hipMemcpyAsync(q->offs.p, offs, (P + 1) * 8, hipMemcpyHostToDevice, s));
+      q->lr.ensure(P * 16 + 16);
+      q->cnt.ensure(P * 8 + 16);
+      q->occ_offs.ensure((P + 1) * 8 + 16);
+      HK_HIP(hipStreamSynchronize(s));
+    } catch (...) {
+      delete q;
+      throw;
+    }
+    *out = q;
+  });
+}
+
+int hkcsa_queries_count(hkcsa_index* h, hkcsa_queries* q) {
+  return guarded([&] {
+    activate(h);
+    need(q != nullptr, HKCSA_E_INVALID, "null query set");
+    hk::query_count(h->ix, q->pats.as<uint8_t>(), q->offs.as<uint64_t>(), q->P, q->lr.as<int64_t>(),
+                    q->cnt.as<uint64_t>());
+    q->have_lr = true;
+    q->have_pos = false;
+  });
+}
+
+int hkcsa_queries_locate(hkcsa_index* h, hkcsa_queries* q, uint64_t* total) {
+  return guarded([&] {
+    activate(h);
+    need(q != nullptr, HKCSA_E_INVALID, "null query set");
+    hipStream_t s = h->ix.stream;
+    hk::query_count(h->ix, q->pats.as<uint8_t>(), q->offs.as<uint64_t>(), q->P, q->lr.as<int64_t>(),
+                    q->cnt.as<uint64_t>());
+    hk::scan_exclusive_u64(h->ix.sw, q->cnt.as<uint64_t>(), q->occ_offs.as<uint64_t>(), q->P, true, s);
+    uint64_t tot = 0;
+    HK_HIP(hipMemcpyAsync(&tot, q->occ_offs.as<uint64_t>() + q->P, 8, hipMemcpyDeviceToHost, s));
+    HK_HIP(hipStreamSynchronize(s));
+    q->pos.ensure(tot * 8 + 16);
+    hk::query_locate_gather(h->ix, q->lr.as<int64_t>(), q->occ_offs.as<uint64_t>(), q->P, q->pos.as<uint64_t>());
+    q->total = tot;
+    q->have_lr = q->have_pos = true;
+    if (total) *total = tot;
+  });
+}
+
+int hkcsa_queries_download(hkcsa_index* h, hkcsa_queries* q, int64_t* lr_out, uint64_t* occ_offs,
+                           uint64_t* pos_out, uint64_t cap) {
+  return guarded([&] {
+    activate(h);
+    need(q != nullptr, HKCSA_E_INVALID, "null query set");
+    need(q->have_lr, HKCSA_E_STATE, "queries not run");
+    hipStream_t s = h->ix.stream;
+    if (lr_out && q->P) HK_HIP(hipMemcpyAsync(lr_out, q->lr.p, q->P * 16, hipMemcpyDeviceToHost, s));
+    if (occ_offs || pos_out) need(q->have_pos, HKCSA_E_STATE, "locate not run");
+    if (occ_offs) HK_HIP(hipMemcpyAsync(occ_offs, q->occ_offs.p, (q->P + 1) * 8, hipMemcpyDeviceToHost, s));
+    if (pos_out && q->total) {
+      need(cap >= q->total, HKCSA_E_RANGE, "position buffer too small");
+      HK_HIP(hipMemcpyAsync(pos_out, q->pos.p, q->total * 8, hipMemcpyDeviceToHost, s));
+    }
+    HK_HIP(hipStreamSynchronize(s));
+  });
+}
+
+void hkcsa_queries_free(hkcsa_queries* q) { delete q; }
+
+int hkcsa_count_batch(hkcsa_index* h, const uint8_t* pats, const uint64_t* offs, uint64_t P, int64_t* lr_out) {
+  hkcsa_queries* q = nullptr;
+  int rc = hkcsa_queries_upload(h, pats, offs, P, &q);
+  if (rc) return rc;
+  rc = hkcsa_queries_count(h, q);
+  if (!rc) rc = hkcsa_queries_download(h, q, lr_out, nullptr, nullptr, 0);
+  hkcsa_queries_free(q);
+  return rc;
+}
+
+int hkcsa_locate_batch(hkcsa_index* h, const uint8_t* pats, const uint64_t* offs, uint64_t P,
+                       uint64_t* occ_offs, uint64_t* pos_out, uint64_t cap) {
+  hkcsa_queries* q = nullptr;
+  int rc = hkcsa_queries_upload(h, pats, offs, P, &q);
+  if (rc) return rc;
+  rc = hkcsa_queries_locate(h, q, nullptr);
+  if (!rc) rc = hkcsa_queries_download(h, q, nullptr, occ_offs, pos_out, pos_out ? cap : 0);
+  hkcsa_queries_free(q);
+  return rc;
+}
+
+// ------------------------------------------------------------ sharded SA
+int hkcsa_build_sa_sharded(hkcsa_index* h, const uint8_t id[128], int nranks, int rank) {
+  return guarded([&] {
+    activate(h);
+    need(id != nullptr && nranks >= 1 && rank >= 0 && rank < nranks, HKCSA_E_INVALID, "bad communicator args");
+    h->ix.have_bwt = h->ix.have_wt = false;
+    hk::build_sa_sharded(h->ix, id, nranks, rank);
+  });
+}
+
+int hkcsa_comm_unique_id(uint8_t id[128]) {
+  return guarded([&] {
+    need(id != nullptr, HKCSA_E_INVALID, "null output");
+    hk::comm_unique_id(id);
+  });
+}
+
+int hkcsa_shard_buckets(void) { return hk::shard_buckets(); }
+
+int hkcsa_shard_histogram(hkcsa_index* h, int nranks, int rank, uint64_t* hist_out) {
+  return guarded([&] {
+    activate(h);
+    need(hist_out != nullptr && nranks >= 1 && rank >= 0 && rank < nranks, HKCSA_E_INVALID, "bad arguments");
+    const int nb = hk::shard_buckets();
+    hk::DevBuf d;
+    d.ensure((size_t)nb * 8);
+    hk::shard_histogram(h->ix, nranks, rank, d.as<uint64_t>());
+    HK_HIP(hipMemcpyAsync(hist_out, d.p, (size_t)nb * 8, hipMemcpyDeviceToHost, h->ix.stream));
+    HK_HIP(hipStreamSynchronize(h->ix.stream));
+  });
+}
+
+int hkcsa_shard_build(hkcsa_index* h, const uint64_t* global_hist, int nranks, int rank) {
+  return guarded([&] {
+    activate(h);
+    need(global_hist != nullptr && nranks >= 1 && rank >= 0 && rank < nranks, HKCSA_E_INVALID, "bad arguments");
+    h->ix.have_bwt = h->ix.have_wt = false;
+    hk::shard_build(h->ix, global_hist, nranks, rank);
+  });
+}
+
+int hkcsa_get_shard_sa(hkcsa_index* h, uint64_t a, uint64_t b, uint64_t* out) {
+  return guarded([&] {
+    activate(h);
+    need(h->ix.sharded && h->ix.have_sa, HKCSA_E_STATE, "no sharded suffix array");
+    need(a == b || out != nullptr, HKCSA_E_INVALID, "null output");
+    hk::shard_get_sa(h->ix, a, b, out);
+  });
+}
+
+int hkcsa_shard_range(hkcsa_index* h, uint64_t* lo, uint64_t* hi) {
+  return guarded([&] {
+    need(h && lo && hi, HKCSA_E_INVALID, "null argument");
+    need(h->ix.sharded, HKCSA_E_STATE, "index is not sharded");
+    *lo = h->ix.shard_lo;
+    *hi = h->ix.shard_hi;
+  });
+}
+
+// ------------------------------------------------------------ timing
+int hkcsa_timing_enable(hkcsa_index* h, int on) {
+  return guarded([&] {
+    activate(h);
+    h->ix.timer.resolve();
+    h->ix.timer.enabled = on != 0;
+  });
+}
+int hkcsa_timing_reset(hkcsa_index* h) {
+  return guarded([&] {
+    activate(h);
+    h->ix.timer.reset();
+  });
+}
+int hkcsa_kernel_stats(hkcsa_index* h, const char* name, uint64_t* launches, double* total_ms, double* alg_bytes) {
+  return guarded([&] {
+    activate(h);
+    need(name != nullptr, HKCSA_E_INVALID, "null name");
+    h->ix.timer.resolve();
+    uint64_t l = 0;
+    double ms = 0, b = 0;
+    for (auto& s : h->ix.timer.stats)
+      if (s.first == name) {
+        l += s.second.launches;
+        ms += s.second.ms;
+        b += s.second.bytes;
+      }
+    if (launches) *launches = l;
+    if (total_ms) *total_ms = ms;
+    if (alg_bytes) *alg_bytes = b;
+  });
+}
+int hkcsa_build_info(hkcsa_index* h, uint64_t* info, int cap) {
+  return guarded([&] {
+    need(h && info && cap >= 0, HKCSA_E_INVALID, "null argument");
+    const auto& v = h->ix.info;
+    for (int i = 0; i < cap; ++i) info[i] = i < (int)v.size() ? v[i] : 0;
+  });
+}
+
+}  // extern "C"

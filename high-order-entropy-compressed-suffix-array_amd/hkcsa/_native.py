@@ -1,0 +1,119 @@
+"""ctypes binding of libhkcsa.so (declarations mirror include/hkcsa.h).
+
+The library is the product path: every index operation runs as HIP kernels on
+the GPU.  There is deliberately no CPU fallback — if the shared object is
+missing or no GPU is visible, calls raise HkcsaError.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("HKCSA_LIB", os.path.join(_HERE, "_lib", "libhkcsa.so"))
+
+u8p = C.POINTER(C.c_uint8)
+u64p = C.POINTER(C.c_uint64)
+i64p = C.POINTER(C.c_int64)
+vp = C.c_void_p
+
+
+class HkcsaError(RuntimeError):
+    """Raised for every non-zero return code of the C-ABI."""
+
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"hkcsa error {code}: {msg}")
+        self.code = code
+
+
+class Opts(C.Structure):
+    _fields_ = [("device", C.c_int32), ("flags", C.c_uint32), ("reserved", C.c_uint64 * 2)]
+
+
+# (name, restype, argtypes)
+_SIGS = [
+    ("hkcsa_abi_version", C.c_int, []),
+    ("hkcsa_device_count", C.c_int, [C.POINTER(C.c_int)]),
+    ("hkcsa_last_error", C.c_char_p, []),
+    ("hkcsa_create", C.c_int, [vp, C.c_uint64, C.POINTER(Opts), C.POINTER(vp)]),
+    ("hkcsa_create_synthetic", C.c_int, [C.c_uint64, vp, C.c_int, C.c_uint64, C.c_uint8, C.POINTER(Opts), C.POINTER(vp)]),
+    ("hkcsa_build_sa", C.c_int, [vp]),
+    ("hkcsa_build_bwt", C.c_int, [vp]),
+    ("hkcsa_build_wt", C.c_int, [vp]),
+    ("hkcsa_build_all", C.c_int, [vp]),
+    ("hkcsa_release_workspace", C.c_int, [vp]),
+    ("hkcsa_synchronize", C.c_int, [vp]),
+    ("hkcsa_free", None, [vp]),
+    ("hkcsa_bwt_gather", C.c_int, [vp, C.c_uint64, vp, vp]),
+    ("hkcsa_use_text_as_bwt", C.c_int, [vp]),
+    ("hkcsa_get_n", C.c_int, [vp, u64p]),
+    ("hkcsa_get_sa", C.c_int, [vp, C.c_uint64, C.c_uint64, vp]),
+    ("hkcsa_get_bwt", C.c_int, [vp, C.c_uint64, C.c_uint64, vp]),
+    ("hkcsa_get_text", C.c_int, [vp, C.c_uint64, C.c_uint64, vp]),
+    ("hkcsa_get_C", C.c_int, [vp, vp]),
+    ("hkcsa_get_alphabet", C.c_int, [vp, vp, C.POINTER(C.c_int)]),
+    ("hkcsa_wt_levels", C.c_int, [vp, C.POINTER(C.c_int)]),
+    ("hkcsa_wt_level", C.c_int, [vp, C.c_int, u64p, vp]),
+    ("hkcsa_rank", C.c_int, [vp, vp, vp, C.c_uint64, vp]),
+    ("hkcsa_count_batch", C.c_int, [vp, vp, vp, C.c_uint64, vp]),
+    ("hkcsa_locate_batch", C.c_int, [vp, vp, vp, C.c_uint64, vp, vp, C.c_uint64]),
+    ("hkcsa_queries_upload", C.c_int, [vp, vp, vp, C.c_uint64, C.POINTER(vp)]),
+    ("hkcsa_queries_count", C.c_int, [vp, vp]),
+    ("hkcsa_queries_locate", C.c_int, [vp, vp, u64p]),
+    ("hkcsa_queries_download", C.c_int, [vp, vp, vp, vp, vp, C.c_uint64]),
+    ("hkcsa_queries_free", None, [vp]),
+    ("hkcsa_extract", C.c_int, [vp, C.c_uint64, C.c_uint64, vp]),
+    ("hkcsa_comm_unique_id", C.c_int, [vp]),
+    ("hkcsa_build_sa_sharded", C.c_int, [vp, vp, C.c_int, C.c_int]),
+    ("hkcsa_shard_range", C.c_int, [vp, u64p, u64p]),
+    ("hkcsa_get_shard_sa", C.c_int, [vp, C.c_uint64, C.c_uint64, vp]),
+    ("hkcsa_shard_buckets", C.c_int, []),
+    ("hkcsa_shard_histogram", C.c_int, [vp, C.c_int, C.c_int, vp]),
+    ("hkcsa_shard_build", C.c_int, [vp, vp, C.c_int, C.c_int]),
+    ("hkcsa_timing_enable", C.c_int, [vp, C.c_int]),
+    ("hkcsa_timing_reset", C.c_int, [vp]),
+    ("hkcsa_kernel_stats", C.c_int, [vp, C.c_char_p, u64p, C.POINTER(C.c_double), C.POINTER(C.c_double)]),
+    ("hkcsa_build_info", C.c_int, [vp, u64p, C.c_int]),
+]
+
+EXPORTED = [s[0] for s in _SIGS]
+
+_lib = None
+_lock = threading.Lock()
+
+
+def load(path: str | None = None):
+    """Load (once) and return the CDLL with typed signatures."""
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        p = path or LIB_PATH
+        if not os.path.exists(p):
+            raise HkcsaError(-1, f"native library not found at {p}; run __graft_entry__.build() "
+                                 "(or make -C high-order-entropy-compressed-suffix-array_amd/csrc)")
+        lib = C.CDLL(p)
+        for name, res, args in _SIGS:
+            f = getattr(lib, name)
+            f.restype = res
+            f.argtypes = args
+        if lib.hkcsa_abi_version() != 1:
+            raise HkcsaError(-1, "ABI version mismatch")
+        _lib = lib
+        return lib
+
+
+def check(rc: int):
+    if rc != 0:
+        msg = _lib.hkcsa_last_error().decode("utf-8", "replace") if _lib else "library not loaded"
+        raise HkcsaError(rc, msg)
+
+
+def device_count() -> int:
+    lib = load()
+    n = C.c_int(0)
+    rc = lib.hkcsa_device_count(C.byref(n))
+    if rc != 0:
+        return 0
+    return n.value

@@ -1,0 +1,173 @@
+/*
+ * hkcsa.h — C-ABI of libhkcsa.so, the MI355X-native H_k-CSA build + query path.
+ *
+ * The reference (ajaynair710/High-Order-Entropy-Compressed-Suffix-Array) has no
+ * FFI: its "boundary" is the Python class EnhancedFMIndex and the module
+ * functions it calls.  Each entry point below states which reference interface
+ * it replaces (file:line under the reference tree).  The Python package
+ * `csa` (high-order-entropy-compressed-suffix-array_amd/csa) binds these with
+ * ctypes; INTEGRATION.md shows the binding.
+ *
+ * Conventions
+ *  - Every function returns 0 on success or a negative HKCSA_E* code; the
+ *    message is available from hkcsa_last_error() (thread-local).
+ *  - Host buffers are caller-owned; device buffers live inside the opaque
+ *    handle.  A handle is not thread-safe (one HIP stream per handle).
+ *  - Texts are byte strings.  The caller appends the reference's '$'
+ *    sentinel itself (csa/enhanced_fm_index.py:9); the library treats '$' as
+ *    an ordinary byte and end-of-text as smaller than every byte, i.e. Python
+ *    str order (csa/suffix_array.py:131-134).
+ *  - Suffix-array entries are 64-bit at the ABI.
+ */
+#ifndef HKCSA_H
+#define HKCSA_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define HKCSA_ABI_VERSION 1
+
+#define HKCSA_OK 0
+#define HKCSA_E_INVALID (-1)   /* bad argument                        */
+#define HKCSA_E_HIP (-2)       /* HIP runtime error                   */
+#define HKCSA_E_STATE (-3)     /* stage not built yet / wrong order   */
+#define HKCSA_E_RANGE (-4)     /* index out of range                  */
+#define HKCSA_E_NOMEM (-5)     /* device allocation failed            */
+#define HKCSA_E_TOOBIG (-6)    /* size beyond what this build handles */
+#define HKCSA_E_DEVICE (-7)    /* kernel reported an internal failure */
+#define HKCSA_E_COMM (-8)      /* RCCL failure                        */
+
+typedef struct hkcsa_index hkcsa_index;
+typedef struct hkcsa_queries hkcsa_queries;
+
+typedef struct hkcsa_opts {
+  int32_t device;   /* HIP device ordinal (-1 = current)                 */
+  uint32_t flags;   /* reserved, 0                                       */
+  uint64_t reserved[2];
+} hkcsa_opts;
+
+/* ---- library ---------------------------------------------------------- */
+int hkcsa_abi_version(void);
+int hkcsa_device_count(int* n);
+const char* hkcsa_last_error(void);
+
+/* ---- construction ----------------------------------------------------- */
+/* Upload text T' (n bytes, sentinel already appended) to the device.
+ * Replaces the text handling of EnhancedFMIndex.__init__
+ * (csa/enhanced_fm_index.py:8-9). */
+int hkcsa_create(const uint8_t* text, uint64_t n, const hkcsa_opts* o, hkcsa_index** out);
+/* Generate a synthetic text on the device: n-1 iid bytes drawn from the
+ * `sigma` symbols `alphabet[0..sigma)` by a counter-based hash of (seed, i),
+ * followed by the byte `terminator`.  Reproducible on the host with
+ * oracle/hkcsa_oracle.c:oracle_synth_text. (bench input, no reference twin) */
+int hkcsa_create_synthetic(uint64_t n, const uint8_t* alphabet, int sigma, uint64_t seed,
+                           uint8_t terminator, const hkcsa_opts* o, hkcsa_index** out);
+/* Suffix array by GPU prefix doubling.  Replaces build_suffix_array
+ * (csa/suffix_array.py:131-134) on T'. */
+int hkcsa_build_sa(hkcsa_index* ix);
+/* BWT gather over SA.  Replaces bwt_transform (csa/bwt.py:3-13). */
+int hkcsa_build_bwt(hkcsa_index* ix);
+/* C array + levelwise wavelet tree over the BWT with interleaved rank lines.
+ * Replaces build_count (utils/utils.py:16-24), build_occ (utils/utils.py:26-32)
+ * as the rank structure, and WaveletTree.build_tree (csa/wavelet_tree.py:72-100). */
+int hkcsa_build_wt(hkcsa_index* ix);
+/* SA + BWT + WT in one call (EnhancedFMIndex.__init__, csa/enhanced_fm_index.py:8-13). */
+int hkcsa_build_all(hkcsa_index* ix);
+/* Drop the construction workspace (keys, ISA, ...) kept for repeated builds. */
+int hkcsa_release_workspace(hkcsa_index* ix);
+int hkcsa_synchronize(hkcsa_index* ix);
+void hkcsa_free(hkcsa_index* ix);
+
+/* Module-level helpers (no index semantics of their own):
+ * BWT gather over a caller-supplied SA (bwt_transform, csa/bwt.py:3-13): out[i] =
+ * text[sa[i]-1], text[n-1] when sa[i]==0; every sa[i] must be < n. */
+int hkcsa_bwt_gather(const uint8_t* text, uint64_t n, const uint64_t* sa, uint8_t* out);
+/* Treat the handle's text itself as the sequence to index with the wavelet tree
+ * (WaveletTree(seq), csa/wavelet_tree.py:66-70; build_occ(bwt), utils/utils.py:26-32). */
+int hkcsa_use_text_as_bwt(hkcsa_index* ix);
+
+/* ---- inspection / parity exports ------------------------------------- */
+int hkcsa_get_n(const hkcsa_index* ix, uint64_t* n);
+/* SA[lo:hi) into out (hi-lo entries). EnhancedFMIndex.suffix_array. */
+int hkcsa_get_sa(hkcsa_index* ix, uint64_t lo, uint64_t hi, uint64_t* out);
+/* BWT[lo:hi). EnhancedFMIndex.bwt. */
+int hkcsa_get_bwt(hkcsa_index* ix, uint64_t lo, uint64_t hi, uint8_t* out);
+/* T'[lo:hi). */
+int hkcsa_get_text(hkcsa_index* ix, uint64_t lo, uint64_t hi, uint8_t* out);
+/* C[b] = #{j : T'[j] < b} for every byte value b (C[256] = n).  For bytes
+ * present in T' this equals EnhancedFMIndex.count (utils/utils.py:16-24). */
+int hkcsa_get_C(hkcsa_index* ix, uint64_t C[257]);
+/* Sorted distinct bytes of T' (WaveletTree.alphabet, csa/wavelet_tree.py:68). */
+int hkcsa_get_alphabet(hkcsa_index* ix, uint8_t syms[256], int* sigma);
+/* Number of levels of the full balanced WT (ceil(log2 sigma)). */
+int hkcsa_wt_levels(hkcsa_index* ix, int* levels);
+/* Level `depth` bitvector, n bits, packed LSB-first into ceil(n/64) words
+ * (words_out may be NULL to query nbits).  The reference's left-spine level
+ * l (csa/wavelet_tree.py:82) is the prefix of depth-l of length |leftmost node|. */
+int hkcsa_wt_level(hkcsa_index* ix, int depth, uint64_t* nbits, uint64_t* words_out);
+/* occ(c_k, i_k) = #c_k in BWT[0:min(i_k, n)) for k < count, 0 for absent bytes.
+ * EnhancedFMIndex.rank (csa/enhanced_fm_index.py:34-40). */
+int hkcsa_rank(hkcsa_index* ix, const uint8_t* c, const uint64_t* i, uint64_t count, uint64_t* out);
+
+/* ---- batched queries -------------------------------------------------- */
+/* Patterns are concatenated bytes `pats` with offsets offs[0..P] (offs[0]=0).
+ * count: lr_out[2p], lr_out[2p+1] = (l, r) of EnhancedFMIndex.find_range
+ * (csa/enhanced_fm_index.py:21-32), (-1,-1) on a miss. */
+int hkcsa_count_batch(hkcsa_index* ix, const uint8_t* pats, const uint64_t* offs, uint64_t P,
+                      int64_t* lr_out);
+/* locate: EnhancedFMIndex.find (csa/enhanced_fm_index.py:15-19), positions in
+ * SA order.  Two-phase: with pos_out == NULL only occ_offs (P+1 entries,
+ * CSR offsets) is filled; then call again with cap >= occ_offs[P]. */
+int hkcsa_locate_batch(hkcsa_index* ix, const uint8_t* pats, const uint64_t* offs, uint64_t P,
+                       uint64_t* occ_offs, uint64_t* pos_out, uint64_t cap);
+/* Device-resident query sets (bench: inputs resident in HBM before timing). */
+int hkcsa_queries_upload(hkcsa_index* ix, const uint8_t* pats, const uint64_t* offs, uint64_t P,
+                         hkcsa_queries** out);
+int hkcsa_queries_count(hkcsa_index* ix, hkcsa_queries* q);                 /* (l,r) on device */
+int hkcsa_queries_locate(hkcsa_index* ix, hkcsa_queries* q, uint64_t* total); /* count+scan+gather */
+int hkcsa_queries_download(hkcsa_index* ix, hkcsa_queries* q, int64_t* lr_out, uint64_t* occ_offs,
+                           uint64_t* pos_out, uint64_t cap);
+void hkcsa_queries_free(hkcsa_queries* q);
+/* text[i:j) of T' (csa.CSA.extract; oracle: Python slicing). */
+int hkcsa_extract(hkcsa_index* ix, uint64_t i, uint64_t j, uint8_t* out);
+
+/* ---- sharded (multi-GPU) suffix-array construction ------------------- */
+/* RCCL unique id (128 bytes) to be broadcast by the caller from rank 0. */
+int hkcsa_comm_unique_id(uint8_t id[128]);
+/* Each rank holds the same T' (created on its own device).  Ranks split the
+ * final SA into contiguous rank ranges by a shared key histogram
+ * (RCCL all-reduce) and sort their slice independently; the slice bounds are
+ * exchanged with an RCCL all-gather.  After the call ix holds SA[lo:hi). */
+int hkcsa_build_sa_sharded(hkcsa_index* ix, const uint8_t id[128], int nranks, int rank);
+int hkcsa_shard_range(hkcsa_index* ix, uint64_t* lo, uint64_t* hi);
+/* Sharded SA slice entries SA[lo+a : lo+b) (a,b relative to the slice). */
+int hkcsa_get_shard_sa(hkcsa_index* ix, uint64_t a, uint64_t b, uint64_t* out);
+/* The same construction in two host-visible phases, for hosts that do their own
+ * collectives (and for single-GPU tests of the partitioning):
+ *   hkcsa_shard_histogram: this rank's key-prefix histogram (hkcsa_shard_buckets()
+ *   bins) over positions [n*rank/nranks, n*(rank+1)/nranks);
+ *   hkcsa_shard_build: builds SA[lo:hi) of this rank from the element-wise sum of
+ *   every rank's histogram. */
+int hkcsa_shard_buckets(void);
+int hkcsa_shard_histogram(hkcsa_index* ix, int nranks, int rank, uint64_t* hist_out);
+int hkcsa_shard_build(hkcsa_index* ix, const uint64_t* global_hist, int nranks, int rank);
+
+/* ---- per-kernel timing (HIP events on the handle's stream) ------------ */
+int hkcsa_timing_enable(hkcsa_index* ix, int on);
+int hkcsa_timing_reset(hkcsa_index* ix);
+/* Aggregated stats for kernels whose name matches `name` exactly.
+ * alg_bytes is the algorithmic byte count summed over launches. */
+int hkcsa_kernel_stats(hkcsa_index* ix, const char* name, uint64_t* launches, double* total_ms,
+                       double* alg_bytes);
+/* Build-stage counters of the last build: radix passes run / skipped,
+ * doubling rounds, active elements per round (up to 64). */
+int hkcsa_build_info(hkcsa_index* ix, uint64_t* info, int cap);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* HKCSA_H */

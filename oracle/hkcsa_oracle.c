@@ -1,0 +1,256 @@
+/*
+ * hkcsa_oracle.c — CPU restatement of the reference's hot path. TEST INFRASTRUCTURE ONLY:
+ * used by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg as the checker;
+ * never linked into or called by the product (libhkcsa.so / the csa package).
+ *
+ * Pinned against the reference's own outputs: the fixtures in tests/golden/ were produced by
+ * importing the reference (tests/golden/make_golden.py) and tests/test_oracle.py checks this
+ * file against every vector there.
+ *
+ * Each function cites the reference code it restates (paths relative to the reference root).
+ */
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+/* ---------------------------------------------------------------- suffix order
+ * csa/suffix_array.py:131-134 sorts (text[i:], i) tuples: Python str order, i.e. code point
+ * order with a proper prefix first.  Suffixes are distinct, so the index never breaks a tie. */
+static const uint8_t* g_t;
+static uint64_t g_n;
+
+static int suffix_cmp(const void* pa, const void* pb) {
+  const uint64_t a = *(const uint64_t*)pa, b = *(const uint64_t*)pb;
+  const uint64_t la = g_n - a, lb = g_n - b;
+  const uint64_t m = la < lb ? la : lb;
+  int c = memcmp(g_t + a, g_t + b, m);
+  if (c) return c;
+  return la < lb ? -1 : (la > lb ? 1 : 0);
+}
+
+int oracle_suffix_array(const uint8_t* t, uint64_t n, uint64_t* sa) {
+  for (uint64_t i = 0; i < n; ++i) sa[i] = i;
+  g_t = t;
+  g_n = n;
+  qsort(sa, n, sizeof(uint64_t), suffix_cmp);
+  return 0;
+}
+
+/* csa/bwt.py:3-13: bwt[i] = text[sa[i]-1], wrapping to text[n-1] */
+void oracle_bwt(const uint8_t* t, uint64_t n, const uint64_t* sa, uint8_t* bwt) {
+  for (uint64_t i = 0; i < n; ++i) bwt[i] = t[sa[i] == 0 ? n - 1 : sa[i] - 1];
+}
+
+/* utils/utils.py:16-24: C[c] = number of symbols < c (C[256] = n) */
+void oracle_count(const uint8_t* t, uint64_t n, uint64_t C[257]) {
+  uint64_t h[256] = {0};
+  for (uint64_t i = 0; i < n; ++i) h[t[i]]++;
+  uint64_t acc = 0;
+  for (int c = 0; c < 256; ++c) {
+    C[c] = acc;
+    acc += h[c];
+  }
+  C[256] = acc;
+}
+
+/* ------------------------------------------------------------------- occ
+ * utils/utils.py:26-32 stores occ[c][i] = #c in bwt[0:i) for every i; here a sampled table
+ * (every 64 positions, all 256 symbols) answers the same query. */
+typedef struct {
+  const uint8_t* bwt;
+  uint64_t n;
+  uint32_t* samp; /* (n/64 + 1) x 256 */
+} occ_t;
+
+void* oracle_occ_new(const uint8_t* bwt, uint64_t n) {
+  occ_t* o = (occ_t*)malloc(sizeof(occ_t));
+  const uint64_t nb = n / 64 + 1;
+  o->bwt = bwt;
+  o->n = n;
+  o->samp = (uint32_t*)calloc(nb * 256, sizeof(uint32_t));
+  uint32_t cur[256] = {0};
+  for (uint64_t i = 0; i <= n; ++i) {
+    if ((i & 63) == 0) memcpy(o->samp + (i >> 6) * 256, cur, sizeof(cur));
+    if (i < n) cur[bwt[i]]++;
+  }
+  return o;
+}
+
+void oracle_occ_free(void* p) {
+  occ_t* o = (occ_t*)p;
+  if (!o) return;
+  free(o->samp);
+  free(o);
+}
+
+/* csa/enhanced_fm_index.py:34-40: rank(c, i) = occ[c][min(i, n)] (absent c -> 0; the caller
+ * handles absent symbols) */
+uint64_t oracle_occ(const void* p, uint8_t c, uint64_t i) {
+  const occ_t* o = (const occ_t*)p;
+  if (i > o->n) i = o->n;
+  uint64_t r = o->samp[(i >> 6) * 256 + c];
+  for (uint64_t k = i & ~(uint64_t)63; k < i; ++k) r += o->bwt[k] == c;
+  return r;
+}
+
+/* csa/enhanced_fm_index.py:21-32 backward search over P patterns (concatenated, offsets) */
+void oracle_find_range(const void* p, const uint64_t C[257], const uint8_t* present, const uint8_t* pats,
+                       const uint64_t* offs, uint64_t P, int64_t* lr) {
+  const occ_t* o = (const occ_t*)p;
+  for (uint64_t q = 0; q < P; ++q) {
+    int64_t l = 0, r = (int64_t)o->n - 1;
+    int ok = 1;
+    for (uint64_t k = offs[q + 1]; k > offs[q];) {
+      --k;
+      const uint8_t c = pats[k];
+      int64_t nl, nr;
+      if (!present[c]) {
+        nl = 0;
+        nr = -1;
+      } else {
+        nl = (int64_t)(oracle_occ(o, c, (uint64_t)l) + C[c]);
+        nr = (int64_t)(oracle_occ(o, c, (uint64_t)(r + 1)) + C[c]) - 1;
+      }
+      if (nl > nr) {
+        ok = 0;
+        break;
+      }
+      l = nl;
+      r = nr;
+    }
+    lr[2 * q] = ok ? l : -1;
+    lr[2 * q + 1] = ok ? r : -1;
+  }
+}
+
+/* ------------------------------------------------------------- SA checker
+ * O(n) proof that sa is THE suffix array of t (so it equals build_suffix_array's output):
+ * sa is a permutation and every adjacent pair is ordered — first symbols, then (when they are
+ * equal) the ranks of the suffixes one further, with end-of-text ranking lowest.
+ * Returns 0 when valid, 1 + offending index otherwise. */
+uint64_t oracle_check_sa(const uint8_t* t, uint64_t n, const uint64_t* sa) {
+  if (n == 0) return 0;
+  uint64_t* isa = (uint64_t*)malloc(n * sizeof(uint64_t));
+  for (uint64_t i = 0; i < n; ++i) isa[i] = UINT64_MAX;
+  for (uint64_t j = 0; j < n; ++j) {
+    if (sa[j] >= n || isa[sa[j]] != UINT64_MAX) {
+      free(isa);
+      return 1 + j;
+    }
+    isa[sa[j]] = j;
+  }
+  for (uint64_t j = 1; j < n; ++j) {
+    const uint64_t a = sa[j - 1], b = sa[j];
+    int ok;
+    if (t[a] != t[b]) ok = t[a] < t[b];
+    else if (a + 1 == n) ok = 1;          /* suffix a is a proper prefix of suffix b */
+    else if (b + 1 == n) ok = 0;
+    else ok = isa[a + 1] < isa[b + 1];
+    if (!ok) {
+      free(isa);
+      return 1 + j;
+    }
+  }
+  free(isa);
+  return 0;
+}
+
+/* ------------------------------------------------------------- synthetic text
+ * Same counter-based generator as the device (hk_sa.hip k_synth). */
+static uint64_t splitmix64(uint64_t x) {
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+
+void oracle_synth_text(uint64_t n, const uint8_t* alpha, int sigma, uint64_t seed, uint8_t term, uint8_t* out) {
+  const uint64_t key = seed * 0xD1B54A32D192ED03ull;
+  for (uint64_t i = 0; i < n; ++i) {
+    if (i + 1 == n) out[i] = term;
+    else out[i] = alpha[(uint32_t)(splitmix64(key ^ i) >> 32) % (uint32_t)sigma];
+  }
+}
+
+/* ------------------------------------------------------------- wavelet tree
+ * csa/wavelet_tree.py:72-100 splits a node's sorted alphabet at len//2 (bit 1 = right half) and
+ * stably filters the sequence into the children; the reference keeps only the leftmost child.
+ * This builds every node, level by level (nodes left to right), returning L levels of n bits
+ * (one byte per bit).  Symbols whose leaf is shallower keep bit 0 and their position. */
+int oracle_wt_levels(const uint8_t* seq, uint64_t n, uint8_t* bits /* 8*n */) {
+  int present[256] = {0}, code[256], sigma = 0;
+  for (uint64_t i = 0; i < n; ++i) present[seq[i]] = 1;
+  for (int c = 0; c < 256; ++c) code[c] = present[c] ? sigma++ : -1;
+  int L = 0;
+  while ((1 << L) < sigma) ++L;
+  uint64_t cnt[257] = {0};
+  for (uint64_t i = 0; i < n; ++i) cnt[code[seq[i]] + 1]++;
+  for (int c = 0; c < sigma; ++c) cnt[c + 1] += cnt[c]; /* cnt[c] = #codes < c */
+  int* cur = (int*)malloc((n + 1) * sizeof(int));
+  int* nxt = (int*)malloc((n + 1) * sizeof(int));
+  for (uint64_t i = 0; i < n; ++i) cur[i] = code[seq[i]];
+  for (int d = 0; d < L; ++d) {
+    uint64_t fill_left[256], fill_right[256];
+    int lo_of[256], hi_of[256], mid_of[256];
+    for (int c = 0; c < sigma; ++c) {
+      int lo = 0, hi = sigma;
+      for (int dd = 0; dd < d && hi - lo > 1; ++dd) {
+        int mid = lo + (hi - lo) / 2;
+        if (c >= mid) lo = mid; else hi = mid;
+      }
+      lo_of[c] = lo;
+      hi_of[c] = hi;
+      mid_of[c] = hi - lo > 1 ? lo + (hi - lo) / 2 : hi;
+    }
+    for (int c = 0; c < sigma; ++c) {
+      fill_left[c] = cnt[lo_of[c]];
+      fill_right[c] = cnt[mid_of[c]];
+    }
+    /* per node fill pointers, keyed by the node's lo */
+    uint64_t fl[256], fr[256];
+    for (int c = 0; c < sigma; ++c) {
+      fl[lo_of[c]] = fill_left[c];
+      fr[lo_of[c]] = fill_right[c];
+    }
+    for (uint64_t i = 0; i < n; ++i) {
+      const int c = cur[i];
+      const int b = (hi_of[c] - lo_of[c] > 1) && c >= mid_of[c];
+      bits[(uint64_t)d * n + i] = (uint8_t)b;
+      if (b) nxt[fr[lo_of[c]]++] = c;
+      else nxt[fl[lo_of[c]]++] = c;
+    }
+    int* tmp = cur;
+    cur = nxt;
+    nxt = tmp;
+  }
+  free(cur);
+  free(nxt);
+  return L;
+}
+
+/* ------------------------------------------------------------- shard partition
+ * Host restatement of the sharded build's partition (hk_shard.hip): the key of a suffix packs
+ * its first q dense codes (code 0 past the end), b bits each; its bucket is the top 14 bits. */
+void oracle_shard_geometry(const uint8_t* t, uint64_t n, int* b, int* q, int* bsh, uint8_t lut[256]) {
+  int present[256] = {0}, sigma = 0;
+  for (uint64_t i = 0; i < n; ++i) present[t[i]] = 1;
+  for (int c = 0; c < 256; ++c) lut[c] = present[c] ? (uint8_t)(++sigma) : 0;
+  int bb = 1;
+  while ((1 << bb) < sigma + 1) ++bb;
+  *b = bb;
+  *q = 64 / bb;
+  *bsh = *q * bb - 14;
+  if (*bsh < 0) *bsh = 0;
+}
+
+void oracle_shard_hist(const uint8_t* t, uint64_t n, uint64_t lo, uint64_t hi, uint64_t* hist /* 16384 */) {
+  int b, q, bsh;
+  uint8_t lut[256];
+  oracle_shard_geometry(t, n, &b, &q, &bsh, lut);
+  memset(hist, 0, 16384 * sizeof(uint64_t));
+  for (uint64_t p = lo; p < hi; ++p) {
+    uint64_t key = 0;
+    for (int j = 0; j < q; ++j) key = (key << b) | (p + j < n ? lut[t[p + j]] : 0);
+    hist[key >> bsh]++;
+  }
+}
