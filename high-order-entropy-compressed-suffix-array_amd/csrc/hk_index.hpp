@@ -17,6 +17,13 @@ struct WtTables {                // per level, per dense code (host mirror of th
   uint8_t depth[256];
 };
 
+// suffix key layout: [q dense codes of b bits][prev-symbol code, pb bits (0 or b)]
+struct KeyGeom {
+  int b = 0, q = 0, pb = 0, key_bits = 0;
+  uint16_t lut[256];   // byte -> dense code + 1 (0 = end of text)
+  uint8_t inv[512];    // dense code + 1 -> byte
+};
+
 // kernel argument bundle for rank walks
 struct WtView {
   const uint64_t* lines[kMaxLevels];
@@ -61,6 +68,7 @@ struct Index {
   DevBuf keys[2], vals[2];
   DevBuf isa;
   DevBuf act[2][3];            // P, J, G of the active list (double-buffered)
+  DevBuf head_slot;            // SA slot of each tied group's head (refinement -> doubling switch)
   DevBuf tile_a, tile_b, tile_c, tile_d;
   DevBuf small;                // scratch for totals etc.
   DevBuf seq[2];               // WT level code sequences
@@ -101,8 +109,12 @@ void shard_get_sa(Index& ix, uint64_t a, uint64_t b, uint64_t* out);
 void build_sa_sharded(Index& ix, const uint8_t id[128], int nranks, int rank);
 void comm_unique_id(uint8_t id[128]);
 
-// shared with the SA code: pack q symbols of b bits each into a key
-void pack_keys(const uint8_t* d_text, uint64_t n, uint64_t lo, uint64_t count, const uint8_t* d_lut,
-               int b, int q, uint64_t* d_keys, hipStream_t s);
+// shared by the single-GPU and sharded builds
+KeyGeom key_geometry(Index& ix, bool with_prev);
+void upload_geometry(Index& ix, const KeyGeom& kg);
+void pack_keys(const uint8_t* d_text, uint64_t n, uint64_t lo, uint64_t count, const uint16_t* d_lut, int b, int q,
+               int pb, uint64_t* d_keys, hipStream_t s);
+template <typename V>
+void refine_after_sort(Index& ix, const KeyGeom& kg, int slot, uint64_t m, bool allow_doubling);
 
 }  // namespace hk

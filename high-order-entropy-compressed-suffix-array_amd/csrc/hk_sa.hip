@@ -1,4 +1,5 @@
-// hk_sa.hip — suffix array by GPU prefix doubling, BWT gather, alphabet/C array.
+// hk_sa.hip — suffix array + BWT construction (single GPU), the refinement loop shared with the
+// sharded build, alphabet/C array and the synthetic-text generator.
 //
 // Semantics follow the reference exactly (SURVEY.md §8 "Exact semantics"):
 //   * SA of T' in Python str order (csa/suffix_array.py:131-134): symbols compare by byte
@@ -6,23 +7,33 @@
 //   * BWT[j] = T'[SA[j]-1], wrapping to T'[n-1] (csa/bwt.py:3-13).
 //   * C[c] = #{symbols < c} (utils/utils.py:16-24).
 //
-// Algorithm (MI355X-first, not a translation of anything in the reference):
-//   1. pack the first q symbols of every suffix into a u64 key (b bits per dense code,
-//      code 0 = end of text), so one LSD radix sort orders suffixes by q symbols;
-//   2. head flags + max-scan give every suffix its group start ("h-rank") in the ISA;
-//      singleton groups are final and leave the active list;
-//   3. each doubling round sorts the active suffixes by (group, ISA[p+h]) and splits groups
-//      until none remain — the classic prefix-doubling invariant, restricted to active suffixes.
+// Algorithm (MI355X-first):
+//   1. every suffix p gets a u64 key = [its first q dense codes, b bits each, code 0 past the
+//      end] [code of T'[p-1]] — the low field is not sorted on; it rides along so that the BWT
+//      symbol of every sorted suffix is read straight out of the sorted keys (no random
+//      gather over the text for the BWT);
+//   2. one onesweep LSD radix sort orders the suffixes by q symbols (HBM-bound passes);
+//   3. tied groups (equal q-prefix) are refined without any rank array: each round sorts the
+//      tied suffixes by (dense group ordinal, next symbols of the suffix read from T');
+//   4. if ties persist for several rounds (long repeats), the build switches to prefix
+//      doubling: it materialises ISA once and sorts the tied suffixes by (group start,
+//      ISA[p+h]), doubling h until no ties remain.
+// High-entropy texts (the sigma=4 bench configs) finish after step 3's first round.
 
 #include "hk_index.hpp"
 
 namespace hk {
 namespace {
 
-// --------------------------------------------------------------- helpers
 constexpr int GR_T = 256;
 constexpr int GR_I = 16;
 constexpr int GR_TILE = GR_T * GR_I;
+constexpr int kChunkRounds = 4;   // refinement rounds before switching to prefix doubling
+
+inline unsigned grid_for(uint64_t n, unsigned per = 256, unsigned cap = 16384) {
+  uint64_t g = ceil_div(n ? n : 1, per);
+  return (unsigned)(g < cap ? g : cap);
+}
 
 __device__ __forceinline__ uint64_t blk_excl_sum(uint64_t v, uint64_t* red, uint64_t* total) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -55,7 +66,7 @@ __device__ __forceinline__ uint64_t blk_excl_max(uint64_t v, uint64_t* red) {
   return carry > exc ? carry : exc;
 }
 
-// ---------------------------------------------------------- kernels
+// ------------------------------------------------------------- alphabet
 __global__ __launch_bounds__(256) void k_byte_hist(const uint8_t* __restrict__ t, uint64_t n,
                                                    unsigned long long* __restrict__ hist) {
   __shared__ uint32_t h[4][256];
@@ -79,20 +90,23 @@ __global__ __launch_bounds__(256) void k_byte_hist(const uint8_t* __restrict__ t
   if (c) atomicAdd(&hist[threadIdx.x], (unsigned long long)c);
 }
 
-// key[i-lo] = code(T[i]) .. code(T[i+q-1]) packed MSB-first, b bits each, code 0 past the end
+// ------------------------------------------------------------- keys
+// key(p) = [code(T[p]) .. code(T[p+q-1])] << pb | code(T[p-1])   (pb = prev-field bits, 0 or b)
 constexpr int PK_TILE = 4096;
-__global__ __launch_bounds__(256) void k_pack_keys(const uint8_t* __restrict__ t, uint64_t n,
-                                                   uint64_t lo, uint64_t count,
-                                                   const uint8_t* __restrict__ lut, int b, int q,
-                                                   uint64_t* __restrict__ keys) {
-  __shared__ uint8_t c[PK_TILE + 64];
-  __shared__ uint8_t L[256];
+__global__ __launch_bounds__(256) void k_pack_keys(const uint8_t* __restrict__ t, uint64_t n, uint64_t lo,
+                                                   uint64_t count, const uint16_t* __restrict__ lut, int b,
+                                                   int q, int pb, uint64_t* __restrict__ keys) {
+  __shared__ uint16_t c[PK_TILE + 72];
+  __shared__ uint16_t L[256];
   L[threadIdx.x] = lut[threadIdx.x];
   __syncthreads();
   const uint64_t base = lo + (uint64_t)blockIdx.x * PK_TILE;
-  for (int i = threadIdx.x; i < PK_TILE + q; i += 256) {
-    const uint64_t p = base + i;
-    c[i] = p < n ? L[t[p]] : 0;
+  for (int i = threadIdx.x; i < PK_TILE + q + 1; i += 256) {
+    const uint64_t p = base + i;  // c[i] holds position base + i - 1
+    uint16_t v;
+    if (i == 0) v = L[t[base == 0 ? n - 1 : base - 1]];
+    else v = (p - 1) < n ? L[t[p - 1]] : 0;
+    c[i] = v;
   }
   __syncthreads();
   const uint64_t end = lo + count;
@@ -102,117 +116,195 @@ __global__ __launch_bounds__(256) void k_pack_keys(const uint8_t* __restrict__ t
     const uint64_t p = base + off;
     if (p < end) {
       uint64_t key = 0;
-      for (int j = 0; j < q; ++j) key = (key << b) | c[off + j];
-      keys[p - lo] = key;
+      for (int j = 1; j <= q; ++j) key = (key << b) | c[off + j];
+      keys[p - lo] = (key << pb) | (pb ? c[off] : 0u);
     }
   }
 }
 
-// per tile: index (or J value) of the last group head, number of suffixes in non-singleton groups
-template <bool HAS_J>
-__global__ __launch_bounds__(GR_T) void k_group_stats(const uint64_t* __restrict__ keys,
-                                                      const uint32_t* __restrict__ J, uint64_t A,
-                                                      uint64_t* __restrict__ tile_last,
-                                                      uint32_t* __restrict__ tile_act) {
-  __shared__ uint64_t red[GR_T / 64];
-  const uint64_t base = (uint64_t)blockIdx.x * GR_TILE + (uint64_t)threadIdx.x * GR_I;
-  int64_t last = -1;
-  uint32_t act = 0;
-  if (base < A) {
-    uint64_t prev = base > 0 ? keys[base - 1] : 0;
-    uint64_t cur = keys[base];
+// ------------------------------------------------------------- refinement
+// A tile of GR_TILE sorted keys (+1 halo each side) is staged in LDS with one pad slot per 16
+// elements, so thread t's 16 consecutive items are read conflict-free (stride 17 x u64).
+constexpr int GR_LDS = GR_TILE + 2 + (GR_TILE + 2) / 16 + 1;
+__device__ __forceinline__ int lpad(int e) { return e + (e >> 4); }
+
+__device__ __forceinline__ void stage_tile_keys(const uint64_t* __restrict__ keys, uint64_t A, uint64_t tbase,
+                                                uint64_t* L) {
+  for (int i = threadIdx.x; i < GR_TILE + 2; i += GR_T) {
+    const uint64_t j = tbase + i - 1;  // slot i holds key[tbase + i - 1]
+    L[lpad(i)] = (tbase + i >= 1 && j < A) ? keys[j] : 0;
+  }
+  __syncthreads();
+}
+
+// head / tied masks of thread t's 16 items from the staged tile
+__device__ __forceinline__ void tile_masks(const uint64_t* L, uint64_t tbase, uint64_t A, int cs, uint32_t& hmask,
+                                           uint32_t& amask) {
+  hmask = amask = 0;
+  const int e0 = threadIdx.x * GR_I;
+  uint64_t prev = L[lpad(e0)] >> cs, cur = L[lpad(e0 + 1)] >> cs;
 #pragma unroll
-    for (int i = 0; i < GR_I; ++i) {
-      const uint64_t j = base + i;
-      if (j >= A) break;
-      const uint64_t nxt = j + 1 < A ? keys[j + 1] : 0;
-      const bool h = (j == 0) || cur != prev;
-      const bool hn = (j + 1 >= A) || nxt != cur;
-      if (h) last = (int64_t)j;
-      act += (h && hn) ? 0u : 1u;
-      prev = cur;
-      cur = nxt;
+  for (int i = 0; i < GR_I; ++i) {
+    const uint64_t j = tbase + e0 + i;
+    const uint64_t nxt = L[lpad(e0 + i + 2)] >> cs;
+    if (j < A) {
+      const bool h = j == 0 || cur != prev;
+      const bool hn = j + 1 >= A || nxt != cur;
+      if (!(h && hn)) {
+        amask |= 1u << i;
+        if (h) hmask |= 1u << i;
+      }
     }
+    prev = cur;
+    cur = nxt;
   }
-  // block max of `last` (as last+1, 0 = none) and sum of act
-  uint64_t lv = (uint64_t)(last + 1);
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    uint64_t t = __shfl_xor(lv, o, 64);
-    lv = lv > t ? lv : t;
-    act += __shfl_xor(act, o, 64);
-  }
-  __shared__ uint32_t redc[GR_T / 64];
+}
+
+// per tile: suffixes in tied groups, and heads of tied groups (keys compared >> cs)
+__global__ __launch_bounds__(GR_T) void k_refine_stats(const uint64_t* __restrict__ keys, uint64_t A, int cs,
+                                                       uint32_t* __restrict__ tact, uint32_t* __restrict__ thead) {
+  __shared__ uint64_t L[GR_LDS];
+  __shared__ uint32_t ra[4], rh[4];
+  const uint64_t tbase = (uint64_t)blockIdx.x * GR_TILE;
+  stage_tile_keys(keys, A, tbase, L);
+  uint32_t hmask, amask;
+  tile_masks(L, tbase, A, cs, hmask, amask);
+  const uint32_t act = wave_sum<uint32_t>((uint32_t)__popc(amask));
+  const uint32_t hd = wave_sum<uint32_t>((uint32_t)__popc(hmask));
   if ((threadIdx.x & 63) == 0) {
-    red[threadIdx.x >> 6] = lv;
-    redc[threadIdx.x >> 6] = act;
+    ra[threadIdx.x >> 6] = act;
+    rh[threadIdx.x >> 6] = hd;
   }
   __syncthreads();
   if (threadIdx.x == 0) {
-    uint64_t m = 0;
-    uint32_t c = 0;
-    for (int i = 0; i < GR_T / 64; ++i) {
-      m = m > red[i] ? m : red[i];
-      c += redc[i];
-    }
-    uint64_t v = 0;
-    if (m) v = HAS_J ? (uint64_t)J[m - 1] : (m - 1);
-    tile_last[blockIdx.x] = v;
-    tile_act[blockIdx.x] = c;
+    tact[blockIdx.x] = ra[0] + ra[1] + ra[2] + ra[3];
+    thead[blockIdx.x] = rh[0] + rh[1] + rh[2] + rh[3];
   }
 }
 
-// assign group starts, update ISA (and SA for doubling rounds), compact the active list
-template <bool HAS_J>
-__global__ __launch_bounds__(GR_T) void k_group_apply(
-    const uint64_t* __restrict__ keys, const uint32_t* __restrict__ P, const uint32_t* __restrict__ J,
-    uint64_t A, const uint64_t* __restrict__ carry_last, const uint64_t* __restrict__ act_off,
-    uint32_t* __restrict__ isa, uint32_t* __restrict__ sa, uint32_t* __restrict__ oP,
-    uint32_t* __restrict__ oJ, uint32_t* __restrict__ oG) {
-  __shared__ uint64_t red[GR_T / 64];
-  const uint64_t base = (uint64_t)blockIdx.x * GR_TILE + (uint64_t)threadIdx.x * GR_I;
-  uint32_t hmask = 0, amask = 0;
-  uint64_t tmax = 0;
-  if (base < A) {
-    uint64_t prev = base > 0 ? keys[base - 1] : 0;
-    uint64_t cur = keys[base];
+// writes SA / BWT entries of every suffix and compacts tied suffixes with their group ordinal.
+// FROM_KEY (initial round, J == identity, SA already in place): the BWT symbol is the key's low
+// field and P is read only for tied suffixes; otherwise BWT symbols are gathered from T'.
+template <typename V, bool FROM_KEY>
+__global__ __launch_bounds__(GR_T) void k_refine_apply(
+    const uint64_t* __restrict__ keys, const V* __restrict__ P, const uint32_t* __restrict__ J, uint64_t A,
+    int cs, const uint64_t* __restrict__ act_off, const uint64_t* __restrict__ head_off, V* __restrict__ sa,
+    uint8_t* __restrict__ bwt, const uint8_t* __restrict__ inv, uint64_t pmask, const uint8_t* __restrict__ t,
+    uint64_t n, V* __restrict__ oP, uint32_t* __restrict__ oJ, uint32_t* __restrict__ oG,
+    uint32_t* __restrict__ head_slot) {
+  __shared__ uint64_t L[GR_LDS];
+  __shared__ uint32_t ra[4], rh[4];
+  __shared__ uint8_t INV[512];
+  if (FROM_KEY) {
+    INV[threadIdx.x] = inv[threadIdx.x];
+    INV[threadIdx.x + 256] = inv[threadIdx.x + 256];
+  }
+  const uint64_t tbase = (uint64_t)blockIdx.x * GR_TILE;
+  stage_tile_keys(keys, A, tbase, L);
+  uint32_t hmask, amask;
+  tile_masks(L, tbase, A, cs, hmask, amask);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const uint32_t ca = __popc(amask), ch = __popc(hmask);
+  const uint32_t ia = wave_incl_sum<uint32_t>(ca), ih = wave_incl_sum<uint32_t>(ch);
+  if (lane == 63) {
+    ra[w] = ia;
+    rh[w] = ih;
+  }
+  __syncthreads();
+  uint64_t oa = act_off[blockIdx.x], oh = head_off[blockIdx.x];
+  for (int i = 0; i < w; ++i) {
+    oa += ra[i];
+    oh += rh[i];
+  }
+  oa += ia - ca;
+  oh += ih - ch;
+  const uint64_t base = tbase + (uint64_t)threadIdx.x * GR_I;
+  if (FROM_KEY && bwt) {
+    // BWT symbols of the 16 items straight from the prev field of the (unshifted) keys
+    if (base + GR_I <= A) {
+      uint32_t wv[4] = {0, 0, 0, 0};
 #pragma unroll
-    for (int i = 0; i < GR_I; ++i) {
-      const uint64_t j = base + i;
-      if (j >= A) break;
-      const uint64_t nxt = j + 1 < A ? keys[j + 1] : 0;
-      const bool h = (j == 0) || cur != prev;
-      const bool hn = (j + 1 >= A) || nxt != cur;
-      if (h) {
-        hmask |= 1u << i;
-        tmax = HAS_J ? (uint64_t)J[j] : j;
+      for (int i = 0; i < GR_I; ++i) {
+        const uint32_t sym = INV[(uint32_t)(L[lpad(threadIdx.x * GR_I + i + 1)] & pmask)];
+        wv[i >> 2] |= sym << (8 * (i & 3));
       }
-      if (!(h && hn)) amask |= 1u << i;
-      prev = cur;
-      cur = nxt;
+      *reinterpret_cast<uint4*>(bwt + base) = make_uint4(wv[0], wv[1], wv[2], wv[3]);
+    } else {
+      for (int i = 0; i < GR_I; ++i)
+        if (base + i < A) bwt[base + i] = INV[(uint32_t)(L[lpad(threadIdx.x * GR_I + i + 1)] & pmask)];
     }
   }
-  const uint64_t carry = carry_last[blockIdx.x];
-  uint64_t gpre = blk_excl_max(tmax, red);
-  gpre = gpre > carry ? gpre : carry;
-  uint64_t tot;
-  uint64_t o = blk_excl_sum((uint64_t)__popc(amask), red, &tot) + act_off[blockIdx.x];
-  uint64_t g = gpre;
-#pragma unroll
+  uint64_t g = oh;  // tied-group heads before this thread's first item
   for (int i = 0; i < GR_I; ++i) {
     const uint64_t j = base + i;
     if (j >= A) break;
-    const uint32_t jv = HAS_J ? J[j] : (uint32_t)j;
-    if (hmask & (1u << i)) g = jv;
-    const uint32_t p = P[j];
-    isa[p] = (uint32_t)g;
-    if (HAS_J) sa[jv] = p;
-    if (amask & (1u << i)) {
-      oP[o] = p;
-      oJ[o] = jv;
-      oG[o] = (uint32_t)g;
-      ++o;
+    if (FROM_KEY) {
+      if (!(amask & (1u << i))) continue;
+      const V p = P[j];
+      if (hmask & (1u << i)) {
+        ++g;
+        if (head_slot) head_slot[g - 1] = (uint32_t)j;
+      }
+      oP[oa] = p;
+      oJ[oa] = (uint32_t)j;
+      oG[oa] = (uint32_t)(g - 1);
+      ++oa;
+    } else {
+      const uint32_t jv = J ? J[j] : (uint32_t)j;
+      const V p = P[j];
+      if (sa) sa[jv] = p;
+      if (bwt) bwt[jv] = t[p == 0 ? n - 1 : (uint64_t)p - 1];
+      if (amask & (1u << i)) {
+        if (hmask & (1u << i)) {
+          ++g;
+          if (head_slot) head_slot[g - 1] = jv;
+        }
+        oP[oa] = p;
+        oJ[oa] = jv;
+        oG[oa] = (uint32_t)(g - 1);
+        ++oa;
+      }
     }
+  }
+}
+
+// chunk refinement key: (group ordinal << (64-gbits)) | next qn codes of the suffix from offset h
+template <typename V>
+__global__ __launch_bounds__(256) void k_refine_keys(const V* __restrict__ P, const uint32_t* __restrict__ G,
+                                                     uint64_t A, const uint8_t* __restrict__ t, uint64_t n,
+                                                     const uint16_t* __restrict__ lut, int b, int qn, int gbits,
+                                                     uint64_t h, uint64_t* __restrict__ keys, V* __restrict__ vals) {
+  __shared__ uint16_t L[256];
+  L[threadIdx.x] = lut[threadIdx.x];
+  __syncthreads();
+  for (uint64_t a = (uint64_t)blockIdx.x * 256 + threadIdx.x; a < A; a += (uint64_t)gridDim.x * 256) {
+    const V p = P[a];
+    const uint64_t s = (uint64_t)p + h;
+    uint64_t chunk = 0;
+    for (int j = 0; j < qn; ++j) {
+      const uint64_t x = s + j;
+      chunk = (chunk << b) | (x < n ? L[t[x]] : 0u);
+    }
+    keys[a] = gbits ? (((uint64_t)G[a] << (64 - gbits)) | chunk) : chunk;
+    vals[a] = p;
+  }
+}
+
+// ------------------------------------------------------------- prefix doubling (u32 positions)
+__global__ __launch_bounds__(256) void k_isa_all(const uint32_t* __restrict__ sa, uint64_t n,
+                                                 uint32_t* __restrict__ isa) {
+  for (uint64_t j = (uint64_t)blockIdx.x * 256 + threadIdx.x; j < n; j += (uint64_t)gridDim.x * 256)
+    isa[sa[j]] = (uint32_t)j;
+}
+
+// tied suffixes: ISA = their group start slot; G becomes the group start slot
+__global__ __launch_bounds__(256) void k_isa_active(const uint32_t* __restrict__ P, uint32_t* __restrict__ G,
+                                                    uint64_t A, const uint32_t* __restrict__ head_slot,
+                                                    uint32_t* __restrict__ isa) {
+  for (uint64_t a = (uint64_t)blockIdx.x * 256 + threadIdx.x; a < A; a += (uint64_t)gridDim.x * 256) {
+    const uint32_t s = head_slot[G[a]];
+    isa[P[a]] = s;
+    G[a] = s;
   }
 }
 
@@ -228,6 +320,108 @@ __global__ __launch_bounds__(256) void k_pair_keys(const uint32_t* __restrict__ 
     const uint64_t s = q < n ? (uint64_t)isa[q] + 1 : 0;
     keys[a] = ((uint64_t)G[a] << 32) | s;
     vals[a] = p;
+  }
+}
+
+// per tile: J of the last group head and the number of tied suffixes
+__global__ __launch_bounds__(GR_T) void k_group_stats(const uint64_t* __restrict__ keys,
+                                                      const uint32_t* __restrict__ J, uint64_t A,
+                                                      uint64_t* __restrict__ tile_last,
+                                                      uint32_t* __restrict__ tile_act) {
+  __shared__ uint64_t red[GR_T / 64];
+  __shared__ uint32_t redc[GR_T / 64];
+  const uint64_t base = (uint64_t)blockIdx.x * GR_TILE + (uint64_t)threadIdx.x * GR_I;
+  int64_t last = -1;
+  uint32_t act = 0;
+  if (base < A) {
+    uint64_t prev = base > 0 ? keys[base - 1] : 0;
+    uint64_t cur = keys[base];
+    for (int i = 0; i < GR_I; ++i) {
+      const uint64_t j = base + i;
+      if (j >= A) break;
+      const uint64_t nxt = j + 1 < A ? keys[j + 1] : 0;
+      const bool h = (j == 0) || cur != prev;
+      const bool hn = (j + 1 >= A) || nxt != cur;
+      if (h) last = (int64_t)j;
+      act += (h && hn) ? 0u : 1u;
+      prev = cur;
+      cur = nxt;
+    }
+  }
+  uint64_t lv = (uint64_t)(last + 1);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    uint64_t tt = __shfl_xor(lv, o, 64);
+    lv = lv > tt ? lv : tt;
+    act += __shfl_xor(act, o, 64);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    red[threadIdx.x >> 6] = lv;
+    redc[threadIdx.x >> 6] = act;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint64_t m = 0;
+    uint32_t c = 0;
+    for (int i = 0; i < GR_T / 64; ++i) {
+      m = m > red[i] ? m : red[i];
+      c += redc[i];
+    }
+    tile_last[blockIdx.x] = m ? (uint64_t)J[m - 1] : 0;
+    tile_act[blockIdx.x] = c;
+  }
+}
+
+// doubling round: group starts into ISA, SA/BWT entries, compaction of the still-tied suffixes
+__global__ __launch_bounds__(GR_T) void k_group_apply(
+    const uint64_t* __restrict__ keys, const uint32_t* __restrict__ P, const uint32_t* __restrict__ J,
+    uint64_t A, const uint64_t* __restrict__ carry_last, const uint64_t* __restrict__ act_off,
+    uint32_t* __restrict__ isa, uint32_t* __restrict__ sa, uint8_t* __restrict__ bwt,
+    const uint8_t* __restrict__ t, uint64_t n, uint32_t* __restrict__ oP, uint32_t* __restrict__ oJ,
+    uint32_t* __restrict__ oG) {
+  __shared__ uint64_t red[GR_T / 64];
+  const uint64_t base = (uint64_t)blockIdx.x * GR_TILE + (uint64_t)threadIdx.x * GR_I;
+  uint32_t hmask = 0, amask = 0;
+  uint64_t tmax = 0;
+  if (base < A) {
+    uint64_t prev = base > 0 ? keys[base - 1] : 0;
+    uint64_t cur = keys[base];
+    for (int i = 0; i < GR_I; ++i) {
+      const uint64_t j = base + i;
+      if (j >= A) break;
+      const uint64_t nxt = j + 1 < A ? keys[j + 1] : 0;
+      const bool h = (j == 0) || cur != prev;
+      const bool hn = (j + 1 >= A) || nxt != cur;
+      if (h) {
+        hmask |= 1u << i;
+        tmax = J[j];
+      }
+      if (!(h && hn)) amask |= 1u << i;
+      prev = cur;
+      cur = nxt;
+    }
+  }
+  const uint64_t carry = carry_last[blockIdx.x];
+  uint64_t gpre = blk_excl_max(tmax, red);
+  gpre = gpre > carry ? gpre : carry;
+  uint64_t tot;
+  uint64_t o = blk_excl_sum((uint64_t)__popc(amask), red, &tot) + act_off[blockIdx.x];
+  uint64_t g = gpre;
+  for (int i = 0; i < GR_I; ++i) {
+    const uint64_t j = base + i;
+    if (j >= A) break;
+    const uint32_t jv = J[j];
+    if (hmask & (1u << i)) g = jv;
+    const uint32_t p = P[j];
+    isa[p] = (uint32_t)g;
+    sa[jv] = p;
+    bwt[jv] = t[p == 0 ? n - 1 : p - 1];
+    if (amask & (1u << i)) {
+      oP[o] = p;
+      oJ[o] = jv;
+      oG[o] = (uint32_t)g;
+      ++o;
+    }
   }
 }
 
@@ -272,12 +466,7 @@ __global__ __launch_bounds__(256) void k_synth(uint8_t* __restrict__ t, uint64_t
   }
 }
 
-inline unsigned grid_for(uint64_t n, unsigned per = 256, unsigned cap = 16384) {
-  uint64_t g = ceil_div(n ? n : 1, per);
-  return (unsigned)(g < cap ? g : cap);
-}
-
-// one grouping step over A sorted keys. Returns the new active count.
+// one doubling grouping step over A sorted pair keys; returns the new tied count
 uint64_t group_step(Index& ix, const uint64_t* keys, const uint32_t* P, const uint32_t* J, uint64_t A,
                     uint32_t* oP, uint32_t* oJ, uint32_t* oG) {
   hipStream_t s = ix.stream;
@@ -291,21 +480,16 @@ uint64_t group_step(Index& ix, const uint64_t* keys, const uint32_t* P, const ui
   uint64_t* cl = ix.tile_c.as<uint64_t>();
   uint64_t* ao = ix.tile_d.as<uint64_t>();
   {
-    TimedLaunch t(ix.timer, "sa_group_stats", (double)A * 8);
-    if (J) k_group_stats<true><<<(unsigned)nt, GR_T, 0, s>>>(keys, J, A, tl, ta);
-    else k_group_stats<false><<<(unsigned)nt, GR_T, 0, s>>>(keys, J, A, tl, ta);
+    TimedLaunch tm(ix.timer, "sa_group_stats", (double)A * 8);
+    k_group_stats<<<(unsigned)nt, GR_T, 0, s>>>(keys, J, A, tl, ta);
     HK_HIP(hipGetLastError());
   }
   scan_exclusive_max_u64(ix.sw, tl, cl, nt, s);
   scan_exclusive_u32_to_u64(ix.sw, ta, ao, nt, true, s);
   {
-    TimedLaunch t(ix.timer, "sa_group_apply", (double)A * (8 + 4 + 4 + 4 + (J ? 8 : 0)));
-    if (J)
-      k_group_apply<true><<<(unsigned)nt, GR_T, 0, s>>>(keys, P, J, A, cl, ao, ix.isa.as<uint32_t>(),
-                                                        ix.sa.as<uint32_t>(), oP, oJ, oG);
-    else
-      k_group_apply<false><<<(unsigned)nt, GR_T, 0, s>>>(keys, P, J, A, cl, ao, ix.isa.as<uint32_t>(),
-                                                         ix.sa.as<uint32_t>(), oP, oJ, oG);
+    TimedLaunch tm(ix.timer, "sa_group_apply", (double)A * (8 + 4 + 4 + 4 + 4 + 1));
+    k_group_apply<<<(unsigned)nt, GR_T, 0, s>>>(keys, P, J, A, cl, ao, ix.isa.as<uint32_t>(), ix.sa.as<uint32_t>(),
+                                               ix.bwt.as<uint8_t>(), ix.text.as<uint8_t>(), ix.n, oP, oJ, oG);
     HK_HIP(hipGetLastError());
   }
   uint64_t na = 0;
@@ -314,13 +498,169 @@ uint64_t group_step(Index& ix, const uint64_t* keys, const uint32_t* P, const ui
   return na;
 }
 
+// one refinement grouping step (stats + scans + apply); returns (tied, groups)
+template <typename V>
+std::pair<uint64_t, uint64_t> refine_step(Index& ix, const KeyGeom& kg, const uint64_t* keys, const V* P,
+                                          const uint32_t* J, uint64_t A, int cs, bool from_key, bool write_sa,
+                                          V* oP, uint32_t* oJ, uint32_t* oG, uint32_t* head_slot) {
+  hipStream_t s = ix.stream;
+  const uint64_t nt = ceil_div(A, GR_TILE);
+  ix.tile_b.ensure((nt + 1) * 4);
+  ix.tile_c.ensure((nt + 1) * 4);
+  ix.tile_a.ensure((nt + 2) * 8);
+  ix.tile_d.ensure((nt + 2) * 8);
+  {
+    TimedLaunch tm(ix.timer, "sa_refine_stats", (double)A * 8);
+    k_refine_stats<<<(unsigned)nt, GR_T, 0, s>>>(keys, A, cs, ix.tile_b.as<uint32_t>(), ix.tile_c.as<uint32_t>());
+    HK_HIP(hipGetLastError());
+  }
+  scan_exclusive_u32_to_u64(ix.sw, ix.tile_b.as<uint32_t>(), ix.tile_a.as<uint64_t>(), nt, true, s);
+  scan_exclusive_u32_to_u64(ix.sw, ix.tile_c.as<uint32_t>(), ix.tile_d.as<uint64_t>(), nt, true, s);
+  uint8_t* bwt = ix.bwt.as<uint8_t>();
+  const uint8_t* inv = ix.small.as<uint8_t>() + 3072;
+  {
+    TimedLaunch tm(ix.timer, "sa_refine_apply", (double)A * (8 + sizeof(V) + (write_sa ? sizeof(V) + 4 : 0) + 1));
+    if (from_key)
+      k_refine_apply<V, true><<<(unsigned)nt, GR_T, 0, s>>>(
+          keys, P, J, A, cs, ix.tile_a.as<uint64_t>(), ix.tile_d.as<uint64_t>(), write_sa ? ix.sa.as<V>() : nullptr,
+          bwt, inv, (1ull << kg.pb) - 1, ix.text.as<uint8_t>(), ix.n, oP, oJ, oG, head_slot);
+    else
+      k_refine_apply<V, false><<<(unsigned)nt, GR_T, 0, s>>>(
+          keys, P, J, A, cs, ix.tile_a.as<uint64_t>(), ix.tile_d.as<uint64_t>(), write_sa ? ix.sa.as<V>() : nullptr,
+          bwt, inv, 0, ix.text.as<uint8_t>(), ix.n, oP, oJ, oG, head_slot);
+    HK_HIP(hipGetLastError());
+  }
+  uint64_t tot[2];
+  HK_HIP(hipMemcpyAsync(&tot[0], ix.tile_a.as<uint64_t>() + nt, 8, hipMemcpyDeviceToHost, s));
+  HK_HIP(hipMemcpyAsync(&tot[1], ix.tile_d.as<uint64_t>() + nt, 8, hipMemcpyDeviceToHost, s));
+  HK_HIP(hipStreamSynchronize(s));
+  return {tot[0], tot[1]};
+}
+
 }  // namespace
 
-void pack_keys(const uint8_t* d_text, uint64_t n, uint64_t lo, uint64_t count, const uint8_t* d_lut,
-               int b, int q, uint64_t* d_keys, hipStream_t s) {
+// ---------------------------------------------------------------- geometry
+KeyGeom key_geometry(Index& ix, bool with_prev) {
+  compute_alphabet(ix);
+  KeyGeom g{};
+  g.b = 1;
+  while ((1 << g.b) < ix.sigma + 1) ++g.b;
+  g.pb = with_prev ? g.b : 0;
+  g.q = (64 - g.pb) / g.b;
+  g.key_bits = g.q * g.b + g.pb;
+  for (int c = 0; c < 256; ++c) g.lut[c] = ix.code_of[c] < 0 ? 0 : (uint16_t)(ix.code_of[c] + 1);
+  memset(g.inv, 0, sizeof(g.inv));
+  for (int k = 0; k < ix.sigma; ++k) g.inv[k + 1] = ix.syms[k];
+  return g;
+}
+
+// device copies of the LUTs: small+2048 = lut (u16[256]), small+3072 = inv (u8[512])
+void upload_geometry(Index& ix, const KeyGeom& kg) {
+  ix.small.ensure(8192);
+  HK_HIP(hipMemcpyAsync(ix.small.as<uint8_t>() + 2048, kg.lut, 512, hipMemcpyHostToDevice, ix.stream));
+  HK_HIP(hipMemcpyAsync(ix.small.as<uint8_t>() + 3072, kg.inv, 512, hipMemcpyHostToDevice, ix.stream));
+}
+
+// Refinement of tied groups after the initial sort of m suffixes (their sorted keys in keys[slot],
+// positions in vals[slot] — which the caller has adopted as ix.sa).  With allow_doubling (single
+// GPU, u32 positions) the loop switches to ISA-based prefix doubling after kChunkRounds rounds.
+template <typename V>
+void refine_after_sort(Index& ix, const KeyGeom& kg, int slot, uint64_t m, bool allow_doubling) {
+  hipStream_t s = ix.stream;
+  const uint16_t* d_lut = reinterpret_cast<const uint16_t*>(ix.small.as<uint8_t>() + 2048);
+  uint64_t* kp[2] = {ix.keys[0].as<uint64_t>(), ix.keys[1].as<uint64_t>()};
+  V* vp[2] = {ix.vals[0].as<V>(), ix.vals[1].as<V>()};
+  for (int i = 0; i < 2; ++i) {
+    ix.act[i][0].ensure(m * sizeof(V) + 16);
+    ix.act[i][1].ensure(m * 4 + 16);
+    ix.act[i][2].ensure(m * 4 + 16);
+  }
+  ix.head_slot.ensure(m * 4 + 16);
+  ix.bwt.ensure(m + 64);
+  int cur = 0;
+  // initial round: keys compared without the prev field; SA already in place; BWT from keys
+  auto r0 = refine_step<V>(ix, kg, kp[slot], ix.sa.as<V>(), nullptr, m, kg.pb, true, false,
+                           ix.act[cur][0].as<V>(), ix.act[cur][1].as<uint32_t>(), ix.act[cur][2].as<uint32_t>(),
+                           ix.head_slot.as<uint32_t>());
+  uint64_t A = r0.first, groups = r0.second;
+  ix.info.push_back(A);
+  uint64_t h = (uint64_t)kg.q;
+  int rounds = 0;
+  while (A > 0) {
+    if (++rounds > 200000) throw ApiError{-7, "suffix refinement did not converge"};
+    if (allow_doubling && rounds > kChunkRounds) break;
+    int gbits = 0;
+    while (gbits < 64 && (1ull << gbits) < groups) ++gbits;
+    const int qn = (64 - gbits) / kg.b;
+    if (qn < 1) throw ApiError{-6, "too many tied groups for one refinement key"};
+    {
+      TimedLaunch tm(ix.timer, "sa_refine_keys", (double)A * (sizeof(V) * 2 + 4 + 8));
+      k_refine_keys<V><<<grid_for(A), 256, 0, s>>>(ix.act[cur][0].as<V>(), ix.act[cur][2].as<uint32_t>(), A,
+                                                   ix.text.as<uint8_t>(), ix.n, d_lut, kg.b, qn, gbits, h, kp[0],
+                                                   vp[0]);
+      HK_HIP(hipGetLastError());
+    }
+    const int sl = radix_sort_pairs<V>(ix.sw, ix.timer, kp, vp, 0, A, 0, 64, false, s);
+    ix.info[0] += ix.sw.passes_run;
+    ix.info[1] += ix.sw.passes_skipped;
+    auto r = refine_step<V>(ix, kg, kp[sl], vp[sl], ix.act[cur][1].as<uint32_t>(), A, 0, false, true,
+                            ix.act[cur ^ 1][0].as<V>(), ix.act[cur ^ 1][1].as<uint32_t>(),
+                            ix.act[cur ^ 1][2].as<uint32_t>(), ix.head_slot.as<uint32_t>());
+    cur ^= 1;
+    A = r.first;
+    groups = r.second;
+    ix.info.push_back(A);
+    h += (uint64_t)qn;
+  }
+  ix.info[2] = (uint64_t)rounds;
+  if (A == 0) return;
+  if constexpr (sizeof(V) == 4) {
+    // ---- prefix doubling from order h: materialise ISA once, then double
+    ix.isa.ensure(ix.n * 4 + 16);
+    {
+      TimedLaunch tm(ix.timer, "sa_isa_scatter", (double)ix.n * 8);
+      k_isa_all<<<grid_for(ix.n), 256, 0, s>>>(ix.sa.as<uint32_t>(), ix.n, ix.isa.as<uint32_t>());
+      HK_HIP(hipGetLastError());
+    }
+    k_isa_active<<<grid_for(A), 256, 0, s>>>(ix.act[cur][0].as<uint32_t>(), ix.act[cur][2].as<uint32_t>(), A,
+                                             ix.head_slot.as<uint32_t>(), ix.isa.as<uint32_t>());
+    HK_HIP(hipGetLastError());
+    int drounds = 0;
+    while (A > 0) {
+      if (++drounds > 64) throw ApiError{-7, "prefix doubling did not converge"};
+      uint32_t* P = ix.act[cur][0].as<uint32_t>();
+      uint32_t* J = ix.act[cur][1].as<uint32_t>();
+      uint32_t* G = ix.act[cur][2].as<uint32_t>();
+      {
+        TimedLaunch tm(ix.timer, "sa_pair_keys", (double)A * (4 + 4 + 4 + 8 + 4));
+        k_pair_keys<<<grid_for(A), 256, 0, s>>>(P, G, A, ix.isa.as<uint32_t>(), ix.n, h, kp[0],
+                                                reinterpret_cast<uint32_t*>(vp[0]));
+        HK_HIP(hipGetLastError());
+      }
+      uint32_t* vq[2] = {reinterpret_cast<uint32_t*>(vp[0]), reinterpret_cast<uint32_t*>(vp[1])};
+      const int sl = radix_sort_pairs<uint32_t>(ix.sw, ix.timer, kp, vq, 0, A, 0, 64, false, s);
+      ix.info[0] += ix.sw.passes_run;
+      ix.info[1] += ix.sw.passes_skipped;
+      A = group_step(ix, kp[sl], vq[sl], J, A, ix.act[cur ^ 1][0].as<uint32_t>(), ix.act[cur ^ 1][1].as<uint32_t>(),
+                     ix.act[cur ^ 1][2].as<uint32_t>());
+      cur ^= 1;
+      ix.info.push_back(A);
+      h *= 2;
+    }
+    ix.info[2] += (uint64_t)drounds << 32;
+  } else {
+    throw ApiError{-7, "prefix doubling fallback needs 32-bit positions"};
+  }
+}
+
+template void refine_after_sort<uint32_t>(Index&, const KeyGeom&, int, uint64_t, bool);
+template void refine_after_sort<uint64_t>(Index&, const KeyGeom&, int, uint64_t, bool);
+
+void pack_keys(const uint8_t* d_text, uint64_t n, uint64_t lo, uint64_t count, const uint16_t* d_lut, int b, int q,
+               int pb, uint64_t* d_keys, hipStream_t s) {
   if (!count) return;
   const uint64_t g = ceil_div(count, PK_TILE);
-  k_pack_keys<<<(unsigned)g, 256, 0, s>>>(d_text, n, lo, count, d_lut, b, q, d_keys);
+  k_pack_keys<<<(unsigned)g, 256, 0, s>>>(d_text, n, lo, count, d_lut, b, q, pb, d_keys);
   HK_HIP(hipGetLastError());
 }
 
@@ -335,7 +675,7 @@ void synth_text(uint8_t* d_text, uint64_t n, const uint8_t* alphabet, int sigma,
 void compute_alphabet(Index& ix) {
   if (ix.have_alpha) return;
   hipStream_t s = ix.stream;
-  ix.small.ensure(4096);
+  ix.small.ensure(8192);
   HK_HIP(hipMemsetAsync(ix.small.p, 0, 256 * 8, s));
   {
     TimedLaunch t(ix.timer, "byte_hist", (double)ix.n);
@@ -370,75 +710,47 @@ void build_sa(Index& ix) {
   ix.info.assign(4, 0);
   ix.sharded = false;
   ix.sa_pos64 = false;
+  ix.have_sa = ix.have_bwt = ix.have_wt = false;
   ix.sa.ensure(n * 4 + 16);
+  ix.bwt.ensure(n + 64);
   if (n <= 1) {
     HK_HIP(hipMemsetAsync(ix.sa.p, 0, 4, s));
+    HK_HIP(hipMemcpyAsync(ix.bwt.p, ix.text.p, n, hipMemcpyDeviceToDevice, s));
     HK_HIP(hipStreamSynchronize(s));
-    ix.have_sa = true;
+    ix.have_sa = ix.have_bwt = true;
     return;
   }
-  // dense codes 1..sigma, 0 = end of text
-  int b = 1;
-  while ((1 << b) < ix.sigma + 1) ++b;
-  int q = 64 / b;
-  uint8_t lut[256];
-  for (int c = 0; c < 256; ++c) lut[c] = ix.code_of[c] < 0 ? 0 : (uint8_t)(ix.code_of[c] + 1);
-  ix.small.ensure(4096);
-  uint8_t* d_lut = ix.small.as<uint8_t>() + 2048;
-  HK_HIP(hipMemcpyAsync(d_lut, lut, 256, hipMemcpyHostToDevice, s));
-
+  // the prev field needs (q+1) symbols per key; for very small alphabets this still leaves q >= 20
+  KeyGeom kg = key_geometry(ix, true);
+  upload_geometry(ix, kg);
+  ix.info[3] = (uint64_t)kg.q;
   for (int i = 0; i < 2; ++i) {
     ix.keys[i].ensure(n * 8 + 16);
     ix.vals[i].ensure(n * 4 + 16);
   }
-  ix.isa.ensure(n * 4 + 16);
   {
     TimedLaunch t(ix.timer, "sa_pack_keys", (double)n * 9);
-    pack_keys(ix.text.as<uint8_t>(), n, 0, n, d_lut, b, q, ix.keys[0].as<uint64_t>(), s);
+    pack_keys(ix.text.as<uint8_t>(), n, 0, n, reinterpret_cast<const uint16_t*>(ix.small.as<uint8_t>() + 2048),
+              kg.b, kg.q, kg.pb, ix.keys[0].as<uint64_t>(), s);
   }
   uint64_t* kp[2] = {ix.keys[0].as<uint64_t>(), ix.keys[1].as<uint64_t>()};
   uint32_t* vp[2] = {ix.vals[0].as<uint32_t>(), ix.vals[1].as<uint32_t>()};
-  int slot = radix_sort_pairs<uint32_t>(ix.sw, ix.timer, kp, vp, 0, n, 0, q * b, true, s);
+  int slot = radix_sort_pairs<uint32_t>(ix.sw, ix.timer, kp, vp, 0, n, kg.pb, kg.key_bits, true, s);
   ix.info[0] += ix.sw.passes_run;
   ix.info[1] += ix.sw.passes_skipped;
   // the sorted values are the SA candidate order: adopt that buffer as SA
   std::swap(ix.sa, ix.vals[slot]);
   ix.vals[slot].ensure(n * 4 + 16);
-  vp[slot] = ix.vals[slot].as<uint32_t>();
-  for (int i = 0; i < 2; ++i)
-    for (int k = 0; k < 3; ++k) ix.act[i][k].ensure(n * 4 + 16);
-
-  uint64_t A = group_step(ix, kp[slot], ix.sa.as<uint32_t>(), nullptr, n, ix.act[0][0].as<uint32_t>(),
-                          ix.act[0][1].as<uint32_t>(), ix.act[0][2].as<uint32_t>());
-  ix.info.push_back(A);
-  uint64_t h = (uint64_t)q;
-  int rounds = 0;
-  while (A > 0) {
-    if (++rounds > 64) throw ApiError{-7, "prefix doubling did not converge"};
-    uint32_t* P = ix.act[0][0].as<uint32_t>();
-    uint32_t* J = ix.act[0][1].as<uint32_t>();
-    uint32_t* G = ix.act[0][2].as<uint32_t>();
-    {
-      TimedLaunch t(ix.timer, "sa_pair_keys", (double)A * (4 + 4 + 4 + 8 + 4));
-      k_pair_keys<<<grid_for(A), 256, 0, s>>>(P, G, A, ix.isa.as<uint32_t>(), n, h, kp[0], vp[0]);
-      HK_HIP(hipGetLastError());
-    }
-    slot = radix_sort_pairs<uint32_t>(ix.sw, ix.timer, kp, vp, 0, A, 0, 64, false, s);
-    ix.info[0] += ix.sw.passes_run;
-    ix.info[1] += ix.sw.passes_skipped;
-    A = group_step(ix, kp[slot], vp[slot], J, A, ix.act[1][0].as<uint32_t>(), ix.act[1][1].as<uint32_t>(),
-                   ix.act[1][2].as<uint32_t>());
-    ix.info.push_back(A);
-    for (int k = 0; k < 3; ++k) std::swap(ix.act[0][k], ix.act[1][k]);
-    h *= 2;
-  }
-  ix.info[2] = (uint64_t)rounds;
-  ix.info[3] = (uint64_t)q;
+  refine_after_sort<uint32_t>(ix, kg, slot, n, true);
+  HK_HIP(hipStreamSynchronize(s));
   ix.have_sa = true;
+  ix.have_bwt = true;
 }
 
 void build_bwt(Index& ix) {
   if (!ix.have_sa) throw ApiError{-3, "build_bwt: suffix array not built"};
+  if (ix.have_bwt) return;   // produced together with the SA
+  if (ix.sharded) throw ApiError{-3, "build_bwt: sharded index holds only a slice"};
   ix.bwt.ensure(ix.n + 64);
   {
     TimedLaunch t(ix.timer, "bwt_gather", (double)ix.n * (4 + 1 + 1));
@@ -464,6 +776,7 @@ void release_workspace(Index& ix) {
     for (int k = 0; k < 3; ++k) ix.act[i][k].release();
   }
   ix.isa.release();
+  ix.head_slot.release();
   ix.tile_a.release();
   ix.tile_b.release();
   ix.tile_c.release();

@@ -226,9 +226,7 @@ __global__ __launch_bounds__(256) void k_hist_offsets(const uint64_t* __restrict
 
 constexpr int OS_T = 512;
 constexpr int OS_I = 16;
-constexpr int OS_W = OS_T / 64;
-constexpr int OS_TILE = OS_T * OS_I;   // 8192 pairs per tile
-constexpr int OS_WSPAN = OS_I * 64;    // 1024 consecutive pairs per wave
+constexpr int OS_TILE = OS_T * OS_I;   // 8192 pairs per tile (production variant)
 constexpr uint64_t ST_VAL_MASK = (1ull << 46) - 1;
 constexpr uint64_t ST_AGG = 1, ST_INC = 2;
 constexpr uint32_t SPIN_LIMIT = 1u << 22;
@@ -237,45 +235,94 @@ __device__ __forceinline__ uint64_t st_pack(uint32_t epoch, uint64_t flag, uint6
   return ((uint64_t)epoch << 48) | (flag << 46) | v;
 }
 
-template <typename V>
+template <typename V, int T, int I>
 struct OsShared {
   union {
-    uint64_t keys[OS_TILE];
-    V vals[OS_TILE];
+    uint64_t keys[T * I];
+    V vals[T * I];
   } stage;
-  uint32_t whist[OS_W][256];   // per-wave digit counts, then per-wave exclusive prefix
-  uint32_t tstart[256];        // tile-local exclusive digit start
-  uint64_t gbase[256];         // global destination base minus tstart
+  uint32_t whist[T / 64][256];   // per-wave digit counts, then per-wave exclusive prefix
+  uint32_t tstart[256];          // tile-local exclusive digit start
+  uint64_t gbase[256];           // global destination base minus tstart
   uint32_t wsum[4];
   uint32_t tile;
 };
 
-template <typename V>
-__global__ __launch_bounds__(OS_T, 4) void k_onesweep(
+// Decoupled lookback for digit d of tile `tile`: sums predecessor counts until an inclusive
+// prefix is found.  Up to LB_WIN predecessor granules are loaded at once (independent sc1 loads),
+// so a chain of k not-yet-inclusive predecessors costs ~k/LB_WIN memory round trips, not k.
+constexpr int LB_WIN = 16;
+__device__ __forceinline__ uint64_t lookback(const uint64_t* status, uint32_t tile, uint32_t d, uint32_t epoch,
+                                             uint32_t* err) {
+  uint64_t excl = 0;
+  int64_t t = (int64_t)tile - 1;
+  uint32_t spins = 0;
+  while (t >= 0) {
+    uint64_t g[LB_WIN];
+#pragma unroll
+    for (int i = 0; i < LB_WIN; ++i) g[i] = (t - i >= 0) ? ld_agent(status + (uint64_t)(t - i) * 256 + d) : 0;
+    int consumed = 0;
+    bool done = false, stalled = false;
+#pragma unroll
+    for (int i = 0; i < LB_WIN; ++i) {
+      if (done || stalled || t - i < 0) continue;
+      const uint64_t flag = (g[i] >> 46) & 3u;
+      if ((uint32_t)(g[i] >> 48) != epoch || flag == 0) {
+        stalled = true;
+        continue;
+      }
+      excl += g[i] & ST_VAL_MASK;
+      ++consumed;
+      if (flag == ST_INC) done = true;
+    }
+    if (done) break;
+    t -= consumed;
+    if (stalled) {
+      if (++spins > SPIN_LIMIT) {
+        atomicOr(err, 1u);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+  }
+  return excl;
+}
+
+// MODE 0 = production.  Diagnostic ablations (wrong results, in-bounds writes):
+//   1 = no decoupled lookback (tile prefix taken as 0)
+//   2 = no lookback and no LDS staging (scatter straight from registers)
+// Order of work per tile: load keys -> wave ranking -> tile digit scan -> keys into LDS in sorted
+// order -> value loads issued -> lookback (its latency overlaps the value loads) -> keys out ->
+// values into LDS -> values out.
+template <typename V, int T, int I, int MODE>
+__global__ __launch_bounds__(T, 4) void k_onesweep(
     const uint64_t* __restrict__ kin, const V* __restrict__ vin, uint64_t* __restrict__ kout,
     V* __restrict__ vout, uint64_t n, uint32_t shift, const uint64_t* __restrict__ goff,
     uint64_t* status, uint32_t* tile_counter, uint32_t epoch, uint32_t* err, int iota) {
-  __shared__ OsShared<V> sh;
+  constexpr int W = T / 64;
+  constexpr int TILE = T * I;
+  constexpr int WSPAN = I * 64;
+  __shared__ OsShared<V, T, I> sh;
   const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
 
-  for (uint32_t i = tid; i < OS_W * 256; i += OS_T) (&sh.whist[0][0])[i] = 0;
+  for (uint32_t i = tid; i < W * 256; i += T) (&sh.whist[0][0])[i] = 0;
   if (tid == 0) sh.tile = atomicAdd(tile_counter, 1u);
   __syncthreads();
   const uint32_t tile = sh.tile;
-  const uint64_t tbase = (uint64_t)tile * OS_TILE;
-  const uint64_t wbase = tbase + (uint64_t)wv * OS_WSPAN;
+  const uint64_t tbase = (uint64_t)tile * TILE;
+  const uint64_t wbase = tbase + (uint64_t)wv * WSPAN;
 
-  uint64_t key[OS_I];
+  uint64_t key[I];
 #pragma unroll
-  for (int k = 0; k < OS_I; ++k) {
+  for (int k = 0; k < I; ++k) {
     const uint64_t j = wbase + (uint64_t)k * 64 + lane;
     key[k] = j < n ? kin[j] : ~0ull;
   }
 
   // ---- rank within the wave (stable: item-major, then lane)
-  uint32_t rk[OS_I];
+  uint32_t rk[I];
 #pragma unroll
-  for (int k = 0; k < OS_I; ++k) {
+  for (int k = 0; k < I; ++k) {
     const uint64_t j = wbase + (uint64_t)k * 64 + lane;
     const bool valid = j < n;
     const uint32_t d = (uint32_t)(key[k] >> shift) & 255u;
@@ -298,7 +345,7 @@ __global__ __launch_bounds__(OS_T, 4) void k_onesweep(
   if (tid < 256) {
     uint32_t run = 0;
 #pragma unroll
-    for (int w = 0; w < OS_W; ++w) {
+    for (int w = 0; w < W; ++w) {
       const uint32_t c = sh.whist[w][tid];
       sh.whist[w][tid] = run;
       run += c;
@@ -318,52 +365,66 @@ __global__ __launch_bounds__(OS_T, 4) void k_onesweep(
     uint32_t carry = 0;
     for (uint32_t w = 0; w < wv; ++w) carry += sh.wsum[w];
     sh.tstart[tid] += carry;
-
-    // ---- publish and look back
-    const uint32_t d = tid;
-    uint64_t* my = status + (uint64_t)tile * 256 + d;
-    uint64_t excl = 0;
-    if (tile == 0) {
-      st_agent(my, st_pack(epoch, ST_INC, tcount));
-    } else {
-      st_agent(my, st_pack(epoch, ST_AGG, tcount));
-      int64_t t = (int64_t)tile - 1;
-      uint32_t spins = 0;
-      while (t >= 0) {
-        const uint64_t s = ld_agent(status + (uint64_t)t * 256 + d);
-        const uint64_t flag = (s >> 46) & 3u;
-        if ((uint32_t)(s >> 48) != epoch || flag == 0) {
-          if (++spins > SPIN_LIMIT) {
-            atomicOr(err, 1u);
-            break;
-          }
-          __builtin_amdgcn_s_sleep(1);
-          continue;
-        }
-        excl += s & ST_VAL_MASK;
-        if (flag == ST_INC) break;
-        --t;
-      }
-      st_agent(my, st_pack(epoch, ST_INC, excl + tcount));
+    if (MODE == 0) {  // publish this tile's counts as early as possible
+      st_agent(status + (uint64_t)tile * 256 + tid, st_pack(epoch, tile == 0 ? ST_INC : ST_AGG, tcount));
     }
-    sh.gbase[d] = goff[d] + excl - sh.tstart[d];
   }
   __syncthreads();
 
-  // ---- keys: stage in sorted order, write out in runs (rk becomes the tile-local rank)
+  if (MODE == 2) {  // ablation: scatter straight from registers
+    if (tid < 256) {
+      uint64_t go = goff[tid];
+      if (go + TILE > n) go = n > (uint64_t)TILE ? n - TILE : 0;
+      sh.gbase[tid] = go;
+    }
+    __syncthreads();
 #pragma unroll
-  for (int k = 0; k < OS_I; ++k) {
+    for (int k = 0; k < I; ++k) {
+      const uint64_t j = wbase + (uint64_t)k * 64 + lane;
+      const uint32_t d = rk[k] >> 16;
+      const uint32_t lr = sh.whist[wv][d] + (rk[k] & 0xFFFFu);
+      if (j < n) {
+        const uint64_t dst = sh.gbase[d] + lr;
+        kout[dst] = key[k];
+        vout[dst] = iota ? (V)j : vin[j];
+      }
+    }
+    return;
+  }
+
+  // ---- keys into LDS in sorted order (rk becomes the tile-local rank)
+#pragma unroll
+  for (int k = 0; k < I; ++k) {
     const uint64_t j = wbase + (uint64_t)k * 64 + lane;
     const uint32_t d = rk[k] >> 16;
     rk[k] = sh.tstart[d] + sh.whist[wv][d] + (rk[k] & 0xFFFFu);
     if (j < n) sh.stage.keys[rk[k]] = key[k];
   }
-  __syncthreads();
-  const uint32_t tile_n = (uint32_t)((n - tbase) < (uint64_t)OS_TILE ? (n - tbase) : OS_TILE);
-  uint32_t dg[OS_I / 4] = {0, 0, 0, 0};   // digits of the staged slots, 4 per register
+  // ---- value loads in flight across the lookback
+  V val[I];
 #pragma unroll
-  for (int i = 0; i < OS_I; ++i) {
-    const uint32_t s = (uint32_t)i * OS_T + tid;
+  for (int k = 0; k < I; ++k) {
+    const uint64_t j = wbase + (uint64_t)k * 64 + lane;
+    val[k] = iota ? (V)j : (j < n ? vin[j] : (V)0);
+  }
+  if (tid < 256) {
+    const uint32_t d = tid;
+    uint64_t excl = 0;
+    if (MODE == 0 && tile > 0) {
+      excl = lookback(status, tile, d, epoch, err);
+      st_agent(status + (uint64_t)tile * 256 + d, st_pack(epoch, ST_INC, excl + tcount));
+    }
+    uint64_t go = goff[d];
+    if (MODE != 0 && go + TILE > n) go = n > (uint64_t)TILE ? n - TILE : 0;  // ablations stay in bounds
+    sh.gbase[d] = go + excl - sh.tstart[d];
+  }
+  __syncthreads();
+
+  const uint32_t tile_n = (uint32_t)((n - tbase) < (uint64_t)TILE ? (n - tbase) : TILE);
+  uint32_t dg[(I + 3) / 4] = {};   // digits of the staged slots, 4 per register
+#pragma unroll
+  for (int i = 0; i < I; ++i) {
+    const uint32_t s = (uint32_t)i * T + tid;
     if (s < tile_n) {
       const uint64_t kk = sh.stage.keys[s];
       const uint32_t d = (uint32_t)(kk >> shift) & 255u;
@@ -372,17 +433,26 @@ __global__ __launch_bounds__(OS_T, 4) void k_onesweep(
     }
   }
   __syncthreads();
-  // ---- values: loaded only now (keeps the ranking phase under 128 VGPRs: 2 blocks/CU)
 #pragma unroll
-  for (int k = 0; k < OS_I; ++k) {
+  for (int k = 0; k < I; ++k) {
     const uint64_t j = wbase + (uint64_t)k * 64 + lane;
-    if (j < n) sh.stage.vals[rk[k]] = iota ? (V)j : vin[j];
+    if (j < n) sh.stage.vals[rk[k]] = val[k];
   }
   __syncthreads();
 #pragma unroll
-  for (int i = 0; i < OS_I; ++i) {
-    const uint32_t s = (uint32_t)i * OS_T + tid;
+  for (int i = 0; i < I; ++i) {
+    const uint32_t s = (uint32_t)i * T + tid;
     if (s < tile_n) vout[sh.gbase[(dg[i >> 2] >> (8 * (i & 3))) & 255u] + s] = sh.stage.vals[s];
+  }
+}
+
+// bandwidth reference for the pass shape: read (key, value), write them back shifted by one tile
+template <typename V>
+__global__ __launch_bounds__(256) void k_copy_pairs(const uint64_t* __restrict__ kin, const V* __restrict__ vin,
+                                                    uint64_t* __restrict__ kout, V* __restrict__ vout, uint64_t n) {
+  for (uint64_t j = (uint64_t)blockIdx.x * 256 + threadIdx.x; j < n; j += (uint64_t)gridDim.x * 256) {
+    kout[j] = kin[j];
+    vout[j] = vin[j];
   }
 }
 
@@ -461,7 +531,7 @@ int radix_sort_pairs(SortWork& w, KernelTimer& tm, uint64_t* k[2], V* v[2], int 
     const int nxt = cur ^ 1;
     {
       TimedLaunch t(tm, "radix_onesweep", (double)n * 2.0 * (8 + sizeof(V)));
-      k_onesweep<V><<<(unsigned)tiles, OS_T, 0, s>>>(
+      k_onesweep<V, OS_T, OS_I, 0><<<(unsigned)tiles, OS_T, 0, s>>>(
           k[cur], iota_pending ? nullptr : v[cur], k[nxt], v[nxt], n, (uint32_t)(bit_lo + 8 * p),
           w.offs.as<uint64_t>() + p * 256, w.status.as<uint64_t>(), w.counters.as<uint32_t>() + p,
           w.epoch, w.err.as<uint32_t>(), iota_pending ? 1 : 0);
@@ -477,6 +547,92 @@ int radix_sort_pairs(SortWork& w, KernelTimer& tm, uint64_t* k[2], V* v[2], int 
   HK_HIP(hipStreamSynchronize(s));
   if (herr) throw ApiError{-7, "radix sort lookback exceeded its spin bound"};
   return cur;
+}
+
+// ---------------------------------------------------------------- diagnostics
+// Times `reps` radix passes of variant (threads x items, mode) over n DNA-text keys (u32 values)
+// plus a plain pair copy of the same bytes; used to decide where a pass spends its time.
+template <int T, int I, int MODE>
+static double time_variant(SortWork& w, uint64_t* k[2], uint32_t* v[2], uint64_t n, int reps, int bit_lo,
+                           const uint64_t* pristine, hipStream_t s) {
+  // every variant starts from the same keys: the ablations scramble the multiset, and an exact
+  // variant's scatter is only in bounds when the keys match the digit offsets
+  HK_HIP(hipMemcpyAsync(k[0], pristine, n * 8, hipMemcpyDeviceToDevice, s));
+  fill_iota<uint32_t>(v[0], n, s);
+  const uint64_t tiles = ceil_div(n, (uint64_t)T * I);
+  w.status.ensure(tiles * 256 * 8);
+  if (tiles > w.status_tiles) w.status_tiles = tiles;
+  HK_HIP(hipMemsetAsync(w.status.p, 0, tiles * 256 * 8, s));
+  w.counters.ensure(64 * 4);
+  w.err.ensure(16);
+  hipEvent_t a, b;
+  HK_HIP(hipEventCreate(&a));
+  HK_HIP(hipEventCreate(&b));
+  float total = 0;
+  for (int r = 0; r < reps + 1; ++r) {
+    HK_HIP(hipMemsetAsync(w.counters.p, 0, 4, s));
+    HK_HIP(hipEventRecord(a, s));
+    k_onesweep<uint32_t, T, I, MODE><<<(unsigned)tiles, T, 0, s>>>(
+        k[r & 1], v[r & 1], k[(r + 1) & 1], v[(r + 1) & 1], n, (uint32_t)(bit_lo + 8 * (r % 7)),
+        w.offs.as<uint64_t>() + (r % 7) * 256, w.status.as<uint64_t>(), w.counters.as<uint32_t>(),
+        (uint32_t)(r + 1), w.err.as<uint32_t>(), 0);
+    HK_HIP(hipGetLastError());
+    HK_HIP(hipEventRecord(b, s));
+    HK_HIP(hipEventSynchronize(b));
+    float ms = 0;
+    HK_HIP(hipEventElapsedTime(&ms, a, b));
+    if (r) total += ms;  // first launch is warm-up
+  }
+  (void)hipEventDestroy(a);
+  (void)hipEventDestroy(b);
+  w.status_tiles = 0;  // epochs restarted; force a clean status on the next real sort
+  w.epoch = 0;
+  return total / reps;
+}
+
+void debug_radix_bench(SortWork& w, uint64_t* k[2], uint32_t* v[2], uint64_t n, int bit_lo, int reps,
+                       double* out, int nout, hipStream_t s) {
+  // digit offsets of the real keys, so that every variant scatters inside the arrays
+  w.hist.ensure(8 * 256 * 8);
+  w.offs.ensure(8 * 256 * 8);
+  HK_HIP(hipMemsetAsync(w.hist.p, 0, 8 * 256 * 8, s));
+  k_digit_hist<<<2048, HG_T, 0, s>>>(k[0], n, bit_lo, 7, w.hist.as<unsigned long long>());
+  k_hist_offsets<<<7, 256, 0, s>>>(w.hist.as<uint64_t>(), w.offs.as<uint64_t>());
+  HK_HIP(hipGetLastError());
+  DevBuf pristine;
+  pristine.ensure(n * 8);
+  HK_HIP(hipMemcpyAsync(pristine.p, k[0], n * 8, hipMemcpyDeviceToDevice, s));
+  const uint64_t* pk = pristine.as<uint64_t>();
+  double r[8] = {0};
+  r[0] = time_variant<512, 16, 0>(w, k, v, n, reps, bit_lo, pk, s);
+  r[1] = time_variant<512, 16, 1>(w, k, v, n, reps, bit_lo, pk, s);
+  r[2] = time_variant<512, 16, 2>(w, k, v, n, reps, bit_lo, pk, s);
+  r[3] = time_variant<256, 16, 0>(w, k, v, n, reps, bit_lo, pk, s);
+  r[4] = time_variant<256, 16, 1>(w, k, v, n, reps, bit_lo, pk, s);
+  r[5] = time_variant<1024, 8, 0>(w, k, v, n, reps, bit_lo, pk, s);
+  {
+    hipEvent_t a, b;
+    HK_HIP(hipEventCreate(&a));
+    HK_HIP(hipEventCreate(&b));
+    float total = 0;
+    for (int q = 0; q < reps + 1; ++q) {
+      HK_HIP(hipEventRecord(a, s));
+      k_copy_pairs<uint32_t><<<8192, 256, 0, s>>>(k[q & 1], v[q & 1], k[(q + 1) & 1], v[(q + 1) & 1], n);
+      HK_HIP(hipEventRecord(b, s));
+      HK_HIP(hipEventSynchronize(b));
+      float ms = 0;
+      HK_HIP(hipEventElapsedTime(&ms, a, b));
+      if (q) total += ms;
+    }
+    (void)hipEventDestroy(a);
+    (void)hipEventDestroy(b);
+    r[6] = total / reps;
+  }
+  uint32_t herr = 0;
+  HK_HIP(hipMemcpyAsync(&herr, w.err.p, 4, hipMemcpyDeviceToHost, s));
+  HK_HIP(hipStreamSynchronize(s));
+  r[7] = herr;
+  for (int i = 0; i < nout && i < 8; ++i) out[i] = r[i];
 }
 
 template int radix_sort_pairs<uint32_t>(SortWork&, KernelTimer&, uint64_t* k[2], uint32_t* v[2],

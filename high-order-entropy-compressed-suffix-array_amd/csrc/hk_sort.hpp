@@ -41,6 +41,11 @@ template <typename V>
 int radix_sort_pairs(SortWork& w, KernelTimer& tm, uint64_t* k[2], V* v[2], int in_slot,
                      uint64_t n, int bit_lo, int bit_hi, bool vals_iota, hipStream_t s);
 
+// diagnostics: per-pass ms of onesweep variants {512x16, 512x16 no-lookback, 512x16 no-lookback
+// no-staging, 256x16, 256x16 no-lookback, 1024x8} and of a plain pair copy; out[7] = error flag
+void debug_radix_bench(SortWork& w, uint64_t* k[2], uint32_t* v[2], uint64_t n, int bit_lo, int reps,
+                       double* out, int nout, hipStream_t s);
+
 // fill v[i] = i
 template <typename V>
 void fill_iota(V* v, uint64_t n, hipStream_t s);

@@ -383,8 +383,8 @@ void query_locate_gather(Index& ix, const int64_t* d_lr, const uint64_t* d_occ_o
   if (!P) return;
   hipStream_t s = ix.stream;
   ix.tile_c.ensure((P + 2) * 8);
-  ix.small.ensure(4096);
-  unsigned long long* nbig = ix.small.as<unsigned long long>() + 384;
+  ix.small.ensure(8192);
+  unsigned long long* nbig = ix.small.as<unsigned long long>() + 512;   // byte 4096: clear of the build LUTs
   HK_HIP(hipMemsetAsync(nbig, 0, 8, s));
   TimedLaunch t(ix.timer, "fm_locate", 0.0);
   k_locate_small<<<grid_for(P, 256, 65535), 256, 0, s>>>(ix.sa.as<uint32_t>(), d_lr, d_occ_offs, P, d_pos,

@@ -481,6 +481,32 @@ int hkcsa_shard_range(hkcsa_index* h, uint64_t* lo, uint64_t* hi) {
   });
 }
 
+// ------------------------------------------------------------ diagnostics
+int hkcsa_debug_radix_bench(uint64_t n, int reps, double* out, int nout) {
+  return guarded([&] {
+    need(out != nullptr && n >= (1u << 16) && reps >= 1, HKCSA_E_INVALID, "bad arguments");
+    hk::Index ix;
+    init_index(ix, nullptr, n);
+    const uint8_t dna[4] = {'A', 'C', 'G', 'T'};
+    hk::synth_text(ix.text.as<uint8_t>(), n, dna, 4, 77, '$', ix.stream);
+    hk::KeyGeom kg = hk::key_geometry(ix, true);
+    hk::upload_geometry(ix, kg);
+    for (int i = 0; i < 2; ++i) {
+      ix.keys[i].ensure(n * 8 + 16);
+      ix.vals[i].ensure(n * 4 + 16);
+    }
+    hk::pack_keys(ix.text.as<uint8_t>(), n, 0, n, reinterpret_cast<const uint16_t*>(ix.small.as<uint8_t>() + 2048),
+                  kg.b, kg.q, kg.pb, ix.keys[0].as<uint64_t>(), ix.stream);
+    hk::fill_iota<uint32_t>(ix.vals[0].as<uint32_t>(), n, ix.stream);
+    uint64_t* kp[2] = {ix.keys[0].as<uint64_t>(), ix.keys[1].as<uint64_t>()};
+    uint32_t* vp[2] = {ix.vals[0].as<uint32_t>(), ix.vals[1].as<uint32_t>()};
+    hk::debug_radix_bench(ix.sw, kp, vp, n, kg.pb, reps, out, nout, ix.stream);
+    HK_HIP(hipStreamSynchronize(ix.stream));
+    (void)hipStreamDestroy(ix.stream);
+    ix.stream = nullptr;
+  });
+}
+
 // ------------------------------------------------------------ timing
 int hkcsa_timing_enable(hkcsa_index* h, int on) {
   return guarded([&] {

@@ -156,6 +156,13 @@ int hkcsa_shard_buckets(void);
 int hkcsa_shard_histogram(hkcsa_index* ix, int nranks, int rank, uint64_t* hist_out);
 int hkcsa_shard_build(hkcsa_index* ix, const uint64_t* global_hist, int nranks, int rank);
 
+/* ---- diagnostics ------------------------------------------------------ */
+/* Per-pass milliseconds of radix-pass variants over n synthetic DNA keys
+ * (u32 values): out = {512x16, 512x16 without lookback, 512x16 without lookback
+ * or LDS staging, 256x16, 256x16 without lookback, 1024x8, plain pair copy,
+ * error flag}.  Ablations produce wrong orders by design; only times matter. */
+int hkcsa_debug_radix_bench(uint64_t n, int reps, double* out, int nout);
+
 /* ---- per-kernel timing (HIP events on the handle's stream) ------------ */
 int hkcsa_timing_enable(hkcsa_index* ix, int on);
 int hkcsa_timing_reset(hkcsa_index* ix);

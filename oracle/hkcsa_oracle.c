@@ -229,28 +229,39 @@ int oracle_wt_levels(const uint8_t* seq, uint64_t n, uint8_t* bits /* 8*n */) {
 }
 
 /* ------------------------------------------------------------- shard partition
- * Host restatement of the sharded build's partition (hk_shard.hip): the key of a suffix packs
- * its first q dense codes (code 0 past the end), b bits each; its bucket is the top 14 bits. */
+ * Host restatement of the sharded build's partition (hk_shard.hip): the key of suffix p packs
+ * its first q dense codes (code 0 past the end, b bits each) above the code of T[p-1]
+ * (T[n-1] for p = 0); q = (64 - b) / b.  Its bucket is the top 14 bits of the key. */
 void oracle_shard_geometry(const uint8_t* t, uint64_t n, int* b, int* q, int* bsh, uint8_t lut[256]) {
   int present[256] = {0}, sigma = 0;
   for (uint64_t i = 0; i < n; ++i) present[t[i]] = 1;
-  for (int c = 0; c < 256; ++c) lut[c] = present[c] ? (uint8_t)(++sigma) : 0;
+  uint16_t code[256];
+  for (int c = 0; c < 256; ++c) code[c] = present[c] ? (uint16_t)(++sigma) : 0;
   int bb = 1;
   while ((1 << bb) < sigma + 1) ++bb;
   *b = bb;
-  *q = 64 / bb;
-  *bsh = *q * bb - 14;
+  *q = (64 - bb) / bb;
+  *bsh = (*q + 1) * bb - 14;
   if (*bsh < 0) *bsh = 0;
+  for (int c = 0; c < 256; ++c) lut[c] = (uint8_t)code[c]; /* callers use lut only when sigma < 256 */
+}
+
+static uint64_t shard_key(const uint8_t* t, uint64_t n, uint64_t p, int b, int q, const uint16_t* code) {
+  uint64_t key = 0;
+  for (int j = 0; j < q; ++j) key = (key << b) | (p + j < n ? code[t[p + j]] : 0);
+  return (key << b) | code[t[p == 0 ? n - 1 : p - 1]];
 }
 
 void oracle_shard_hist(const uint8_t* t, uint64_t n, uint64_t lo, uint64_t hi, uint64_t* hist /* 16384 */) {
-  int b, q, bsh;
-  uint8_t lut[256];
-  oracle_shard_geometry(t, n, &b, &q, &bsh, lut);
+  int present[256] = {0}, sigma = 0;
+  for (uint64_t i = 0; i < n; ++i) present[t[i]] = 1;
+  uint16_t code[256];
+  for (int c = 0; c < 256; ++c) code[c] = present[c] ? (uint16_t)(++sigma) : 0;
+  int b = 1;
+  while ((1 << b) < sigma + 1) ++b;
+  const int q = (64 - b) / b;
+  int bsh = (q + 1) * b - 14;
+  if (bsh < 0) bsh = 0;
   memset(hist, 0, 16384 * sizeof(uint64_t));
-  for (uint64_t p = lo; p < hi; ++p) {
-    uint64_t key = 0;
-    for (int j = 0; j < q; ++j) key = (key << b) | (p + j < n ? lut[t[p + j]] : 0);
-    hist[key >> bsh]++;
-  }
+  for (uint64_t p = lo; p < hi; ++p) hist[shard_key(t, n, p, b, q, code) >> bsh]++;
 }

@@ -1,0 +1,120 @@
+"""The reference's class/module surface (csa.*, utils.*) running on the GPU, checked against
+the known-answer vectors generated from the reference (tests/golden/kat.json)."""
+import numpy as np
+import pytest
+
+from oracle import ref_port
+
+pytestmark = pytest.mark.gpu
+
+WORDS = ["banana", "mississippi", "ACGTTGCAAC", "", "a", "$", "this is an example text"]
+
+
+@pytest.mark.parametrize("word", WORDS)
+def test_enhanced_fm_index_kat(kat, word):
+    from csa.enhanced_fm_index import EnhancedFMIndex
+    k = kat[word]
+    idx = EnhancedFMIndex(word)
+    assert idx.text == word + "$"
+    assert idx.suffix_array == k["sa"]
+    assert idx.bwt == k["bwt"]
+    assert idx.count == k["C"]
+    for p, want in k["find"].items():
+        assert idx.find(p) == want, p
+        assert list(idx.find_range(p)) == k["find_range"][p], p
+    port = ref_port.FMIndexPort(word)
+    for ch in sorted(set(word + "$")) + ["\x7f", "zz"]:
+        for i in [0, 1, 2, len(word), len(word) + 1, len(word) + 5, -1]:
+            assert idx.rank(ch, i) == (port.occ[ch][min(i, len(word) + 1)] if ch in port.occ else 0), (ch, i)
+    assert set(idx.occ.keys()) == set(port.occ.keys())
+    for ch in port.occ:
+        assert list(idx.occ[ch]) == port.occ[ch]
+
+
+def test_wavelet_tree_kat(kat):
+    from csa.wavelet_tree import WaveletTree
+    demo = "this is an example text"
+    wt = WaveletTree(demo)
+    assert wt.compress() == kat["demo_wt_compress"]
+    assert ["".join(str(int(b)) for b in rs.bit_vector) for rs in wt.rank_structures] == kat["demo_wt_bits"]
+    assert wt.m == kat["demo_wt_m"]
+    assert wt.decompress(wt.compress()) == demo
+    for word in ["banana", "mississippi", "ACGTTGCAAC"]:
+        k = kat[word]
+        wt = WaveletTree(k["bwt"])
+        assert len(wt.tree) == len(k["wt_bwt"])
+        for (g, L, R, _), want in zip(wt.tree, k["wt_bwt"]):
+            assert "".join(L) == want["left"] and "".join(R) == want["right"]
+            assert "".join(map(str, g)) == want["golomb"]
+        assert wt.occ("a" if word == "banana" else k["bwt"][0], len(k["bwt"])) == k["bwt"].count(
+            "a" if word == "banana" else k["bwt"][0])
+
+
+def test_wavelet_tree_random_cases(random_cases):
+    from conftest import wt_golden_levels
+    from csa.wavelet_tree import WaveletTree
+    for name in random_cases.names:
+        if not name.endswith(("_n64", "_n1000")):
+            continue
+        c = random_cases.get(name)
+        wt = WaveletTree(c["bwt"].tobytes().decode("latin-1"))
+        gold = wt_golden_levels(c)
+        assert len(wt.tree) == len(gold), name
+        for (g, L, R, nxt), rs, want in zip(wt.tree, wt.rank_structures, gold):
+            assert np.array_equal(rs.bit_vector, want["bits"]), name
+            assert np.array_equal(np.asarray(g, np.uint8), want["golomb"]), name
+            assert "".join(L).encode("latin-1") == want["left"]
+            assert "".join(R).encode("latin-1") == want["right"]
+            assert "".join(nxt).encode("latin-1") == want["next"]
+        if gold:
+            assert wt.m == int(c["wt_m"][0])
+        if "wtq_i" in c:
+            for i, r, s in zip(c["wtq_i"], c["wtq_rank"], c["wtq_select"]):
+                assert int(wt.rank("A", int(i))) == int(r)
+                assert int(wt.select("A", int(i))) == int(s)
+
+
+def test_module_functions(kat):
+    from csa.bwt import bwt_transform
+    from csa.suffix_array import build_suffix_array, ksa
+    from utils.utils import build_count, build_occ
+    assert ksa("banana") == kat["ksa_banana"]
+    for word in ["banana", "mississippi", "ACGTTGCAAC"]:
+        k = kat[word]
+        tp = word + "$"
+        sa = build_suffix_array(tp)
+        assert sa == k["sa"]
+        assert bwt_transform(tp, sa) == k["bwt"]
+        assert build_count(tp) == k["C"]
+        occ = build_occ(k["bwt"])
+        assert dict((c, list(v)) for c, v in occ.items()) == ref_port.occ_table(k["bwt"])
+    assert build_suffix_array("") == [] and bwt_transform("", []) == ""
+
+
+def test_csa_surface():
+    from csa import CSA, CompressedSuffixArray
+    from csa.csa import CompressedSuffixArray as C2
+    assert CompressedSuffixArray is CSA and C2 is CSA
+    text = "mississippi$" * 50
+    csa = CompressedSuffixArray(text, epsilon=0.5)
+    port = ref_port.FMIndexPort(text)
+    for p in ["ssi", "mississippi", "i$m", "x", "", "pp", "$"]:
+        assert csa.locate(p) == port.find(p)
+        l, r = port.find_range(p)
+        assert csa.count(p) == (0 if l == -1 else r - l + 1)
+    assert csa.count_many(["ssi", "x"]) == [csa.count("ssi"), 0]
+    assert csa.locate_many(["ssi"]) == [csa.locate("ssi")]
+    for i, j in [(0, 5), (3, 3), (-4, None), (10, 2), (0, 10 ** 9), (-10 ** 9, 4)]:
+        assert csa.extract(i, j) == text[i:j]
+
+
+def test_unicode_text_remap():
+    from csa.enhanced_fm_index import EnhancedFMIndex
+    text = "αβγαβ€αβ"
+    idx = EnhancedFMIndex(text)
+    port = ref_port.FMIndexPort(text)
+    assert idx.suffix_array == port.suffix_array
+    assert idx.bwt == port.bwt
+    assert idx.count == port.count
+    for p in ["αβ", "β€", "€α", "z", "ααα"]:
+        assert idx.find(p) == port.find(p)

@@ -1,0 +1,202 @@
+"""GPU parity: the HIP path (through the C-ABI) against the golden vectors generated from the
+reference, and against the CPU oracle on seeded inputs; full-size configs through the O(n)
+SA checker.  Every comparison is bit-exact (integer / byte / index work)."""
+import hashlib
+
+import numpy as np
+import pytest
+
+from conftest import locs_of, patterns_of, wt_golden_levels
+from oracle import oracle
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def hk():
+    import hkcsa
+    if hkcsa.device_count() < 1:
+        pytest.fail("no GPU visible: the HIP path is required (there is no CPU fallback)")
+    return hkcsa
+
+
+def _build(hk, tp: bytes):
+    dev = hk.DeviceIndex.from_bytes(tp, device=0)
+    dev.build_all()
+    return dev
+
+
+def _check_against_golden_case(dev, c, name):
+    n = len(c["sa"])
+    assert np.array_equal(dev.sa(), c["sa"].astype(np.uint64)), name
+    assert np.array_equal(dev.bwt(), c["bwt"]), name
+    C = dev.C()
+    assert np.array_equal(C[c["C_sym"]], c["C_val"].astype(np.uint64)), name
+    present = set(c["C_sym"].tolist())
+    ranks = dev.rank(c["occ_c"], np.minimum(c["occ_i"], np.iinfo(np.int64).max).astype(np.uint64))
+    want = c["occ_v"].astype(np.uint64)
+    got = np.where(np.isin(c["occ_c"], list(present)), ranks, 0)
+    assert np.array_equal(got, want), name
+    pats = patterns_of(c)
+    assert np.array_equal(dev.count_ranges(pats), c["pat_lr"]), name
+    offs, pos = dev.locate(pats)
+    got_l = [[int(x) for x in pos[offs[i]:offs[i + 1]]] for i in range(len(pats))]
+    assert got_l == locs_of(c), name
+    gold = wt_golden_levels(c)
+    if gold:
+        assert dev.wt_levels() >= len(gold)
+    for lv, g in enumerate(gold):
+        bits = dev.wt_level_bits(lv)
+        assert len(bits) == n
+        assert np.array_equal(bits[:len(g["bits"])], g["bits"]), (name, lv)
+
+
+def test_random_golden_cases(hk, random_cases):
+    for name in random_cases.names:
+        c = random_cases.get(name)
+        dev = _build(hk, c["text"].tobytes() + b"$")
+        _check_against_golden_case(dev, c, name)
+        dev.close()
+
+
+def test_large_golden_cases(hk, large_cases):
+    for name in large_cases.names:
+        c = large_cases.get(name)
+        dev = _build(hk, c["text"].tobytes() + b"$")
+        sa = dev.sa()
+        assert hashlib.sha256(sa.astype("<u4").tobytes()).hexdigest() == str(c["sa_sha256"][0]), name
+        assert hashlib.sha256(dev.bwt().tobytes()).hexdigest() == str(c["bwt_sha256"][0]), name
+        assert np.array_equal(sa[c["sa_i"]], c["sa_v"].astype(np.uint64)), name
+        pats = patterns_of(c)
+        assert np.array_equal(dev.count_ranges(pats), c["pat_lr"]), name
+        offs, pos = dev.locate(pats)
+        got = [[int(x) for x in pos[offs[i]:offs[i + 1]]] for i in range(len(pats))]
+        assert got == locs_of(c), name
+        dev.close()
+
+
+def _texts():
+    rng = np.random.default_rng(99)
+    yield "dna_1M", oracle.synth_text((1 << 20) + 1, b"ACGT", seed=7)
+    yield "bytes_1M", oracle.synth_text((1 << 20) + 1, bytes(range(256)), seed=8)
+    yield "binary_256K", oracle.synth_text((1 << 18) + 1, b"ab", seed=9)
+    yield "printable_1M", oracle.synth_text((1 << 20) + 1, bytes(range(0x20, 0x7F)), seed=10)
+    base = rng.integers(0, 4, size=5000).astype(np.uint8) + ord("A")
+    rep = np.tile(base, 40)                                   # long repeats: many doubling rounds
+    rep[rng.integers(0, len(rep), size=50)] = ord("T")
+    yield "repeats_200K", np.concatenate([rep, [ord("$")]]).astype(np.uint8)
+    yield "periodic_64K", np.frombuffer(b"abc" * 21845 + b"$", dtype=np.uint8)
+    yield "run_a_20K", np.frombuffer(b"a" * 20000 + b"$", dtype=np.uint8)
+    yield "single", np.frombuffer(b"$", dtype=np.uint8)
+    yield "two", np.frombuffer(b"z$", dtype=np.uint8)
+    yield "nul_bytes", np.frombuffer(bytes([0, 0, 1, 0, 0, 0, 1, 1, 0]) + b"$", dtype=np.uint8)
+
+
+@pytest.mark.parametrize("name,text", list(_texts()))
+def test_sa_bwt_wt_vs_oracle(hk, name, text):
+    dev = _build(hk, text.tobytes())
+    sa = dev.sa()
+    assert oracle.check_sa(text, sa) == 0, name
+    if len(text) <= (1 << 20) + 1 and not name.startswith(("run_", "periodic", "repeats")):
+        assert np.array_equal(sa, oracle.suffix_array(text)), name
+    bwt = dev.bwt()
+    assert np.array_equal(bwt, oracle.bwt(text, sa)), name
+    assert np.array_equal(dev.C(), oracle.count_array(text)), name
+    full = oracle.wt_levels(bwt)
+    assert dev.wt_levels() == len(full), name
+    for lv in range(len(full)):
+        assert np.array_equal(dev.wt_level_bits(lv), full[lv]), (name, lv)
+    # random rank queries (incl. i > n clamp and absent symbols)
+    rng = np.random.default_rng(len(text))
+    cs = rng.integers(0, 256, size=2000).astype(np.uint8)
+    cs[:500] = text[rng.integers(0, len(text), size=500)]
+    idx = rng.integers(0, len(text) + 10, size=2000).astype(np.uint64)
+    fm = oracle.FM(text, sa)
+    want = np.array([fm.rank(int(c), int(i)) for c, i in zip(cs, idx)], dtype=np.uint64)
+    assert np.array_equal(dev.rank(cs, idx), want), name
+    # count / locate of substrings, random strings, '$' quirk patterns and the empty pattern
+    n = len(text)
+    pats = [b"", b"$", bytes(text[-3:])]
+    for _ in range(400):
+        m = int(rng.integers(1, 24))
+        s = int(rng.integers(0, max(1, n - m)))
+        pats.append(text[s:s + m].tobytes())
+    for _ in range(100):
+        m = int(rng.integers(1, 8))
+        pats.append(bytes(rng.choice(np.unique(text), size=m)))
+    assert np.array_equal(dev.count_ranges(pats), fm.find_range(pats)), name
+    offs, pos = dev.locate(pats)
+    want_l = fm.find(pats)
+    got_l = [[int(x) for x in pos[offs[i]:offs[i + 1]]] for i in range(len(pats))]
+    assert got_l == want_l, name
+    dev.close()
+
+
+def test_repeated_builds_are_identical(hk):
+    text = oracle.synth_text(300001, b"ACGT", seed=33)
+    dev = hk.DeviceIndex.from_bytes(text, device=0)
+    dev.build_sa()
+    a = dev.sa()
+    dev.build_sa()
+    b = dev.sa()
+    assert np.array_equal(a, b)
+    assert oracle.check_sa(text, a) == 0
+    dev.close()
+
+
+def test_synthetic_matches_host_generator(hk):
+    dev = hk.DeviceIndex.synthetic(100001, b"ACGT", seed=4)
+    assert np.array_equal(dev.text(), oracle.synth_text(100001, b"ACGT", seed=4))
+    dev.close()
+
+
+def test_full_size_config1_256MiB(hk):
+    """configs[1]: 256 MiB sigma=4 text — SA checked in O(n), BWT recomputed, counts sampled."""
+    n = (1 << 28) + 1
+    dev = hk.DeviceIndex.synthetic(n, b"ACGT", seed=2)
+    dev.build_sa()
+    dev.build_bwt()
+    sa = dev.sa()
+    text = oracle.synth_text(n, b"ACGT", seed=2)
+    assert np.array_equal(dev.text(0, 4096), text[:4096])
+    assert oracle.check_sa(text, sa) == 0
+    assert np.array_equal(dev.bwt(), oracle.bwt(text, sa))
+    dev.close()
+
+
+@pytest.mark.parametrize("nranks", [2, 3])
+def test_shard_two_phase_emulated(hk, nranks):
+    text = oracle.synth_text(400001, b"ACGT", seed=12)
+    ref = oracle.suffix_array(text)
+    devs = [hk.DeviceIndex.from_bytes(text, device=0) for _ in range(nranks)]
+    g = sum(d.shard_histogram(nranks, r) for r, d in enumerate(devs))
+    assert int(g.sum()) == len(text)
+    assert np.array_equal(g, oracle.shard_hist(text, 0, len(text)))
+    parts = []
+    from hkcsa.shard import slice_bounds
+    bounds = slice_bounds(g, len(text), nranks)
+    for r, d in enumerate(devs):
+        d.shard_build(g, nranks, r)
+        assert d.shard_range() == bounds[r]
+        parts.append(d.shard_sa())
+        d.close()
+    assert np.array_equal(np.concatenate(parts), ref)
+
+
+def test_shard_rccl_single_rank(hk):
+    text = oracle.synth_text(200001, bytes(range(0x20, 0x7F)), seed=13)
+    dev = hk.DeviceIndex.from_bytes(text, device=0)
+    dev.build_sa_sharded(hk.comm_unique_id(), 1, 0)
+    assert dev.shard_range() == (0, len(text))
+    assert np.array_equal(dev.shard_sa(), oracle.suffix_array(text))
+    dev.close()
+
+
+def test_timing_stats(hk):
+    dev = hk.DeviceIndex.synthetic(1 << 20, b"ACGT", seed=1)
+    dev.timing(True)
+    dev.build_sa()
+    dev.synchronize()
+    l, ms, b = dev.kernel_stats("radix_onesweep")
+    assert l >= 1 and ms > 0 and b > 0
+    dev.close()

@@ -1,0 +1,82 @@
+"""Host-side logic of the package (no GPU): codec, pattern packing, the reference's
+rank/select and Golomb-Rice classes, shard slice bounds."""
+import numpy as np
+import pytest
+
+from conftest import wt_golden_levels
+from csa.wavelet_tree import GolombRiceEncoder, SuccinctRankSelect
+from hkcsa import TextCodec, pack_patterns
+from hkcsa.shard import slice_bounds
+from oracle import oracle
+
+
+def test_codec_identity_latin1():
+    c = TextCodec("banana$")
+    assert c.identity
+    assert c.encode_text("banana$") == b"banana$"
+    assert c.encode_pattern("an") == b"an"
+    assert c.encode_pattern("€") is None
+    assert c.decode(b"nab") == "nab"
+
+
+def test_codec_remap_preserves_order():
+    t = "αβγα$"
+    c = TextCodec(t)
+    assert not c.identity
+    enc = c.encode_text(t)
+    assert sorted(enc) == [c.encode_symbol(ch) for ch in sorted(t)]
+    assert c.decode(enc) == t
+    assert c.encode_pattern("x") is None
+
+
+def test_codec_too_many_symbols():
+    with pytest.raises(ValueError):
+        TextCodec("".join(chr(0x400 + i) for i in range(300)))
+
+
+def test_pack_patterns():
+    d, o = pack_patterns([b"ab", b"", b"xyz"])
+    assert d.tobytes() == b"abxyz"
+    assert list(o) == [0, 2, 2, 5]
+    d, o = pack_patterns([])
+    assert len(d) == 0 and list(o) == [0]
+
+
+def test_rank_select_and_golomb_vs_golden(random_cases):
+    checked = 0
+    for name in random_cases.names:
+        c = random_cases.get(name)
+        for g in wt_golden_levels(c):
+            enc = GolombRiceEncoder(g["bits"])
+            assert np.array_equal(np.asarray(enc.encode(g["bits"]), np.uint8), g["golomb"]), name
+            rs = SuccinctRankSelect(g["bits"])
+            assert int(rs.rank(len(g["bits"]))) == int(g["bits"].sum())
+            checked += 1
+        if "wtq_i" in c:
+            gl = wt_golden_levels(c)[-1]
+            rs = SuccinctRankSelect(gl["bits"])
+            for i, r, s in zip(c["wtq_i"], c["wtq_rank"], c["wtq_select"]):
+                assert int(rs.rank(int(i) + 1)) == int(r), name
+                assert int(rs.select(int(i))) == int(s), name
+    assert checked > 100
+
+
+def test_golomb_m_matches_kat(kat):
+    for word in ["banana", "mississippi", "ACGTTGCAAC"]:
+        lv = kat[word]["wt_bwt"]
+        if lv:
+            bits = [int(x) for x in lv[0]["bits"]]
+            assert GolombRiceEncoder(bits).m == kat[word]["wt_bwt_m"]
+
+
+@pytest.mark.parametrize("nranks", [1, 2, 3, 8])
+def test_slice_bounds_tile_the_sa(nranks):
+    t = oracle.synth_text(20000, b"ACGT", seed=4)
+    h = oracle.shard_hist(t, 0, len(t))
+    b = slice_bounds(h, len(t), nranks)
+    assert b[0][0] == 0 and b[-1][1] == len(t)
+    for (lo, hi), (lo2, _) in zip(b, b[1:]):
+        assert hi == lo2 and lo <= hi
+    # slices stay near n/N for a high-entropy text
+    for lo, hi in b:
+        assert abs((hi - lo) - len(t) / nranks) < 0.05 * len(t) + 64
