@@ -17,12 +17,15 @@ struct WtTables {                // per level, per dense code (host mirror of th
   uint8_t depth[256];
 };
 
-// suffix key layout: [q dense codes of b bits][prev-symbol code, pb bits (0 or b)]
+// suffix key layout: [q dense codes as one mixed-radix number, radix R = sigma'+1, code 0 = end
+// of text][code of the preceding symbol, pb bits].  Sorting uses bits [pb, key_bits).
 struct KeyGeom {
-  int b = 0, q = 0, pb = 0, key_bits = 0;
+  int q = 0, pb = 0, sym_bits = 0, key_bits = 0;
+  uint64_t R = 2;
   uint16_t lut[256];   // byte -> dense code + 1 (0 = end of text)
   uint8_t inv[512];    // dense code + 1 -> byte
 };
+int mixed_radix_bits(uint64_t R, int q);   // bits of R^q - 1 (65 when it does not fit 64 bits)
 
 // kernel argument bundle for rank walks
 struct WtView {
@@ -112,8 +115,8 @@ void comm_unique_id(uint8_t id[128]);
 // shared by the single-GPU and sharded builds
 KeyGeom key_geometry(Index& ix, bool with_prev);
 void upload_geometry(Index& ix, const KeyGeom& kg);
-void pack_keys(const uint8_t* d_text, uint64_t n, uint64_t lo, uint64_t count, const uint16_t* d_lut, int b, int q,
-               int pb, uint64_t* d_keys, hipStream_t s);
+void pack_keys(const uint8_t* d_text, uint64_t n, uint64_t lo, uint64_t count, const uint16_t* d_lut, uint64_t R,
+               int q, int pb, uint64_t* d_keys, hipStream_t s);
 template <typename V>
 void refine_after_sort(Index& ix, const KeyGeom& kg, int slot, uint64_t m, bool allow_doubling);
 

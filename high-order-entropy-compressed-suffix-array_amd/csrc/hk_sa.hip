@@ -20,6 +20,8 @@
 //      ISA[p+h]), doubling h until no ties remain.
 // High-entropy texts (the sigma=4 bench configs) finish after step 3's first round.
 
+#include <cmath>
+
 #include "hk_index.hpp"
 
 namespace hk {
@@ -91,10 +93,10 @@ __global__ __launch_bounds__(256) void k_byte_hist(const uint8_t* __restrict__ t
 }
 
 // ------------------------------------------------------------- keys
-// key(p) = [code(T[p]) .. code(T[p+q-1])] << pb | code(T[p-1])   (pb = prev-field bits, 0 or b)
+// key(p) = (code(T[p]) .. code(T[p+q-1]) as a radix-R number) << pb | code(T[p-1])
 constexpr int PK_TILE = 4096;
 __global__ __launch_bounds__(256) void k_pack_keys(const uint8_t* __restrict__ t, uint64_t n, uint64_t lo,
-                                                   uint64_t count, const uint16_t* __restrict__ lut, int b,
+                                                   uint64_t count, const uint16_t* __restrict__ lut, uint64_t R,
                                                    int q, int pb, uint64_t* __restrict__ keys) {
   __shared__ uint16_t c[PK_TILE + 72];
   __shared__ uint16_t L[256];
@@ -116,7 +118,7 @@ __global__ __launch_bounds__(256) void k_pack_keys(const uint8_t* __restrict__ t
     const uint64_t p = base + off;
     if (p < end) {
       uint64_t key = 0;
-      for (int j = 1; j <= q; ++j) key = (key << b) | c[off + j];
+      for (int j = 1; j <= q; ++j) key = key * R + c[off + j];
       keys[p - lo] = (key << pb) | (pb ? c[off] : 0u);
     }
   }
@@ -268,11 +270,11 @@ __global__ __launch_bounds__(GR_T) void k_refine_apply(
   }
 }
 
-// chunk refinement key: (group ordinal << (64-gbits)) | next qn codes of the suffix from offset h
+// chunk refinement key: (group ordinal << (64-gbits)) | next qn codes of the suffix from offset h (radix R)
 template <typename V>
 __global__ __launch_bounds__(256) void k_refine_keys(const V* __restrict__ P, const uint32_t* __restrict__ G,
                                                      uint64_t A, const uint8_t* __restrict__ t, uint64_t n,
-                                                     const uint16_t* __restrict__ lut, int b, int qn, int gbits,
+                                                     const uint16_t* __restrict__ lut, uint64_t R, int qn, int gbits,
                                                      uint64_t h, uint64_t* __restrict__ keys, V* __restrict__ vals) {
   __shared__ uint16_t L[256];
   L[threadIdx.x] = lut[threadIdx.x];
@@ -283,7 +285,7 @@ __global__ __launch_bounds__(256) void k_refine_keys(const V* __restrict__ P, co
     uint64_t chunk = 0;
     for (int j = 0; j < qn; ++j) {
       const uint64_t x = s + j;
-      chunk = (chunk << b) | (x < n ? L[t[x]] : 0u);
+      chunk = chunk * R + (x < n ? L[t[x]] : 0u);
     }
     keys[a] = gbits ? (((uint64_t)G[a] << (64 - gbits)) | chunk) : chunk;
     vals[a] = p;
@@ -540,14 +542,47 @@ std::pair<uint64_t, uint64_t> refine_step(Index& ix, const KeyGeom& kg, const ui
 }  // namespace
 
 // ---------------------------------------------------------------- geometry
+int mixed_radix_bits(uint64_t R, int q) {
+  unsigned __int128 p = 1;
+  for (int i = 0; i < q; ++i) {
+    p *= R;
+    if (p > ((unsigned __int128)1 << 64)) return 65;
+  }
+  p -= 1;
+  int b = 0;
+  while (p) {
+    ++b;
+    p >>= 1;
+  }
+  return b;
+}
+
+// Symbols per key: minimise (radix passes) * n + 10 * (expected tied suffixes), the latter from the
+// iid collision rate sum(p_c^2)^q of the symbol histogram (ties are refined, not wrong — this only
+// decides speed; texts with repeats tie more, refinement/doubling absorb that).
 KeyGeom key_geometry(Index& ix, bool with_prev) {
   compute_alphabet(ix);
   KeyGeom g{};
-  g.b = 1;
-  while ((1 << g.b) < ix.sigma + 1) ++g.b;
-  g.pb = with_prev ? g.b : 0;
-  g.q = (64 - g.pb) / g.b;
-  g.key_bits = g.q * g.b + g.pb;
+  g.R = (uint64_t)ix.sigma + 1;
+  int pbits = 1;
+  while ((1 << pbits) < ix.sigma + 1) ++pbits;
+  g.pb = with_prev ? pbits : 0;
+  double p2 = 0;
+  const double n = (double)(ix.n ? ix.n : 1);
+  for (int c = 0; c < 256; ++c) p2 += ((double)ix.byte_hist[c] / n) * ((double)ix.byte_hist[c] / n);
+  double best = 1e300;
+  for (int q = 1; q <= 64; ++q) {
+    const int sb = mixed_radix_bits(g.R, q);
+    if (g.pb + sb > 64) break;
+    const double ties = std::min(n, n * n * std::pow(p2, (double)q));
+    const double cost = (double)((sb + 7) / 8) * n + 10.0 * ties;
+    if (cost <= best) {
+      best = cost;
+      g.q = q;
+      g.sym_bits = sb;
+    }
+  }
+  g.key_bits = g.pb + g.sym_bits;
   for (int c = 0; c < 256; ++c) g.lut[c] = ix.code_of[c] < 0 ? 0 : (uint16_t)(ix.code_of[c] + 1);
   memset(g.inv, 0, sizeof(g.inv));
   for (int k = 0; k < ix.sigma; ++k) g.inv[k + 1] = ix.syms[k];
@@ -591,12 +626,13 @@ void refine_after_sort(Index& ix, const KeyGeom& kg, int slot, uint64_t m, bool 
     if (allow_doubling && rounds > kChunkRounds) break;
     int gbits = 0;
     while (gbits < 64 && (1ull << gbits) < groups) ++gbits;
-    const int qn = (64 - gbits) / kg.b;
+    int qn = 0;
+    while (gbits + mixed_radix_bits(kg.R, qn + 1) <= 64) ++qn;
     if (qn < 1) throw ApiError{-6, "too many tied groups for one refinement key"};
     {
       TimedLaunch tm(ix.timer, "sa_refine_keys", (double)A * (sizeof(V) * 2 + 4 + 8));
       k_refine_keys<V><<<grid_for(A), 256, 0, s>>>(ix.act[cur][0].as<V>(), ix.act[cur][2].as<uint32_t>(), A,
-                                                   ix.text.as<uint8_t>(), ix.n, d_lut, kg.b, qn, gbits, h, kp[0],
+                                                   ix.text.as<uint8_t>(), ix.n, d_lut, kg.R, qn, gbits, h, kp[0],
                                                    vp[0]);
       HK_HIP(hipGetLastError());
     }
@@ -656,11 +692,11 @@ void refine_after_sort(Index& ix, const KeyGeom& kg, int slot, uint64_t m, bool 
 template void refine_after_sort<uint32_t>(Index&, const KeyGeom&, int, uint64_t, bool);
 template void refine_after_sort<uint64_t>(Index&, const KeyGeom&, int, uint64_t, bool);
 
-void pack_keys(const uint8_t* d_text, uint64_t n, uint64_t lo, uint64_t count, const uint16_t* d_lut, int b, int q,
-               int pb, uint64_t* d_keys, hipStream_t s) {
+void pack_keys(const uint8_t* d_text, uint64_t n, uint64_t lo, uint64_t count, const uint16_t* d_lut, uint64_t R,
+               int q, int pb, uint64_t* d_keys, hipStream_t s) {
   if (!count) return;
   const uint64_t g = ceil_div(count, PK_TILE);
-  k_pack_keys<<<(unsigned)g, 256, 0, s>>>(d_text, n, lo, count, d_lut, b, q, pb, d_keys);
+  k_pack_keys<<<(unsigned)g, 256, 0, s>>>(d_text, n, lo, count, d_lut, R, q, pb, d_keys);
   HK_HIP(hipGetLastError());
 }
 
@@ -731,7 +767,7 @@ void build_sa(Index& ix) {
   {
     TimedLaunch t(ix.timer, "sa_pack_keys", (double)n * 9);
     pack_keys(ix.text.as<uint8_t>(), n, 0, n, reinterpret_cast<const uint16_t*>(ix.small.as<uint8_t>() + 2048),
-              kg.b, kg.q, kg.pb, ix.keys[0].as<uint64_t>(), s);
+              kg.R, kg.q, kg.pb, ix.keys[0].as<uint64_t>(), s);
   }
   uint64_t* kp[2] = {ix.keys[0].as<uint64_t>(), ix.keys[1].as<uint64_t>()};
   uint32_t* vp[2] = {ix.vals[0].as<uint32_t>(), ix.vals[1].as<uint32_t>()};

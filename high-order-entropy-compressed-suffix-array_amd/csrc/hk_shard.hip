@@ -34,9 +34,9 @@ struct ShardComm {  // one RCCL communicator per process (one process per GPU)
 };
 
 // key of suffix p from LDS-staged codes: c[off] = code(T[p-1]), c[off+1..off+q] = code(T[p..])
-__device__ __forceinline__ uint64_t key_at(const uint16_t* c, int off, int b, int q, int pb) {
+__device__ __forceinline__ uint64_t key_at(const uint16_t* c, int off, uint64_t R, int q, int pb) {
   uint64_t key = 0;
-  for (int j = 1; j <= q; ++j) key = (key << b) | c[off + j];
+  for (int j = 1; j <= q; ++j) key = key * R + c[off + j];
   return (key << pb) | (pb ? c[off] : 0u);
 }
 
@@ -49,7 +49,7 @@ __device__ __forceinline__ void stage_codes(uint16_t* c, const uint16_t* L, cons
 }
 
 __global__ __launch_bounds__(256) void k_shard_hist(const uint8_t* __restrict__ t, uint64_t n, uint64_t lo,
-                                                    uint64_t hi, const uint16_t* __restrict__ lut, int b, int q,
+                                                    uint64_t hi, const uint16_t* __restrict__ lut, uint64_t R, int q,
                                                     int pb, int bsh, unsigned long long* __restrict__ hist) {
   __shared__ uint32_t H[SH_BUCKETS];
   __shared__ uint16_t c[PS_TILE + 72];
@@ -62,7 +62,7 @@ __global__ __launch_bounds__(256) void k_shard_hist(const uint8_t* __restrict__ 
     __syncthreads();
     for (int k = 0; k < PS_TILE / 256; ++k) {
       const int off = k * 256 + threadIdx.x;
-      if (base + off < hi) atomicAdd(&H[key_at(c, off, b, q, pb) >> bsh], 1u);
+      if (base + off < hi) atomicAdd(&H[key_at(c, off, R, q, pb) >> bsh], 1u);
     }
     __syncthreads();
   }
@@ -72,7 +72,7 @@ __global__ __launch_bounds__(256) void k_shard_hist(const uint8_t* __restrict__ 
 
 template <typename V>
 __global__ __launch_bounds__(256) void k_pack_select(const uint8_t* __restrict__ t, uint64_t n,
-                                                     const uint16_t* __restrict__ lut, int b, int q, int pb, int bsh,
+                                                     const uint16_t* __restrict__ lut, uint64_t R, int q, int pb, int bsh,
                                                      uint32_t blo, uint32_t bhi, uint64_t* __restrict__ keys,
                                                      V* __restrict__ vals, unsigned long long* counter) {
   __shared__ uint16_t c[PS_TILE + 72];
@@ -90,7 +90,7 @@ __global__ __launch_bounds__(256) void k_pack_select(const uint8_t* __restrict__
 #pragma unroll
     for (int k = 0; k < PS_TILE / 256; ++k) {
       const int off = k * 256 + threadIdx.x;
-      kk[k] = key_at(c, off, b, q, pb);
+      kk[k] = key_at(c, off, R, q, pb);
       const uint32_t bk = (uint32_t)(kk[k] >> bsh);
       if (base + off < n && bk >= blo && bk < bhi) sel |= 1u << k;
     }
@@ -177,7 +177,7 @@ void shard_build_t(Index& ix, const uint64_t* ghist, int nranks, int rank) {
   {
     TimedLaunch t(ix.timer, "shard_pack_select", (double)n + (double)m * (8 + sizeof(V)));
     k_pack_select<V><<<grid_for(n, PS_TILE, 8192), 256, 0, s>>>(
-        ix.text.as<uint8_t>(), n, reinterpret_cast<const uint16_t*>(ix.small.as<uint8_t>() + 2048), kg.b, kg.q,
+        ix.text.as<uint8_t>(), n, reinterpret_cast<const uint16_t*>(ix.small.as<uint8_t>() + 2048), kg.R, kg.q,
         kg.pb, bsh, blo, bhi, ix.keys[0].as<uint64_t>(), ix.vals[0].as<V>(), d_counter);
     HK_HIP(hipGetLastError());
   }
@@ -210,7 +210,7 @@ void shard_histogram(Index& ix, int nranks, int rank, uint64_t* d_hist) {
   if (hi > lo) {
     TimedLaunch t(ix.timer, "shard_hist", (double)(hi - lo));
     k_shard_hist<<<grid_for(hi - lo, PS_TILE, 2048), 256, 0, s>>>(
-        ix.text.as<uint8_t>(), ix.n, lo, hi, reinterpret_cast<const uint16_t*>(ix.small.as<uint8_t>() + 2048), kg.b,
+        ix.text.as<uint8_t>(), ix.n, lo, hi, reinterpret_cast<const uint16_t*>(ix.small.as<uint8_t>() + 2048), kg.R,
         kg.q, kg.pb, bucket_shift(kg), reinterpret_cast<unsigned long long*>(d_hist));
     HK_HIP(hipGetLastError());
   }

@@ -251,7 +251,7 @@ struct OsShared {
 // Decoupled lookback for digit d of tile `tile`: sums predecessor counts until an inclusive
 // prefix is found.  Up to LB_WIN predecessor granules are loaded at once (independent sc1 loads),
 // so a chain of k not-yet-inclusive predecessors costs ~k/LB_WIN memory round trips, not k.
-constexpr int LB_WIN = 16;
+template <int LB_WIN>
 __device__ __forceinline__ uint64_t lookback(const uint64_t* status, uint32_t tile, uint32_t d, uint32_t epoch,
                                              uint32_t* err) {
   uint64_t excl = 0;
@@ -288,13 +288,17 @@ __device__ __forceinline__ uint64_t lookback(const uint64_t* status, uint32_t ti
   return excl;
 }
 
-// MODE 0 = production.  Diagnostic ablations (wrong results, in-bounds writes):
+// MODE 0 = decoupled lookback (single kernel per pass).
+// MODE 4 = downsweep of the reduce-then-scan pass: the tile's global digit offsets come from a
+//          precomputed table tpre[tile * 256 + d] (no in-kernel hand-off); `goff` is that table.
+// Diagnostic ablations (wrong results, in-bounds writes):
 //   1 = no decoupled lookback (tile prefix taken as 0)
 //   2 = no lookback and no LDS staging (scatter straight from registers)
+//   3 = lookback with tile id = workgroup id (no tile counter)
 // Order of work per tile: load keys -> wave ranking -> tile digit scan -> keys into LDS in sorted
 // order -> value loads issued -> lookback (its latency overlaps the value loads) -> keys out ->
 // values into LDS -> values out.
-template <typename V, int T, int I, int MODE>
+template <typename V, int T, int I, int MODE, int LBW = 16>
 __global__ __launch_bounds__(T, 4) void k_onesweep(
     const uint64_t* __restrict__ kin, const V* __restrict__ vin, uint64_t* __restrict__ kout,
     V* __restrict__ vout, uint64_t n, uint32_t shift, const uint64_t* __restrict__ goff,
@@ -306,9 +310,10 @@ __global__ __launch_bounds__(T, 4) void k_onesweep(
   const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
 
   for (uint32_t i = tid; i < W * 256; i += T) (&sh.whist[0][0])[i] = 0;
-  if (tid == 0) sh.tile = atomicAdd(tile_counter, 1u);
+  if (MODE != 3 && MODE != 4 && tid == 0) sh.tile = atomicAdd(tile_counter, 1u);
   __syncthreads();
-  const uint32_t tile = sh.tile;
+  // MODE 3: tile id = workgroup id (relies on in-order workgroup dispatch; spins stay bounded)
+  const uint32_t tile = (MODE == 3 || MODE == 4) ? blockIdx.x : sh.tile;
   const uint64_t tbase = (uint64_t)tile * TILE;
   const uint64_t wbase = tbase + (uint64_t)wv * WSPAN;
 
@@ -365,7 +370,7 @@ __global__ __launch_bounds__(T, 4) void k_onesweep(
     uint32_t carry = 0;
     for (uint32_t w = 0; w < wv; ++w) carry += sh.wsum[w];
     sh.tstart[tid] += carry;
-    if (MODE == 0) {  // publish this tile's counts as early as possible
+    if (MODE == 0 || MODE == 3) {  // publish this tile's counts as early as possible
       st_agent(status + (uint64_t)tile * 256 + tid, st_pack(epoch, tile == 0 ? ST_INC : ST_AGG, tcount));
     }
   }
@@ -410,12 +415,12 @@ __global__ __launch_bounds__(T, 4) void k_onesweep(
   if (tid < 256) {
     const uint32_t d = tid;
     uint64_t excl = 0;
-    if (MODE == 0 && tile > 0) {
-      excl = lookback(status, tile, d, epoch, err);
+    if ((MODE == 0 || MODE == 3) && tile > 0) {
+      excl = lookback<LBW>(status, tile, d, epoch, err);
       st_agent(status + (uint64_t)tile * 256 + d, st_pack(epoch, ST_INC, excl + tcount));
     }
-    uint64_t go = goff[d];
-    if (MODE != 0 && go + TILE > n) go = n > (uint64_t)TILE ? n - TILE : 0;  // ablations stay in bounds
+    uint64_t go = MODE == 4 ? (uint64_t)reinterpret_cast<const uint32_t*>(goff)[(uint64_t)tile * 256 + d] : goff[d];
+    if ((MODE == 1 || MODE == 2) && go + TILE > n) go = n > (uint64_t)TILE ? n - TILE : 0;  // ablations in bounds
     sh.gbase[d] = go + excl - sh.tstart[d];
   }
   __syncthreads();
@@ -552,7 +557,7 @@ int radix_sort_pairs(SortWork& w, KernelTimer& tm, uint64_t* k[2], V* v[2], int 
 // ---------------------------------------------------------------- diagnostics
 // Times `reps` radix passes of variant (threads x items, mode) over n DNA-text keys (u32 values)
 // plus a plain pair copy of the same bytes; used to decide where a pass spends its time.
-template <int T, int I, int MODE>
+template <int T, int I, int MODE, int LBW = 16>
 static double time_variant(SortWork& w, uint64_t* k[2], uint32_t* v[2], uint64_t n, int reps, int bit_lo,
                            const uint64_t* pristine, hipStream_t s) {
   // every variant starts from the same keys: the ablations scramble the multiset, and an exact
@@ -572,7 +577,7 @@ static double time_variant(SortWork& w, uint64_t* k[2], uint32_t* v[2], uint64_t
   for (int r = 0; r < reps + 1; ++r) {
     HK_HIP(hipMemsetAsync(w.counters.p, 0, 4, s));
     HK_HIP(hipEventRecord(a, s));
-    k_onesweep<uint32_t, T, I, MODE><<<(unsigned)tiles, T, 0, s>>>(
+    k_onesweep<uint32_t, T, I, MODE, LBW><<<(unsigned)tiles, T, 0, s>>>(
         k[r & 1], v[r & 1], k[(r + 1) & 1], v[(r + 1) & 1], n, (uint32_t)(bit_lo + 8 * (r % 7)),
         w.offs.as<uint64_t>() + (r % 7) * 256, w.status.as<uint64_t>(), w.counters.as<uint32_t>(),
         (uint32_t)(r + 1), w.err.as<uint32_t>(), 0);
@@ -606,10 +611,10 @@ void debug_radix_bench(SortWork& w, uint64_t* k[2], uint32_t* v[2], uint64_t n, 
   double r[8] = {0};
   r[0] = time_variant<512, 16, 0>(w, k, v, n, reps, bit_lo, pk, s);
   r[1] = time_variant<512, 16, 1>(w, k, v, n, reps, bit_lo, pk, s);
-  r[2] = time_variant<512, 16, 2>(w, k, v, n, reps, bit_lo, pk, s);
-  r[3] = time_variant<256, 16, 0>(w, k, v, n, reps, bit_lo, pk, s);
-  r[4] = time_variant<256, 16, 1>(w, k, v, n, reps, bit_lo, pk, s);
-  r[5] = time_variant<1024, 8, 0>(w, k, v, n, reps, bit_lo, pk, s);
+  r[2] = time_variant<512, 16, 0, 4>(w, k, v, n, reps, bit_lo, pk, s);
+  r[3] = time_variant<512, 16, 0, 32>(w, k, v, n, reps, bit_lo, pk, s);
+  r[4] = time_variant<512, 16, 0, 64>(w, k, v, n, reps, bit_lo, pk, s);
+  r[5] = time_variant<512, 16, 0, 8>(w, k, v, n, reps, bit_lo, pk, s);
   {
     hipEvent_t a, b;
     HK_HIP(hipEventCreate(&a));

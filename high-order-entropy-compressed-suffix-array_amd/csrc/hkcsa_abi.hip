@@ -481,6 +481,18 @@ int hkcsa_shard_range(hkcsa_index* h, uint64_t* lo, uint64_t* hi) {
   });
 }
 
+int hkcsa_key_geometry(hkcsa_index* h, int* q, int* pb, uint64_t* radix, int* key_bits) {
+  return guarded([&] {
+    activate(h);
+    need(q && pb && radix && key_bits, HKCSA_E_INVALID, "null output");
+    hk::KeyGeom kg = hk::key_geometry(h->ix, true);
+    *q = kg.q;
+    *pb = kg.pb;
+    *radix = kg.R;
+    *key_bits = kg.key_bits;
+  });
+}
+
 // ------------------------------------------------------------ diagnostics
 int hkcsa_debug_radix_bench(uint64_t n, int reps, double* out, int nout) {
   return guarded([&] {
@@ -496,7 +508,7 @@ int hkcsa_debug_radix_bench(uint64_t n, int reps, double* out, int nout) {
       ix.vals[i].ensure(n * 4 + 16);
     }
     hk::pack_keys(ix.text.as<uint8_t>(), n, 0, n, reinterpret_cast<const uint16_t*>(ix.small.as<uint8_t>() + 2048),
-                  kg.b, kg.q, kg.pb, ix.keys[0].as<uint64_t>(), ix.stream);
+                  kg.R, kg.q, kg.pb, ix.keys[0].as<uint64_t>(), ix.stream);
     hk::fill_iota<uint32_t>(ix.vals[0].as<uint32_t>(), n, ix.stream);
     uint64_t* kp[2] = {ix.keys[0].as<uint64_t>(), ix.keys[1].as<uint64_t>()};
     uint32_t* vp[2] = {ix.vals[0].as<uint32_t>(), ix.vals[1].as<uint32_t>()};

@@ -156,6 +156,10 @@ int hkcsa_shard_buckets(void);
 int hkcsa_shard_histogram(hkcsa_index* ix, int nranks, int rank, uint64_t* hist_out);
 int hkcsa_shard_build(hkcsa_index* ix, const uint64_t* global_hist, int nranks, int rank);
 
+/* Suffix-key geometry chosen for this text (parity export for the shard tests):
+ * q symbols as a radix-`radix` number above a pb-bit preceding-symbol field. */
+int hkcsa_key_geometry(hkcsa_index* ix, int* q, int* pb, uint64_t* radix, int* key_bits);
+
 /* ---- diagnostics ------------------------------------------------------ */
 /* Per-pass milliseconds of radix-pass variants over n synthetic DNA keys
  * (u32 values): out = {512x16, 512x16 without lookback, 512x16 without lookback

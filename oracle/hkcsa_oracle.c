@@ -12,6 +12,7 @@
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
+#include <math.h>
 
 /* ---------------------------------------------------------------- suffix order
  * csa/suffix_array.py:131-134 sorts (text[i:], i) tuples: Python str order, i.e. code point
@@ -229,39 +230,69 @@ int oracle_wt_levels(const uint8_t* seq, uint64_t n, uint8_t* bits /* 8*n */) {
 }
 
 /* ------------------------------------------------------------- shard partition
- * Host restatement of the sharded build's partition (hk_shard.hip): the key of suffix p packs
- * its first q dense codes (code 0 past the end, b bits each) above the code of T[p-1]
- * (T[n-1] for p = 0); q = (64 - b) / b.  Its bucket is the top 14 bits of the key. */
-void oracle_shard_geometry(const uint8_t* t, uint64_t n, int* b, int* q, int* bsh, uint8_t lut[256]) {
-  int present[256] = {0}, sigma = 0;
-  for (uint64_t i = 0; i < n; ++i) present[t[i]] = 1;
-  uint16_t code[256];
-  for (int c = 0; c < 256; ++c) code[c] = present[c] ? (uint16_t)(++sigma) : 0;
-  int bb = 1;
-  while ((1 << bb) < sigma + 1) ++bb;
-  *b = bb;
-  *q = (64 - bb) / bb;
-  *bsh = (*q + 1) * bb - 14;
-  if (*bsh < 0) *bsh = 0;
-  for (int c = 0; c < 256; ++c) lut[c] = (uint8_t)code[c]; /* callers use lut only when sigma < 256 */
+ * Host restatement of the sharded build's partition (hk_sa.hip key_geometry, hk_shard.hip):
+ * the key of suffix p is its first q dense codes (code 0 past the end) as one radix-R number,
+ * R = sigma + 1, shifted above the pb-bit code of T[p-1] (T[n-1] for p = 0).  q minimises
+ * passes * n + 10 * min(n, n^2 * sum(p_c^2)^q).  The bucket is the top 14 bits of the key. */
+static int mixed_radix_bits(uint64_t R, int q) {
+  unsigned __int128 p = 1;
+  for (int i = 0; i < q; ++i) {
+    p *= R;
+    if (p > ((unsigned __int128)1 << 64)) return 65;
+  }
+  p -= 1;
+  int b = 0;
+  while (p) {
+    ++b;
+    p >>= 1;
+  }
+  return b;
 }
 
-static uint64_t shard_key(const uint8_t* t, uint64_t n, uint64_t p, int b, int q, const uint16_t* code) {
-  uint64_t key = 0;
-  for (int j = 0; j < q; ++j) key = (key << b) | (p + j < n ? code[t[p + j]] : 0);
-  return (key << b) | code[t[p == 0 ? n - 1 : p - 1]];
+int oracle_key_geometry(const uint8_t* t, uint64_t n, int* q_out, int* pb_out, uint64_t* R_out, int* kb_out,
+                        uint16_t code[256]) {
+  uint64_t h[256] = {0};
+  for (uint64_t i = 0; i < n; ++i) h[t[i]]++;
+  int sigma = 0;
+  for (int c = 0; c < 256; ++c) code[c] = h[c] ? (uint16_t)(++sigma) : 0;
+  const uint64_t R = (uint64_t)sigma + 1;
+  int pb = 1;
+  while ((1 << pb) < sigma + 1) ++pb;
+  double p2 = 0, nn = (double)(n ? n : 1);
+  for (int c = 0; c < 256; ++c) p2 += ((double)h[c] / nn) * ((double)h[c] / nn);
+  double best = 1e300;
+  int bq = 1, bsb = 0;
+  for (int q = 1; q <= 64; ++q) {
+    const int sb = mixed_radix_bits(R, q);
+    if (pb + sb > 64) break;
+    double ties = nn * nn * pow(p2, (double)q);
+    if (ties > nn) ties = nn;
+    const double cost = (double)((sb + 7) / 8) * nn + 10.0 * ties;
+    if (cost <= best) {
+      best = cost;
+      bq = q;
+      bsb = sb;
+    }
+  }
+  *q_out = bq;
+  *pb_out = pb;
+  *R_out = R;
+  *kb_out = pb + bsb;
+  return sigma;
 }
 
 void oracle_shard_hist(const uint8_t* t, uint64_t n, uint64_t lo, uint64_t hi, uint64_t* hist /* 16384 */) {
-  int present[256] = {0}, sigma = 0;
-  for (uint64_t i = 0; i < n; ++i) present[t[i]] = 1;
   uint16_t code[256];
-  for (int c = 0; c < 256; ++c) code[c] = present[c] ? (uint16_t)(++sigma) : 0;
-  int b = 1;
-  while ((1 << b) < sigma + 1) ++b;
-  const int q = (64 - b) / b;
-  int bsh = (q + 1) * b - 14;
+  int q, pb, kb;
+  uint64_t R;
+  oracle_key_geometry(t, n, &q, &pb, &R, &kb, code);
+  int bsh = kb - 14;
   if (bsh < 0) bsh = 0;
   memset(hist, 0, 16384 * sizeof(uint64_t));
-  for (uint64_t p = lo; p < hi; ++p) hist[shard_key(t, n, p, b, q, code) >> bsh]++;
+  for (uint64_t p = lo; p < hi; ++p) {
+    uint64_t key = 0;
+    for (int j = 0; j < q; ++j) key = key * R + (p + j < n ? code[t[p + j]] : 0);
+    key = (key << pb) | code[t[p == 0 ? n - 1 : p - 1]];
+    hist[key >> bsh]++;
+  }
 }

@@ -53,6 +53,7 @@ def lib():
         L.oracle_wt_levels.argtypes = [vp, u64, vp]
         L.oracle_wt_levels.restype = C.c_int
         L.oracle_shard_hist.argtypes = [vp, u64, u64, u64, vp]
+        L.oracle_key_geometry.argtypes = [vp, u64, vp, vp, vp, vp, vp]
         _lib = L
     return _lib
 
@@ -118,6 +119,16 @@ def shard_hist(t, lo: int, hi: int) -> np.ndarray:
     h = np.zeros(16384, dtype=np.uint64)
     lib().oracle_shard_hist(_p(t), len(t), lo, hi, _p(h))
     return h
+
+
+def key_geometry(t) -> tuple[int, int, int, int]:
+    """(q, pb, radix, key_bits) the build chooses for text t."""
+    t = _u8(t)
+    q, pb, kb = C.c_int(0), C.c_int(0), C.c_int(0)
+    R = C.c_uint64(0)
+    code = np.zeros(256, dtype=np.uint16)
+    lib().oracle_key_geometry(_p(t), len(t), C.byref(q), C.byref(pb), C.byref(R), C.byref(kb), _p(code))
+    return q.value, pb.value, R.value, kb.value
 
 
 class FM:
