@@ -80,7 +80,20 @@ def cpu_baseline(sample_n: int, npat: int, seed: int = 3) -> dict:
     }
 
 
+def pmc_traffic_gb() -> float | None:
+    """HBM GB per radix_onesweep launch measured with rocprofv3 PMC counters on this config
+    (tools_pmc_summary.py -> profiles/pmc_radix_onesweep.json; FETCH_SIZE x2 gfx950 correction)."""
+    p = os.path.join(ROOT, "profiles", "pmc_radix_onesweep.json")
+    try:
+        with open(p) as f:
+            return float(json.load(f)["traffic_gb_per_launch"])
+    except Exception:
+        return None
+
+
 def roofline(dev: DeviceIndex, traffic_gb: float | None) -> dict:
+    if traffic_gb is None:
+        traffic_gb = pmc_traffic_gb()
     launches, ms, alg_bytes = dev.kernel_stats("radix_onesweep")
     if not launches:
         return {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None,
@@ -137,8 +150,9 @@ def run_single(args) -> dict:
     value = args.steps * n / 2**20 / wall
     info = dev.build_info()
     roof = roofline(dev, args.traffic_gb)
-    stages = stage_breakdown(dev, ["radix_hist", "radix_onesweep", "sa_pack_keys", "sa_group_stats",
-                                   "sa_group_apply", "sa_pair_keys", "bwt_gather", "byte_hist"])
+    stages = stage_breakdown(dev, ["radix_hist", "radix_onesweep", "radix_onesweep_small", "sa_pack_keys",
+                                   "sa_refine_stats", "sa_refine_apply", "sa_refine_keys", "sa_isa_scatter",
+                                   "sa_group_stats", "sa_group_apply", "sa_pair_keys", "bwt_gather", "byte_hist"])
     log(f"[bench] SA+BWT {wall / args.steps * 1e3:.2f} ms/step -> {value:.1f} MB/s; info={info[:8]}")
 
     # full build (adds the wavelet tree) and batched locate
@@ -273,7 +287,7 @@ def main():
     ap.add_argument("--cpu-patterns", type=int, default=1000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-gb", type=float, default=None,
-                    help="PMC-measured HBM GB per radix pass (from profiles/), reported as roofline.traffic")
+                    help="PMC-measured HBM GB per radix pass; default: profiles/pmc_radix_onesweep.json")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))

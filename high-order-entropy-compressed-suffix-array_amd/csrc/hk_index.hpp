@@ -116,7 +116,7 @@ void comm_unique_id(uint8_t id[128]);
 KeyGeom key_geometry(Index& ix, bool with_prev);
 void upload_geometry(Index& ix, const KeyGeom& kg);
 void pack_keys(const uint8_t* d_text, uint64_t n, uint64_t lo, uint64_t count, const uint16_t* d_lut, uint64_t R,
-               int q, int pb, uint64_t* d_keys, hipStream_t s);
+               int q, int pb, uint64_t* d_keys, hipStream_t s, uint64_t* d_hist0 = nullptr);
 template <typename V>
 void refine_after_sort(Index& ix, const KeyGeom& kg, int slot, uint64_t m, bool allow_doubling);
 

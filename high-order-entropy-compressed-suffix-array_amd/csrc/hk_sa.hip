@@ -93,35 +93,53 @@ __global__ __launch_bounds__(256) void k_byte_hist(const uint8_t* __restrict__ t
 }
 
 // ------------------------------------------------------------- keys
-// key(p) = (code(T[p]) .. code(T[p+q-1]) as a radix-R number) << pb | code(T[p-1])
+// key(p) = (code(T[p]) .. code(T[p+q-1]) as a radix-R number) << pb | code(T[p-1]);
+// also histograms the first sorted digit (bits [pb, pb+8)) for the radix sort's first pass.
 constexpr int PK_TILE = 4096;
 __global__ __launch_bounds__(256) void k_pack_keys(const uint8_t* __restrict__ t, uint64_t n, uint64_t lo,
                                                    uint64_t count, const uint16_t* __restrict__ lut, uint64_t R,
-                                                   int q, int pb, uint64_t* __restrict__ keys) {
+                                                   int q, int pb, int ck, uint64_t Rck, uint64_t Rlast,
+                                                   uint64_t* __restrict__ keys, unsigned long long* __restrict__ hist0) {
   __shared__ uint16_t c[PK_TILE + 72];
   __shared__ uint16_t L[256];
+  __shared__ uint32_t H[256];
   L[threadIdx.x] = lut[threadIdx.x];
-  __syncthreads();
-  const uint64_t base = lo + (uint64_t)blockIdx.x * PK_TILE;
-  for (int i = threadIdx.x; i < PK_TILE + q + 1; i += 256) {
-    const uint64_t p = base + i;  // c[i] holds position base + i - 1
-    uint16_t v;
-    if (i == 0) v = L[t[base == 0 ? n - 1 : base - 1]];
-    else v = (p - 1) < n ? L[t[p - 1]] : 0;
-    c[i] = v;
-  }
+  H[threadIdx.x] = 0;
   __syncthreads();
   const uint64_t end = lo + count;
-#pragma unroll 4
-  for (int k = 0; k < PK_TILE / 256; ++k) {
-    const int off = k * 256 + threadIdx.x;
-    const uint64_t p = base + off;
-    if (p < end) {
-      uint64_t key = 0;
-      for (int j = 1; j <= q; ++j) key = key * R + c[off + j];
-      keys[p - lo] = (key << pb) | (pb ? c[off] : 0u);
+  for (uint64_t base = lo + (uint64_t)blockIdx.x * PK_TILE; base < end; base += (uint64_t)gridDim.x * PK_TILE) {
+    for (int i = threadIdx.x; i < PK_TILE + q + 1; i += 256) {
+      const uint64_t p = base + i;  // c[i] holds position base + i - 1
+      uint16_t v;
+      if (i == 0) v = L[t[base == 0 ? n - 1 : base - 1]];
+      else v = (p - 1) < n ? L[t[p - 1]] : 0;
+      c[i] = v;
     }
+    __syncthreads();
+#pragma unroll 4
+    for (int k = 0; k < PK_TILE / 256; ++k) {
+      const int off = k * 256 + threadIdx.x;
+      const uint64_t p = base + off;
+      if (p < end) {
+        // radix-R Horner in 24-bit chunks (R^ck < 2^24: one v_mul_u32_u24 + add per symbol),
+        // chunks combined in 64-bit
+        uint64_t key = 0;
+        int j = 1;
+        while (j <= q) {
+          const int len = q - j + 1 < ck ? q - j + 1 : ck;
+          uint32_t cv = 0;
+          for (int u = 0; u < len; ++u) cv = __umul24(cv, (uint32_t)R) + c[off + j + u];
+          key = key * (len == ck ? Rck : Rlast) + cv;
+          j += len;
+        }
+        key = (key << pb) | (pb ? c[off] : 0u);
+        keys[p - lo] = key;
+        if (hist0) atomicAdd(&H[(uint32_t)(key >> pb) & 255u], 1u);
+      }
+    }
+    __syncthreads();
   }
+  if (hist0 && H[threadIdx.x]) atomicAdd(&hist0[threadIdx.x], (unsigned long long)H[threadIdx.x]);
 }
 
 // ------------------------------------------------------------- refinement
@@ -693,10 +711,20 @@ template void refine_after_sort<uint32_t>(Index&, const KeyGeom&, int, uint64_t,
 template void refine_after_sort<uint64_t>(Index&, const KeyGeom&, int, uint64_t, bool);
 
 void pack_keys(const uint8_t* d_text, uint64_t n, uint64_t lo, uint64_t count, const uint16_t* d_lut, uint64_t R,
-               int q, int pb, uint64_t* d_keys, hipStream_t s) {
+               int q, int pb, uint64_t* d_keys, hipStream_t s, uint64_t* d_hist0) {
+  if (d_hist0) HK_HIP(hipMemsetAsync(d_hist0, 0, 256 * 8, s));
   if (!count) return;
-  const uint64_t g = ceil_div(count, PK_TILE);
-  k_pack_keys<<<(unsigned)g, 256, 0, s>>>(d_text, n, lo, count, d_lut, R, q, pb, d_keys);
+  const uint64_t g = std::min<uint64_t>(ceil_div(count, PK_TILE), 4096);
+  int ck = 1;  // symbols per 24-bit chunk
+  uint64_t Rck = R;
+  while (Rck * R < (1ull << 24)) {
+    Rck *= R;
+    ++ck;
+  }
+  uint64_t Rlast = 1;
+  for (int i = 0; i < (q % ck ? q % ck : ck); ++i) Rlast *= R;
+  k_pack_keys<<<(unsigned)g, 256, 0, s>>>(d_text, n, lo, count, d_lut, R, q, pb, ck, Rck, Rlast, d_keys,
+                                          reinterpret_cast<unsigned long long*>(d_hist0));
   HK_HIP(hipGetLastError());
 }
 
@@ -764,14 +792,15 @@ void build_sa(Index& ix) {
     ix.keys[i].ensure(n * 8 + 16);
     ix.vals[i].ensure(n * 4 + 16);
   }
+  uint64_t* d_hist0 = ix.small.as<uint64_t>() + 640;   // byte 5120 of the scratch
   {
     TimedLaunch t(ix.timer, "sa_pack_keys", (double)n * 9);
     pack_keys(ix.text.as<uint8_t>(), n, 0, n, reinterpret_cast<const uint16_t*>(ix.small.as<uint8_t>() + 2048),
-              kg.R, kg.q, kg.pb, ix.keys[0].as<uint64_t>(), s);
+              kg.R, kg.q, kg.pb, ix.keys[0].as<uint64_t>(), s, d_hist0);
   }
   uint64_t* kp[2] = {ix.keys[0].as<uint64_t>(), ix.keys[1].as<uint64_t>()};
   uint32_t* vp[2] = {ix.vals[0].as<uint32_t>(), ix.vals[1].as<uint32_t>()};
-  int slot = radix_sort_pairs<uint32_t>(ix.sw, ix.timer, kp, vp, 0, n, kg.pb, kg.key_bits, true, s);
+  int slot = radix_sort_pairs<uint32_t>(ix.sw, ix.timer, kp, vp, 0, n, kg.pb, kg.key_bits, true, s, d_hist0);
   ix.info[0] += ix.sw.passes_run;
   ix.info[1] += ix.sw.passes_skipped;
   // the sorted values are the SA candidate order: adopt that buffer as SA

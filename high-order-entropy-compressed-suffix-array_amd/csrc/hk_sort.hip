@@ -227,6 +227,7 @@ __global__ __launch_bounds__(256) void k_hist_offsets(const uint64_t* __restrict
 constexpr int OS_T = 512;
 constexpr int OS_I = 16;
 constexpr int OS_TILE = OS_T * OS_I;   // 8192 pairs per tile (production variant)
+constexpr uint64_t kSmallSort = 1ull << 24;   // below this, sorts use the 256-thread tile variant
 constexpr uint64_t ST_VAL_MASK = (1ull << 46) - 1;
 constexpr uint64_t ST_AGG = 1, ST_INC = 2;
 constexpr uint32_t SPIN_LIMIT = 1u << 22;
@@ -244,6 +245,7 @@ struct OsShared {
   uint32_t whist[T / 64][256];   // per-wave digit counts, then per-wave exclusive prefix
   uint32_t tstart[256];          // tile-local exclusive digit start
   uint64_t gbase[256];           // global destination base minus tstart
+  uint32_t nhist[256];           // histogram of the NEXT pass's digit over this tile
   uint32_t wsum[4];
   uint32_t tile;
 };
@@ -298,11 +300,12 @@ __device__ __forceinline__ uint64_t lookback(const uint64_t* status, uint32_t ti
 // Order of work per tile: load keys -> wave ranking -> tile digit scan -> keys into LDS in sorted
 // order -> value loads issued -> lookback (its latency overlaps the value loads) -> keys out ->
 // values into LDS -> values out.
-template <typename V, int T, int I, int MODE, int LBW = 16>
+template <typename V, int T, int I, int MODE, int LBW = 4>
 __global__ __launch_bounds__(T, 4) void k_onesweep(
     const uint64_t* __restrict__ kin, const V* __restrict__ vin, uint64_t* __restrict__ kout,
     V* __restrict__ vout, uint64_t n, uint32_t shift, const uint64_t* __restrict__ goff,
-    uint64_t* status, uint32_t* tile_counter, uint32_t epoch, uint32_t* err, int iota) {
+    uint64_t* status, uint32_t* tile_counter, uint32_t epoch, uint32_t* err, int iota, int next_shift,
+    unsigned long long* __restrict__ hpart) {
   constexpr int W = T / 64;
   constexpr int TILE = T * I;
   constexpr int WSPAN = I * 64;
@@ -310,6 +313,7 @@ __global__ __launch_bounds__(T, 4) void k_onesweep(
   const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
 
   for (uint32_t i = tid; i < W * 256; i += T) (&sh.whist[0][0])[i] = 0;
+  if (tid < 256) sh.nhist[tid] = 0;
   if (MODE != 3 && MODE != 4 && tid == 0) sh.tile = atomicAdd(tile_counter, 1u);
   __syncthreads();
   // MODE 3: tile id = workgroup id (relies on in-order workgroup dispatch; spins stay bounded)
@@ -412,6 +416,17 @@ __global__ __launch_bounds__(T, 4) void k_onesweep(
     const uint64_t j = wbase + (uint64_t)k * 64 + lane;
     val[k] = iota ? (V)j : (j < n ? vin[j] : (V)0);
   }
+  const uint32_t tile_n = (uint32_t)((n - tbase) < (uint64_t)TILE ? (n - tbase) : TILE);
+  if (next_shift >= 0) {
+    // the next pass's digit histogram (the key multiset is the same in every pass); with 512
+    // threads the upper 256 count it from the staged keys while the lower 256 look back
+    __syncthreads();
+    if (T < 512 || tid >= 256) {
+      const uint32_t t0 = T < 512 ? tid : tid - 256, tn = T < 512 ? T : T - 256;
+      for (uint32_t s2 = t0; s2 < tile_n; s2 += tn)
+        atomicAdd(&sh.nhist[(uint32_t)(sh.stage.keys[s2] >> next_shift) & 255u], 1u);
+    }
+  }
   if (tid < 256) {
     const uint32_t d = tid;
     uint64_t excl = 0;
@@ -424,8 +439,11 @@ __global__ __launch_bounds__(T, 4) void k_onesweep(
     sh.gbase[d] = go + excl - sh.tstart[d];
   }
   __syncthreads();
+  if (next_shift >= 0 && tid < 256) {
+    const uint32_t c = sh.nhist[tid];
+    if (c) atomicAdd(&hpart[(uint64_t)(tile & 63) * 256 + tid], (unsigned long long)c);
+  }
 
-  const uint32_t tile_n = (uint32_t)((n - tbase) < (uint64_t)TILE ? (n - tbase) : TILE);
   uint32_t dg[(I + 3) / 4] = {};   // digits of the staged slots, 4 per register
 #pragma unroll
   for (int i = 0; i < I; ++i) {
@@ -449,6 +467,14 @@ __global__ __launch_bounds__(T, 4) void k_onesweep(
     const uint32_t s = (uint32_t)i * T + tid;
     if (s < tile_n) vout[sh.gbase[(dg[i >> 2] >> (8 * (i & 3))) & 255u] + s] = sh.stage.vals[s];
   }
+}
+
+// hist[d] = sum of the 64 partial histograms written by a pass
+__global__ __launch_bounds__(256) void k_hist_reduce(const unsigned long long* __restrict__ hpart,
+                                                     uint64_t* __restrict__ hist) {
+  uint64_t a = 0;
+  for (int p = 0; p < 64; ++p) a += hpart[p * 256 + threadIdx.x];
+  hist[threadIdx.x] = a;
 }
 
 // bandwidth reference for the pass shape: read (key, value), write them back shifted by one tile
@@ -479,8 +505,8 @@ void fill_iota(V* v, uint64_t n, hipStream_t s) {
 }
 
 template <typename V>
-int radix_sort_pairs(SortWork& w, KernelTimer& tm, uint64_t* k[2], V* v[2], int in_slot,
-                     uint64_t n, int bit_lo, int bit_hi, bool vals_iota, hipStream_t s) {
+int radix_sort_pairs(SortWork& w, KernelTimer& tm, uint64_t* k[2], V* v[2], int in_slot, uint64_t n, int bit_lo,
+                     int bit_hi, bool vals_iota, hipStream_t s, const uint64_t* d_hist0) {
   w.passes_run = 0;
   w.passes_skipped = 0;
   int cur = in_slot;
@@ -490,11 +516,16 @@ int radix_sort_pairs(SortWork& w, KernelTimer& tm, uint64_t* k[2], V* v[2], int 
   }
   const int np = (bit_hi - bit_lo + 7) / 8;
   if (np > 8) throw ApiError{-1, "radix_sort_pairs: more than 64 key bits"};
-  const uint64_t tiles = ceil_div(n, OS_TILE);
+  // large sorts: 512 threads x 16 keys per tile ("radix_onesweep", the roofline kernel);
+  // small sorts (refinement of tied suffixes): 256 x 16, its own kernel symbol and timer name
+  const bool small = n < kSmallSort;
+  const uint64_t tile_elems = small ? 256 * OS_I : OS_TILE;
+  const uint64_t tiles = ceil_div(n, tile_elems);
   if (tiles > 0xFFFFFFFFull) throw ApiError{-6, "radix_sort_pairs: too many tiles"};
 
-  w.hist.ensure(8 * 256 * 8);
+  w.hist.ensure(9 * 256 * 8);
   w.offs.ensure(8 * 256 * 8);
+  w.hpart.ensure(64 * 256 * 8);
   w.counters.ensure(64 * 4);
   w.err.ensure(16);
   if (tiles > w.status_tiles || !w.status.p) {
@@ -503,29 +534,36 @@ int radix_sort_pairs(SortWork& w, KernelTimer& tm, uint64_t* k[2], V* v[2], int 
     w.status_tiles = tiles;
     w.epoch = 0;
   }
-
-  // 1. histograms of every digit (one read of the keys)
-  HK_HIP(hipMemsetAsync(w.hist.p, 0, 8 * 256 * 8, s));
-  {
-    TimedLaunch t(tm, "radix_hist", (double)n * 8);
-    unsigned g = (unsigned)std::min<uint64_t>(ceil_div(n, HG_PER_BLOCK), 2048);
-    k_digit_hist<<<g, HG_T, 0, s>>>(k[cur], n, bit_lo, np, w.hist.as<unsigned long long>());
-    HK_HIP(hipGetLastError());
-  }
-  k_hist_offsets<<<np, 256, 0, s>>>(w.hist.as<uint64_t>(), w.offs.as<uint64_t>());
-  HK_HIP(hipGetLastError());
-  HK_HIP(hipMemcpyAsync(w.h_hist, w.hist.p, np * 256 * 8, hipMemcpyDeviceToHost, s));
   HK_HIP(hipMemsetAsync(w.counters.p, 0, 64 * 4, s));
   HK_HIP(hipMemsetAsync(w.err.p, 0, 4, s));
-  HK_HIP(hipStreamSynchronize(s));
+  uint64_t* hist = w.hist.as<uint64_t>();
+
+  // histogram of one digit straight from the keys in buffer `cur` (first digit, or after a skip)
+  auto digit_hist = [&](int p) {
+    HK_HIP(hipMemsetAsync(hist + p * 256, 0, 256 * 8, s));
+    TimedLaunch t(tm, "radix_hist", (double)n * 8);
+    unsigned g = (unsigned)std::min<uint64_t>(ceil_div(n, HG_PER_BLOCK), 2048);
+    k_digit_hist<<<g, HG_T, 0, s>>>(k[cur], n, bit_lo + 8 * p, 1,
+                                    reinterpret_cast<unsigned long long*>(hist + p * 256));
+    HK_HIP(hipGetLastError());
+  };
+  if (d_hist0) HK_HIP(hipMemcpyAsync(hist, d_hist0, 256 * 8, hipMemcpyDeviceToDevice, s));
+  else digit_hist(0);
 
   bool iota_pending = vals_iota;
   for (int p = 0; p < np; ++p) {
+    // the digit's histogram is complete here: offsets + single-bucket (skippable) check
+    k_hist_offsets<<<1, 256, 0, s>>>(hist + p * 256, w.offs.as<uint64_t>() + p * 256);
+    HK_HIP(hipGetLastError());
+    HK_HIP(hipMemcpyAsync(w.h_hist + p * 256, hist + p * 256, 256 * 8, hipMemcpyDeviceToHost, s));
+    HK_HIP(hipStreamSynchronize(s));
     bool trivial = false;
     for (int d = 0; d < 256; ++d)
       if (w.h_hist[p * 256 + d] == n) trivial = true;
+    const bool has_next = p + 1 < np;
     if (trivial) {
       w.passes_skipped++;
+      if (has_next) digit_hist(p + 1);
       continue;
     }
     if (w.epoch >= 0xFFFF) {
@@ -533,13 +571,26 @@ int radix_sort_pairs(SortWork& w, KernelTimer& tm, uint64_t* k[2], V* v[2], int 
       w.epoch = 0;
     }
     w.epoch++;
+    if (has_next) HK_HIP(hipMemsetAsync(w.hpart.p, 0, 64 * 256 * 8, s));
     const int nxt = cur ^ 1;
     {
-      TimedLaunch t(tm, "radix_onesweep", (double)n * 2.0 * (8 + sizeof(V)));
-      k_onesweep<V, OS_T, OS_I, 0><<<(unsigned)tiles, OS_T, 0, s>>>(
-          k[cur], iota_pending ? nullptr : v[cur], k[nxt], v[nxt], n, (uint32_t)(bit_lo + 8 * p),
-          w.offs.as<uint64_t>() + p * 256, w.status.as<uint64_t>(), w.counters.as<uint32_t>() + p,
-          w.epoch, w.err.as<uint32_t>(), iota_pending ? 1 : 0);
+      TimedLaunch t(tm, small ? "radix_onesweep_small" : "radix_onesweep", (double)n * 2.0 * (8 + sizeof(V)));
+      if (small)
+        k_onesweep<V, 256, OS_I, 0><<<(unsigned)tiles, 256, 0, s>>>(
+            k[cur], iota_pending ? nullptr : v[cur], k[nxt], v[nxt], n, (uint32_t)(bit_lo + 8 * p),
+            w.offs.as<uint64_t>() + p * 256, w.status.as<uint64_t>(), w.counters.as<uint32_t>() + p, w.epoch,
+            w.err.as<uint32_t>(), iota_pending ? 1 : 0, has_next ? bit_lo + 8 * (p + 1) : -1,
+            w.hpart.as<unsigned long long>());
+      else
+        k_onesweep<V, OS_T, OS_I, 0><<<(unsigned)tiles, OS_T, 0, s>>>(
+            k[cur], iota_pending ? nullptr : v[cur], k[nxt], v[nxt], n, (uint32_t)(bit_lo + 8 * p),
+            w.offs.as<uint64_t>() + p * 256, w.status.as<uint64_t>(), w.counters.as<uint32_t>() + p, w.epoch,
+            w.err.as<uint32_t>(), iota_pending ? 1 : 0, has_next ? bit_lo + 8 * (p + 1) : -1,
+            w.hpart.as<unsigned long long>());
+      HK_HIP(hipGetLastError());
+    }
+    if (has_next) {
+      k_hist_reduce<<<1, 256, 0, s>>>(w.hpart.as<unsigned long long>(), hist + (p + 1) * 256);
       HK_HIP(hipGetLastError());
     }
     iota_pending = false;
@@ -580,7 +631,7 @@ static double time_variant(SortWork& w, uint64_t* k[2], uint32_t* v[2], uint64_t
     k_onesweep<uint32_t, T, I, MODE, LBW><<<(unsigned)tiles, T, 0, s>>>(
         k[r & 1], v[r & 1], k[(r + 1) & 1], v[(r + 1) & 1], n, (uint32_t)(bit_lo + 8 * (r % 7)),
         w.offs.as<uint64_t>() + (r % 7) * 256, w.status.as<uint64_t>(), w.counters.as<uint32_t>(),
-        (uint32_t)(r + 1), w.err.as<uint32_t>(), 0);
+        (uint32_t)(r + 1), w.err.as<uint32_t>(), 0, -1, nullptr);
     HK_HIP(hipGetLastError());
     HK_HIP(hipEventRecord(b, s));
     HK_HIP(hipEventSynchronize(b));
@@ -611,9 +662,9 @@ void debug_radix_bench(SortWork& w, uint64_t* k[2], uint32_t* v[2], uint64_t n, 
   double r[8] = {0};
   r[0] = time_variant<512, 16, 0>(w, k, v, n, reps, bit_lo, pk, s);
   r[1] = time_variant<512, 16, 1>(w, k, v, n, reps, bit_lo, pk, s);
-  r[2] = time_variant<512, 16, 0, 4>(w, k, v, n, reps, bit_lo, pk, s);
-  r[3] = time_variant<512, 16, 0, 32>(w, k, v, n, reps, bit_lo, pk, s);
-  r[4] = time_variant<512, 16, 0, 64>(w, k, v, n, reps, bit_lo, pk, s);
+  r[2] = time_variant<512, 16, 0, 1>(w, k, v, n, reps, bit_lo, pk, s);
+  r[3] = time_variant<512, 16, 0, 2>(w, k, v, n, reps, bit_lo, pk, s);
+  r[4] = time_variant<512, 16, 0, 4>(w, k, v, n, reps, bit_lo, pk, s);
   r[5] = time_variant<512, 16, 0, 8>(w, k, v, n, reps, bit_lo, pk, s);
   {
     hipEvent_t a, b;
@@ -641,9 +692,9 @@ void debug_radix_bench(SortWork& w, uint64_t* k[2], uint32_t* v[2], uint64_t n, 
 }
 
 template int radix_sort_pairs<uint32_t>(SortWork&, KernelTimer&, uint64_t* k[2], uint32_t* v[2],
-                                        int, uint64_t, int, int, bool, hipStream_t);
+                                        int, uint64_t, int, int, bool, hipStream_t, const uint64_t*);
 template int radix_sort_pairs<uint64_t>(SortWork&, KernelTimer&, uint64_t* k[2], uint64_t* v[2],
-                                        int, uint64_t, int, int, bool, hipStream_t);
+                                        int, uint64_t, int, int, bool, hipStream_t, const uint64_t*);
 template void fill_iota<uint32_t>(uint32_t*, uint64_t, hipStream_t);
 template void fill_iota<uint64_t>(uint64_t*, uint64_t, hipStream_t);
 

@@ -10,7 +10,8 @@ namespace hk {
 struct SortWork {
   DevBuf status;       // lookback granules: tiles x 256 x u64 (epoch | flag | value)
   DevBuf counters;     // dynamic tile-id counters, one per pass (64 x u32)
-  DevBuf hist;         // 8 x 256 u64 digit histograms
+  DevBuf hist;         // 9 x 256 u64 digit histograms (row p = digit p of the current sort)
+  DevBuf hpart;        // 64 x 256 u64 partial histograms of the next digit, written by a pass
   DevBuf offs;         // 8 x 256 u64 exclusive digit offsets
   DevBuf err;          // u32 error flag (lookback spin bound exceeded)
   DevBuf scan_tmp;     // scan partials (multi-level)
@@ -36,10 +37,12 @@ void scan_exclusive_max_u64(SortWork& w, const uint64_t* in, uint64_t* out, uint
 // Stable LSD radix sort of n pairs on key bits [bit_lo, bit_hi).  Ping-pongs between
 // (k[0],v[0]) and (k[1],v[1]); the input is in slot `in_slot`; returns the slot holding the
 // result.  If vals_iota, the values of the input are taken to be 0..n-1 (v[in_slot] unused).
-// Digits whose histogram shows a single bucket are skipped.
+// d_hist0 (nullable): device histogram (256 x u64) of the first digit, if the key producer
+// already computed it.  Each pass computes the next digit's histogram on the fly; digits whose
+// histogram shows a single bucket are skipped.
 template <typename V>
-int radix_sort_pairs(SortWork& w, KernelTimer& tm, uint64_t* k[2], V* v[2], int in_slot,
-                     uint64_t n, int bit_lo, int bit_hi, bool vals_iota, hipStream_t s);
+int radix_sort_pairs(SortWork& w, KernelTimer& tm, uint64_t* k[2], V* v[2], int in_slot, uint64_t n, int bit_lo,
+                     int bit_hi, bool vals_iota, hipStream_t s, const uint64_t* d_hist0 = nullptr);
 
 // diagnostics: per-pass ms of onesweep variants {512x16, 512x16 no-lookback, 512x16 no-lookback
 // no-staging, 256x16, 256x16 no-lookback, 1024x8} and of a plain pair copy; out[7] = error flag
