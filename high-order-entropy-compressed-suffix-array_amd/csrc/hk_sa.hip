@@ -100,7 +100,7 @@ __global__ __launch_bounds__(256) void k_pack_keys(const uint8_t* __restrict__ t
                                                    uint64_t count, const uint16_t* __restrict__ lut, uint64_t R,
                                                    int q, int pb, int ck, uint64_t Rck, uint64_t Rlast,
                                                    uint64_t* __restrict__ keys, unsigned long long* __restrict__ hist0) {
-  __shared__ uint16_t c[PK_TILE + 72];
+  __shared__ uint16_t c[PK_TILE + 72];   // q <= 64 symbols of look-ahead
   __shared__ uint16_t L[256];
   __shared__ uint32_t H[256];
   L[threadIdx.x] = lut[threadIdx.x];
@@ -108,12 +108,21 @@ __global__ __launch_bounds__(256) void k_pack_keys(const uint8_t* __restrict__ t
   __syncthreads();
   const uint64_t end = lo + count;
   for (uint64_t base = lo + (uint64_t)blockIdx.x * PK_TILE; base < end; base += (uint64_t)gridDim.x * PK_TILE) {
-    for (int i = threadIdx.x; i < PK_TILE + q + 1; i += 256) {
-      const uint64_t p = base + i;  // c[i] holds position base + i - 1
-      uint16_t v;
-      if (i == 0) v = L[t[base == 0 ? n - 1 : base - 1]];
-      else v = (p - 1) < n ? L[t[p - 1]] : 0;
-      c[i] = v;
+    // c[i] holds the code of position base + i - 1; positions [base, base + PK_TILE + 64) are read
+    // as aligned 32-bit words where the text allows it (base is a multiple of PK_TILE)
+    if (threadIdx.x == 0) c[0] = L[t[base == 0 ? n - 1 : base - 1]];
+    for (int wI = threadIdx.x; wI < (PK_TILE + 64) / 4; wI += 256) {
+      const uint64_t p = base + 4 * (uint64_t)wI;
+      if (p + 4 <= n) {
+        const uint32_t w4 = *reinterpret_cast<const uint32_t*>(t + p);
+        c[4 * wI + 1] = L[w4 & 255];
+        c[4 * wI + 2] = L[(w4 >> 8) & 255];
+        c[4 * wI + 3] = L[(w4 >> 16) & 255];
+        c[4 * wI + 4] = L[w4 >> 24];
+      } else {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) c[4 * wI + 1 + u] = p + u < n ? L[t[p + u]] : 0;
+      }
     }
     __syncthreads();
 #pragma unroll 4
@@ -150,10 +159,17 @@ __device__ __forceinline__ int lpad(int e) { return e + (e >> 4); }
 
 __device__ __forceinline__ void stage_tile_keys(const uint64_t* __restrict__ keys, uint64_t A, uint64_t tbase,
                                                 uint64_t* L) {
-  for (int i = threadIdx.x; i < GR_TILE + 2; i += GR_T) {
-    const uint64_t j = tbase + i - 1;  // slot i holds key[tbase + i - 1]
-    L[lpad(i)] = (tbase + i >= 1 && j < A) ? keys[j] : 0;
+  // slot i holds key[tbase + i - 1]; 16 coalesced loads per thread are issued back to back
+  uint64_t v[GR_I];
+#pragma unroll
+  for (int k = 0; k < GR_I; ++k) {
+    const uint64_t j = tbase + threadIdx.x + (uint64_t)k * GR_T;
+    v[k] = j < A ? keys[j] : 0;
   }
+  if (threadIdx.x == 0) L[lpad(0)] = tbase > 0 ? keys[tbase - 1] : 0;
+  if (threadIdx.x == 1) L[lpad(GR_TILE + 1)] = tbase + GR_TILE < A ? keys[tbase + GR_TILE] : 0;
+#pragma unroll
+  for (int k = 0; k < GR_I; ++k) L[lpad(threadIdx.x + k * GR_T + 1)] = v[k];
   __syncthreads();
 }
 
@@ -301,9 +317,17 @@ __global__ __launch_bounds__(256) void k_refine_keys(const V* __restrict__ P, co
     const V p = P[a];
     const uint64_t s = (uint64_t)p + h;
     uint64_t chunk = 0;
+    // the qn symbols from s, read as aligned 32-bit words (the text buffer has >= 64 bytes of pad)
+    const uint64_t w0 = s & ~3ull;
+    uint32_t word = s < n ? *reinterpret_cast<const uint32_t*>(t + w0) : 0u;
+    uint64_t wpos = w0;
     for (int j = 0; j < qn; ++j) {
       const uint64_t x = s + j;
-      chunk = chunk * R + (x < n ? L[t[x]] : 0u);
+      if ((x & ~3ull) != wpos) {
+        wpos = x & ~3ull;
+        word = wpos < n ? *reinterpret_cast<const uint32_t*>(t + wpos) : 0u;
+      }
+      chunk = chunk * R + (x < n ? L[(word >> (8 * (x & 3))) & 255u] : 0u);
     }
     keys[a] = gbits ? (((uint64_t)G[a] << (64 - gbits)) | chunk) : chunk;
     vals[a] = p;

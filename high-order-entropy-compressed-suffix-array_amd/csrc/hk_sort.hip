@@ -662,10 +662,10 @@ void debug_radix_bench(SortWork& w, uint64_t* k[2], uint32_t* v[2], uint64_t n, 
   double r[8] = {0};
   r[0] = time_variant<512, 16, 0>(w, k, v, n, reps, bit_lo, pk, s);
   r[1] = time_variant<512, 16, 1>(w, k, v, n, reps, bit_lo, pk, s);
-  r[2] = time_variant<512, 16, 0, 1>(w, k, v, n, reps, bit_lo, pk, s);
-  r[3] = time_variant<512, 16, 0, 2>(w, k, v, n, reps, bit_lo, pk, s);
+  r[2] = time_variant<1024, 16, 0, 4>(w, k, v, n, reps, bit_lo, pk, s);
+  r[3] = time_variant<1024, 12, 0, 4>(w, k, v, n, reps, bit_lo, pk, s);
   r[4] = time_variant<512, 16, 0, 4>(w, k, v, n, reps, bit_lo, pk, s);
-  r[5] = time_variant<512, 16, 0, 8>(w, k, v, n, reps, bit_lo, pk, s);
+  r[5] = time_variant<1024, 16, 1, 4>(w, k, v, n, reps, bit_lo, pk, s);
   {
     hipEvent_t a, b;
     HK_HIP(hipEventCreate(&a));
