@@ -219,9 +219,10 @@ def run_single(args) -> dict:
 def run_sharded(args, rank: int, world: int, local_rank: int) -> dict | None:
     import torch
     import torch.distributed as dist
+    torch.cuda.set_device(local_rank)
     per = args.text_bytes
     n = per * world + 1
-    dev = DeviceIndex.synthetic(n, DNA, seed=args.seed, device=local_rank)
+    dev = DeviceIndex.synthetic(n, DNA, seed=args.seed, device=local_rank, flags=1 if args.pos64 else 0)
     uid = [comm_unique_id() if rank == 0 else None]
     dist.broadcast_object_list(uid, src=0)
     uid = uid[0]
@@ -264,7 +265,8 @@ def run_sharded(args, rank: int, world: int, local_rank: int) -> dict | None:
             "config": {"workload": f"{world} GiB synthetic sigma=4 text sharded over {world} GPUs: key-histogram "
                                    "RCCL all-reduce, per-rank slice sort + refinement, RCCL all-gather of slice "
                                    "bounds", "text_symbols": n, "sigma": 4,
-                       "parallelism": f"sa-slices x{world}", "positions": "u64" if n >= 2**32 - 1 else "u32"},
+                       "parallelism": f"sa-slices x{world}",
+                       "positions": "u64" if (n >= 2**32 - 1 or args.pos64) else "u32"},
             "roofline": roof,
             "locate_patterns_per_s": None,
             "detail": {"rank0_slice": [lo, hi]},
@@ -286,6 +288,8 @@ def main():
     ap.add_argument("--cpu-sample", type=int, default=1 << 16)
     ap.add_argument("--cpu-patterns", type=int, default=1000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--sharded", action="store_true", help="use the sharded (multi-GPU) build even at N=1")
+    ap.add_argument("--pos64", action="store_true", help="sharded build with 64-bit positions at any n")
     ap.add_argument("--traffic-gb", type=float, default=None,
                     help="PMC-measured HBM GB per radix pass; default: profiles/pmc_radix_onesweep.json")
     args = ap.parse_args()
@@ -293,9 +297,12 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1 or args.gpus > 1:
+    if world > 1 or args.gpus > 1 or args.sharded:
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29533")
+        os.environ.setdefault("RANK", "0")
+        os.environ.setdefault("WORLD_SIZE", "1")
         dist.init_process_group(backend="gloo")
         world = dist.get_world_size()
         rank = dist.get_rank()

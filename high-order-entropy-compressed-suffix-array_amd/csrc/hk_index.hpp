@@ -8,6 +8,7 @@
 namespace hk {
 
 constexpr int kMaxLevels = 8;
+constexpr uint32_t kFlagPos64 = 1u;   // hkcsa_opts.flags: 64-bit positions in sharded builds at any n
 constexpr int kLineBits = 448;   // 7 data words per 64-B rank line (word 0 = ones before the line)
 
 struct WtTables {                // per level, per dense code (host mirror of the device tables)
@@ -43,6 +44,7 @@ struct WtView {
 
 struct Index {
   int device = 0;
+  uint32_t flags = 0;          // hkcsa_opts.flags
   hipStream_t stream = nullptr;
   uint64_t n = 0;
   DevBuf text;                 // T' (n bytes + 64 pad)
@@ -109,6 +111,7 @@ int shard_buckets();
 void shard_histogram(Index& ix, int nranks, int rank, uint64_t* d_hist);
 void shard_build(Index& ix, const uint64_t* h_global_hist, int nranks, int rank);
 void shard_get_sa(Index& ix, uint64_t a, uint64_t b, uint64_t* out);
+void shard_get_bwt(Index& ix, uint64_t a, uint64_t b, uint8_t* out);
 void build_sa_sharded(Index& ix, const uint8_t id[128], int nranks, int rank);
 void comm_unique_id(uint8_t id[128]);
 

@@ -217,11 +217,19 @@ void shard_histogram(Index& ix, int nranks, int rank, uint64_t* d_hist) {
 }
 
 void shard_build(Index& ix, const uint64_t* h_global_hist, int nranks, int rank) {
-  if (ix.n > 0xFFFFFFFEull) shard_build_t<uint64_t>(ix, h_global_hist, nranks, rank);
+  if (ix.n > 0xFFFFFFFEull || (ix.flags & kFlagPos64)) shard_build_t<uint64_t>(ix, h_global_hist, nranks, rank);
   else shard_build_t<uint32_t>(ix, h_global_hist, nranks, rank);
 }
 
 int shard_buckets() { return SH_BUCKETS; }
+
+void shard_get_bwt(Index& ix, uint64_t a, uint64_t b, uint8_t* out) {
+  const uint64_t m = ix.shard_hi - ix.shard_lo;
+  if (!(a <= b && b <= m)) throw ApiError{-4, "shard BWT range out of bounds"};
+  if (a == b) return;
+  HK_HIP(hipMemcpyAsync(out, ix.bwt.as<uint8_t>() + a, b - a, hipMemcpyDeviceToHost, ix.stream));
+  HK_HIP(hipStreamSynchronize(ix.stream));
+}
 
 void shard_get_sa(Index& ix, uint64_t a, uint64_t b, uint64_t* out) {
   const uint64_t m = ix.shard_hi - ix.shard_lo;

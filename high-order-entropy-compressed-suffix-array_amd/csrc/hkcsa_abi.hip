@@ -65,6 +65,7 @@ void init_index(hk::Index& ix, const hkcsa_opts* o, uint64_t n) {
   need(dev < cnt, HKCSA_E_INVALID, "device ordinal out of range");
   HK_HIP(hipSetDevice(dev));
   ix.device = dev;
+  ix.flags = o ? o->flags : 0u;
   HK_HIP(hipStreamCreateWithFlags(&ix.stream, hipStreamNonBlocking));
   ix.timer.stream = ix.stream;
   ix.n = n;
@@ -469,6 +470,15 @@ int hkcsa_get_shard_sa(hkcsa_index* h, uint64_t a, uint64_t b, uint64_t* out) {
     need(h->ix.sharded && h->ix.have_sa, HKCSA_E_STATE, "no sharded suffix array");
     need(a == b || out != nullptr, HKCSA_E_INVALID, "null output");
     hk::shard_get_sa(h->ix, a, b, out);
+  });
+}
+
+int hkcsa_get_shard_bwt(hkcsa_index* h, uint64_t a, uint64_t b, uint8_t* out) {
+  return guarded([&] {
+    activate(h);
+    need(h->ix.sharded && h->ix.have_bwt, HKCSA_E_STATE, "no sharded BWT");
+    need(a == b || out != nullptr, HKCSA_E_INVALID, "null output");
+    hk::shard_get_bwt(h->ix, a, b, out);
   });
 }
 

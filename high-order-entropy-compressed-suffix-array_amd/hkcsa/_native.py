@@ -68,6 +68,7 @@ _SIGS = [
     ("hkcsa_build_sa_sharded", C.c_int, [vp, vp, C.c_int, C.c_int]),
     ("hkcsa_shard_range", C.c_int, [vp, u64p, u64p]),
     ("hkcsa_get_shard_sa", C.c_int, [vp, C.c_uint64, C.c_uint64, vp]),
+    ("hkcsa_get_shard_bwt", C.c_int, [vp, C.c_uint64, C.c_uint64, vp]),
     ("hkcsa_shard_buckets", C.c_int, []),
     ("hkcsa_shard_histogram", C.c_int, [vp, C.c_int, C.c_int, vp]),
     ("hkcsa_shard_build", C.c_int, [vp, vp, C.c_int, C.c_int]),

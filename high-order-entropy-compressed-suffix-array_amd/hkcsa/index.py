@@ -75,6 +75,9 @@ class QuerySet:
             pass
 
 
+FLAG_POS64 = 1   # HKCSA_FLAG_POS64: 64-bit positions in sharded builds at any n
+
+
 class DeviceIndex:
     """One text T' resident in HBM plus its SA / BWT / wavelet tree."""
 
@@ -85,23 +88,23 @@ class DeviceIndex:
 
     # ------------------------------------------------------------ creation
     @classmethod
-    def from_bytes(cls, data, device: int = -1) -> "DeviceIndex":
+    def from_bytes(cls, data, device: int = -1, flags: int = 0) -> "DeviceIndex":
         lib = N.load()
         arr = np.frombuffer(bytes(data), dtype=np.uint8) if isinstance(data, (bytes, bytearray)) else \
             np.ascontiguousarray(data, dtype=np.uint8)
         if len(arr) == 0:
             raise ValueError("DeviceIndex needs a non-empty text (append the sentinel first)")
-        o = N.Opts(device=device)
+        o = N.Opts(device=device, flags=flags)
         h = C.c_void_p()
         N.check(lib.hkcsa_create(_ptr(arr), len(arr), C.byref(o), C.byref(h)))
         return cls(h, len(arr))
 
     @classmethod
     def synthetic(cls, n: int, alphabet: bytes, seed: int, terminator: int = ord("$"),
-                  device: int = -1) -> "DeviceIndex":
+                  device: int = -1, flags: int = 0) -> "DeviceIndex":
         lib = N.load()
         a = np.frombuffer(bytes(alphabet), dtype=np.uint8)
-        o = N.Opts(device=device)
+        o = N.Opts(device=device, flags=flags)
         h = C.c_void_p()
         N.check(lib.hkcsa_create_synthetic(n, _ptr(a), len(a), seed, terminator, C.byref(o), C.byref(h)))
         return cls(h, n)
@@ -243,6 +246,12 @@ class DeviceIndex:
         lo, hi = self.shard_range()
         out = np.empty(max(1, hi - lo), dtype=np.uint64)
         N.check(self.lib.hkcsa_get_shard_sa(self.h, 0, hi - lo, _ptr(out)))
+        return out[:hi - lo]
+
+    def shard_bwt(self) -> np.ndarray:
+        lo, hi = self.shard_range()
+        out = np.empty(max(1, hi - lo), dtype=np.uint8)
+        N.check(self.lib.hkcsa_get_shard_bwt(self.h, 0, hi - lo, _ptr(out)))
         return out[:hi - lo]
 
     # ------------------------------------------------------------ timing

@@ -44,9 +44,11 @@ extern "C" {
 typedef struct hkcsa_index hkcsa_index;
 typedef struct hkcsa_queries hkcsa_queries;
 
+#define HKCSA_FLAG_POS64 1u  /* sharded builds keep 64-bit positions at any n */
+
 typedef struct hkcsa_opts {
   int32_t device;   /* HIP device ordinal (-1 = current)                 */
-  uint32_t flags;   /* reserved, 0                                       */
+  uint32_t flags;   /* HKCSA_FLAG_* bits, 0 by default                   */
   uint64_t reserved[2];
 } hkcsa_opts;
 
@@ -146,6 +148,9 @@ int hkcsa_build_sa_sharded(hkcsa_index* ix, const uint8_t id[128], int nranks, i
 int hkcsa_shard_range(hkcsa_index* ix, uint64_t* lo, uint64_t* hi);
 /* Sharded SA slice entries SA[lo+a : lo+b) (a,b relative to the slice). */
 int hkcsa_get_shard_sa(hkcsa_index* ix, uint64_t a, uint64_t b, uint64_t* out);
+/* BWT of the slice: out[j] = T'[SA[lo+a+j]-1] (wrapping), j < b-a — the rows
+ * bwt_transform (csa/bwt.py:4-9) emits for this rank's SA range. */
+int hkcsa_get_shard_bwt(hkcsa_index* ix, uint64_t a, uint64_t b, uint8_t* out);
 /* The same construction in two host-visible phases, for hosts that do their own
  * collectives (and for single-GPU tests of the partitioning):
  *   hkcsa_shard_histogram: this rank's key-prefix histogram (hkcsa_shard_buckets()

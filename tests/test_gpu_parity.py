@@ -164,11 +164,13 @@ def test_full_size_config1_256MiB(hk):
     dev.close()
 
 
-@pytest.mark.parametrize("nranks", [2, 3])
-def test_shard_two_phase_emulated(hk, nranks):
-    text = oracle.synth_text(400001, b"ACGT", seed=12)
+@pytest.mark.parametrize("nranks,flags", [(2, 0), (3, 0), (2, 1), (4, 1)])
+def test_shard_two_phase_emulated(hk, nranks, flags):
+    """Ranks emulated on one GPU; flags=1 forces the 64-bit position kernels (n >= 2^32 path)."""
+    text = oracle.synth_text(400001, b"ACGT", seed=12 + nranks)
     ref = oracle.suffix_array(text)
-    devs = [hk.DeviceIndex.from_bytes(text, device=0) for _ in range(nranks)]
+    ref_bwt = oracle.bwt(text, ref)
+    devs = [hk.DeviceIndex.from_bytes(text, device=0, flags=flags) for _ in range(nranks)]
     g = sum(d.shard_histogram(nranks, r) for r, d in enumerate(devs))
     assert int(g.sum()) == len(text)
     assert np.array_equal(g, oracle.shard_hist(text, 0, len(text)))
@@ -179,16 +181,21 @@ def test_shard_two_phase_emulated(hk, nranks):
         d.shard_build(g, nranks, r)
         assert d.shard_range() == bounds[r]
         parts.append(d.shard_sa())
+        lo, hi = bounds[r]
+        assert np.array_equal(d.shard_bwt(), ref_bwt[lo:hi]), r
         d.close()
     assert np.array_equal(np.concatenate(parts), ref)
 
 
-def test_shard_rccl_single_rank(hk):
+@pytest.mark.parametrize("flags", [0, 1])
+def test_shard_rccl_single_rank(hk, flags):
     text = oracle.synth_text(200001, bytes(range(0x20, 0x7F)), seed=13)
-    dev = hk.DeviceIndex.from_bytes(text, device=0)
+    dev = hk.DeviceIndex.from_bytes(text, device=0, flags=flags)
     dev.build_sa_sharded(hk.comm_unique_id(), 1, 0)
     assert dev.shard_range() == (0, len(text))
-    assert np.array_equal(dev.shard_sa(), oracle.suffix_array(text))
+    sa = oracle.suffix_array(text)
+    assert np.array_equal(dev.shard_sa(), sa)
+    assert np.array_equal(dev.shard_bwt(), oracle.bwt(text, sa))
     dev.close()
 
 
