@@ -7,7 +7,8 @@ exposes the reference's view of it:
     .rank_structures[l] for the reference's left-spine levels (:72-100).  Level l
     of the reference is the prefix of device level l of length |leftmost node|
     (SURVEY.md §8 "WT levels"), so it is read straight from HBM.
-  * .m, .compress() (:151-156) — Golomb-Rice parameters/codes of those levels.
+  * .m, .compress() (:151-156) — Golomb-Rice parameters/codes of those levels,
+    coded on the GPU (hkcsa_wt_golomb); GolombRiceEncoder stays as the host class.
   * .rank(c, i) / .select(c, k) keep the reference's behaviour of ignoring `c`
     and answering on the last level (:133-149).
   * .alphabet ends as the reference leaves it (the last left alphabet, :99).
@@ -101,11 +102,12 @@ class WaveletTree:
         while width > 1:
             half = width // 2
             left, right = alpha[:half], alpha[half:width]
-            bits = self._dev.wt_level_bits(level)[:ccode[width]]
-            enc_g = GolombRiceEncoder(bits)
-            gbits = enc_g.encode(bits)
+            nbits = ccode[width]
+            bits = self._dev.wt_level_bits(level)[:nbits]
+            m, _, code = self._dev.wt_golomb(level, nbits)      # GPU Golomb-Rice pass (:84-86)
+            gbits = code.tolist()
             if self.m is None:
-                self.m = enc_g.m
+                self.m = m
             nxt = cur[bits == 0]
             next_text = list(self._codec.decode(nxt.tobytes()))
             self.tree.append((gbits, left, right, next_text))

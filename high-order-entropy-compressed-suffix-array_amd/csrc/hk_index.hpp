@@ -77,6 +77,7 @@ struct Index {
   DevBuf tile_a, tile_b, tile_c, tile_d;
   DevBuf small;                // scratch for totals etc.
   DevBuf seq[2];               // WT level code sequences
+  DevBuf gr_tmp[2], gr_out;    // Golomb-Rice coding of a level (per-word carries/offsets, code words)
 
   // sharded construction
   bool sharded = false;
@@ -105,6 +106,15 @@ void query_locate_gather(Index& ix, const int64_t* d_lr, const uint64_t* d_occ_o
                          uint64_t* d_pos);
 void query_rank(Index& ix, const uint8_t* d_c, const uint64_t* d_i, uint64_t k, uint64_t* d_out);
 void wt_level_words(Index& ix, int depth, uint64_t* d_words);
+
+// Golomb-Rice code of the first nbits bits of a level (csa/wavelet_tree.py:27-63); with write,
+// the code words are left in ix.gr_out
+struct GolombResult {
+  uint32_t m = 1;
+  uint64_t ones = 0, bits = 0;
+};
+uint32_t golomb_m(uint64_t ones, uint64_t total);
+GolombResult wt_golomb(Index& ix, int depth, uint64_t nbits, uint32_t m_override, bool write);
 
 // sharded SA (RCCL)
 int shard_buckets();

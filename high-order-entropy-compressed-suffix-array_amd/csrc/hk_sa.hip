@@ -23,6 +23,7 @@
 #include <cmath>
 
 #include "hk_index.hpp"
+#include "hk_keys.hpp"
 
 namespace hk {
 namespace {
@@ -108,40 +109,14 @@ __global__ __launch_bounds__(256) void k_pack_keys(const uint8_t* __restrict__ t
   __syncthreads();
   const uint64_t end = lo + count;
   for (uint64_t base = lo + (uint64_t)blockIdx.x * PK_TILE; base < end; base += (uint64_t)gridDim.x * PK_TILE) {
-    // c[i] holds the code of position base + i - 1; positions [base, base + PK_TILE + 64) are read
-    // as aligned 32-bit words where the text allows it (base is a multiple of PK_TILE)
-    if (threadIdx.x == 0) c[0] = L[t[base == 0 ? n - 1 : base - 1]];
-    for (int wI = threadIdx.x; wI < (PK_TILE + 64) / 4; wI += 256) {
-      const uint64_t p = base + 4 * (uint64_t)wI;
-      if (p + 4 <= n) {
-        const uint32_t w4 = *reinterpret_cast<const uint32_t*>(t + p);
-        c[4 * wI + 1] = L[w4 & 255];
-        c[4 * wI + 2] = L[(w4 >> 8) & 255];
-        c[4 * wI + 3] = L[(w4 >> 16) & 255];
-        c[4 * wI + 4] = L[w4 >> 24];
-      } else {
-#pragma unroll
-        for (int u = 0; u < 4; ++u) c[4 * wI + 1 + u] = p + u < n ? L[t[p + u]] : 0;
-      }
-    }
+    stage_text_codes<PK_TILE, 256>(c, L, t, n, base);
     __syncthreads();
 #pragma unroll 4
     for (int k = 0; k < PK_TILE / 256; ++k) {
       const int off = k * 256 + threadIdx.x;
       const uint64_t p = base + off;
       if (p < end) {
-        // radix-R Horner in 24-bit chunks (R^ck < 2^24: one v_mul_u32_u24 + add per symbol),
-        // chunks combined in 64-bit
-        uint64_t key = 0;
-        int j = 1;
-        while (j <= q) {
-          const int len = q - j + 1 < ck ? q - j + 1 : ck;
-          uint32_t cv = 0;
-          for (int u = 0; u < len; ++u) cv = __umul24(cv, (uint32_t)R) + c[off + j + u];
-          key = key * (len == ck ? Rck : Rlast) + cv;
-          j += len;
-        }
-        key = (key << pb) | (pb ? c[off] : 0u);
+        const uint64_t key = key_chunked(c, off, R, q, pb, ck, Rck, Rlast);
         keys[p - lo] = key;
         if (hist0) atomicAdd(&H[(uint32_t)(key >> pb) & 255u], 1u);
       }
@@ -739,15 +714,8 @@ void pack_keys(const uint8_t* d_text, uint64_t n, uint64_t lo, uint64_t count, c
   if (d_hist0) HK_HIP(hipMemsetAsync(d_hist0, 0, 256 * 8, s));
   if (!count) return;
   const uint64_t g = std::min<uint64_t>(ceil_div(count, PK_TILE), 4096);
-  int ck = 1;  // symbols per 24-bit chunk
-  uint64_t Rck = R;
-  while (Rck * R < (1ull << 24)) {
-    Rck *= R;
-    ++ck;
-  }
-  uint64_t Rlast = 1;
-  for (int i = 0; i < (q % ck ? q % ck : ck); ++i) Rlast *= R;
-  k_pack_keys<<<(unsigned)g, 256, 0, s>>>(d_text, n, lo, count, d_lut, R, q, pb, ck, Rck, Rlast, d_keys,
+  const KeyChunks kc = key_chunks(R, q);
+  k_pack_keys<<<(unsigned)g, 256, 0, s>>>(d_text, n, lo, count, d_lut, R, q, pb, kc.ck, kc.Rck, kc.Rlast, d_keys,
                                           reinterpret_cast<unsigned long long*>(d_hist0));
   HK_HIP(hipGetLastError());
 }

@@ -19,6 +19,7 @@
 #include <cstring>
 
 #include "hk_index.hpp"
+#include "hk_keys.hpp"
 
 namespace hk {
 namespace {
@@ -33,36 +34,31 @@ struct ShardComm {  // one RCCL communicator per process (one process per GPU)
   uint8_t id[128];
 };
 
-// key of suffix p from LDS-staged codes: c[off] = code(T[p-1]), c[off+1..off+q] = code(T[p..])
-__device__ __forceinline__ uint64_t key_at(const uint16_t* c, int off, uint64_t R, int q, int pb) {
-  uint64_t key = 0;
-  for (int j = 1; j <= q; ++j) key = key * R + c[off + j];
-  return (key << pb) | (pb ? c[off] : 0u);
-}
-
-__device__ __forceinline__ void stage_codes(uint16_t* c, const uint16_t* L, const uint8_t* __restrict__ t,
-                                            uint64_t n, uint64_t base, int q) {
-  for (int i = threadIdx.x; i < PS_TILE + q + 1; i += 256) {
-    const uint64_t p = base + i;  // c[i] holds position base + i - 1
-    c[i] = i == 0 ? L[t[base == 0 ? n - 1 : base - 1]] : ((p - 1) < n ? L[t[p - 1]] : 0);
-  }
-}
+// bucket of a key: its top SH_BUCKET_BITS bits (key >> bsh)
+struct BucketGeom {
+  uint64_t R, Rck, Rlast, Rrest;
+  int q, pb, ck, bsh;
+};
 
 __global__ __launch_bounds__(256) void k_shard_hist(const uint8_t* __restrict__ t, uint64_t n, uint64_t lo,
-                                                    uint64_t hi, const uint16_t* __restrict__ lut, uint64_t R, int q,
-                                                    int pb, int bsh, unsigned long long* __restrict__ hist) {
+                                                    uint64_t hi, const uint16_t* __restrict__ lut, BucketGeom g,
+                                                    unsigned long long* __restrict__ hist) {
   __shared__ uint32_t H[SH_BUCKETS];
   __shared__ uint16_t c[PS_TILE + 72];
   __shared__ uint16_t L[256];
   L[threadIdx.x] = lut[threadIdx.x];
   for (int i = threadIdx.x; i < SH_BUCKETS; i += 256) H[i] = 0;
   __syncthreads();
-  for (uint64_t base = lo + (uint64_t)blockIdx.x * PS_TILE; base < hi; base += (uint64_t)gridDim.x * PS_TILE) {
-    stage_codes(c, L, t, n, base, q);
+  // tiles are aligned to PS_TILE in absolute positions so the staged text loads stay aligned
+  const uint64_t first = lo / PS_TILE * PS_TILE;
+  for (uint64_t base = first + (uint64_t)blockIdx.x * PS_TILE; base < hi; base += (uint64_t)gridDim.x * PS_TILE) {
+    stage_text_codes<PS_TILE, 256>(c, L, t, n, base);
     __syncthreads();
     for (int k = 0; k < PS_TILE / 256; ++k) {
       const int off = k * 256 + threadIdx.x;
-      if (base + off < hi) atomicAdd(&H[key_at(c, off, R, q, pb) >> bsh], 1u);
+      const uint64_t p = base + off;
+      if (p >= lo && p < hi)
+        atomicAdd(&H[key_chunked(c, off, g.R, g.q, g.pb, g.ck, g.Rck, g.Rlast) >> g.bsh], 1u);
     }
     __syncthreads();
   }
@@ -70,10 +66,13 @@ __global__ __launch_bounds__(256) void k_shard_hist(const uint8_t* __restrict__ 
     if (H[i]) atomicAdd(&hist[i], (unsigned long long)H[i]);
 }
 
+// Every rank scans all of T' and keeps the suffixes whose bucket lies in [blo, bhi).  The first
+// 24-bit chunk of the key bounds the bucket to [bucket(lower), bucket(upper)]; when that interval
+// misses the rank's range (the common case: (N-1)/N of all positions) the full key is never built.
 template <typename V>
 __global__ __launch_bounds__(256) void k_pack_select(const uint8_t* __restrict__ t, uint64_t n,
-                                                     const uint16_t* __restrict__ lut, uint64_t R, int q, int pb, int bsh,
-                                                     uint32_t blo, uint32_t bhi, uint64_t* __restrict__ keys,
+                                                     const uint16_t* __restrict__ lut, BucketGeom g, uint32_t blo,
+                                                     uint32_t bhi, uint64_t* __restrict__ keys,
                                                      V* __restrict__ vals, unsigned long long* counter) {
   __shared__ uint16_t c[PS_TILE + 72];
   __shared__ uint16_t L[256];
@@ -82,17 +81,34 @@ __global__ __launch_bounds__(256) void k_pack_select(const uint8_t* __restrict__
   L[threadIdx.x] = lut[threadIdx.x];
   __syncthreads();
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const bool pretest = g.q > g.ck;
+  const uint64_t pbmask = (1ull << g.pb) - 1;
   for (uint64_t base = (uint64_t)blockIdx.x * PS_TILE; base < n; base += (uint64_t)gridDim.x * PS_TILE) {
-    stage_codes(c, L, t, n, base, q);
+    stage_text_codes<PS_TILE, 256>(c, L, t, n, base);
     __syncthreads();
     uint64_t kk[PS_TILE / 256];
     uint32_t sel = 0;
 #pragma unroll
     for (int k = 0; k < PS_TILE / 256; ++k) {
       const int off = k * 256 + threadIdx.x;
-      kk[k] = key_at(c, off, R, q, pb);
-      const uint32_t bk = (uint32_t)(kk[k] >> bsh);
-      if (base + off < n && bk >= blo && bk < bhi) sel |= 1u << k;
+      kk[k] = 0;
+      if (base + off < n) {
+        if (pretest) {
+          const uint32_t cv0 = chunk_value(c, off + 1, g.ck, (uint32_t)g.R);
+          const uint64_t lower = (uint64_t)cv0 * g.Rrest;
+          const uint32_t b_lo = (uint32_t)((lower << g.pb) >> g.bsh);
+          const uint32_t b_hi = (uint32_t)((((lower + g.Rrest - 1) << g.pb) | pbmask) >> g.bsh);
+          if (b_hi >= blo && b_lo < bhi) {
+            kk[k] = key_from(c, off, g.R, g.q, g.pb, g.ck, g.Rck, g.Rlast, g.ck + 1, cv0);
+            const uint32_t bk = (uint32_t)(kk[k] >> g.bsh);
+            if (bk >= blo && bk < bhi) sel |= 1u << k;
+          }
+        } else {
+          kk[k] = key_chunked(c, off, g.R, g.q, g.pb, g.ck, g.Rck, g.Rlast);
+          const uint32_t bk = (uint32_t)(kk[k] >> g.bsh);
+          if (bk >= blo && bk < bhi) sel |= 1u << k;
+        }
+      }
     }
     const uint32_t cnt = __popc(sel);
     const uint32_t inc = wave_incl_sum<uint32_t>(cnt);
@@ -131,12 +147,16 @@ int bucket_shift(const KeyGeom& kg) {
   return sh < 0 ? 0 : sh;
 }
 
+BucketGeom bucket_geom(const KeyGeom& kg) {
+  const KeyChunks kc = key_chunks(kg.R, kg.q);
+  return BucketGeom{kg.R, kc.Rck, kc.Rlast, kc.Rrest, kg.q, kg.pb, kc.ck, bucket_shift(kg)};
+}
+
 template <typename V>
 void shard_build_t(Index& ix, const uint64_t* ghist, int nranks, int rank) {
   const uint64_t n = ix.n;
   hipStream_t s = ix.stream;
   KeyGeom kg = key_geometry(ix, true);
-  const int bsh = bucket_shift(kg);
   // splitters: rank r owns buckets [B[r], B[r+1]) — the first bucket whose prefix count reaches r*n/N
   std::vector<uint64_t> cum(SH_BUCKETS + 1, 0);
   for (int i = 0; i < SH_BUCKETS; ++i) cum[i + 1] = cum[i] + ghist[i];
@@ -177,8 +197,8 @@ void shard_build_t(Index& ix, const uint64_t* ghist, int nranks, int rank) {
   {
     TimedLaunch t(ix.timer, "shard_pack_select", (double)n + (double)m * (8 + sizeof(V)));
     k_pack_select<V><<<grid_for(n, PS_TILE, 8192), 256, 0, s>>>(
-        ix.text.as<uint8_t>(), n, reinterpret_cast<const uint16_t*>(ix.small.as<uint8_t>() + 2048), kg.R, kg.q,
-        kg.pb, bsh, blo, bhi, ix.keys[0].as<uint64_t>(), ix.vals[0].as<V>(), d_counter);
+        ix.text.as<uint8_t>(), n, reinterpret_cast<const uint16_t*>(ix.small.as<uint8_t>() + 2048),
+        bucket_geom(kg), blo, bhi, ix.keys[0].as<uint64_t>(), ix.vals[0].as<V>(), d_counter);
     HK_HIP(hipGetLastError());
   }
   uint64_t got = 0;
@@ -210,8 +230,8 @@ void shard_histogram(Index& ix, int nranks, int rank, uint64_t* d_hist) {
   if (hi > lo) {
     TimedLaunch t(ix.timer, "shard_hist", (double)(hi - lo));
     k_shard_hist<<<grid_for(hi - lo, PS_TILE, 2048), 256, 0, s>>>(
-        ix.text.as<uint8_t>(), ix.n, lo, hi, reinterpret_cast<const uint16_t*>(ix.small.as<uint8_t>() + 2048), kg.R,
-        kg.q, kg.pb, bucket_shift(kg), reinterpret_cast<unsigned long long*>(d_hist));
+        ix.text.as<uint8_t>(), ix.n, lo, hi, reinterpret_cast<const uint16_t*>(ix.small.as<uint8_t>() + 2048),
+        bucket_geom(kg), reinterpret_cast<unsigned long long*>(d_hist));
     HK_HIP(hipGetLastError());
   }
 }

@@ -301,7 +301,7 @@ __device__ __forceinline__ uint64_t lookback(const uint64_t* status, uint32_t ti
 // order -> value loads issued -> lookback (its latency overlaps the value loads) -> keys out ->
 // values into LDS -> values out.
 template <typename V, int T, int I, int MODE, int LBW = 4>
-__global__ __launch_bounds__(T, 4) void k_onesweep(
+__global__ __launch_bounds__(T, T >= 512 ? 4 : 3) void k_onesweep(
     const uint64_t* __restrict__ kin, const V* __restrict__ vin, uint64_t* __restrict__ kout,
     V* __restrict__ vout, uint64_t n, uint32_t shift, const uint64_t* __restrict__ goff,
     uint64_t* status, uint32_t* tile_counter, uint32_t epoch, uint32_t* err, int iota, int next_shift,

@@ -302,6 +302,28 @@ int hkcsa_wt_level(hkcsa_index* h, int depth, uint64_t* nbits, uint64_t* words_o
   });
 }
 
+int hkcsa_wt_golomb(hkcsa_index* h, int depth, uint64_t nbits, uint32_t m_override, uint32_t* m_out,
+                    uint64_t* ones_out, uint64_t* code_bits, uint64_t* words_out, uint64_t cap_words) {
+  return guarded([&] {
+    activate(h);
+    need(h->ix.have_wt, HKCSA_E_STATE, "wavelet tree not built");
+    need(depth >= 0 && depth < h->ix.wt_levels, HKCSA_E_RANGE, "level out of range");
+    need(nbits <= h->ix.n, HKCSA_E_RANGE, "prefix longer than the level");
+    need(m_override < 64, HKCSA_E_INVALID, "m must be below 64");
+    const hk::GolombResult r = hk::wt_golomb(h->ix, depth, nbits, m_override, words_out != nullptr);
+    if (m_out) *m_out = r.m;
+    if (ones_out) *ones_out = r.ones;
+    if (code_bits) *code_bits = r.bits;
+    if (!words_out) return;
+    const uint64_t nw = hk::ceil_div(r.bits, 64);
+    need(cap_words >= nw, HKCSA_E_RANGE, "output buffer too small for the code");
+    if (nw) {
+      HK_HIP(hipMemcpyAsync(words_out, h->ix.gr_out.p, nw * 8, hipMemcpyDeviceToHost, h->ix.stream));
+      HK_HIP(hipStreamSynchronize(h->ix.stream));
+    }
+  });
+}
+
 int hkcsa_rank(hkcsa_index* h, const uint8_t* c, const uint64_t* i, uint64_t count, uint64_t* out) {
   return guarded([&] {
     activate(h);

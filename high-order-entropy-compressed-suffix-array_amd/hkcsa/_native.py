@@ -67,6 +67,8 @@ _SIGS = [
     ("hkcsa_comm_unique_id", C.c_int, [vp]),
     ("hkcsa_build_sa_sharded", C.c_int, [vp, vp, C.c_int, C.c_int]),
     ("hkcsa_shard_range", C.c_int, [vp, u64p, u64p]),
+    ("hkcsa_wt_golomb", C.c_int, [vp, C.c_int, C.c_uint64, C.c_uint32, C.POINTER(C.c_uint32), u64p, u64p, vp,
+                                  C.c_uint64]),
     ("hkcsa_get_shard_sa", C.c_int, [vp, C.c_uint64, C.c_uint64, vp]),
     ("hkcsa_get_shard_bwt", C.c_int, [vp, C.c_uint64, C.c_uint64, vp]),
     ("hkcsa_shard_buckets", C.c_int, []),

@@ -193,6 +193,22 @@ class DeviceIndex:
         bits = np.unpackbits(words.view(np.uint8), bitorder="little")
         return bits[:nb.value]
 
+    def wt_golomb(self, depth: int, nbits: int | None = None, m: int = 0, sizes_only: bool = False):
+        """Golomb-Rice code of level `depth`'s first nbits bits: (m, ones, code bits as u8 0/1 array)
+        — or (m, ones, code length) with sizes_only."""
+        nbits = self.n if nbits is None else nbits
+        mo, ones, nb = C.c_uint32(0), C.c_uint64(0), C.c_uint64(0)
+        if sizes_only:
+            N.check(self.lib.hkcsa_wt_golomb(self.h, depth, nbits, m, C.byref(mo), C.byref(ones), C.byref(nb),
+                                             None, 0))
+            return mo.value, ones.value, nb.value
+        N.check(self.lib.hkcsa_wt_golomb(self.h, depth, nbits, m, C.byref(mo), C.byref(ones), C.byref(nb), None, 0))
+        words = np.zeros(max(1, (nb.value + 63) // 64), dtype=np.uint64)
+        N.check(self.lib.hkcsa_wt_golomb(self.h, depth, nbits, m, C.byref(mo), C.byref(ones), C.byref(nb),
+                                         _ptr(words), len(words)))
+        bits = np.unpackbits(words.view(np.uint8), bitorder="little")[:nb.value]
+        return mo.value, ones.value, bits
+
     def rank(self, cs, idx) -> np.ndarray:
         cs = np.ascontiguousarray(cs, dtype=np.uint8)
         idx = np.ascontiguousarray(idx, dtype=np.uint64)

@@ -111,6 +111,15 @@ int hkcsa_wt_levels(hkcsa_index* ix, int* levels);
  * (words_out may be NULL to query nbits).  The reference's left-spine level
  * l (csa/wavelet_tree.py:82) is the prefix of depth-l of length |leftmost node|. */
 int hkcsa_wt_level(hkcsa_index* ix, int depth, uint64_t* nbits, uint64_t* words_out);
+/* Golomb-Rice code of the runs of ones in the first `nbits` bits of level
+ * `depth` — GolombRiceEncoder(bitmap).encode(bitmap) of csa/wavelet_tree.py:27-63
+ * as build_tree applies it (:84-86).  m = the reference's rule from the ones
+ * density (float log2, truncated, at least 1) unless m_override > 0 (< 64).
+ * Outputs: *m_out, *ones_out (popcount of the prefix), *code_bits (length of
+ * the code); words_out (nullable: sizes only) receives ceil(code_bits/64)
+ * words, code bit j at bit j%64 of word j/64; cap_words is its capacity. */
+int hkcsa_wt_golomb(hkcsa_index* ix, int depth, uint64_t nbits, uint32_t m_override, uint32_t* m_out,
+                    uint64_t* ones_out, uint64_t* code_bits, uint64_t* words_out, uint64_t cap_words);
 /* occ(c_k, i_k) = #c_k in BWT[0:min(i_k, n)) for k < count, 0 for absent bytes.
  * EnhancedFMIndex.rank (csa/enhanced_fm_index.py:34-40). */
 int hkcsa_rank(hkcsa_index* ix, const uint8_t* c, const uint64_t* i, uint64_t count, uint64_t* out);

@@ -296,3 +296,28 @@ void oracle_shard_hist(const uint8_t* t, uint64_t n, uint64_t lo, uint64_t hi, u
     hist[key >> bsh]++;
   }
 }
+
+/* Golomb-Rice code of the runs of ones of bits[0:n) with parameter m
+ * (csa/wavelet_tree.py:40-63): per maximal run of L ones, L/m zeros, a one, then L%m in m
+ * binary digits MSB first.  Writes the code as 0/1 bytes into out (NULL: size only) and
+ * returns its length. */
+uint64_t oracle_golomb(const uint8_t* bits, uint64_t n, uint32_t m, uint8_t* out) {
+  uint64_t o = 0, run = 0;
+  for (uint64_t i = 0; i <= n; ++i) {
+    if (i < n && bits[i]) {
+      ++run;
+      continue;
+    }
+    if (run) {
+      const uint64_t q = run / m, r = run % m;
+      if (out) {
+        for (uint64_t k = 0; k < q; ++k) out[o + k] = 0;
+        out[o + q] = 1;
+        for (uint32_t k = 0; k < m; ++k) out[o + q + 1 + k] = (uint8_t)((r >> (m - 1 - k)) & 1);
+      }
+      o += q + 1 + m;
+      run = 0;
+    }
+  }
+  return o;
+}

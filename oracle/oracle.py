@@ -54,6 +54,8 @@ def lib():
         L.oracle_wt_levels.restype = C.c_int
         L.oracle_shard_hist.argtypes = [vp, u64, u64, u64, vp]
         L.oracle_key_geometry.argtypes = [vp, u64, vp, vp, vp, vp, vp]
+        L.oracle_golomb.argtypes = [vp, u64, C.c_uint32, vp]
+        L.oracle_golomb.restype = u64
         _lib = L
     return _lib
 
@@ -129,6 +131,25 @@ def key_geometry(t) -> tuple[int, int, int, int]:
     code = np.zeros(256, dtype=np.uint16)
     lib().oracle_key_geometry(_p(t), len(t), C.byref(q), C.byref(pb), C.byref(R), C.byref(kb), _p(code))
     return q.value, pb.value, R.value, kb.value
+
+
+def golomb_m(ones: int, total: int) -> int:
+    """csa/wavelet_tree.py:32-38 (Python float arithmetic, as the reference)."""
+    import math
+    if ones == 0:
+        return 1
+    return max(1, int(math.log2(1 / (ones / total))))
+
+
+def golomb(bits, m: int | None = None) -> tuple[int, np.ndarray]:
+    """(m, code bits) of GolombRiceEncoder(bits).encode(bits) (csa/wavelet_tree.py:27-63)."""
+    b = np.ascontiguousarray(bits, dtype=np.uint8)
+    if m is None:
+        m = golomb_m(int(b.sum()), int(b.size))
+    nb = lib().oracle_golomb(_p(b) if b.size else None, b.size, m, None)
+    out = np.zeros(max(1, nb), dtype=np.uint8)
+    lib().oracle_golomb(_p(b) if b.size else None, b.size, m, _p(out))
+    return m, out[:nb]
 
 
 class FM:

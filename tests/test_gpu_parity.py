@@ -49,6 +49,11 @@ def _check_against_golden_case(dev, c, name):
         bits = dev.wt_level_bits(lv)
         assert len(bits) == n
         assert np.array_equal(bits[:len(g["bits"])], g["bits"]), (name, lv)
+        m, ones, code = dev.wt_golomb(lv, len(g["bits"]))
+        assert np.array_equal(code, g["golomb"]), (name, lv)
+        assert ones == int(g["bits"].sum())
+        if lv == 0:
+            assert m == int(c["wt_m"][0]), name
 
 
 def test_random_golden_cases(hk, random_cases):
@@ -132,6 +137,41 @@ def test_sa_bwt_wt_vs_oracle(hk, name, text):
     dev.close()
 
 
+def _binary_level_cases():
+    rng = np.random.default_rng(21)
+    yield "alternating", np.tile([0, 1], 3000)
+    yield "all_ones", np.ones(5000, np.int64)
+    yield "no_ones", np.zeros(999, np.int64)
+    yield "one_long_run", np.concatenate([np.zeros(37), np.ones(1500), np.zeros(3)])
+    runs = []
+    for _ in range(400):                      # runs around the 64-bit word / 448-bit line seams
+        runs += [0] * int(rng.integers(1, 70)) + [1] * int(rng.choice([1, 2, 63, 64, 65, 447, 448, 449, 900]))
+    yield "seams", np.array(runs)
+    for p in (0.01, 0.25, 0.5, 0.75, 0.97):
+        yield f"iid_{p}", (rng.random(200_003) < p).astype(np.int64)
+
+
+@pytest.mark.parametrize("name,bits", list(_binary_level_cases()))
+def test_golomb_level_vs_oracle(hk, name, bits):
+    """Level 0 of sequence over {a} | {b, c} is the bit pattern itself: Golomb-code prefixes of it."""
+    seq = np.where(np.asarray(bits) == 1, ord("b"), ord("a")).astype(np.uint8)
+    dev = hk.DeviceIndex.from_bytes(np.concatenate([seq, np.array([ord("c")], np.uint8)]), device=0)
+    dev.use_text_as_bwt()
+    dev.build_wt()
+    lvl = dev.wt_level_bits(0)
+    n = len(seq)
+    rng = np.random.default_rng(n)
+    for nb in sorted({0, 1, 63, 64, 65, 447, 448, 449, n, n + 1, int(rng.integers(1, n + 1))}):
+        ref_bits = lvl[:nb]
+        for m in (0, 1, 5):
+            got_m, ones, code = dev.wt_golomb(0, nb, m)
+            want_m, want = oracle.golomb(ref_bits, m if m else None)
+            assert got_m == want_m, (name, nb, m)
+            assert ones == int(ref_bits.sum())
+            assert np.array_equal(code, want), (name, nb, m)
+    dev.close()
+
+
 def test_repeated_builds_are_identical(hk):
     text = oracle.synth_text(300001, b"ACGT", seed=33)
     dev = hk.DeviceIndex.from_bytes(text, device=0)
@@ -160,7 +200,15 @@ def test_full_size_config1_256MiB(hk):
     text = oracle.synth_text(n, b"ACGT", seed=2)
     assert np.array_equal(dev.text(0, 4096), text[:4096])
     assert oracle.check_sa(text, sa) == 0
-    assert np.array_equal(dev.bwt(), oracle.bwt(text, sa))
+    bwt = oracle.bwt(text, sa)
+    assert np.array_equal(dev.bwt(), bwt)
+    # WT + Golomb-Rice code of every level at full size (§8f-1)
+    dev.build_wt()
+    full = oracle.wt_levels(bwt)
+    for lv in range(len(full)):
+        m, ones, code = dev.wt_golomb(lv)
+        wm, want = oracle.golomb(full[lv])
+        assert m == wm and ones == int(full[lv].sum()) and np.array_equal(code, want), lv
     dev.close()
 
 
@@ -204,6 +252,8 @@ def test_timing_stats(hk):
     dev.timing(True)
     dev.build_sa()
     dev.synchronize()
-    l, ms, b = dev.kernel_stats("radix_onesweep")
+    l, ms, b = dev.kernel_stats("radix_onesweep_small")   # < 2^24 keys: the small-sort variant
     assert l >= 1 and ms > 0 and b > 0
+    l, ms, b = dev.kernel_stats("sa_pack_keys")
+    assert l == 1 and ms > 0 and b > 0
     dev.close()

@@ -101,6 +101,35 @@ def test_random_cases_python_wt(random_cases):
             assert levels[0]["m"] == int(c["wt_m"][0])
 
 
+def test_golomb_c_oracle_vs_golden(random_cases):
+    """oracle_golomb (C) with the reference's m on every golden left-spine level."""
+    seen = 0
+    for name in random_cases.names:
+        c = random_cases.get(name)
+        for lv, g in enumerate(wt_golden_levels(c)):
+            m, code = oracle.golomb(g["bits"])
+            assert np.array_equal(code, g["golomb"]), (name, lv)
+            if lv == 0:
+                assert m == int(c["wt_m"][0]), name
+            seen += 1
+    assert seen > 100
+
+
+def test_golomb_c_oracle_vs_port():
+    rng = np.random.default_rng(5)
+    cases = [np.zeros(0, np.uint8), np.ones(200, np.uint8), np.zeros(77, np.uint8),
+             np.tile([1, 0], 100).astype(np.uint8)]
+    for p in (0.02, 0.3, 0.5, 0.9, 0.995):
+        cases.append((rng.random(3000) < p).astype(np.uint8))
+    for bits in cases:
+        m_ref = ref_port.golomb_m(bits.tolist()) if bits.size else 1
+        for m in (None, 1, 3, 17):
+            mm, code = oracle.golomb(bits, m)
+            want = ref_port.golomb_encode(bits.tolist(), m_ref if m is None else m)
+            assert np.array_equal(code, np.asarray(want, np.uint8))
+            assert mm == (m_ref if m is None else m)
+
+
 def test_random_cases_entropy(random_cases):
     for name in random_cases.names[:40]:
         c = random_cases.get(name)
