@@ -8,21 +8,44 @@ come from the working EnhancedFMIndex (csa/enhanced_fm_index.py:15-32):
   count(p)    = r - l + 1 of find_range(p), 0 on a miss
   locate(p)   = find(p): positions of T' = text + '$' in SA order
   extract(i,j)= text[i:j] with Python slice semantics (oracle: plain slicing)
-`epsilon` is accepted and recorded; this round keeps the full SA resident
-(SA sampling for the epsilon space/time trade-off is the next stage).
+`epsilon` sets the space/time trade-off: the SA is sampled every
+s = ceil(log2(n') ** epsilon) text positions (epsilon=0 keeps every entry), then
+the full SA, BWT array and text are released from HBM (hkcsa_compact); locate,
+suffix_array, bwt and extract then run as LF walks over the wavelet tree to the
+samples and return exactly what the full arrays would.  compact=False keeps
+the full arrays resident (fastest locate).
 """
 from __future__ import annotations
+
+import math
 
 from .enhanced_fm_index import EnhancedFMIndex
 
 
+def sample_rate(n: int, epsilon: float) -> int:
+    """Samples every ceil(log2(n) ** epsilon) positions (1 = the full SA)."""
+    if epsilon <= 0:
+        return 1
+    return max(1, int(math.ceil(math.log2(max(2, n)) ** epsilon)))
+
+
 class CSA:
-    def __init__(self, text, epsilon: float = 0.5):
+    def __init__(self, text, epsilon: float = 0.5, compact: bool = True):
         if not isinstance(text, str):
             text = "".join(text)
         self.text = text
         self.epsilon = epsilon
         self._fm = EnhancedFMIndex(text)
+        self.sample_rate = sample_rate(len(text) + 1, epsilon)
+        self.compressed = compact
+        if compact:
+            dev = self._fm.device_index
+            dev.build_samples(self.sample_rate)
+            dev.compact()
+
+    def space(self) -> dict:
+        """Resident HBM bytes by structure (hkcsa_space)."""
+        return self._fm.device_index.space()
 
     def __len__(self):
         return len(self.text)

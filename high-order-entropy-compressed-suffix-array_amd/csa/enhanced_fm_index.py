@@ -2,7 +2,8 @@
 
 Same constructor, attributes and methods; construction and every query run on
 the GPU through libhkcsa.so:
-  * __init__      -> hkcsa_build_all: SA (prefix doubling), BWT gather, C array
+  * __init__      -> hkcsa_build_all: SA (LSD radix sort of q-symbol suffix keys + tie
+                     refinement; the BWT falls out of the sorted keys), C array
                      and the levelwise wavelet tree (replaces the O(n*sigma) occ table)
   * find_range    -> batched backward search kernel (one lane per pattern)
   * find          -> find_range + SA gather, positions in SA order (:15-19)

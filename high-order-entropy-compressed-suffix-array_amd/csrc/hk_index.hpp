@@ -79,6 +79,15 @@ struct Index {
   DevBuf seq[2];               // WT level code sequences
   DevBuf gr_tmp[2], gr_out;    // Golomb-Rice coding of a level (per-word carries/offsets, code words)
 
+  // SA/ISA samples (compressed mode, hk_sample.hip)
+  bool have_text = true;       // false after compact(): T' is then read back by LF walks
+  bool bwt_in_wt = false;      // the BWT array was released; BWT[i] comes from the WT
+  bool have_samples = false;
+  uint32_t smp_rate = 0;
+  uint64_t smp_count = 0, smp_fixn = 0;
+  int smp_cstar = 0;
+  DevBuf smp_mark, smp_sa, smp_isa, smp_fix, smp_inv;
+
   // sharded construction
   bool sharded = false;
   bool sa_pos64 = false;       // sharded slices of texts with n >= 2^32 hold u64 positions
@@ -106,6 +115,15 @@ void query_locate_gather(Index& ix, const int64_t* d_lr, const uint64_t* d_occ_o
                          uint64_t* d_pos);
 void query_rank(Index& ix, const uint8_t* d_c, const uint64_t* d_i, uint64_t k, uint64_t* d_out);
 void wt_level_words(Index& ix, int depth, uint64_t* d_words);
+
+// SA sampling: samples every `rate` text positions, exact-LF fix table; compact() drops SA, BWT
+// array, text and workspace, after which SA / BWT / text are answered by LF walks
+void build_samples(Index& ix, uint32_t rate);
+void compact(Index& ix);
+void sampled_locate_gather(Index& ix, const int64_t* d_lr, const uint64_t* d_occ_offs, uint64_t P, uint64_t* d_pos);
+void sampled_sa_range(Index& ix, uint64_t lo, uint64_t count, uint64_t* d_out);
+void wt_bwt_range(Index& ix, uint64_t lo, uint64_t count, uint8_t* d_out);
+void sampled_extract(Index& ix, uint64_t i, uint64_t j, uint8_t* d_out);
 
 // Golomb-Rice code of the first nbits bits of a level (csa/wavelet_tree.py:27-63); with write,
 // the code words are left in ix.gr_out

@@ -19,6 +19,7 @@
 //   tables in LDS).
 
 #include "hk_index.hpp"
+#include "hk_wtq.hpp"
 
 namespace hk {
 
@@ -38,24 +39,6 @@ WtView Index::view() const {
 }
 
 namespace {
-
-__device__ __forceinline__ uint64_t rank1(const uint64_t* __restrict__ lines, uint64_t x) {
-  const uint32_t x6 = (uint32_t)(x >> 6);
-  const uint64_t li = x6 / 7u;
-  const uint32_t off = (uint32_t)(x - li * kLineBits);
-  const ulonglong2* L = reinterpret_cast<const ulonglong2*>(lines + li * 8);
-  const ulonglong2 a = L[0], b = L[1], c = L[2], d = L[3];
-  const uint64_t w[7] = {a.y, b.x, b.y, c.x, c.y, d.x, d.y};
-  const uint32_t wi = off >> 6, bi = off & 63u;
-  const uint64_t pm = (1ull << bi) - 1ull;
-  uint64_t r = a.x;
-#pragma unroll
-  for (int k = 0; k < 7; ++k) {
-    const uint64_t m = (uint32_t)k < wi ? ~0ull : ((uint32_t)k == wi ? pm : 0ull);
-    r += (uint64_t)__popcll(w[k] & m);
-  }
-  return r;
-}
 
 __global__ __launch_bounds__(256) void k_map_codes(const uint8_t* __restrict__ in, uint64_t n,
                                                    const int16_t* __restrict__ code,
@@ -152,49 +135,6 @@ __global__ __launch_bounds__(256) void k_wt_extract(const uint64_t* __restrict__
 }
 
 // ------------------------------------------------------------ queries
-struct QShared {
-  uint64_t obn[kMaxLevels][256];
-  uint64_t rbase[kMaxLevels][256];
-  uint8_t bit[kMaxLevels][256];
-  uint8_t depth[256];
-  int16_t code[256];
-  const uint64_t* lines[kMaxLevels];
-};
-
-__device__ __forceinline__ void load_qshared(QShared& q, const WtView& v) {
-  const int t = threadIdx.x;  // blockDim == 256
-  q.depth[t] = v.depth[t];
-  q.code[t] = v.code[t];
-  for (int d = 0; d < v.levels; ++d) {
-    if (t < v.sigma) {
-      q.obn[d][t] = v.obn[d * 256 + t];
-      q.rbase[d][t] = v.rbase[d * 256 + t];
-    }
-    q.bit[d][t] = v.bit[d * 256 + t];
-  }
-  if (t < kMaxLevels) q.lines[t] = v.lines[t];
-  __syncthreads();
-}
-
-// LF step of the pair (xl, xr) for code c: returns the leaf positions
-__device__ __forceinline__ void lf_pair(const QShared& q, int c, uint64_t& xl, uint64_t& xr) {
-  const int dep = q.depth[c];
-  for (int d = 0; d < dep; ++d) {
-    const uint64_t* L = q.lines[d];
-    const uint64_t rl = rank1(L, xl);
-    const uint64_t rr = rank1(L, xr);
-    if (q.bit[d][c]) {
-      const uint64_t rb = q.rbase[d][c];
-      xl = rb + rl;
-      xr = rb + rr;
-    } else {
-      const uint64_t o = q.obn[d][c];
-      xl = xl - rl + o;
-      xr = xr - rr + o;
-    }
-  }
-}
-
 __global__ __launch_bounds__(256) void k_count(WtView v, const uint8_t* __restrict__ pats,
                                                const uint64_t* __restrict__ offs, uint64_t P,
                                                int64_t* __restrict__ lr, uint64_t* __restrict__ cnt) {
@@ -379,6 +319,7 @@ void query_count(Index& ix, const uint8_t* d_pats, const uint64_t* d_offs, uint6
 
 void query_locate_gather(Index& ix, const int64_t* d_lr, const uint64_t* d_occ_offs, uint64_t P,
                          uint64_t* d_pos) {
+  if (!ix.have_sa && ix.have_samples) return sampled_locate_gather(ix, d_lr, d_occ_offs, P, d_pos);
   if (!ix.have_sa) throw ApiError{-3, "locate: suffix array not built"};
   if (!P) return;
   hipStream_t s = ix.stream;

@@ -128,6 +128,7 @@ int hkcsa_create_synthetic(uint64_t n, const uint8_t* alphabet, int sigma, uint6
 int hkcsa_build_sa(hkcsa_index* h) {
   return guarded([&] {
     activate(h);
+    need(h->ix.have_text, HKCSA_E_STATE, "text released by hkcsa_compact");
     h->ix.have_bwt = h->ix.have_wt = false;
     hk::build_sa(h->ix);
   });
@@ -135,6 +136,7 @@ int hkcsa_build_sa(hkcsa_index* h) {
 int hkcsa_build_bwt(hkcsa_index* h) {
   return guarded([&] {
     activate(h);
+    need(h->ix.have_text, HKCSA_E_STATE, "text released by hkcsa_compact");
     h->ix.have_wt = false;
     hk::build_bwt(h->ix);
   });
@@ -142,12 +144,14 @@ int hkcsa_build_bwt(hkcsa_index* h) {
 int hkcsa_build_wt(hkcsa_index* h) {
   return guarded([&] {
     activate(h);
+    if (h->ix.bwt_in_wt) return;   // compacted: the WT is the only copy of the BWT
     hk::build_wt(h->ix);
   });
 }
 int hkcsa_build_all(hkcsa_index* h) {
   return guarded([&] {
     activate(h);
+    need(h->ix.have_text, HKCSA_E_STATE, "text released by hkcsa_compact");
     hk::build_sa(h->ix);
     hk::build_bwt(h->ix);
     hk::build_wt(h->ix);
@@ -160,6 +164,42 @@ int hkcsa_release_workspace(hkcsa_index* h) {
     hk::release_workspace(h->ix);
   });
 }
+int hkcsa_build_samples(hkcsa_index* h, uint32_t rate) {
+  return guarded([&] {
+    activate(h);
+    need(rate >= 1, HKCSA_E_INVALID, "sample rate must be >= 1");
+    need(h->ix.have_text, HKCSA_E_STATE, "text released by hkcsa_compact");
+    need(h->ix.have_sa && !h->ix.sharded, HKCSA_E_STATE, "suffix array not built");
+    if (!h->ix.have_bwt) hk::build_bwt(h->ix);
+    hk::build_samples(h->ix, rate);
+  });
+}
+
+int hkcsa_compact(hkcsa_index* h) {
+  return guarded([&] {
+    activate(h);
+    need(h->ix.have_samples, HKCSA_E_STATE, "build the SA samples first");
+    hk::compact(h->ix);
+  });
+}
+
+int hkcsa_space(hkcsa_index* h, uint64_t out[8]) {
+  return guarded([&] {
+    activate(h);
+    need(out != nullptr, HKCSA_E_INVALID, "null output");
+    const hk::Index& ix = h->ix;
+    const uint64_t nl = ix.n / hk::kLineBits + 1;
+    out[0] = ix.have_text ? ix.n : 0;
+    out[1] = ix.have_sa ? ix.n * (ix.sa_pos64 ? 8 : 4) : 0;
+    out[2] = (ix.have_bwt && !ix.bwt_in_wt) ? ix.n : 0;
+    out[3] = ix.have_wt ? (uint64_t)ix.wt_levels * nl * 64 : 0;
+    out[4] = ix.have_samples ? nl * 64 : 0;
+    out[5] = ix.have_samples ? ix.smp_count * 8 + ix.smp_fixn * 4 : 0;
+    out[6] = ix.smp_rate;
+    out[7] = ix.have_samples ? 1 : 0;
+  });
+}
+
 int hkcsa_synchronize(hkcsa_index* h) {
   return guarded([&] {
     activate(h);
@@ -203,6 +243,7 @@ int hkcsa_bwt_gather(const uint8_t* text, uint64_t n, const uint64_t* sa, uint8_
 int hkcsa_use_text_as_bwt(hkcsa_index* h) {
   return guarded([&] {
     activate(h);
+    need(h->ix.have_text, HKCSA_E_STATE, "text released by hkcsa_compact");
     h->ix.bwt.ensure(h->ix.n + 64);
     HK_HIP(hipMemcpyAsync(h->ix.bwt.p, h->ix.text.p, h->ix.n, hipMemcpyDeviceToDevice, h->ix.stream));
     HK_HIP(hipStreamSynchronize(h->ix.stream));
@@ -221,11 +262,19 @@ int hkcsa_get_n(const hkcsa_index* h, uint64_t* n) {
 int hkcsa_get_sa(hkcsa_index* h, uint64_t lo, uint64_t hi, uint64_t* out) {
   return guarded([&] {
     activate(h);
-    need(h->ix.have_sa && !h->ix.sharded, HKCSA_E_STATE, "suffix array not built");
+    need((h->ix.have_sa || h->ix.have_samples) && !h->ix.sharded, HKCSA_E_STATE, "suffix array not built");
     need(lo <= hi && hi <= h->ix.n, HKCSA_E_RANGE, "SA range out of bounds");
     need(hi == lo || out, HKCSA_E_INVALID, "null output");
     const uint64_t c = hi - lo;
     if (!c) return;
+    if (!h->ix.have_sa) {   // compressed mode: LF walks to the samples
+      hk::DevBuf tmp;
+      tmp.ensure(c * 8);
+      hk::sampled_sa_range(h->ix, lo, c, tmp.as<uint64_t>());
+      HK_HIP(hipMemcpyAsync(out, tmp.p, c * 8, hipMemcpyDeviceToHost, h->ix.stream));
+      HK_HIP(hipStreamSynchronize(h->ix.stream));
+      return;
+    }
     std::vector<uint32_t> tmp(c);
     HK_HIP(hipMemcpyAsync(tmp.data(), h->ix.sa.as<uint32_t>() + lo, c * 4, hipMemcpyDeviceToHost, h->ix.stream));
     HK_HIP(hipStreamSynchronize(h->ix.stream));
@@ -240,6 +289,14 @@ int hkcsa_get_bwt(hkcsa_index* h, uint64_t lo, uint64_t hi, uint8_t* out) {
     need(lo <= hi && hi <= h->ix.n, HKCSA_E_RANGE, "BWT range out of bounds");
     if (hi == lo) return;
     need(out != nullptr, HKCSA_E_INVALID, "null output");
+    if (h->ix.bwt_in_wt) {
+      hk::DevBuf tmp;
+      tmp.ensure(hi - lo);
+      hk::wt_bwt_range(h->ix, lo, hi - lo, tmp.as<uint8_t>());
+      HK_HIP(hipMemcpyAsync(out, tmp.p, hi - lo, hipMemcpyDeviceToHost, h->ix.stream));
+      HK_HIP(hipStreamSynchronize(h->ix.stream));
+      return;
+    }
     HK_HIP(hipMemcpyAsync(out, h->ix.bwt.as<uint8_t>() + lo, hi - lo, hipMemcpyDeviceToHost, h->ix.stream));
     HK_HIP(hipStreamSynchronize(h->ix.stream));
   });
@@ -251,6 +308,14 @@ int hkcsa_get_text(hkcsa_index* h, uint64_t lo, uint64_t hi, uint8_t* out) {
     need(lo <= hi && hi <= h->ix.n, HKCSA_E_RANGE, "text range out of bounds");
     if (hi == lo) return;
     need(out != nullptr, HKCSA_E_INVALID, "null output");
+    if (!h->ix.have_text) {   // compressed mode: LF walks from the ISA samples
+      hk::DevBuf tmp;
+      tmp.ensure(hi - lo);
+      hk::sampled_extract(h->ix, lo, hi, tmp.as<uint8_t>());
+      HK_HIP(hipMemcpyAsync(out, tmp.p, hi - lo, hipMemcpyDeviceToHost, h->ix.stream));
+      HK_HIP(hipStreamSynchronize(h->ix.stream));
+      return;
+    }
     HK_HIP(hipMemcpyAsync(out, h->ix.text.as<uint8_t>() + lo, hi - lo, hipMemcpyDeviceToHost, h->ix.stream));
     HK_HIP(hipStreamSynchronize(h->ix.stream));
   });
@@ -449,6 +514,7 @@ int hkcsa_locate_batch(hkcsa_index* h, const uint8_t* pats, const uint64_t* offs
 int hkcsa_build_sa_sharded(hkcsa_index* h, const uint8_t id[128], int nranks, int rank) {
   return guarded([&] {
     activate(h);
+    need(h->ix.have_text, HKCSA_E_STATE, "text released by hkcsa_compact");
     need(id != nullptr && nranks >= 1 && rank >= 0 && rank < nranks, HKCSA_E_INVALID, "bad communicator args");
     h->ix.have_bwt = h->ix.have_wt = false;
     hk::build_sa_sharded(h->ix, id, nranks, rank);
@@ -467,6 +533,7 @@ int hkcsa_shard_buckets(void) { return hk::shard_buckets(); }
 int hkcsa_shard_histogram(hkcsa_index* h, int nranks, int rank, uint64_t* hist_out) {
   return guarded([&] {
     activate(h);
+    need(h->ix.have_text, HKCSA_E_STATE, "text released by hkcsa_compact");
     need(hist_out != nullptr && nranks >= 1 && rank >= 0 && rank < nranks, HKCSA_E_INVALID, "bad arguments");
     const int nb = hk::shard_buckets();
     hk::DevBuf d;
@@ -480,6 +547,7 @@ int hkcsa_shard_histogram(hkcsa_index* h, int nranks, int rank, uint64_t* hist_o
 int hkcsa_shard_build(hkcsa_index* h, const uint64_t* global_hist, int nranks, int rank) {
   return guarded([&] {
     activate(h);
+    need(h->ix.have_text, HKCSA_E_STATE, "text released by hkcsa_compact");
     need(global_hist != nullptr && nranks >= 1 && rank >= 0 && rank < nranks, HKCSA_E_INVALID, "bad arguments");
     h->ix.have_bwt = h->ix.have_wt = false;
     hk::shard_build(h->ix, global_hist, nranks, rank);

@@ -142,6 +142,20 @@ class DeviceIndex:
     def synchronize(self):
         N.check(self.lib.hkcsa_synchronize(self.h))
 
+    def build_samples(self, rate: int):
+        """SA/ISA samples every `rate` positions (hkcsa_build_samples)."""
+        N.check(self.lib.hkcsa_build_samples(self.h, int(rate)))
+
+    def compact(self):
+        """Drop SA, BWT array, text and workspace; queries continue from the WT + samples."""
+        N.check(self.lib.hkcsa_compact(self.h))
+
+    def space(self) -> dict:
+        out = np.zeros(8, dtype=np.uint64)
+        N.check(self.lib.hkcsa_space(self.h, _ptr(out)))
+        keys = ["text", "sa", "bwt", "wt", "sample_marks", "samples", "sample_rate", "sampled"]
+        return {k: int(v) for k, v in zip(keys, out)}
+
     # ------------------------------------------------------------ exports
     def sa(self, lo: int = 0, hi: int | None = None) -> np.ndarray:
         hi = self.n if hi is None else hi

@@ -81,6 +81,19 @@ int hkcsa_build_wt(hkcsa_index* ix);
 int hkcsa_build_all(hkcsa_index* ix);
 /* Drop the construction workspace (keys, ISA, ...) kept for repeated builds. */
 int hkcsa_release_workspace(hkcsa_index* ix);
+/* SA sampling for the epsilon space/time contract of CompressedSuffixArray(text, epsilon)
+ * (tests/benchmark.py:25,32; the class itself is absent from the reference, csa/csa.py:3):
+ * keeps SA[i] for the rows with SA[i] % rate == 0, the row of every position k*rate, and the
+ * exact LF of the rows whose BWT symbol is T'[n-1] (the wrapped row, csa/bwt.py:8-11).
+ * Needs the single-GPU SA; builds the BWT/WT if missing. */
+int hkcsa_build_samples(hkcsa_index* ix, uint32_t rate);
+/* Compressed mode: release SA, BWT array, T' and workspace.  Afterwards SA entries, locate,
+ * BWT bytes and text/extract are answered by LF walks over the WT to the samples — results
+ * identical to the full arrays; construction calls fail with HKCSA_E_STATE. */
+int hkcsa_compact(hkcsa_index* ix);
+/* Resident bytes: out[0] text, [1] SA, [2] BWT array, [3] WT rank lines, [4] sample marks,
+ * [5] SA/ISA samples + LF fixes, [6] sample rate, [7] 1 if samples are built. */
+int hkcsa_space(hkcsa_index* ix, uint64_t out[8]);
 int hkcsa_synchronize(hkcsa_index* ix);
 void hkcsa_free(hkcsa_index* ix);
 
@@ -144,7 +157,7 @@ int hkcsa_queries_download(hkcsa_index* ix, hkcsa_queries* q, int64_t* lr_out, u
                            uint64_t* pos_out, uint64_t cap);
 void hkcsa_queries_free(hkcsa_queries* q);
 /* text[i:j) of T' (csa.CSA.extract; oracle: Python slicing). */
-int hkcsa_extract(hkcsa_index* ix, uint64_t i, uint64_t j, uint8_t* out);
+int hkcsa_extract(hkcsa_index* ix, uint64_t i, uint64_t j, uint8_t* out);   /* T'[i:j); LF walks when compacted */
 
 /* ---- sharded (multi-GPU) suffix-array construction ------------------- */
 /* RCCL unique id (128 bytes) to be broadcast by the caller from rank 0. */

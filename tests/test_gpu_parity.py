@@ -257,3 +257,59 @@ def test_timing_stats(hk):
     l, ms, b = dev.kernel_stats("sa_pack_keys")
     assert l == 1 and ms > 0 and b > 0
     dev.close()
+
+
+def _sampled_texts():
+    yield "dna_200K", oracle.synth_text(200_001, b"ACGT", seed=41)
+    yield "bytes_64K", oracle.synth_text(65_537, bytes(range(256)), seed=42)
+    t = oracle.synth_text(50_001, b"AC$G", seed=43)            # '$' inside the text: LF fix rows
+    yield "dollars_50K", t
+    yield "periodic_30K", np.frombuffer(b"abcab" * 6000 + b"$", dtype=np.uint8)
+    yield "run_5K", np.frombuffer(b"a" * 5000 + b"$", dtype=np.uint8)
+    yield "two", np.frombuffer(b"z$", dtype=np.uint8)
+    yield "single", np.frombuffer(b"$", dtype=np.uint8)
+
+
+@pytest.mark.parametrize("name,text", list(_sampled_texts()))
+@pytest.mark.parametrize("rate", [1, 3, 6, 32])
+def test_sampled_compressed_mode(hk, name, text, rate):
+    """hkcsa_build_samples + hkcsa_compact: SA, BWT, text, extract, count and locate answered by
+    LF walks equal the full arrays (and the oracle)."""
+    n = len(text)
+    dev = _build(hk, text.tobytes())
+    sa = dev.sa()
+    bwt = dev.bwt()
+    assert np.array_equal(sa, oracle.suffix_array(text)), name
+    rng = np.random.default_rng(rate * 1000 + n)
+    pats = [b"", b"$", bytes(text[-2:])]
+    for _ in range(300):
+        m = int(rng.integers(1, 12))
+        s = int(rng.integers(0, max(1, n - m)))
+        pats.append(text[s:s + m].tobytes())
+    lr_full = dev.count_ranges(pats)
+    offs_full, pos_full = dev.locate(pats)
+    dev.build_samples(rate)
+    dev.compact()
+    sp = dev.space()
+    assert sp["sa"] == 0 and sp["text"] == 0 and sp["bwt"] == 0 and sp["sampled"] == 1
+    assert sp["sample_rate"] == rate
+    assert np.array_equal(dev.sa(), sa), name
+    assert np.array_equal(dev.bwt(), bwt), name
+    assert np.array_equal(dev.text(), text), name
+    for _ in range(50):
+        i = int(rng.integers(0, n))
+        j = int(rng.integers(i, n + 1))
+        assert dev.extract(i, j) == text[i:j].tobytes(), (name, i, j)
+    assert np.array_equal(dev.count_ranges(pats), lr_full), name
+    offs, pos = dev.locate(pats)
+    assert np.array_equal(offs, offs_full) and np.array_equal(pos, pos_full), name
+    with pytest.raises(hk.HkcsaError):
+        dev.build_sa()
+    dev.close()
+
+
+def test_compact_needs_samples(hk):
+    dev = _build(hk, b"banana$")
+    with pytest.raises(hk.HkcsaError):
+        dev.compact()
+    dev.close()

@@ -80,3 +80,11 @@ def test_slice_bounds_tile_the_sa(nranks):
     # slices stay near n/N for a high-entropy text
     for lo, hi in b:
         assert abs((hi - lo) - len(t) / nranks) < 0.05 * len(t) + 64
+
+
+def test_csa_sample_rate():
+    from csa.csa import sample_rate
+    assert sample_rate(2**30 + 1, 0.5) == 6       # ceil(sqrt(30.000...))
+    assert sample_rate(2**20 + 1, 1.0) == 21
+    assert sample_rate(1000, 0) == 1
+    assert sample_rate(1, 0.5) == 1
