@@ -53,6 +53,55 @@ __device__ __forceinline__ void stage_text_codes(uint16_t* c, const uint16_t* L,
   }
 }
 
+// The same staging split in two so a tile's text loads can be issued a tile ahead (software
+// pipelining: the loads of tile i+1 are in flight while tile i is processed).  The text buffer
+// holds n + 64 bytes, so an aligned word starting below n is always readable.
+template <int TILE, int NT>
+struct TextWords {
+  static constexpr int NWORDS = (TILE + 64) / 4;
+  static constexpr int PER = (NWORDS + NT - 1) / NT;
+  uint32_t w[PER];
+  uint32_t prev;
+};
+
+template <int TILE, int NT>
+__device__ __forceinline__ void load_text_words(TextWords<TILE, NT>& tw, const uint8_t* __restrict__ t, uint64_t n,
+                                                uint64_t base) {
+#pragma unroll
+  for (int i = 0; i < TextWords<TILE, NT>::PER; ++i) {
+    const int wI = threadIdx.x + i * NT;
+    const uint64_t p = base + 4 * (uint64_t)wI;
+    tw.w[i] = (wI < TextWords<TILE, NT>::NWORDS && p < n) ? *reinterpret_cast<const uint32_t*>(t + p) : 0u;
+  }
+  tw.prev = threadIdx.x == 0 ? t[base == 0 ? n - 1 : base - 1] : 0u;
+}
+
+template <int TILE, int NT>
+__device__ __forceinline__ void store_text_codes(uint16_t* c, const uint16_t* L, const TextWords<TILE, NT>& tw,
+                                                 uint64_t n, uint64_t base) {
+  if (threadIdx.x == 0) c[0] = L[tw.prev];
+#pragma unroll
+  for (int i = 0; i < TextWords<TILE, NT>::PER; ++i) {
+    const int wI = threadIdx.x + i * NT;
+    if (wI < TextWords<TILE, NT>::NWORDS) {
+      const uint64_t p = base + 4 * (uint64_t)wI;
+      const uint32_t w4 = tw.w[i];
+      if (p + 4 <= n) {
+        c[4 * wI + 1] = L[w4 & 255];
+        c[4 * wI + 2] = L[(w4 >> 8) & 255];
+        c[4 * wI + 3] = L[(w4 >> 16) & 255];
+        c[4 * wI + 4] = L[w4 >> 24];
+      } else {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) c[4 * wI + 1 + u] = p + u < n ? L[(w4 >> (8 * u)) & 255] : 0;
+      }
+    }
+  }
+}
+
+// Staged code arrays hold tile + 64 look-ahead codes; kCodePad leaves a little slack past that.
+constexpr int kCodePad = 72 + 16;
+
 // value of `len` codes starting at c[j] (len <= ck)
 __device__ __forceinline__ uint32_t chunk_value(const uint16_t* c, int j, int len, uint32_t R) {
   uint32_t cv = 0;

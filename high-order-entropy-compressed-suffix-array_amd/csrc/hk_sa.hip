@@ -101,16 +101,20 @@ __global__ __launch_bounds__(256) void k_pack_keys(const uint8_t* __restrict__ t
                                                    uint64_t count, const uint16_t* __restrict__ lut, uint64_t R,
                                                    int q, int pb, int ck, uint64_t Rck, uint64_t Rlast,
                                                    uint64_t* __restrict__ keys, unsigned long long* __restrict__ hist0) {
-  __shared__ uint16_t c[PK_TILE + 72];   // q <= 64 symbols of look-ahead
+  __shared__ uint16_t c[PK_TILE + kCodePad];   // q <= 64 symbols of look-ahead
   __shared__ uint16_t L[256];
   __shared__ uint32_t H[256];
   L[threadIdx.x] = lut[threadIdx.x];
   H[threadIdx.x] = 0;
   __syncthreads();
   const uint64_t end = lo + count;
-  for (uint64_t base = lo + (uint64_t)blockIdx.x * PK_TILE; base < end; base += (uint64_t)gridDim.x * PK_TILE) {
-    stage_text_codes<PK_TILE, 256>(c, L, t, n, base);
+  const uint64_t stride = (uint64_t)gridDim.x * PK_TILE;
+  TextWords<PK_TILE, 256> tw;
+  if (lo + (uint64_t)blockIdx.x * PK_TILE < end) load_text_words(tw, t, n, lo + (uint64_t)blockIdx.x * PK_TILE);
+  for (uint64_t base = lo + (uint64_t)blockIdx.x * PK_TILE; base < end; base += stride) {
+    store_text_codes(c, L, tw, n, base);
     __syncthreads();
+    if (base + stride < end) load_text_words(tw, t, n, base + stride);   // next tile's text in flight
 #pragma unroll 4
     for (int k = 0; k < PK_TILE / 256; ++k) {
       const int off = k * 256 + threadIdx.x;

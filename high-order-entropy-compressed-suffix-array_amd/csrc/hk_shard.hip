@@ -34,9 +34,10 @@ struct ShardComm {  // one RCCL communicator per process (one process per GPU)
   uint8_t id[128];
 };
 
-// bucket of a key: its top SH_BUCKET_BITS bits (key >> bsh)
+// bucket of a key: its top SH_BUCKET_BITS bits (key >> bsh).  With key = m << pb | prev and
+// bsh >= pb, bucket in [blo, bhi) <=> m in [Mlo, Mhi) (see sel_geom).
 struct BucketGeom {
-  uint64_t R, Rck, Rlast, Rrest;
+  uint64_t R, Rck, Rlast;
   int q, pb, ck, bsh;
 };
 
@@ -44,7 +45,7 @@ __global__ __launch_bounds__(256) void k_shard_hist(const uint8_t* __restrict__ 
                                                     uint64_t hi, const uint16_t* __restrict__ lut, BucketGeom g,
                                                     unsigned long long* __restrict__ hist) {
   __shared__ uint32_t H[SH_BUCKETS];
-  __shared__ uint16_t c[PS_TILE + 72];
+  __shared__ uint16_t c[PS_TILE + kCodePad];
   __shared__ uint16_t L[256];
   L[threadIdx.x] = lut[threadIdx.x];
   for (int i = threadIdx.x; i < SH_BUCKETS; i += 256) H[i] = 0;
@@ -66,70 +67,132 @@ __global__ __launch_bounds__(256) void k_shard_hist(const uint8_t* __restrict__ 
     if (H[i]) atomicAdd(&hist[i], (unsigned long long)H[i]);
 }
 
-// Every rank scans all of T' and keeps the suffixes whose bucket lies in [blo, bhi).  The first
-// 24-bit chunk of the key bounds the bucket to [bucket(lower), bucket(upper)]; when that interval
-// misses the rank's range (the common case: (N-1)/N of all positions) the full key is never built.
+// Every rank scans all of T' and keeps the suffixes whose bucket lies in [blo, bhi).
+//
+// Pre-test on raw bytes (no LDS, no code lookup): the first h symbols of a suffix, as a radix-R
+// prefix P, bound its key to [P·W, (P+1)·W), W = R^(q-h); with A / B the prefixes holding the
+// range ends, P in (A, B) is inside the rank's range, P outside [A, B] is not, and P == A or B
+// needs the full key.  The code map is strictly increasing, so comparing prefixes equals
+// comparing the h raw bytes big-endian against byte images of the thresholds (SelGeom, host):
+// each thread holds 32 text bytes in registers and tests its 16 consecutive positions with a
+// few shifts, byte swaps and 64-bit compares.  Positions whose h bytes run past T' take the
+// full-key path too.
+//
+// Block b owns the contiguous tiles [b*tpb, (b+1)*tpb): a count pass (registers only, one
+// reduction per block), an exclusive scan of the block counts, and a write pass that stages the
+// tile's codes in LDS, lists the selected offsets in LDS and builds their keys densely, so the
+// key / position stores are coalesced and no global atomics are needed.
+struct SelGeom {
+  uint64_t TL, TH, TA, TB, topmask;
+  int h;
+  uint32_t flags;
+};
+constexpr uint32_t SEL_NOPRE = 1, SEL_EMPTY = 2, SEL_HAS_A = 4, SEL_HAS_B = 8;
+
+__device__ __forceinline__ uint64_t key_global(const uint8_t* __restrict__ t, uint64_t n, const uint16_t* L,
+                                               uint64_t p, uint64_t R, int q, int pb) {
+  uint64_t key = 0;
+  for (int j = 0; j < q; ++j) key = key * R + (p + j < n ? L[t[p + j]] : 0u);
+  return (key << pb) | (pb ? L[t[p == 0 ? n - 1 : p - 1]] : 0u);
+}
+
+// selection bits of the 16 positions p0 .. p0+15 (bit k: p0 + k)
+__device__ __forceinline__ uint32_t select16(const uint8_t* __restrict__ t, uint64_t n, uint64_t p0,
+                                             const uint16_t* L, const BucketGeom& g, const SelGeom& sg,
+                                             uint32_t blo, uint32_t bhi) {
+  if (p0 >= n) return 0;
+  const uint4 a = *reinterpret_cast<const uint4*>(t + p0);        // T' has 64 readable pad bytes
+  const uint4 b = *reinterpret_cast<const uint4*>(t + p0 + 16);
+  const uint32_t w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+  uint32_t acc = 0, amb = 0;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const int j = k >> 2, sh = k & 3;
+    const uint32_t d0 = __builtin_amdgcn_alignbyte(w[j + 1], w[j], sh);
+    const uint32_t d1 = __builtin_amdgcn_alignbyte(w[j + 2], w[j + 1], sh);
+    const uint64_t be = (((uint64_t)__builtin_bswap32(d0) << 32) | __builtin_bswap32(d1)) & sg.topmask;
+    const bool in = !(sg.flags & SEL_EMPTY) && be >= sg.TL && be <= sg.TH;
+    const bool eq = ((sg.flags & SEL_HAS_A) && be == sg.TA) || ((sg.flags & SEL_HAS_B) && be == sg.TB);
+    if (in) acc |= 1u << k;
+    if (eq || p0 + k + sg.h > n || (sg.flags & SEL_NOPRE)) amb |= 1u << k;
+  }
+  amb &= (p0 + 16 <= n) ? 0xFFFFu : ((1u << (n - p0)) - 1u);
+  acc &= ~amb;
+  while (amb) {   // rare: boundary prefixes and the last h positions
+    const int k = __ffs(amb) - 1;
+    amb &= amb - 1;
+    const uint32_t bk = (uint32_t)(key_global(t, n, L, p0 + k, g.R, g.q, g.pb) >> g.bsh);
+    if (bk >= blo && bk < bhi) acc |= 1u << k;
+  }
+  if (p0 + 16 > n) acc &= (1u << (n - p0)) - 1u;
+  return acc;
+}
+
+__global__ __launch_bounds__(256) void k_select_count(const uint8_t* __restrict__ t, uint64_t n, uint64_t tpb,
+                                                      const uint16_t* __restrict__ lut, BucketGeom g, SelGeom sg,
+                                                      uint32_t blo, uint32_t bhi, uint64_t* __restrict__ block_cnt) {
+  __shared__ uint16_t L[256];
+  __shared__ uint64_t red[4];
+  L[threadIdx.x] = lut[threadIdx.x];
+  __syncthreads();
+  const uint64_t tiles = (n + PS_TILE - 1) / PS_TILE;
+  const uint64_t t0 = (uint64_t)blockIdx.x * tpb;
+  const uint64_t t1 = t0 + tpb < tiles ? t0 + tpb : tiles;
+  uint64_t cnt = 0;
+  for (uint64_t ti = t0; ti < t1; ++ti)
+    cnt += __popc(select16(t, n, ti * PS_TILE + 16 * threadIdx.x, L, g, sg, blo, bhi));
+  cnt = wave_sum(cnt);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = cnt;
+  __syncthreads();
+  if (threadIdx.x == 0) block_cnt[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+}
+
 template <typename V>
-__global__ __launch_bounds__(256) void k_pack_select(const uint8_t* __restrict__ t, uint64_t n,
-                                                     const uint16_t* __restrict__ lut, BucketGeom g, uint32_t blo,
-                                                     uint32_t bhi, uint64_t* __restrict__ keys,
-                                                     V* __restrict__ vals, unsigned long long* counter) {
-  __shared__ uint16_t c[PS_TILE + 72];
+__global__ __launch_bounds__(256) void k_select_write(const uint8_t* __restrict__ t, uint64_t n, uint64_t tpb,
+                                                      const uint16_t* __restrict__ lut, BucketGeom g, SelGeom sg,
+                                                      uint32_t blo, uint32_t bhi,
+                                                      const uint64_t* __restrict__ block_off,
+                                                      uint64_t* __restrict__ keys, V* __restrict__ vals) {
+  __shared__ uint16_t c[PS_TILE + kCodePad];
+  __shared__ uint16_t list[PS_TILE];
   __shared__ uint16_t L[256];
   __shared__ uint32_t red[4];
-  __shared__ unsigned long long gbase;
   L[threadIdx.x] = lut[threadIdx.x];
   __syncthreads();
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const bool pretest = g.q > g.ck;
-  const uint64_t pbmask = (1ull << g.pb) - 1;
-  for (uint64_t base = (uint64_t)blockIdx.x * PS_TILE; base < n; base += (uint64_t)gridDim.x * PS_TILE) {
-    stage_text_codes<PS_TILE, 256>(c, L, t, n, base);
-    __syncthreads();
-    uint64_t kk[PS_TILE / 256];
-    uint32_t sel = 0;
-#pragma unroll
-    for (int k = 0; k < PS_TILE / 256; ++k) {
-      const int off = k * 256 + threadIdx.x;
-      kk[k] = 0;
-      if (base + off < n) {
-        if (pretest) {
-          const uint32_t cv0 = chunk_value(c, off + 1, g.ck, (uint32_t)g.R);
-          const uint64_t lower = (uint64_t)cv0 * g.Rrest;
-          const uint32_t b_lo = (uint32_t)((lower << g.pb) >> g.bsh);
-          const uint32_t b_hi = (uint32_t)((((lower + g.Rrest - 1) << g.pb) | pbmask) >> g.bsh);
-          if (b_hi >= blo && b_lo < bhi) {
-            kk[k] = key_from(c, off, g.R, g.q, g.pb, g.ck, g.Rck, g.Rlast, g.ck + 1, cv0);
-            const uint32_t bk = (uint32_t)(kk[k] >> g.bsh);
-            if (bk >= blo && bk < bhi) sel |= 1u << k;
-          }
-        } else {
-          kk[k] = key_chunked(c, off, g.R, g.q, g.pb, g.ck, g.Rck, g.Rlast);
-          const uint32_t bk = (uint32_t)(kk[k] >> g.bsh);
-          if (bk >= blo && bk < bhi) sel |= 1u << k;
-        }
-      }
-    }
+  const uint64_t tiles = (n + PS_TILE - 1) / PS_TILE;
+  const uint64_t t0 = (uint64_t)blockIdx.x * tpb;
+  const uint64_t t1 = t0 + tpb < tiles ? t0 + tpb : tiles;
+  uint64_t run = block_off[blockIdx.x];
+  for (uint64_t ti = t0; ti < t1; ++ti) {
+    const uint64_t base = ti * PS_TILE;
+    uint32_t sel = select16(t, n, base + 16 * threadIdx.x, L, g, sg, blo, bhi);
     const uint32_t cnt = __popc(sel);
     const uint32_t inc = wave_incl_sum<uint32_t>(cnt);
     if (lane == 63) red[w] = inc;
-    __syncthreads();
-    uint32_t carry = 0, tot = 0;
+    const uint32_t any = __syncthreads_or(sel != 0);
+    if (!any) continue;   // block-uniform: nothing of this tile is ours
+    uint32_t o = inc - cnt;
+    uint32_t tot = 0;
+#pragma unroll
     for (int i = 0; i < 4; ++i) {
-      if (i < w) carry += red[i];
+      if (i < w) o += red[i];
       tot += red[i];
     }
-    if (threadIdx.x == 0) gbase = tot ? atomicAdd(counter, (unsigned long long)tot) : 0ull;
+    while (sel) {
+      const int k = __ffs(sel) - 1;
+      sel &= sel - 1;
+      list[o++] = (uint16_t)(16 * threadIdx.x + k);
+    }
+    stage_text_codes<PS_TILE, 256>(c, L, t, n, base);
     __syncthreads();
-    uint64_t o = gbase + carry + inc - cnt;
-#pragma unroll
-    for (int k = 0; k < PS_TILE / 256; ++k)
-      if (sel & (1u << k)) {
-        keys[o] = kk[k];
-        vals[o] = (V)(base + k * 256 + threadIdx.x);
-        ++o;
-      }
-    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < tot; i += 256) {
+      const int off = list[i];
+      keys[run + i] = key_chunked(c, off, g.R, g.q, g.pb, g.ck, g.Rck, g.Rlast);
+      vals[run + i] = (V)(base + off);
+    }
+    run += tot;
+    __syncthreads();   // list / c / red are rewritten by the next tile
   }
 }
 
@@ -149,7 +212,92 @@ int bucket_shift(const KeyGeom& kg) {
 
 BucketGeom bucket_geom(const KeyGeom& kg) {
   const KeyChunks kc = key_chunks(kg.R, kg.q);
-  return BucketGeom{kg.R, kc.Rck, kc.Rlast, kc.Rrest, kg.q, kg.pb, kc.ck, bucket_shift(kg)};
+  return BucketGeom{kg.R, kc.Rck, kc.Rlast, kg.q, kg.pb, kc.ck, bucket_shift(kg)};
+}
+
+// Byte-image thresholds of the pre-test (see k_select_count).  Prefixes of in-text positions have
+// digits 1..R-1 only (0 = past the end), so "P > A" becomes "P >= the smallest zero-free prefix
+// above A" and "P < B" becomes "P <= the largest zero-free prefix below B".
+SelGeom sel_geom(const KeyGeom& kg, const BucketGeom& g, uint32_t blo, uint32_t bhi) {
+  SelGeom sg{};
+  const uint64_t R = kg.R;
+  int h = 1;
+  uint64_t Rh = R;
+  while (Rh < (1ull << 16) && h < 8) {
+    Rh *= R;
+    ++h;
+  }
+  if (g.bsh < g.pb || kg.q <= h || bhi <= blo) {
+    sg.flags = SEL_NOPRE;
+    sg.h = 0;
+    sg.topmask = 0;
+    return sg;
+  }
+  unsigned __int128 W = 1;
+  for (int i = h; i < kg.q; ++i) W *= R;
+  const unsigned __int128 Mlo = ((unsigned __int128)blo << g.bsh) >> g.pb;
+  const unsigned __int128 Mhi = ((unsigned __int128)bhi << g.bsh) >> g.pb;
+  const unsigned __int128 A = Mlo / W, B = (Mhi - 1) / W;
+  auto digits = [&](uint64_t P, int* d) {
+    for (int i = h - 1; i >= 0; --i) { d[i] = (int)(P % R); P /= R; }
+  };
+  auto zero_free = [&](uint64_t P) {
+    int d[8];
+    digits(P, d);
+    for (int i = 0; i < h; ++i) if (!d[i]) return false;
+    return true;
+  };
+  auto bytes_of = [&](uint64_t P) {   // big-endian byte image, top-aligned in 64 bits
+    int d[8];
+    digits(P, d);
+    uint64_t v = 0;
+    for (int i = 0; i < h; ++i) v = (v << 8) | kg.inv[d[i]];
+    return v << (8 * (8 - h));
+  };
+  // smallest zero-free value >= P (or Rh when none)
+  auto up0 = [&](uint64_t P) -> uint64_t {
+    while (P < Rh && !zero_free(P)) {
+      int d[8];
+      digits(P, d);
+      int i = 0;
+      while (d[i]) ++i;                       // most significant zero digit
+      for (int k = i; k < h; ++k) d[k] = 1;   // smallest zero-free completion
+      uint64_t v = 0;
+      for (int k = 0; k < h; ++k) v = v * R + (uint64_t)d[k];
+      P = v;
+    }
+    return P;
+  };
+  // largest zero-free value <= P (or -1 when none)
+  auto down0 = [&](int64_t P) -> int64_t {
+    while (P >= 0 && !zero_free((uint64_t)P)) {
+      int d[8];
+      digits((uint64_t)P, d);
+      int i = 0;
+      while (d[i]) ++i;
+      uint64_t pre = 0;
+      for (int k = 0; k < i; ++k) pre = pre * R + (uint64_t)d[k];
+      uint64_t scale = 1;
+      for (int k = i; k < h; ++k) scale *= R;
+      P = (int64_t)(pre * scale) - 1;          // borrow: digits i.. become R-1
+    }
+    return P;
+  };
+  sg.h = h;
+  sg.topmask = ~0ull << (8 * (8 - h));
+  const uint64_t a = A < Rh ? (uint64_t)A : Rh;
+  const uint64_t bb = B < Rh ? (uint64_t)B : Rh;
+  const uint64_t lo = up0(a < Rh ? a + 1 : Rh);
+  const int64_t hi = down0((int64_t)(bb < Rh ? bb : Rh) - 1);
+  if (lo >= Rh || hi < 0 || (int64_t)lo > hi) {
+    sg.flags |= SEL_EMPTY;
+  } else {
+    sg.TL = bytes_of(lo);
+    sg.TH = bytes_of((uint64_t)hi);
+  }
+  if (a < Rh && zero_free(a)) { sg.flags |= SEL_HAS_A; sg.TA = bytes_of(a); }
+  if (bb < Rh && zero_free(bb)) { sg.flags |= SEL_HAS_B; sg.TB = bytes_of(bb); }
+  return sg;
 }
 
 template <typename V>
@@ -187,22 +335,35 @@ void shard_build_t(Index& ix, const uint64_t* ghist, int nranks, int rank) {
     return;
   }
   upload_geometry(ix, kg);
-  ix.small.ensure(8192);
-  unsigned long long* d_counter = ix.small.as<unsigned long long>() + 448;
-  HK_HIP(hipMemsetAsync(d_counter, 0, 8, s));
+  uint64_t got = 0;
   for (int i = 0; i < 2; ++i) {
     ix.keys[i].ensure(m * 8 + 16);
     ix.vals[i].ensure(m * sizeof(V) + 16);
   }
   {
-    TimedLaunch t(ix.timer, "shard_pack_select", (double)n + (double)m * (8 + sizeof(V)));
-    k_pack_select<V><<<grid_for(n, PS_TILE, 8192), 256, 0, s>>>(
-        ix.text.as<uint8_t>(), n, reinterpret_cast<const uint16_t*>(ix.small.as<uint8_t>() + 2048),
-        bucket_geom(kg), blo, bhi, ix.keys[0].as<uint64_t>(), ix.vals[0].as<V>(), d_counter);
-    HK_HIP(hipGetLastError());
+    const uint64_t tiles = ceil_div(n, (uint64_t)PS_TILE);
+    const uint64_t G = tiles < 8192 ? tiles : 8192;
+    const uint64_t tpb = ceil_div(tiles, G);
+    const unsigned grid = (unsigned)ceil_div(tiles, tpb);
+    ix.tile_d.ensure((grid + 1) * 8);
+    uint64_t* bc = ix.tile_d.as<uint64_t>();
+    const uint16_t* lut = reinterpret_cast<const uint16_t*>(ix.small.as<uint8_t>() + 2048);
+    const BucketGeom bg = bucket_geom(kg);
+    const SelGeom sg = sel_geom(kg, bg, blo, bhi);
+    {
+      TimedLaunch t(ix.timer, "shard_select_count", (double)n);
+      k_select_count<<<grid, 256, 0, s>>>(ix.text.as<uint8_t>(), n, tpb, lut, bg, sg, blo, bhi, bc);
+      HK_HIP(hipGetLastError());
+    }
+    scan_exclusive_u64(ix.sw, bc, bc, grid, true, s);
+    {
+      TimedLaunch t(ix.timer, "shard_pack_select", (double)n + (double)m * (8 + sizeof(V)));
+      k_select_write<V><<<grid, 256, 0, s>>>(ix.text.as<uint8_t>(), n, tpb, lut, bg, sg, blo, bhi, bc,
+                                             ix.keys[0].as<uint64_t>(), ix.vals[0].as<V>());
+      HK_HIP(hipGetLastError());
+    }
+    HK_HIP(hipMemcpyAsync(&got, bc + grid, 8, hipMemcpyDeviceToHost, s));
   }
-  uint64_t got = 0;
-  HK_HIP(hipMemcpyAsync(&got, d_counter, 8, hipMemcpyDeviceToHost, s));
   HK_HIP(hipStreamSynchronize(s));
   if (got != m) throw ApiError{-7, "shard selection count mismatch"};
   uint64_t* kp[2] = {ix.keys[0].as<uint64_t>(), ix.keys[1].as<uint64_t>()};

@@ -212,10 +212,13 @@ def test_full_size_config1_256MiB(hk):
     dev.close()
 
 
-@pytest.mark.parametrize("nranks,flags", [(2, 0), (3, 0), (2, 1), (4, 1)])
-def test_shard_two_phase_emulated(hk, nranks, flags):
-    """Ranks emulated on one GPU; flags=1 forces the 64-bit position kernels (n >= 2^32 path)."""
-    text = oracle.synth_text(400001, b"ACGT", seed=12 + nranks)
+@pytest.mark.parametrize("nranks,flags,alpha", [(2, 0, b"ACGT"), (3, 0, b"ACGT"), (2, 1, b"ACGT"), (4, 1, b"ACGT"),
+                                               (5, 0, bytes(range(256))), (3, 0, b"ab"), (7, 0, b"AC$GT"),
+                                               (6, 1, bytes(range(0x20, 0x7F)))])
+def test_shard_two_phase_emulated(hk, nranks, flags, alpha):
+    """Ranks emulated on one GPU; flags=1 forces the 64-bit position kernels (n >= 2^32 path).
+    Alphabets cover the byte-image pre-test thresholds for radix 3 .. 257."""
+    text = oracle.synth_text(400001, alpha, seed=12 + nranks)
     ref = oracle.suffix_array(text)
     ref_bwt = oracle.bwt(text, ref)
     devs = [hk.DeviceIndex.from_bytes(text, device=0, flags=flags) for _ in range(nranks)]

@@ -17,7 +17,7 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)),
                                 "high-order-entropy-compressed-suffix-array_amd"))
 from hkcsa import DeviceIndex  # noqa: E402
 
-STAGES = ["shard_hist", "shard_pack_select", "radix_hist", "radix_onesweep", "radix_onesweep_small",
+STAGES = ["shard_hist", "shard_select_count", "shard_pack_select", "radix_hist", "radix_onesweep", "radix_onesweep_small",
           "sa_refine_stats", "sa_refine_apply", "sa_refine_keys"]
 
 
