@@ -9,6 +9,7 @@ namespace hk {
 
 constexpr int kMaxLevels = 8;
 constexpr uint32_t kFlagPos64 = 1u;   // hkcsa_opts.flags: 64-bit positions in sharded builds at any n
+constexpr uint32_t kFlagNoSplit = 2u; // ... and sort them as whole u64 values (no split low/high halves)
 constexpr int kLineBits = 448;   // 7 data words per 64-B rank line (word 0 = ones before the line)
 
 struct WtTables {                // per level, per dense code (host mirror of the device tables)
@@ -124,6 +125,9 @@ void sampled_locate_gather(Index& ix, const int64_t* d_lr, const uint64_t* d_occ
 void sampled_sa_range(Index& ix, uint64_t lo, uint64_t count, uint64_t* d_out);
 void wt_bwt_range(Index& ix, uint64_t lo, uint64_t count, uint8_t* d_out);
 void sampled_extract(Index& ix, uint64_t i, uint64_t j, uint8_t* d_out);
+
+// empirical k-th order entropy of T' (csa/high_order_entropy.py:4-32) from SA runs
+double entropy_k(Index& ix, int k);
 
 // Golomb-Rice code of the first nbits bits of a level (csa/wavelet_tree.py:27-63); with write,
 // the code words are left in ix.gr_out

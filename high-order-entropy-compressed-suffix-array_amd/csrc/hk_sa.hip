@@ -578,7 +578,7 @@ int mixed_radix_bits(uint64_t R, int q) {
   return b;
 }
 
-// Symbols per key: minimise (radix passes) * n + 10 * (expected tied suffixes), the latter from the
+// Symbols per key: minimise (radix passes) * n + 30 * (expected tied suffixes), the latter from the
 // iid collision rate sum(p_c^2)^q of the symbol histogram (ties are refined, not wrong — this only
 // decides speed; texts with repeats tie more, refinement/doubling absorb that).
 KeyGeom key_geometry(Index& ix, bool with_prev) {
@@ -596,7 +596,7 @@ KeyGeom key_geometry(Index& ix, bool with_prev) {
     const int sb = mixed_radix_bits(g.R, q);
     if (g.pb + sb > 64) break;
     const double ties = std::min(n, n * n * std::pow(p2, (double)q));
-    const double cost = (double)((sb + 7) / 8) * n + 10.0 * ties;
+    const double cost = (double)((sb + 7) / 8) * n + 30.0 * ties;   // a tie costs ~30 element-passes (measured)
     if (cost <= best) {
       best = cost;
       g.q = q;

@@ -147,12 +147,14 @@ __global__ __launch_bounds__(256) void k_select_count(const uint8_t* __restrict_
   if (threadIdx.x == 0) block_cnt[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
 }
 
+// V = u32 with hb > 0: split positions — the low 32 bits go to vals, the high hb bits below the
+// key (key << hb | pos >> 32), outside the sorted bit range; k_split_join reassembles them.
 template <typename V>
 __global__ __launch_bounds__(256) void k_select_write(const uint8_t* __restrict__ t, uint64_t n, uint64_t tpb,
                                                       const uint16_t* __restrict__ lut, BucketGeom g, SelGeom sg,
                                                       uint32_t blo, uint32_t bhi,
                                                       const uint64_t* __restrict__ block_off,
-                                                      uint64_t* __restrict__ keys, V* __restrict__ vals) {
+                                                      uint64_t* __restrict__ keys, V* __restrict__ vals, int hb) {
   __shared__ uint16_t c[PS_TILE + kCodePad];
   __shared__ uint16_t list[PS_TILE];
   __shared__ uint16_t L[256];
@@ -188,11 +190,23 @@ __global__ __launch_bounds__(256) void k_select_write(const uint8_t* __restrict_
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < tot; i += 256) {
       const int off = list[i];
-      keys[run + i] = key_chunked(c, off, g.R, g.q, g.pb, g.ck, g.Rck, g.Rlast);
-      vals[run + i] = (V)(base + off);
+      const uint64_t p = base + off;
+      const uint64_t key = key_chunked(c, off, g.R, g.q, g.pb, g.ck, g.Rck, g.Rlast);
+      keys[run + i] = hb ? (key << hb) | (p >> 32) : key;
+      vals[run + i] = (V)p;
     }
     run += tot;
     __syncthreads();   // list / c / red are rewritten by the next tile
+  }
+}
+
+__global__ __launch_bounds__(256) void k_split_join(uint64_t* __restrict__ keys, const uint32_t* __restrict__ lo32,
+                                                    uint64_t m, int hb, uint64_t* __restrict__ sa) {
+  const uint64_t mask = (1ull << hb) - 1;
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < m; i += (uint64_t)gridDim.x * 256) {
+    const uint64_t k = keys[i];
+    sa[i] = ((k & mask) << 32) | lo32[i];
+    keys[i] = k >> hb;
   }
 }
 
@@ -335,6 +349,14 @@ void shard_build_t(Index& ix, const uint64_t* ghist, int nranks, int rank) {
     return;
   }
   upload_geometry(ix, kg);
+  // 64-bit positions: sort u32 low halves with the high bits parked below the key (24 instead of
+  // 32 bytes per pair and pass) when they fit in the 64-bit key
+  int hb = 0;
+  if (sizeof(V) == 8 && !(ix.flags & kFlagNoSplit)) {
+    hb = 1;
+    while (((n - 1) >> 32) >> hb) ++hb;
+    if (kg.key_bits + hb > 64) hb = 0;
+  }
   uint64_t got = 0;
   for (int i = 0; i < 2; ++i) {
     ix.keys[i].ensure(m * 8 + 16);
@@ -358,8 +380,12 @@ void shard_build_t(Index& ix, const uint64_t* ghist, int nranks, int rank) {
     scan_exclusive_u64(ix.sw, bc, bc, grid, true, s);
     {
       TimedLaunch t(ix.timer, "shard_pack_select", (double)n + (double)m * (8 + sizeof(V)));
-      k_select_write<V><<<grid, 256, 0, s>>>(ix.text.as<uint8_t>(), n, tpb, lut, bg, sg, blo, bhi, bc,
-                                             ix.keys[0].as<uint64_t>(), ix.vals[0].as<V>());
+      if (hb)
+        k_select_write<uint32_t><<<grid, 256, 0, s>>>(ix.text.as<uint8_t>(), n, tpb, lut, bg, sg, blo, bhi, bc,
+                                                      ix.keys[0].as<uint64_t>(), ix.vals[0].as<uint32_t>(), hb);
+      else
+        k_select_write<V><<<grid, 256, 0, s>>>(ix.text.as<uint8_t>(), n, tpb, lut, bg, sg, blo, bhi, bc,
+                                               ix.keys[0].as<uint64_t>(), ix.vals[0].as<V>(), 0);
       HK_HIP(hipGetLastError());
     }
     HK_HIP(hipMemcpyAsync(&got, bc + grid, 8, hipMemcpyDeviceToHost, s));
@@ -367,12 +393,21 @@ void shard_build_t(Index& ix, const uint64_t* ghist, int nranks, int rank) {
   HK_HIP(hipStreamSynchronize(s));
   if (got != m) throw ApiError{-7, "shard selection count mismatch"};
   uint64_t* kp[2] = {ix.keys[0].as<uint64_t>(), ix.keys[1].as<uint64_t>()};
-  V* vp[2] = {ix.vals[0].as<V>(), ix.vals[1].as<V>()};
-  const int slot = radix_sort_pairs<V>(ix.sw, ix.timer, kp, vp, 0, m, kg.pb, kg.key_bits, false, s);
+  int slot;
+  if (hb) {
+    uint32_t* vq[2] = {ix.vals[0].as<uint32_t>(), ix.vals[1].as<uint32_t>()};
+    slot = radix_sort_pairs<uint32_t>(ix.sw, ix.timer, kp, vq, 0, m, kg.pb + hb, kg.key_bits + hb, false, s);
+    TimedLaunch t(ix.timer, "shard_split_join", (double)m * (8 + 4 + 8 + 8));
+    k_split_join<<<grid_for(m, 256, 16384), 256, 0, s>>>(kp[slot], vq[slot], m, hb, ix.sa.as<uint64_t>());
+    HK_HIP(hipGetLastError());
+  } else {
+    V* vp[2] = {ix.vals[0].as<V>(), ix.vals[1].as<V>()};
+    slot = radix_sort_pairs<V>(ix.sw, ix.timer, kp, vp, 0, m, kg.pb, kg.key_bits, false, s);
+    std::swap(ix.sa, ix.vals[slot]);
+    ix.vals[slot].ensure(m * sizeof(V) + 16);
+  }
   ix.info[0] += ix.sw.passes_run;
   ix.info[1] += ix.sw.passes_skipped;
-  std::swap(ix.sa, ix.vals[slot]);
-  ix.vals[slot].ensure(m * sizeof(V) + 16);
   refine_after_sort<V>(ix, kg, slot, m, false);
   HK_HIP(hipStreamSynchronize(s));
   ix.have_sa = true;

@@ -175,6 +175,14 @@ int hkcsa_build_samples(hkcsa_index* h, uint32_t rate) {
   });
 }
 
+int hkcsa_entropy(hkcsa_index* h, int k, double* out) {
+  return guarded([&] {
+    activate(h);
+    need(out != nullptr, HKCSA_E_INVALID, "null output");
+    *out = hk::entropy_k(h->ix, k);
+  });
+}
+
 int hkcsa_compact(hkcsa_index* h) {
   return guarded([&] {
     activate(h);

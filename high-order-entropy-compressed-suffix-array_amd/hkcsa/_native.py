@@ -69,6 +69,7 @@ _SIGS = [
     ("hkcsa_shard_range", C.c_int, [vp, u64p, u64p]),
     ("hkcsa_build_samples", C.c_int, [vp, C.c_uint32]),
     ("hkcsa_compact", C.c_int, [vp]),
+    ("hkcsa_entropy", C.c_int, [vp, C.c_int, C.POINTER(C.c_double)]),
     ("hkcsa_space", C.c_int, [vp, vp]),
     ("hkcsa_wt_golomb", C.c_int, [vp, C.c_int, C.c_uint64, C.c_uint32, C.POINTER(C.c_uint32), u64p, u64p, vp,
                                   C.c_uint64]),

@@ -150,6 +150,12 @@ class DeviceIndex:
         """Drop SA, BWT array, text and workspace; queries continue from the WT + samples."""
         N.check(self.lib.hkcsa_compact(self.h))
 
+    def entropy(self, k: int) -> float:
+        """Empirical H_k of the stored buffer (hkcsa_entropy)."""
+        out = C.c_double(0)
+        N.check(self.lib.hkcsa_entropy(self.h, int(k), C.byref(out)))
+        return out.value
+
     def space(self) -> dict:
         out = np.zeros(8, dtype=np.uint64)
         N.check(self.lib.hkcsa_space(self.h, _ptr(out)))

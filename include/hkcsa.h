@@ -44,7 +44,9 @@ extern "C" {
 typedef struct hkcsa_index hkcsa_index;
 typedef struct hkcsa_queries hkcsa_queries;
 
-#define HKCSA_FLAG_POS64 1u  /* sharded builds keep 64-bit positions at any n */
+#define HKCSA_FLAG_POS64 1u    /* sharded builds keep 64-bit positions at any n             */
+#define HKCSA_FLAG_NO_SPLIT 2u /* sort 64-bit positions whole (default: u32 low halves, the  */
+                               /* high bits parked below the key)                           */
 
 typedef struct hkcsa_opts {
   int32_t device;   /* HIP device ordinal (-1 = current)                 */
@@ -91,6 +93,12 @@ int hkcsa_build_samples(hkcsa_index* ix, uint32_t rate);
  * BWT bytes and text/extract are answered by LF walks over the WT to the samples — results
  * identical to the full arrays; construction calls fail with HKCSA_E_STATE. */
 int hkcsa_compact(hkcsa_index* ix);
+/* Empirical k-th order entropy of the whole buffer T (csa/high_order_entropy.py:4-32,
+ * calculate_high_order_entropy): H_0 for k = 0; for k > 0 the sum over length-k contexts w of
+ * (n_w / n) * H_0(symbols following w) over positions i < n - k; 0 when n <= k or k < 0.
+ * Builds the SA if missing (contexts are SA runs).  Double precision; the reference's
+ * summation order differs, so agreement is to rounding (relative 1e-9 in the tests). */
+int hkcsa_entropy(hkcsa_index* ix, int k, double* out);
 /* Resident bytes: out[0] text, [1] SA, [2] BWT array, [3] WT rank lines, [4] sample marks,
  * [5] SA/ISA samples + LF fixes, [6] sample rate, [7] 1 if samples are built. */
 int hkcsa_space(hkcsa_index* ix, uint64_t out[8]);

@@ -233,7 +233,7 @@ int oracle_wt_levels(const uint8_t* seq, uint64_t n, uint8_t* bits /* 8*n */) {
  * Host restatement of the sharded build's partition (hk_sa.hip key_geometry, hk_shard.hip):
  * the key of suffix p is its first q dense codes (code 0 past the end) as one radix-R number,
  * R = sigma + 1, shifted above the pb-bit code of T[p-1] (T[n-1] for p = 0).  q minimises
- * passes * n + 10 * min(n, n^2 * sum(p_c^2)^q).  The bucket is the top 14 bits of the key. */
+ * passes * n + 30 * min(n, n^2 * sum(p_c^2)^q).  The bucket is the top 14 bits of the key. */
 static int mixed_radix_bits(uint64_t R, int q) {
   unsigned __int128 p = 1;
   for (int i = 0; i < q; ++i) {
@@ -267,7 +267,7 @@ int oracle_key_geometry(const uint8_t* t, uint64_t n, int* q_out, int* pb_out, u
     if (pb + sb > 64) break;
     double ties = nn * nn * pow(p2, (double)q);
     if (ties > nn) ties = nn;
-    const double cost = (double)((sb + 7) / 8) * nn + 10.0 * ties;
+    const double cost = (double)((sb + 7) / 8) * nn + 30.0 * ties;
     if (cost <= best) {
       best = cost;
       bq = q;

@@ -152,6 +152,36 @@ def golomb(bits, m: int | None = None) -> tuple[int, np.ndarray]:
     return m, out[:nb]
 
 
+def entropy(t, k: int) -> float:
+    """Empirical H_k (csa/high_order_entropy.py:4-32) by numpy k-mer counting: (k+1)-grams packed
+    base sigma into int64 (needs (k+1)·log2(sigma) < 63), counted with np.unique."""
+    import math
+    t = _u8(t)
+    n = len(t)
+    if n == 0 or k < 0:
+        return 0.0
+    syms, codes = np.unique(t, return_inverse=True)
+    if k == 0:
+        c = np.bincount(codes).astype(np.float64)
+        p = c / n
+        return float(-(p * np.log2(p)).sum())
+    if n <= k:
+        return 0.0
+    sig = max(2, len(syms))
+    if (k + 1) * math.log2(sig) >= 62:
+        raise ValueError("context too long for the packed oracle")
+    m = n - k
+    ctx = np.zeros(m, dtype=np.int64)
+    for j in range(k):
+        ctx = ctx * sig + codes[j:j + m]
+    pair = ctx * sig + codes[k:k + m]
+    _, cw = np.unique(ctx, return_counts=True)
+    _, cp = np.unique(pair, return_counts=True)
+    cw = cw.astype(np.float64)
+    cp = cp.astype(np.float64)
+    return float(((cw * np.log2(cw)).sum() - (cp * np.log2(cp)).sum()) / n)
+
+
 class FM:
     """Backward search over T' with the oracle's occ table (csa/enhanced_fm_index.py)."""
 

@@ -106,6 +106,28 @@ def test_csa_surface():
     assert csa.locate_many(["ssi"]) == [csa.locate("ssi")]
     for i, j in [(0, 5), (3, 3), (-4, None), (10, 2), (0, 10 ** 9), (-10 ** 9, 4)]:
         assert csa.extract(i, j) == text[i:j]
+    # epsilon=0.5 compacts: SA, BWT array and text left HBM; answers come from LF walks
+    sp = csa.space()
+    assert sp["sa"] == 0 and sp["text"] == 0 and sp["sampled"] == 1 and sp["sample_rate"] == csa.sample_rate
+    assert csa.suffix_array == port.suffix_array and csa.bwt == port.bwt
+    full = CompressedSuffixArray(text, epsilon=0.5, compact=False)
+    assert full.space()["sa"] > 0 and full.locate("ssi") == csa.locate("ssi")
+    for eps in (0, 1.0):
+        c = CompressedSuffixArray(text, epsilon=eps)
+        assert c.locate("issi") == port.find("issi")
+
+
+def test_high_order_entropy_dropin(kat, random_cases):
+    from csa.high_order_entropy import calculate_high_order_entropy as hk
+    demo = "this is an example text"
+    for k, v in enumerate(kat["entropy_demo"]):
+        assert hk(demo, k) == pytest.approx(v, rel=1e-9, abs=1e-12)
+    assert hk("", 2) == 0 and hk("abc", -1) == 0 and hk("ab", 2) == 0 and hk("ab", 5) == 0
+    for name in random_cases.names[::7]:
+        c = random_cases.get(name)
+        t = c["text"].tobytes().decode("latin-1")
+        for k in range(4):
+            assert hk(t, k) == pytest.approx(float(c["entropy"][k]), rel=1e-9, abs=1e-12), (name, k)
 
 
 def test_unicode_text_remap():

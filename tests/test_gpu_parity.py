@@ -213,10 +213,12 @@ def test_full_size_config1_256MiB(hk):
 
 
 @pytest.mark.parametrize("nranks,flags,alpha", [(2, 0, b"ACGT"), (3, 0, b"ACGT"), (2, 1, b"ACGT"), (4, 1, b"ACGT"),
-                                               (5, 0, bytes(range(256))), (3, 0, b"ab"), (7, 0, b"AC$GT"),
-                                               (6, 1, bytes(range(0x20, 0x7F)))])
+                                               (4, 3, b"ACGT"), (5, 0, bytes(range(256))), (3, 0, b"ab"),
+                                               (7, 0, b"AC$GT"), (6, 1, bytes(range(0x20, 0x7F))),
+                                               (3, 3, bytes(range(256)))])
 def test_shard_two_phase_emulated(hk, nranks, flags, alpha):
-    """Ranks emulated on one GPU; flags=1 forces the 64-bit position kernels (n >= 2^32 path).
+    """Ranks emulated on one GPU; flags=1 forces the 64-bit position kernels (n >= 2^32 path: split
+    u32 sort values), flags=3 the whole-u64 value sort.
     Alphabets cover the byte-image pre-test thresholds for radix 3 .. 257."""
     text = oracle.synth_text(400001, alpha, seed=12 + nranks)
     ref = oracle.suffix_array(text)
@@ -238,7 +240,7 @@ def test_shard_two_phase_emulated(hk, nranks, flags, alpha):
     assert np.array_equal(np.concatenate(parts), ref)
 
 
-@pytest.mark.parametrize("flags", [0, 1])
+@pytest.mark.parametrize("flags", [0, 1, 3])
 def test_shard_rccl_single_rank(hk, flags):
     text = oracle.synth_text(200001, bytes(range(0x20, 0x7F)), seed=13)
     dev = hk.DeviceIndex.from_bytes(text, device=0, flags=flags)
@@ -315,4 +317,41 @@ def test_compact_needs_samples(hk):
     dev = _build(hk, b"banana$")
     with pytest.raises(hk.HkcsaError):
         dev.compact()
+    dev.close()
+
+
+def test_entropy_golden(hk, random_cases):
+    """hkcsa_entropy against calculate_high_order_entropy's own outputs (golden), k = 0..3."""
+    for name in random_cases.names:
+        c = random_cases.get(name)
+        t = c["text"]
+        if len(t) == 0:
+            continue
+        dev = hk.DeviceIndex.from_bytes(t.tobytes(), device=0)
+        for k in range(4):
+            assert dev.entropy(k) == pytest.approx(float(c["entropy"][k]), rel=1e-9, abs=1e-12), (name, k)
+        dev.close()
+
+
+@pytest.mark.parametrize("name,text,ks", [
+    ("dna_4M", oracle.synth_text(1 << 22, b"ACGT", seed=51), [1, 2, 5, 8, 13]),
+    ("bytes_1M", oracle.synth_text(1 << 20, bytes(range(256)), seed=52), [1, 2, 3]),
+    ("binary_1M", oracle.synth_text(1 << 20, b"ab", seed=53), [1, 7, 20, 40]),
+    ("periodic", np.frombuffer(b"abcab" * 20000, dtype=np.uint8), [1, 3, 6]),
+    ("run", np.frombuffer(b"a" * 5000, dtype=np.uint8), [0, 1, 4]),
+])
+def test_entropy_vs_oracle(hk, name, text, ks):
+    dev = hk.DeviceIndex.from_bytes(text.tobytes(), device=0)
+    for k in [0] + ks:
+        assert dev.entropy(k) == pytest.approx(oracle.entropy(text, k), rel=1e-9, abs=1e-12), (name, k)
+    assert dev.entropy(-1) == 0.0 and dev.entropy(len(text)) == 0.0
+    dev.close()
+
+
+def test_entropy_64MiB(hk):
+    n = 1 << 26
+    dev = hk.DeviceIndex.synthetic(n, b"ACGT", seed=54, terminator=ord("A"))
+    text = oracle.synth_text(n, b"ACGT", seed=54, terminator=ord("A"))
+    for k in (2, 6):
+        assert dev.entropy(k) == pytest.approx(oracle.entropy(text, k), rel=1e-9), k
     dev.close()

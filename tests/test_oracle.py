@@ -130,6 +130,17 @@ def test_golomb_c_oracle_vs_port():
             assert mm == (m_ref if m is None else m)
 
 
+def test_entropy_numpy_oracle(random_cases, kat):
+    for name in random_cases.names:
+        c = random_cases.get(name)
+        t = c["text"]
+        for k in range(4):
+            assert oracle.entropy(t, k) == pytest.approx(float(c["entropy"][k]), rel=1e-9, abs=1e-12), (name, k)
+    demo = b"this is an example text"
+    for kk, v in enumerate(kat["entropy_demo"]):
+        assert oracle.entropy(demo, kk) == pytest.approx(v, rel=1e-9, abs=1e-12)
+
+
 def test_random_cases_entropy(random_cases):
     for name in random_cases.names[:40]:
         c = random_cases.get(name)
