@@ -202,8 +202,9 @@ def run_single(args) -> dict:
         "vs_baseline": None,
         "dtype": "u8",
         "data": "synthetic",
-        "config": {"workload": "1 GiB synthetic sigma=4 text: HIP prefix-doubling SA + BWT gather "
-                               "(configs[1] pipeline at the metric's 1 GiB), then WT + 1M batched "
+        "config": {"workload": "1 GiB synthetic sigma=4 text: SA by HIP LSD radix sort of mixed-radix "
+                               "suffix keys + tie refinement, BWT from the sorted keys (configs[1] "
+                               "pipeline at the metric's 1 GiB), then WT + 1M batched "
                                f"{args.plen}-symbol locate()",
                    "text_symbols": n, "sigma": 4, "positions": "u32"},
         "roofline": roof,
@@ -275,7 +276,17 @@ def run_sharded(args, rank: int, world: int, local_rank: int) -> dict | None:
     return res
 
 
+def _stdout_for_result():
+    """Route fd 1 to stderr for the run (RCCL / gloo print banners on stdout) and return a
+    stream on the original stdout, so the result stays the only line there."""
+    sys.stdout.flush()
+    saved = os.dup(1)
+    os.dup2(2, 1)
+    return os.fdopen(saved, "w")
+
+
 def main():
+    result_out = _stdout_for_result()
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
@@ -316,7 +327,7 @@ def main():
     if res is not None:
         if "cpu_baseline" not in res:
             res["cpu_baseline"] = None
-        print(json.dumps(res), flush=True)
+        print(json.dumps(res), file=result_out, flush=True)
 
 
 if __name__ == "__main__":

@@ -141,7 +141,9 @@ GolombResult wt_golomb(Index& ix, int depth, uint64_t nbits, uint32_t m_override
 // sharded SA (RCCL)
 int shard_buckets();
 void shard_histogram(Index& ix, int nranks, int rank, uint64_t* d_hist);
-void shard_build(Index& ix, const uint64_t* h_global_hist, int nranks, int rank);
+void shard_counts(Index& ix, const uint64_t* h_global_hist, int nranks, int rank, uint64_t* d_below);
+void shard_build(Index& ix, const uint64_t* h_global_hist, const uint64_t* h_global_below, int nranks, int rank);
+int shard_sample();
 void shard_get_sa(Index& ix, uint64_t a, uint64_t b, uint64_t* out);
 void shard_get_bwt(Index& ix, uint64_t a, uint64_t b, uint8_t* out);
 void build_sa_sharded(Index& ix, const uint8_t id[128], int nranks, int rank);

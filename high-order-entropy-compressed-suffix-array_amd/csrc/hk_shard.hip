@@ -2,17 +2,20 @@
 //
 // Every rank holds the same T' (≤ 288 GB HBM each makes replication cheap) and owns one
 // contiguous range of the FINAL suffix array:
-//   1. each rank histograms the 14-bit key prefix of its block of positions; one RCCL
-//      all-reduce gives the global histogram, so all ranks derive identical splitters
-//      (bucket ranges) and their slice bounds [lo, hi) without further exchange;
-//   2. each rank scans all of T' and keeps the suffixes whose bucket it owns (pack + select,
-//      reading T' once, writing only its ~n/N pairs);
-//   3. it radix-sorts its slice by the q-symbol key and refines tied groups by sorting on
+//   1. each rank histograms the 14-bit key prefix of every 16th position of its block; one RCCL
+//      all-reduce gives the sampled global histogram, from which all ranks derive the same
+//      splitter buckets B_1 < ... < B_{N-1};
+//   2. each rank counts, over its block, the suffixes below every splitter (a register-only byte
+//      pre-test against the splitters' prefix images); a second all-reduce of N+1 counts gives
+//      the exact slice bounds [lo, hi) of every rank;
+//   3. each rank scans all of T' and keeps the suffixes whose bucket it owns (count + scan +
+//      write, reading T' twice, writing only its ~n/N pairs);
+//   4. it radix-sorts its slice by the q-symbol key and refines tied groups by sorting on
 //      (dense group ordinal, next symbols of the suffix) read straight from the replicated
 //      text — no rank exchange is needed because every comparison stays inside one slice;
-//   4. an RCCL all-gather of the slice bounds merges the per-rank ranges into the global SA
-//      layout (and checks that they tile [0, n)).
-// Positions are 64-bit when n ≥ 2^32 (the 4 GiB + 1 config).
+//   5. an RCCL all-gather of the slice bounds checks that the slices tile [0, n).
+// Positions are 64-bit when n ≥ 2^32 (the 4 GiB + 1 config); they are sorted as u32 low halves
+// with the high bits parked below the key.
 
 #include <rccl/rccl.h>
 
@@ -27,6 +30,7 @@ namespace {
 constexpr int SH_BUCKET_BITS = 14;
 constexpr int SH_BUCKETS = 1 << SH_BUCKET_BITS;
 constexpr int PS_TILE = 4096;
+constexpr int SH_SAMPLE = 16;   // histogram sample stride (splitters need balance, not exact counts)
 
 struct ShardComm {  // one RCCL communicator per process (one process per GPU)
   ncclComm_t comm = nullptr;
@@ -41,30 +45,108 @@ struct BucketGeom {
   int q, pb, ck, bsh;
 };
 
+__device__ __forceinline__ uint64_t key_global(const uint8_t* __restrict__ t, uint64_t n, const uint16_t* L,
+                                               uint64_t p, uint64_t R, int q, int pb) {
+  uint64_t key = 0;
+  for (int j = 0; j < q; ++j) key = key * R + (p + j < n ? L[t[p + j]] : 0u);
+  return (key << pb) | (pb ? L[t[p == 0 ? n - 1 : p - 1]] : 0u);
+}
+
+// sampled histogram: positions p in [lo, hi) with p % SH_SAMPLE == 0
 __global__ __launch_bounds__(256) void k_shard_hist(const uint8_t* __restrict__ t, uint64_t n, uint64_t lo,
                                                     uint64_t hi, const uint16_t* __restrict__ lut, BucketGeom g,
                                                     unsigned long long* __restrict__ hist) {
   __shared__ uint32_t H[SH_BUCKETS];
-  __shared__ uint16_t c[PS_TILE + kCodePad];
   __shared__ uint16_t L[256];
   L[threadIdx.x] = lut[threadIdx.x];
   for (int i = threadIdx.x; i < SH_BUCKETS; i += 256) H[i] = 0;
   __syncthreads();
-  // tiles are aligned to PS_TILE in absolute positions so the staged text loads stay aligned
-  const uint64_t first = lo / PS_TILE * PS_TILE;
-  for (uint64_t base = first + (uint64_t)blockIdx.x * PS_TILE; base < hi; base += (uint64_t)gridDim.x * PS_TILE) {
-    stage_text_codes<PS_TILE, 256>(c, L, t, n, base);
-    __syncthreads();
-    for (int k = 0; k < PS_TILE / 256; ++k) {
-      const int off = k * 256 + threadIdx.x;
-      const uint64_t p = base + off;
-      if (p >= lo && p < hi)
-        atomicAdd(&H[key_chunked(c, off, g.R, g.q, g.pb, g.ck, g.Rck, g.Rlast) >> g.bsh], 1u);
-    }
-    __syncthreads();
-  }
+  const uint64_t j0 = (lo + SH_SAMPLE - 1) / SH_SAMPLE, j1 = (hi + SH_SAMPLE - 1) / SH_SAMPLE;
+  for (uint64_t j = j0 + (uint64_t)blockIdx.x * 256 + threadIdx.x; j < j1; j += (uint64_t)gridDim.x * 256)
+    atomicAdd(&H[key_global(t, n, L, j * SH_SAMPLE, g.R, g.q, g.pb) >> g.bsh], 1u);
+  __syncthreads();
   for (int i = threadIdx.x; i < SH_BUCKETS; i += 256)
     if (H[i]) atomicAdd(&hist[i], (unsigned long long)H[i]);
+}
+
+// Exact slice sizes: below[r] += #{p in [lo, hi) : bucket(p) < B_r} for the splitters.  Same
+// byte pre-test as the selection (see below): with A_r = floor(M_r / W) the prefix holding the
+// splitter, P < A_r is below, P > A_r is not, P == A_r (or a window past the end) takes the
+// full key.  Thresholds are byte images: "below" <=> window <= ID_r.
+struct BelowImg {
+  uint64_t ID, IA;
+  uint32_t flags;   // 1: some prefix is below (ID valid), 2: IA valid
+  uint32_t B;       // splitter bucket
+};
+constexpr int SH_MAX_RANKS = 64;
+
+__global__ __launch_bounds__(256) void k_shard_below(const uint8_t* __restrict__ t, uint64_t n, uint64_t lo,
+                                                     uint64_t hi, const uint16_t* __restrict__ lut, BucketGeom g,
+                                                     int h, uint64_t topmask, int nopre,
+                                                     const BelowImg* __restrict__ img, int nthr,
+                                                     unsigned long long* __restrict__ below) {
+  __shared__ uint16_t L[256];
+  __shared__ BelowImg I[SH_MAX_RANKS];
+  __shared__ uint32_t cnt[SH_MAX_RANKS];
+  L[threadIdx.x] = lut[threadIdx.x];
+  if ((int)threadIdx.x < nthr) {
+    I[threadIdx.x] = img[threadIdx.x];
+    cnt[threadIdx.x] = 0;
+  }
+  __syncthreads();
+  const uint64_t g0 = lo / 16, g1 = (hi + 15) / 16;
+  for (uint64_t gi = g0 + (uint64_t)blockIdx.x * 256 + threadIdx.x; gi < g1; gi += (uint64_t)gridDim.x * 256) {
+    const uint64_t p0 = gi * 16;
+    uint32_t valid = 0xFFFFu;
+    if (p0 < lo) valid &= 0xFFFFu << (lo - p0);
+    if (p0 + 16 > hi) valid &= (1u << (hi - p0)) - 1u;
+    const uint4 a = *reinterpret_cast<const uint4*>(t + p0);
+    const uint4 b = *reinterpret_cast<const uint4*>(t + p0 + 16);
+    const uint32_t w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    uint64_t be[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const int j = k >> 2, sh = k & 3;
+      const uint32_t d0 = __builtin_amdgcn_alignbyte(w[j + 1], w[j], sh);
+      const uint32_t d1 = __builtin_amdgcn_alignbyte(w[j + 2], w[j + 1], sh);
+      be[k] = (((uint64_t)__builtin_bswap32(d0) << 32) | __builtin_bswap32(d1)) & topmask;
+    }
+    uint32_t amb = 0;
+    if (nopre) amb = valid;
+    else if (p0 + 16 + h > n) {
+#pragma unroll
+      for (int k = 0; k < 16; ++k)
+        if (p0 + k + h > n) amb |= 1u << k;
+      amb &= valid;
+    }
+    for (int r = 0; r < nthr; ++r) {   // a position equal to any splitter prefix takes the full key
+      const BelowImg im = I[r];
+      if (!(im.flags & 2u)) continue;
+#pragma unroll
+      for (int k = 0; k < 16; ++k)
+        if (be[k] == im.IA) amb |= 1u << k;
+    }
+    amb &= valid;
+    for (int r = 0; r < nthr; ++r) {
+      const BelowImg im = I[r];
+      if (!(im.flags & 1u)) continue;
+      uint32_t bl = 0;
+#pragma unroll
+      for (int k = 0; k < 16; ++k)
+        if (be[k] <= im.ID) bl |= 1u << k;
+      bl &= valid & ~amb;
+      if (bl) atomicAdd(&cnt[r], (uint32_t)__popc(bl));
+    }
+    while (amb) {   // rare: splitter prefixes and the last h positions
+      const int k = __ffs(amb) - 1;
+      amb &= amb - 1;
+      const uint32_t bk = (uint32_t)(key_global(t, n, L, p0 + k, g.R, g.q, g.pb) >> g.bsh);
+      for (int r = 0; r < nthr; ++r)
+        if (bk < I[r].B) atomicAdd(&cnt[r], 1u);
+    }
+  }
+  __syncthreads();
+  if ((int)threadIdx.x < nthr && cnt[threadIdx.x]) atomicAdd(&below[threadIdx.x], (unsigned long long)cnt[threadIdx.x]);
 }
 
 // Every rank scans all of T' and keeps the suffixes whose bucket lies in [blo, bhi).
@@ -89,12 +171,6 @@ struct SelGeom {
 };
 constexpr uint32_t SEL_NOPRE = 1, SEL_EMPTY = 2, SEL_HAS_A = 4, SEL_HAS_B = 8;
 
-__device__ __forceinline__ uint64_t key_global(const uint8_t* __restrict__ t, uint64_t n, const uint16_t* L,
-                                               uint64_t p, uint64_t R, int q, int pb) {
-  uint64_t key = 0;
-  for (int j = 0; j < q; ++j) key = key * R + (p + j < n ? L[t[p + j]] : 0u);
-  return (key << pb) | (pb ? L[t[p == 0 ? n - 1 : p - 1]] : 0u);
-}
 
 // selection bits of the 16 positions p0 .. p0+15 (bit k: p0 + k)
 __device__ __forceinline__ uint32_t select16(const uint8_t* __restrict__ t, uint64_t n, uint64_t p0,
@@ -229,61 +305,58 @@ BucketGeom bucket_geom(const KeyGeom& kg) {
   return BucketGeom{kg.R, kc.Rck, kc.Rlast, kg.q, kg.pb, kc.ck, bucket_shift(kg)};
 }
 
-// Byte-image thresholds of the pre-test (see k_select_count).  Prefixes of in-text positions have
-// digits 1..R-1 only (0 = past the end), so "P > A" becomes "P >= the smallest zero-free prefix
-// above A" and "P < B" becomes "P <= the largest zero-free prefix below B".
-SelGeom sel_geom(const KeyGeom& kg, const BucketGeom& g, uint32_t blo, uint32_t bhi) {
-  SelGeom sg{};
-  const uint64_t R = kg.R;
-  int h = 1;
-  uint64_t Rh = R;
-  while (Rh < (1ull << 16) && h < 8) {
-    Rh *= R;
-    ++h;
+// Byte images of h-symbol prefixes.  Prefixes of in-text positions have digits 1..R-1 only
+// (0 = past the end), and digit d is byte inv[d], increasing in d — so comparing zero-free
+// prefixes equals comparing their h raw bytes big-endian.
+struct PrefixImages {
+  const KeyGeom& kg;
+  uint64_t R = 2, Rh = 2;
+  int h = 0;
+  bool usable = false;      // false: every position takes the full key
+  unsigned __int128 W = 1;  // R^(q-h)
+  uint64_t topmask = 0;
+
+  PrefixImages(const KeyGeom& k, const BucketGeom& g) : kg(k), R(k.R) {
+    h = 1;
+    Rh = R;
+    while (Rh < (1ull << 16) && h < 8) {
+      Rh *= R;
+      ++h;
+    }
+    usable = g.bsh >= g.pb && kg.q > h;
+    for (int i = h; i < kg.q; ++i) W *= R;
+    topmask = ~0ull << (8 * (8 - h));
   }
-  if (g.bsh < g.pb || kg.q <= h || bhi <= blo) {
-    sg.flags = SEL_NOPRE;
-    sg.h = 0;
-    sg.topmask = 0;
-    return sg;
-  }
-  unsigned __int128 W = 1;
-  for (int i = h; i < kg.q; ++i) W *= R;
-  const unsigned __int128 Mlo = ((unsigned __int128)blo << g.bsh) >> g.pb;
-  const unsigned __int128 Mhi = ((unsigned __int128)bhi << g.bsh) >> g.pb;
-  const unsigned __int128 A = Mlo / W, B = (Mhi - 1) / W;
-  auto digits = [&](uint64_t P, int* d) {
+  void digits(uint64_t P, int* d) const {
     for (int i = h - 1; i >= 0; --i) { d[i] = (int)(P % R); P /= R; }
-  };
-  auto zero_free = [&](uint64_t P) {
+  }
+  bool zero_free(uint64_t P) const {
     int d[8];
     digits(P, d);
     for (int i = 0; i < h; ++i) if (!d[i]) return false;
     return true;
-  };
-  auto bytes_of = [&](uint64_t P) {   // big-endian byte image, top-aligned in 64 bits
+  }
+  uint64_t image(uint64_t P) const {   // big-endian byte image, top-aligned in 64 bits
     int d[8];
     digits(P, d);
     uint64_t v = 0;
     for (int i = 0; i < h; ++i) v = (v << 8) | kg.inv[d[i]];
     return v << (8 * (8 - h));
-  };
-  // smallest zero-free value >= P (or Rh when none)
-  auto up0 = [&](uint64_t P) -> uint64_t {
+  }
+  uint64_t up0(uint64_t P) const {     // smallest zero-free value >= P (Rh when none)
     while (P < Rh && !zero_free(P)) {
       int d[8];
       digits(P, d);
       int i = 0;
-      while (d[i]) ++i;                       // most significant zero digit
-      for (int k = i; k < h; ++k) d[k] = 1;   // smallest zero-free completion
+      while (d[i]) ++i;
+      for (int k = i; k < h; ++k) d[k] = 1;
       uint64_t v = 0;
       for (int k = 0; k < h; ++k) v = v * R + (uint64_t)d[k];
       P = v;
     }
     return P;
-  };
-  // largest zero-free value <= P (or -1 when none)
-  auto down0 = [&](int64_t P) -> int64_t {
+  }
+  int64_t down0(int64_t P) const {     // largest zero-free value <= P (-1 when none)
     while (P >= 0 && !zero_free((uint64_t)P)) {
       int d[8];
       digits((uint64_t)P, d);
@@ -293,50 +366,96 @@ SelGeom sel_geom(const KeyGeom& kg, const BucketGeom& g, uint32_t blo, uint32_t 
       for (int k = 0; k < i; ++k) pre = pre * R + (uint64_t)d[k];
       uint64_t scale = 1;
       for (int k = i; k < h; ++k) scale *= R;
-      P = (int64_t)(pre * scale) - 1;          // borrow: digits i.. become R-1
+      P = (int64_t)(pre * scale) - 1;
     }
     return P;
-  };
-  sg.h = h;
-  sg.topmask = ~0ull << (8 * (8 - h));
-  const uint64_t a = A < Rh ? (uint64_t)A : Rh;
-  const uint64_t bb = B < Rh ? (uint64_t)B : Rh;
-  const uint64_t lo = up0(a < Rh ? a + 1 : Rh);
-  const int64_t hi = down0((int64_t)(bb < Rh ? bb : Rh) - 1);
-  if (lo >= Rh || hi < 0 || (int64_t)lo > hi) {
+  }
+  // the prefix holding mixed value M (clamped to Rh)
+  uint64_t prefix_of(unsigned __int128 M) const {
+    const unsigned __int128 A = M / W;
+    return A < Rh ? (uint64_t)A : Rh;
+  }
+  unsigned __int128 mixed_of_bucket(uint64_t B, int bsh, int pb) const {
+    return ((unsigned __int128)B << bsh) >> pb;
+  }
+};
+
+// Selection of buckets [blo, bhi): accept iff TL <= window <= TH, full key on TA / TB.
+SelGeom sel_geom(const KeyGeom& kg, const BucketGeom& g, uint32_t blo, uint32_t bhi) {
+  SelGeom sg{};
+  const PrefixImages pi(kg, g);
+  if (!pi.usable || bhi <= blo) {
+    sg.flags = SEL_NOPRE;
+    return sg;
+  }
+  const uint64_t a = pi.prefix_of(pi.mixed_of_bucket(blo, g.bsh, g.pb));
+  const uint64_t bb = pi.prefix_of(pi.mixed_of_bucket(bhi, g.bsh, g.pb) - 1);
+  sg.h = pi.h;
+  sg.topmask = pi.topmask;
+  const uint64_t lo = pi.up0(a < pi.Rh ? a + 1 : pi.Rh);
+  const int64_t hi = pi.down0((int64_t)(bb < pi.Rh ? bb : pi.Rh) - 1);
+  if (lo >= pi.Rh || hi < 0 || (int64_t)lo > hi) {
     sg.flags |= SEL_EMPTY;
   } else {
-    sg.TL = bytes_of(lo);
-    sg.TH = bytes_of((uint64_t)hi);
+    sg.TL = pi.image(lo);
+    sg.TH = pi.image((uint64_t)hi);
   }
-  if (a < Rh && zero_free(a)) { sg.flags |= SEL_HAS_A; sg.TA = bytes_of(a); }
-  if (bb < Rh && zero_free(bb)) { sg.flags |= SEL_HAS_B; sg.TB = bytes_of(bb); }
+  if (a < pi.Rh && pi.zero_free(a)) { sg.flags |= SEL_HAS_A; sg.TA = pi.image(a); }
+  if (bb < pi.Rh && pi.zero_free(bb)) { sg.flags |= SEL_HAS_B; sg.TB = pi.image(bb); }
   return sg;
 }
 
+// "bucket < B": P < A below, P == A full key, else not below (A = prefix holding B's first key)
+BelowImg below_img(const PrefixImages& pi, const BucketGeom& g, uint32_t B) {
+  BelowImg im{};
+  im.B = B;
+  if (!pi.usable) return im;
+  const uint64_t a = pi.prefix_of(pi.mixed_of_bucket(B, g.bsh, g.pb));
+  const int64_t d = pi.down0((int64_t)a - 1);
+  if (d >= 0) {
+    im.flags |= 1u;
+    im.ID = pi.image((uint64_t)d);
+  }
+  if (a < pi.Rh && pi.zero_free(a)) {
+    im.flags |= 2u;
+    im.IA = pi.image(a);
+  }
+  return im;
+}
+
+// splitter buckets B_0 = 0 < ... < B_N = SH_BUCKETS from the sampled global histogram
+std::vector<uint32_t> splitters(const uint64_t* ghist, int nranks) {
+  std::vector<uint64_t> cum(SH_BUCKETS + 1, 0);
+  for (int i = 0; i < SH_BUCKETS; ++i) cum[i + 1] = cum[i] + ghist[i];
+  const uint64_t tot = cum[SH_BUCKETS];
+  std::vector<uint32_t> B(nranks + 1);
+  for (int r = 0; r <= nranks; ++r) {
+    if (r == 0) { B[r] = 0; continue; }
+    if (r == nranks) { B[r] = SH_BUCKETS; continue; }
+    const uint64_t target = (uint64_t)((__uint128_t)tot * (uint64_t)r / (uint64_t)nranks);
+    uint32_t lo = 0, hi = SH_BUCKETS;
+    while (lo < hi) {  // smallest B with cum[B] >= target
+      const uint32_t mid = (lo + hi) / 2;
+      if (cum[mid] >= target) hi = mid; else lo = mid + 1;
+    }
+    B[r] = lo;
+  }
+  return B;
+}
+
 template <typename V>
-void shard_build_t(Index& ix, const uint64_t* ghist, int nranks, int rank) {
+void shard_build_t(Index& ix, const uint64_t* ghist, const uint64_t* gbelow, int nranks, int rank) {
   const uint64_t n = ix.n;
   hipStream_t s = ix.stream;
   KeyGeom kg = key_geometry(ix, true);
-  // splitters: rank r owns buckets [B[r], B[r+1]) — the first bucket whose prefix count reaches r*n/N
-  std::vector<uint64_t> cum(SH_BUCKETS + 1, 0);
-  for (int i = 0; i < SH_BUCKETS; ++i) cum[i + 1] = cum[i] + ghist[i];
-  if (cum[SH_BUCKETS] != n) throw ApiError{-7, "global shard histogram does not sum to n"};
-  auto split = [&](int r) -> uint32_t {
-    if (r <= 0) return 0;
-    if (r >= nranks) return SH_BUCKETS;
-    const uint64_t target = (uint64_t)((__uint128_t)n * (uint64_t)r / (uint64_t)nranks);
-    uint32_t lo = 0, hi = SH_BUCKETS;
-    while (lo < hi) {  // smallest B with cum[B] >= target
-      uint32_t mid = (lo + hi) / 2;
-      if (cum[mid] >= target) hi = mid; else lo = mid + 1;
-    }
-    return lo;
-  };
-  const uint32_t blo = split(rank), bhi = split(rank + 1);
-  ix.shard_lo = cum[blo];
-  ix.shard_hi = cum[bhi];
+  // splitters: rank r owns buckets [B[r], B[r+1]); its SA slice is [below(B[r]), below(B[r+1]))
+  const std::vector<uint32_t> B = splitters(ghist, nranks);
+  if (gbelow[0] != 0 || gbelow[nranks] != n) throw ApiError{-7, "global splitter counts do not cover n"};
+  for (int r = 0; r < nranks; ++r)
+    if (gbelow[r] > gbelow[r + 1]) throw ApiError{-7, "global splitter counts are not monotone"};
+  const uint32_t blo = B[rank], bhi = B[rank + 1];
+  ix.shard_lo = gbelow[rank];
+  ix.shard_hi = gbelow[rank + 1];
   const uint64_t m = ix.shard_hi - ix.shard_lo;
   ix.info.assign(4, 0);
   ix.info[3] = (uint64_t)kg.q;
@@ -424,20 +543,49 @@ void shard_histogram(Index& ix, int nranks, int rank, uint64_t* d_hist) {
   upload_geometry(ix, kg);
   HK_HIP(hipMemsetAsync(d_hist, 0, SH_BUCKETS * 8, s));
   if (hi > lo) {
-    TimedLaunch t(ix.timer, "shard_hist", (double)(hi - lo));
-    k_shard_hist<<<grid_for(hi - lo, PS_TILE, 2048), 256, 0, s>>>(
+    TimedLaunch t(ix.timer, "shard_hist", (double)(hi - lo) / SH_SAMPLE * (kg.q + 1));
+    k_shard_hist<<<grid_for((hi - lo) / SH_SAMPLE + 1, 256, 512), 256, 0, s>>>(
         ix.text.as<uint8_t>(), ix.n, lo, hi, reinterpret_cast<const uint16_t*>(ix.small.as<uint8_t>() + 2048),
         bucket_geom(kg), reinterpret_cast<unsigned long long*>(d_hist));
     HK_HIP(hipGetLastError());
   }
 }
 
-void shard_build(Index& ix, const uint64_t* h_global_hist, int nranks, int rank) {
-  if (ix.n > 0xFFFFFFFEull || (ix.flags & kFlagPos64)) shard_build_t<uint64_t>(ix, h_global_hist, nranks, rank);
-  else shard_build_t<uint32_t>(ix, h_global_hist, nranks, rank);
+void shard_counts(Index& ix, const uint64_t* h_global_hist, int nranks, int rank, uint64_t* d_below) {
+  if (nranks > SH_MAX_RANKS) throw ApiError{-2, "at most 64 ranks"};
+  KeyGeom kg = key_geometry(ix, true);
+  hipStream_t s = ix.stream;
+  const uint64_t lo = (uint64_t)((__uint128_t)ix.n * (uint64_t)rank / (uint64_t)nranks);
+  const uint64_t hi = (uint64_t)((__uint128_t)ix.n * (uint64_t)(rank + 1) / (uint64_t)nranks);
+  upload_geometry(ix, kg);
+  const BucketGeom g = bucket_geom(kg);
+  const PrefixImages pi(kg, g);
+  const std::vector<uint32_t> B = splitters(h_global_hist, nranks);
+  std::vector<BelowImg> img(nranks + 1);
+  for (int r = 0; r <= nranks; ++r) img[r] = below_img(pi, g, B[r]);
+  ix.tile_d.ensure(sizeof(BelowImg) * (nranks + 1) + 64);
+  HK_HIP(hipMemcpyAsync(ix.tile_d.p, img.data(), sizeof(BelowImg) * (nranks + 1), hipMemcpyHostToDevice, s));
+  HK_HIP(hipMemsetAsync(d_below, 0, 8 * (nranks + 1), s));
+  if (hi > lo) {
+    TimedLaunch t(ix.timer, "shard_below", (double)(hi - lo));
+    k_shard_below<<<grid_for((hi - lo) / 16 + 2, 256, 4096), 256, 0, s>>>(
+        ix.text.as<uint8_t>(), ix.n, lo, hi, reinterpret_cast<const uint16_t*>(ix.small.as<uint8_t>() + 2048), g,
+        pi.h, pi.topmask, pi.usable ? 0 : 1, ix.tile_d.as<BelowImg>(), nranks + 1,
+        reinterpret_cast<unsigned long long*>(d_below));
+    HK_HIP(hipGetLastError());
+  }
+  HK_HIP(hipStreamSynchronize(s));   // img staging buffer reuse
+}
+
+void shard_build(Index& ix, const uint64_t* h_global_hist, const uint64_t* h_global_below, int nranks, int rank) {
+  if (ix.n > 0xFFFFFFFEull || (ix.flags & kFlagPos64))
+    shard_build_t<uint64_t>(ix, h_global_hist, h_global_below, nranks, rank);
+  else
+    shard_build_t<uint32_t>(ix, h_global_hist, h_global_below, nranks, rank);
 }
 
 int shard_buckets() { return SH_BUCKETS; }
+int shard_sample() { return SH_SAMPLE; }
 
 void shard_get_bwt(Index& ix, uint64_t a, uint64_t b, uint8_t* out) {
   const uint64_t m = ix.shard_hi - ix.shard_lo;
@@ -488,7 +636,16 @@ void build_sa_sharded(Index& ix, const uint8_t id[128], int nranks, int rank) {
   std::vector<uint64_t> h(SH_BUCKETS);
   HK_HIP(hipMemcpyAsync(h.data(), hist.p, SH_BUCKETS * 8, hipMemcpyDeviceToHost, s));
   HK_HIP(hipStreamSynchronize(s));
-  shard_build(ix, h.data(), nranks, rank);
+  // exact slice sizes: per-rank counts below every splitter, summed
+  shard_counts(ix, h.data(), nranks, rank, hist.as<uint64_t>());
+  {
+    TimedLaunch t(ix.timer, "rccl_allreduce_counts", (double)(nranks + 1) * 8);
+    ncclcheck(ncclAllReduce(hist.p, hist.p, nranks + 1, ncclUint64, ncclSum, g_comm.comm, s), "ncclAllReduce");
+  }
+  std::vector<uint64_t> below(nranks + 1);
+  HK_HIP(hipMemcpyAsync(below.data(), hist.p, (nranks + 1) * 8, hipMemcpyDeviceToHost, s));
+  HK_HIP(hipStreamSynchronize(s));
+  shard_build(ix, h.data(), below.data(), nranks, rank);
   // merge: all-gather every rank's slice bounds and check that they tile [0, n)
   DevBuf bounds;
   bounds.ensure((size_t)nranks * 16 + 16);

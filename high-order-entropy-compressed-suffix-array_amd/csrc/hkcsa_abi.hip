@@ -537,6 +537,7 @@ int hkcsa_comm_unique_id(uint8_t id[128]) {
 }
 
 int hkcsa_shard_buckets(void) { return hk::shard_buckets(); }
+int hkcsa_shard_sample(void) { return hk::shard_sample(); }
 
 int hkcsa_shard_histogram(hkcsa_index* h, int nranks, int rank, uint64_t* hist_out) {
   return guarded([&] {
@@ -552,13 +553,29 @@ int hkcsa_shard_histogram(hkcsa_index* h, int nranks, int rank, uint64_t* hist_o
   });
 }
 
-int hkcsa_shard_build(hkcsa_index* h, const uint64_t* global_hist, int nranks, int rank) {
+int hkcsa_shard_counts(hkcsa_index* h, const uint64_t* global_hist, int nranks, int rank, uint64_t* below_out) {
   return guarded([&] {
     activate(h);
     need(h->ix.have_text, HKCSA_E_STATE, "text released by hkcsa_compact");
-    need(global_hist != nullptr && nranks >= 1 && rank >= 0 && rank < nranks, HKCSA_E_INVALID, "bad arguments");
+    need(global_hist && below_out && nranks >= 1 && nranks <= 64 && rank >= 0 && rank < nranks, HKCSA_E_INVALID,
+         "bad arguments");
+    hk::DevBuf d;
+    d.ensure((size_t)(nranks + 1) * 8);
+    hk::shard_counts(h->ix, global_hist, nranks, rank, d.as<uint64_t>());
+    HK_HIP(hipMemcpyAsync(below_out, d.p, (size_t)(nranks + 1) * 8, hipMemcpyDeviceToHost, h->ix.stream));
+    HK_HIP(hipStreamSynchronize(h->ix.stream));
+  });
+}
+
+int hkcsa_shard_build(hkcsa_index* h, const uint64_t* global_hist, const uint64_t* global_below, int nranks,
+                      int rank) {
+  return guarded([&] {
+    activate(h);
+    need(h->ix.have_text, HKCSA_E_STATE, "text released by hkcsa_compact");
+    need(global_hist && global_below && nranks >= 1 && nranks <= 64 && rank >= 0 && rank < nranks,
+         HKCSA_E_INVALID, "bad arguments");
     h->ix.have_bwt = h->ix.have_wt = false;
-    hk::shard_build(h->ix, global_hist, nranks, rank);
+    hk::shard_build(h->ix, global_hist, global_below, nranks, rank);
   });
 }
 

@@ -77,7 +77,9 @@ _SIGS = [
     ("hkcsa_get_shard_bwt", C.c_int, [vp, C.c_uint64, C.c_uint64, vp]),
     ("hkcsa_shard_buckets", C.c_int, []),
     ("hkcsa_shard_histogram", C.c_int, [vp, C.c_int, C.c_int, vp]),
-    ("hkcsa_shard_build", C.c_int, [vp, vp, C.c_int, C.c_int]),
+    ("hkcsa_shard_sample", C.c_int, []),
+    ("hkcsa_shard_counts", C.c_int, [vp, vp, C.c_int, C.c_int, vp]),
+    ("hkcsa_shard_build", C.c_int, [vp, vp, vp, C.c_int, C.c_int]),
     ("hkcsa_key_geometry", C.c_int, [vp, C.POINTER(C.c_int), C.POINTER(C.c_int), u64p, C.POINTER(C.c_int)]),
     ("hkcsa_debug_radix_bench", C.c_int, [C.c_uint64, C.c_int, vp, C.c_int]),
     ("hkcsa_timing_enable", C.c_int, [vp, C.c_int]),

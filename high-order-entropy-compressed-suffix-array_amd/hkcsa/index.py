@@ -269,9 +269,16 @@ class DeviceIndex:
         N.check(self.lib.hkcsa_shard_histogram(self.h, nranks, rank, _ptr(out)))
         return out
 
-    def shard_build(self, global_hist: np.ndarray, nranks: int, rank: int):
+    def shard_counts(self, global_hist: np.ndarray, nranks: int, rank: int) -> np.ndarray:
         g = np.ascontiguousarray(global_hist, dtype=np.uint64)
-        N.check(self.lib.hkcsa_shard_build(self.h, _ptr(g), nranks, rank))
+        out = np.zeros(nranks + 1, dtype=np.uint64)
+        N.check(self.lib.hkcsa_shard_counts(self.h, _ptr(g), nranks, rank, _ptr(out)))
+        return out
+
+    def shard_build(self, global_hist: np.ndarray, global_below: np.ndarray, nranks: int, rank: int):
+        g = np.ascontiguousarray(global_hist, dtype=np.uint64)
+        b = np.ascontiguousarray(global_below, dtype=np.uint64)
+        N.check(self.lib.hkcsa_shard_build(self.h, _ptr(g), _ptr(b), nranks, rank))
 
     def shard_range(self) -> tuple[int, int]:
         lo, hi = C.c_uint64(0), C.c_uint64(0)

@@ -1,16 +1,18 @@
 """Host orchestration of the sharded suffix-array build (see csrc/hk_shard.hip).
 
 The native entry point hkcsa_build_sa_sharded does the whole exchange itself over
-RCCL.  This module is the two-phase variant for hosts that run their own
+RCCL.  This module is the three-phase variant for hosts that run their own
 collectives (torch.distributed over RCCL or gloo):
 
-    h = dev.shard_histogram(N, r)            # this rank's 14-bit key-prefix histogram
-    g = allreduce_sum(h)                     # one collective, 16384 u64
-    dev.shard_build(g, N, r)                 # independent slice sort + refinement
+    h = dev.shard_histogram(N, r)            # sampled 14-bit key-prefix histogram of the block
+    g = allreduce_sum(h)                     # collective 1: 16384 u64
+    c = dev.shard_counts(g, N, r)            # block suffixes below each splitter
+    G = allreduce_sum(c)                     # collective 2: N+1 u64 -> exact slice bounds
+    dev.shard_build(g, G, N, r)              # independent slice sort + refinement
 
-slice_bounds() restates the splitter rule of hk_shard.hip (shard_build_t): rank r
-owns buckets [B_r, B_{r+1}) where B_r is the first bucket whose prefix count
-reaches floor(n*r/N); its slice of the final SA is [cum[B_r], cum[B_{r+1})).
+split_buckets() restates the splitter rule of hk_shard.hip (splitters): B_r is the first
+bucket whose sampled prefix count reaches floor(S*r/N), S = the sample total; rank r
+owns buckets [B_r, B_{r+1}) and its SA slice is [G[r], G[r+1]).
 """
 from __future__ import annotations
 
@@ -19,31 +21,32 @@ from typing import Callable
 import numpy as np
 
 SH_BUCKETS = 1 << 14
+SH_SAMPLE = 16
 
 
-def split_buckets(global_hist, n: int, nranks: int) -> list[int]:
+def split_buckets(global_hist, nranks: int) -> list[int]:
     cum = np.concatenate(([0], np.cumsum(np.asarray(global_hist, dtype=np.uint64))))
-    if int(cum[-1]) != n:
-        raise ValueError("histogram does not sum to n")
+    tot = int(cum[-1])
     out = [0]
     for r in range(1, nranks):
-        target = (n * r) // nranks
+        target = (tot * r) // nranks
         out.append(int(np.searchsorted(cum, target, side="left")))
     out.append(len(cum) - 1)
     return out
 
 
-def slice_bounds(global_hist, n: int, nranks: int) -> list[tuple[int, int]]:
-    cum = np.concatenate(([0], np.cumsum(np.asarray(global_hist, dtype=np.uint64))))
-    b = split_buckets(global_hist, n, nranks)
-    return [(int(cum[b[r]]), int(cum[b[r + 1]])) for r in range(nranks)]
+def slice_bounds(global_below, nranks: int) -> list[tuple[int, int]]:
+    g = [int(x) for x in global_below]
+    return [(g[r], g[r + 1]) for r in range(nranks)]
 
 
 def sharded_build(dev, nranks: int, rank: int, allreduce_sum: Callable[[np.ndarray], np.ndarray]):
-    """Two-phase sharded SA build; returns this rank's (lo, hi) slice of the SA."""
+    """Three-phase sharded SA build; returns this rank's (lo, hi) slice of the SA."""
     h = dev.shard_histogram(nranks, rank)
     g = allreduce_sum(h)
-    dev.shard_build(g, nranks, rank)
+    c = dev.shard_counts(g, nranks, rank)
+    below = allreduce_sum(c)
+    dev.shard_build(g, below, nranks, rank)
     return dev.shard_range()
 
 

@@ -171,9 +171,10 @@ int hkcsa_extract(hkcsa_index* ix, uint64_t i, uint64_t j, uint8_t* out);   /* T
 /* RCCL unique id (128 bytes) to be broadcast by the caller from rank 0. */
 int hkcsa_comm_unique_id(uint8_t id[128]);
 /* Each rank holds the same T' (created on its own device).  Ranks split the
- * final SA into contiguous rank ranges by a shared key histogram
- * (RCCL all-reduce) and sort their slice independently; the slice bounds are
- * exchanged with an RCCL all-gather.  After the call ix holds SA[lo:hi). */
+ * final SA into contiguous rank ranges by a shared sampled key histogram (RCCL
+ * all-reduce), fix the exact slice sizes with a second all-reduce of N+1 counts,
+ * and sort their slice independently; the slice bounds are checked with an RCCL
+ * all-gather.  After the call ix holds SA[lo:hi) (and its BWT rows). */
 int hkcsa_build_sa_sharded(hkcsa_index* ix, const uint8_t id[128], int nranks, int rank);
 int hkcsa_shard_range(hkcsa_index* ix, uint64_t* lo, uint64_t* hi);
 /* Sharded SA slice entries SA[lo+a : lo+b) (a,b relative to the slice). */
@@ -181,15 +182,23 @@ int hkcsa_get_shard_sa(hkcsa_index* ix, uint64_t a, uint64_t b, uint64_t* out);
 /* BWT of the slice: out[j] = T'[SA[lo+a+j]-1] (wrapping), j < b-a — the rows
  * bwt_transform (csa/bwt.py:4-9) emits for this rank's SA range. */
 int hkcsa_get_shard_bwt(hkcsa_index* ix, uint64_t a, uint64_t b, uint8_t* out);
-/* The same construction in two host-visible phases, for hosts that do their own
- * collectives (and for single-GPU tests of the partitioning):
- *   hkcsa_shard_histogram: this rank's key-prefix histogram (hkcsa_shard_buckets()
- *   bins) over positions [n*rank/nranks, n*(rank+1)/nranks);
- *   hkcsa_shard_build: builds SA[lo:hi) of this rank from the element-wise sum of
- *   every rank's histogram. */
+/* The same construction in three host-visible phases, for hosts that do their own
+ * collectives (and for single-GPU tests of the partitioning).  Rank r's block is
+ * the positions [n*r/N, n*(r+1)/N):
+ *   hkcsa_shard_histogram: key-prefix histogram (hkcsa_shard_buckets() bins) of the
+ *     block's positions p with p % hkcsa_shard_sample() == 0;
+ *   hkcsa_shard_counts: with G = the element-wise sum of every rank's histogram,
+ *     below_out[j] (j = 0..N) = #suffixes of the block whose bucket is below
+ *     splitter j (splitters derived from G; below_out[0] = 0);
+ *   hkcsa_shard_build: builds SA[lo:hi) of this rank from G and the element-wise
+ *     sum of every rank's below_out (lo, hi = its entries r and r+1). */
 int hkcsa_shard_buckets(void);
+int hkcsa_shard_sample(void);
 int hkcsa_shard_histogram(hkcsa_index* ix, int nranks, int rank, uint64_t* hist_out);
-int hkcsa_shard_build(hkcsa_index* ix, const uint64_t* global_hist, int nranks, int rank);
+int hkcsa_shard_counts(hkcsa_index* ix, const uint64_t* global_hist, int nranks, int rank,
+                       uint64_t* below_out);
+int hkcsa_shard_build(hkcsa_index* ix, const uint64_t* global_hist, const uint64_t* global_below,
+                      int nranks, int rank);
 
 /* Suffix-key geometry chosen for this text (parity export for the shard tests):
  * q symbols as a radix-`radix` number above a pb-bit preceding-symbol field. */

@@ -281,6 +281,17 @@ int oracle_key_geometry(const uint8_t* t, uint64_t n, int* q_out, int* pb_out, u
   return sigma;
 }
 
+/* bucket (top 14 key bits) of suffix p under the build's key geometry */
+static uint64_t shard_bucket(const uint8_t* t, uint64_t n, uint64_t p, const uint16_t* code, int q, int pb,
+                             uint64_t R, int bsh) {
+  uint64_t key = 0;
+  for (int j = 0; j < q; ++j) key = key * R + (p + j < n ? code[t[p + j]] : 0);
+  key = (key << pb) | code[t[p == 0 ? n - 1 : p - 1]];
+  return key >> bsh;
+}
+
+/* Sampled key-prefix histogram of positions p in [lo, hi) with p % 16 == 0 (hk_shard.hip,
+ * SH_SAMPLE): the splitters only need balance; exact slice sizes come from oracle_shard_below. */
 void oracle_shard_hist(const uint8_t* t, uint64_t n, uint64_t lo, uint64_t hi, uint64_t* hist /* 16384 */) {
   uint16_t code[256];
   int q, pb, kb;
@@ -289,11 +300,22 @@ void oracle_shard_hist(const uint8_t* t, uint64_t n, uint64_t lo, uint64_t hi, u
   int bsh = kb - 14;
   if (bsh < 0) bsh = 0;
   memset(hist, 0, 16384 * sizeof(uint64_t));
+  for (uint64_t p = (lo + 15) / 16 * 16; p < hi; p += 16) hist[shard_bucket(t, n, p, code, q, pb, R, bsh)]++;
+}
+
+/* below[j] = #{p in [lo, hi) : bucket(p) < B[j]} for j < nb */
+void oracle_shard_below(const uint8_t* t, uint64_t n, uint64_t lo, uint64_t hi, const uint32_t* B, int nb,
+                        uint64_t* below) {
+  uint16_t code[256];
+  int q, pb, kb;
+  uint64_t R;
+  oracle_key_geometry(t, n, &q, &pb, &R, &kb, code);
+  int bsh = kb - 14;
+  if (bsh < 0) bsh = 0;
+  for (int j = 0; j < nb; ++j) below[j] = 0;
   for (uint64_t p = lo; p < hi; ++p) {
-    uint64_t key = 0;
-    for (int j = 0; j < q; ++j) key = key * R + (p + j < n ? code[t[p + j]] : 0);
-    key = (key << pb) | code[t[p == 0 ? n - 1 : p - 1]];
-    hist[key >> bsh]++;
+    const uint64_t b = shard_bucket(t, n, p, code, q, pb, R, bsh);
+    for (int j = 0; j < nb; ++j) below[j] += b < B[j];
   }
 }
 

@@ -53,6 +53,7 @@ def lib():
         L.oracle_wt_levels.argtypes = [vp, u64, vp]
         L.oracle_wt_levels.restype = C.c_int
         L.oracle_shard_hist.argtypes = [vp, u64, u64, u64, vp]
+        L.oracle_shard_below.argtypes = [vp, u64, u64, u64, vp, C.c_int, vp]
         L.oracle_key_geometry.argtypes = [vp, u64, vp, vp, vp, vp, vp]
         L.oracle_golomb.argtypes = [vp, u64, C.c_uint32, vp]
         L.oracle_golomb.restype = u64
@@ -121,6 +122,15 @@ def shard_hist(t, lo: int, hi: int) -> np.ndarray:
     h = np.zeros(16384, dtype=np.uint64)
     lib().oracle_shard_hist(_p(t), len(t), lo, hi, _p(h))
     return h
+
+
+def shard_below(t, lo: int, hi: int, splitters) -> np.ndarray:
+    """#positions p in [lo, hi) whose 14-bit key bucket is below each splitter."""
+    t = _u8(t)
+    B = np.ascontiguousarray(splitters, dtype=np.uint32)
+    out = np.zeros(len(B), dtype=np.uint64)
+    lib().oracle_shard_below(_p(t), len(t), lo, hi, _p(B), len(B), _p(out))
+    return out
 
 
 def key_geometry(t) -> tuple[int, int, int, int]:

@@ -32,9 +32,14 @@ class OracleShardDevice:
         lo, hi = self.n * rank // nranks, self.n * (rank + 1) // nranks
         return self.o.shard_hist(self.t, lo, hi)
 
-    def shard_build(self, g, nranks, rank):
+    def shard_counts(self, g, nranks, rank):
+        from hkcsa.shard import split_buckets
+        lo, hi = self.n * rank // nranks, self.n * (rank + 1) // nranks
+        return self.o.shard_below(self.t, lo, hi, split_buckets(g, nranks))
+
+    def shard_build(self, g, below, nranks, rank):
         from hkcsa.shard import slice_bounds
-        self.lo, self.hi = slice_bounds(g, self.n, nranks)[rank]
+        self.lo, self.hi = slice_bounds(below, nranks)[rank]
         full = self.o.suffix_array(self.t)  # the oracle's SA restricted to the owned rank range
         self.slice = full[self.lo:self.hi]
 

@@ -225,13 +225,17 @@ def test_shard_two_phase_emulated(hk, nranks, flags, alpha):
     ref_bwt = oracle.bwt(text, ref)
     devs = [hk.DeviceIndex.from_bytes(text, device=0, flags=flags) for _ in range(nranks)]
     g = sum(d.shard_histogram(nranks, r) for r, d in enumerate(devs))
-    assert int(g.sum()) == len(text)
+    assert int(g.sum()) == (len(text) + 15) // 16          # every 16th position (hkcsa_shard_sample)
     assert np.array_equal(g, oracle.shard_hist(text, 0, len(text)))
+    from hkcsa.shard import slice_bounds, split_buckets
+    B = split_buckets(g, nranks)
+    below = sum(d.shard_counts(g, nranks, r) for r, d in enumerate(devs))
+    assert np.array_equal(below, oracle.shard_below(text, 0, len(text), B))
+    assert int(below[-1]) == len(text)
     parts = []
-    from hkcsa.shard import slice_bounds
-    bounds = slice_bounds(g, len(text), nranks)
+    bounds = slice_bounds(below, nranks)
     for r, d in enumerate(devs):
-        d.shard_build(g, nranks, r)
+        d.shard_build(g, below, nranks, r)
         assert d.shard_range() == bounds[r]
         parts.append(d.shard_sa())
         lo, hi = bounds[r]
