@@ -5,7 +5,7 @@ cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 if [ "${TESTS:-1}" = "1" ]; then
-  timeout -k 10 900 python -m pytest tests -m gpu -x -q > gpurun_out/gpu_tests.log 2>&1
+  timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1
   rc=$?
   echo "pytest rc=$rc"; tail -15 gpurun_out/gpu_tests.log
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
