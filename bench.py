@@ -126,7 +126,7 @@ def stage_breakdown(dev: DeviceIndex, names) -> dict:
 
 def run_single(args) -> dict:
     n = args.text_bytes + 1
-    dev = DeviceIndex.synthetic(n, DNA, seed=args.seed, device=0)
+    dev = DeviceIndex.synthetic(n, DNA, seed=args.seed, device=0, flags=4 if args.global_sort else 0)
     log(f"[bench] text n={n} resident on device")
     for _ in range(args.warmup):
         dev.build_sa()
@@ -150,7 +150,8 @@ def run_single(args) -> dict:
     value = args.steps * n / 2**20 / wall
     info = dev.build_info()
     roof = roofline(dev, args.traffic_gb)
-    stages = stage_breakdown(dev, ["radix_hist", "radix_onesweep", "radix_onesweep_small", "sa_pack_keys",
+    stages = stage_breakdown(dev, ["sa_bucket_hist", "sa_bucket_sort", "sa_big_gather",
+                                   "radix_hist", "radix_onesweep", "radix_onesweep_small", "sa_pack_keys",
                                    "sa_refine_stats", "sa_refine_apply", "sa_refine_keys", "sa_isa_scatter",
                                    "sa_group_stats", "sa_group_apply", "sa_pair_keys", "bwt_gather", "byte_hist"])
     log(f"[bench] SA+BWT {wall / args.steps * 1e3:.2f} ms/step -> {value:.1f} MB/s; info={info[:8]}")
@@ -301,6 +302,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--sharded", action="store_true", help="use the sharded (multi-GPU) build even at N=1")
     ap.add_argument("--pos64", action="store_true", help="sharded build with 64-bit positions at any n")
+    ap.add_argument("--global-sort", action="store_true",
+                    help="single-GPU build by full-width LSD sort of the keys (no LDS bucket sorts)")
     ap.add_argument("--traffic-gb", type=float, default=None,
                     help="PMC-measured HBM GB per radix pass; default: profiles/pmc_radix_onesweep.json")
     args = ap.parse_args()

@@ -1,0 +1,936 @@
+// hk_bucket.hip — single-GPU suffix array + BWT by bucket sort (the default build).
+//
+// Replaces build_suffix_array (csa/suffix_array.py:131-134) + bwt_transform (csa/bwt.py:3-13) for
+// one GPU.  Result identical to the reference's SA (Python str order, '$' an ordinary byte,
+// proper prefix first) and BWT (wrap at SA == 0).
+//
+// Pipeline (HBM bytes per suffix in brackets, 1 GiB sigma=4 figures):
+//   1. k_bucket_hist   [1]   histogram of the top D bits of every suffix key, from the text;
+//   2. k_pack_keyed    [1+8] u64 key per suffix = [q symbols, radix Rk][code of T'[p-1]];
+//   3. two LSD onesweep passes over the top D key bits (hk_sort.hip) [20 + 24]: the suffixes are
+//      then grouped by bucket, buckets in order, each bucket a contiguous range;
+//   4. k_bucket_sort   [12+5] one workgroup per bucket (<= 18432 suffixes): keys to registers,
+//      LDS radix sort over the bits that vary inside the bucket, SA and BWT written in sorted order,
+//      suffixes with equal keys appended to a tie list;
+//   5. buckets too large for one workgroup (skewed texts) are sorted together on the global
+//      path (radix sort of (bucket ordinal, low key bits)); a text whose suffixes mostly fall in
+//      such buckets takes the global path whole;
+//   6. ties are refined from symbol q on (hk_sa.hip refine_loop), falling back to prefix
+//      doubling for long repeats.
+// Keyed layout: the sorted field has no end-of-text code and no code for a terminal that occurs
+// once at n-1 (see KeyGeom) — sigma=4 DNA + '$' packs 2 bits per symbol, so 24 symbols fit the
+// 48 bits that two 8-bit passes + a 32-bit LDS sort cover.
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+
+#include "hk_index.hpp"
+#include "hk_keys.hpp"
+
+namespace hk {
+namespace {
+
+struct KeyedArgs {
+  uint64_t Rk, Rck, Rlast;
+  uint64_t s_start;
+  int q, ck, pb, hq;   // hq > 0: the bucket is the first hq symbols (radix 2^k, exact split)
+};
+
+inline KeyedArgs keyed_args(const KeyGeom& kg, uint64_t n) {
+  const KeyChunks kc = key_chunks(kg.Rk, kg.q);
+  KeyedArgs a{kg.Rk, kc.Rck, kc.Rlast, kg.s_start, kg.q, kc.ck, kg.pb, 0};
+  (void)n;
+  return a;
+}
+
+// sym field of suffix p: its first q keyed codes as a radix-Rk number, or the boundary key of a
+// short suffix.  c[off] holds T'[p-1], c[off+1..] T'[p..]; each code is keyed code | byte << 8.
+__device__ __forceinline__ uint64_t keyed_sym(const uint16_t* c, int off, uint64_t p, const KeyedArgs& g,
+                                              const uint64_t* SK) {
+  if (p >= g.s_start) return SK[p - g.s_start];
+  uint64_t key = 0;
+  int j = 1;
+  while (j <= g.q) {
+    const int len = g.q - j + 1 < g.ck ? g.q - j + 1 : g.ck;
+    uint32_t cv = 0;
+    for (int u = 0; u < len; ++u) cv = __umul24(cv, (uint32_t)g.Rk) + (c[off + j + u] & 255u);
+    key = key * (len == g.ck ? g.Rck : g.Rlast) + cv;
+    j += len;
+  }
+  return key;
+}
+
+// ------------------------------------------------------------ 1. bucket histogram
+// One pass over the text, all 2^D <= 65536 bins in LDS as u16 pairs (128 KiB).  A counter that
+// reaches 0x8000 is drained to the global histogram by the lane whose add took it there (the lane
+// sees 0x7FFF returned); the 32k headroom above covers the adds in flight until its subtract lands.
+constexpr int BH_T = 1024;
+constexpr int BH_PER = 16;                  // consecutive positions per thread (radix-2^k path)
+constexpr int BH_TILE = BH_T * BH_PER;      // 16384 positions per tile
+constexpr int BH_STAGE = 4096;              // staged tile of the generic (mixed-radix) path
+
+__device__ __forceinline__ void bh_add(uint32_t* H, uint32_t b, unsigned long long* __restrict__ hist) {
+  const uint32_t sh = 16u * (b & 1u);
+  const uint32_t old = atomicAdd(&H[b >> 1], 1u << sh);
+  if (((old >> sh) & 0xFFFFu) == 0x7FFFu) {
+    atomicSub(&H[b >> 1], 0x8000u << sh);
+    atomicAdd(&hist[b], 0x8000ull);
+  }
+}
+
+template <bool HQ>
+__global__ __launch_bounds__(BH_T, 1) void k_bucket_hist(const uint8_t* __restrict__ t, uint64_t n,
+                                                         const uint16_t* __restrict__ lutk,
+                                                         const uint64_t* __restrict__ skey, KeyedArgs g, int bsh,
+                                                         int D, unsigned long long* __restrict__ hist) {
+  __shared__ uint32_t H[32768];
+  __shared__ uint16_t c[HQ ? 1 : BH_STAGE + kCodePad];
+  __shared__ uint16_t L[256];
+  __shared__ uint64_t SK[72];
+  const uint32_t tid = threadIdx.x;
+  for (uint32_t i = tid; i < 32768; i += BH_T) H[i] = 0;
+  if (tid < 256) L[tid] = lutk[tid];
+  if (tid < 72) SK[tid] = skey[tid];
+  __syncthreads();
+  const uint64_t lim = n < g.s_start ? n : g.s_start;   // positions with a text window
+  if (HQ) {
+    const int lb = 31 - __clz((uint32_t)g.Rk);
+    const uint32_t bmask = (1u << D) - 1;
+    const uint64_t stride = (uint64_t)gridDim.x * BH_TILE;
+    uint64_t base = (uint64_t)blockIdx.x * BH_TILE;
+    uint4 w0 = make_uint4(0, 0, 0, 0), w1 = w0;
+    if (base + (uint64_t)tid * BH_PER < n) {
+      const uint4* src = reinterpret_cast<const uint4*>(t + base + (uint64_t)tid * BH_PER);
+      w0 = src[0];
+      w1 = src[1];
+    }
+    for (; base < n; base += stride) {
+      const uint64_t p0 = base + (uint64_t)tid * BH_PER;
+      const uint32_t wd[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+      if (p0 + stride < n) {   // next tile's bytes in flight
+        const uint4* src = reinterpret_cast<const uint4*>(t + p0 + stride);
+        w0 = src[0];
+        w1 = src[1];
+      }
+      if (p0 < lim) {
+        // rolling window over bytes i = 0 .. 30 (static register indices); the window ending at
+        // byte i is the bucket of position p0 + i - (hq - 1)
+        uint32_t b = 0;
+#pragma unroll
+        for (int i = 0; i < 2 * BH_PER - 1; ++i) {
+          b = ((b << lb) | (L[(wd[i >> 2] >> (8 * (i & 3))) & 255u] & 255u)) & bmask;
+          const int j = i - (g.hq - 1);
+          if (j >= 0 && j < BH_PER && p0 + j < lim) bh_add(H, b, hist);
+        }
+      }
+      for (uint64_t p = p0 > lim ? p0 : lim; p < p0 + BH_PER && p < n; ++p)
+        bh_add(H, (uint32_t)(SK[p - g.s_start] >> bsh), hist);
+    }
+  } else {
+    for (uint64_t base = (uint64_t)blockIdx.x * BH_STAGE; base < n; base += (uint64_t)gridDim.x * BH_STAGE) {
+      stage_text_codes<BH_STAGE, BH_T>(c, L, t, n, base);
+      __syncthreads();
+#pragma unroll
+      for (int k = 0; k < BH_STAGE / BH_T; ++k) {
+        const int off = k * BH_T + tid;
+        const uint64_t p = base + off;
+        if (p < n) bh_add(H, (uint32_t)(keyed_sym(c, off, p, g, SK) >> bsh), hist);
+      }
+      __syncthreads();
+    }
+  }
+  __syncthreads();
+  const uint32_t nb = 1u << D;
+  for (uint32_t i = tid; i < 32768; i += BH_T) {
+    const uint32_t v = H[i];
+    if ((v & 0xFFFFu) && 2 * i < nb) atomicAdd(&hist[2 * i], (unsigned long long)(v & 0xFFFFu));
+    if ((v >> 16) && 2 * i + 1 < nb) atomicAdd(&hist[2 * i + 1], (unsigned long long)(v >> 16));
+  }
+}
+
+// ------------------------------------------------------------ 2. keys
+constexpr int PKK_TILE = 4096;
+__global__ __launch_bounds__(256) void k_pack_keyed(const uint8_t* __restrict__ t, uint64_t n,
+                                                    const uint16_t* __restrict__ lutk,
+                                                    const uint16_t* __restrict__ lutp,
+                                                    const uint64_t* __restrict__ skey, KeyedArgs g,
+                                                    uint64_t* __restrict__ keys) {
+  __shared__ uint16_t c[PKK_TILE + kCodePad];
+  __shared__ uint16_t L[256], LP[256];
+  __shared__ uint64_t SK[72];
+  L[threadIdx.x] = lutk[threadIdx.x];
+  LP[threadIdx.x] = lutp[threadIdx.x];
+  if (threadIdx.x < 72) SK[threadIdx.x] = skey[threadIdx.x];
+  __syncthreads();
+  const uint64_t stride = (uint64_t)gridDim.x * PKK_TILE;
+  TextWords<PKK_TILE, 256> tw;
+  if ((uint64_t)blockIdx.x * PKK_TILE < n) load_text_words(tw, t, n, (uint64_t)blockIdx.x * PKK_TILE);
+  for (uint64_t base = (uint64_t)blockIdx.x * PKK_TILE; base < n; base += stride) {
+    store_text_codes(c, L, tw, n, base);
+    __syncthreads();
+    if (base + stride < n) load_text_words(tw, t, n, base + stride);
+#pragma unroll 4
+    for (int k = 0; k < PKK_TILE / 256; ++k) {
+      const int off = k * 256 + threadIdx.x;
+      const uint64_t p = base + off;
+      if (p < n) keys[p] = (keyed_sym(c, off, p, g, SK) << g.pb) | LP[c[off] >> 8];
+    }
+    __syncthreads();
+  }
+}
+
+// ------------------------------------------------------------ 4. LDS bucket sort
+constexpr int BS_T = 1024;
+constexpr int BS_W = BS_T / 64;
+constexpr int BS_I = 18;
+constexpr int BS_CAP = BS_T * BS_I;   // 18432 suffixes per workgroup
+constexpr int BS_WSPAN = BS_I * 64;
+
+struct BsShared {
+  uint32_t buf[BS_CAP];          // exchange buffer (one u32 plane at a time)
+  uint16_t prev[BS_CAP];         // BWT code (prev field, <= 9 bits) of each suffix, by original slot
+  uint32_t whist[BS_W][256];     // per-wave digit counts -> per-wave exclusive prefix
+  uint32_t tstart[256];          // block-wide exclusive digit start
+  uint32_t wsum[4];
+  uint64_t rv[2][BS_W];
+  uint8_t inv[512];
+};
+
+// One workgroup sorts items[blockIdx.x] = {start, count} of the bucket-grouped (keys, vals):
+// radix passes over the key bits that vary inside the range (LDS exchange of the local key planes
+// and of index|prev), then SA[start + r] / BWT[start + r] in sorted order, ties to the list.
+// diagnostic stamps (TRACE): shader-clock time at the phase boundaries of workgroup 0's wave 0
+__device__ __forceinline__ uint64_t stamp() {
+  uint64_t t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
+
+template <bool WIDE, bool TRACE = false>
+__global__ __launch_bounds__(BS_T, 1) void k_bucket_sort(const uint64_t* __restrict__ keys,
+                                                         const uint32_t* __restrict__ vals,
+                                                         const uint2* __restrict__ items, int pb, int sb,
+                                                         const uint8_t* __restrict__ inv, uint32_t* __restrict__ sa,
+                                                         uint8_t* __restrict__ bwt, uint64_t* __restrict__ tie_k,
+                                                         uint32_t* __restrict__ tie_v,
+                                                         unsigned long long* __restrict__ tie_n,
+                                                         uint64_t* __restrict__ trace) {
+  __shared__ BsShared sh;
+  uint64_t ts[8] = {0};
+  if (TRACE) ts[0] = stamp();
+  const uint2 it = items[blockIdx.x];
+  const uint32_t start = it.x, cnt = it.y;
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  // workgroup-uniform bases: every per-item index below is a 32-bit offset from them
+  const uint64_t* __restrict__ kb = keys + start;
+  const uint32_t* __restrict__ vb = vals + start;
+  uint32_t* __restrict__ sab = sa + start;
+  uint8_t* __restrict__ bwb = bwt + start;
+  // slot of item k is s0 + 64 k (immediate LDS offsets); bit k of vmask = slot k holds a suffix
+  uint32_t s0 = wv * BS_WSPAN + lane;
+  uint32_t vmask = 0;
+#pragma unroll
+  for (int k = 0; k < BS_I; ++k) vmask |= (s0 + 64u * k < cnt ? 1u : 0u) << k;
+  const uint64_t symmask = sb >= 64 ? ~0ull : ((1ull << sb) - 1);
+  const uint32_t pmask = (1u << pb) - 1;
+  if (tid < 512) sh.inv[tid] = inv[tid];
+
+  // ---- load (original order: slot e = wv*WSPAN + k*64 + lane) and the varying-bit range; the
+  // positions are gathered by original slot at the end (fewer live registers through the passes)
+  uint64_t key[BS_I];
+  uint64_t vor = 0, vand = ~0ull;
+#pragma unroll
+  for (int k = 0; k < BS_I; ++k) {
+    key[k] = ((vmask >> k) & 1u) ? kb[s0 + 64u * k] : 0;
+  }
+#pragma unroll
+  for (int k = 0; k < BS_I; ++k) {
+    if (((vmask >> k) & 1u)) {
+      const uint64_t sym = (key[k] >> pb) & symmask;
+      vor |= sym;
+      vand &= sym;
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    vor |= __shfl_xor(vor, o, 64);
+    vand &= __shfl_xor(vand, o, 64);
+  }
+  if (lane == 0) {
+    sh.rv[0][wv] = vor;
+    sh.rv[1][wv] = vand;
+  }
+  __syncthreads();
+  vor = 0;
+  vand = ~0ull;
+#pragma unroll
+  for (int w = 0; w < BS_W; ++w) {
+    vor |= sh.rv[0][w];
+    vand &= sh.rv[1][w];
+  }
+  // prev fields by original slot (read back by the sorted index at the end)
+#pragma unroll
+  for (int k = 0; k < BS_I; ++k)
+    if ((vmask >> k) & 1u) sh.prev[s0 + 64u * k] = (uint16_t)((uint32_t)key[k] & pmask);
+  if (TRACE) ts[1] = stamp();
+  const uint64_t var = vor ^ vand;
+  const int lo = var ? __builtin_ctzll(var) : 0;
+  const int width = var ? 64 - __builtin_clzll(var) - lo : 0;
+
+  // live through the passes: the local key plane(s) and the original slot, 16 bits per item
+  // packed two to a register (as are the per-pass ranks) — 36 registers narrow, 54 wide
+  constexpr int BS_H = (BS_I + 1) / 2;
+  uint32_t klo[BS_I], khi[BS_I], ix2[BS_H];
+#pragma unroll
+  for (int k = 0; k < BS_I; ++k) {
+    const uint64_t lk = ((key[k] >> pb) & symmask) >> lo;
+    klo[k] = (uint32_t)lk;
+    khi[k] = WIDE ? (uint32_t)(lk >> 32) : 0u;
+  }
+#pragma unroll
+  for (int h = 0; h < BS_H; ++h)
+    ix2[h] = (s0 + 128u * h) | (2 * h + 1 < BS_I ? (s0 + 128u * h + 64u) << 16 : 0u);
+  uint16_t* buf16 = reinterpret_cast<uint16_t*>(sh.buf);
+
+  auto digit_of = [](uint32_t lo32, uint32_t hi32, int d) -> uint32_t {
+    if (!WIDE) return (lo32 >> d) & 255u;
+    return (uint32_t)((((uint64_t)hi32 << 32) | lo32) >> d) & 255u;
+  };
+  // ---- radix passes over the varying bits (uniform digits skipped)
+  for (int d0 = 0; d0 < width; d0 += 8) {
+    const uint32_t dmask = (uint32_t)((var >> lo) >> d0) & 255u;
+    if (!dmask) continue;
+    const int nb = 32 - __clz(dmask);   // highest varying bit of the digit + 1
+    asm volatile("" : "+v"(s0));   // slot addresses are cheap: recompute them per pass, do not keep 18
+    for (uint32_t i = tid; i < BS_W * 256; i += BS_T) (&sh.whist[0][0])[i] = 0;
+    __syncthreads();
+    uint32_t rk2[BS_H];
+#pragma unroll
+    for (int k = 0; k < BS_I; ++k) {
+      const bool valid = ((vmask >> k) & 1u);
+      const uint32_t dg = digit_of(klo[k], khi[k], d0);
+      uint64_t m = ballot64(valid);
+      for (int b = 0; b < nb; ++b) {
+        const bool bit = (dg >> b) & 1u;
+        const uint64_t bb = ballot64(bit);
+        m &= bit ? bb : ~bb;
+      }
+      const uint32_t below = mbcnt(m);
+      const uint32_t prior = sh.whist[wv][dg];
+      if (valid && below == 0) sh.whist[wv][dg] = prior + (uint32_t)__popcll(m);
+      const uint32_t wr = (prior + below) & 0xFFFFu;
+      if (k & 1) rk2[k >> 1] |= wr << 16; else rk2[k >> 1] = wr;
+    }
+    __syncthreads();
+    if (tid < 256) {
+      uint32_t run = 0;
+#pragma unroll
+      for (int w = 0; w < BS_W; ++w) {
+        const uint32_t cc = sh.whist[w][tid];
+        sh.whist[w][tid] = run;
+        run += cc;
+      }
+      const uint32_t inc = wave_incl_sum<uint32_t>(run);
+      if (lane == 63) sh.wsum[wv] = inc;
+      sh.tstart[tid] = inc - run;
+    }
+    __syncthreads();
+    if (tid < 256) {
+      uint32_t carry = 0;
+      for (uint32_t w = 0; w < wv; ++w) carry += sh.wsum[w];
+      sh.tstart[tid] += carry;
+    }
+    __syncthreads();
+    // destination rank of item k (recomputed from the digit each time it is needed)
+    auto dst = [&](int k) -> uint32_t {
+      const uint32_t dg = digit_of(klo[k], khi[k], d0);
+      return sh.tstart[dg] + sh.whist[wv][dg] + ((rk2[k >> 1] >> (16 * (k & 1))) & 0xFFFFu);
+    };
+    // exchange through LDS: write at the new rank, read back in slot order.  The index plane goes
+    // first (its destinations come from the key planes, which must still be in place).
+#pragma unroll
+    for (int k = 0; k < BS_I; ++k)
+      if (((vmask >> k) & 1u)) buf16[dst(k)] = (uint16_t)(ix2[k >> 1] >> (16 * (k & 1)));
+    __syncthreads();
+#pragma unroll
+    for (int h = 0; h < BS_H; ++h) {
+      const uint32_t a0 = buf16[(s0 + 128u * h)];
+      const uint32_t a1 = 2 * h + 1 < BS_I ? (uint32_t)buf16[(s0 + 128u * h + 64u)] : 0u;
+      ix2[h] = a0 | (a1 << 16);
+    }
+    __syncthreads();
+    if (WIDE) {
+      // rk2 -> absolute destinations are needed twice more: keep them in the rank registers
+#pragma unroll
+      for (int k = 0; k < BS_I; ++k)
+        if (((vmask >> k) & 1u)) sh.buf[dst(k)] = khi[k];
+      __syncthreads();
+      uint32_t nh[BS_I];
+#pragma unroll
+      for (int k = 0; k < BS_I; ++k) nh[k] = sh.buf[(s0 + 64u * k)];
+      __syncthreads();
+#pragma unroll
+      for (int k = 0; k < BS_I; ++k)
+        if (((vmask >> k) & 1u)) sh.buf[dst(k)] = klo[k];
+      __syncthreads();
+#pragma unroll
+      for (int k = 0; k < BS_I; ++k) {
+        khi[k] = nh[k];
+        klo[k] = sh.buf[(s0 + 64u * k)];
+      }
+      __syncthreads();
+    } else {
+#pragma unroll
+      for (int k = 0; k < BS_I; ++k)
+        if (((vmask >> k) & 1u)) sh.buf[dst(k)] = klo[k];
+      __syncthreads();
+#pragma unroll
+      for (int k = 0; k < BS_I; ++k) klo[k] = sh.buf[(s0 + 64u * k)];
+      __syncthreads();
+    }
+  }
+
+  // ---- ties: equal local keys next to each other in sorted order
+  if (TRACE) ts[2] = stamp();
+  asm volatile("" : "+v"(s0));
+  uint32_t tmask = 0, hmask = 0;
+#pragma unroll
+  for (int k = 0; k < BS_I; ++k) sh.buf[(s0 + 64u * k)] = klo[k];
+  __syncthreads();
+  uint32_t eqp = 0, eqn = 0;
+#pragma unroll
+  for (int k = 0; k < BS_I; ++k) {
+    const uint32_t r = (s0 + 64u * k);
+    if ((vmask >> k) & 1u) {
+      if (r > 0 && sh.buf[r - 1] == klo[k]) eqp |= 1u << k;
+      if (r + 1 < cnt && sh.buf[r + 1] == klo[k]) eqn |= 1u << k;
+    }
+  }
+  if (WIDE) {
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < BS_I; ++k) sh.buf[(s0 + 64u * k)] = khi[k];
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < BS_I; ++k) {
+      const uint32_t r = (s0 + 64u * k);
+      if (r < cnt) {
+        if (r > 0 && sh.buf[r - 1] != khi[k]) eqp &= ~(1u << k);
+        if (r + 1 < cnt && sh.buf[r + 1] != khi[k]) eqn &= ~(1u << k);
+      }
+    }
+  }
+  tmask = eqp | eqn;
+  hmask = tmask & ~eqp;
+  __syncthreads();
+
+  // ---- SA / BWT in sorted order: the positions are loaded coalesced in original order, staged in
+  // LDS by original slot and read back by the sorted index (no random global gathers)
+  if (TRACE) ts[3] = stamp();
+#pragma unroll
+  for (int k = 0; k < BS_I; ++k)
+    if ((vmask >> k) & 1u) sh.buf[s0 + 64u * k] = vb[s0 + 64u * k];
+  __syncthreads();
+  if (TRACE) ts[4] = stamp();
+#pragma unroll
+  for (int k = 0; k < BS_I; ++k) {
+    const uint32_t r = (s0 + 64u * k);
+    const bool valid = (vmask >> k) & 1u;
+    uint32_t p = 0;
+    if (valid) {
+      const uint32_t o = (ix2[k >> 1] >> (16 * (k & 1))) & 0xFFFFu;
+      p = sh.buf[o];
+      sab[r] = p;
+      bwb[r] = sh.inv[sh.prev[o]];
+    }
+    const bool tied = valid && ((tmask >> k) & 1u);
+    const uint64_t tb = ballot64(tied);
+    if (tb) {
+      uint64_t base = 0;
+      if (lane == 0) base = atomicAdd(tie_n, (unsigned long long)__popcll(tb));
+      base = __shfl(base, 0, 64);
+      if (tied) {
+        const uint64_t a = base + mbcnt(tb);
+        tie_k[a] = (((uint64_t)start + r) << 1) | ((hmask >> k) & 1u);
+        tie_v[a] = p;
+      }
+    }
+  }
+  if (TRACE) {
+    ts[5] = stamp();
+    if (tid == 0)
+      for (int i = 0; i < 6; ++i) trace[(uint64_t)blockIdx.x * 8 + i] = ts[i];
+  }
+}
+
+// ------------------------------------------------------------ 5. big buckets
+// compacted copy of the big buckets: key top D bits replaced by the big-bucket ordinal, J = slot
+__global__ __launch_bounds__(256) void k_big_gather(const uint64_t* __restrict__ keys,
+                                                    const uint32_t* __restrict__ vals,
+                                                    const uint64_t* __restrict__ bstart,
+                                                    const uint64_t* __restrict__ cstart, uint32_t nbig,
+                                                    uint64_t total, int lowbits, uint64_t* __restrict__ ok,
+                                                    uint32_t* __restrict__ ov, uint32_t* __restrict__ oj) {
+  for (uint64_t a = (uint64_t)blockIdx.x * 256 + threadIdx.x; a < total; a += (uint64_t)gridDim.x * 256) {
+    uint32_t lo = 0, hi = nbig;   // last g with cstart[g] <= a
+    while (hi - lo > 1) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (cstart[mid] <= a) lo = mid; else hi = mid;
+    }
+    const uint64_t src = bstart[lo] + (a - cstart[lo]);
+    const uint64_t k = keys[src];
+    ok[a] = ((uint64_t)lo << lowbits) | (lowbits ? (k & ((1ull << lowbits) - 1)) : 0);
+    ov[a] = vals[src];
+    oj[a] = (uint32_t)src;
+  }
+}
+
+// ------------------------------------------------------------ 6. ties
+// refine_step's (P, J, G) output of the big path appended to the tie list
+__global__ __launch_bounds__(256) void k_tie_append(const uint32_t* __restrict__ P, const uint32_t* __restrict__ J,
+                                                    const uint32_t* __restrict__ G, uint64_t A, uint64_t at,
+                                                    uint64_t* __restrict__ tie_k, uint32_t* __restrict__ tie_v) {
+  for (uint64_t a = (uint64_t)blockIdx.x * 256 + threadIdx.x; a < A; a += (uint64_t)gridDim.x * 256) {
+    const bool head = a == 0 || G[a] != G[a - 1];
+    tie_k[at + a] = ((uint64_t)J[a] << 1) | (head ? 1u : 0u);
+    tie_v[at + a] = P[a];
+  }
+}
+
+__global__ __launch_bounds__(256) void k_tie_split(const uint64_t* __restrict__ tk, const uint32_t* __restrict__ tv,
+                                                   uint64_t A, uint32_t* __restrict__ P, uint32_t* __restrict__ J,
+                                                   uint32_t* __restrict__ H) {
+  for (uint64_t a = (uint64_t)blockIdx.x * 256 + threadIdx.x; a < A; a += (uint64_t)gridDim.x * 256) {
+    const uint64_t k = tk[a];
+    P[a] = tv[a];
+    J[a] = (uint32_t)(k >> 1);
+    H[a] = (uint32_t)(k & 1u);
+  }
+}
+
+// G = inclusive head count - 1 (in place over H); head_slot[G] = J of the head
+__global__ __launch_bounds__(256) void k_tie_groups(const uint64_t* __restrict__ hx, const uint32_t* __restrict__ J,
+                                                    uint64_t A, uint32_t* __restrict__ GH,
+                                                    uint32_t* __restrict__ head_slot) {
+  for (uint64_t a = (uint64_t)blockIdx.x * 256 + threadIdx.x; a < A; a += (uint64_t)gridDim.x * 256) {
+    const uint32_t h = GH[a];
+    const uint32_t g = (uint32_t)(hx[a] + h - 1);
+    GH[a] = g;
+    if (h) head_slot[g] = J[a];
+  }
+}
+
+inline unsigned grid_of(uint64_t n, unsigned cap = 16384) {
+  uint64_t g = ceil_div(n ? n : 1, 256);
+  return (unsigned)(g < cap ? g : cap);
+}
+
+int bits_of(unsigned __int128 v) {
+  int b = 0;
+  while (v) {
+    ++b;
+    v >>= 1;
+  }
+  return b;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------- geometry
+KeyGeom key_geometry_keyed(Index& ix) {
+  compute_alphabet(ix);
+  const uint64_t n = ix.n;
+  KeyGeom g{};
+  g.keyed = true;
+  g.R = (uint64_t)ix.sigma + 1;
+  int pbits = 1;
+  while ((1 << pbits) < ix.sigma + 1) ++pbits;
+  g.pb = pbits;
+  for (int c = 0; c < 256; ++c) g.lut[c] = ix.code_of[c] < 0 ? 0 : (uint16_t)(ix.code_of[c] + 1);
+  memset(g.inv, 0, sizeof(g.inv));
+  for (int k = 0; k < ix.sigma; ++k) g.inv[k + 1] = ix.syms[k];
+
+  // the last bytes of T' (short suffixes)
+  const uint64_t nt = std::min<uint64_t>(n, 70);
+  uint8_t tail[72] = {0};
+  HK_HIP(hipMemcpyAsync(tail, ix.text.as<uint8_t>() + (n - nt), nt, hipMemcpyDeviceToHost, ix.stream));
+  HK_HIP(hipStreamSynchronize(ix.stream));
+  const uint8_t term = tail[nt - 1];
+  const bool unkeyed = ix.byte_hist[term] == 1 && ix.sigma >= 2;
+  int codek[256];
+  int Rk = 0, m_term = 0;
+  for (int b = 0; b < 256; ++b) {
+    codek[b] = 0;
+    if (!ix.byte_hist[b] || (unkeyed && b == term)) continue;
+    if (b < term) ++m_term;
+    codek[b] = Rk++;
+  }
+  if (!unkeyed) m_term = 0;
+  g.Rk = (uint64_t)std::max(Rk, 2);
+  for (int b = 0; b < 256; ++b) g.lutk[b] = (uint16_t)(codek[b] | (b << 8));
+  double p2 = 0;
+  for (int b = 0; b < 256; ++b)
+    if (ix.byte_hist[b] && !(unkeyed && b == term)) {
+      const double f = (double)ix.byte_hist[b] / (double)n;
+      p2 += f * f;
+    }
+  // short-suffix keys for a given q; returns the sym bits (or 99 when they do not fit)
+  auto shorts = [&](int q, uint64_t* skey, uint64_t& s_start, unsigned __int128* span) -> int {
+    unsigned __int128 Rq = 1;
+    for (int i = 0; i < q; ++i) {
+      Rq *= g.Rk;
+      if (Rq > ((unsigned __int128)1 << 64)) return 99;
+    }
+    const uint64_t back = unkeyed ? (uint64_t)q : (uint64_t)q - 1;
+    s_start = n > back ? n - back : 0;
+    unsigned __int128 mx = Rq - 1;
+    for (uint64_t p = s_start; p < n; ++p) {
+      const uint64_t ul = unkeyed ? n - 1 - p : n - p;
+      unsigned __int128 v = 0;
+      for (uint64_t i = 0; i < ul; ++i) v = v * g.Rk + (unsigned)codek[tail[p + i - (n - nt)]];
+      v = v * g.Rk + (unsigned)(unkeyed ? m_term : 0);
+      for (uint64_t i = ul + 1; i < (uint64_t)q; ++i) v *= g.Rk;
+      if (skey) skey[p - s_start] = (uint64_t)v;
+      if (v > mx) mx = v;
+    }
+    if (span) *span = mx + 1;
+    return std::max(1, bits_of(mx));
+  };
+  // bucket = sym >> bsh: the largest shift that keeps the uniform-model mean bucket at <= 16.5k
+  // suffixes (one LDS sort holds 18432), with D = sb - bsh in [1, 16] (0 when one sort holds all)
+  auto shift_for = [&](int sb, unsigned __int128 span) -> int {
+    if (n <= (uint64_t)BS_CAP) return sb;
+    const double l = std::log2(16500.0 * (double)span / (double)n);
+    int b = (int)std::floor(l);
+    b = std::min(b, sb - 1);
+    b = std::max(b, sb - 16);
+    return std::max(b, 0);
+  };
+  int qn = 0, qw = 0, sbn = 0, sbw = 0, bsn = 0, bsw = 0;
+  for (int q = 1; q <= 64; ++q) {
+    uint64_t ss;
+    unsigned __int128 span = 0;
+    const int sb = shorts(q, nullptr, ss, &span);
+    if (sb == 99 || g.pb + sb > 64) break;
+    const int bs = shift_for(sb, span);
+    qw = q;
+    sbw = sb;
+    bsw = bs;
+    if (bs <= 32) {
+      qn = q;
+      sbn = sb;
+      bsn = bs;
+    }
+  }
+  if (qw == 0) throw ApiError{-6, "keyed geometry: no symbol count fits a 64-bit key"};
+  auto ties = [&](int q) { return std::min((double)n, (double)n * (double)n * std::pow(p2, (double)q)); };
+  const bool narrow = qn > 0 && (qn == qw || ties(qn) <= std::max(64.0, (double)n / 2048.0));
+  g.q = narrow ? qn : qw;
+  g.sym_bits = narrow ? sbn : sbw;
+  g.bucket_bits = g.sym_bits - (narrow ? bsn : bsw);
+  shorts(g.q, g.skey, g.s_start, nullptr);
+  g.nS = (uint32_t)(n - g.s_start);
+  // exact order of the short suffixes (bytes compare like Python str over latin-1 code points)
+  std::vector<uint64_t> ord(g.nS);
+  for (uint32_t i = 0; i < g.nS; ++i) ord[i] = g.s_start + i;
+  std::sort(ord.begin(), ord.end(), [&](uint64_t a, uint64_t b) {
+    const uint8_t* pa = tail + (a - (n - nt));
+    const uint8_t* pb2 = tail + (b - (n - nt));
+    const uint64_t la = n - a, lb = n - b;
+    const int c = memcmp(pa, pb2, std::min(la, lb));
+    return c < 0 || (c == 0 && la < lb);
+  });
+  for (uint32_t r = 0; r < g.nS; ++r) g.srank[ord[r] - g.s_start] = r;
+  g.key_bits = g.pb + g.sym_bits;
+  return g;
+}
+
+// ---------------------------------------------------------------- ties -> refinement
+template <typename V>
+void refine_from_ties(Index& ix, const KeyGeom& kg, uint64_t A, bool allow_doubling) {
+  if (A == 0) return;
+  hipStream_t s = ix.stream;
+  for (int i = 0; i < 2; ++i) {
+    ix.act[i][0].ensure(A * sizeof(V) + 16);
+    ix.act[i][1].ensure(A * 4 + 16);
+    ix.act[i][2].ensure(A * 4 + 16);
+  }
+  ix.head_slot.ensure(A * 4 + 16);
+  // order the list by slot: key = J << 1 | head
+  uint64_t* kp[2] = {ix.ties_k.as<uint64_t>(), ix.keys[1].as<uint64_t>()};
+  uint32_t* vp[2] = {ix.ties_v.as<uint32_t>(), ix.vals[1].as<uint32_t>()};
+  int hb = 1;
+  while (hb < 64 && ((ix.n << 1) >> hb)) ++hb;
+  const int sl = radix_sort_pairs<uint32_t>(ix.sw, ix.timer, kp, vp, 0, A, 0, hb, false, s);
+  uint32_t* P = reinterpret_cast<uint32_t*>(ix.act[0][0].as<V>());
+  uint32_t* J = ix.act[0][1].as<uint32_t>();
+  uint32_t* GH = ix.act[0][2].as<uint32_t>();
+  k_tie_split<<<grid_of(A), 256, 0, s>>>(kp[sl], vp[sl], A, P, J, GH);
+  HK_HIP(hipGetLastError());
+  uint64_t* hx = kp[sl ^ 1];   // u64 scratch (A + 1)
+  scan_exclusive_u32_to_u64(ix.sw, GH, hx, A, true, s);
+  k_tie_groups<<<grid_of(A), 256, 0, s>>>(hx, J, A, GH, ix.head_slot.as<uint32_t>());
+  HK_HIP(hipGetLastError());
+  uint64_t groups = 0;
+  HK_HIP(hipMemcpyAsync(&groups, hx + A, 8, hipMemcpyDeviceToHost, s));
+  HK_HIP(hipStreamSynchronize(s));
+  refine_loop<V>(ix, kg, 0, A, groups, allow_doubling);
+}
+
+template void refine_from_ties<uint32_t>(Index&, const KeyGeom&, uint64_t, bool);
+
+// ---------------------------------------------------------------- driver
+void build_sa_bucketed(Index& ix) {
+  const uint64_t n = ix.n;
+  hipStream_t s = ix.stream;
+  if (n >= 0xFFFFFFFFull) throw ApiError{-6, "single-GPU build supports n < 2^32 - 1"};
+  compute_alphabet(ix);
+  ix.info.assign(8, 0);
+  ix.sharded = false;
+  ix.sa_pos64 = false;
+  ix.have_sa = ix.have_bwt = ix.have_wt = false;
+  ix.sa.ensure(n * 4 + 16);
+  ix.bwt.ensure(n + 64);
+  if (n <= 1) {
+    HK_HIP(hipMemsetAsync(ix.sa.p, 0, 4, s));
+    HK_HIP(hipMemcpyAsync(ix.bwt.p, ix.text.p, n, hipMemcpyDeviceToDevice, s));
+    HK_HIP(hipStreamSynchronize(s));
+    ix.have_sa = ix.have_bwt = true;
+    return;
+  }
+  const KeyGeom kg = key_geometry_keyed(ix);
+  upload_geometry(ix, kg);
+  ix.info[3] = (uint64_t)kg.q;
+  const int D = kg.bucket_bits, sb = kg.sym_bits, pb = kg.pb;
+  const int bsh = sb - D;
+  const uint8_t* small = ix.small.as<uint8_t>();
+  const uint16_t* d_lutp = reinterpret_cast<const uint16_t*>(small + 2048);
+  const uint16_t* d_lutk = reinterpret_cast<const uint16_t*>(small + 2560);
+  const uint64_t* d_skey = reinterpret_cast<const uint64_t*>(small + 3584);
+  const uint8_t* d_inv = small + 3072;
+  KeyedArgs ka = keyed_args(kg, n);
+  {
+    // first hq symbols are exactly the top D bits when Rk = 2^k, k | D and no short key exceeds Rk^q - 1
+    const int lb = (kg.Rk & (kg.Rk - 1)) == 0 ? __builtin_ctzll(kg.Rk) : 0;
+    if (lb && D > 0 && D % lb == 0 && sb == lb * kg.q) ka.hq = D / lb;
+  }
+
+  // ---- 1. bucket histogram
+  const uint32_t nbins = 1u << D;
+  std::vector<uint64_t> hist(nbins, 0);
+  if (D > 0) {
+    ix.bk_hist.ensure((uint64_t)nbins * 8);
+    HK_HIP(hipMemsetAsync(ix.bk_hist.p, 0, (uint64_t)nbins * 8, s));
+    {
+      TimedLaunch t(ix.timer, "sa_bucket_hist", (double)n);
+      if (ka.hq > 0) {
+        const unsigned grid = (unsigned)std::min<uint64_t>(ceil_div(n, BH_TILE), 256);
+        k_bucket_hist<true><<<grid, BH_T, 0, s>>>(ix.text.as<uint8_t>(), n, d_lutk, d_skey, ka, bsh, D,
+                                                  ix.bk_hist.as<unsigned long long>());
+      } else {
+        const unsigned grid = (unsigned)std::min<uint64_t>(ceil_div(n, BH_STAGE), 256);
+        k_bucket_hist<false><<<grid, BH_T, 0, s>>>(ix.text.as<uint8_t>(), n, d_lutk, d_skey, ka, bsh, D,
+                                                   ix.bk_hist.as<unsigned long long>());
+      }
+      HK_HIP(hipGetLastError());
+    }
+    HK_HIP(hipMemcpyAsync(hist.data(), ix.bk_hist.p, (uint64_t)nbins * 8, hipMemcpyDeviceToHost, s));
+    HK_HIP(hipStreamSynchronize(s));
+  } else {
+    hist[0] = n;
+  }
+
+  // ---- 2. work items (whole buckets, packed while they fit) and big buckets
+  std::vector<uint2> items_n, items_w;
+  std::vector<uint64_t> big_start, big_cstart;
+  uint64_t big_total = 0;
+  {
+    const bool wide_geom = bsh > 32;
+    uint64_t off = 0, istart = 0, icnt = 0;
+    uint32_t ib0 = 0;
+    auto flush = [&](uint32_t last_b) {
+      if (!icnt) return;
+      const int wb = bsh + (last_b != ib0 ? 32 - __builtin_clz(last_b ^ ib0) : 0);
+      (wb > 32 ? items_w : items_n).push_back(make_uint2((uint32_t)istart, (uint32_t)icnt));
+      icnt = 0;
+    };
+    uint32_t prev_b = 0;
+    for (uint32_t b = 0; b < nbins; ++b) {
+      const uint64_t c = hist[b];
+      if (!c) continue;
+      if (c > (uint64_t)BS_CAP) {
+        flush(prev_b);
+        big_cstart.push_back(big_total);
+        big_start.push_back(off);
+        big_total += c;
+      } else {
+        const bool keep_narrow = !wide_geom && icnt &&
+                                 bsh + (32 - __builtin_clz(b ^ ib0)) > 32;
+        if (icnt && (icnt + c > (uint64_t)BS_CAP || keep_narrow)) flush(prev_b);
+        if (!icnt) {
+          istart = off;
+          ib0 = b;
+        }
+        icnt += c;
+        prev_b = b;
+      }
+      off += c;
+    }
+    flush(prev_b);
+  }
+  ix.info[4] = items_n.size() + items_w.size();
+  ix.info[5] = big_start.size();
+  ix.info[6] = big_total;
+
+  for (int i = 0; i < 2; ++i) {
+    ix.keys[i].ensure(n * 8 + 16);
+    ix.vals[i].ensure(n * 4 + 16);
+  }
+  uint64_t* kp[2] = {ix.keys[0].as<uint64_t>(), ix.keys[1].as<uint64_t>()};
+  uint32_t* vp[2] = {ix.vals[0].as<uint32_t>(), ix.vals[1].as<uint32_t>()};
+  {
+    TimedLaunch t(ix.timer, "sa_pack_keys", (double)n * 9);
+    const uint64_t g = std::min<uint64_t>(ceil_div(n, PKK_TILE), 4096);
+    k_pack_keyed<<<(unsigned)g, 256, 0, s>>>(ix.text.as<uint8_t>(), n, d_lutk, d_lutp, d_skey, ka, kp[0]);
+    HK_HIP(hipGetLastError());
+  }
+
+  if (big_total > n / 2) {
+    // skewed text: the global path (full LSD radix sort + refinement from the keys)
+    const int slot = radix_sort_pairs<uint32_t>(ix.sw, ix.timer, kp, vp, 0, n, pb, pb + sb, true, s);
+    ix.info[0] += ix.sw.passes_run;
+    ix.info[1] += ix.sw.passes_skipped;
+    std::swap(ix.sa, ix.vals[slot]);
+    ix.vals[slot].ensure(n * 4 + 16);
+    ix.info[7] = 1;
+    refine_after_sort<uint32_t>(ix, kg, slot, n, true);
+    HK_HIP(hipStreamSynchronize(s));
+    ix.have_sa = ix.have_bwt = true;
+    return;
+  }
+
+  // ---- 3. LSD passes over the top D bits (digit histograms are marginals of the bucket histogram)
+  int slot = 0;
+  if (D > 0) {
+    uint64_t h0[256] = {0};
+    const int lowd = std::min(D, 8);
+    for (uint32_t b = 0; b < nbins; ++b) h0[b & ((1u << lowd) - 1)] += hist[b];
+    uint64_t* d_h0 = reinterpret_cast<uint64_t*>(ix.small.as<uint8_t>() + 5120);
+    HK_HIP(hipMemcpyAsync(d_h0, h0, sizeof(h0), hipMemcpyHostToDevice, s));
+    slot = radix_sort_pairs<uint32_t>(ix.sw, ix.timer, kp, vp, 0, n, pb + bsh, pb + sb, true, s, d_h0);
+    ix.info[0] += ix.sw.passes_run;
+    ix.info[1] += ix.sw.passes_skipped;
+  } else {
+    fill_iota<uint32_t>(vp[0], n, s);
+  }
+
+  // ---- 4. LDS sorts of the buckets
+  ix.ties_k.ensure(n * 8 + 16);
+  ix.ties_v.ensure(n * 4 + 16);
+  ix.ties_n.ensure(16);
+  HK_HIP(hipMemsetAsync(ix.ties_n.p, 0, 8, s));
+  {
+    const uint64_t ni = items_n.size() + items_w.size();
+    ix.bk_items.ensure(ni * sizeof(uint2) + 16);
+    if (!items_n.empty())
+      HK_HIP(hipMemcpyAsync(ix.bk_items.p, items_n.data(), items_n.size() * sizeof(uint2), hipMemcpyHostToDevice, s));
+    if (!items_w.empty())
+      HK_HIP(hipMemcpyAsync(ix.bk_items.as<uint2>() + items_n.size(), items_w.data(), items_w.size() * sizeof(uint2),
+                            hipMemcpyHostToDevice, s));
+    TimedLaunch t(ix.timer, "sa_bucket_sort", (double)(n - big_total) * (8 + 4 + 4 + 1));
+    static const bool trace = getenv("HKCSA_BS_TRACE") != nullptr;   // diagnostic phase stamps
+    DevBuf tbuf;
+    if (trace) tbuf.ensure(ni * 64 + 64);
+    uint64_t* tr = tbuf.as<uint64_t>();
+    if (!items_n.empty()) {
+      if (trace)
+        k_bucket_sort<false, true><<<(unsigned)items_n.size(), BS_T, 0, s>>>(
+            kp[slot], vp[slot], ix.bk_items.as<uint2>(), pb, sb, d_inv, ix.sa.as<uint32_t>(), ix.bwt.as<uint8_t>(),
+            ix.ties_k.as<uint64_t>(), ix.ties_v.as<uint32_t>(), ix.ties_n.as<unsigned long long>(), tr);
+      else
+        k_bucket_sort<false><<<(unsigned)items_n.size(), BS_T, 0, s>>>(
+            kp[slot], vp[slot], ix.bk_items.as<uint2>(), pb, sb, d_inv, ix.sa.as<uint32_t>(), ix.bwt.as<uint8_t>(),
+            ix.ties_k.as<uint64_t>(), ix.ties_v.as<uint32_t>(), ix.ties_n.as<unsigned long long>(), nullptr);
+    }
+    if (!items_w.empty())
+      k_bucket_sort<true><<<(unsigned)items_w.size(), BS_T, 0, s>>>(
+          kp[slot], vp[slot], ix.bk_items.as<uint2>() + items_n.size(), pb, sb, d_inv, ix.sa.as<uint32_t>(),
+          ix.bwt.as<uint8_t>(), ix.ties_k.as<uint64_t>(), ix.ties_v.as<uint32_t>(),
+          ix.ties_n.as<unsigned long long>(), nullptr);
+    HK_HIP(hipGetLastError());
+    if (trace && !items_n.empty()) {
+      std::vector<uint64_t> h(items_n.size() * 8);
+      HK_HIP(hipMemcpyAsync(h.data(), tr, h.size() * 8, hipMemcpyDeviceToHost, s));
+      HK_HIP(hipStreamSynchronize(s));
+      double acc[5] = {0, 0, 0, 0, 0};
+      uint64_t t_lo = ~0ull, t_hi = 0;
+      for (size_t w = 0; w < items_n.size(); ++w) {
+        for (int i = 0; i < 5; ++i) acc[i] += (double)(h[w * 8 + i + 1] - h[w * 8 + i]);
+        t_lo = std::min(t_lo, h[w * 8]);
+        t_hi = std::max(t_hi, h[w * 8 + 5]);
+      }
+      fprintf(stderr, "[bucket_sort trace] %zu WGs, mean cycles: load %.0f, passes %.0f, ties %.0f, "
+              "stage %.0f, out %.0f; span %.3g cycles\n", items_n.size(), acc[0] / items_n.size(),
+              acc[1] / items_n.size(), acc[2] / items_n.size(), acc[3] / items_n.size(), acc[4] / items_n.size(),
+              (double)(t_hi - t_lo));
+    }
+  }
+  uint64_t ntie = 0;
+  HK_HIP(hipMemcpyAsync(&ntie, ix.ties_n.p, 8, hipMemcpyDeviceToHost, s));
+  HK_HIP(hipStreamSynchronize(s));
+
+  // ---- 5. big buckets on the global path
+  if (big_total) {
+    const uint32_t nbig = (uint32_t)big_start.size();
+    int gbits = 1;
+    while ((1ull << gbits) < nbig) ++gbits;
+    const int lowbits = pb + bsh;
+    for (int i = 0; i < 2; ++i) {
+      ix.big_k[i].ensure(big_total * 8 + 16);
+      ix.big_v[i].ensure(big_total * 4 + 16);
+    }
+    ix.big_j.ensure(big_total * 4 + 16);
+    ix.tile_a.ensure(nbig * 8 + 16);
+    ix.tile_c.ensure(nbig * 8 + 16);
+    HK_HIP(hipMemcpyAsync(ix.tile_a.p, big_start.data(), nbig * 8, hipMemcpyHostToDevice, s));
+    HK_HIP(hipMemcpyAsync(ix.tile_c.p, big_cstart.data(), nbig * 8, hipMemcpyHostToDevice, s));
+    {
+      TimedLaunch t(ix.timer, "sa_big_gather", (double)big_total * (12 + 16));
+      k_big_gather<<<grid_of(big_total), 256, 0, s>>>(kp[slot], vp[slot], ix.tile_a.as<uint64_t>(),
+                                                     ix.tile_c.as<uint64_t>(), nbig, big_total, lowbits,
+                                                     ix.big_k[0].as<uint64_t>(), ix.big_v[0].as<uint32_t>(),
+                                                     ix.big_j.as<uint32_t>());
+      HK_HIP(hipGetLastError());
+    }
+    uint64_t* bk[2] = {ix.big_k[0].as<uint64_t>(), ix.big_k[1].as<uint64_t>()};
+    uint32_t* bv[2] = {ix.big_v[0].as<uint32_t>(), ix.big_v[1].as<uint32_t>()};
+    const int bsl = radix_sort_pairs<uint32_t>(ix.sw, ix.timer, bk, bv, 0, big_total, pb, lowbits + gbits, false, s);
+    ix.info[0] += ix.sw.passes_run;
+    ix.info[1] += ix.sw.passes_skipped;
+    for (int i = 0; i < 3; ++i) ix.act[0][i].ensure(big_total * 4 + 16);
+    ix.head_slot.ensure(big_total * 4 + 16);
+    const auto r = refine_step_u32(ix, kg, bk[bsl], bv[bsl], ix.big_j.as<uint32_t>(), big_total, pb,
+                                   ix.act[0][0].as<uint32_t>(), ix.act[0][1].as<uint32_t>(),
+                                   ix.act[0][2].as<uint32_t>());
+    if (r.first) {
+      k_tie_append<<<grid_of(r.first), 256, 0, s>>>(ix.act[0][0].as<uint32_t>(), ix.act[0][1].as<uint32_t>(),
+                                                   ix.act[0][2].as<uint32_t>(), r.first, ntie,
+                                                   ix.ties_k.as<uint64_t>(), ix.ties_v.as<uint32_t>());
+      HK_HIP(hipGetLastError());
+      ntie += r.first;
+    }
+  }
+  ix.info.push_back(ntie);
+
+  // ---- 6. refinement of the ties
+  refine_from_ties<uint32_t>(ix, kg, ntie, true);
+  HK_HIP(hipStreamSynchronize(s));
+  ix.have_sa = true;
+  ix.have_bwt = true;
+}
+
+}  // namespace hk

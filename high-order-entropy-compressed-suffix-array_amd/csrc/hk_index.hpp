@@ -2,6 +2,7 @@
 #pragma once
 
 #include <cstring>
+#include <utility>
 
 #include "hk_sort.hpp"
 
@@ -10,6 +11,7 @@ namespace hk {
 constexpr int kMaxLevels = 8;
 constexpr uint32_t kFlagPos64 = 1u;   // hkcsa_opts.flags: 64-bit positions in sharded builds at any n
 constexpr uint32_t kFlagNoSplit = 2u; // ... and sort them as whole u64 values (no split low/high halves)
+constexpr uint32_t kFlagGlobalSort = 4u; // single GPU: full LSD sort of the keys (no bucket sorts)
 constexpr int kLineBits = 448;   // 7 data words per 64-B rank line (word 0 = ones before the line)
 
 struct WtTables {                // per level, per dense code (host mirror of the device tables)
@@ -26,6 +28,20 @@ struct KeyGeom {
   uint64_t R = 2;
   uint16_t lut[256];   // byte -> dense code + 1 (0 = end of text)
   uint8_t inv[512];    // dense code + 1 -> byte
+  // ---- keyed layout (single-GPU bucket build, hk_bucket.hip).  The sorted field is the first q
+  // symbols in radix Rk over the *keyed* alphabet: every symbol except a terminal that occurs
+  // once, at n-1 (the reference's '$').  There is no end-of-text code.  The suffixes whose
+  // q-window reaches the end or the unkeyed terminal ("short" suffixes, positions
+  // [s_start, n), at most q of them) get the exact boundary key B(s) (the smallest window value
+  // that sorts after them) and are ordered among themselves by srank in the first refinement.
+  bool keyed = false;
+  uint64_t Rk = 2;
+  uint16_t lutk[256];        // byte -> keyed code in the low byte | byte << 8
+  uint64_t s_start = 0;      // first short suffix
+  uint32_t nS = 0;           // n - s_start
+  uint64_t skey[72];         // B(s) of the short suffixes (sym field, not shifted)
+  uint32_t srank[72];        // exact order of the short suffixes among themselves
+  int bucket_bits = 0;       // D: top bits of the sym field sorted by the LSD passes
 };
 int mixed_radix_bits(uint64_t R, int q);   // bits of R^q - 1 (65 when it does not fit 64 bits)
 
@@ -75,6 +91,9 @@ struct Index {
   DevBuf isa;
   DevBuf act[2][3];            // P, J, G of the active list (double-buffered)
   DevBuf head_slot;            // SA slot of each tied group's head (refinement -> doubling switch)
+  DevBuf ties_k, ties_v, ties_n;   // unordered tie list of the bucket build (J<<1|head, P), count
+  DevBuf big_k[2], big_v[2], big_j; // big buckets of the bucket build (sorted on the global path)
+  DevBuf bk_items, bk_hist;       // bucket work items, bucket histogram
   DevBuf tile_a, tile_b, tile_c, tile_d;
   DevBuf small;                // scratch for totals etc.
   DevBuf seq[2];               // WT level code sequences
@@ -151,6 +170,17 @@ void comm_unique_id(uint8_t id[128]);
 
 // shared by the single-GPU and sharded builds
 KeyGeom key_geometry(Index& ix, bool with_prev);
+KeyGeom key_geometry_keyed(Index& ix);   // keyed layout (hk_bucket.hip)
+void build_sa_bucketed(Index& ix);       // single-GPU SA + BWT: 2 LSD passes + LDS bucket sorts
+// tie list (J << 1 | head, P) of m entries in (k, v) -> refinement loop (from symbol offset h)
+template <typename V>
+void refine_from_ties(Index& ix, const KeyGeom& kg, uint64_t A, bool allow_doubling);
+template <typename V>
+void refine_loop(Index& ix, const KeyGeom& kg, int cur, uint64_t A, uint64_t groups, bool allow_doubling);
+// SA/BWT of A sorted (keys, P) at slots J; ties (compared >> cs) compacted to (oP, oJ, oG)
+std::pair<uint64_t, uint64_t> refine_step_u32(Index& ix, const KeyGeom& kg, const uint64_t* keys,
+                                              const uint32_t* P, const uint32_t* J, uint64_t A, int cs,
+                                              uint32_t* oP, uint32_t* oJ, uint32_t* oG);
 void upload_geometry(Index& ix, const KeyGeom& kg);
 void pack_keys(const uint8_t* d_text, uint64_t n, uint64_t lo, uint64_t count, const uint16_t* d_lut, uint64_t R,
                int q, int pb, uint64_t* d_keys, hipStream_t s, uint64_t* d_hist0 = nullptr);

@@ -283,30 +283,41 @@ __global__ __launch_bounds__(GR_T) void k_refine_apply(
   }
 }
 
-// chunk refinement key: (group ordinal << (64-gbits)) | next qn codes of the suffix from offset h (radix R)
+// chunk refinement key: (group ordinal << (64-gbits)) | next qn codes of the suffix from offset h (radix R).
+// Keyed layout: short suffixes (p >= s_start) tied with others in the first round take their exact
+// rank among the short suffixes (srank < nS); every other chunk is offset by nS, so a short
+// suffix sorts before the equal-key long suffixes (its boundary key B(s) is the smallest window
+// value that sorts after it).
 template <typename V>
 __global__ __launch_bounds__(256) void k_refine_keys(const V* __restrict__ P, const uint32_t* __restrict__ G,
                                                      uint64_t A, const uint8_t* __restrict__ t, uint64_t n,
                                                      const uint16_t* __restrict__ lut, uint64_t R, int qn, int gbits,
-                                                     uint64_t h, uint64_t* __restrict__ keys, V* __restrict__ vals) {
+                                                     uint64_t h, uint64_t* __restrict__ keys, V* __restrict__ vals,
+                                                     uint64_t s_start, uint32_t nS,
+                                                     const uint32_t* __restrict__ srank) {
   __shared__ uint16_t L[256];
   L[threadIdx.x] = lut[threadIdx.x];
   __syncthreads();
   for (uint64_t a = (uint64_t)blockIdx.x * 256 + threadIdx.x; a < A; a += (uint64_t)gridDim.x * 256) {
     const V p = P[a];
-    const uint64_t s = (uint64_t)p + h;
     uint64_t chunk = 0;
-    // the qn symbols from s, read as aligned 32-bit words (the text buffer has >= 64 bytes of pad)
-    const uint64_t w0 = s & ~3ull;
-    uint32_t word = s < n ? *reinterpret_cast<const uint32_t*>(t + w0) : 0u;
-    uint64_t wpos = w0;
-    for (int j = 0; j < qn; ++j) {
-      const uint64_t x = s + j;
-      if ((x & ~3ull) != wpos) {
-        wpos = x & ~3ull;
-        word = wpos < n ? *reinterpret_cast<const uint32_t*>(t + wpos) : 0u;
+    if ((uint64_t)p >= s_start) {
+      chunk = srank[(uint64_t)p - s_start];
+    } else {
+      const uint64_t s = (uint64_t)p + h;
+      // the qn symbols from s, read as aligned 32-bit words (the text buffer has >= 64 bytes of pad)
+      const uint64_t w0 = s & ~3ull;
+      uint32_t word = s < n ? *reinterpret_cast<const uint32_t*>(t + w0) : 0u;
+      uint64_t wpos = w0;
+      for (int j = 0; j < qn; ++j) {
+        const uint64_t x = s + j;
+        if ((x & ~3ull) != wpos) {
+          wpos = x & ~3ull;
+          word = wpos < n ? *reinterpret_cast<const uint32_t*>(t + wpos) : 0u;
+        }
+        chunk = chunk * R + (x < n ? L[(word >> (8 * (x & 3))) & 255u] : 0u);
       }
-      chunk = chunk * R + (x < n ? L[(word >> (8 * (x & 3))) & 255u] : 0u);
+      chunk += nS;
     }
     keys[a] = gbits ? (((uint64_t)G[a] << (64 - gbits)) | chunk) : chunk;
     vals[a] = p;
@@ -615,17 +626,25 @@ void upload_geometry(Index& ix, const KeyGeom& kg) {
   ix.small.ensure(8192);
   HK_HIP(hipMemcpyAsync(ix.small.as<uint8_t>() + 2048, kg.lut, 512, hipMemcpyHostToDevice, ix.stream));
   HK_HIP(hipMemcpyAsync(ix.small.as<uint8_t>() + 3072, kg.inv, 512, hipMemcpyHostToDevice, ix.stream));
+  if (kg.keyed) {   // small+2560 = lutk (u16[256]), +3584 = skey (u64[72]), +7168 = srank (u32[72])
+    HK_HIP(hipMemcpyAsync(ix.small.as<uint8_t>() + 2560, kg.lutk, 512, hipMemcpyHostToDevice, ix.stream));
+    HK_HIP(hipMemcpyAsync(ix.small.as<uint8_t>() + 3584, kg.skey, sizeof(kg.skey), hipMemcpyHostToDevice,
+                          ix.stream));
+    HK_HIP(hipMemcpyAsync(ix.small.as<uint8_t>() + 7168, kg.srank, sizeof(kg.srank), hipMemcpyHostToDevice,
+                          ix.stream));
+  }
+  HK_HIP(hipStreamSynchronize(ix.stream));   // kg may be a host temporary
 }
+
+template <typename V>
+void refine_loop(Index& ix, const KeyGeom& kg, int cur, uint64_t A, uint64_t groups, bool allow_doubling);
 
 // Refinement of tied groups after the initial sort of m suffixes (their sorted keys in keys[slot],
 // positions in vals[slot] — which the caller has adopted as ix.sa).  With allow_doubling (single
 // GPU, u32 positions) the loop switches to ISA-based prefix doubling after kChunkRounds rounds.
 template <typename V>
 void refine_after_sort(Index& ix, const KeyGeom& kg, int slot, uint64_t m, bool allow_doubling) {
-  hipStream_t s = ix.stream;
-  const uint16_t* d_lut = reinterpret_cast<const uint16_t*>(ix.small.as<uint8_t>() + 2048);
   uint64_t* kp[2] = {ix.keys[0].as<uint64_t>(), ix.keys[1].as<uint64_t>()};
-  V* vp[2] = {ix.vals[0].as<V>(), ix.vals[1].as<V>()};
   for (int i = 0; i < 2; ++i) {
     ix.act[i][0].ensure(m * sizeof(V) + 16);
     ix.act[i][1].ensure(m * 4 + 16);
@@ -633,13 +652,25 @@ void refine_after_sort(Index& ix, const KeyGeom& kg, int slot, uint64_t m, bool 
   }
   ix.head_slot.ensure(m * 4 + 16);
   ix.bwt.ensure(m + 64);
-  int cur = 0;
   // initial round: keys compared without the prev field; SA already in place; BWT from keys
   auto r0 = refine_step<V>(ix, kg, kp[slot], ix.sa.as<V>(), nullptr, m, kg.pb, true, false,
-                           ix.act[cur][0].as<V>(), ix.act[cur][1].as<uint32_t>(), ix.act[cur][2].as<uint32_t>(),
+                           ix.act[0][0].as<V>(), ix.act[0][1].as<uint32_t>(), ix.act[0][2].as<uint32_t>(),
                            ix.head_slot.as<uint32_t>());
-  uint64_t A = r0.first, groups = r0.second;
-  ix.info.push_back(A);
+  ix.info.push_back(r0.first);
+  refine_loop<V>(ix, kg, 0, r0.first, r0.second, allow_doubling);
+}
+
+// The tied suffixes (P, J = SA slot, G = dense group ordinal in slot order) are in act[cur];
+// each round sorts them by (G, next symbols from offset h) and re-groups.
+template <typename V>
+void refine_loop(Index& ix, const KeyGeom& kg, int cur, uint64_t A, uint64_t groups, bool allow_doubling) {
+  hipStream_t s = ix.stream;
+  const uint16_t* d_lut = reinterpret_cast<const uint16_t*>(ix.small.as<uint8_t>() + 2048);
+  const uint32_t* d_srank = reinterpret_cast<const uint32_t*>(ix.small.as<uint8_t>() + 7168);
+  const uint64_t s_start = kg.keyed ? kg.s_start : ~0ull;
+  const uint32_t nS = kg.keyed ? kg.nS : 0u;
+  uint64_t* kp[2] = {ix.keys[0].as<uint64_t>(), ix.keys[1].as<uint64_t>()};
+  V* vp[2] = {ix.vals[0].as<V>(), ix.vals[1].as<V>()};
   uint64_t h = (uint64_t)kg.q;
   int rounds = 0;
   while (A > 0) {
@@ -647,14 +678,21 @@ void refine_after_sort(Index& ix, const KeyGeom& kg, int slot, uint64_t m, bool 
     if (allow_doubling && rounds > kChunkRounds) break;
     int gbits = 0;
     while (gbits < 64 && (1ull << gbits) < groups) ++gbits;
+    auto fits = [&](int qq) {   // G in the top gbits, chunk + nS (<= R^qq - 1 + nS) below
+      if (mixed_radix_bits(kg.R, qq) > 64 - gbits) return false;
+      unsigned __int128 top = 1;
+      for (int i = 0; i < qq; ++i) top *= kg.R;
+      top = top - 1 + nS;
+      return top < ((unsigned __int128)1 << (64 - gbits));
+    };
     int qn = 0;
-    while (gbits + mixed_radix_bits(kg.R, qn + 1) <= 64) ++qn;
+    while (qn < 64 && fits(qn + 1)) ++qn;
     if (qn < 1) throw ApiError{-6, "too many tied groups for one refinement key"};
     {
       TimedLaunch tm(ix.timer, "sa_refine_keys", (double)A * (sizeof(V) * 2 + 4 + 8));
       k_refine_keys<V><<<grid_for(A), 256, 0, s>>>(ix.act[cur][0].as<V>(), ix.act[cur][2].as<uint32_t>(), A,
                                                    ix.text.as<uint8_t>(), ix.n, d_lut, kg.R, qn, gbits, h, kp[0],
-                                                   vp[0]);
+                                                   vp[0], s_start, nS, d_srank);
       HK_HIP(hipGetLastError());
     }
     const int sl = radix_sort_pairs<V>(ix.sw, ix.timer, kp, vp, 0, A, 0, 64, false, s);
@@ -712,6 +750,14 @@ void refine_after_sort(Index& ix, const KeyGeom& kg, int slot, uint64_t m, bool 
 
 template void refine_after_sort<uint32_t>(Index&, const KeyGeom&, int, uint64_t, bool);
 template void refine_after_sort<uint64_t>(Index&, const KeyGeom&, int, uint64_t, bool);
+std::pair<uint64_t, uint64_t> refine_step_u32(Index& ix, const KeyGeom& kg, const uint64_t* keys,
+                                              const uint32_t* P, const uint32_t* J, uint64_t A, int cs,
+                                              uint32_t* oP, uint32_t* oJ, uint32_t* oG) {
+  return refine_step<uint32_t>(ix, kg, keys, P, J, A, cs, false, true, oP, oJ, oG, ix.head_slot.as<uint32_t>());
+}
+
+template void refine_loop<uint32_t>(Index&, const KeyGeom&, int, uint64_t, uint64_t, bool);
+template void refine_loop<uint64_t>(Index&, const KeyGeom&, int, uint64_t, uint64_t, bool);
 
 void pack_keys(const uint8_t* d_text, uint64_t n, uint64_t lo, uint64_t count, const uint16_t* d_lut, uint64_t R,
                int q, int pb, uint64_t* d_keys, hipStream_t s, uint64_t* d_hist0) {
@@ -763,6 +809,10 @@ void compute_alphabet(Index& ix) {
 }
 
 void build_sa(Index& ix) {
+  if (!(ix.flags & kFlagGlobalSort)) {
+    build_sa_bucketed(ix);
+    return;
+  }
   const uint64_t n = ix.n;
   hipStream_t s = ix.stream;
   if (n >= 0xFFFFFFFFull) throw ApiError{-6, "single-GPU build supports n < 2^32 - 1"};

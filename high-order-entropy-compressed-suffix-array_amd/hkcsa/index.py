@@ -76,6 +76,7 @@ class QuerySet:
 
 
 FLAG_POS64 = 1   # HKCSA_FLAG_POS64: 64-bit positions in sharded builds at any n
+FLAG_GLOBAL_SORT = 4   # HKCSA_FLAG_GLOBAL_SORT: single-GPU build by full-width LSD sort (no bucket sorts)
 
 
 class DeviceIndex:

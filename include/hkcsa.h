@@ -47,6 +47,8 @@ typedef struct hkcsa_queries hkcsa_queries;
 #define HKCSA_FLAG_POS64 1u    /* sharded builds keep 64-bit positions at any n             */
 #define HKCSA_FLAG_NO_SPLIT 2u /* sort 64-bit positions whole (default: u32 low halves, the  */
                                /* high bits parked below the key)                           */
+#define HKCSA_FLAG_GLOBAL_SORT 4u /* single-GPU build: full-width LSD radix sort of every     */
+                                  /* suffix key (default: top-bit passes + LDS bucket sorts) */
 
 typedef struct hkcsa_opts {
   int32_t device;   /* HIP device ordinal (-1 = current)                 */
@@ -218,8 +220,10 @@ int hkcsa_timing_reset(hkcsa_index* ix);
  * alg_bytes is the algorithmic byte count summed over launches. */
 int hkcsa_kernel_stats(hkcsa_index* ix, const char* name, uint64_t* launches, double* total_ms,
                        double* alg_bytes);
-/* Build-stage counters of the last build: radix passes run / skipped,
- * doubling rounds, active elements per round (up to 64). */
+/* Build-stage counters of the last build: [0] radix passes run, [1] skipped,
+ * [2] refinement rounds (doubling rounds << 32), [3] symbols per key; bucket build:
+ * [4] LDS work items, [5] big buckets, [6] suffixes in big buckets, [7] 1 = global path;
+ * then tied suffixes per round (up to cap). */
 int hkcsa_build_info(hkcsa_index* ix, uint64_t* info, int cap);
 
 #ifdef __cplusplus
