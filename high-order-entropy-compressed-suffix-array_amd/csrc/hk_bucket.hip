@@ -183,25 +183,27 @@ __global__ __launch_bounds__(256) void k_pack_keyed(const uint8_t* __restrict__ 
 
 // ------------------------------------------------------------ 4. LDS bucket sort
 constexpr int BS_T = 1024;
-constexpr int BS_W = BS_T / 64;
-constexpr int BS_I = 18;
+constexpr int BS_W = BS_T / 64;       // 16 waves
+constexpr int BS_I = 18;              // suffixes per thread
+constexpr int BS_H = BS_I / 2;        // 16-bit per-item values are packed two to a register
 constexpr int BS_CAP = BS_T * BS_I;   // 18432 suffixes per workgroup
 constexpr int BS_WSPAN = BS_I * 64;
+constexpr int BS_V = BS_W;            // per-wave digit histograms, in element order
 
 struct BsShared {
-  uint32_t buf[BS_CAP];          // exchange buffer (one u32 plane at a time)
-  uint16_t prev[BS_CAP];         // BWT code (prev field, <= 9 bits) of each suffix, by original slot
-  uint32_t whist[BS_W][256];     // per-wave digit counts -> per-wave exclusive prefix
-  uint32_t tstart[256];          // block-wide exclusive digit start
+  uint32_t buf[BS_CAP];          // u32 plane: local key exchange; positions at the end
+  uint16_t aux[BS_CAP];          // u16 plane: original-slot exchange (prev codes packed in the key),
+                                 // or the prev codes by original slot (when they do not fit the key)
+  uint64_t mt[BS_W][256];        // per-wave match masks (lanes holding a digit), zero between items;
+                                 // mt[0..1] double as the scan's per-group prefixes
+  uint32_t whist[BS_V][256];     // digit counts per wave -> destination base per wave
+  uint32_t wloc[256];            // scan: wave-local exclusive digit start
   uint32_t wsum[4];
   uint64_t rv[2][BS_W];
-  uint8_t inv[512];
+  uint8_t inv[256];
 };
 
-// One workgroup sorts items[blockIdx.x] = {start, count} of the bucket-grouped (keys, vals):
-// radix passes over the key bits that vary inside the range (LDS exchange of the local key planes
-// and of index|prev), then SA[start + r] / BWT[start + r] in sorted order, ties to the list.
-// diagnostic stamps (TRACE): shader-clock time at the phase boundaries of workgroup 0's wave 0
+// diagnostic stamps (TRACE): shader-clock time at the phase boundaries
 __device__ __forceinline__ uint64_t stamp() {
   uint64_t t;
   __builtin_amdgcn_sched_barrier(0);
@@ -210,6 +212,12 @@ __device__ __forceinline__ uint64_t stamp() {
   return t;
 }
 
+// One workgroup sorts items[blockIdx.x] = {start, count} of the bucket-grouped (keys, vals): LSD
+// radix passes over the key bits that vary inside the range (wave ballot ranking in two
+// independent chains per thread, one 1024-thread scan of the 32 x 256 counts, LDS exchange of the
+// local key and original-slot planes), then SA[start + r] / BWT[start + r] in sorted order and
+// equal keys to the tie list.  The BWT code rides in the key word above the varying bits when it
+// fits (one exchange phase per pass), else it waits in LDS by original slot.
 template <bool WIDE, bool TRACE = false>
 __global__ __launch_bounds__(BS_T, 1) void k_bucket_sort(const uint64_t* __restrict__ keys,
                                                          const uint32_t* __restrict__ vals,
@@ -237,19 +245,18 @@ __global__ __launch_bounds__(BS_T, 1) void k_bucket_sort(const uint64_t* __restr
   for (int k = 0; k < BS_I; ++k) vmask |= (s0 + 64u * k < cnt ? 1u : 0u) << k;
   const uint64_t symmask = sb >= 64 ? ~0ull : ((1ull << sb) - 1);
   const uint32_t pmask = (1u << pb) - 1;
-  if (tid < 512) sh.inv[tid] = inv[tid];
+  if (tid < 256) sh.inv[tid] = inv[tid];
+  for (uint32_t i = tid; i < BS_V * 256; i += BS_T) (&sh.whist[0][0])[i] = 0;
+  for (uint32_t i = tid; i < BS_W * 256; i += BS_T) (&sh.mt[0][0])[i] = 0;
 
-  // ---- load (original order: slot e = wv*WSPAN + k*64 + lane) and the varying-bit range; the
-  // positions are gathered by original slot at the end (fewer live registers through the passes)
+  // ---- load (original order) and the varying-bit range of the sym fields
   uint64_t key[BS_I];
   uint64_t vor = 0, vand = ~0ull;
 #pragma unroll
-  for (int k = 0; k < BS_I; ++k) {
-    key[k] = ((vmask >> k) & 1u) ? kb[s0 + 64u * k] : 0;
-  }
+  for (int k = 0; k < BS_I; ++k) key[k] = ((vmask >> k) & 1u) ? kb[s0 + 64u * k] : 0;
 #pragma unroll
   for (int k = 0; k < BS_I; ++k) {
-    if (((vmask >> k) & 1u)) {
+    if ((vmask >> k) & 1u) {
       const uint64_t sym = (key[k] >> pb) & symmask;
       vor |= sym;
       vand &= sym;
@@ -272,160 +279,194 @@ __global__ __launch_bounds__(BS_T, 1) void k_bucket_sort(const uint64_t* __restr
     vor |= sh.rv[0][w];
     vand &= sh.rv[1][w];
   }
-  // prev fields by original slot (read back by the sorted index at the end)
-#pragma unroll
-  for (int k = 0; k < BS_I; ++k)
-    if ((vmask >> k) & 1u) sh.prev[s0 + 64u * k] = (uint16_t)((uint32_t)key[k] & pmask);
-  if (TRACE) ts[1] = stamp();
   const uint64_t var = vor ^ vand;
   const int lo = var ? __builtin_ctzll(var) : 0;
   const int width = var ? 64 - __builtin_clzll(var) - lo : 0;
+  const bool packprev = !WIDE && width + pb <= 32;
+  const uint32_t kmask = width >= 32 ? ~0u : ((1u << width) - 1);
 
   // live through the passes: the local key plane(s) and the original slot, 16 bits per item
-  // packed two to a register (as are the per-pass ranks) — 36 registers narrow, 54 wide
-  constexpr int BS_H = (BS_I + 1) / 2;
+  // packed two to a register (as are the per-pass ranks)
   uint32_t klo[BS_I], khi[BS_I], ix2[BS_H];
 #pragma unroll
   for (int k = 0; k < BS_I; ++k) {
-    const uint64_t lk = ((key[k] >> pb) & symmask) >> lo;
-    klo[k] = (uint32_t)lk;
+    // varying bits only (the constant bits above them would collide with the packed prev code)
+    const uint64_t lk = (((key[k] >> pb) & symmask) >> lo) & (width >= 64 ? ~0ull : ((1ull << width) - 1));
+    const uint32_t pv = (uint32_t)key[k] & pmask;
+    klo[k] = (uint32_t)lk | (packprev ? pv << width : 0u);
     khi[k] = WIDE ? (uint32_t)(lk >> 32) : 0u;
+    if (!packprev && ((vmask >> k) & 1u)) sh.aux[s0 + 64u * k] = (uint16_t)pv;
   }
+  // ix2[j] = original slots of items j (low half) and j + BS_H (high half)
 #pragma unroll
-  for (int h = 0; h < BS_H; ++h)
-    ix2[h] = (s0 + 128u * h) | (2 * h + 1 < BS_I ? (s0 + 128u * h + 64u) << 16 : 0u);
+  for (int j = 0; j < BS_H; ++j) ix2[j] = (s0 + 64u * j) | ((s0 + 64u * (j + BS_H)) << 16);
   uint16_t* buf16 = reinterpret_cast<uint16_t*>(sh.buf);
+  __syncthreads();
+  if (TRACE) ts[1] = stamp();
 
-  auto digit_of = [](uint32_t lo32, uint32_t hi32, int d) -> uint32_t {
-    if (!WIDE) return (lo32 >> d) & 255u;
-    return (uint32_t)((((uint64_t)hi32 << 32) | lo32) >> d) & 255u;
+  auto half = [](const uint32_t* a2, int k) -> uint32_t {
+    return k < BS_H ? (a2[k] & 0xFFFFu) : (a2[k - BS_H] >> 16);
   };
   // ---- radix passes over the varying bits (uniform digits skipped)
   for (int d0 = 0; d0 < width; d0 += 8) {
     const uint32_t dmask = (uint32_t)((var >> lo) >> d0) & 255u;
     if (!dmask) continue;
     const int nb = 32 - __clz(dmask);   // highest varying bit of the digit + 1
-    asm volatile("" : "+v"(s0));   // slot addresses are cheap: recompute them per pass, do not keep 18
-    for (uint32_t i = tid; i < BS_W * 256; i += BS_T) (&sh.whist[0][0])[i] = 0;
-    __syncthreads();
+    const uint32_t dm = (1u << nb) - 1;
+    auto digit_of = [&](int k) -> uint32_t {
+      if (!WIDE) return (klo[k] >> d0) & dm;
+      return (uint32_t)((((uint64_t)khi[k] << 32) | klo[k]) >> d0) & dm;
+    };
+    asm volatile("" : "+v"(s0));   // slot addresses are cheap: recompute them per pass
+    // ranking (stable: item-major, then lane): each lane ORs its bit into the wave's mask of its
+    // digit and reads the mask back — the lanes sharing the digit — instead of 8 ballots; the
+    // group's lowest lane advances the wave's digit count and clears the mask
     uint32_t rk2[BS_H];
 #pragma unroll
     for (int k = 0; k < BS_I; ++k) {
-      const bool valid = ((vmask >> k) & 1u);
-      const uint32_t dg = digit_of(klo[k], khi[k], d0);
-      uint64_t m = ballot64(valid);
-      for (int b = 0; b < nb; ++b) {
-        const bool bit = (dg >> b) & 1u;
-        const uint64_t bb = ballot64(bit);
-        m &= bit ? bb : ~bb;
-      }
+      const bool valid = (vmask >> k) & 1u;
+      const uint32_t dg = digit_of(k);
+      uint64_t* ms = &sh.mt[wv][dg];
+      if (valid) __hip_atomic_fetch_or(ms, 1ull << lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      const uint64_t m = __hip_atomic_load(ms, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       const uint32_t below = mbcnt(m);
       const uint32_t prior = sh.whist[wv][dg];
-      if (valid && below == 0) sh.whist[wv][dg] = prior + (uint32_t)__popcll(m);
+      if (valid && below == 0) {
+        __hip_atomic_store(ms, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        sh.whist[wv][dg] = prior + (uint32_t)__popcll(m);
+      }
       const uint32_t wr = (prior + below) & 0xFFFFu;
-      if (k & 1) rk2[k >> 1] |= wr << 16; else rk2[k >> 1] = wr;
+      if (k < BS_H) rk2[k] = wr; else rk2[k - BS_H] |= wr << 16;
     }
     __syncthreads();
-    if (tid < 256) {
-      uint32_t run = 0;
+    if (TRACE && d0 == 0) ts[6] = stamp();
+    // scan of the 16 x 256 counts by all 1024 threads: group g = tid >> 8 owns waves 4g .. 4g+3
+    // of digit d = tid & 255
+    {
+      uint32_t(*gpre)[256] = reinterpret_cast<uint32_t(*)[256]>(&sh.mt[0][0]);
+      const uint32_t d = tid & 255u, g = tid >> 8;
+      uint32_t c4[4], run = 0;
 #pragma unroll
-      for (int w = 0; w < BS_W; ++w) {
-        const uint32_t cc = sh.whist[w][tid];
-        sh.whist[w][tid] = run;
-        run += cc;
+      for (int i = 0; i < 4; ++i) c4[i] = sh.whist[4 * g + i][d];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        sh.whist[4 * g + i][d] = run;
+        run += c4[i];
       }
-      const uint32_t inc = wave_incl_sum<uint32_t>(run);
-      if (lane == 63) sh.wsum[wv] = inc;
-      sh.tstart[tid] = inc - run;
-    }
-    __syncthreads();
-    if (tid < 256) {
+      gpre[g][d] = run;
+      __syncthreads();
+      if (tid < 256) {
+        uint32_t gp = 0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const uint32_t v = gpre[q][d];
+          gpre[q][d] = gp;
+          gp += v;
+        }
+        const uint32_t inc = wave_incl_sum<uint32_t>(gp);
+        if (lane == 63) sh.wsum[wv] = inc;
+        sh.wloc[d] = inc - gp;
+      }
+      __syncthreads();
       uint32_t carry = 0;
-      for (uint32_t w = 0; w < wv; ++w) carry += sh.wsum[w];
-      sh.tstart[tid] += carry;
-    }
-    __syncthreads();
-    // destination rank of item k (recomputed from the digit each time it is needed)
-    auto dst = [&](int k) -> uint32_t {
-      const uint32_t dg = digit_of(klo[k], khi[k], d0);
-      return sh.tstart[dg] + sh.whist[wv][dg] + ((rk2[k >> 1] >> (16 * (k & 1))) & 0xFFFFu);
-    };
-    // exchange through LDS: write at the new rank, read back in slot order.  The index plane goes
-    // first (its destinations come from the key planes, which must still be in place).
+      for (uint32_t w = 0; w < (d >> 6); ++w) carry += sh.wsum[w];
+      const uint32_t base = sh.wloc[d] + carry + gpre[g][d];
 #pragma unroll
-    for (int k = 0; k < BS_I; ++k)
-      if (((vmask >> k) & 1u)) buf16[dst(k)] = (uint16_t)(ix2[k >> 1] >> (16 * (k & 1)));
-    __syncthreads();
-#pragma unroll
-    for (int h = 0; h < BS_H; ++h) {
-      const uint32_t a0 = buf16[(s0 + 128u * h)];
-      const uint32_t a1 = 2 * h + 1 < BS_I ? (uint32_t)buf16[(s0 + 128u * h + 64u)] : 0u;
-      ix2[h] = a0 | (a1 << 16);
+      for (int i = 0; i < 4; ++i) sh.whist[4 * g + i][d] += base;
+      __syncthreads();
+      reinterpret_cast<uint32_t*>(&sh.mt[0][0])[tid] = 0;   // gpre back to clean match masks
     }
-    __syncthreads();
-    if (WIDE) {
-      // rk2 -> absolute destinations are needed twice more: keep them in the rank registers
+    if (TRACE && d0 == 0) ts[7] = stamp();
+    auto dst = [&](int k) -> uint32_t { return sh.whist[wv][digit_of(k)] + half(rk2, k); };
+    if (packprev) {
+      // one exchange phase: key word (with the prev code) and original slot together
 #pragma unroll
       for (int k = 0; k < BS_I; ++k)
-        if (((vmask >> k) & 1u)) sh.buf[dst(k)] = khi[k];
+        if ((vmask >> k) & 1u) {
+          const uint32_t D = dst(k);
+          sh.buf[D] = klo[k];
+          sh.aux[D] = (uint16_t)half(ix2, k);
+        }
       __syncthreads();
-      uint32_t nh[BS_I];
+      for (uint32_t i = tid; i < BS_V * 256; i += BS_T) (&sh.whist[0][0])[i] = 0;
 #pragma unroll
-      for (int k = 0; k < BS_I; ++k) nh[k] = sh.buf[(s0 + 64u * k)];
-      __syncthreads();
+      for (int k = 0; k < BS_I; ++k) klo[k] = sh.buf[s0 + 64u * k];
 #pragma unroll
-      for (int k = 0; k < BS_I; ++k)
-        if (((vmask >> k) & 1u)) sh.buf[dst(k)] = klo[k];
-      __syncthreads();
-#pragma unroll
-      for (int k = 0; k < BS_I; ++k) {
-        khi[k] = nh[k];
-        klo[k] = sh.buf[(s0 + 64u * k)];
-      }
+      for (int j = 0; j < BS_H; ++j) ix2[j] = (uint32_t)sh.aux[s0 + 64u * j] | ((uint32_t)sh.aux[s0 + 64u * (j + BS_H)] << 16);
       __syncthreads();
     } else {
 #pragma unroll
       for (int k = 0; k < BS_I; ++k)
-        if (((vmask >> k) & 1u)) sh.buf[dst(k)] = klo[k];
+        if ((vmask >> k) & 1u) buf16[dst(k)] = (uint16_t)half(ix2, k);
       __syncthreads();
 #pragma unroll
-      for (int k = 0; k < BS_I; ++k) klo[k] = sh.buf[(s0 + 64u * k)];
+      for (int j = 0; j < BS_H; ++j) ix2[j] = (uint32_t)buf16[s0 + 64u * j] | ((uint32_t)buf16[s0 + 64u * (j + BS_H)] << 16);
       __syncthreads();
+      if (WIDE) {
+#pragma unroll
+        for (int k = 0; k < BS_I; ++k)
+          if ((vmask >> k) & 1u) sh.buf[dst(k)] = khi[k];
+        __syncthreads();
+        uint32_t nh[BS_I];
+#pragma unroll
+        for (int k = 0; k < BS_I; ++k) nh[k] = sh.buf[s0 + 64u * k];
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < BS_I; ++k)
+          if ((vmask >> k) & 1u) sh.buf[dst(k)] = klo[k];
+        __syncthreads();
+        for (uint32_t i = tid; i < BS_V * 256; i += BS_T) (&sh.whist[0][0])[i] = 0;
+#pragma unroll
+        for (int k = 0; k < BS_I; ++k) {
+          khi[k] = nh[k];
+          klo[k] = sh.buf[s0 + 64u * k];
+        }
+        __syncthreads();
+      } else {
+#pragma unroll
+        for (int k = 0; k < BS_I; ++k)
+          if ((vmask >> k) & 1u) sh.buf[dst(k)] = klo[k];
+        __syncthreads();
+        for (uint32_t i = tid; i < BS_V * 256; i += BS_T) (&sh.whist[0][0])[i] = 0;
+#pragma unroll
+        for (int k = 0; k < BS_I; ++k) klo[k] = sh.buf[s0 + 64u * k];
+        __syncthreads();
+      }
     }
   }
 
   // ---- ties: equal local keys next to each other in sorted order
   if (TRACE) ts[2] = stamp();
   asm volatile("" : "+v"(s0));
-  uint32_t tmask = 0, hmask = 0;
 #pragma unroll
-  for (int k = 0; k < BS_I; ++k) sh.buf[(s0 + 64u * k)] = klo[k];
+  for (int k = 0; k < BS_I; ++k) sh.buf[s0 + 64u * k] = klo[k] & kmask;
   __syncthreads();
   uint32_t eqp = 0, eqn = 0;
 #pragma unroll
   for (int k = 0; k < BS_I; ++k) {
-    const uint32_t r = (s0 + 64u * k);
+    const uint32_t r = s0 + 64u * k;
+    const uint32_t v = klo[k] & kmask;
     if ((vmask >> k) & 1u) {
-      if (r > 0 && sh.buf[r - 1] == klo[k]) eqp |= 1u << k;
-      if (r + 1 < cnt && sh.buf[r + 1] == klo[k]) eqn |= 1u << k;
+      if (r > 0 && sh.buf[r - 1] == v) eqp |= 1u << k;
+      if (r + 1 < cnt && sh.buf[r + 1] == v) eqn |= 1u << k;
     }
   }
   if (WIDE) {
     __syncthreads();
 #pragma unroll
-    for (int k = 0; k < BS_I; ++k) sh.buf[(s0 + 64u * k)] = khi[k];
+    for (int k = 0; k < BS_I; ++k) sh.buf[s0 + 64u * k] = khi[k];
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < BS_I; ++k) {
-      const uint32_t r = (s0 + 64u * k);
-      if (r < cnt) {
+      const uint32_t r = s0 + 64u * k;
+      if ((vmask >> k) & 1u) {
         if (r > 0 && sh.buf[r - 1] != khi[k]) eqp &= ~(1u << k);
         if (r + 1 < cnt && sh.buf[r + 1] != khi[k]) eqn &= ~(1u << k);
       }
     }
   }
-  tmask = eqp | eqn;
-  hmask = tmask & ~eqp;
+  const uint32_t tmask = eqp | eqn;
+  const uint32_t hmask = tmask & ~eqp;
   __syncthreads();
 
   // ---- SA / BWT in sorted order: the positions are loaded coalesced in original order, staged in
@@ -438,14 +479,15 @@ __global__ __launch_bounds__(BS_T, 1) void k_bucket_sort(const uint64_t* __restr
   if (TRACE) ts[4] = stamp();
 #pragma unroll
   for (int k = 0; k < BS_I; ++k) {
-    const uint32_t r = (s0 + 64u * k);
+    const uint32_t r = s0 + 64u * k;
     const bool valid = (vmask >> k) & 1u;
     uint32_t p = 0;
     if (valid) {
-      const uint32_t o = (ix2[k >> 1] >> (16 * (k & 1))) & 0xFFFFu;
+      const uint32_t o = half(ix2, k);
       p = sh.buf[o];
       sab[r] = p;
-      bwb[r] = sh.inv[sh.prev[o]];
+      const uint32_t pv = packprev ? (klo[k] >> width) & pmask : (uint32_t)sh.aux[o];
+      bwb[r] = sh.inv[pv];
     }
     const bool tied = valid && ((tmask >> k) & 1u);
     const uint64_t tb = ballot64(tied);
@@ -463,7 +505,7 @@ __global__ __launch_bounds__(BS_T, 1) void k_bucket_sort(const uint64_t* __restr
   if (TRACE) {
     ts[5] = stamp();
     if (tid == 0)
-      for (int i = 0; i < 6; ++i) trace[(uint64_t)blockIdx.x * 8 + i] = ts[i];
+      for (int i = 0; i < 8; ++i) trace[(uint64_t)blockIdx.x * 8 + i] = ts[i];
   }
 }
 
@@ -547,12 +589,16 @@ KeyGeom key_geometry_keyed(Index& ix) {
   KeyGeom g{};
   g.keyed = true;
   g.R = (uint64_t)ix.sigma + 1;
+  // prev field = dense code (no end code in the keyed layout): bits(sigma - 1), at least 1
   int pbits = 1;
-  while ((1 << pbits) < ix.sigma + 1) ++pbits;
+  while ((1 << pbits) < ix.sigma) ++pbits;
   g.pb = pbits;
-  for (int c = 0; c < 256; ++c) g.lut[c] = ix.code_of[c] < 0 ? 0 : (uint16_t)(ix.code_of[c] + 1);
+  for (int c = 0; c < 256; ++c) {
+    g.lut[c] = ix.code_of[c] < 0 ? 0 : (uint16_t)(ix.code_of[c] + 1);   // refinement: 0 = end of text
+    g.lutp[c] = ix.code_of[c] < 0 ? 0 : (uint16_t)ix.code_of[c];
+  }
   memset(g.inv, 0, sizeof(g.inv));
-  for (int k = 0; k < ix.sigma; ++k) g.inv[k + 1] = ix.syms[k];
+  for (int k = 0; k < ix.sigma; ++k) g.inv[k] = ix.syms[k];
 
   // the last bytes of T' (short suffixes)
   const uint64_t nt = std::min<uint64_t>(n, 70);
@@ -610,28 +656,28 @@ KeyGeom key_geometry_keyed(Index& ix) {
     b = std::max(b, sb - 16);
     return std::max(b, 0);
   };
-  int qn = 0, qw = 0, sbn = 0, sbw = 0, bsn = 0, bsw = 0;
+  // Symbols per key by cost, in units of one LDS radix pass over all suffixes: the passes over the
+  // local (below-bucket) bits, 30% more when they need the wide (two-plane) kernel, plus ~13 per
+  // expected tied suffix (refinement: text gathers, a 64-bit sort and a regrouping pass), from the
+  // iid collision rate sum(p_c^2)^q of the keyed symbols.
+  auto ties = [&](int q) { return std::min((double)n, (double)n * (double)n * std::pow(p2, (double)q)); };
+  double best = 1e300;
   for (int q = 1; q <= 64; ++q) {
     uint64_t ss;
     unsigned __int128 span = 0;
     const int sb = shorts(q, nullptr, ss, &span);
     if (sb == 99 || g.pb + sb > 64) break;
     const int bs = shift_for(sb, span);
-    qw = q;
-    sbw = sb;
-    bsw = bs;
-    if (bs <= 32) {
-      qn = q;
-      sbn = sb;
-      bsn = bs;
+    const double passes = (double)((bs + 7) / 8) * (bs > 32 ? 1.3 : 1.0);
+    const double cost = passes + 13.0 * ties(q) / (double)n;
+    if (cost <= best) {
+      best = cost;
+      g.q = q;
+      g.sym_bits = sb;
+      g.bucket_bits = sb - bs;
     }
   }
-  if (qw == 0) throw ApiError{-6, "keyed geometry: no symbol count fits a 64-bit key"};
-  auto ties = [&](int q) { return std::min((double)n, (double)n * (double)n * std::pow(p2, (double)q)); };
-  const bool narrow = qn > 0 && (qn == qw || ties(qn) <= std::max(64.0, (double)n / 2048.0));
-  g.q = narrow ? qn : qw;
-  g.sym_bits = narrow ? sbn : sbw;
-  g.bucket_bits = g.sym_bits - (narrow ? bsn : bsw);
+  if (g.q == 0) throw ApiError{-6, "keyed geometry: no symbol count fits a 64-bit key"};
   shorts(g.q, g.skey, g.s_start, nullptr);
   g.nS = (uint32_t)(n - g.s_start);
   // exact order of the short suffixes (bytes compare like Python str over latin-1 code points)
@@ -708,7 +754,7 @@ void build_sa_bucketed(Index& ix) {
   const int D = kg.bucket_bits, sb = kg.sym_bits, pb = kg.pb;
   const int bsh = sb - D;
   const uint8_t* small = ix.small.as<uint8_t>();
-  const uint16_t* d_lutp = reinterpret_cast<const uint16_t*>(small + 2048);
+  const uint16_t* d_lutp = reinterpret_cast<const uint16_t*>(small + 4608);
   const uint16_t* d_lutk = reinterpret_cast<const uint16_t*>(small + 2560);
   const uint64_t* d_skey = reinterpret_cast<const uint64_t*>(small + 3584);
   const uint8_t* d_inv = small + 3072;
@@ -873,10 +919,15 @@ void build_sa_bucketed(Index& ix) {
         t_lo = std::min(t_lo, h[w * 8]);
         t_hi = std::max(t_hi, h[w * 8 + 5]);
       }
-      fprintf(stderr, "[bucket_sort trace] %zu WGs, mean cycles: load %.0f, passes %.0f, ties %.0f, "
-              "stage %.0f, out %.0f; span %.3g cycles\n", items_n.size(), acc[0] / items_n.size(),
-              acc[1] / items_n.size(), acc[2] / items_n.size(), acc[3] / items_n.size(), acc[4] / items_n.size(),
-              (double)(t_hi - t_lo));
+      double r0 = 0, r1 = 0;
+      for (size_t w = 0; w < items_n.size(); ++w) {
+        r0 += (double)(h[w * 8 + 6] - h[w * 8 + 1]);
+        r1 += (double)(h[w * 8 + 7] - h[w * 8 + 6]);
+      }
+      fprintf(stderr, "[bucket_sort trace] %zu WGs, mean cycles: load %.0f, passes %.0f (pass 0: rank %.0f, "
+              "scan %.0f), ties %.0f, stage %.0f, out %.0f; span %.3g cycles\n", items_n.size(),
+              acc[0] / items_n.size(), acc[1] / items_n.size(), r0 / items_n.size(), r1 / items_n.size(),
+              acc[2] / items_n.size(), acc[3] / items_n.size(), acc[4] / items_n.size(), (double)(t_hi - t_lo));
     }
   }
   uint64_t ntie = 0;

@@ -37,6 +37,7 @@ struct KeyGeom {
   bool keyed = false;
   uint64_t Rk = 2;
   uint16_t lutk[256];        // byte -> keyed code in the low byte | byte << 8
+  uint16_t lutp[256];        // byte -> dense code (the prev field of keyed keys; inv[] is by dense code)
   uint64_t s_start = 0;      // first short suffix
   uint32_t nS = 0;           // n - s_start
   uint64_t skey[72];         // B(s) of the short suffixes (sym field, not shifted)

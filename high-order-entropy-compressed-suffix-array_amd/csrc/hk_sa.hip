@@ -626,8 +626,9 @@ void upload_geometry(Index& ix, const KeyGeom& kg) {
   ix.small.ensure(8192);
   HK_HIP(hipMemcpyAsync(ix.small.as<uint8_t>() + 2048, kg.lut, 512, hipMemcpyHostToDevice, ix.stream));
   HK_HIP(hipMemcpyAsync(ix.small.as<uint8_t>() + 3072, kg.inv, 512, hipMemcpyHostToDevice, ix.stream));
-  if (kg.keyed) {   // small+2560 = lutk (u16[256]), +3584 = skey (u64[72]), +7168 = srank (u32[72])
+  if (kg.keyed) {   // small+2560 = lutk, +4608 = lutp (u16[256]), +3584 = skey (u64[72]), +7168 = srank (u32[72])
     HK_HIP(hipMemcpyAsync(ix.small.as<uint8_t>() + 2560, kg.lutk, 512, hipMemcpyHostToDevice, ix.stream));
+    HK_HIP(hipMemcpyAsync(ix.small.as<uint8_t>() + 4608, kg.lutp, 512, hipMemcpyHostToDevice, ix.stream));
     HK_HIP(hipMemcpyAsync(ix.small.as<uint8_t>() + 3584, kg.skey, sizeof(kg.skey), hipMemcpyHostToDevice,
                           ix.stream));
     HK_HIP(hipMemcpyAsync(ix.small.as<uint8_t>() + 7168, kg.srank, sizeof(kg.srank), hipMemcpyHostToDevice,
