@@ -32,36 +32,6 @@
 namespace hk {
 namespace {
 
-struct KeyedArgs {
-  uint64_t Rk, Rck, Rlast;
-  uint64_t s_start;
-  int q, ck, pb, hq;   // hq > 0: the bucket is the first hq symbols (radix 2^k, exact split)
-};
-
-inline KeyedArgs keyed_args(const KeyGeom& kg, uint64_t n) {
-  const KeyChunks kc = key_chunks(kg.Rk, kg.q);
-  KeyedArgs a{kg.Rk, kc.Rck, kc.Rlast, kg.s_start, kg.q, kc.ck, kg.pb, 0};
-  (void)n;
-  return a;
-}
-
-// sym field of suffix p: its first q keyed codes as a radix-Rk number, or the boundary key of a
-// short suffix.  c[off] holds T'[p-1], c[off+1..] T'[p..]; each code is keyed code | byte << 8.
-__device__ __forceinline__ uint64_t keyed_sym(const uint16_t* c, int off, uint64_t p, const KeyedArgs& g,
-                                              const uint64_t* SK) {
-  if (p >= g.s_start) return SK[p - g.s_start];
-  uint64_t key = 0;
-  int j = 1;
-  while (j <= g.q) {
-    const int len = g.q - j + 1 < g.ck ? g.q - j + 1 : g.ck;
-    uint32_t cv = 0;
-    for (int u = 0; u < len; ++u) cv = __umul24(cv, (uint32_t)g.Rk) + (c[off + j + u] & 255u);
-    key = key * (len == g.ck ? g.Rck : g.Rlast) + cv;
-    j += len;
-  }
-  return key;
-}
-
 // ------------------------------------------------------------ 1. bucket histogram
 // One pass over the text, all 2^D <= 65536 bins in LDS as u16 pairs (128 KiB).  A counter that
 // reaches 0x8000 is drained to the global histogram by the lane whose add took it there (the lane
@@ -758,7 +728,8 @@ void build_sa_bucketed(Index& ix) {
   const uint16_t* d_lutk = reinterpret_cast<const uint16_t*>(small + 2560);
   const uint64_t* d_skey = reinterpret_cast<const uint64_t*>(small + 3584);
   const uint8_t* d_inv = small + 3072;
-  KeyedArgs ka = keyed_args(kg, n);
+  const KeyChunks kch = key_chunks(kg.Rk, kg.q);
+  KeyedArgs ka{kg.Rk, kch.Rck, kch.Rlast, kg.s_start, kg.q, kch.ck, kg.pb, 0};
   {
     // first hq symbols are exactly the top D bits when Rk = 2^k, k | D and no short key exceeds Rk^q - 1
     const int lb = (kg.Rk & (kg.Rk - 1)) == 0 ? __builtin_ctzll(kg.Rk) : 0;
@@ -838,15 +809,16 @@ void build_sa_bucketed(Index& ix) {
   }
   uint64_t* kp[2] = {ix.keys[0].as<uint64_t>(), ix.keys[1].as<uint64_t>()};
   uint32_t* vp[2] = {ix.vals[0].as<uint32_t>(), ix.vals[1].as<uint32_t>()};
-  {
+  auto pack = [&]() {
     TimedLaunch t(ix.timer, "sa_pack_keys", (double)n * 9);
     const uint64_t g = std::min<uint64_t>(ceil_div(n, PKK_TILE), 4096);
     k_pack_keyed<<<(unsigned)g, 256, 0, s>>>(ix.text.as<uint8_t>(), n, d_lutk, d_lutp, d_skey, ka, kp[0]);
     HK_HIP(hipGetLastError());
-  }
+  };
 
   if (big_total > n / 2) {
     // skewed text: the global path (full LSD radix sort + refinement from the keys)
+    pack();
     const int slot = radix_sort_pairs<uint32_t>(ix.sw, ix.timer, kp, vp, 0, n, pb, pb + sb, true, s);
     ix.info[0] += ix.sw.passes_run;
     ix.info[1] += ix.sw.passes_skipped;
@@ -867,10 +839,13 @@ void build_sa_bucketed(Index& ix) {
     for (uint32_t b = 0; b < nbins; ++b) h0[b & ((1u << lowd) - 1)] += hist[b];
     uint64_t* d_h0 = reinterpret_cast<uint64_t*>(ix.small.as<uint8_t>() + 5120);
     HK_HIP(hipMemcpyAsync(d_h0, h0, sizeof(h0), hipMemcpyHostToDevice, s));
-    slot = radix_sort_pairs<uint32_t>(ix.sw, ix.timer, kp, vp, 0, n, pb + bsh, pb + sb, true, s, d_h0);
+    // the first pass builds the keys from the text (no separate key array write + read)
+    const TextKeySrc tks{ix.text.as<uint8_t>(), n, d_lutk, d_lutp, d_skey, ka};
+    slot = radix_sort_pairs<uint32_t>(ix.sw, ix.timer, kp, vp, 0, n, pb + bsh, pb + sb, true, s, d_h0, &tks);
     ix.info[0] += ix.sw.passes_run;
     ix.info[1] += ix.sw.passes_skipped;
   } else {
+    pack();
     fill_iota<uint32_t>(vp[0], n, s);
   }
 

@@ -127,4 +127,41 @@ __device__ __forceinline__ uint64_t key_chunked(const uint16_t* c, int off, uint
   return key_from(c, off, R, q, pb, ck, Rck, Rlast, 1, 0);
 }
 
+
+// ---------------------------------------------------------------- keyed layout (see KeyGeom)
+struct KeyedArgs {
+  uint64_t Rk, Rck, Rlast;
+  uint64_t s_start;
+  int q, ck, pb, hq;   // hq > 0: the bucket is the first hq symbols (radix 2^k, exact split)
+};
+
+// sym field of suffix p: its first q keyed codes as a radix-Rk number, or the boundary key of a
+// short suffix.  c[off] holds T'[p-1], c[off+1..] T'[p..]; each code is keyed code | byte << 8.
+__device__ __forceinline__ uint64_t keyed_sym(const uint16_t* c, int off, uint64_t p, const KeyedArgs& g,
+                                              const uint64_t* SK) {
+  if (p >= g.s_start) return SK[p - g.s_start];
+  uint64_t key = 0;
+  int j = 1;
+  while (j <= g.q) {
+    const int len = g.q - j + 1 < g.ck ? g.q - j + 1 : g.ck;
+    uint32_t cv = 0;
+    for (int u = 0; u < len; ++u) cv = __umul24(cv, (uint32_t)g.Rk) + (c[off + j + u] & 255u);
+    key = key * (len == g.ck ? g.Rck : g.Rlast) + cv;
+    j += len;
+  }
+  return key;
+}
+
+
+// Text-side key source of a radix pass that builds its keys itself (the first pass of the
+// single-GPU bucket build): key(p) = keyed_sym(p) << pb | dense code of T'[p-1].
+struct TextKeySrc {
+  const uint8_t* text;
+  uint64_t n;
+  const uint16_t* lutk;   // keyed code | byte << 8
+  const uint16_t* lutp;   // byte -> dense code
+  const uint64_t* skey;   // boundary keys of the short suffixes
+  KeyedArgs g;
+};
+
 }  // namespace hk

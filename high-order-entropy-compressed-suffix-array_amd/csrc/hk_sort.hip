@@ -241,7 +241,10 @@ struct OsShared {
   union {
     uint64_t keys[T * I];
     V vals[T * I];
+    uint16_t codes[T * I + kCodePad];   // text-keyed first pass: the tile's text codes
   } stage;
+  uint16_t L[256], LP[256];      // text-keyed first pass: keyed / dense code tables
+  uint64_t SK[72];               // ... and the short suffixes' boundary keys
   uint32_t whist[T / 64][256];   // per-wave digit counts, then per-wave exclusive prefix
   uint32_t tstart[256];          // tile-local exclusive digit start
   uint64_t gbase[256];           // global destination base minus tstart
@@ -300,12 +303,14 @@ __device__ __forceinline__ uint64_t lookback(const uint64_t* status, uint32_t ti
 // Order of work per tile: load keys -> wave ranking -> tile digit scan -> keys into LDS in sorted
 // order -> value loads issued -> lookback (its latency overlaps the value loads) -> keys out ->
 // values into LDS -> values out.
-template <typename V, int T, int I, int MODE, int LBW = 4>
+// FT: the pass reads the text instead of keys and builds each suffix's keyed key in registers from
+// the tile's text codes staged in LDS (the first pass of the bucket build; values are positions).
+template <typename V, int T, int I, int MODE, int LBW = 4, bool FT = false>
 __global__ __launch_bounds__(T, T >= 512 ? 4 : 3) void k_onesweep(
     const uint64_t* __restrict__ kin, const V* __restrict__ vin, uint64_t* __restrict__ kout,
     V* __restrict__ vout, uint64_t n, uint32_t shift, const uint64_t* __restrict__ goff,
     uint64_t* status, uint32_t* tile_counter, uint32_t epoch, uint32_t* err, int iota, int next_shift,
-    unsigned long long* __restrict__ hpart) {
+    unsigned long long* __restrict__ hpart, TextKeySrc src = TextKeySrc{}) {
   constexpr int W = T / 64;
   constexpr int TILE = T * I;
   constexpr int WSPAN = I * 64;
@@ -322,10 +327,28 @@ __global__ __launch_bounds__(T, T >= 512 ? 4 : 3) void k_onesweep(
   const uint64_t wbase = tbase + (uint64_t)wv * WSPAN;
 
   uint64_t key[I];
+  if constexpr (FT) {
+    if (tid < 256) {
+      sh.L[tid] = src.lutk[tid];
+      sh.LP[tid] = src.lutp[tid];
+    }
+    if (tid < 72) sh.SK[tid] = src.skey[tid];
+    __syncthreads();
+    stage_text_codes<TILE, T>(sh.stage.codes, sh.L, src.text, n, tbase);
+    __syncthreads();
 #pragma unroll
-  for (int k = 0; k < I; ++k) {
-    const uint64_t j = wbase + (uint64_t)k * 64 + lane;
-    key[k] = j < n ? kin[j] : ~0ull;
+    for (int k = 0; k < I; ++k) {
+      const uint64_t j = wbase + (uint64_t)k * 64 + lane;
+      const int off = (int)(j - tbase);
+      key[k] = j < n ? (keyed_sym(sh.stage.codes, off, j, src.g, sh.SK) << src.g.pb) | sh.LP[sh.stage.codes[off] >> 8]
+                     : ~0ull;
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < I; ++k) {
+      const uint64_t j = wbase + (uint64_t)k * 64 + lane;
+      key[k] = j < n ? kin[j] : ~0ull;
+    }
   }
 
   // ---- rank within the wave (stable: item-major, then lane)
@@ -506,7 +529,7 @@ void fill_iota(V* v, uint64_t n, hipStream_t s) {
 
 template <typename V>
 int radix_sort_pairs(SortWork& w, KernelTimer& tm, uint64_t* k[2], V* v[2], int in_slot, uint64_t n, int bit_lo,
-                     int bit_hi, bool vals_iota, hipStream_t s, const uint64_t* d_hist0) {
+                     int bit_hi, bool vals_iota, hipStream_t s, const uint64_t* d_hist0, const TextKeySrc* src) {
   w.passes_run = 0;
   w.passes_skipped = 0;
   int cur = in_slot;
@@ -547,6 +570,7 @@ int radix_sort_pairs(SortWork& w, KernelTimer& tm, uint64_t* k[2], V* v[2], int 
                                     reinterpret_cast<unsigned long long*>(hist + p * 256));
     HK_HIP(hipGetLastError());
   };
+  if (src && (!d_hist0 || !vals_iota)) throw ApiError{-1, "radix_sort_pairs: text keys need hist0 and iota values"};
   if (d_hist0) HK_HIP(hipMemcpyAsync(hist, d_hist0, 256 * 8, hipMemcpyDeviceToDevice, s));
   else digit_hist(0);
 
@@ -560,6 +584,8 @@ int radix_sort_pairs(SortWork& w, KernelTimer& tm, uint64_t* k[2], V* v[2], int 
     bool trivial = false;
     for (int d = 0; d < 256; ++d)
       if (w.h_hist[p * 256 + d] == n) trivial = true;
+    const bool from_text = src && p == 0;   // builds the keys: never skipped
+    if (from_text) trivial = false;
     const bool has_next = p + 1 < np;
     if (trivial) {
       w.passes_skipped++;
@@ -574,8 +600,23 @@ int radix_sort_pairs(SortWork& w, KernelTimer& tm, uint64_t* k[2], V* v[2], int 
     if (has_next) HK_HIP(hipMemsetAsync(w.hpart.p, 0, 64 * 256 * 8, s));
     const int nxt = cur ^ 1;
     {
-      TimedLaunch t(tm, small ? "radix_onesweep_small" : "radix_onesweep", (double)n * 2.0 * (8 + sizeof(V)));
-      if (small)
+      // algorithmic bytes: read key + value, write key + value; the text-keyed pass reads 1 B of text
+      // and no value
+      const double ab = from_text ? (double)n * (1 + 8 + sizeof(V)) : (double)n * 2.0 * (8 + sizeof(V));
+      TimedLaunch t(tm, from_text ? (small ? "radix_onesweep_text_small" : "radix_onesweep_text")
+                                  : (small ? "radix_onesweep_small" : "radix_onesweep"), ab);
+      if (from_text) {
+        if (small)
+          k_onesweep<V, 256, OS_I, 0, 4, true><<<(unsigned)tiles, 256, 0, s>>>(
+              nullptr, nullptr, k[nxt], v[nxt], n, (uint32_t)(bit_lo + 8 * p), w.offs.as<uint64_t>() + p * 256,
+              w.status.as<uint64_t>(), w.counters.as<uint32_t>() + p, w.epoch, w.err.as<uint32_t>(), 1,
+              has_next ? bit_lo + 8 * (p + 1) : -1, w.hpart.as<unsigned long long>(), *src);
+        else
+          k_onesweep<V, OS_T, OS_I, 0, 4, true><<<(unsigned)tiles, OS_T, 0, s>>>(
+              nullptr, nullptr, k[nxt], v[nxt], n, (uint32_t)(bit_lo + 8 * p), w.offs.as<uint64_t>() + p * 256,
+              w.status.as<uint64_t>(), w.counters.as<uint32_t>() + p, w.epoch, w.err.as<uint32_t>(), 1,
+              has_next ? bit_lo + 8 * (p + 1) : -1, w.hpart.as<unsigned long long>(), *src);
+      } else if (small)
         k_onesweep<V, 256, OS_I, 0><<<(unsigned)tiles, 256, 0, s>>>(
             k[cur], iota_pending ? nullptr : v[cur], k[nxt], v[nxt], n, (uint32_t)(bit_lo + 8 * p),
             w.offs.as<uint64_t>() + p * 256, w.status.as<uint64_t>(), w.counters.as<uint32_t>() + p, w.epoch,
@@ -692,9 +733,11 @@ void debug_radix_bench(SortWork& w, uint64_t* k[2], uint32_t* v[2], uint64_t n, 
 }
 
 template int radix_sort_pairs<uint32_t>(SortWork&, KernelTimer&, uint64_t* k[2], uint32_t* v[2],
-                                        int, uint64_t, int, int, bool, hipStream_t, const uint64_t*);
+                                        int, uint64_t, int, int, bool, hipStream_t, const uint64_t*,
+                                        const TextKeySrc*);
 template int radix_sort_pairs<uint64_t>(SortWork&, KernelTimer&, uint64_t* k[2], uint64_t* v[2],
-                                        int, uint64_t, int, int, bool, hipStream_t, const uint64_t*);
+                                        int, uint64_t, int, int, bool, hipStream_t, const uint64_t*,
+                                        const TextKeySrc*);
 template void fill_iota<uint32_t>(uint32_t*, uint64_t, hipStream_t);
 template void fill_iota<uint64_t>(uint64_t*, uint64_t, hipStream_t);
 

@@ -261,10 +261,14 @@ def test_timing_stats(hk):
     dev.timing(True)
     dev.build_sa()
     dev.synchronize()
-    l, ms, b = dev.kernel_stats("radix_onesweep_small")   # < 2^24 keys: the small-sort variant
-    assert l >= 1 and ms > 0 and b > 0
-    l, ms, b = dev.kernel_stats("sa_pack_keys")
+    # < 2^24 keys: the small-sort variants; the first pass builds the keys from the text
+    l, ms, b = dev.kernel_stats("radix_onesweep_text_small")
     assert l == 1 and ms > 0 and b > 0
+    l, ms, b = dev.kernel_stats("radix_onesweep_small")
+    assert l >= 1 and ms > 0 and b > 0
+    l, ms, b = dev.kernel_stats("sa_bucket_sort")
+    assert l == 1 and ms > 0 and b > 0
+    assert dev.kernel_stats("sa_pack_keys")[0] == 0
     dev.close()
 
 
