@@ -151,6 +151,7 @@ def run_single(args) -> dict:
     info = dev.build_info()
     roof = roofline(dev, args.traffic_gb)
     stages = stage_breakdown(dev, ["sa_bucket_hist", "sa_bucket_sort", "sa_big_gather", "radix_onesweep_text",
+                                   "radix_table_text", "radix_tile_hist",
                                    "radix_hist", "radix_onesweep", "radix_onesweep_small", "sa_pack_keys",
                                    "sa_refine_stats", "sa_refine_apply", "sa_refine_keys", "sa_isa_scatter",
                                    "sa_group_stats", "sa_group_apply", "sa_pair_keys", "bwt_gather", "byte_hist"])

@@ -38,8 +38,8 @@ namespace {
 // sees 0x7FFF returned); the 32k headroom above covers the adds in flight until its subtract lands.
 constexpr int BH_T = 1024;
 constexpr int BH_PER = 16;                  // consecutive positions per thread (radix-2^k path)
-constexpr int BH_TILE = BH_T * BH_PER;      // 16384 positions per tile
-constexpr int BH_STAGE = 4096;              // staged tile of the generic (mixed-radix) path
+constexpr int BH_TILE = BH_T * BH_PER;      // 16384 positions per iteration = 2 radix tiles
+constexpr int BH_STAGE = 4096;              // staged positions per iteration of the generic path
 
 __device__ __forceinline__ void bh_add(uint32_t* H, uint32_t b, unsigned long long* __restrict__ hist) {
   const uint32_t sh = 16u * (b & 1u);
@@ -50,11 +50,13 @@ __device__ __forceinline__ void bh_add(uint32_t* H, uint32_t b, unsigned long lo
   }
 }
 
+// Workgroup w covers the positions [w*span, (w+1)*span) (span a multiple of BH_TILE).
 template <bool HQ>
 __global__ __launch_bounds__(BH_T, 1) void k_bucket_hist(const uint8_t* __restrict__ t, uint64_t n,
                                                          const uint16_t* __restrict__ lutk,
                                                          const uint64_t* __restrict__ skey, KeyedArgs g, int bsh,
-                                                         int D, unsigned long long* __restrict__ hist) {
+                                                         int D, unsigned long long* __restrict__ hist,
+                                                         uint64_t span) {
   __shared__ uint32_t H[32768];
   __shared__ uint16_t c[HQ ? 1 : BH_STAGE + kCodePad];
   __shared__ uint16_t L[256];
@@ -65,26 +67,28 @@ __global__ __launch_bounds__(BH_T, 1) void k_bucket_hist(const uint8_t* __restri
   if (tid < 72) SK[tid] = skey[tid];
   __syncthreads();
   const uint64_t lim = n < g.s_start ? n : g.s_start;   // positions with a text window
+  const uint64_t lo = (uint64_t)blockIdx.x * span;
+  const uint64_t hi = lo + span < n ? lo + span : n;
   if (HQ) {
     const int lb = 31 - __clz((uint32_t)g.Rk);
     const uint32_t bmask = (1u << D) - 1;
-    const uint64_t stride = (uint64_t)gridDim.x * BH_TILE;
-    uint64_t base = (uint64_t)blockIdx.x * BH_TILE;
+    uint64_t base = lo;
     uint4 w0 = make_uint4(0, 0, 0, 0), w1 = w0;
-    if (base + (uint64_t)tid * BH_PER < n) {
+    if (base + (uint64_t)tid * BH_PER < hi) {
       const uint4* src = reinterpret_cast<const uint4*>(t + base + (uint64_t)tid * BH_PER);
       w0 = src[0];
       w1 = src[1];
     }
-    for (; base < n; base += stride) {
+    for (; base < hi; base += BH_TILE) {
       const uint64_t p0 = base + (uint64_t)tid * BH_PER;
       const uint32_t wd[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
-      if (p0 + stride < n) {   // next tile's bytes in flight
-        const uint4* src = reinterpret_cast<const uint4*>(t + p0 + stride);
+      if (p0 + BH_TILE < hi) {   // next iteration's bytes in flight
+        const uint4* src = reinterpret_cast<const uint4*>(t + p0 + BH_TILE);
         w0 = src[0];
         w1 = src[1];
       }
-      if (p0 < lim) {
+      const uint64_t lim2 = lim < hi ? lim : hi;
+      if (p0 < lim2) {
         // rolling window over bytes i = 0 .. 30 (static register indices); the window ending at
         // byte i is the bucket of position p0 + i - (hq - 1)
         uint32_t b = 0;
@@ -92,21 +96,21 @@ __global__ __launch_bounds__(BH_T, 1) void k_bucket_hist(const uint8_t* __restri
         for (int i = 0; i < 2 * BH_PER - 1; ++i) {
           b = ((b << lb) | (L[(wd[i >> 2] >> (8 * (i & 3))) & 255u] & 255u)) & bmask;
           const int j = i - (g.hq - 1);
-          if (j >= 0 && j < BH_PER && p0 + j < lim) bh_add(H, b, hist);
+          if (j >= 0 && j < BH_PER && p0 + j < lim2) bh_add(H, b, hist);
         }
       }
-      for (uint64_t p = p0 > lim ? p0 : lim; p < p0 + BH_PER && p < n; ++p)
+      for (uint64_t p = p0 > lim ? p0 : lim; p < p0 + BH_PER && p < hi; ++p)
         bh_add(H, (uint32_t)(SK[p - g.s_start] >> bsh), hist);
     }
   } else {
-    for (uint64_t base = (uint64_t)blockIdx.x * BH_STAGE; base < n; base += (uint64_t)gridDim.x * BH_STAGE) {
+    for (uint64_t base = lo; base < hi; base += BH_STAGE) {
       stage_text_codes<BH_STAGE, BH_T>(c, L, t, n, base);
       __syncthreads();
 #pragma unroll
       for (int k = 0; k < BH_STAGE / BH_T; ++k) {
         const int off = k * BH_T + tid;
         const uint64_t p = base + off;
-        if (p < n) bh_add(H, (uint32_t)(keyed_sym(c, off, p, g, SK) >> bsh), hist);
+        if (p < hi) bh_add(H, (uint32_t)(keyed_sym(c, off, p, g, SK) >> bsh), hist);
       }
       __syncthreads();
     }
@@ -734,6 +738,7 @@ void build_sa_bucketed(Index& ix) {
     // first hq symbols are exactly the top D bits when Rk = 2^k, k | D and no short key exceeds Rk^q - 1
     const int lb = (kg.Rk & (kg.Rk - 1)) == 0 ? __builtin_ctzll(kg.Rk) : 0;
     if (lb && D > 0 && D % lb == 0 && sb == lb * kg.q) ka.hq = D / lb;
+    if (lb && sb == lb * kg.q) ka.lb = lb;
   }
 
   // ---- 1. bucket histogram
@@ -744,15 +749,15 @@ void build_sa_bucketed(Index& ix) {
     HK_HIP(hipMemsetAsync(ix.bk_hist.p, 0, (uint64_t)nbins * 8, s));
     {
       TimedLaunch t(ix.timer, "sa_bucket_hist", (double)n);
-      if (ka.hq > 0) {
-        const unsigned grid = (unsigned)std::min<uint64_t>(ceil_div(n, BH_TILE), 256);
+      const uint64_t tiles = ceil_div(n, (uint64_t)BH_TILE);
+      const uint64_t tpw = ceil_div(tiles, 256);   // one workgroup per CU
+      const unsigned grid = (unsigned)ceil_div(tiles, tpw);
+      if (ka.hq > 0)
         k_bucket_hist<true><<<grid, BH_T, 0, s>>>(ix.text.as<uint8_t>(), n, d_lutk, d_skey, ka, bsh, D,
-                                                  ix.bk_hist.as<unsigned long long>());
-      } else {
-        const unsigned grid = (unsigned)std::min<uint64_t>(ceil_div(n, BH_STAGE), 256);
+                                                  ix.bk_hist.as<unsigned long long>(), tpw * BH_TILE);
+      else
         k_bucket_hist<false><<<grid, BH_T, 0, s>>>(ix.text.as<uint8_t>(), n, d_lutk, d_skey, ka, bsh, D,
-                                                   ix.bk_hist.as<unsigned long long>());
-      }
+                                                   ix.bk_hist.as<unsigned long long>(), tpw * BH_TILE);
       HK_HIP(hipGetLastError());
     }
     HK_HIP(hipMemcpyAsync(hist.data(), ix.bk_hist.p, (uint64_t)nbins * 8, hipMemcpyDeviceToHost, s));
@@ -834,13 +839,15 @@ void build_sa_bucketed(Index& ix) {
   // ---- 3. LSD passes over the top D bits (digit histograms are marginals of the bucket histogram)
   int slot = 0;
   if (D > 0) {
+    // the first pass builds the keys from the text (no key array is written and re-read); both
+    // passes are onesweep passes with decoupled lookback (measured faster on MI355X than a
+    // reduce-then-scan with per-tile offset tables, which adds table traffic to every tile)
+    const TextKeySrc tks{ix.text.as<uint8_t>(), n, d_lutk, d_lutp, d_skey, ka};
     uint64_t h0[256] = {0};
     const int lowd = std::min(D, 8);
     for (uint32_t b = 0; b < nbins; ++b) h0[b & ((1u << lowd) - 1)] += hist[b];
     uint64_t* d_h0 = reinterpret_cast<uint64_t*>(ix.small.as<uint8_t>() + 5120);
     HK_HIP(hipMemcpyAsync(d_h0, h0, sizeof(h0), hipMemcpyHostToDevice, s));
-    // the first pass builds the keys from the text (no separate key array write + read)
-    const TextKeySrc tks{ix.text.as<uint8_t>(), n, d_lutk, d_lutp, d_skey, ka};
     slot = radix_sort_pairs<uint32_t>(ix.sw, ix.timer, kp, vp, 0, n, pb + bsh, pb + sb, true, s, d_h0, &tks);
     ix.info[0] += ix.sw.passes_run;
     ix.info[1] += ix.sw.passes_skipped;

@@ -133,6 +133,7 @@ struct KeyedArgs {
   uint64_t Rk, Rck, Rlast;
   uint64_t s_start;
   int q, ck, pb, hq;   // hq > 0: the bucket is the first hq symbols (radix 2^k, exact split)
+  int lb = 0;          // radix 2^lb with sym = q*lb bits exactly: keys are bit windows of a packed stream
 };
 
 // sym field of suffix p: its first q keyed codes as a radix-Rk number, or the boundary key of a
@@ -163,5 +164,75 @@ struct TextKeySrc {
   const uint64_t* skey;   // boundary keys of the short suffixes
   KeyedArgs g;
 };
+
+// The keys of one radix tile straight from the text (item k of lane `lane` of a wave is suffix
+// wbase + 64k + lane).  Radix 2^lb (src.g.lb): each staging thread maps 32 text bytes to codes and
+// packs them MSB-first into lb words; a key is the q*lb-bit window at bit off*lb of that stream
+// (3 LDS words).  Otherwise the tile's codes are staged and each key is a chunked Horner sum.
+// LDS: codes[T*I + kCodePad] (generic) or pk[(T*I + 64)/4 + 4] + raw[T*I + 64] (packed), which
+// may alias each other; contains barriers (call from every thread of the block).
+template <int T, int I>
+__device__ __forceinline__ void text_keys(uint64_t (&key)[I], const TextKeySrc& src, uint64_t n, uint64_t tbase,
+                                          uint64_t wbase, uint32_t lane, uint16_t* codes, uint32_t* pk,
+                                          uint8_t* raw, uint32_t* prev0, const uint16_t* L, const uint16_t* LP,
+                                          const uint64_t* SK) {
+  constexpr int TILE = T * I;
+  const uint32_t tid = threadIdx.x;
+  if (src.g.lb) {
+    // radix 2^lb: each staging thread maps 32 text bytes to codes and packs them MSB-first into
+    // lb words; a key is then the q*lb-bit window at bit off*lb of the stream (3 LDS words)
+    const int lb = src.g.lb;
+    if (tid == 0) *prev0 = src.text[tbase == 0 ? n - 1 : tbase - 1];
+    for (uint32_t c = tid; c < (uint32_t)(TILE + 64) / 32; c += T) {
+      const uint64_t p0 = tbase + 32ull * c;
+      uint4 a = make_uint4(0, 0, 0, 0), b = a;
+      if (p0 < n) {   // T' has 64 readable pad bytes; positions past n only feed short suffixes
+        const uint4* q4 = reinterpret_cast<const uint4*>(src.text + p0);
+        a = q4[0];
+        b = q4[1];
+      }
+      const uint32_t w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+      *reinterpret_cast<uint4*>(&raw[32 * c]) = a;
+      *reinterpret_cast<uint4*>(&raw[32 * c + 16]) = b;
+      const int per = 32 / lb;   // codes per word
+      for (int o = 0; o < lb; ++o) {
+        uint32_t word = 0;
+        for (int u = 0; u < per; ++u) {
+          const int i = o * per + u;
+          word = (word << lb) | (L[(w[i >> 2] >> (8 * (i & 3))) & 255u] & 255u);
+        }
+        pk[c * lb + o] = word;
+      }
+    }
+    __syncthreads();
+    const int kbits = src.g.q * lb;
+#pragma unroll
+    for (int k = 0; k < I; ++k) {
+      const uint64_t j = wbase + (uint64_t)k * 64 + lane;
+      const uint32_t off = (uint32_t)(j - tbase);
+      uint64_t sym;
+      if (j >= src.g.s_start) {
+        sym = j < n ? SK[j - src.g.s_start] : 0;
+      } else {
+        const uint32_t bit = off * (uint32_t)lb, w0 = bit >> 5, o = bit & 31u;
+        const uint64_t hi = ((uint64_t)pk[w0] << 32) | pk[w0 + 1];
+        const uint64_t win = o ? (hi << o) | (pk[w0 + 2] >> (32 - o)) : hi;
+        sym = kbits >= 64 ? win : win >> (64 - kbits);
+      }
+      const uint32_t pbyte = off ? raw[off - 1] : *prev0;
+      key[k] = j < n ? (sym << src.g.pb) | LP[pbyte] : ~0ull;
+    }
+  } else {
+    stage_text_codes<TILE, T>(codes, L, src.text, n, tbase);
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < I; ++k) {
+      const uint64_t j = wbase + (uint64_t)k * 64 + lane;
+      const int off = (int)(j - tbase);
+      key[k] = j < n ? (keyed_sym(codes, off, j, src.g, SK) << src.g.pb) | LP[codes[off] >> 8]
+                     : ~0ull;
+    }
+  }
+}
 
 }  // namespace hk

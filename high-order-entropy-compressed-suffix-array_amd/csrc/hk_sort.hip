@@ -4,8 +4,9 @@
 // algorithmic bytes 2*N*(K+V) per 8-bit pass).  One launch per digit:
 //   * every workgroup takes a tile id from an atomic counter (so all lower tiles have
 //     started: the lookback below always makes progress),
-//   * ranks its 8192 keys with wave64 ballot multisplit (8 ballots per item, a per-wave
-//     LDS histogram carries counts across the wave's 16 items, stable order),
+//   * ranks its 8192 keys per wave with an LDS match-mask table (a lane ORs its bit into its
+//     digit's mask, reads back the lanes sharing the digit; a per-wave LDS histogram carries
+//     counts across the wave's 16 items, stable order),
 //   * publishes its 256 digit counts as 8-byte {epoch|flag|count} granules written and
 //     polled with relaxed agent-scope (sc1) accesses — the granule IS the flag, so no
 //     fences are needed (MI355X_MICROARCH.md §visibility, R2 granules),
@@ -242,7 +243,12 @@ struct OsShared {
     uint64_t keys[T * I];
     V vals[T * I];
     uint16_t codes[T * I + kCodePad];   // text-keyed first pass: the tile's text codes
+    struct {                            // ... radix 2^lb: codes packed MSB-first, and raw bytes
+      uint32_t pk[(T * I + 64) / 4 + 4];
+      uint8_t raw[T * I + 64];
+    } ft;
   } stage;
+  uint32_t prev0;                // text-keyed first pass: T'[tile base - 1]
   uint16_t L[256], LP[256];      // text-keyed first pass: keyed / dense code tables
   uint64_t SK[72];               // ... and the short suffixes' boundary keys
   uint32_t whist[T / 64][256];   // per-wave digit counts, then per-wave exclusive prefix
@@ -334,15 +340,8 @@ __global__ __launch_bounds__(T, T >= 512 ? 4 : 3) void k_onesweep(
     }
     if (tid < 72) sh.SK[tid] = src.skey[tid];
     __syncthreads();
-    stage_text_codes<TILE, T>(sh.stage.codes, sh.L, src.text, n, tbase);
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < I; ++k) {
-      const uint64_t j = wbase + (uint64_t)k * 64 + lane;
-      const int off = (int)(j - tbase);
-      key[k] = j < n ? (keyed_sym(sh.stage.codes, off, j, src.g, sh.SK) << src.g.pb) | sh.LP[sh.stage.codes[off] >> 8]
-                     : ~0ull;
-    }
+    text_keys<T, I>(key, src, n, tbase, wbase, lane, sh.stage.codes, sh.stage.ft.pk, sh.stage.ft.raw, &sh.prev0,
+                    sh.L, sh.LP, sh.SK);
   } else {
 #pragma unroll
     for (int k = 0; k < I; ++k) {
@@ -351,23 +350,29 @@ __global__ __launch_bounds__(T, T >= 512 ? 4 : 3) void k_onesweep(
     }
   }
 
-  // ---- rank within the wave (stable: item-major, then lane)
+  // ---- rank within the wave (stable: item-major, then lane).  The lanes sharing a digit come from
+  // a per-wave match-mask table in the (still unused) staging area: each lane ORs its bit into its
+  // digit's mask and reads the mask back; the group's lowest lane advances the wave's count and
+  // clears the mask (LDS ops in wave order) — no per-bit ballots.
+  uint64_t* const mtab = reinterpret_cast<uint64_t*>(&sh.stage);
+  if (FT) __syncthreads();   // the staging area held the tile's text
+  for (uint32_t i = tid; i < (uint32_t)W * 256; i += T) mtab[i] = 0;
+  __syncthreads();
+  uint64_t* const mt = mtab + wv * 256;
   uint32_t rk[I];
 #pragma unroll
   for (int k = 0; k < I; ++k) {
     const uint64_t j = wbase + (uint64_t)k * 64 + lane;
     const bool valid = j < n;
     const uint32_t d = (uint32_t)(key[k] >> shift) & 255u;
-    uint64_t m = ballot64(valid);
-#pragma unroll
-    for (int b = 0; b < 8; ++b) {
-      const bool bit = (d >> b) & 1u;
-      const uint64_t bb = ballot64(bit);
-      m &= bit ? bb : ~bb;
-    }
+    if (valid) __hip_atomic_fetch_or(mt + d, 1ull << lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    const uint64_t m = __hip_atomic_load(mt + d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     const uint32_t below = mbcnt(m);
     const uint32_t prior = sh.whist[wv][d];
-    if (valid && below == 0) sh.whist[wv][d] = prior + (uint32_t)__popcll(m);
+    if (valid && below == 0) {
+      __hip_atomic_store(mt + d, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      sh.whist[wv][d] = prior + (uint32_t)__popcll(m);
+    }
     rk[k] = ((prior + below) & 0xFFFFu) | (d << 16);
   }
   __syncthreads();
@@ -457,7 +462,7 @@ __global__ __launch_bounds__(T, T >= 512 ? 4 : 3) void k_onesweep(
       excl = lookback<LBW>(status, tile, d, epoch, err);
       st_agent(status + (uint64_t)tile * 256 + d, st_pack(epoch, ST_INC, excl + tcount));
     }
-    uint64_t go = MODE == 4 ? (uint64_t)reinterpret_cast<const uint32_t*>(goff)[(uint64_t)tile * 256 + d] : goff[d];
+    uint64_t go = MODE == 4 ? goff[(uint64_t)tile * 256 + d] : goff[d];
     if ((MODE == 1 || MODE == 2) && go + TILE > n) go = n > (uint64_t)TILE ? n - TILE : 0;  // ablations in bounds
     sh.gbase[d] = go + excl - sh.tstart[d];
   }
