@@ -192,13 +192,16 @@ __device__ __forceinline__ uint64_t stamp() {
 // local key and original-slot planes), then SA[start + r] / BWT[start + r] in sorted order and
 // equal keys to the tie list.  The BWT code rides in the key word above the varying bits when it
 // fits (one exchange phase per pass), else it waits in LDS by original slot.
-template <bool WIDE, bool TRACE = false>
+// Key layout: [sym, sb bits][prev code, pb bits][position bits 32.., hb bits] (hb > 0 only for
+// the 64-bit positions of sharded builds: values hold the low 32 bits, V = uint64_t outputs).
+template <bool WIDE, bool TRACE = false, typename V = uint32_t>
 __global__ __launch_bounds__(BS_T, 1) void k_bucket_sort(const uint64_t* __restrict__ keys,
                                                          const uint32_t* __restrict__ vals,
-                                                         const uint2* __restrict__ items, int pb, int sb,
-                                                         const uint8_t* __restrict__ inv, uint32_t* __restrict__ sa,
+                                                         const uint2* __restrict__ items, int pb, int sb, int hb,
+                                                         uint64_t symbias,
+                                                         const uint8_t* __restrict__ inv, V* __restrict__ sa,
                                                          uint8_t* __restrict__ bwt, uint64_t* __restrict__ tie_k,
-                                                         uint32_t* __restrict__ tie_v,
+                                                         V* __restrict__ tie_v,
                                                          unsigned long long* __restrict__ tie_n,
                                                          uint64_t* __restrict__ trace) {
   __shared__ BsShared sh;
@@ -210,7 +213,7 @@ __global__ __launch_bounds__(BS_T, 1) void k_bucket_sort(const uint64_t* __restr
   // workgroup-uniform bases: every per-item index below is a 32-bit offset from them
   const uint64_t* __restrict__ kb = keys + start;
   const uint32_t* __restrict__ vb = vals + start;
-  uint32_t* __restrict__ sab = sa + start;
+  V* __restrict__ sab = sa + start;
   uint8_t* __restrict__ bwb = bwt + start;
   // slot of item k is s0 + 64 k (immediate LDS offsets); bit k of vmask = slot k holds a suffix
   uint32_t s0 = wv * BS_WSPAN + lane;
@@ -219,6 +222,8 @@ __global__ __launch_bounds__(BS_T, 1) void k_bucket_sort(const uint64_t* __restr
   for (int k = 0; k < BS_I; ++k) vmask |= (s0 + 64u * k < cnt ? 1u : 0u) << k;
   const uint64_t symmask = sb >= 64 ? ~0ull : ((1ull << sb) - 1);
   const uint32_t pmask = (1u << pb) - 1;
+  const int pbe = pb + hb;                       // sym field starts here
+  const uint32_t himask = (1u << hb) - 1;
   if (tid < 256) sh.inv[tid] = inv[tid];
   for (uint32_t i = tid; i < BS_V * 256; i += BS_T) (&sh.whist[0][0])[i] = 0;
   for (uint32_t i = tid; i < BS_W * 256; i += BS_T) (&sh.mt[0][0])[i] = 0;
@@ -231,7 +236,7 @@ __global__ __launch_bounds__(BS_T, 1) void k_bucket_sort(const uint64_t* __restr
 #pragma unroll
   for (int k = 0; k < BS_I; ++k) {
     if ((vmask >> k) & 1u) {
-      const uint64_t sym = (key[k] >> pb) & symmask;
+      const uint64_t sym = ((key[k] >> pbe) & symmask) - symbias;
       vor |= sym;
       vand &= sym;
     }
@@ -256,7 +261,7 @@ __global__ __launch_bounds__(BS_T, 1) void k_bucket_sort(const uint64_t* __restr
   const uint64_t var = vor ^ vand;
   const int lo = var ? __builtin_ctzll(var) : 0;
   const int width = var ? 64 - __builtin_clzll(var) - lo : 0;
-  const bool packprev = !WIDE && width + pb <= 32;
+  const bool packprev = !WIDE && width + pb + hb <= 32;
   const uint32_t kmask = width >= 32 ? ~0u : ((1u << width) - 1);
 
   // live through the passes: the local key plane(s) and the original slot, 16 bits per item
@@ -265,8 +270,10 @@ __global__ __launch_bounds__(BS_T, 1) void k_bucket_sort(const uint64_t* __restr
 #pragma unroll
   for (int k = 0; k < BS_I; ++k) {
     // varying bits only (the constant bits above them would collide with the packed prev code)
-    const uint64_t lk = (((key[k] >> pb) & symmask) >> lo) & (width >= 64 ? ~0ull : ((1ull << width) - 1));
-    const uint32_t pv = (uint32_t)key[k] & pmask;
+    const uint64_t lk = ((((key[k] >> pbe) & symmask) - symbias) >> lo) & (width >= 64 ? ~0ull : ((1ull << width) - 1));
+    // prev code and position high bits ride together: in the key word above the varying bits, or
+    // in the u16 plane by original slot
+    const uint32_t pv = ((uint32_t)(key[k] >> hb) & pmask) | (((uint32_t)key[k] & himask) << pb);
     klo[k] = (uint32_t)lk | (packprev ? pv << width : 0u);
     khi[k] = WIDE ? (uint32_t)(lk >> 32) : 0u;
     if (!packprev && ((vmask >> k) & 1u)) sh.aux[s0 + 64u * k] = (uint16_t)pv;
@@ -455,13 +462,13 @@ __global__ __launch_bounds__(BS_T, 1) void k_bucket_sort(const uint64_t* __restr
   for (int k = 0; k < BS_I; ++k) {
     const uint32_t r = s0 + 64u * k;
     const bool valid = (vmask >> k) & 1u;
-    uint32_t p = 0;
+    V p = 0;
     if (valid) {
       const uint32_t o = half(ix2, k);
-      p = sh.buf[o];
+      const uint32_t pv = packprev ? (klo[k] >> width) & ((1u << (pb + hb)) - 1) : (uint32_t)sh.aux[o];
+      p = (V)(((uint64_t)(pv >> pb) << 32) | sh.buf[o]);
       sab[r] = p;
-      const uint32_t pv = packprev ? (klo[k] >> width) & pmask : (uint32_t)sh.aux[o];
-      bwb[r] = sh.inv[pv];
+      bwb[r] = sh.inv[pv & pmask];
     }
     const bool tied = valid && ((tmask >> k) & 1u);
     const uint64_t tb = ballot64(tied);
@@ -517,8 +524,9 @@ __global__ __launch_bounds__(256) void k_tie_append(const uint32_t* __restrict__
   }
 }
 
-__global__ __launch_bounds__(256) void k_tie_split(const uint64_t* __restrict__ tk, const uint32_t* __restrict__ tv,
-                                                   uint64_t A, uint32_t* __restrict__ P, uint32_t* __restrict__ J,
+template <typename V>
+__global__ __launch_bounds__(256) void k_tie_split(const uint64_t* __restrict__ tk, const V* __restrict__ tv,
+                                                   uint64_t A, V* __restrict__ P, uint32_t* __restrict__ J,
                                                    uint32_t* __restrict__ H) {
   for (uint64_t a = (uint64_t)blockIdx.x * 256 + threadIdx.x; a < A; a += (uint64_t)gridDim.x * 256) {
     const uint64_t k = tk[a];
@@ -545,6 +553,18 @@ inline unsigned grid_of(uint64_t n, unsigned cap = 16384) {
   return (unsigned)(g < cap ? g : cap);
 }
 
+// bucket = sym >> bsh for m suffixes whose sym fields span `span` values: the largest shift that keeps
+// the uniform-model mean bucket at <= 16.5k suffixes (one LDS sort holds 18432), with D = sb - bsh in
+// [1, 16] (bsh = sb, i.e. one bucket, when one sort holds all)
+int bucket_shift(uint64_t m, int sb, unsigned __int128 span) {
+  if (m <= (uint64_t)BS_CAP) return sb;
+  const double l = std::log2(16500.0 * (double)span / (double)m);
+  int b = (int)std::floor(l);
+  b = std::min(b, sb - 1);
+  b = std::max(b, sb - 16);
+  return std::max(b, 0);
+}
+
 int bits_of(unsigned __int128 v) {
   int b = 0;
   while (v) {
@@ -554,10 +574,131 @@ int bits_of(unsigned __int128 v) {
   return b;
 }
 
+
+// Work items of the LDS bucket sort: consecutive whole buckets packed up to one workgroup's capacity
+// (kept narrow — local keys within 32 bits — when the geometry allows), and the buckets too large for
+// one workgroup.  hist[b] = suffixes in bucket b, buckets in sorted order.
+struct BucketPlan {
+  std::vector<uint2> items_n, items_w;       // {start, count}: narrow / wide local keys
+  std::vector<uint64_t> big_start, big_cstart;
+  uint64_t big_total = 0;
+};
+
+BucketPlan plan_buckets(const std::vector<uint64_t>& hist, int bsh) {
+  BucketPlan pl;
+  const bool wide_geom = bsh > 32;
+  uint64_t off = 0, istart = 0, icnt = 0;
+  uint32_t ib0 = 0;
+  auto flush = [&](uint32_t last_b) {
+    if (!icnt) return;
+    const int wb = bsh + (last_b != ib0 ? 32 - __builtin_clz(last_b ^ ib0) : 0);
+    (wb > 32 ? pl.items_w : pl.items_n).push_back(make_uint2((uint32_t)istart, (uint32_t)icnt));
+    icnt = 0;
+  };
+  uint32_t prev_b = 0;
+  for (uint32_t b = 0; b < (uint32_t)hist.size(); ++b) {
+    const uint64_t c = hist[b];
+    if (!c) continue;
+    if (c > (uint64_t)BS_CAP) {
+      flush(prev_b);
+      pl.big_cstart.push_back(pl.big_total);
+      pl.big_start.push_back(off);
+      pl.big_total += c;
+    } else {
+      const bool keep_narrow = !wide_geom && icnt && bsh + (32 - __builtin_clz(b ^ ib0)) > 32;
+      if (icnt && (icnt + c > (uint64_t)BS_CAP || keep_narrow)) flush(prev_b);
+      if (!icnt) {
+        istart = off;
+        ib0 = b;
+      }
+      icnt += c;
+      prev_b = b;
+    }
+    off += c;
+  }
+  flush(prev_b);
+  return pl;
+}
+
+// Launches the LDS sorts of the plan's work items over the bucket-grouped (keys, vals); writes
+// sa / bwt in sorted order and appends the tied suffixes to ix.ties_*; returns the tie count.
+template <typename V>
+uint64_t sort_bucket_items(Index& ix, const BucketPlan& plan, const uint64_t* keys, const uint32_t* vals, uint64_t m,
+                           int pb, int sb, int hb, uint64_t symbias, V* sa, uint8_t* bwt) {
+  hipStream_t s = ix.stream;
+  const uint8_t* d_inv = ix.small.as<uint8_t>() + 3072;
+  ix.ties_k.ensure(m * 8 + 16);
+  ix.ties_v.ensure(m * sizeof(V) + 16);
+  ix.ties_n.ensure(16);
+  HK_HIP(hipMemsetAsync(ix.ties_n.p, 0, 8, s));
+  const uint64_t nn = plan.items_n.size(), nw = plan.items_w.size();
+  ix.bk_items.ensure((nn + nw) * sizeof(uint2) + 16);
+  if (nn) HK_HIP(hipMemcpyAsync(ix.bk_items.p, plan.items_n.data(), nn * sizeof(uint2), hipMemcpyHostToDevice, s));
+  if (nw)
+    HK_HIP(hipMemcpyAsync(ix.bk_items.as<uint2>() + nn, plan.items_w.data(), nw * sizeof(uint2),
+                          hipMemcpyHostToDevice, s));
+  {
+    TimedLaunch t(ix.timer, "sa_bucket_sort", (double)(m - plan.big_total) * (8 + 4 + 4 + 1));
+    static const bool trace = getenv("HKCSA_BS_TRACE") != nullptr;   // diagnostic phase stamps
+    DevBuf tbuf;
+    if (trace && nn) tbuf.ensure(nn * 64 + 64);
+    if (nn) {
+      if (trace && sizeof(V) == 4)
+        k_bucket_sort<false, true, V><<<(unsigned)nn, BS_T, 0, s>>>(
+            keys, vals, ix.bk_items.as<uint2>(), pb, sb, hb, symbias, d_inv, sa, bwt, ix.ties_k.as<uint64_t>(),
+            ix.ties_v.as<V>(), ix.ties_n.as<unsigned long long>(), tbuf.as<uint64_t>());
+      else
+        k_bucket_sort<false, false, V><<<(unsigned)nn, BS_T, 0, s>>>(
+            keys, vals, ix.bk_items.as<uint2>(), pb, sb, hb, symbias, d_inv, sa, bwt, ix.ties_k.as<uint64_t>(),
+            ix.ties_v.as<V>(), ix.ties_n.as<unsigned long long>(), nullptr);
+    }
+    if (nw)
+      k_bucket_sort<true, false, V><<<(unsigned)nw, BS_T, 0, s>>>(
+          keys, vals, ix.bk_items.as<uint2>() + nn, pb, sb, hb, symbias, d_inv, sa, bwt, ix.ties_k.as<uint64_t>(),
+          ix.ties_v.as<V>(), ix.ties_n.as<unsigned long long>(), nullptr);
+    HK_HIP(hipGetLastError());
+    if (trace && nn && sizeof(V) == 4) {
+      std::vector<uint64_t> h(nn * 8);
+      HK_HIP(hipMemcpyAsync(h.data(), tbuf.p, h.size() * 8, hipMemcpyDeviceToHost, s));
+      HK_HIP(hipStreamSynchronize(s));
+      double acc[7] = {0, 0, 0, 0, 0, 0, 0};
+      for (size_t w = 0; w < nn; ++w) {
+        for (int i = 0; i < 5; ++i) acc[i] += (double)(h[w * 8 + i + 1] - h[w * 8 + i]);
+        acc[5] += (double)(h[w * 8 + 6] - h[w * 8 + 1]);
+        acc[6] += (double)(h[w * 8 + 7] - h[w * 8 + 6]);
+      }
+      fprintf(stderr, "[bucket_sort trace] %zu WGs, mean cycles: load %.0f, passes %.0f (pass 0: rank %.0f, "
+              "scan %.0f), ties %.0f, stage %.0f, out %.0f\n", (size_t)nn, acc[0] / nn, acc[1] / nn, acc[5] / nn,
+              acc[6] / nn, acc[2] / nn, acc[3] / nn, acc[4] / nn);
+    }
+  }
+  uint64_t ntie = 0;
+  HK_HIP(hipMemcpyAsync(&ntie, ix.ties_n.p, 8, hipMemcpyDeviceToHost, s));
+  HK_HIP(hipStreamSynchronize(s));
+  return ntie;
+}
+
+// histogram of ((key >> pbe) - symbias) >> bsh over the keys (u16-pair LDS bins, as k_bucket_hist)
+__global__ __launch_bounds__(BH_T, 1) void k_key_bucket_hist(const uint64_t* __restrict__ keys, uint64_t m, int pbe,
+                                                             uint64_t symbias, int bsh, uint32_t nbins,
+                                                             unsigned long long* __restrict__ hist) {
+  __shared__ uint32_t H[32768];
+  for (uint32_t i = threadIdx.x; i < 32768; i += BH_T) H[i] = 0;
+  __syncthreads();
+  for (uint64_t j = (uint64_t)blockIdx.x * BH_T + threadIdx.x; j < m; j += (uint64_t)gridDim.x * BH_T)
+    bh_add(H, (uint32_t)(((keys[j] >> pbe) - symbias) >> bsh), hist);
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < 32768; i += BH_T) {
+    const uint32_t v = H[i];
+    if ((v & 0xFFFFu) && 2 * i < nbins) atomicAdd(&hist[2 * i], (unsigned long long)(v & 0xFFFFu));
+    if ((v >> 16) && 2 * i + 1 < nbins) atomicAdd(&hist[2 * i + 1], (unsigned long long)(v >> 16));
+  }
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------- geometry
-KeyGeom key_geometry_keyed(Index& ix) {
+KeyGeom key_geometry_keyed(Index& ix, int reserve) {
   compute_alphabet(ix);
   const uint64_t n = ix.n;
   KeyGeom g{};
@@ -620,16 +761,7 @@ KeyGeom key_geometry_keyed(Index& ix) {
     if (span) *span = mx + 1;
     return std::max(1, bits_of(mx));
   };
-  // bucket = sym >> bsh: the largest shift that keeps the uniform-model mean bucket at <= 16.5k
-  // suffixes (one LDS sort holds 18432), with D = sb - bsh in [1, 16] (0 when one sort holds all)
-  auto shift_for = [&](int sb, unsigned __int128 span) -> int {
-    if (n <= (uint64_t)BS_CAP) return sb;
-    const double l = std::log2(16500.0 * (double)span / (double)n);
-    int b = (int)std::floor(l);
-    b = std::min(b, sb - 1);
-    b = std::max(b, sb - 16);
-    return std::max(b, 0);
-  };
+  auto shift_for = [&](int sb, unsigned __int128 span) { return bucket_shift(n, sb, span); };
   // Symbols per key by cost, in units of one LDS radix pass over all suffixes: the passes over the
   // local (below-bucket) bits, 30% more when they need the wide (two-plane) kernel, plus ~13 per
   // expected tied suffix (refinement: text gathers, a 64-bit sort and a regrouping pass), from the
@@ -640,7 +772,7 @@ KeyGeom key_geometry_keyed(Index& ix) {
     uint64_t ss;
     unsigned __int128 span = 0;
     const int sb = shorts(q, nullptr, ss, &span);
-    if (sb == 99 || g.pb + sb > 64) break;
+    if (sb == 99 || g.pb + sb + reserve > 64) break;
     const int bs = shift_for(sb, span);
     const double passes = (double)((bs + 7) / 8) * (bs > 32 ? 1.3 : 1.0);
     const double cost = passes + 13.0 * ties(q) / (double)n;
@@ -682,14 +814,14 @@ void refine_from_ties(Index& ix, const KeyGeom& kg, uint64_t A, bool allow_doubl
   ix.head_slot.ensure(A * 4 + 16);
   // order the list by slot: key = J << 1 | head
   uint64_t* kp[2] = {ix.ties_k.as<uint64_t>(), ix.keys[1].as<uint64_t>()};
-  uint32_t* vp[2] = {ix.ties_v.as<uint32_t>(), ix.vals[1].as<uint32_t>()};
+  V* vp[2] = {ix.ties_v.as<V>(), ix.vals[1].as<V>()};
   int hb = 1;
   while (hb < 64 && ((ix.n << 1) >> hb)) ++hb;
-  const int sl = radix_sort_pairs<uint32_t>(ix.sw, ix.timer, kp, vp, 0, A, 0, hb, false, s);
-  uint32_t* P = reinterpret_cast<uint32_t*>(ix.act[0][0].as<V>());
+  const int sl = radix_sort_pairs<V>(ix.sw, ix.timer, kp, vp, 0, A, 0, hb, false, s);
+  V* P = ix.act[0][0].as<V>();
   uint32_t* J = ix.act[0][1].as<uint32_t>();
   uint32_t* GH = ix.act[0][2].as<uint32_t>();
-  k_tie_split<<<grid_of(A), 256, 0, s>>>(kp[sl], vp[sl], A, P, J, GH);
+  k_tie_split<V><<<grid_of(A), 256, 0, s>>>(kp[sl], vp[sl], A, P, J, GH);
   HK_HIP(hipGetLastError());
   uint64_t* hx = kp[sl ^ 1];   // u64 scratch (A + 1)
   scan_exclusive_u32_to_u64(ix.sw, GH, hx, A, true, s);
@@ -702,6 +834,62 @@ void refine_from_ties(Index& ix, const KeyGeom& kg, uint64_t A, bool allow_doubl
 }
 
 template void refine_from_ties<uint32_t>(Index&, const KeyGeom&, uint64_t, bool);
+template void refine_from_ties<uint64_t>(Index&, const KeyGeom&, uint64_t, bool);
+
+// ---------------------------------------------------------------- one sharded slice
+template <typename V>
+bool bucket_sort_slice(Index& ix, const KeyGeom& kg, uint64_t m, int hb, uint64_t kmin, uint64_t kmax) {
+  hipStream_t s = ix.stream;
+  const int pb = kg.pb, sb = kg.sym_bits, pbe = pb + hb;
+  const int sbl = std::max(1, bits_of((unsigned __int128)(kmax - kmin)));   // bits of the slice's sym range
+  const int bsh = bucket_shift(m, sbl, (unsigned __int128)(kmax - kmin) + 1);
+  const int D = sbl - bsh;
+  const uint32_t nbins = 1u << D;
+  std::vector<uint64_t> hist(nbins, 0);
+  uint64_t* kp[2] = {ix.keys[0].as<uint64_t>(), ix.keys[1].as<uint64_t>()};
+  uint32_t* vp[2] = {reinterpret_cast<uint32_t*>(ix.vals[0].p), reinterpret_cast<uint32_t*>(ix.vals[1].p)};
+  if (D > 0) {
+    ix.bk_hist.ensure((uint64_t)nbins * 8);
+    HK_HIP(hipMemsetAsync(ix.bk_hist.p, 0, (uint64_t)nbins * 8, s));
+    {
+      TimedLaunch t(ix.timer, "sa_bucket_hist", (double)m * 8);
+      k_key_bucket_hist<<<(unsigned)std::min<uint64_t>(ceil_div(m, BH_T * 16), 256), BH_T, 0, s>>>(
+          kp[0], m, pbe, kmin, bsh, nbins, ix.bk_hist.as<unsigned long long>());
+      HK_HIP(hipGetLastError());
+    }
+    HK_HIP(hipMemcpyAsync(hist.data(), ix.bk_hist.p, (uint64_t)nbins * 8, hipMemcpyDeviceToHost, s));
+    HK_HIP(hipStreamSynchronize(s));
+  } else {
+    hist[0] = m;
+  }
+  const BucketPlan plan = plan_buckets(hist, bsh);
+  ix.info[4] = plan.items_n.size() + plan.items_w.size();
+  ix.info[5] = plan.big_start.size();
+  ix.info[6] = plan.big_total;
+  if (plan.big_total) return false;
+  int slot = 0;
+  if (D > 0) {
+    uint64_t h0[256] = {0};
+    const int lowd = std::min(D, 8);
+    for (uint32_t b = 0; b < nbins; ++b) h0[b & ((1u << lowd) - 1)] += hist[b];
+    uint64_t* d_h0 = reinterpret_cast<uint64_t*>(ix.small.as<uint8_t>() + 5120);
+    HK_HIP(hipMemcpyAsync(d_h0, h0, sizeof(h0), hipMemcpyHostToDevice, s));
+    // digits of (key - kmin << pbe): the slice's local bucket is the D bits above bsh
+    slot = radix_sort_pairs<uint32_t>(ix.sw, ix.timer, kp, vp, 0, m, pbe + bsh, pbe + bsh + D, false, s, d_h0,
+                                      nullptr, kmin << pbe);
+    ix.info[0] += ix.sw.passes_run;
+    ix.info[1] += ix.sw.passes_skipped;
+  }
+  ix.bwt.ensure(m + 64);
+  const uint64_t ntie = sort_bucket_items<V>(ix, plan, kp[slot], vp[slot], m, pb, sb, hb, kmin, ix.sa.as<V>(),
+                                             ix.bwt.as<uint8_t>());
+  ix.info.push_back(ntie);
+  refine_from_ties<V>(ix, kg, ntie, false);
+  return true;
+}
+
+template bool bucket_sort_slice<uint32_t>(Index&, const KeyGeom&, uint64_t, int, uint64_t, uint64_t);
+template bool bucket_sort_slice<uint64_t>(Index&, const KeyGeom&, uint64_t, int, uint64_t, uint64_t);
 
 // ---------------------------------------------------------------- driver
 void build_sa_bucketed(Index& ix) {
@@ -731,7 +919,6 @@ void build_sa_bucketed(Index& ix) {
   const uint16_t* d_lutp = reinterpret_cast<const uint16_t*>(small + 4608);
   const uint16_t* d_lutk = reinterpret_cast<const uint16_t*>(small + 2560);
   const uint64_t* d_skey = reinterpret_cast<const uint64_t*>(small + 3584);
-  const uint8_t* d_inv = small + 3072;
   const KeyChunks kch = key_chunks(kg.Rk, kg.q);
   KeyedArgs ka{kg.Rk, kch.Rck, kch.Rlast, kg.s_start, kg.q, kch.ck, kg.pb, 0};
   {
@@ -767,43 +954,12 @@ void build_sa_bucketed(Index& ix) {
   }
 
   // ---- 2. work items (whole buckets, packed while they fit) and big buckets
-  std::vector<uint2> items_n, items_w;
-  std::vector<uint64_t> big_start, big_cstart;
-  uint64_t big_total = 0;
-  {
-    const bool wide_geom = bsh > 32;
-    uint64_t off = 0, istart = 0, icnt = 0;
-    uint32_t ib0 = 0;
-    auto flush = [&](uint32_t last_b) {
-      if (!icnt) return;
-      const int wb = bsh + (last_b != ib0 ? 32 - __builtin_clz(last_b ^ ib0) : 0);
-      (wb > 32 ? items_w : items_n).push_back(make_uint2((uint32_t)istart, (uint32_t)icnt));
-      icnt = 0;
-    };
-    uint32_t prev_b = 0;
-    for (uint32_t b = 0; b < nbins; ++b) {
-      const uint64_t c = hist[b];
-      if (!c) continue;
-      if (c > (uint64_t)BS_CAP) {
-        flush(prev_b);
-        big_cstart.push_back(big_total);
-        big_start.push_back(off);
-        big_total += c;
-      } else {
-        const bool keep_narrow = !wide_geom && icnt &&
-                                 bsh + (32 - __builtin_clz(b ^ ib0)) > 32;
-        if (icnt && (icnt + c > (uint64_t)BS_CAP || keep_narrow)) flush(prev_b);
-        if (!icnt) {
-          istart = off;
-          ib0 = b;
-        }
-        icnt += c;
-        prev_b = b;
-      }
-      off += c;
-    }
-    flush(prev_b);
-  }
+  const BucketPlan plan = plan_buckets(hist, bsh);
+  const std::vector<uint2>& items_n = plan.items_n;
+  const std::vector<uint2>& items_w = plan.items_w;
+  const std::vector<uint64_t>& big_start = plan.big_start;
+  const std::vector<uint64_t>& big_cstart = plan.big_cstart;
+  const uint64_t big_total = plan.big_total;
   ix.info[4] = items_n.size() + items_w.size();
   ix.info[5] = big_start.size();
   ix.info[6] = big_total;
@@ -857,64 +1013,8 @@ void build_sa_bucketed(Index& ix) {
   }
 
   // ---- 4. LDS sorts of the buckets
-  ix.ties_k.ensure(n * 8 + 16);
-  ix.ties_v.ensure(n * 4 + 16);
-  ix.ties_n.ensure(16);
-  HK_HIP(hipMemsetAsync(ix.ties_n.p, 0, 8, s));
-  {
-    const uint64_t ni = items_n.size() + items_w.size();
-    ix.bk_items.ensure(ni * sizeof(uint2) + 16);
-    if (!items_n.empty())
-      HK_HIP(hipMemcpyAsync(ix.bk_items.p, items_n.data(), items_n.size() * sizeof(uint2), hipMemcpyHostToDevice, s));
-    if (!items_w.empty())
-      HK_HIP(hipMemcpyAsync(ix.bk_items.as<uint2>() + items_n.size(), items_w.data(), items_w.size() * sizeof(uint2),
-                            hipMemcpyHostToDevice, s));
-    TimedLaunch t(ix.timer, "sa_bucket_sort", (double)(n - big_total) * (8 + 4 + 4 + 1));
-    static const bool trace = getenv("HKCSA_BS_TRACE") != nullptr;   // diagnostic phase stamps
-    DevBuf tbuf;
-    if (trace) tbuf.ensure(ni * 64 + 64);
-    uint64_t* tr = tbuf.as<uint64_t>();
-    if (!items_n.empty()) {
-      if (trace)
-        k_bucket_sort<false, true><<<(unsigned)items_n.size(), BS_T, 0, s>>>(
-            kp[slot], vp[slot], ix.bk_items.as<uint2>(), pb, sb, d_inv, ix.sa.as<uint32_t>(), ix.bwt.as<uint8_t>(),
-            ix.ties_k.as<uint64_t>(), ix.ties_v.as<uint32_t>(), ix.ties_n.as<unsigned long long>(), tr);
-      else
-        k_bucket_sort<false><<<(unsigned)items_n.size(), BS_T, 0, s>>>(
-            kp[slot], vp[slot], ix.bk_items.as<uint2>(), pb, sb, d_inv, ix.sa.as<uint32_t>(), ix.bwt.as<uint8_t>(),
-            ix.ties_k.as<uint64_t>(), ix.ties_v.as<uint32_t>(), ix.ties_n.as<unsigned long long>(), nullptr);
-    }
-    if (!items_w.empty())
-      k_bucket_sort<true><<<(unsigned)items_w.size(), BS_T, 0, s>>>(
-          kp[slot], vp[slot], ix.bk_items.as<uint2>() + items_n.size(), pb, sb, d_inv, ix.sa.as<uint32_t>(),
-          ix.bwt.as<uint8_t>(), ix.ties_k.as<uint64_t>(), ix.ties_v.as<uint32_t>(),
-          ix.ties_n.as<unsigned long long>(), nullptr);
-    HK_HIP(hipGetLastError());
-    if (trace && !items_n.empty()) {
-      std::vector<uint64_t> h(items_n.size() * 8);
-      HK_HIP(hipMemcpyAsync(h.data(), tr, h.size() * 8, hipMemcpyDeviceToHost, s));
-      HK_HIP(hipStreamSynchronize(s));
-      double acc[5] = {0, 0, 0, 0, 0};
-      uint64_t t_lo = ~0ull, t_hi = 0;
-      for (size_t w = 0; w < items_n.size(); ++w) {
-        for (int i = 0; i < 5; ++i) acc[i] += (double)(h[w * 8 + i + 1] - h[w * 8 + i]);
-        t_lo = std::min(t_lo, h[w * 8]);
-        t_hi = std::max(t_hi, h[w * 8 + 5]);
-      }
-      double r0 = 0, r1 = 0;
-      for (size_t w = 0; w < items_n.size(); ++w) {
-        r0 += (double)(h[w * 8 + 6] - h[w * 8 + 1]);
-        r1 += (double)(h[w * 8 + 7] - h[w * 8 + 6]);
-      }
-      fprintf(stderr, "[bucket_sort trace] %zu WGs, mean cycles: load %.0f, passes %.0f (pass 0: rank %.0f, "
-              "scan %.0f), ties %.0f, stage %.0f, out %.0f; span %.3g cycles\n", items_n.size(),
-              acc[0] / items_n.size(), acc[1] / items_n.size(), r0 / items_n.size(), r1 / items_n.size(),
-              acc[2] / items_n.size(), acc[3] / items_n.size(), acc[4] / items_n.size(), (double)(t_hi - t_lo));
-    }
-  }
-  uint64_t ntie = 0;
-  HK_HIP(hipMemcpyAsync(&ntie, ix.ties_n.p, 8, hipMemcpyDeviceToHost, s));
-  HK_HIP(hipStreamSynchronize(s));
+  uint64_t ntie = sort_bucket_items<uint32_t>(ix, plan, kp[slot], vp[slot], n, pb, sb, 0, 0, ix.sa.as<uint32_t>(),
+                                              ix.bwt.as<uint8_t>());
 
   // ---- 5. big buckets on the global path
   if (big_total) {

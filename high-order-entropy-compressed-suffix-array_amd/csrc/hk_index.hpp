@@ -171,8 +171,13 @@ void comm_unique_id(uint8_t id[128]);
 
 // shared by the single-GPU and sharded builds
 KeyGeom key_geometry(Index& ix, bool with_prev);
-KeyGeom key_geometry_keyed(Index& ix);   // keyed layout (hk_bucket.hip)
+KeyGeom key_geometry_keyed(Index& ix, int reserve = 0);   // keyed layout; reserve = low key bits kept free
 void build_sa_bucketed(Index& ix);       // single-GPU SA + BWT: 2 LSD passes + LDS bucket sorts
+// Bucket build of one sharded slice: m keyed keys [sym][prev][position bits 32.., hb bits] in keys[0],
+// low position bits (u32) in vals[0], sym fields within [kmin, kmax].  Writes the slice's SA (V) and
+// BWT and refines ties; false (nothing written) when a bucket exceeds one LDS sort.
+template <typename V>
+bool bucket_sort_slice(Index& ix, const KeyGeom& kg, uint64_t m, int hb, uint64_t kmin, uint64_t kmax);
 // tie list (J << 1 | head, P) of m entries in (k, v) -> refinement loop (from symbol offset h)
 template <typename V>
 void refine_from_ties(Index& ix, const KeyGeom& kg, uint64_t A, bool allow_doubling);

@@ -38,8 +38,8 @@ struct ShardComm {  // one RCCL communicator per process (one process per GPU)
   uint8_t id[128];
 };
 
-// bucket of a key: its top SH_BUCKET_BITS bits (key >> bsh).  With key = m << pb | prev and
-// bsh >= pb, bucket in [blo, bhi) <=> m in [Mlo, Mhi) (see sel_geom).
+// bucket of a key: its top SH_BUCKET_BITS bits (key >> bsh) under partition_geometry (pb = 0, so
+// bucket in [blo, bhi) <=> the q-symbol prefix value lies in [Mlo, Mhi), see sel_geom).
 struct BucketGeom {
   uint64_t R, Rck, Rlast;
   int q, pb, ck, bsh;
@@ -223,25 +223,38 @@ __global__ __launch_bounds__(256) void k_select_count(const uint8_t* __restrict_
   if (threadIdx.x == 0) block_cnt[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
 }
 
-// V = u32 with hb > 0: split positions — the low 32 bits go to vals, the high hb bits below the
-// key (key << hb | pos >> 32), outside the sorted bit range; k_split_join reassembles them.
+// Keys of the selected suffixes in the keyed layout of the single-GPU bucket build (see
+// key_geometry_keyed): [sym][dense code of T'[p-1], pb bits][position bits 32.., hb bits].  With
+// hb > 0 (V = u32) the low 32 position bits go to vals and the high bits sit below the key,
+// outside the sorted bit range; k_split_join reassembles them.  kmm[0..1] collect the min / max
+// sym of the slice (the bucket range of its LDS sorts).
 template <typename V>
 __global__ __launch_bounds__(256) void k_select_write(const uint8_t* __restrict__ t, uint64_t n, uint64_t tpb,
-                                                      const uint16_t* __restrict__ lut, BucketGeom g, SelGeom sg,
-                                                      uint32_t blo, uint32_t bhi,
+                                                      const uint16_t* __restrict__ lut,
+                                                      const uint16_t* __restrict__ lutk,
+                                                      const uint16_t* __restrict__ lutp,
+                                                      const uint64_t* __restrict__ skey, KeyedArgs ka,
+                                                      BucketGeom g, SelGeom sg, uint32_t blo, uint32_t bhi,
                                                       const uint64_t* __restrict__ block_off,
-                                                      uint64_t* __restrict__ keys, V* __restrict__ vals, int hb) {
+                                                      uint64_t* __restrict__ keys, V* __restrict__ vals, int hb,
+                                                      unsigned long long* __restrict__ kmm) {
   __shared__ uint16_t c[PS_TILE + kCodePad];
   __shared__ uint16_t list[PS_TILE];
-  __shared__ uint16_t L[256];
+  __shared__ uint16_t L[256], LK[256], LP[256];
+  __shared__ uint64_t SK[64];
   __shared__ uint32_t red[4];
   L[threadIdx.x] = lut[threadIdx.x];
+  LK[threadIdx.x] = lutk[threadIdx.x];
+  LP[threadIdx.x] = lutp[threadIdx.x];
+  if (threadIdx.x < 64 && ka.s_start + threadIdx.x < n) SK[threadIdx.x] = skey[threadIdx.x];
   __syncthreads();
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int pbe = ka.pb + hb;
   const uint64_t tiles = (n + PS_TILE - 1) / PS_TILE;
   const uint64_t t0 = (uint64_t)blockIdx.x * tpb;
   const uint64_t t1 = t0 + tpb < tiles ? t0 + tpb : tiles;
   uint64_t run = block_off[blockIdx.x];
+  uint64_t kmin = ~0ull, kmax = 0;
   for (uint64_t ti = t0; ti < t1; ++ti) {
     const uint64_t base = ti * PS_TILE;
     uint32_t sel = select16(t, n, base + 16 * threadIdx.x, L, g, sg, blo, bhi);
@@ -262,17 +275,30 @@ __global__ __launch_bounds__(256) void k_select_write(const uint8_t* __restrict_
       sel &= sel - 1;
       list[o++] = (uint16_t)(16 * threadIdx.x + k);
     }
-    stage_text_codes<PS_TILE, 256>(c, L, t, n, base);
+    stage_text_codes<PS_TILE, 256>(c, LK, t, n, base);
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < tot; i += 256) {
       const int off = list[i];
       const uint64_t p = base + off;
-      const uint64_t key = key_chunked(c, off, g.R, g.q, g.pb, g.ck, g.Rck, g.Rlast);
-      keys[run + i] = hb ? (key << hb) | (p >> 32) : key;
+      const uint64_t sym = keyed_sym(c, off, p, ka, SK);
+      kmin = sym < kmin ? sym : kmin;
+      kmax = sym > kmax ? sym : kmax;
+      uint64_t key = (sym << pbe) | ((uint64_t)LP[c[off] >> 8] << hb);
+      if (hb) key |= p >> 32;
+      keys[run + i] = key;
       vals[run + i] = (V)p;
     }
     run += tot;
     __syncthreads();   // list / c / red are rewritten by the next tile
+  }
+  for (int d = 32; d >= 1; d >>= 1) {
+    const uint64_t a = __shfl_xor(kmin, d), b = __shfl_xor(kmax, d);
+    kmin = a < kmin ? a : kmin;
+    kmax = b > kmax ? b : kmax;
+  }
+  if (lane == 0 && kmin <= kmax) {
+    atomicMin(&kmm[0], (unsigned long long)kmin);
+    atomicMax(&kmm[1], (unsigned long long)kmax);
   }
 }
 
@@ -293,6 +319,20 @@ inline unsigned grid_for(uint64_t n, unsigned per = 256, unsigned cap = 16384) {
 
 void ncclcheck(ncclResult_t r, const char* what) {
   if (r != ncclSuccess) throw ApiError{-8, std::string(what) + ": " + ncclGetErrorString(r)};
+}
+
+// Partition geometry: the prefix key of the splitters.  No prev field (pb = 0: a bucket has to be
+// a range of the suffix order, which a prev field below a short key would split) and as many
+// symbols as fit in 64 bits, so the top SH_BUCKET_BITS bits split the prefixes as finely as
+// possible.  oracle/hkcsa_oracle.c partition_geometry restates it.
+KeyGeom partition_geometry(Index& ix) {
+  KeyGeom g = key_geometry(ix, false);
+  g.pb = 0;
+  g.q = 1;
+  while (g.q < 64 && mixed_radix_bits(g.R, g.q + 1) <= 64) ++g.q;
+  g.sym_bits = mixed_radix_bits(g.R, g.q);
+  g.key_bits = g.sym_bits;
+  return g;
 }
 
 int bucket_shift(const KeyGeom& kg) {
@@ -447,7 +487,7 @@ template <typename V>
 void shard_build_t(Index& ix, const uint64_t* ghist, const uint64_t* gbelow, int nranks, int rank) {
   const uint64_t n = ix.n;
   hipStream_t s = ix.stream;
-  KeyGeom kg = key_geometry(ix, true);
+  const KeyGeom kg = partition_geometry(ix);   // selection geometry (same as phases 1-2)
   // splitters: rank r owns buckets [B[r], B[r+1]); its SA slice is [below(B[r]), below(B[r+1]))
   const std::vector<uint32_t> B = splitters(ghist, nranks);
   if (gbelow[0] != 0 || gbelow[nranks] != n) throw ApiError{-7, "global splitter counts do not cover n"};
@@ -457,26 +497,33 @@ void shard_build_t(Index& ix, const uint64_t* ghist, const uint64_t* gbelow, int
   ix.shard_lo = gbelow[rank];
   ix.shard_hi = gbelow[rank + 1];
   const uint64_t m = ix.shard_hi - ix.shard_lo;
-  ix.info.assign(4, 0);
-  ix.info[3] = (uint64_t)kg.q;
+  ix.info.assign(8, 0);
   ix.sharded = true;
   ix.sa_pos64 = sizeof(V) == 8;
   ix.have_sa = ix.have_bwt = ix.have_wt = false;
   ix.sa.ensure(m * sizeof(V) + 16);
+  ix.bwt.ensure(m + 64);
   if (!m) {
-    ix.have_sa = true;
+    ix.have_sa = ix.have_bwt = true;
     return;
   }
-  upload_geometry(ix, kg);
-  // 64-bit positions: sort u32 low halves with the high bits parked below the key (24 instead of
-  // 32 bytes per pair and pass) when they fit in the 64-bit key
+  // 64-bit positions: sort u32 low halves with the high bits parked below the key (20 instead of
+  // 24 bytes per pair and pass); NO_SPLIT sorts whole u64 values on the global path
+  const bool whole = sizeof(V) == 8 && (ix.flags & kFlagNoSplit);
   int hb = 0;
-  if (sizeof(V) == 8 && !(ix.flags & kFlagNoSplit)) {
+  if (sizeof(V) == 8 && !whole) {
     hb = 1;
     while (((n - 1) >> 32) >> hb) ++hb;
-    if (kg.key_bits + hb > 64) hb = 0;
   }
+  // sort geometry: the keyed layout of the single-GPU bucket build, hb bits reserved
+  const KeyGeom kk = key_geometry_keyed(ix, hb);
+  ix.info[3] = (uint64_t)kk.q;
+  upload_geometry(ix, kk);
+  const uint8_t* small = ix.small.as<uint8_t>();
+  const KeyChunks kch = key_chunks(kk.Rk, kk.q);
+  const KeyedArgs ka{kk.Rk, kch.Rck, kch.Rlast, kk.s_start, kk.q, kch.ck, kk.pb, 0};
   uint64_t got = 0;
+  uint64_t kmm[2] = {~0ull, 0};
   for (int i = 0; i < 2; ++i) {
     ix.keys[i].ensure(m * 8 + 16);
     ix.vals[i].ensure(m * sizeof(V) + 16);
@@ -486,9 +533,14 @@ void shard_build_t(Index& ix, const uint64_t* ghist, const uint64_t* gbelow, int
     const uint64_t G = tiles < 8192 ? tiles : 8192;
     const uint64_t tpb = ceil_div(tiles, G);
     const unsigned grid = (unsigned)ceil_div(tiles, tpb);
-    ix.tile_d.ensure((grid + 1) * 8);
+    ix.tile_d.ensure((grid + 1) * 8 + 16);
     uint64_t* bc = ix.tile_d.as<uint64_t>();
-    const uint16_t* lut = reinterpret_cast<const uint16_t*>(ix.small.as<uint8_t>() + 2048);
+    unsigned long long* d_kmm = reinterpret_cast<unsigned long long*>(bc + grid + 1);
+    HK_HIP(hipMemcpyAsync(d_kmm, kmm, 16, hipMemcpyHostToDevice, s));
+    const uint16_t* lut = reinterpret_cast<const uint16_t*>(small + 2048);
+    const uint16_t* lutk = reinterpret_cast<const uint16_t*>(small + 2560);
+    const uint16_t* lutp = reinterpret_cast<const uint16_t*>(small + 4608);
+    const uint64_t* skey = reinterpret_cast<const uint64_t*>(small + 3584);
     const BucketGeom bg = bucket_geom(kg);
     const SelGeom sg = sel_geom(kg, bg, blo, bhi);
     {
@@ -500,34 +552,46 @@ void shard_build_t(Index& ix, const uint64_t* ghist, const uint64_t* gbelow, int
     {
       TimedLaunch t(ix.timer, "shard_pack_select", (double)n + (double)m * (8 + sizeof(V)));
       if (hb)
-        k_select_write<uint32_t><<<grid, 256, 0, s>>>(ix.text.as<uint8_t>(), n, tpb, lut, bg, sg, blo, bhi, bc,
-                                                      ix.keys[0].as<uint64_t>(), ix.vals[0].as<uint32_t>(), hb);
+        k_select_write<uint32_t><<<grid, 256, 0, s>>>(ix.text.as<uint8_t>(), n, tpb, lut, lutk, lutp, skey, ka, bg,
+                                                      sg, blo, bhi, bc, ix.keys[0].as<uint64_t>(),
+                                                      ix.vals[0].as<uint32_t>(), hb, d_kmm);
       else
-        k_select_write<V><<<grid, 256, 0, s>>>(ix.text.as<uint8_t>(), n, tpb, lut, bg, sg, blo, bhi, bc,
-                                               ix.keys[0].as<uint64_t>(), ix.vals[0].as<V>(), 0);
+        k_select_write<V><<<grid, 256, 0, s>>>(ix.text.as<uint8_t>(), n, tpb, lut, lutk, lutp, skey, ka, bg, sg,
+                                               blo, bhi, bc, ix.keys[0].as<uint64_t>(), ix.vals[0].as<V>(), 0,
+                                               d_kmm);
       HK_HIP(hipGetLastError());
     }
     HK_HIP(hipMemcpyAsync(&got, bc + grid, 8, hipMemcpyDeviceToHost, s));
+    HK_HIP(hipMemcpyAsync(kmm, d_kmm, 16, hipMemcpyDeviceToHost, s));
   }
   HK_HIP(hipStreamSynchronize(s));
   if (got != m) throw ApiError{-7, "shard selection count mismatch"};
+  if (kmm[0] > kmm[1]) throw ApiError{-7, "shard selection produced no keys"};
+  // LDS bucket sorts over the slice's sym range, unless a bucket is too big for them
+  if (!whole && !(ix.flags & kFlagGlobalSort) && bucket_sort_slice<V>(ix, kk, m, hb, kmm[0], kmm[1])) {
+    HK_HIP(hipStreamSynchronize(s));
+    ix.have_sa = ix.have_bwt = true;
+    return;
+  }
+  ix.info[7] = 1;
+  const int pbe = kk.pb + hb;
   uint64_t* kp[2] = {ix.keys[0].as<uint64_t>(), ix.keys[1].as<uint64_t>()};
   int slot;
   if (hb) {
     uint32_t* vq[2] = {ix.vals[0].as<uint32_t>(), ix.vals[1].as<uint32_t>()};
-    slot = radix_sort_pairs<uint32_t>(ix.sw, ix.timer, kp, vq, 0, m, kg.pb + hb, kg.key_bits + hb, false, s);
+    slot = radix_sort_pairs<uint32_t>(ix.sw, ix.timer, kp, vq, 0, m, pbe, pbe + kk.sym_bits, false, s);
     TimedLaunch t(ix.timer, "shard_split_join", (double)m * (8 + 4 + 8 + 8));
     k_split_join<<<grid_for(m, 256, 16384), 256, 0, s>>>(kp[slot], vq[slot], m, hb, ix.sa.as<uint64_t>());
     HK_HIP(hipGetLastError());
   } else {
     V* vp[2] = {ix.vals[0].as<V>(), ix.vals[1].as<V>()};
-    slot = radix_sort_pairs<V>(ix.sw, ix.timer, kp, vp, 0, m, kg.pb, kg.key_bits, false, s);
+    slot = radix_sort_pairs<V>(ix.sw, ix.timer, kp, vp, 0, m, kk.pb, kk.pb + kk.sym_bits, false, s);
     std::swap(ix.sa, ix.vals[slot]);
     ix.vals[slot].ensure(m * sizeof(V) + 16);
   }
   ix.info[0] += ix.sw.passes_run;
   ix.info[1] += ix.sw.passes_skipped;
-  refine_after_sort<V>(ix, kg, slot, m, false);
+  refine_after_sort<V>(ix, kk, slot, m, false);
   HK_HIP(hipStreamSynchronize(s));
   ix.have_sa = true;
   ix.have_bwt = true;   // BWT of the slice (bwt[j] for SA[lo + j])
@@ -536,7 +600,7 @@ void shard_build_t(Index& ix, const uint64_t* ghist, const uint64_t* gbelow, int
 }  // namespace
 
 void shard_histogram(Index& ix, int nranks, int rank, uint64_t* d_hist) {
-  KeyGeom kg = key_geometry(ix, true);
+  KeyGeom kg = partition_geometry(ix);
   hipStream_t s = ix.stream;
   const uint64_t lo = (uint64_t)((__uint128_t)ix.n * (uint64_t)rank / (uint64_t)nranks);
   const uint64_t hi = (uint64_t)((__uint128_t)ix.n * (uint64_t)(rank + 1) / (uint64_t)nranks);
@@ -553,7 +617,7 @@ void shard_histogram(Index& ix, int nranks, int rank, uint64_t* d_hist) {
 
 void shard_counts(Index& ix, const uint64_t* h_global_hist, int nranks, int rank, uint64_t* d_below) {
   if (nranks > SH_MAX_RANKS) throw ApiError{-2, "at most 64 ranks"};
-  KeyGeom kg = key_geometry(ix, true);
+  KeyGeom kg = partition_geometry(ix);
   hipStream_t s = ix.stream;
   const uint64_t lo = (uint64_t)((__uint128_t)ix.n * (uint64_t)rank / (uint64_t)nranks);
   const uint64_t hi = (uint64_t)((__uint128_t)ix.n * (uint64_t)(rank + 1) / (uint64_t)nranks);

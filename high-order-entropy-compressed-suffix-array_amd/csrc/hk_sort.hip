@@ -176,7 +176,7 @@ constexpr int HG_PER_BLOCK = HG_T * 16;
 // digit histograms for `np` consecutive 8-bit digits starting at bit `lo`
 __global__ __launch_bounds__(HG_T) void k_digit_hist(const uint64_t* __restrict__ keys, uint64_t n,
                                                      int lo, int np,
-                                                     unsigned long long* __restrict__ hist) {
+                                                     unsigned long long* __restrict__ hist, uint64_t kbias = 0) {
   __shared__ uint32_t h[8][256];
   for (int i = threadIdx.x; i < 8 * 256; i += HG_T) (&h[0][0])[i] = 0;
   __syncthreads();
@@ -186,10 +186,10 @@ __global__ __launch_bounds__(HG_T) void k_digit_hist(const uint64_t* __restrict_
     bool two = j + 1 < n;
     if (two) {
       const ulonglong2 kk = *reinterpret_cast<const ulonglong2*>(keys + j);
-      a = kk.x;
-      b = kk.y;
+      a = kk.x - kbias;
+      b = kk.y - kbias;
     } else {
-      a = keys[j];
+      a = keys[j] - kbias;
       b = 0;
     }
     for (int p = 0; p < np; ++p) {
@@ -316,7 +316,7 @@ __global__ __launch_bounds__(T, T >= 512 ? 4 : 3) void k_onesweep(
     const uint64_t* __restrict__ kin, const V* __restrict__ vin, uint64_t* __restrict__ kout,
     V* __restrict__ vout, uint64_t n, uint32_t shift, const uint64_t* __restrict__ goff,
     uint64_t* status, uint32_t* tile_counter, uint32_t epoch, uint32_t* err, int iota, int next_shift,
-    unsigned long long* __restrict__ hpart, TextKeySrc src = TextKeySrc{}) {
+    unsigned long long* __restrict__ hpart, TextKeySrc src = TextKeySrc{}, uint64_t kbias = 0) {
   constexpr int W = T / 64;
   constexpr int TILE = T * I;
   constexpr int WSPAN = I * 64;
@@ -364,7 +364,7 @@ __global__ __launch_bounds__(T, T >= 512 ? 4 : 3) void k_onesweep(
   for (int k = 0; k < I; ++k) {
     const uint64_t j = wbase + (uint64_t)k * 64 + lane;
     const bool valid = j < n;
-    const uint32_t d = (uint32_t)(key[k] >> shift) & 255u;
+    const uint32_t d = (uint32_t)((key[k] - kbias) >> shift) & 255u;
     if (valid) __hip_atomic_fetch_or(mt + d, 1ull << lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     const uint64_t m = __hip_atomic_load(mt + d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     const uint32_t below = mbcnt(m);
@@ -452,7 +452,7 @@ __global__ __launch_bounds__(T, T >= 512 ? 4 : 3) void k_onesweep(
     if (T < 512 || tid >= 256) {
       const uint32_t t0 = T < 512 ? tid : tid - 256, tn = T < 512 ? T : T - 256;
       for (uint32_t s2 = t0; s2 < tile_n; s2 += tn)
-        atomicAdd(&sh.nhist[(uint32_t)(sh.stage.keys[s2] >> next_shift) & 255u], 1u);
+        atomicAdd(&sh.nhist[(uint32_t)((sh.stage.keys[s2] - kbias) >> next_shift) & 255u], 1u);
     }
   }
   if (tid < 256) {
@@ -478,7 +478,7 @@ __global__ __launch_bounds__(T, T >= 512 ? 4 : 3) void k_onesweep(
     const uint32_t s = (uint32_t)i * T + tid;
     if (s < tile_n) {
       const uint64_t kk = sh.stage.keys[s];
-      const uint32_t d = (uint32_t)(kk >> shift) & 255u;
+      const uint32_t d = (uint32_t)((kk - kbias) >> shift) & 255u;
       dg[i >> 2] |= d << (8 * (i & 3));
       kout[sh.gbase[d] + s] = kk;
     }
@@ -534,7 +534,8 @@ void fill_iota(V* v, uint64_t n, hipStream_t s) {
 
 template <typename V>
 int radix_sort_pairs(SortWork& w, KernelTimer& tm, uint64_t* k[2], V* v[2], int in_slot, uint64_t n, int bit_lo,
-                     int bit_hi, bool vals_iota, hipStream_t s, const uint64_t* d_hist0, const TextKeySrc* src) {
+                     int bit_hi, bool vals_iota, hipStream_t s, const uint64_t* d_hist0, const TextKeySrc* src,
+                     uint64_t kbias) {
   w.passes_run = 0;
   w.passes_skipped = 0;
   int cur = in_slot;
@@ -572,7 +573,7 @@ int radix_sort_pairs(SortWork& w, KernelTimer& tm, uint64_t* k[2], V* v[2], int 
     TimedLaunch t(tm, "radix_hist", (double)n * 8);
     unsigned g = (unsigned)std::min<uint64_t>(ceil_div(n, HG_PER_BLOCK), 2048);
     k_digit_hist<<<g, HG_T, 0, s>>>(k[cur], n, bit_lo + 8 * p, 1,
-                                    reinterpret_cast<unsigned long long*>(hist + p * 256));
+                                    reinterpret_cast<unsigned long long*>(hist + p * 256), kbias);
     HK_HIP(hipGetLastError());
   };
   if (src && (!d_hist0 || !vals_iota)) throw ApiError{-1, "radix_sort_pairs: text keys need hist0 and iota values"};
@@ -626,13 +627,13 @@ int radix_sort_pairs(SortWork& w, KernelTimer& tm, uint64_t* k[2], V* v[2], int 
             k[cur], iota_pending ? nullptr : v[cur], k[nxt], v[nxt], n, (uint32_t)(bit_lo + 8 * p),
             w.offs.as<uint64_t>() + p * 256, w.status.as<uint64_t>(), w.counters.as<uint32_t>() + p, w.epoch,
             w.err.as<uint32_t>(), iota_pending ? 1 : 0, has_next ? bit_lo + 8 * (p + 1) : -1,
-            w.hpart.as<unsigned long long>());
+            w.hpart.as<unsigned long long>(), TextKeySrc{}, kbias);
       else
         k_onesweep<V, OS_T, OS_I, 0><<<(unsigned)tiles, OS_T, 0, s>>>(
             k[cur], iota_pending ? nullptr : v[cur], k[nxt], v[nxt], n, (uint32_t)(bit_lo + 8 * p),
             w.offs.as<uint64_t>() + p * 256, w.status.as<uint64_t>(), w.counters.as<uint32_t>() + p, w.epoch,
             w.err.as<uint32_t>(), iota_pending ? 1 : 0, has_next ? bit_lo + 8 * (p + 1) : -1,
-            w.hpart.as<unsigned long long>());
+            w.hpart.as<unsigned long long>(), TextKeySrc{}, kbias);
       HK_HIP(hipGetLastError());
     }
     if (has_next) {
@@ -739,10 +740,10 @@ void debug_radix_bench(SortWork& w, uint64_t* k[2], uint32_t* v[2], uint64_t n, 
 
 template int radix_sort_pairs<uint32_t>(SortWork&, KernelTimer&, uint64_t* k[2], uint32_t* v[2],
                                         int, uint64_t, int, int, bool, hipStream_t, const uint64_t*,
-                                        const TextKeySrc*);
+                                        const TextKeySrc*, uint64_t);
 template int radix_sort_pairs<uint64_t>(SortWork&, KernelTimer&, uint64_t* k[2], uint64_t* v[2],
                                         int, uint64_t, int, int, bool, hipStream_t, const uint64_t*,
-                                        const TextKeySrc*);
+                                        const TextKeySrc*, uint64_t);
 template void fill_iota<uint32_t>(uint32_t*, uint64_t, hipStream_t);
 template void fill_iota<uint64_t>(uint64_t*, uint64_t, hipStream_t);
 

@@ -42,10 +42,11 @@ void scan_exclusive_max_u64(SortWork& w, const uint64_t* in, uint64_t* out, uint
 // already computed it.  Each pass computes the next digit's histogram on the fly; digits whose
 // histogram shows a single bucket are skipped.
 // src (nullable): the first pass builds the keys from the text (k[in_slot] unused; vals_iota required).
+// kbias: digits are taken from key - kbias (every key >= kbias; the keys themselves are unchanged).
 template <typename V>
 int radix_sort_pairs(SortWork& w, KernelTimer& tm, uint64_t* k[2], V* v[2], int in_slot, uint64_t n, int bit_lo,
                      int bit_hi, bool vals_iota, hipStream_t s, const uint64_t* d_hist0 = nullptr,
-                     const TextKeySrc* src = nullptr);
+                     const TextKeySrc* src = nullptr, uint64_t kbias = 0);
 
 // diagnostics: per-pass ms of onesweep variants {512x16, 512x16 no-lookback, 512x16 no-lookback
 // no-staging, 256x16, 256x16 no-lookback, 1024x8} and of a plain pair copy; out[7] = error flag

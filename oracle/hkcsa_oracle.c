@@ -281,7 +281,23 @@ int oracle_key_geometry(const uint8_t* t, uint64_t n, int* q_out, int* pb_out, u
   return sigma;
 }
 
-/* bucket (top 14 key bits) of suffix p under the build's key geometry */
+/* Partition geometry of the sharded build (hk_shard.hip partition_geometry): codes and R as
+ * above, no prev field (pb = 0: a bucket must be a range of the suffix order, which the prev
+ * field would split), and as many symbols as fit in 64 bits, so the top 14 bits are as fine a
+ * prefix split as possible. */
+static int partition_geometry(const uint8_t* t, uint64_t n, int* q_out, int* pb_out, uint64_t* R_out, int* kb_out,
+                              uint16_t code[256]) {
+  int q, pb, kb;
+  const int sigma = oracle_key_geometry(t, n, &q, &pb, R_out, &kb, code);
+  q = 1;
+  while (q < 64 && mixed_radix_bits(*R_out, q + 1) <= 64) ++q;
+  *q_out = q;
+  *pb_out = 0;
+  *kb_out = mixed_radix_bits(*R_out, q);
+  return sigma;
+}
+
+/* bucket (top 14 key bits) of suffix p under the partition geometry */
 static uint64_t shard_bucket(const uint8_t* t, uint64_t n, uint64_t p, const uint16_t* code, int q, int pb,
                              uint64_t R, int bsh) {
   uint64_t key = 0;
@@ -296,7 +312,7 @@ void oracle_shard_hist(const uint8_t* t, uint64_t n, uint64_t lo, uint64_t hi, u
   uint16_t code[256];
   int q, pb, kb;
   uint64_t R;
-  oracle_key_geometry(t, n, &q, &pb, &R, &kb, code);
+  partition_geometry(t, n, &q, &pb, &R, &kb, code);
   int bsh = kb - 14;
   if (bsh < 0) bsh = 0;
   memset(hist, 0, 16384 * sizeof(uint64_t));
@@ -309,7 +325,7 @@ void oracle_shard_below(const uint8_t* t, uint64_t n, uint64_t lo, uint64_t hi, 
   uint16_t code[256];
   int q, pb, kb;
   uint64_t R;
-  oracle_key_geometry(t, n, &q, &pb, &R, &kb, code);
+  partition_geometry(t, n, &q, &pb, &R, &kb, code);
   int bsh = kb - 14;
   if (bsh < 0) bsh = 0;
   for (int j = 0; j < nb; ++j) below[j] = 0;
