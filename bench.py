@@ -249,6 +249,11 @@ def run_sharded(args, rank: int, world: int, local_rank: int) -> dict | None:
     wall = float(el.item())
     lo, hi = dev.shard_range()
     roof = roofline(dev, args.traffic_gb)
+    stages = stage_breakdown(dev, ["shard_hist", "shard_below", "shard_select_count", "shard_pack_select",
+                                   "rccl_allreduce_hist", "rccl_allreduce_counts", "rccl_allgather_bounds",
+                                   "sa_bucket_hist", "sa_bucket_sort", "radix_hist", "radix_onesweep",
+                                   "radix_onesweep_small", "shard_split_join", "sa_refine_stats",
+                                   "sa_refine_apply", "sa_refine_keys", "scan"])
     res = None
     if rank == 0:
         value = args.steps * n / 2**20 / wall
@@ -272,7 +277,7 @@ def run_sharded(args, rank: int, world: int, local_rank: int) -> dict | None:
                        "positions": "u64" if (n >= 2**32 - 1 or args.pos64) else "u32"},
             "roofline": roof,
             "locate_patterns_per_s": None,
-            "detail": {"rank0_slice": [lo, hi]},
+            "detail": {"rank0_slice": [lo, hi], "stages_ms_total": stages, "build_info": dev.build_info()[:16]},
         }
     dev.close()
     return res

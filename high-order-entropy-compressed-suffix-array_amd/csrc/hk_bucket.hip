@@ -228,15 +228,33 @@ __global__ __launch_bounds__(BS_T, 1) void k_bucket_sort(const uint64_t* __restr
   for (uint32_t i = tid; i < BS_V * 256; i += BS_T) (&sh.whist[0][0])[i] = 0;
   for (uint32_t i = tid; i < BS_W * 256; i += BS_T) (&sh.mt[0][0])[i] = 0;
 
-  // ---- load (original order) and the varying-bit range of the sym fields
+  // ---- load (original order), the item's smallest sym field, and the varying-bit range of the
+  // sym fields above it (local keys are sym - min: a bin that straddles a power of two stays narrow)
   uint64_t key[BS_I];
-  uint64_t vor = 0, vand = ~0ull;
 #pragma unroll
   for (int k = 0; k < BS_I; ++k) key[k] = ((vmask >> k) & 1u) ? kb[s0 + 64u * k] : 0;
+  uint64_t xmin = ~0ull;
+#pragma unroll
+  for (int k = 0; k < BS_I; ++k)
+    if ((vmask >> k) & 1u) {
+      const uint64_t x = ((key[k] >> pbe) & symmask) - symbias;
+      xmin = x < xmin ? x : xmin;
+    }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const uint64_t t = __shfl_xor(xmin, o, 64);
+    xmin = t < xmin ? t : xmin;
+  }
+  if (lane == 0) sh.rv[0][wv] = xmin;
+  __syncthreads();
+#pragma unroll
+  for (int w = 0; w < BS_W; ++w) xmin = sh.rv[0][w] < xmin ? sh.rv[0][w] : xmin;
+  const uint64_t base = symbias + xmin;
+  uint64_t vor = 0, vand = ~0ull;
 #pragma unroll
   for (int k = 0; k < BS_I; ++k) {
     if ((vmask >> k) & 1u) {
-      const uint64_t sym = ((key[k] >> pbe) & symmask) - symbias;
+      const uint64_t sym = ((key[k] >> pbe) & symmask) - base;
       vor |= sym;
       vand &= sym;
     }
@@ -246,6 +264,7 @@ __global__ __launch_bounds__(BS_T, 1) void k_bucket_sort(const uint64_t* __restr
     vor |= __shfl_xor(vor, o, 64);
     vand &= __shfl_xor(vand, o, 64);
   }
+  __syncthreads();   // every wave has read rv[0]
   if (lane == 0) {
     sh.rv[0][wv] = vor;
     sh.rv[1][wv] = vand;
@@ -270,7 +289,7 @@ __global__ __launch_bounds__(BS_T, 1) void k_bucket_sort(const uint64_t* __restr
 #pragma unroll
   for (int k = 0; k < BS_I; ++k) {
     // varying bits only (the constant bits above them would collide with the packed prev code)
-    const uint64_t lk = ((((key[k] >> pbe) & symmask) - symbias) >> lo) & (width >= 64 ? ~0ull : ((1ull << width) - 1));
+    const uint64_t lk = ((((key[k] >> pbe) & symmask) - base) >> lo) & (width >= 64 ? ~0ull : ((1ull << width) - 1));
     // prev code and position high bits ride together: in the key word above the varying bits, or
     // in the u16 plane by original slot
     const uint32_t pv = ((uint32_t)(key[k] >> hb) & pmask) | (((uint32_t)key[k] & himask) << pb);
@@ -448,6 +467,23 @@ __global__ __launch_bounds__(BS_T, 1) void k_bucket_sort(const uint64_t* __restr
   }
   const uint32_t tmask = eqp | eqn;
   const uint32_t hmask = tmask & ~eqp;
+  // tie-list space: one global atomic per workgroup (a per-wave atomic on the single counter
+  // serialises in L2 when ties are frequent), each thread's ties at a block-scanned offset
+  const uint32_t nt = __popc(tmask & vmask);
+  const uint32_t tinc = wave_incl_sum<uint32_t>(nt);
+  uint32_t* const wt = reinterpret_cast<uint32_t*>(&sh.rv[0][0]);   // rv is free after the load
+  if (lane == 63) wt[wv] = tinc;
+  __syncthreads();
+  if (tid == 0) {
+    uint32_t tot = 0;
+#pragma unroll
+    for (int w = 0; w < BS_W; ++w) tot += wt[w];
+    const uint64_t b = tot ? atomicAdd(tie_n, (unsigned long long)tot) : 0ull;
+    sh.rv[1][0] = b;
+  }
+  __syncthreads();
+  uint64_t tpos = sh.rv[1][0] + (tinc - nt);
+  for (uint32_t w = 0; w < wv; ++w) tpos += wt[w];
   __syncthreads();
 
   // ---- SA / BWT in sorted order: the positions are loaded coalesced in original order, staged in
@@ -470,17 +506,10 @@ __global__ __launch_bounds__(BS_T, 1) void k_bucket_sort(const uint64_t* __restr
       sab[r] = p;
       bwb[r] = sh.inv[pv & pmask];
     }
-    const bool tied = valid && ((tmask >> k) & 1u);
-    const uint64_t tb = ballot64(tied);
-    if (tb) {
-      uint64_t base = 0;
-      if (lane == 0) base = atomicAdd(tie_n, (unsigned long long)__popcll(tb));
-      base = __shfl(base, 0, 64);
-      if (tied) {
-        const uint64_t a = base + mbcnt(tb);
-        tie_k[a] = (((uint64_t)start + r) << 1) | ((hmask >> k) & 1u);
-        tie_v[a] = p;
-      }
+    if (valid && ((tmask >> k) & 1u)) {
+      tie_k[tpos] = (((uint64_t)start + r) << 1) | ((hmask >> k) & 1u);
+      tie_v[tpos] = p;
+      ++tpos;
     }
   }
   if (TRACE) {
@@ -678,15 +707,30 @@ uint64_t sort_bucket_items(Index& ix, const BucketPlan& plan, const uint64_t* ke
   return ntie;
 }
 
-// histogram of ((key >> pbe) - symbias) >> bsh over the keys (u16-pair LDS bins, as k_bucket_hist)
-__global__ __launch_bounds__(BH_T, 1) void k_key_bucket_hist(const uint64_t* __restrict__ keys, uint64_t m, int pbe,
-                                                             uint64_t symbias, int bsh, uint32_t nbins,
+// histogram of ((key >> pbe) - symbias) >> bsh over the keys (u16-pair LDS bins, as k_bucket_hist).
+// MUL: bins by multiplication instead, bin = hi64((sym - symbias) * mul) — exactly 2^16 bins over the
+// slice's sym range wherever it starts — and each key gets its bin in the free bits above the sym
+// field (bit binpos), where the LSD passes find it.
+template <bool MUL>
+__global__ __launch_bounds__(BH_T, 1) void k_key_bucket_hist(uint64_t* __restrict__ keys, uint64_t m, int pbe,
+                                                             uint64_t symmask, uint64_t symbias, int bsh,
+                                                             uint64_t mul, int binpos, uint32_t nbins,
                                                              unsigned long long* __restrict__ hist) {
   __shared__ uint32_t H[32768];
   for (uint32_t i = threadIdx.x; i < 32768; i += BH_T) H[i] = 0;
   __syncthreads();
-  for (uint64_t j = (uint64_t)blockIdx.x * BH_T + threadIdx.x; j < m; j += (uint64_t)gridDim.x * BH_T)
-    bh_add(H, (uint32_t)(((keys[j] >> pbe) - symbias) >> bsh), hist);
+  for (uint64_t j = (uint64_t)blockIdx.x * BH_T + threadIdx.x; j < m; j += (uint64_t)gridDim.x * BH_T) {
+    const uint64_t k = keys[j];
+    const uint64_t x = ((k >> pbe) & symmask) - symbias;
+    uint32_t b;
+    if (MUL) {
+      b = (uint32_t)__umul64hi(x, mul);
+      keys[j] = k | ((uint64_t)b << binpos);
+    } else {
+      b = (uint32_t)(x >> bsh);
+    }
+    bh_add(H, b, hist);
+  }
   __syncthreads();
   for (uint32_t i = threadIdx.x; i < 32768; i += BH_T) {
     const uint32_t v = H[i];
@@ -841,9 +885,24 @@ template <typename V>
 bool bucket_sort_slice(Index& ix, const KeyGeom& kg, uint64_t m, int hb, uint64_t kmin, uint64_t kmax) {
   hipStream_t s = ix.stream;
   const int pb = kg.pb, sb = kg.sym_bits, pbe = pb + hb;
+  const uint64_t symmask = sb >= 64 ? ~0ull : ((1ull << sb) - 1);
+  const unsigned __int128 span = (unsigned __int128)(kmax - kmin) + 1;
   const int sbl = std::max(1, bits_of((unsigned __int128)(kmax - kmin)));   // bits of the slice's sym range
-  const int bsh = bucket_shift(m, sbl, (unsigned __int128)(kmax - kmin) + 1);
-  const int D = sbl - bsh;
+  int bsh = bucket_shift(m, sbl, span);
+  int D = sbl - bsh;
+  // Shift bins cover [kmin, kmin + 2^(bsh+D)): a range just past a power of two wastes half of the
+  // 2^16 bins, leaving every bucket over one sort's capacity.  Multiplicative bins (exactly 2^16
+  // over the range) need 16 free key bits above the sym field and one extra key write.
+  const int binpos = pbe + sb;
+  const bool mul = m > (uint64_t)BS_CAP &&
+                   ((double)m / (double)(((kmax - kmin) >> bsh) + 1) > 16500.0 || (ix.flags & kFlagMulBins)) &&
+                   binpos + 16 <= 64 && span > ((unsigned __int128)1 << 16);
+  uint64_t M = 0;
+  if (mul) {
+    M = (uint64_t)((((unsigned __int128)1) << 80) / span);   // hi64(x * M) < 2^16 for x < span
+    D = 16;
+    bsh = std::max(0, bits_of(span >> 16)) + 1;              // local sym bits of one bin (at most)
+  }
   const uint32_t nbins = 1u << D;
   std::vector<uint64_t> hist(nbins, 0);
   uint64_t* kp[2] = {ix.keys[0].as<uint64_t>(), ix.keys[1].as<uint64_t>()};
@@ -852,9 +911,14 @@ bool bucket_sort_slice(Index& ix, const KeyGeom& kg, uint64_t m, int hb, uint64_
     ix.bk_hist.ensure((uint64_t)nbins * 8);
     HK_HIP(hipMemsetAsync(ix.bk_hist.p, 0, (uint64_t)nbins * 8, s));
     {
-      TimedLaunch t(ix.timer, "sa_bucket_hist", (double)m * 8);
-      k_key_bucket_hist<<<(unsigned)std::min<uint64_t>(ceil_div(m, BH_T * 16), 256), BH_T, 0, s>>>(
-          kp[0], m, pbe, kmin, bsh, nbins, ix.bk_hist.as<unsigned long long>());
+      TimedLaunch t(ix.timer, "sa_bucket_hist", (double)m * (mul ? 16 : 8));
+      const unsigned g = (unsigned)std::min<uint64_t>(ceil_div(m, BH_T * 16), 256);
+      if (mul)
+        k_key_bucket_hist<true><<<g, BH_T, 0, s>>>(kp[0], m, pbe, symmask, kmin, 0, M, binpos, nbins,
+                                                   ix.bk_hist.as<unsigned long long>());
+      else
+        k_key_bucket_hist<false><<<g, BH_T, 0, s>>>(kp[0], m, pbe, symmask, kmin, bsh, 0, 0, nbins,
+                                                    ix.bk_hist.as<unsigned long long>());
       HK_HIP(hipGetLastError());
     }
     HK_HIP(hipMemcpyAsync(hist.data(), ix.bk_hist.p, (uint64_t)nbins * 8, hipMemcpyDeviceToHost, s));
@@ -866,6 +930,14 @@ bool bucket_sort_slice(Index& ix, const KeyGeom& kg, uint64_t m, int hb, uint64_
   ix.info[4] = plan.items_n.size() + plan.items_w.size();
   ix.info[5] = plan.big_start.size();
   ix.info[6] = plan.big_total;
+  static const bool dbg = getenv("HKCSA_SHARD_DEBUG") != nullptr;   // diagnostic: slice plan
+  if (dbg) {
+    uint64_t hmax = 0, nz = 0;
+    for (uint64_t c : hist) { hmax = std::max(hmax, c); nz += c != 0; }
+    fprintf(stderr, "[slice] m=%llu sbl=%d bsh=%d D=%d mul=%d nonempty=%llu max=%llu narrow=%zu wide=%zu big=%zu\n",
+            (unsigned long long)m, sbl, bsh, D, (int)mul, (unsigned long long)nz, (unsigned long long)hmax,
+            plan.items_n.size(), plan.items_w.size(), plan.big_start.size());
+  }
   if (plan.big_total) return false;
   int slot = 0;
   if (D > 0) {
@@ -874,9 +946,13 @@ bool bucket_sort_slice(Index& ix, const KeyGeom& kg, uint64_t m, int hb, uint64_
     for (uint32_t b = 0; b < nbins; ++b) h0[b & ((1u << lowd) - 1)] += hist[b];
     uint64_t* d_h0 = reinterpret_cast<uint64_t*>(ix.small.as<uint8_t>() + 5120);
     HK_HIP(hipMemcpyAsync(d_h0, h0, sizeof(h0), hipMemcpyHostToDevice, s));
-    // digits of (key - kmin << pbe): the slice's local bucket is the D bits above bsh
-    slot = radix_sort_pairs<uint32_t>(ix.sw, ix.timer, kp, vp, 0, m, pbe + bsh, pbe + bsh + D, false, s, d_h0,
-                                      nullptr, kmin << pbe);
+    // digits of (key - kmin << pbe): the slice's local bucket is the D bits above bsh (or the bin
+    // field above the sym field)
+    if (mul)
+      slot = radix_sort_pairs<uint32_t>(ix.sw, ix.timer, kp, vp, 0, m, binpos, binpos + 16, false, s, d_h0);
+    else
+      slot = radix_sort_pairs<uint32_t>(ix.sw, ix.timer, kp, vp, 0, m, pbe + bsh, pbe + bsh + D, false, s, d_h0,
+                                        nullptr, kmin << pbe);
     ix.info[0] += ix.sw.passes_run;
     ix.info[1] += ix.sw.passes_skipped;
   }

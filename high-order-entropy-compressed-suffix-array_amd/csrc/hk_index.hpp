@@ -11,7 +11,8 @@ namespace hk {
 constexpr int kMaxLevels = 8;
 constexpr uint32_t kFlagPos64 = 1u;   // hkcsa_opts.flags: 64-bit positions in sharded builds at any n
 constexpr uint32_t kFlagNoSplit = 2u; // ... and sort them as whole u64 values (no split low/high halves)
-constexpr uint32_t kFlagGlobalSort = 4u; // single GPU: full LSD sort of the keys (no bucket sorts)
+constexpr uint32_t kFlagGlobalSort = 4u; // full LSD sort of the keys (no bucket sorts)
+constexpr uint32_t kFlagMulBins = 8u;    // sharded slices: force multiplicative bucket bins
 constexpr int kLineBits = 448;   // 7 data words per 64-B rank line (word 0 = ones before the line)
 
 struct WtTables {                // per level, per dense code (host mirror of the device tables)

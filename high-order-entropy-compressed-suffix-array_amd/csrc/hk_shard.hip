@@ -19,6 +19,8 @@
 
 #include <rccl/rccl.h>
 
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 
 #include "hk_index.hpp"
@@ -62,8 +64,19 @@ __global__ __launch_bounds__(256) void k_shard_hist(const uint8_t* __restrict__ 
   for (int i = threadIdx.x; i < SH_BUCKETS; i += 256) H[i] = 0;
   __syncthreads();
   const uint64_t j0 = (lo + SH_SAMPLE - 1) / SH_SAMPLE, j1 = (hi + SH_SAMPLE - 1) / SH_SAMPLE;
-  for (uint64_t j = j0 + (uint64_t)blockIdx.x * 256 + threadIdx.x; j < j1; j += (uint64_t)gridDim.x * 256)
-    atomicAdd(&H[key_global(t, n, L, j * SH_SAMPLE, g.R, g.q, g.pb) >> g.bsh], 1u);
+  for (uint64_t j = j0 + (uint64_t)blockIdx.x * 256 + threadIdx.x; j < j1; j += (uint64_t)gridDim.x * 256) {
+    // the first 32 symbols from two 16-byte loads (p is a multiple of 16; T' has 64 pad bytes)
+    const uint64_t p = j * SH_SAMPLE;
+    const uint4 a = *reinterpret_cast<const uint4*>(t + p);
+    const uint4 b = *reinterpret_cast<const uint4*>(t + p + 16);
+    const uint32_t w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    uint64_t key = 0;
+#pragma unroll
+    for (int i = 0; i < 32; ++i)
+      if (i < g.q) key = key * g.R + (p + i < n ? L[(w[i >> 2] >> (8 * (i & 3))) & 255u] : 0u);
+    for (int i = 32; i < g.q; ++i) key = key * g.R + (p + i < n ? L[t[p + i]] : 0u);
+    atomicAdd(&H[key >> g.bsh], 1u);
+  }
   __syncthreads();
   for (int i = threadIdx.x; i < SH_BUCKETS; i += 256)
     if (H[i]) atomicAdd(&hist[i], (unsigned long long)H[i]);
@@ -567,6 +580,11 @@ void shard_build_t(Index& ix, const uint64_t* ghist, const uint64_t* gbelow, int
   HK_HIP(hipStreamSynchronize(s));
   if (got != m) throw ApiError{-7, "shard selection count mismatch"};
   if (kmm[0] > kmm[1]) throw ApiError{-7, "shard selection produced no keys"};
+  static const bool dbg = getenv("HKCSA_SHARD_DEBUG") != nullptr;   // diagnostic: slice geometry
+  if (dbg)
+    fprintf(stderr, "[shard] rank %d/%d m=%llu q=%d sb=%d pb=%d hb=%d kmin=%llx kmax=%llx\n", rank, nranks,
+            (unsigned long long)m, kk.q, kk.sym_bits, kk.pb, hb, (unsigned long long)kmm[0],
+            (unsigned long long)kmm[1]);
   // LDS bucket sorts over the slice's sym range, unless a bucket is too big for them
   if (!whole && !(ix.flags & kFlagGlobalSort) && bucket_sort_slice<V>(ix, kk, m, hb, kmm[0], kmm[1])) {
     HK_HIP(hipStreamSynchronize(s));

@@ -76,7 +76,8 @@ class QuerySet:
 
 
 FLAG_POS64 = 1   # HKCSA_FLAG_POS64: 64-bit positions in sharded builds at any n
-FLAG_GLOBAL_SORT = 4   # HKCSA_FLAG_GLOBAL_SORT: single-GPU build by full-width LSD sort (no bucket sorts)
+FLAG_GLOBAL_SORT = 4   # HKCSA_FLAG_GLOBAL_SORT: build by full-width LSD sort (no bucket sorts)
+FLAG_MUL_BINS = 8      # HKCSA_FLAG_MUL_BINS: sharded slices use multiplicative bucket bins (diagnostic)
 
 
 class DeviceIndex:

@@ -45,10 +45,12 @@ typedef struct hkcsa_index hkcsa_index;
 typedef struct hkcsa_queries hkcsa_queries;
 
 #define HKCSA_FLAG_POS64 1u    /* sharded builds keep 64-bit positions at any n             */
-#define HKCSA_FLAG_NO_SPLIT 2u /* sort 64-bit positions whole (default: u32 low halves, the  */
-                               /* high bits parked below the key)                           */
-#define HKCSA_FLAG_GLOBAL_SORT 4u /* single-GPU build: full-width LSD radix sort of every     */
-                                  /* suffix key (default: top-bit passes + LDS bucket sorts) */
+#define HKCSA_FLAG_NO_SPLIT 2u /* sharded: sort 64-bit positions whole on the global path    */
+                               /* (default: u32 low halves, the high bits below the key)    */
+#define HKCSA_FLAG_GLOBAL_SORT 4u /* full-width LSD radix sort of every suffix key (default:   */
+                                  /* top-bit passes + LDS bucket sorts); single GPU and slices */
+#define HKCSA_FLAG_MUL_BINS 8u /* sharded slices: multiplicative bucket bins even where the  */
+                               /* shift bins would do (diagnostic; chosen automatically)    */
 
 typedef struct hkcsa_opts {
   int32_t device;   /* HIP device ordinal (-1 = current)                 */

@@ -216,11 +216,14 @@ def test_full_size_config1_256MiB(hk):
                                                (4, 3, b"ACGT"), (5, 0, bytes(range(256))), (3, 0, b"ab"),
                                                (7, 0, b"AC$GT"), (6, 1, bytes(range(0x20, 0x7F))),
                                                (3, 3, bytes(range(256))), (3, 4, b"ACGT"), (2, 5, b"ACGT"),
-                                               (3, 0, b"aaaaaaaaaaaaaaab"), (2, 1, b"aaaaaaaab")])
+                                               (3, 0, b"aaaaaaaaaaaaaaab"), (2, 1, b"aaaaaaaab"),
+                                               (3, 8, b"ACGT"), (2, 9, bytes(range(0x20, 0x7F))),
+                                               (4, 8, b"aaaaaaaab")])
 def test_shard_two_phase_emulated(hk, nranks, flags, alpha):
     """Ranks emulated on one GPU; flags=1 forces the 64-bit position kernels (n >= 2^32 path: split
     u32 sort values), flags=3 the whole-u64 value sort, flags=4 the global sort of each slice instead
-    of its LDS bucket sorts; the skewed alphabets give slices whose big buckets take the global path.
+    of its LDS bucket sorts, flags=8 multiplicative bucket bins; the skewed alphabets give slices
+    whose big buckets take the global path.
     Alphabets cover the byte-image pre-test thresholds for radix 3 .. 257."""
     text = oracle.synth_text(400001, alpha, seed=12 + nranks)
     ref = oracle.suffix_array(text)

@@ -1,0 +1,12 @@
+#!/bin/bash
+# Round profile: rocprofv3 kernel stats of the default N=1 bench, PMC HBM traffic of the radix
+# passes (separate FETCH_SIZE / WRITE_SIZE passes), and the emulated per-rank work at N=8.
+cd "$GRAFT_REPO_ROOT" || exit 1
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_bench -o run -- \
+    python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/prof_bench.json 2> gpurun_out/prof_bench.err || exit $?
+echo "stats ok"
+bash tools_gpu_pmc.sh || exit $?
+timeout -k 10 400 python3 tools_shard_emulate.py --nranks 8 --ranks 0 3 7 --pos64 > gpurun_out/emul8.jsonl 2> gpurun_out/emul8.err || exit $?
+cat gpurun_out/emul8.jsonl

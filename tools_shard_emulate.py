@@ -17,8 +17,9 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)),
                                 "high-order-entropy-compressed-suffix-array_amd"))
 from hkcsa import DeviceIndex  # noqa: E402
 
-STAGES = ["shard_hist", "shard_select_count", "shard_pack_select", "radix_hist", "radix_onesweep", "radix_onesweep_small",
-          "sa_refine_stats", "sa_refine_apply", "sa_refine_keys"]
+STAGES = ["shard_select_count", "shard_pack_select", "sa_bucket_hist", "sa_bucket_sort", "radix_hist",
+          "radix_onesweep", "radix_onesweep_small", "shard_split_join", "sa_refine_stats", "sa_refine_apply",
+          "sa_refine_keys"]
 
 
 def main():
@@ -33,14 +34,15 @@ def main():
     n = args.per_rank * N + 1
     dev = DeviceIndex.synthetic(n, b"ACGT", seed=2, device=0, flags=1 if args.pos64 else 0)
     g = dev.shard_histogram(1, 0)
+    below = sum(dev.shard_counts(g, N, r) for r in range(N))   # every rank's block, summed
     for r in args.ranks:
-        dev.shard_build(g, N, r)  # warm-up (workspace growth)
+        dev.shard_build(g, below, N, r)  # warm-up (workspace growth)
         dev.synchronize()
         dev.timing_reset()
         dev.timing(True)
         t0 = time.perf_counter()
         for _ in range(args.reps):
-            dev.shard_build(g, N, r)
+            dev.shard_build(g, below, N, r)
         dev.synchronize()
         wall = (time.perf_counter() - t0) / args.reps
         dev.timing(False)
