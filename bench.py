@@ -251,9 +251,9 @@ def run_sharded(args, rank: int, world: int, local_rank: int) -> dict | None:
     roof = roofline(dev, args.traffic_gb)
     stages = stage_breakdown(dev, ["shard_hist", "shard_below", "shard_select_count", "shard_pack_select",
                                    "rccl_allreduce_hist", "rccl_allreduce_counts", "rccl_allgather_bounds",
-                                   "sa_bucket_hist", "sa_bucket_sort", "radix_hist", "radix_onesweep",
+                                   "sa_bin_starts", "sa_bucket_sort", "radix_hist", "radix_onesweep",
                                    "radix_onesweep_small", "shard_split_join", "sa_refine_stats",
-                                   "sa_refine_apply", "sa_refine_keys", "scan"])
+                                   "sa_refine_apply", "sa_refine_keys"])
     res = None
     if rank == 0:
         value = args.steps * n / 2**20 / wall

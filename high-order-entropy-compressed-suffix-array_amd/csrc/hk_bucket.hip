@@ -707,36 +707,20 @@ uint64_t sort_bucket_items(Index& ix, const BucketPlan& plan, const uint64_t* ke
   return ntie;
 }
 
-// histogram of ((key >> pbe) - symbias) >> bsh over the keys (u16-pair LDS bins, as k_bucket_hist).
-// MUL: bins by multiplication instead, bin = hi64((sym - symbias) * mul) — exactly 2^16 bins over the
-// slice's sym range wherever it starts — and each key gets its bin in the free bits above the sym
-// field (bit binpos), where the LSD passes find it.
-template <bool MUL>
-__global__ __launch_bounds__(BH_T, 1) void k_key_bucket_hist(uint64_t* __restrict__ keys, uint64_t m, int pbe,
-                                                             uint64_t symmask, uint64_t symbias, int bsh,
-                                                             uint64_t mul, int binpos, uint32_t nbins,
-                                                             unsigned long long* __restrict__ hist) {
-  __shared__ uint32_t H[32768];
-  for (uint32_t i = threadIdx.x; i < 32768; i += BH_T) H[i] = 0;
-  __syncthreads();
-  for (uint64_t j = (uint64_t)blockIdx.x * BH_T + threadIdx.x; j < m; j += (uint64_t)gridDim.x * BH_T) {
-    const uint64_t k = keys[j];
-    const uint64_t x = ((k >> pbe) & symmask) - symbias;
-    uint32_t b;
-    if (MUL) {
-      b = (uint32_t)__umul64hi(x, mul);
-      keys[j] = k | ((uint64_t)b << binpos);
-    } else {
-      b = (uint32_t)(x >> bsh);
-    }
-    bh_add(H, b, hist);
+// starts[b] = first index of bin b in keys sorted by bin = ((key - kbias) >> shift) & (nbins - 1)
+// (one lower-bound search per bin); starts[nbins] = m
+__global__ __launch_bounds__(256) void k_bin_starts(const uint64_t* __restrict__ keys, uint64_t m, uint64_t kbias,
+                                                    int shift, uint32_t nbins, uint64_t* __restrict__ starts) {
+  const uint32_t b = blockIdx.x * 256 + threadIdx.x;
+  if (b > nbins) return;
+  uint64_t lo = 0, hi = m;
+  if (b == nbins) lo = m;
+  while (lo < hi) {
+    const uint64_t mid = lo + (hi - lo) / 2;
+    if ((((keys[mid] - kbias) >> shift) & (nbins - 1)) < b) lo = mid + 1;
+    else hi = mid;
   }
-  __syncthreads();
-  for (uint32_t i = threadIdx.x; i < 32768; i += BH_T) {
-    const uint32_t v = H[i];
-    if ((v & 0xFFFFu) && 2 * i < nbins) atomicAdd(&hist[2 * i], (unsigned long long)(v & 0xFFFFu));
-    if ((v >> 16) && 2 * i + 1 < nbins) atomicAdd(&hist[2 * i + 1], (unsigned long long)(v >> 16));
-  }
+  starts[b] = lo;
 }
 
 }  // namespace
@@ -777,6 +761,15 @@ KeyGeom key_geometry_keyed(Index& ix, int reserve) {
   if (!unkeyed) m_term = 0;
   g.Rk = (uint64_t)std::max(Rk, 2);
   for (int b = 0; b < 256; ++b) g.lutk[b] = (uint16_t)(codek[b] | (b << 8));
+  {
+    int below = 0;
+    for (int b = 0; b < 256; ++b) {
+      const bool k = ix.byte_hist[b] && !(unkeyed && b == term);
+      g.kdig[b] = (uint16_t)below;
+      g.kflag[b] = k ? 1 : 0;
+      below += k ? 1 : 0;
+    }
+  }
   double p2 = 0;
   for (int b = 0; b < 256; ++b)
     if (ix.byte_hist[b] && !(unkeyed && b == term)) {
@@ -881,91 +874,98 @@ template void refine_from_ties<uint32_t>(Index&, const KeyGeom&, uint64_t, bool)
 template void refine_from_ties<uint64_t>(Index&, const KeyGeom&, uint64_t, bool);
 
 // ---------------------------------------------------------------- one sharded slice
-template <typename V>
-bool bucket_sort_slice(Index& ix, const KeyGeom& kg, uint64_t m, int hb, uint64_t kmin, uint64_t kmax) {
-  hipStream_t s = ix.stream;
-  const int pb = kg.pb, sb = kg.sym_bits, pbe = pb + hb;
-  const uint64_t symmask = sb >= 64 ? ~0ull : ((1ull << sb) - 1);
+SliceBins slice_bins(uint64_t m, const KeyGeom& kg, int hb, uint64_t kmin, uint64_t kmax, bool force_mul) {
+  SliceBins b;
+  b.kmin = kmin;
+  b.kmax = kmax;
+  b.binpos = kg.pb + hb + kg.sym_bits;
   const unsigned __int128 span = (unsigned __int128)(kmax - kmin) + 1;
   const int sbl = std::max(1, bits_of((unsigned __int128)(kmax - kmin)));   // bits of the slice's sym range
-  int bsh = bucket_shift(m, sbl, span);
-  int D = sbl - bsh;
-  // Shift bins cover [kmin, kmin + 2^(bsh+D)): a range just past a power of two wastes half of the
-  // 2^16 bins, leaving every bucket over one sort's capacity.  Multiplicative bins (exactly 2^16
-  // over the range) need 16 free key bits above the sym field and one extra key write.
-  const int binpos = pbe + sb;
-  const bool mul = m > (uint64_t)BS_CAP &&
-                   ((double)m / (double)(((kmax - kmin) >> bsh) + 1) > 16500.0 || (ix.flags & kFlagMulBins)) &&
-                   binpos + 16 <= 64 && span > ((unsigned __int128)1 << 16);
-  uint64_t M = 0;
-  if (mul) {
-    M = (uint64_t)((((unsigned __int128)1) << 80) / span);   // hi64(x * M) < 2^16 for x < span
-    D = 16;
-    bsh = std::max(0, bits_of(span >> 16)) + 1;              // local sym bits of one bin (at most)
+  b.bsh = bucket_shift(m, sbl, span);
+  b.D = sbl - b.bsh;
+  if (b.D <= 0) {
+    b.D = 0;
+    return b;
   }
+  // Shift bins cover [kmin, kmin + 2^(bsh+D)): a range just past a power of two wastes half of the
+  // 2^16 bins and leaves every bucket over one sort's capacity.  Multiplicative bins (exactly 2^16
+  // over the range) need 16 free key bits above the sym field.
+  const double mean = (double)m / (double)(((kmax - kmin) >> b.bsh) + 1);
+  if ((mean > 16500.0 || force_mul) && b.binpos + 16 <= 64 && span > ((unsigned __int128)1 << 16)) {
+    b.mul = (uint64_t)((((unsigned __int128)1) << 80) / span);   // hi64(x * mul) < 2^16 for x < span
+    b.D = 16;
+    b.bsh = bits_of(span >> 16) + 1;
+  }
+  return b;
+}
+
+template <typename V>
+bool bucket_sort_slice(Index& ix, const KeyGeom& kg, uint64_t m, int hb, const SliceBins& bins, const uint64_t* d_h0) {
+  hipStream_t s = ix.stream;
+  const int pb = kg.pb, sb = kg.sym_bits, pbe = pb + hb;
+  const int D = bins.D;
   const uint32_t nbins = 1u << D;
   std::vector<uint64_t> hist(nbins, 0);
   uint64_t* kp[2] = {ix.keys[0].as<uint64_t>(), ix.keys[1].as<uint64_t>()};
   uint32_t* vp[2] = {reinterpret_cast<uint32_t*>(ix.vals[0].p), reinterpret_cast<uint32_t*>(ix.vals[1].p)};
+  int slot = 0;
   if (D > 0) {
-    ix.bk_hist.ensure((uint64_t)nbins * 8);
-    HK_HIP(hipMemsetAsync(ix.bk_hist.p, 0, (uint64_t)nbins * 8, s));
+    // LSD passes over the bin: the bin field above the sym field (mul), or the D bits of
+    // (key - kmin << pbe) above bsh
+    const uint64_t kbias = bins.mul ? 0 : bins.kmin << pbe;
+    const int shift = bins.mul ? bins.binpos : pbe + bins.bsh;
+    slot = radix_sort_pairs<uint32_t>(ix.sw, ix.timer, kp, vp, 0, m, shift, shift + D, false, s, d_h0, nullptr,
+                                      kbias);
+    ix.info[0] += ix.sw.passes_run;
+    ix.info[1] += ix.sw.passes_skipped;
+    ix.bk_hist.ensure((uint64_t)(nbins + 1) * 8);
     {
-      TimedLaunch t(ix.timer, "sa_bucket_hist", (double)m * (mul ? 16 : 8));
-      const unsigned g = (unsigned)std::min<uint64_t>(ceil_div(m, BH_T * 16), 256);
-      if (mul)
-        k_key_bucket_hist<true><<<g, BH_T, 0, s>>>(kp[0], m, pbe, symmask, kmin, 0, M, binpos, nbins,
-                                                   ix.bk_hist.as<unsigned long long>());
-      else
-        k_key_bucket_hist<false><<<g, BH_T, 0, s>>>(kp[0], m, pbe, symmask, kmin, bsh, 0, 0, nbins,
-                                                    ix.bk_hist.as<unsigned long long>());
+      TimedLaunch t(ix.timer, "sa_bin_starts", (double)(nbins + 1) * 8);
+      k_bin_starts<<<(nbins + 1 + 255) / 256, 256, 0, s>>>(kp[slot], m, kbias, shift, nbins,
+                                                          ix.bk_hist.as<uint64_t>());
       HK_HIP(hipGetLastError());
     }
-    HK_HIP(hipMemcpyAsync(hist.data(), ix.bk_hist.p, (uint64_t)nbins * 8, hipMemcpyDeviceToHost, s));
+    std::vector<uint64_t> st(nbins + 1);
+    HK_HIP(hipMemcpyAsync(st.data(), ix.bk_hist.p, (uint64_t)(nbins + 1) * 8, hipMemcpyDeviceToHost, s));
     HK_HIP(hipStreamSynchronize(s));
+    for (uint32_t b = 0; b < nbins; ++b) hist[b] = st[b + 1] - st[b];
   } else {
     hist[0] = m;
   }
-  const BucketPlan plan = plan_buckets(hist, bsh);
+  const BucketPlan plan = plan_buckets(hist, bins.bsh);
   ix.info[4] = plan.items_n.size() + plan.items_w.size();
   ix.info[5] = plan.big_start.size();
   ix.info[6] = plan.big_total;
   static const bool dbg = getenv("HKCSA_SHARD_DEBUG") != nullptr;   // diagnostic: slice plan
   if (dbg) {
     uint64_t hmax = 0, nz = 0;
-    for (uint64_t c : hist) { hmax = std::max(hmax, c); nz += c != 0; }
-    fprintf(stderr, "[slice] m=%llu sbl=%d bsh=%d D=%d mul=%d nonempty=%llu max=%llu narrow=%zu wide=%zu big=%zu\n",
-            (unsigned long long)m, sbl, bsh, D, (int)mul, (unsigned long long)nz, (unsigned long long)hmax,
-            plan.items_n.size(), plan.items_w.size(), plan.big_start.size());
+    for (uint64_t c : hist) {
+      hmax = std::max(hmax, c);
+      nz += c != 0;
+    }
+    fprintf(stderr, "[slice] m=%llu bsh=%d D=%d mul=%d nonempty=%llu max=%llu narrow=%zu wide=%zu big=%zu\n",
+            (unsigned long long)m, bins.bsh, D, bins.mul ? 1 : 0, (unsigned long long)nz,
+            (unsigned long long)hmax, plan.items_n.size(), plan.items_w.size(), plan.big_start.size());
   }
-  if (plan.big_total) return false;
-  int slot = 0;
-  if (D > 0) {
-    uint64_t h0[256] = {0};
-    const int lowd = std::min(D, 8);
-    for (uint32_t b = 0; b < nbins; ++b) h0[b & ((1u << lowd) - 1)] += hist[b];
-    uint64_t* d_h0 = reinterpret_cast<uint64_t*>(ix.small.as<uint8_t>() + 5120);
-    HK_HIP(hipMemcpyAsync(d_h0, h0, sizeof(h0), hipMemcpyHostToDevice, s));
-    // digits of (key - kmin << pbe): the slice's local bucket is the D bits above bsh (or the bin
-    // field above the sym field)
-    if (mul)
-      slot = radix_sort_pairs<uint32_t>(ix.sw, ix.timer, kp, vp, 0, m, binpos, binpos + 16, false, s, d_h0);
-    else
-      slot = radix_sort_pairs<uint32_t>(ix.sw, ix.timer, kp, vp, 0, m, pbe + bsh, pbe + bsh + D, false, s, d_h0,
-                                        nullptr, kmin << pbe);
-    ix.info[0] += ix.sw.passes_run;
-    ix.info[1] += ix.sw.passes_skipped;
+  if (plan.big_total) {
+    if (slot != 0) {   // the global path starts from keys[0] / vals[0]
+      std::swap(ix.keys[0], ix.keys[1]);
+      std::swap(ix.vals[0], ix.vals[1]);
+    }
+    return false;
   }
   ix.bwt.ensure(m + 64);
-  const uint64_t ntie = sort_bucket_items<V>(ix, plan, kp[slot], vp[slot], m, pb, sb, hb, kmin, ix.sa.as<V>(),
-                                             ix.bwt.as<uint8_t>());
+  const uint64_t ntie = sort_bucket_items<V>(ix, plan, kp[slot], vp[slot], m, pb, sb, hb, bins.kmin,
+                                             ix.sa.as<V>(), ix.bwt.as<uint8_t>());
   ix.info.push_back(ntie);
   refine_from_ties<V>(ix, kg, ntie, false);
   return true;
 }
 
-template bool bucket_sort_slice<uint32_t>(Index&, const KeyGeom&, uint64_t, int, uint64_t, uint64_t);
-template bool bucket_sort_slice<uint64_t>(Index&, const KeyGeom&, uint64_t, int, uint64_t, uint64_t);
+template bool bucket_sort_slice<uint32_t>(Index&, const KeyGeom&, uint64_t, int, const SliceBins&,
+                                          const uint64_t*);
+template bool bucket_sort_slice<uint64_t>(Index&, const KeyGeom&, uint64_t, int, const SliceBins&,
+                                          const uint64_t*);
 
 // ---------------------------------------------------------------- driver
 void build_sa_bucketed(Index& ix) {

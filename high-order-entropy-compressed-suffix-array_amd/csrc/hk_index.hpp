@@ -44,6 +44,8 @@ struct KeyGeom {
   uint64_t skey[72];         // B(s) of the short suffixes (sym field, not shifted)
   uint32_t srank[72];        // exact order of the short suffixes among themselves
   int bucket_bits = 0;       // D: top bits of the sym field sorted by the LSD passes
+  uint16_t kdig[256];        // byte -> number of keyed bytes below it (its keyed code when keyed)
+  uint8_t kflag[256];        // byte -> 1 when keyed
 };
 int mixed_radix_bits(uint64_t R, int q);   // bits of R^q - 1 (65 when it does not fit 64 bits)
 
@@ -174,11 +176,21 @@ void comm_unique_id(uint8_t id[128]);
 KeyGeom key_geometry(Index& ix, bool with_prev);
 KeyGeom key_geometry_keyed(Index& ix, int reserve = 0);   // keyed layout; reserve = low key bits kept free
 void build_sa_bucketed(Index& ix);       // single-GPU SA + BWT: 2 LSD passes + LDS bucket sorts
-// Bucket build of one sharded slice: m keyed keys [sym][prev][position bits 32.., hb bits] in keys[0],
-// low position bits (u32) in vals[0], sym fields within [kmin, kmax].  Writes the slice's SA (V) and
-// BWT and refines ties; false (nothing written) when a bucket exceeds one LDS sort.
+// Bucket bins of one slice's sym fields, all within [kmin, kmax]: shift bins (sym - kmin) >> bsh, or
+// multiplicative bins hi64((sym - kmin) * mul) (exactly 2^16 over the range, stored in the key at
+// bit binpos) where shift bins would waste half of the range.  D = 0: one bin.
+struct SliceBins {
+  uint64_t kmin = 0, kmax = 0, mul = 0;
+  int bsh = 0;      // shift bins: the shift; mul bins: an upper bound on one bin's sym bits
+  int D = 0, binpos = 0;
+};
+SliceBins slice_bins(uint64_t m, const KeyGeom& kg, int hb, uint64_t kmin, uint64_t kmax, bool force_mul);
+// Bucket build of one sharded slice: m keyed keys [bin][sym][prev][position bits 32.., hb bits] in
+// keys[0] (bin field in mul mode only), low position bits (u32) in vals[0], d_h0 = histogram of the
+// bins' low byte.  Writes the slice's SA (V) and BWT and refines ties; false (nothing written) when
+// a bucket exceeds one LDS sort.
 template <typename V>
-bool bucket_sort_slice(Index& ix, const KeyGeom& kg, uint64_t m, int hb, uint64_t kmin, uint64_t kmax);
+bool bucket_sort_slice(Index& ix, const KeyGeom& kg, uint64_t m, int hb, const SliceBins& bins, const uint64_t* d_h0);
 // tie list (J << 1 | head, P) of m entries in (k, v) -> refinement loop (from symbol offset h)
 template <typename V>
 void refine_from_ties(Index& ix, const KeyGeom& kg, uint64_t A, bool allow_doubling);

@@ -237,10 +237,13 @@ __global__ __launch_bounds__(256) void k_select_count(const uint8_t* __restrict_
 }
 
 // Keys of the selected suffixes in the keyed layout of the single-GPU bucket build (see
-// key_geometry_keyed): [sym][dense code of T'[p-1], pb bits][position bits 32.., hb bits].  With
-// hb > 0 (V = u32) the low 32 position bits go to vals and the high bits sit below the key,
-// outside the sorted bit range; k_split_join reassembles them.  kmm[0..1] collect the min / max
-// sym of the slice (the bucket range of its LDS sorts).
+// key_geometry_keyed): [bin][sym][dense code of T'[p-1], pb bits][position bits 32.., hb bits],
+// the bin field only for multiplicative bins.  With hb > 0 (V = u32) the low 32 position bits go
+// to vals and the high bits sit below the key, outside the sorted bit range; k_split_join
+// reassembles them.  Keys come from the tile's keyed codes staged in LDS (measured faster than
+// building each selected key from global text words, even at 1/8 selection density).
+// kmm[0..1] collect the exact min / max sym (checked against the slice bounds), hist0 the
+// histogram of the bins' low byte (the first LSD pass).
 template <typename V>
 __global__ __launch_bounds__(256) void k_select_write(const uint8_t* __restrict__ t, uint64_t n, uint64_t tpb,
                                                       const uint16_t* __restrict__ lut,
@@ -250,15 +253,18 @@ __global__ __launch_bounds__(256) void k_select_write(const uint8_t* __restrict_
                                                       BucketGeom g, SelGeom sg, uint32_t blo, uint32_t bhi,
                                                       const uint64_t* __restrict__ block_off,
                                                       uint64_t* __restrict__ keys, V* __restrict__ vals, int hb,
-                                                      unsigned long long* __restrict__ kmm) {
+                                                      SliceBins sbn, unsigned long long* __restrict__ kmm,
+                                                      unsigned long long* __restrict__ hist0) {
   __shared__ uint16_t c[PS_TILE + kCodePad];
   __shared__ uint16_t list[PS_TILE];
   __shared__ uint16_t L[256], LK[256], LP[256];
   __shared__ uint64_t SK[64];
   __shared__ uint32_t red[4];
+  __shared__ uint32_t H0[256];
   L[threadIdx.x] = lut[threadIdx.x];
   LK[threadIdx.x] = lutk[threadIdx.x];
   LP[threadIdx.x] = lutp[threadIdx.x];
+  H0[threadIdx.x] = 0;
   if (threadIdx.x < 64 && ka.s_start + threadIdx.x < n) SK[threadIdx.x] = skey[threadIdx.x];
   __syncthreads();
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -298,6 +304,12 @@ __global__ __launch_bounds__(256) void k_select_write(const uint8_t* __restrict_
       kmax = sym > kmax ? sym : kmax;
       uint64_t key = (sym << pbe) | ((uint64_t)LP[c[off] >> 8] << hb);
       if (hb) key |= p >> 32;
+      if (sbn.D > 0) {
+        const uint64_t x = sym - sbn.kmin;
+        const uint32_t bin = sbn.mul ? (uint32_t)__umul64hi(x, sbn.mul) : (uint32_t)(x >> sbn.bsh);
+        if (sbn.mul) key |= (uint64_t)bin << sbn.binpos;
+        atomicAdd(&H0[bin & 255u], 1u);
+      }
       keys[run + i] = key;
       vals[run + i] = (V)p;
     }
@@ -313,6 +325,8 @@ __global__ __launch_bounds__(256) void k_select_write(const uint8_t* __restrict_
     atomicMin(&kmm[0], (unsigned long long)kmin);
     atomicMax(&kmm[1], (unsigned long long)kmax);
   }
+  __syncthreads();
+  if (H0[threadIdx.x]) atomicAdd(&hist0[threadIdx.x], (unsigned long long)H0[threadIdx.x]);
 }
 
 __global__ __launch_bounds__(256) void k_split_join(uint64_t* __restrict__ keys, const uint32_t* __restrict__ lo32,
@@ -496,6 +510,42 @@ std::vector<uint32_t> splitters(const uint64_t* ghist, int nranks) {
   return B;
 }
 
+// Bounds of the keyed sym fields of the suffixes whose partition bucket lies in [blo, bhi), from
+// the partition keys alone.  A partition key spells a string: digit d >= 1 is byte inv[d], digit 0
+// ends it.  Every suffix of the range is >= the string of the range's first key and <= that of its
+// last.  Digit of byte b in keyed radix: kdig[b] (the keyed bytes below b; its keyed code when b is
+// keyed); the string stops after a non-keyed byte (the unique terminal: a short suffix, whose
+// boundary key is exactly that prefix followed by zeros) or at its end.  The lower bound fills the
+// remaining digits with 0, the upper bound with Rk - 1; both are monotone in the string, so the
+// slice's sym fields lie in [lo, hi].
+std::pair<uint64_t, uint64_t> slice_sym_bounds(const KeyGeom& pg, int bsh_p, uint32_t blo, uint32_t bhi,
+                                               const KeyGeom& kk) {
+  unsigned __int128 Rq = 1;
+  for (int i = 0; i < pg.q; ++i) Rq *= pg.R;
+  auto bound = [&](unsigned __int128 pkey, bool upper) -> uint64_t {
+    if (pkey > Rq - 1) pkey = Rq - 1;   // the last bucket's top key may lie past R^q - 1
+    std::vector<int> d(pg.q);
+    for (int i = pg.q - 1; i >= 0; --i) {
+      d[i] = (int)(pkey % pg.R);
+      pkey /= pg.R;
+    }
+    unsigned __int128 v = 0;
+    int i = 0;
+    while (i < kk.q && i < pg.q && d[i] != 0) {
+      const uint8_t b = pg.inv[d[i]];
+      v = v * kk.Rk + kk.kdig[b];
+      ++i;
+      if (!kk.kflag[b]) break;
+    }
+    for (; i < kk.q; ++i) v = v * kk.Rk + (upper ? kk.Rk - 1 : 0);
+    const unsigned __int128 mx = kk.sym_bits >= 64 ? ~(uint64_t)0 : ((((unsigned __int128)1) << kk.sym_bits) - 1);
+    return (uint64_t)(v < mx ? v : mx);
+  };
+  const uint64_t lo = bound((unsigned __int128)blo << bsh_p, false);
+  const uint64_t hi = bound((((unsigned __int128)bhi) << bsh_p) - 1, true);
+  return {lo, hi};
+}
+
 template <typename V>
 void shard_build_t(Index& ix, const uint64_t* ghist, const uint64_t* gbelow, int nranks, int rank) {
   const uint64_t n = ix.n;
@@ -535,12 +585,19 @@ void shard_build_t(Index& ix, const uint64_t* ghist, const uint64_t* gbelow, int
   const uint8_t* small = ix.small.as<uint8_t>();
   const KeyChunks kch = key_chunks(kk.Rk, kk.q);
   const KeyedArgs ka{kk.Rk, kch.Rck, kch.Rlast, kk.s_start, kk.q, kch.ck, kk.pb, 0};
+  const BucketGeom bg = bucket_geom(kg);
+  // bucket bins of the slice from its sym bounds (known before any key is built)
+  const auto kb = slice_sym_bounds(kg, bg.bsh, blo, bhi, kk);
+  const bool global = whole || (ix.flags & kFlagGlobalSort);
+  SliceBins sbn = global ? SliceBins{} : slice_bins(m, kk, hb, kb.first, kb.second, ix.flags & kFlagMulBins);
   uint64_t got = 0;
   uint64_t kmm[2] = {~0ull, 0};
   for (int i = 0; i < 2; ++i) {
     ix.keys[i].ensure(m * 8 + 16);
     ix.vals[i].ensure(m * sizeof(V) + 16);
   }
+  uint64_t* d_h0 = reinterpret_cast<uint64_t*>(ix.small.as<uint8_t>() + 5120);
+  HK_HIP(hipMemsetAsync(d_h0, 0, 256 * 8, s));
   {
     const uint64_t tiles = ceil_div(n, (uint64_t)PS_TILE);
     const uint64_t G = tiles < 8192 ? tiles : 8192;
@@ -554,7 +611,6 @@ void shard_build_t(Index& ix, const uint64_t* ghist, const uint64_t* gbelow, int
     const uint16_t* lutk = reinterpret_cast<const uint16_t*>(small + 2560);
     const uint16_t* lutp = reinterpret_cast<const uint16_t*>(small + 4608);
     const uint64_t* skey = reinterpret_cast<const uint64_t*>(small + 3584);
-    const BucketGeom bg = bucket_geom(kg);
     const SelGeom sg = sel_geom(kg, bg, blo, bhi);
     {
       TimedLaunch t(ix.timer, "shard_select_count", (double)n);
@@ -564,14 +620,15 @@ void shard_build_t(Index& ix, const uint64_t* ghist, const uint64_t* gbelow, int
     scan_exclusive_u64(ix.sw, bc, bc, grid, true, s);
     {
       TimedLaunch t(ix.timer, "shard_pack_select", (double)n + (double)m * (8 + sizeof(V)));
+      unsigned long long* h0 = reinterpret_cast<unsigned long long*>(d_h0);
       if (hb)
         k_select_write<uint32_t><<<grid, 256, 0, s>>>(ix.text.as<uint8_t>(), n, tpb, lut, lutk, lutp, skey, ka, bg,
                                                       sg, blo, bhi, bc, ix.keys[0].as<uint64_t>(),
-                                                      ix.vals[0].as<uint32_t>(), hb, d_kmm);
+                                                      ix.vals[0].as<uint32_t>(), hb, sbn, d_kmm, h0);
       else
         k_select_write<V><<<grid, 256, 0, s>>>(ix.text.as<uint8_t>(), n, tpb, lut, lutk, lutp, skey, ka, bg, sg,
-                                               blo, bhi, bc, ix.keys[0].as<uint64_t>(), ix.vals[0].as<V>(), 0,
-                                               d_kmm);
+                                               blo, bhi, bc, ix.keys[0].as<uint64_t>(), ix.vals[0].as<V>(), 0, sbn,
+                                               d_kmm, h0);
       HK_HIP(hipGetLastError());
     }
     HK_HIP(hipMemcpyAsync(&got, bc + grid, 8, hipMemcpyDeviceToHost, s));
@@ -582,11 +639,12 @@ void shard_build_t(Index& ix, const uint64_t* ghist, const uint64_t* gbelow, int
   if (kmm[0] > kmm[1]) throw ApiError{-7, "shard selection produced no keys"};
   static const bool dbg = getenv("HKCSA_SHARD_DEBUG") != nullptr;   // diagnostic: slice geometry
   if (dbg)
-    fprintf(stderr, "[shard] rank %d/%d m=%llu q=%d sb=%d pb=%d hb=%d kmin=%llx kmax=%llx\n", rank, nranks,
-            (unsigned long long)m, kk.q, kk.sym_bits, kk.pb, hb, (unsigned long long)kmm[0],
-            (unsigned long long)kmm[1]);
-  // LDS bucket sorts over the slice's sym range, unless a bucket is too big for them
-  if (!whole && !(ix.flags & kFlagGlobalSort) && bucket_sort_slice<V>(ix, kk, m, hb, kmm[0], kmm[1])) {
+    fprintf(stderr, "[shard] rank %d/%d m=%llu q=%d sb=%d pb=%d hb=%d sym [%llx, %llx] bounds [%llx, %llx]\n", rank,
+            nranks, (unsigned long long)m, kk.q, kk.sym_bits, kk.pb, hb, (unsigned long long)kmm[0],
+            (unsigned long long)kmm[1], (unsigned long long)kb.first, (unsigned long long)kb.second);
+  if (kmm[0] < kb.first || kmm[1] > kb.second) throw ApiError{-7, "slice sym fields outside their bounds"};
+  // LDS bucket sorts over the slice's bins, unless a bucket is too big for them
+  if (!global && bucket_sort_slice<V>(ix, kk, m, hb, sbn, d_h0)) {
     HK_HIP(hipStreamSynchronize(s));
     ix.have_sa = ix.have_bwt = true;
     return;
