@@ -98,6 +98,7 @@ struct Index {
   DevBuf ties_k, ties_v, ties_n;   // unordered tie list of the bucket build (J<<1|head, P), count
   DevBuf big_k[2], big_v[2], big_j; // big buckets of the bucket build (sorted on the global path)
   DevBuf bk_items, bk_hist;       // bucket work items, bucket histogram
+  DevBuf sel;                     // sharded build: selection masks of the slice (u16 per 16 positions)
   DevBuf tile_a, tile_b, tile_c, tile_d;
   DevBuf small;                // scratch for totals etc.
   DevBuf seq[2];               // WT level code sequences

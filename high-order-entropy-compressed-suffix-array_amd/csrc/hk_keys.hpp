@@ -154,37 +154,65 @@ __device__ __forceinline__ uint64_t keyed_sym(const uint16_t* c, int off, uint64
 }
 
 
+// keyed sym of up to 28 symbols held in 8 little-endian words starting at byte `sh` of w[0]:
+// realigned with alignbyte, then a fully unrolled chunked Horner (uniform branches on q / ck)
+__device__ __forceinline__ uint64_t keyed_horner28(const uint32_t (&w)[8], uint32_t sh, const KeyedArgs& g,
+                                                   const uint16_t* LK) {
+  uint32_t r[7];
+#pragma unroll
+  for (int i = 0; i < 7; ++i) r[i] = __builtin_amdgcn_alignbyte(w[i + 1], w[i], sh);
+  uint64_t key = 0;
+  uint32_t cv = 0;
+  int in = 0;
+#pragma unroll
+  for (int j = 0; j < 28; ++j) {
+    if (j < g.q) {
+      cv = __umul24(cv, (uint32_t)g.Rk) + (LK[(r[j >> 2] >> (8 * (j & 3))) & 255u] & 255u);
+      if (++in == g.ck || j == g.q - 1) {
+        key = key * (in == g.ck ? g.Rck : g.Rlast) + cv;
+        cv = 0;
+        in = 0;
+      }
+    }
+  }
+  return key;
+}
+
+// keyed_sym of the suffix whose first byte is byte b of the LDS word array W (the text staged as
+// raw words); short suffixes are the caller's
+__device__ __forceinline__ uint64_t keyed_sym_words(const uint32_t* W, uint32_t b, const KeyedArgs& g,
+                                                    const uint16_t* LK) {
+  if (g.q <= 28) {
+    uint32_t w[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) w[i] = W[(b >> 2) + i];
+    return keyed_horner28(w, b & 3u, g, LK);
+  }
+  const uint8_t* B = reinterpret_cast<const uint8_t*>(W) + b;
+  uint64_t key = 0;
+  int j = 0;
+  while (j < g.q) {
+    const int len = g.q - j < g.ck ? g.q - j : g.ck;
+    uint32_t cv = 0;
+    for (int u = 0; u < len; ++u) cv = __umul24(cv, (uint32_t)g.Rk) + (LK[B[j + u]] & 255u);
+    key = key * (len == g.ck ? g.Rck : g.Rlast) + cv;
+    j += len;
+  }
+  return key;
+}
+
 // keyed_sym of suffix p read straight from the text (aligned word loads, bytes through the keyed
 // code table LK), for passes that build keys of scattered positions without staging their tile.
 __device__ __forceinline__ uint64_t keyed_sym_text(const uint8_t* __restrict__ t, uint64_t p, const KeyedArgs& g,
                                                    const uint16_t* LK, const uint64_t* SK) {
   if (p >= g.s_start) return SK[p - g.s_start];
   if (g.q <= 28) {
-    // up to 28 symbols: eight independent word loads (T' has 64 readable pad bytes), realigned to
-    // p with alignbyte, then a fully unrolled chunked Horner (uniform branches on q / ck)
+    // up to 28 symbols: eight independent word loads (T' has 64 readable pad bytes)
     const uint32_t* wp = reinterpret_cast<const uint32_t*>(t + (p & ~3ull));
     uint32_t w[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) w[i] = wp[i];
-    const uint32_t sh = (uint32_t)(p & 3u);
-    uint32_t r[7];
-#pragma unroll
-    for (int i = 0; i < 7; ++i) r[i] = __builtin_amdgcn_alignbyte(w[i + 1], w[i], sh);
-    uint64_t key = 0;
-    uint32_t cv = 0;
-    int in = 0;
-#pragma unroll
-    for (int j = 0; j < 28; ++j) {
-      if (j < g.q) {
-        cv = __umul24(cv, (uint32_t)g.Rk) + (LK[(r[j >> 2] >> (8 * (j & 3))) & 255u] & 255u);
-        if (++in == g.ck || j == g.q - 1) {
-          key = key * (in == g.ck ? g.Rck : g.Rlast) + cv;
-          cv = 0;
-          in = 0;
-        }
-      }
-    }
-    return key;
+    return keyed_horner28(w, (uint32_t)(p & 3u), g, LK);
   }
   const uint32_t* w = reinterpret_cast<const uint32_t*>(t + (p & ~3ull));
   uint32_t cur = w[0] >> (8u * (uint32_t)(p & 3u));

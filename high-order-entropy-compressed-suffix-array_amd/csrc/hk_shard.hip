@@ -22,6 +22,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <type_traits>
 
 #include "hk_index.hpp"
 #include "hk_keys.hpp"
@@ -219,7 +220,8 @@ __device__ __forceinline__ uint32_t select16(const uint8_t* __restrict__ t, uint
 
 __global__ __launch_bounds__(256) void k_select_count(const uint8_t* __restrict__ t, uint64_t n, uint64_t tpb,
                                                       const uint16_t* __restrict__ lut, BucketGeom g, SelGeom sg,
-                                                      uint32_t blo, uint32_t bhi, uint64_t* __restrict__ block_cnt) {
+                                                      uint32_t blo, uint32_t bhi, uint64_t* __restrict__ block_cnt,
+                                                      uint16_t* __restrict__ masks) {
   __shared__ uint16_t L[256];
   __shared__ uint64_t red[4];
   L[threadIdx.x] = lut[threadIdx.x];
@@ -228,8 +230,12 @@ __global__ __launch_bounds__(256) void k_select_count(const uint8_t* __restrict_
   const uint64_t t0 = (uint64_t)blockIdx.x * tpb;
   const uint64_t t1 = t0 + tpb < tiles ? t0 + tpb : tiles;
   uint64_t cnt = 0;
-  for (uint64_t ti = t0; ti < t1; ++ti)
-    cnt += __popc(select16(t, n, ti * PS_TILE + 16 * threadIdx.x, L, g, sg, blo, bhi));
+#pragma unroll 2
+  for (uint64_t ti = t0; ti < t1; ++ti) {
+    const uint32_t sel = select16(t, n, ti * PS_TILE + 16 * threadIdx.x, L, g, sg, blo, bhi);
+    masks[ti * 256 + threadIdx.x] = (uint16_t)sel;   // the write pass reads these instead of re-testing
+    cnt += __popc(sel);
+  }
   cnt = wave_sum(cnt);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = cnt;
   __syncthreads();
@@ -244,24 +250,26 @@ __global__ __launch_bounds__(256) void k_select_count(const uint8_t* __restrict_
 // building each selected key from global text words, even at 1/8 selection density).
 // kmm[0..1] collect the exact min / max sym (checked against the slice bounds), hist0 the
 // histogram of the bins' low byte (the first LSD pass).
-template <typename V>
+// RAW (sparse slices): the tile is staged as raw text words and only the selected suffixes' bytes
+// go through the code table; otherwise the whole tile is staged as keyed codes.
+template <typename V, bool RAW>
 __global__ __launch_bounds__(256) void k_select_write(const uint8_t* __restrict__ t, uint64_t n, uint64_t tpb,
-                                                      const uint16_t* __restrict__ lut,
+                                                      const uint16_t* __restrict__ masks,
                                                       const uint16_t* __restrict__ lutk,
                                                       const uint16_t* __restrict__ lutp,
                                                       const uint64_t* __restrict__ skey, KeyedArgs ka,
-                                                      BucketGeom g, SelGeom sg, uint32_t blo, uint32_t bhi,
                                                       const uint64_t* __restrict__ block_off,
                                                       uint64_t* __restrict__ keys, V* __restrict__ vals, int hb,
                                                       SliceBins sbn, unsigned long long* __restrict__ kmm,
                                                       unsigned long long* __restrict__ hist0) {
-  __shared__ uint16_t c[PS_TILE + kCodePad];
+  constexpr int NW = (PS_TILE + 72) / 4 + 2;   // raw words: bytes [base - 4, base + PS_TILE + 68 + 8)
+  __shared__ uint16_t c[RAW ? 1 : PS_TILE + kCodePad];
+  __shared__ uint32_t W[RAW ? NW : 1];
   __shared__ uint16_t list[PS_TILE];
-  __shared__ uint16_t L[256], LK[256], LP[256];
+  __shared__ uint16_t LK[256], LP[256];
   __shared__ uint64_t SK[64];
   __shared__ uint32_t red[4];
   __shared__ uint32_t H0[256];
-  L[threadIdx.x] = lut[threadIdx.x];
   LK[threadIdx.x] = lutk[threadIdx.x];
   LP[threadIdx.x] = lutp[threadIdx.x];
   H0[threadIdx.x] = 0;
@@ -274,9 +282,32 @@ __global__ __launch_bounds__(256) void k_select_write(const uint8_t* __restrict_
   const uint64_t t1 = t0 + tpb < tiles ? t0 + tpb : tiles;
   uint64_t run = block_off[blockIdx.x];
   uint64_t kmin = ~0ull, kmax = 0;
+  // software pipelining: the next tile's mask and text words are loaded while this tile is built
+  constexpr int RPER = (NW + 255) / 256;
+  uint32_t nsel = 0, pw[RPER];
+  TextWords<PS_TILE, 256> tw;
+  auto prefetch = [&](uint64_t ti) {
+    nsel = masks[ti * 256 + threadIdx.x];
+    if (RAW) {
+#pragma unroll
+      for (int k = 0; k < RPER; ++k) {
+        const int i = threadIdx.x + 256 * k;
+        const int64_t a = (int64_t)(ti * PS_TILE) - 4 + 4 * i;
+        pw[k] = (i < NW && a >= 0 && (uint64_t)a < n) ? *reinterpret_cast<const uint32_t*>(t + a) : 0u;
+      }
+    } else {
+      load_text_words<PS_TILE, 256>(tw, t, n, ti * PS_TILE);
+    }
+  };
+  if (t0 < t1) prefetch(t0);
   for (uint64_t ti = t0; ti < t1; ++ti) {
     const uint64_t base = ti * PS_TILE;
-    uint32_t sel = select16(t, n, base + 16 * threadIdx.x, L, g, sg, blo, bhi);
+    uint32_t sel = nsel;
+    uint32_t cw[RPER];
+#pragma unroll
+    for (int k = 0; k < RPER; ++k) cw[k] = pw[k];
+    const TextWords<PS_TILE, 256> ctw = tw;
+    if (ti + 1 < t1) prefetch(ti + 1);
     const uint32_t cnt = __popc(sel);
     const uint32_t inc = wave_incl_sum<uint32_t>(cnt);
     if (lane == 63) red[w] = inc;
@@ -294,15 +325,29 @@ __global__ __launch_bounds__(256) void k_select_write(const uint8_t* __restrict_
       sel &= sel - 1;
       list[o++] = (uint16_t)(16 * threadIdx.x + k);
     }
-    stage_text_codes<PS_TILE, 256>(c, LK, t, n, base);
+    if (RAW) {
+#pragma unroll
+      for (int k = 0; k < RPER; ++k)
+        if (threadIdx.x + 256 * k < (unsigned)NW) W[threadIdx.x + 256 * k] = cw[k];
+    } else {
+      store_text_codes<PS_TILE, 256>(c, LK, ctw, n, base);
+    }
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < tot; i += 256) {
       const int off = list[i];
       const uint64_t p = base + off;
-      const uint64_t sym = keyed_sym(c, off, p, ka, SK);
+      uint64_t sym;
+      uint32_t pbyte;
+      if (RAW) {
+        sym = p >= ka.s_start ? SK[p - ka.s_start] : keyed_sym_words(W, (uint32_t)off + 4, ka, LK);
+        pbyte = p == 0 ? t[n - 1] : (W[(off + 3) >> 2] >> (8 * ((off + 3) & 3))) & 255u;
+      } else {
+        sym = keyed_sym(c, off, p, ka, SK);
+        pbyte = c[off] >> 8;
+      }
       kmin = sym < kmin ? sym : kmin;
       kmax = sym > kmax ? sym : kmax;
-      uint64_t key = (sym << pbe) | ((uint64_t)LP[c[off] >> 8] << hb);
+      uint64_t key = (sym << pbe) | ((uint64_t)LP[pbyte] << hb);
       if (hb) key |= p >> 32;
       if (sbn.D > 0) {
         const uint64_t x = sym - sbn.kmin;
@@ -314,7 +359,7 @@ __global__ __launch_bounds__(256) void k_select_write(const uint8_t* __restrict_
       vals[run + i] = (V)p;
     }
     run += tot;
-    __syncthreads();   // list / c / red are rewritten by the next tile
+    __syncthreads();   // list / staging / red are rewritten by the next tile
   }
   for (int d = 32; d >= 1; d >>= 1) {
     const uint64_t a = __shfl_xor(kmin, d), b = __shfl_xor(kmax, d);
@@ -604,6 +649,7 @@ void shard_build_t(Index& ix, const uint64_t* ghist, const uint64_t* gbelow, int
     const uint64_t tpb = ceil_div(tiles, G);
     const unsigned grid = (unsigned)ceil_div(tiles, tpb);
     ix.tile_d.ensure((grid + 1) * 8 + 16);
+    ix.sel.ensure(tiles * 256 * 2 + 16);   // selection masks, one u16 per 16 positions
     uint64_t* bc = ix.tile_d.as<uint64_t>();
     unsigned long long* d_kmm = reinterpret_cast<unsigned long long*>(bc + grid + 1);
     HK_HIP(hipMemcpyAsync(d_kmm, kmm, 16, hipMemcpyHostToDevice, s));
@@ -614,21 +660,32 @@ void shard_build_t(Index& ix, const uint64_t* ghist, const uint64_t* gbelow, int
     const SelGeom sg = sel_geom(kg, bg, blo, bhi);
     {
       TimedLaunch t(ix.timer, "shard_select_count", (double)n);
-      k_select_count<<<grid, 256, 0, s>>>(ix.text.as<uint8_t>(), n, tpb, lut, bg, sg, blo, bhi, bc);
+      k_select_count<<<grid, 256, 0, s>>>(ix.text.as<uint8_t>(), n, tpb, lut, bg, sg, blo, bhi, bc,
+                                          ix.sel.as<uint16_t>());
       HK_HIP(hipGetLastError());
     }
     scan_exclusive_u64(ix.sw, bc, bc, grid, true, s);
     {
       TimedLaunch t(ix.timer, "shard_pack_select", (double)n + (double)m * (8 + sizeof(V)));
       unsigned long long* h0 = reinterpret_cast<unsigned long long*>(d_h0);
-      if (hb)
-        k_select_write<uint32_t><<<grid, 256, 0, s>>>(ix.text.as<uint8_t>(), n, tpb, lut, lutk, lutp, skey, ka, bg,
-                                                      sg, blo, bhi, bc, ix.keys[0].as<uint64_t>(),
-                                                      ix.vals[0].as<uint32_t>(), hb, sbn, d_kmm, h0);
-      else
-        k_select_write<V><<<grid, 256, 0, s>>>(ix.text.as<uint8_t>(), n, tpb, lut, lutk, lutp, skey, ka, bg, sg,
-                                               blo, bhi, bc, ix.keys[0].as<uint64_t>(), ix.vals[0].as<V>(), 0, sbn,
-                                               d_kmm, h0);
+      // sparse slices stage raw words (only the selected suffixes' bytes are converted)
+      const bool raw = m * 3 < n;
+      const uint16_t* mk = ix.sel.as<uint16_t>();
+      uint64_t* k0 = ix.keys[0].as<uint64_t>();
+      auto launch = [&](auto vtag, auto rawtag, void* v) {
+        using VT = decltype(vtag);
+        k_select_write<VT, decltype(rawtag)::value><<<grid, 256, 0, s>>>(
+            ix.text.as<uint8_t>(), n, tpb, mk, lutk, lutp, skey, ka, bc, k0, reinterpret_cast<VT*>(v), hb, sbn,
+            d_kmm, h0);
+      };
+      void* v0 = ix.vals[0].p;
+      if (hb) {
+        if (raw) launch(uint32_t{}, std::true_type{}, v0);
+        else launch(uint32_t{}, std::false_type{}, v0);
+      } else {
+        if (raw) launch(V{}, std::true_type{}, v0);
+        else launch(V{}, std::false_type{}, v0);
+      }
       HK_HIP(hipGetLastError());
     }
     HK_HIP(hipMemcpyAsync(&got, bc + grid, 8, hipMemcpyDeviceToHost, s));
