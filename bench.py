@@ -1,21 +1,23 @@
 #!/usr/bin/env python3
 """Headline benchmark: SA build MB/s + batched locate() patterns/s (BASELINE.json).
 
-N = 1 (default): configs[1]'s pipeline on the metric's 1 GiB sigma=4 text — one "step"
-  is HIP prefix-doubling SA + BWT gather of T' = 2^30 iid ACGT symbols + '$', text
-  resident in HBM before timing.  After the timed steps the wavelet tree is built and
-  1M random 16-symbol substrings are located in batches (count + SA gather), reported as
-  locate_patterns_per_s.
-N > 1 (torchrun, one process per GPU): the sharded construction (hkcsa_build_sa_sharded:
-  RCCL all-reduce of the key histogram, independent slice sorts, RCCL all-gather of the
-  slice bounds) of an N GiB text, i.e. weak scaling at 1 GiB of suffixes per GPU; value =
-  all ranks' text MB / max-over-ranks time.
+N = 1 (default): configs[1]'s pipeline on the metric's 1 GiB sigma=4 text — one "step" is the
+  SA + BWT build of T' = 2^30 iid ACGT symbols + '$' (text resident in HBM before timing): keyed
+  suffix keys, bucket histogram, two LSD radix passes over the bucket bits (the first builds the
+  keys from the text), LDS bucket sorts that write SA and BWT, refinement of the tied suffixes.
+  After the timed steps the wavelet tree is built and 1M random 16-symbol substrings are located in
+  batches (count + SA gather), reported as locate_patterns_per_s.
+N > 1 (torchrun, one process per GPU): the sharded construction (hkcsa_build_sa_sharded: RCCL
+  all-reduce of the partition histogram and of the slice counts, independent slice sorts, RCCL
+  all-gather of the slice bounds) of an N GiB text, i.e. weak scaling at 1 GiB of suffixes per GPU;
+  value = all ranks' text MB / max-over-ranks time.
 
 The JSON line also carries:
-  roofline      — the radix scatter pass (radix_onesweep) timed with HIP events on the
-                  library's stream; achieved = 2*N*(8+4) algorithmic bytes per launch /
-                  mean launch time; peak = 8000 GB/s (MI355X HBM3E); traffic from PMC
-                  counters (profiles/) when given via --traffic-gb.
+  roofline      — the dominant kernel of the timed steps (largest summed time among the bucket
+                  sort and the two radix passes) timed with HIP events on the library's stream:
+                  achieved = its algorithmic bytes per launch / mean launch time, peak = 8000 GB/s
+                  (MI355X HBM3E), traffic = PMC-measured HBM bytes per launch (profiles/
+                  pmc_kernels.json); the other two kernels under roofline["others"].
   cpu_baseline  — the pure-Python restatement of the reference (oracle/ref_port.py:
                   naive suffix sort, dense occ, dict backward search), one core, on a
                   bounded sample (rank 0, N = 1 only).
@@ -80,39 +82,46 @@ def cpu_baseline(sample_n: int, npat: int, seed: int = 3) -> dict:
     }
 
 
-def pmc_traffic_gb() -> float | None:
-    """HBM GB per radix_onesweep launch measured with rocprofv3 PMC counters on this config
-    (tools_pmc_summary.py -> profiles/pmc_radix_onesweep.json; FETCH_SIZE x2 gfx950 correction)."""
-    p = os.path.join(ROOT, "profiles", "pmc_radix_onesweep.json")
+# kernels whose roofline bench.py reports: the dominant one (largest summed time) as `roofline`,
+# the others under roofline["others"]
+ROOF_KERNELS = ("sa_bucket_sort", "radix_onesweep_text", "radix_onesweep")
+
+
+def pmc_traffic_gb(name: str) -> float | None:
+    """HBM GB per launch of timer `name`'s kernel, measured with rocprofv3 PMC counters on this config
+    (tools_gpu_pmc.sh + tools_pmc_summary.py -> profiles/pmc_kernels.json; FETCH_SIZE x2 gfx950 correction)."""
+    p = os.path.join(ROOT, "profiles", "pmc_kernels.json")
     try:
         with open(p) as f:
-            return float(json.load(f)["traffic_gb_per_launch"])
+            return float(json.load(f)[name]["traffic_gb_per_launch"])
     except Exception:
         return None
 
 
-def roofline(dev: DeviceIndex, traffic_gb: float | None) -> dict:
-    if traffic_gb is None:
-        traffic_gb = pmc_traffic_gb()
-    launches, ms, alg_bytes = dev.kernel_stats("radix_onesweep")
+def kernel_roofline(dev: DeviceIndex, name: str) -> dict | None:
+    launches, ms, alg_bytes = dev.kernel_stats(name)
     if not launches:
-        return {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None,
-                "traffic": None}
+        return None
     per_launch_bytes = alg_bytes / launches
     avg_s = ms / launches / 1e3
     achieved = per_launch_bytes / avg_s / 1e9
-    return {
-        "bound": "hbm",
-        "achieved": round(achieved, 1),
-        "peak": HBM_PEAK_GBS,
-        "unit": "GB/s",
-        "frac": round(achieved / HBM_PEAK_GBS, 4),
-        "traffic": traffic_gb,
-        "kernel": "radix_onesweep",
-        "launches": launches,
-        "avg_launch_ms": round(ms / launches, 4),
-        "alg_bytes_per_launch": per_launch_bytes,
-    }
+    return {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": pmc_traffic_gb(name), "kernel": name,
+            "launches": launches, "avg_launch_ms": round(ms / launches, 4), "total_ms": round(ms, 3),
+            "alg_bytes_per_launch": per_launch_bytes}
+
+
+def roofline(dev: DeviceIndex, traffic_gb: float | None) -> dict:
+    rows = [r for r in (kernel_roofline(dev, k) for k in ROOF_KERNELS) if r]
+    if not rows:
+        return {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None,
+                "traffic": None}
+    dom = max(rows, key=lambda r: r["total_ms"])
+    if traffic_gb is not None:
+        dom["traffic"] = traffic_gb
+    dom["others"] = [{k: r[k] for k in ("kernel", "achieved", "frac", "traffic", "avg_launch_ms")}
+                     for r in rows if r is not dom]
+    return dom
 
 
 def stage_breakdown(dev: DeviceIndex, names) -> dict:
@@ -204,10 +213,10 @@ def run_single(args) -> dict:
         "vs_baseline": None,
         "dtype": "u8",
         "data": "synthetic",
-        "config": {"workload": "1 GiB synthetic sigma=4 text: SA by HIP LSD radix sort of mixed-radix "
-                               "suffix keys + tie refinement, BWT from the sorted keys (configs[1] "
-                               "pipeline at the metric's 1 GiB), then WT + 1M batched "
-                               f"{args.plen}-symbol locate()",
+        "config": {"workload": "1 GiB synthetic sigma=4 text: SA + BWT by the HIP bucket build (LSD "
+                               "radix passes over the bucket bits, LDS bucket sorts writing SA and BWT, "
+                               "tie refinement; configs[1] pipeline at the metric's 1 GiB), then WT + "
+                               f"1M batched {args.plen}-symbol locate()",
                    "text_symbols": n, "sigma": 4, "positions": "u32"},
         "roofline": roof,
         "locate_patterns_per_s": loc["locate_patterns_per_s"] if loc else None,
@@ -249,6 +258,11 @@ def run_sharded(args, rank: int, world: int, local_rank: int) -> dict | None:
     wall = float(el.item())
     lo, hi = dev.shard_range()
     roof = roofline(dev, args.traffic_gb)
+    # the PMC summaries in profiles/ are of the single-GPU launches: not this slice's kernels
+    if args.traffic_gb is None:
+        roof["traffic"] = None
+        for o in roof.get("others", []):
+            o["traffic"] = None
     stages = stage_breakdown(dev, ["shard_hist", "shard_below", "shard_select_count", "shard_pack_select",
                                    "rccl_allreduce_hist", "rccl_allreduce_counts", "rccl_allgather_bounds",
                                    "sa_bin_starts", "sa_bucket_sort", "radix_hist", "radix_onesweep",
@@ -270,9 +284,10 @@ def run_sharded(args, rank: int, world: int, local_rank: int) -> dict | None:
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic",
-            "config": {"workload": f"{world} GiB synthetic sigma=4 text sharded over {world} GPUs: key-histogram "
-                                   "RCCL all-reduce, per-rank slice sort + refinement, RCCL all-gather of slice "
-                                   "bounds", "text_symbols": n, "sigma": 4,
+            "config": {"workload": f"{world} GiB synthetic sigma=4 text sharded over {world} GPUs: partition "
+                                   "histogram + slice counts by RCCL all-reduce, per-rank slice selection, LSD "
+                                   "passes over the slice's bucket bits, LDS bucket sorts, tie refinement, RCCL "
+                                   "all-gather of the slice bounds", "text_symbols": n, "sigma": 4,
                        "parallelism": f"sa-slices x{world}",
                        "positions": "u64" if (n >= 2**32 - 1 or args.pos64) else "u32"},
             "roofline": roof,
@@ -303,7 +318,7 @@ def main():
     ap.add_argument("--patterns", type=int, default=1_000_000)
     ap.add_argument("--plen", type=int, default=16)
     ap.add_argument("--query-reps", type=int, default=5)
-    ap.add_argument("--cpu-sample", type=int, default=1 << 16)
+    ap.add_argument("--cpu-sample", type=int, default=1 << 17)
     ap.add_argument("--cpu-patterns", type=int, default=1000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--sharded", action="store_true", help="use the sharded (multi-GPU) build even at N=1")
@@ -311,7 +326,7 @@ def main():
     ap.add_argument("--global-sort", action="store_true",
                     help="single-GPU build by full-width LSD sort of the keys (no LDS bucket sorts)")
     ap.add_argument("--traffic-gb", type=float, default=None,
-                    help="PMC-measured HBM GB per radix pass; default: profiles/pmc_radix_onesweep.json")
+                    help="PMC-measured HBM GB per launch of the dominant kernel; default: profiles/pmc_kernels.json")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))

@@ -202,11 +202,9 @@ __device__ __forceinline__ void bs_load_keys(const uint64_t* __restrict__ keys, 
   for (int k = 0; k < BS_I; ++k) key[k] = sl + 64u * k < it.y ? kb[sl + 64u * k] : 0;
 }
 
-// One work item of the LDS bucket sort, its keys in `key` (slot order).  While it finishes, the
-// cache lines of work item `pf` — the one that should start on this CU next — are touched so that
-// its key and position loads hit L2 / the Infinity Cache instead of HBM.
+// One work item of the LDS bucket sort, its keys in `key` (slot order).
 template <bool WIDE, bool TRACE, typename V>
-__device__ __forceinline__ void bucket_sort_item(BsShared& sh, uint2 it, uint2 pf, const uint64_t (&key)[BS_I],
+__device__ __forceinline__ void bucket_sort_item(BsShared& sh, uint2 it, const uint64_t (&key)[BS_I],
                                                  uint32_t item, const uint64_t* __restrict__ keys,
                                                  const uint32_t* __restrict__ vals, int pb, int sb, int hb,
                                                  uint64_t symbias, V* __restrict__ sa, uint8_t* __restrict__ bwt,
@@ -437,20 +435,13 @@ __device__ __forceinline__ void bucket_sort_item(BsShared& sh, uint2 it, uint2 p
     }
   }
 
-  // ---- this item's positions (in flight across the tie phase), then one dword of every 128-B line
-  // of item pf's keys and positions (the memory clobber keeps the compiler from hoisting the loads
-  // into the passes, where registers are full)
+  // ---- this item's positions, in flight across the tie phase (measured faster than loading them
+  // after it; touching the next item's lines ahead of time was slower).  The memory clobber keeps
+  // the compiler from hoisting the loads into the passes, where registers are full.
   asm volatile("" ::: "memory");
   uint32_t vv[BS_I];
 #pragma unroll
   for (int k = 0; k < BS_I; ++k) vv[k] = ((vmask >> k) & 1u) ? vb[s0 + 64u * k] : 0u;
-  uint32_t touch = 0;
-  {
-    const uint32_t* __restrict__ pk = reinterpret_cast<const uint32_t*>(keys + pf.x);
-    const uint32_t* __restrict__ pv = vals + pf.x;
-    for (uint32_t d = tid * 32; d < 2 * pf.y; d += BS_T * 32) touch |= pk[d];
-    for (uint32_t d = tid * 32; d < pf.y; d += BS_T * 32) touch |= pv[d];
-  }
 
   // ---- ties: equal local keys next to each other in sorted order
   if (TRACE) ts[2] = stamp();
@@ -529,7 +520,6 @@ __device__ __forceinline__ void bucket_sort_item(BsShared& sh, uint2 it, uint2 p
       ++tpos;
     }
   }
-  asm volatile("" ::"v"(touch));   // keeps the touch loads (their data is not needed)
   if (TRACE) {
     ts[5] = stamp();
     if (tid == 0)
@@ -537,14 +527,12 @@ __device__ __forceinline__ void bucket_sort_item(BsShared& sh, uint2 it, uint2 p
   }
 }
 
-// One workgroup per work item (one per CU at a time: the sort takes 158 KiB of LDS); workgroup b
-// touches item b + ncu, which the dispatcher should start on a CU of the same XCD once the first
-// ncu items are done.
+// One workgroup per work item (one per CU at a time: the sort takes 158 KiB of LDS).
 template <bool WIDE, bool TRACE = false, typename V = uint32_t>
 __global__ __launch_bounds__(BS_T, 1) void k_bucket_sort(const uint64_t* __restrict__ keys,
                                                          const uint32_t* __restrict__ vals,
-                                                         const uint2* __restrict__ items, uint32_t nitems,
-                                                         uint32_t ncu, int pb, int sb, int hb, uint64_t symbias,
+                                                         const uint2* __restrict__ items, int pb, int sb, int hb,
+                                                         uint64_t symbias,
                                                          const uint8_t* __restrict__ inv, V* __restrict__ sa,
                                                          uint8_t* __restrict__ bwt, uint64_t* __restrict__ tie_k,
                                                          V* __restrict__ tie_v,
@@ -553,10 +541,9 @@ __global__ __launch_bounds__(BS_T, 1) void k_bucket_sort(const uint64_t* __restr
   __shared__ BsShared sh;
   if (threadIdx.x < 256) sh.inv[threadIdx.x] = inv[threadIdx.x];
   const uint2 it = items[blockIdx.x];
-  const uint2 pf = blockIdx.x + ncu < nitems ? items[blockIdx.x + ncu] : make_uint2(0, 0);
   uint64_t key[BS_I];
   bs_load_keys(keys, it, key);
-  bucket_sort_item<WIDE, TRACE, V>(sh, it, pf, key, blockIdx.x, keys, vals, pb, sb, hb, symbias, sa, bwt, tie_k,
+  bucket_sort_item<WIDE, TRACE, V>(sh, it, key, blockIdx.x, keys, vals, pb, sb, hb, symbias, sa, bwt, tie_k,
                                    tie_v, tie_n, trace);
 }
 
@@ -710,24 +697,22 @@ uint64_t sort_bucket_items(Index& ix, const BucketPlan& plan, const uint64_t* ke
   {
     TimedLaunch t(ix.timer, "sa_bucket_sort", (double)(m - plan.big_total) * (8 + 4 + 4 + 1));
     static const bool trace = getenv("HKCSA_BS_TRACE") != nullptr;   // diagnostic phase stamps
-    int ncu = 0;   // workgroup b touches item b + ncu (k_bucket_sort)
-    HK_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, ix.device));
     const unsigned grid_n = (unsigned)nn, grid_w = (unsigned)nw;
     DevBuf tbuf;
     if (trace && nn) tbuf.ensure(nn * 64 + 64);
     if (nn) {
       if (trace && sizeof(V) == 4)
         k_bucket_sort<false, true, V><<<grid_n, BS_T, 0, s>>>(
-            keys, vals, ix.bk_items.as<uint2>(), (uint32_t)nn, (uint32_t)ncu, pb, sb, hb, symbias, d_inv, sa, bwt, ix.ties_k.as<uint64_t>(),
+            keys, vals, ix.bk_items.as<uint2>(), pb, sb, hb, symbias, d_inv, sa, bwt, ix.ties_k.as<uint64_t>(),
             ix.ties_v.as<V>(), ix.ties_n.as<unsigned long long>(), tbuf.as<uint64_t>());
       else
         k_bucket_sort<false, false, V><<<grid_n, BS_T, 0, s>>>(
-            keys, vals, ix.bk_items.as<uint2>(), (uint32_t)nn, (uint32_t)ncu, pb, sb, hb, symbias, d_inv, sa, bwt, ix.ties_k.as<uint64_t>(),
+            keys, vals, ix.bk_items.as<uint2>(), pb, sb, hb, symbias, d_inv, sa, bwt, ix.ties_k.as<uint64_t>(),
             ix.ties_v.as<V>(), ix.ties_n.as<unsigned long long>(), nullptr);
     }
     if (nw)
       k_bucket_sort<true, false, V><<<grid_w, BS_T, 0, s>>>(
-          keys, vals, ix.bk_items.as<uint2>() + nn, (uint32_t)nw, (uint32_t)ncu, pb, sb, hb, symbias, d_inv, sa, bwt, ix.ties_k.as<uint64_t>(),
+          keys, vals, ix.bk_items.as<uint2>() + nn, pb, sb, hb, symbias, d_inv, sa, bwt, ix.ties_k.as<uint64_t>(),
           ix.ties_v.as<V>(), ix.ties_n.as<unsigned long long>(), nullptr);
     HK_HIP(hipGetLastError());
     if (trace && nn && sizeof(V) == 4) {
