@@ -140,3 +140,21 @@ def test_unicode_text_remap():
     assert idx.count == port.count
     for p in ["αβ", "β€", "€α", "z", "ααα"]:
         assert idx.find(p) == port.find(p)
+
+
+def test_run_full_benchmark_harness(capsys):
+    """tests/benchmark.py:54-106 over the GPU CSA: the reference's fields, one locate per length and
+    iteration, occurrence counts equal to the restatement's find()."""
+    from utils.benchmark import print_benchmark_summary, run_full_benchmark
+    text = "mississippi$" * 1000
+    res = run_full_benchmark(text, pattern_lengths=[5, 10, 50, 100, 500, 1000], iterations=2, seed=11)
+    assert res.construction_time > 0 and res.total_time >= res.construction_time
+    assert sorted(res.pattern_times) == [5, 10, 50, 100, 500, 1000]
+    assert res.peak_memory >= res.construction_memory and res.device_bytes > 0
+    from utils.patterns import generate_random_patterns
+    port = ref_port.FMIndexPort(text)
+    for p in generate_random_patterns(text, [5, 10, 50, 100, 500, 1000], seed=11):
+        assert res.occurrences[len(p)] == len(port.find(p))
+    print_benchmark_summary(res)
+    out = capsys.readouterr().out
+    assert "=== Benchmark Summary ===" in out and "Peak Memory" in out

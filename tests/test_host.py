@@ -94,3 +94,28 @@ def test_csa_sample_rate():
     assert sample_rate(2**20 + 1, 1.0) == 21
     assert sample_rate(1000, 0) == 1
     assert sample_rate(1, 0.5) == 1
+
+
+def test_generate_random_patterns_reference_semantics():
+    """tests/test_patterns.py:3-9: one substring per length, clipped to the text, at a random
+    offset — here seedable; the seeded draw equals the reference's draw from random.Random(seed)."""
+    import random
+    from utils.patterns import generate_random_patterns, sample_substrings
+    text = "mississippi$" * 7
+    lens = [1, 5, 10, 50, 100, 1000]
+    pats = generate_random_patterns(text, lens, seed=7)
+    assert [len(p) for p in pats] == [min(n, len(text)) for n in lens]
+    assert all(p in text for p in pats)
+    rng = random.Random(7)
+    want = []
+    for n in lens:
+        a = min(n, len(text))
+        s = rng.randint(0, len(text) - a)
+        want.append(text[s:s + a])
+    assert pats == want
+    assert generate_random_patterns("", [3]) == [""]
+    data, offs = sample_substrings(text.encode(), 50, 4, seed=3)
+    assert len(offs) == 51 and int(offs[-1]) == len(data) == 200
+    blob = text.encode()
+    for i in range(50):
+        assert data[offs[i]:offs[i + 1]].tobytes() in blob
