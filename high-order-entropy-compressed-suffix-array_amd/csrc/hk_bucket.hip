@@ -798,6 +798,9 @@ KeyGeom key_geometry_keyed(Index& ix, int reserve) {
       g.kflag[b] = k ? 1 : 0;
       below += k ? 1 : 0;
     }
+    memset(g.k2d, 0, sizeof(g.k2d));
+    for (int b = 0; b < 256; ++b)
+      if (g.kflag[b]) g.k2d[codek[b]] = g.lutp[b];
   }
   double p2 = 0;
   for (int b = 0; b < 256; ++b)
@@ -1030,7 +1033,8 @@ void build_sa_bucketed(Index& ix) {
     // first hq symbols are exactly the top D bits when Rk = 2^k, k | D and no short key exceeds Rk^q - 1
     const int lb = (kg.Rk & (kg.Rk - 1)) == 0 ? __builtin_ctzll(kg.Rk) : 0;
     if (lb && D > 0 && D % lb == 0 && sb == lb * kg.q) ka.hq = D / lb;
-    if (lb && sb == lb * kg.q) ka.lb = lb;
+    // packed bit windows need whole codes per 32-bit word: lb in {1, 2, 4, 8}
+    if (lb && 32 % lb == 0 && sb == lb * kg.q) ka.lb = lb;
   }
 
   // ---- 1. bucket histogram

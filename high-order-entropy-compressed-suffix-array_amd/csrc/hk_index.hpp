@@ -46,6 +46,7 @@ struct KeyGeom {
   int bucket_bits = 0;       // D: top bits of the sym field sorted by the LSD passes
   uint16_t kdig[256];        // byte -> number of keyed bytes below it (its keyed code when keyed)
   uint8_t kflag[256];        // byte -> 1 when keyed
+  uint16_t k2d[256];         // keyed code -> dense code (the prev field of a keyed byte)
 };
 int mixed_radix_bits(uint64_t R, int q);   // bits of R^q - 1 (65 when it does not fit 64 bits)
 

@@ -633,6 +633,8 @@ void upload_geometry(Index& ix, const KeyGeom& kg) {
                           ix.stream));
     HK_HIP(hipMemcpyAsync(ix.small.as<uint8_t>() + 7168, kg.srank, sizeof(kg.srank), hipMemcpyHostToDevice,
                           ix.stream));
+    HK_HIP(hipMemcpyAsync(ix.small.as<uint8_t>() + 7456, kg.k2d, sizeof(kg.k2d), hipMemcpyHostToDevice,
+                          ix.stream));   // +7456 = k2d (u16[256])
   }
   HK_HIP(hipStreamSynchronize(ix.stream));   // kg may be a host temporary
 }

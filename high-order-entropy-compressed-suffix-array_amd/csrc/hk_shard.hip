@@ -194,6 +194,13 @@ __device__ __forceinline__ uint32_t select16(const uint8_t* __restrict__ t, uint
   const uint4 a = *reinterpret_cast<const uint4*>(t + p0);        // T' has 64 readable pad bytes
   const uint4 b = *reinterpret_cast<const uint4*>(t + p0 + 16);
   const uint32_t w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+  // Branch-free per position (short-circuit && / || on per-lane values compiled to exec-mask
+  // juggling that made this loop scalar-ALU bound): in range <=> be - TL <= TH - TL (unsigned);
+  // an absent TA / TB is replaced by one that is present or by ~0, which at worst sends an
+  // all-0xFF window down the exact path.
+  const uint64_t span = sg.TH - sg.TL;
+  const uint64_t TB = (sg.flags & SEL_HAS_B) ? sg.TB : ~0ull;
+  const uint64_t TA = (sg.flags & SEL_HAS_A) ? sg.TA : TB;
   uint32_t acc = 0, amb = 0;
 #pragma unroll
   for (int k = 0; k < 16; ++k) {
@@ -201,10 +208,14 @@ __device__ __forceinline__ uint32_t select16(const uint8_t* __restrict__ t, uint
     const uint32_t d0 = __builtin_amdgcn_alignbyte(w[j + 1], w[j], sh);
     const uint32_t d1 = __builtin_amdgcn_alignbyte(w[j + 2], w[j + 1], sh);
     const uint64_t be = (((uint64_t)__builtin_bswap32(d0) << 32) | __builtin_bswap32(d1)) & sg.topmask;
-    const bool in = !(sg.flags & SEL_EMPTY) && be >= sg.TL && be <= sg.TH;
-    const bool eq = ((sg.flags & SEL_HAS_A) && be == sg.TA) || ((sg.flags & SEL_HAS_B) && be == sg.TB);
-    if (in) acc |= 1u << k;
-    if (eq || p0 + k + sg.h > n || (sg.flags & SEL_NOPRE)) amb |= 1u << k;
+    acc |= (be - sg.TL <= span) ? (1u << k) : 0u;
+    amb |= ((be == TA) | (be == TB)) ? (1u << k) : 0u;
+  }
+  if (sg.flags & SEL_EMPTY) acc = 0;
+  if (sg.flags & SEL_NOPRE) amb = 0xFFFFu;
+  if (p0 + 16 + sg.h > n) {   // windows running past T': the exact path
+#pragma unroll
+    for (int k = 0; k < 16; ++k) amb |= (p0 + k + sg.h > n) ? (1u << k) : 0u;
   }
   amb &= (p0 + 16 <= n) ? 0xFFFFu : ((1u << (n - p0)) - 1u);
   acc &= ~amb;
@@ -250,21 +261,30 @@ __global__ __launch_bounds__(256) void k_select_count(const uint8_t* __restrict_
 // building each selected key from global text words, even at 1/8 selection density).
 // kmm[0..1] collect the exact min / max sym (checked against the slice bounds), hist0 the
 // histogram of the bins' low byte (the first LSD pass).
-// RAW (sparse slices): the tile is staged as raw text words and only the selected suffixes' bytes
-// go through the code table; otherwise the whole tile is staged as keyed codes.
-template <typename V, bool RAW>
+// MODE 0 (dense slices): the tile is staged as keyed codes.  MODE 1 (sparse slices): staged as raw
+// text words, only the selected suffixes' bytes go through the code table.  MODE 2 (sparse, keyed
+// radix 2^lb with lb | 32): raw words, then one pass packs the tile's codes MSB-first into lb-bit
+// fields and every key is a q*lb-bit window of that stream (three LDS words, no per-symbol loop).
+template <typename V, int MODE>
 __global__ __launch_bounds__(256) void k_select_write(const uint8_t* __restrict__ t, uint64_t n, uint64_t tpb,
                                                       const uint16_t* __restrict__ masks,
                                                       const uint16_t* __restrict__ lutk,
                                                       const uint16_t* __restrict__ lutp,
+                                                      const uint16_t* __restrict__ k2d,
                                                       const uint64_t* __restrict__ skey, KeyedArgs ka,
                                                       const uint64_t* __restrict__ block_off,
                                                       uint64_t* __restrict__ keys, V* __restrict__ vals, int hb,
                                                       SliceBins sbn, unsigned long long* __restrict__ kmm,
                                                       unsigned long long* __restrict__ hist0) {
-  constexpr int NW = (PS_TILE + 72) / 4 + 2;   // raw words: bytes [base - 4, base + PS_TILE + 68 + 8)
+  constexpr bool RAW = MODE >= 1;
+  // raw words: bytes [base - 4, base + PS_TILE + 108), enough for the last packed word at lb = 1
+  constexpr int NW = (PS_TILE + 112) / 4;
+  constexpr int NSYM = PS_TILE + 68;           // packed symbols: positions base - 1 .. base + PS_TILE + 66
+  constexpr int NPK = NSYM / 4 + 4;            // packed words for lb <= 8
   __shared__ uint16_t c[RAW ? 1 : PS_TILE + kCodePad];
   __shared__ uint32_t W[RAW ? NW : 1];
+  __shared__ uint32_t PK[MODE == 2 ? NPK : 1];
+  __shared__ uint16_t K2D[MODE == 2 ? 256 : 1];
   __shared__ uint16_t list[PS_TILE];
   __shared__ uint16_t LK[256], LP[256];
   __shared__ uint64_t SK[64];
@@ -273,10 +293,12 @@ __global__ __launch_bounds__(256) void k_select_write(const uint8_t* __restrict_
   LK[threadIdx.x] = lutk[threadIdx.x];
   LP[threadIdx.x] = lutp[threadIdx.x];
   H0[threadIdx.x] = 0;
+  if (MODE == 2) K2D[threadIdx.x] = k2d[threadIdx.x];
   if (threadIdx.x < 64 && ka.s_start + threadIdx.x < n) SK[threadIdx.x] = skey[threadIdx.x];
   __syncthreads();
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int pbe = ka.pb + hb;
+  const int lb = ka.lb, per = MODE == 2 ? 32 / ka.lb : 1, kbits = ka.q * ka.lb;
   const uint64_t tiles = (n + PS_TILE - 1) / PS_TILE;
   const uint64_t t0 = (uint64_t)blockIdx.x * tpb;
   const uint64_t t1 = t0 + tpb < tiles ? t0 + tpb : tiles;
@@ -333,21 +355,44 @@ __global__ __launch_bounds__(256) void k_select_write(const uint8_t* __restrict_
       store_text_codes<PS_TILE, 256>(c, LK, ctw, n, base);
     }
     __syncthreads();
+    if (MODE == 2) {
+      // symbol s (position base - 1 + s) is byte s + 3 of W; word wd packs symbols [wd*per, +per)
+      const uint8_t* WB = reinterpret_cast<const uint8_t*>(W);
+      for (int wd = threadIdx.x; wd * per < NSYM; wd += 256) {
+        uint32_t word = 0;
+        for (int u = 0; u < per; ++u) word = (word << lb) | (LK[WB[wd * per + u + 3]] & 255u);
+        PK[wd] = word;
+      }
+      __syncthreads();
+    }
     for (uint32_t i = threadIdx.x; i < tot; i += 256) {
       const int off = list[i];
       const uint64_t p = base + off;
       uint64_t sym;
-      uint32_t pbyte;
-      if (RAW) {
+      uint32_t pcode;   // dense code of T'[p-1]
+      if (MODE == 2) {
+        if (p >= ka.s_start) {
+          sym = SK[p - ka.s_start];
+        } else {
+          const uint32_t bit = (uint32_t)(off + 1) * lb, w0 = bit >> 5, o = bit & 31u;
+          const uint64_t hi = ((uint64_t)PK[w0] << 32) | PK[w0 + 1];
+          const uint64_t win = o ? (hi << o) | (PK[w0 + 2] >> (32 - o)) : hi;
+          sym = kbits >= 64 ? win : win >> (64 - kbits);
+        }
+        // T'[p-1] is a keyed byte except for p = 0 (the terminal before it)
+        const uint32_t pbit = (uint32_t)off * lb;
+        const uint32_t kc = (PK[pbit >> 5] >> (32 - lb - (pbit & 31u))) & ((1u << lb) - 1u);
+        pcode = p == 0 ? LP[t[n - 1]] : K2D[kc];
+      } else if (RAW) {
         sym = p >= ka.s_start ? SK[p - ka.s_start] : keyed_sym_words(W, (uint32_t)off + 4, ka, LK);
-        pbyte = p == 0 ? t[n - 1] : (W[(off + 3) >> 2] >> (8 * ((off + 3) & 3))) & 255u;
+        pcode = LP[p == 0 ? t[n - 1] : (W[(off + 3) >> 2] >> (8 * ((off + 3) & 3))) & 255u];
       } else {
         sym = keyed_sym(c, off, p, ka, SK);
-        pbyte = c[off] >> 8;
+        pcode = LP[c[off] >> 8];
       }
       kmin = sym < kmin ? sym : kmin;
       kmax = sym > kmax ? sym : kmax;
-      uint64_t key = (sym << pbe) | ((uint64_t)LP[pbyte] << hb);
+      uint64_t key = (sym << pbe) | ((uint64_t)pcode << hb);
       if (hb) key |= p >> 32;
       if (sbn.D > 0) {
         const uint64_t x = sym - sbn.kmin;
@@ -629,7 +674,13 @@ void shard_build_t(Index& ix, const uint64_t* ghist, const uint64_t* gbelow, int
   upload_geometry(ix, kk);
   const uint8_t* small = ix.small.as<uint8_t>();
   const KeyChunks kch = key_chunks(kk.Rk, kk.q);
-  const KeyedArgs ka{kk.Rk, kch.Rck, kch.Rlast, kk.s_start, kk.q, kch.ck, kk.pb, 0};
+  KeyedArgs ka{kk.Rk, kch.Rck, kch.Rlast, kk.s_start, kk.q, kch.ck, kk.pb, 0};
+  {
+    // keyed radix 2^lb with whole codes per 32-bit word and the sym field exactly q*lb bits:
+    // keys are bit windows of a packed code stream (k_select_write MODE 2)
+    const int lb = (kk.Rk & (kk.Rk - 1)) == 0 ? __builtin_ctzll(kk.Rk) : 0;
+    if (lb && 32 % lb == 0 && kk.sym_bits == lb * kk.q) ka.lb = lb;
+  }
   const BucketGeom bg = bucket_geom(kg);
   // bucket bins of the slice from its sym bounds (known before any key is built)
   const auto kb = slice_sym_bounds(kg, bg.bsh, blo, bhi, kk);
@@ -668,23 +719,31 @@ void shard_build_t(Index& ix, const uint64_t* ghist, const uint64_t* gbelow, int
     {
       TimedLaunch t(ix.timer, "shard_pack_select", (double)n + (double)m * (8 + sizeof(V)));
       unsigned long long* h0 = reinterpret_cast<unsigned long long*>(d_h0);
-      // sparse slices stage raw words (only the selected suffixes' bytes are converted)
-      const bool raw = m * 3 < n;
+      // sparse slices stage raw words (only the selected suffixes' bytes are converted), packed
+      // lb-bit codes when the keyed radix is 2^lb with lb | 32
+      const bool sparse = m * 3 < n;
+      const int mode = !sparse ? 0 : (ka.lb ? 2 : 1);
       const uint16_t* mk = ix.sel.as<uint16_t>();
+      const uint16_t* k2d = reinterpret_cast<const uint16_t*>(small + 7456);
       uint64_t* k0 = ix.keys[0].as<uint64_t>();
-      auto launch = [&](auto vtag, auto rawtag, void* v) {
+      auto launch = [&](auto vtag, auto modetag, void* v) {
         using VT = decltype(vtag);
-        k_select_write<VT, decltype(rawtag)::value><<<grid, 256, 0, s>>>(
-            ix.text.as<uint8_t>(), n, tpb, mk, lutk, lutp, skey, ka, bc, k0, reinterpret_cast<VT*>(v), hb, sbn,
-            d_kmm, h0);
+        k_select_write<VT, decltype(modetag)::value><<<grid, 256, 0, s>>>(
+            ix.text.as<uint8_t>(), n, tpb, mk, lutk, lutp, k2d, skey, ka, bc, k0, reinterpret_cast<VT*>(v), hb,
+            sbn, d_kmm, h0);
       };
+      using M0 = std::integral_constant<int, 0>;
+      using M1 = std::integral_constant<int, 1>;
+      using M2 = std::integral_constant<int, 2>;
       void* v0 = ix.vals[0].p;
       if (hb) {
-        if (raw) launch(uint32_t{}, std::true_type{}, v0);
-        else launch(uint32_t{}, std::false_type{}, v0);
+        if (mode == 2) launch(uint32_t{}, M2{}, v0);
+        else if (mode == 1) launch(uint32_t{}, M1{}, v0);
+        else launch(uint32_t{}, M0{}, v0);
       } else {
-        if (raw) launch(V{}, std::true_type{}, v0);
-        else launch(V{}, std::false_type{}, v0);
+        if (mode == 2) launch(V{}, M2{}, v0);
+        else if (mode == 1) launch(V{}, M1{}, v0);
+        else launch(V{}, M0{}, v0);
       }
       HK_HIP(hipGetLastError());
     }

@@ -45,6 +45,10 @@ def _cases():
     # skewed binary: wide local keys and big buckets (most suffixes start with a's)
     yield "skewed_binary_4M", np.concatenate([_rand(1 << 22, b"ab", 29, p=[0.9, 0.1]),
                                               [ord("$")]]).astype(np.uint8)
+    # keyed radix 2^3 and 2^5 (codes do not tile a 32-bit word) and 2^4
+    yield "radix8_1M", oracle.synth_text((1 << 20) + 1, b"ACDEFGHI", seed=32)
+    yield "radix16_1M", oracle.synth_text((1 << 20) + 1, b"ABCDEFGHIJKLMNOP", seed=33)
+    yield "radix32_1M", oracle.synth_text((1 << 20) + 1, bytes(range(0x41, 0x61)), seed=34)
     yield "bytes_2M", oracle.synth_text((1 << 21) + 1, bytes(range(256)), seed=30)
     yield "printable_3M", oracle.synth_text(3 * (1 << 20) + 1, bytes(range(0x20, 0x7F)), seed=31)
     base = rng.integers(0, 4, size=3000).astype(np.uint8) + ord("A")
