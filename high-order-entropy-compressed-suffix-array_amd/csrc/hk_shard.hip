@@ -722,7 +722,7 @@ void shard_build_t(Index& ix, const uint64_t* ghist, const uint64_t* gbelow, int
       // sparse slices stage raw words (only the selected suffixes' bytes are converted), packed
       // lb-bit codes when the keyed radix is 2^lb with lb | 32
       const bool sparse = m * 3 < n;
-      const int mode = !sparse ? 0 : (ka.lb ? 2 : 1);
+      const int mode = ka.lb ? 2 : (sparse ? 1 : 0);
       const uint16_t* mk = ix.sel.as<uint16_t>();
       const uint16_t* k2d = reinterpret_cast<const uint16_t*>(small + 7456);
       uint64_t* k0 = ix.keys[0].as<uint64_t>();
