@@ -186,13 +186,11 @@ struct SelGeom {
 constexpr uint32_t SEL_NOPRE = 1, SEL_EMPTY = 2, SEL_HAS_A = 4, SEL_HAS_B = 8;
 
 
-// selection bits of the 16 positions p0 .. p0+15 (bit k: p0 + k)
-__device__ __forceinline__ uint32_t select16(const uint8_t* __restrict__ t, uint64_t n, uint64_t p0,
-                                             const uint16_t* L, const BucketGeom& g, const SelGeom& sg,
-                                             uint32_t blo, uint32_t bhi) {
+// selection bits of the 16 positions p0 .. p0+15 (bit k: p0 + k) from their 32 text bytes a, b
+__device__ __forceinline__ uint32_t select16w(const uint4& a, const uint4& b, const uint8_t* __restrict__ t,
+                                              uint64_t n, uint64_t p0, const uint16_t* L, const BucketGeom& g,
+                                              const SelGeom& sg, uint32_t blo, uint32_t bhi) {
   if (p0 >= n) return 0;
-  const uint4 a = *reinterpret_cast<const uint4*>(t + p0);        // T' has 64 readable pad bytes
-  const uint4 b = *reinterpret_cast<const uint4*>(t + p0 + 16);
   const uint32_t w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
   // Branch-free per position (short-circuit && / || on per-lane values compiled to exec-mask
   // juggling that made this loop scalar-ALU bound): in range <=> be - TL <= TH - TL (unsigned);
@@ -229,6 +227,7 @@ __device__ __forceinline__ uint32_t select16(const uint8_t* __restrict__ t, uint
   return acc;
 }
 
+
 __global__ __launch_bounds__(256) void k_select_count(const uint8_t* __restrict__ t, uint64_t n, uint64_t tpb,
                                                       const uint16_t* __restrict__ lut, BucketGeom g, SelGeom sg,
                                                       uint32_t blo, uint32_t bhi, uint64_t* __restrict__ block_cnt,
@@ -241,11 +240,27 @@ __global__ __launch_bounds__(256) void k_select_count(const uint8_t* __restrict_
   const uint64_t t0 = (uint64_t)blockIdx.x * tpb;
   const uint64_t t1 = t0 + tpb < tiles ? t0 + tpb : tiles;
   uint64_t cnt = 0;
-#pragma unroll 2
-  for (uint64_t ti = t0; ti < t1; ++ti) {
-    const uint32_t sel = select16(t, n, ti * PS_TILE + 16 * threadIdx.x, L, g, sg, blo, bhi);
-    masks[ti * 256 + threadIdx.x] = (uint16_t)sel;   // the write pass reads these instead of re-testing
-    cnt += __popc(sel);
+  // four tiles per round: their eight 16-byte loads are in flight together
+  constexpr int U = 4;
+  for (uint64_t ti = t0; ti < t1; ti += U) {
+    uint4 a[U], b[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint64_t p0 = (ti + u) * PS_TILE + 16 * threadIdx.x;
+      if (ti + u < t1 && p0 < n) {
+        a[u] = *reinterpret_cast<const uint4*>(t + p0);
+        b[u] = *reinterpret_cast<const uint4*>(t + p0 + 16);
+      } else {
+        a[u] = b[u] = make_uint4(0, 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (ti + u >= t1) break;
+      const uint32_t sel = select16w(a[u], b[u], t, n, (ti + u) * PS_TILE + 16 * threadIdx.x, L, g, sg, blo, bhi);
+      masks[(ti + u) * 256 + threadIdx.x] = (uint16_t)sel;   // the write pass reads these instead of re-testing
+      cnt += __popc(sel);
+    }
   }
   cnt = wave_sum(cnt);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = cnt;
