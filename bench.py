@@ -159,7 +159,8 @@ def run_single(args) -> dict:
     value = args.steps * n / 2**20 / wall
     info = dev.build_info()
     roof = roofline(dev, args.traffic_gb)
-    stages = stage_breakdown(dev, ["sa_bucket_hist", "sa_bucket_sort", "sa_big_gather", "radix_onesweep_text",
+    stages = stage_breakdown(dev, ["sa_bucket_hist", "sa_digit_hist", "sa_bin_starts", "sa_bucket_sort",
+                                   "sa_big_gather", "radix_onesweep_text",
                                    "radix_table_text", "radix_tile_hist",
                                    "radix_hist", "radix_onesweep", "radix_onesweep_small", "sa_pack_keys",
                                    "sa_refine_stats", "sa_refine_apply", "sa_refine_keys", "sa_isa_scatter",

@@ -51,18 +51,27 @@ __device__ __forceinline__ void bh_add(uint32_t* H, uint32_t b, unsigned long lo
 }
 
 // Workgroup w covers the positions [w*span, (w+1)*span) (span a multiple of BH_TILE).
-template <bool HQ>
+// DIG (HQ only): only the low 8 bits of the bucket — the first LSD pass's digit — into per-wave
+// 256-bin LDS histograms (the bucket counts come from the sorted keys afterwards, k_bin_starts).
+template <bool HQ, bool DIG = false>
 __global__ __launch_bounds__(BH_T, 1) void k_bucket_hist(const uint8_t* __restrict__ t, uint64_t n,
                                                          const uint16_t* __restrict__ lutk,
                                                          const uint64_t* __restrict__ skey, KeyedArgs g, int bsh,
                                                          int D, unsigned long long* __restrict__ hist,
                                                          uint64_t span) {
-  __shared__ uint32_t H[32768];
+  __shared__ uint32_t H[DIG ? 1 : 32768];
+  __shared__ uint32_t HD[DIG ? BH_T / 64 : 1][256];
   __shared__ uint16_t c[HQ ? 1 : BH_STAGE + kCodePad];
   __shared__ uint16_t L[256];
   __shared__ uint64_t SK[72];
   const uint32_t tid = threadIdx.x;
-  for (uint32_t i = tid; i < 32768; i += BH_T) H[i] = 0;
+  uint32_t* const hd = &HD[DIG ? tid >> 6 : 0][0];
+  auto add = [&](uint32_t b) {
+    if (DIG) atomicAdd(&hd[b & 255u], 1u);
+    else bh_add(H, b, hist);
+  };
+  if (DIG) for (uint32_t i = tid; i < (BH_T / 64) * 256; i += BH_T) (&HD[0][0])[i] = 0;
+  else for (uint32_t i = tid; i < 32768; i += BH_T) H[i] = 0;
   if (tid < 256) L[tid] = lutk[tid];
   if (tid < 72) SK[tid] = skey[tid];
   __syncthreads();
@@ -96,11 +105,11 @@ __global__ __launch_bounds__(BH_T, 1) void k_bucket_hist(const uint8_t* __restri
         for (int i = 0; i < 2 * BH_PER - 1; ++i) {
           b = ((b << lb) | (L[(wd[i >> 2] >> (8 * (i & 3))) & 255u] & 255u)) & bmask;
           const int j = i - (g.hq - 1);
-          if (j >= 0 && j < BH_PER && p0 + j < lim2) bh_add(H, b, hist);
+          if (j >= 0 && j < BH_PER && p0 + j < lim2) add(b);
         }
       }
       for (uint64_t p = p0 > lim ? p0 : lim; p < p0 + BH_PER && p < hi; ++p)
-        bh_add(H, (uint32_t)(SK[p - g.s_start] >> bsh), hist);
+        add((uint32_t)(SK[p - g.s_start] >> bsh));
     }
   } else {
     for (uint64_t base = lo; base < hi; base += BH_STAGE) {
@@ -116,6 +125,15 @@ __global__ __launch_bounds__(BH_T, 1) void k_bucket_hist(const uint8_t* __restri
     }
   }
   __syncthreads();
+  if (DIG) {
+    if (tid < 256) {
+      uint64_t v = 0;
+#pragma unroll
+      for (int w = 0; w < BH_T / 64; ++w) v += HD[w][tid];
+      if (v) atomicAdd(&hist[tid], (unsigned long long)v);
+    }
+    return;
+  }
   const uint32_t nb = 1u << D;
   for (uint32_t i = tid; i < 32768; i += BH_T) {
     const uint32_t v = H[i];
@@ -1037,10 +1055,23 @@ void build_sa_bucketed(Index& ix) {
     if (lb && 32 % lb == 0 && sb == lb * kg.q) ka.lb = lb;
   }
 
-  // ---- 1. bucket histogram
+  // ---- 1. bucket histogram.  Radix 2^k with whole-symbol buckets: only the first LSD pass's digit
+  // histogram is taken from the text now; the bucket counts come from the sorted keys after the
+  // passes (bin starts by binary search), which saves the 64K-bin histogram pass.
   const uint32_t nbins = 1u << D;
   std::vector<uint64_t> hist(nbins, 0);
-  if (D > 0) {
+  uint64_t* d_h0 = reinterpret_cast<uint64_t*>(ix.small.as<uint8_t>() + 5120);
+  const bool late_hist = D > 0 && ka.hq > 0;
+  if (late_hist) {
+    HK_HIP(hipMemsetAsync(d_h0, 0, 256 * 8, s));
+    TimedLaunch t(ix.timer, "sa_digit_hist", (double)n);
+    const uint64_t tiles = ceil_div(n, (uint64_t)BH_TILE);
+    const uint64_t tpw = ceil_div(tiles, 512);   // two workgroups per CU (small LDS)
+    const unsigned grid = (unsigned)ceil_div(tiles, tpw);
+    k_bucket_hist<true, true><<<grid, BH_T, 0, s>>>(ix.text.as<uint8_t>(), n, d_lutk, d_skey, ka, bsh, D,
+                                                    reinterpret_cast<unsigned long long*>(d_h0), tpw * BH_TILE);
+    HK_HIP(hipGetLastError());
+  } else if (D > 0) {
     ix.bk_hist.ensure((uint64_t)nbins * 8);
     HK_HIP(hipMemsetAsync(ix.bk_hist.p, 0, (uint64_t)nbins * 8, s));
     {
@@ -1048,18 +1079,43 @@ void build_sa_bucketed(Index& ix) {
       const uint64_t tiles = ceil_div(n, (uint64_t)BH_TILE);
       const uint64_t tpw = ceil_div(tiles, 256);   // one workgroup per CU
       const unsigned grid = (unsigned)ceil_div(tiles, tpw);
-      if (ka.hq > 0)
-        k_bucket_hist<true><<<grid, BH_T, 0, s>>>(ix.text.as<uint8_t>(), n, d_lutk, d_skey, ka, bsh, D,
-                                                  ix.bk_hist.as<unsigned long long>(), tpw * BH_TILE);
-      else
-        k_bucket_hist<false><<<grid, BH_T, 0, s>>>(ix.text.as<uint8_t>(), n, d_lutk, d_skey, ka, bsh, D,
-                                                   ix.bk_hist.as<unsigned long long>(), tpw * BH_TILE);
+      k_bucket_hist<false><<<grid, BH_T, 0, s>>>(ix.text.as<uint8_t>(), n, d_lutk, d_skey, ka, bsh, D,
+                                                 ix.bk_hist.as<unsigned long long>(), tpw * BH_TILE);
       HK_HIP(hipGetLastError());
     }
     HK_HIP(hipMemcpyAsync(hist.data(), ix.bk_hist.p, (uint64_t)nbins * 8, hipMemcpyDeviceToHost, s));
     HK_HIP(hipStreamSynchronize(s));
   } else {
     hist[0] = n;
+  }
+
+  for (int i = 0; i < 2; ++i) {
+    ix.keys[i].ensure(n * 8 + 16);
+    ix.vals[i].ensure(n * 4 + 16);
+  }
+  uint64_t* kp[2] = {ix.keys[0].as<uint64_t>(), ix.keys[1].as<uint64_t>()};
+  uint32_t* vp[2] = {ix.vals[0].as<uint32_t>(), ix.vals[1].as<uint32_t>()};
+  const TextKeySrc tks{ix.text.as<uint8_t>(), n, d_lutk, d_lutp, d_skey, ka};
+  int slot = 0;
+  bool sorted_by_bucket = false;
+  if (late_hist) {
+    // ---- LSD passes over the bucket bits (the first builds the keys from the text), then the
+    // bucket counts from the sorted keys
+    slot = radix_sort_pairs<uint32_t>(ix.sw, ix.timer, kp, vp, 0, n, pb + bsh, pb + sb, true, s, d_h0, &tks);
+    ix.info[0] += ix.sw.passes_run;
+    ix.info[1] += ix.sw.passes_skipped;
+    sorted_by_bucket = true;
+    ix.bk_hist.ensure((uint64_t)(nbins + 1) * 8);
+    {
+      TimedLaunch t(ix.timer, "sa_bin_starts", (double)(nbins + 1) * 8);
+      k_bin_starts<<<(nbins + 1 + 255) / 256, 256, 0, s>>>(kp[slot], n, 0, pb + bsh, nbins,
+                                                          ix.bk_hist.as<uint64_t>());
+      HK_HIP(hipGetLastError());
+    }
+    std::vector<uint64_t> st(nbins + 1);
+    HK_HIP(hipMemcpyAsync(st.data(), ix.bk_hist.p, (uint64_t)(nbins + 1) * 8, hipMemcpyDeviceToHost, s));
+    HK_HIP(hipStreamSynchronize(s));
+    for (uint32_t b = 0; b < nbins; ++b) hist[b] = st[b + 1] - st[b];
   }
 
   // ---- 2. work items (whole buckets, packed while they fit) and big buckets
@@ -1073,12 +1129,6 @@ void build_sa_bucketed(Index& ix) {
   ix.info[5] = big_start.size();
   ix.info[6] = big_total;
 
-  for (int i = 0; i < 2; ++i) {
-    ix.keys[i].ensure(n * 8 + 16);
-    ix.vals[i].ensure(n * 4 + 16);
-  }
-  uint64_t* kp[2] = {ix.keys[0].as<uint64_t>(), ix.keys[1].as<uint64_t>()};
-  uint32_t* vp[2] = {ix.vals[0].as<uint32_t>(), ix.vals[1].as<uint32_t>()};
   auto pack = [&]() {
     TimedLaunch t(ix.timer, "sa_pack_keys", (double)n * 9);
     const uint64_t g = std::min<uint64_t>(ceil_div(n, PKK_TILE), 4096);
@@ -1088,8 +1138,14 @@ void build_sa_bucketed(Index& ix) {
 
   if (big_total > n / 2) {
     // skewed text: the global path (full LSD radix sort + refinement from the keys)
-    pack();
-    const int slot = radix_sort_pairs<uint32_t>(ix.sw, ix.timer, kp, vp, 0, n, pb, pb + sb, true, s);
+    int gs;
+    if (sorted_by_bucket) {
+      gs = radix_sort_pairs<uint32_t>(ix.sw, ix.timer, kp, vp, slot, n, pb, pb + sb, false, s);
+    } else {
+      pack();
+      gs = radix_sort_pairs<uint32_t>(ix.sw, ix.timer, kp, vp, 0, n, pb, pb + sb, true, s);
+    }
+    const int slot = gs;
     ix.info[0] += ix.sw.passes_run;
     ix.info[1] += ix.sw.passes_skipped;
     std::swap(ix.sa, ix.vals[slot]);
@@ -1102,16 +1158,15 @@ void build_sa_bucketed(Index& ix) {
   }
 
   // ---- 3. LSD passes over the top D bits (digit histograms are marginals of the bucket histogram)
-  int slot = 0;
-  if (D > 0) {
+  if (sorted_by_bucket) {
+    // done above
+  } else if (D > 0) {
     // the first pass builds the keys from the text (no key array is written and re-read); both
     // passes are onesweep passes with decoupled lookback (measured faster on MI355X than a
     // reduce-then-scan with per-tile offset tables, which adds table traffic to every tile)
-    const TextKeySrc tks{ix.text.as<uint8_t>(), n, d_lutk, d_lutp, d_skey, ka};
     uint64_t h0[256] = {0};
     const int lowd = std::min(D, 8);
     for (uint32_t b = 0; b < nbins; ++b) h0[b & ((1u << lowd) - 1)] += hist[b];
-    uint64_t* d_h0 = reinterpret_cast<uint64_t*>(ix.small.as<uint8_t>() + 5120);
     HK_HIP(hipMemcpyAsync(d_h0, h0, sizeof(h0), hipMemcpyHostToDevice, s));
     slot = radix_sort_pairs<uint32_t>(ix.sw, ix.timer, kp, vp, 0, n, pb + bsh, pb + sb, true, s, d_h0, &tks);
     ix.info[0] += ix.sw.passes_run;
