@@ -5,7 +5,7 @@ gfx950 reports half of the bytes of wide coalesced reads (MI355X_MICROARCH.md §
 exact for streaming stores.  Per bench timer name, the n-element launches of its kernel are averaged:
   sa_bucket_sort       k_bucket_sort<false, ...>          (LDS bucket sorts)
   radix_onesweep_text  k_onesweep<unsigned int, 512, 16, 0, 4, true>   (first pass, keys from text)
-  radix_onesweep       k_onesweep<unsigned int, 512, 16, 0, 4, false>  (second pass)
+  radix_onesweep       k_onesweep<unsigned int, 1024, 16, 0, 4, false> (second pass)
 """
 import csv, json, os, sys
 
@@ -14,7 +14,7 @@ src = sys.argv[1] if len(sys.argv) > 1 else os.path.join(root, "gpurun_out")
 KERNELS = {
     "sa_bucket_sort": lambda k: "k_bucket_sort<false" in k,
     "radix_onesweep_text": lambda k: "k_onesweep<unsigned int, 512, 16, 0, 4, true>" in k,
-    "radix_onesweep": lambda k: "k_onesweep<unsigned int, 512, 16, 0, 4, false>" in k,
+    "radix_onesweep": lambda k: "k_onesweep<unsigned int, 1024, 16, 0, 4, false>" in k,
 }
 
 
