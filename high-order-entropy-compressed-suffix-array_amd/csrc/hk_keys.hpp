@@ -254,17 +254,19 @@ struct TextKeySrc {
 // (3 LDS words).  Otherwise the tile's codes are staged and each key is a chunked Horner sum.
 // LDS: codes[T*I + kCodePad] (generic) or pk[(T*I + 64)/4 + 4] + raw[T*I + 64] (packed), which
 // may alias each other; contains barriers (call from every thread of the block).
-template <int T, int I>
+// LB > 0: the packed path with lb = LB known at compile time (fully unrolled packing, static
+// register indices); LB = 0: lb from src.g.lb at run time (0 = the Horner path).
+template <int T, int I, int LB = 0>
 __device__ __forceinline__ void text_keys(uint64_t (&key)[I], const TextKeySrc& src, uint64_t n, uint64_t tbase,
                                           uint64_t wbase, uint32_t lane, uint16_t* codes, uint32_t* pk,
                                           uint8_t* raw, uint32_t* prev0, const uint16_t* L, const uint16_t* LP,
                                           const uint64_t* SK) {
   constexpr int TILE = T * I;
   const uint32_t tid = threadIdx.x;
-  if (src.g.lb) {
+  if (LB || src.g.lb) {
     // radix 2^lb: each staging thread maps 32 text bytes to codes and packs them MSB-first into
     // lb words; a key is then the q*lb-bit window at bit off*lb of the stream (3 LDS words)
-    const int lb = src.g.lb;
+    const int lb = LB ? LB : src.g.lb;
     if (tid == 0) *prev0 = src.text[tbase == 0 ? n - 1 : tbase - 1];
     for (uint32_t c = tid; c < (uint32_t)(TILE + 64) / 32; c += T) {
       const uint64_t p0 = tbase + 32ull * c;
@@ -277,14 +279,28 @@ __device__ __forceinline__ void text_keys(uint64_t (&key)[I], const TextKeySrc& 
       const uint32_t w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
       *reinterpret_cast<uint4*>(&raw[32 * c]) = a;
       *reinterpret_cast<uint4*>(&raw[32 * c + 16]) = b;
-      const int per = 32 / lb;   // codes per word
-      for (int o = 0; o < lb; ++o) {
-        uint32_t word = 0;
-        for (int u = 0; u < per; ++u) {
-          const int i = o * per + u;
-          word = (word << lb) | (L[(w[i >> 2] >> (8 * (i & 3))) & 255u] & 255u);
+      if (LB) {
+        constexpr int PER = LB ? 32 / LB : 1;
+#pragma unroll
+        for (int o = 0; o < LB; ++o) {
+          uint32_t word = 0;
+#pragma unroll
+          for (int u = 0; u < PER; ++u) {
+            const int i = o * PER + u;
+            word = (word << LB) | (L[(w[i >> 2] >> (8 * (i & 3))) & 255u] & 255u);
+          }
+          pk[c * LB + o] = word;
         }
-        pk[c * lb + o] = word;
+      } else {
+        const int per = 32 / lb;   // codes per word
+        for (int o = 0; o < lb; ++o) {
+          uint32_t word = 0;
+          for (int u = 0; u < per; ++u) {
+            const int i = o * per + u;
+            word = (word << lb) | (L[(w[i >> 2] >> (8 * (i & 3))) & 255u] & 255u);
+          }
+          pk[c * lb + o] = word;
+        }
       }
     }
     __syncthreads();

@@ -313,7 +313,7 @@ __device__ __forceinline__ uint64_t lookback(const uint64_t* status, uint32_t ti
 // values into LDS -> values out.
 // FT: the pass reads the text instead of keys and builds each suffix's keyed key in registers from
 // the tile's text codes staged in LDS (the first pass of the bucket build; values are positions).
-template <typename V, int T, int I, int MODE, int LBW = 4, bool FT = false>
+template <typename V, int T, int I, int MODE, int LBW = 4, bool FT = false, int LB = 0>
 __global__ __launch_bounds__(T, T >= 512 ? 4 : 3) void k_onesweep(
     const uint64_t* __restrict__ kin, const V* __restrict__ vin, uint64_t* __restrict__ kout,
     V* __restrict__ vout, uint64_t n, uint32_t shift, const uint64_t* __restrict__ goff,
@@ -342,7 +342,7 @@ __global__ __launch_bounds__(T, T >= 512 ? 4 : 3) void k_onesweep(
     }
     if (tid < 72) sh.SK[tid] = src.skey[tid];
     __syncthreads();
-    text_keys<T, I>(key, src, n, tbase, wbase, lane, sh.stage.codes, sh.stage.ft.pk, sh.stage.ft.raw, &sh.prev0,
+    text_keys<T, I, LB>(key, src, n, tbase, wbase, lane, sh.stage.codes, sh.stage.ft.pk, sh.stage.ft.raw, &sh.prev0,
                     sh.L, sh.LP, sh.SK);
   } else {
 #pragma unroll
@@ -621,6 +621,11 @@ int radix_sort_pairs(SortWork& w, KernelTimer& tm, uint64_t* k[2], V* v[2], int 
       if (from_text) {
         if (small)
           k_onesweep<V, 256, OS_I, 0, 4, true><<<(unsigned)tiles, 256, 0, s>>>(
+              nullptr, nullptr, k[nxt], v[nxt], n, (uint32_t)(bit_lo + 8 * p), w.offs.as<uint64_t>() + p * 256,
+              w.status.as<uint64_t>(), w.counters.as<uint32_t>() + p, w.epoch, w.err.as<uint32_t>(), 1,
+              has_next ? bit_lo + 8 * (p + 1) : -1, w.hpart.as<unsigned long long>(), *src);
+        else if (src->g.lb == 2)   // DNA: packing fully unrolled
+          k_onesweep<V, OS_T, OS_I, 0, 4, true, 2><<<(unsigned)tiles, OS_T, 0, s>>>(
               nullptr, nullptr, k[nxt], v[nxt], n, (uint32_t)(bit_lo + 8 * p), w.offs.as<uint64_t>() + p * 256,
               w.status.as<uint64_t>(), w.counters.as<uint32_t>() + p, w.epoch, w.err.as<uint32_t>(), 1,
               has_next ? bit_lo + 8 * (p + 1) : -1, w.hpart.as<unsigned long long>(), *src);

@@ -13,8 +13,8 @@ root = os.path.dirname(os.path.abspath(__file__))
 src = sys.argv[1] if len(sys.argv) > 1 else os.path.join(root, "gpurun_out")
 KERNELS = {
     "sa_bucket_sort": lambda k: "k_bucket_sort<false" in k,
-    "radix_onesweep_text": lambda k: "k_onesweep<unsigned int, 512, 16, 0, 4, true>" in k,
-    "radix_onesweep": lambda k: "k_onesweep<unsigned int, 1024, 16, 0, 4, false>" in k,
+    "radix_onesweep_text": lambda k: "k_onesweep<unsigned int, 512, 16, 0, 4, true" in k,
+    "radix_onesweep": lambda k: "k_onesweep<unsigned int, 1024, 16, 0, 4, false" in k,
 }
 
 
