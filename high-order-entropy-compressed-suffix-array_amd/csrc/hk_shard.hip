@@ -280,7 +280,7 @@ __global__ __launch_bounds__(256) void k_select_count(const uint8_t* __restrict_
 // text words, only the selected suffixes' bytes go through the code table.  MODE 2 (sparse, keyed
 // radix 2^lb with lb | 32): raw words, then one pass packs the tile's codes MSB-first into lb-bit
 // fields and every key is a q*lb-bit window of that stream (three LDS words, no per-symbol loop).
-template <typename V, int MODE>
+template <typename V, int MODE, int LB = 0>
 __global__ __launch_bounds__(256) void k_select_write(const uint8_t* __restrict__ t, uint64_t n, uint64_t tpb,
                                                       const uint16_t* __restrict__ masks,
                                                       const uint16_t* __restrict__ lutk,
@@ -313,7 +313,7 @@ __global__ __launch_bounds__(256) void k_select_write(const uint8_t* __restrict_
   __syncthreads();
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int pbe = ka.pb + hb;
-  const int lb = ka.lb, per = MODE == 2 ? 32 / ka.lb : 1, kbits = ka.q * ka.lb;
+  const int lb = LB ? LB : ka.lb, per = MODE == 2 ? 32 / lb : 1, kbits = ka.q * lb;
   const uint64_t tiles = (n + PS_TILE - 1) / PS_TILE;
   const uint64_t t0 = (uint64_t)blockIdx.x * tpb;
   const uint64_t t1 = t0 + tpb < tiles ? t0 + tpb : tiles;
@@ -375,7 +375,13 @@ __global__ __launch_bounds__(256) void k_select_write(const uint8_t* __restrict_
       const uint8_t* WB = reinterpret_cast<const uint8_t*>(W);
       for (int wd = threadIdx.x; wd * per < NSYM; wd += 256) {
         uint32_t word = 0;
-        for (int u = 0; u < per; ++u) word = (word << lb) | (LK[WB[wd * per + u + 3]] & 255u);
+        if (LB) {   // compile-time lb: unrolled
+          constexpr int PER = LB ? 32 / LB : 1;
+#pragma unroll
+          for (int u = 0; u < PER; ++u) word = (word << LB) | (LK[WB[wd * PER + u + 3]] & 255u);
+        } else {
+          for (int u = 0; u < per; ++u) word = (word << lb) | (LK[WB[wd * per + u + 3]] & 255u);
+        }
         PK[wd] = word;
       }
       __syncthreads();
@@ -743,9 +749,15 @@ void shard_build_t(Index& ix, const uint64_t* ghist, const uint64_t* gbelow, int
       uint64_t* k0 = ix.keys[0].as<uint64_t>();
       auto launch = [&](auto vtag, auto modetag, void* v) {
         using VT = decltype(vtag);
-        k_select_write<VT, decltype(modetag)::value><<<grid, 256, 0, s>>>(
-            ix.text.as<uint8_t>(), n, tpb, mk, lutk, lutp, k2d, skey, ka, bc, k0, reinterpret_cast<VT*>(v), hb,
-            sbn, d_kmm, h0);
+        constexpr int MD = decltype(modetag)::value;
+        if (MD == 2 && ka.lb == 2)   // DNA: the packing loop unrolled
+          k_select_write<VT, MD, 2><<<grid, 256, 0, s>>>(
+              ix.text.as<uint8_t>(), n, tpb, mk, lutk, lutp, k2d, skey, ka, bc, k0, reinterpret_cast<VT*>(v), hb,
+              sbn, d_kmm, h0);
+        else
+          k_select_write<VT, MD><<<grid, 256, 0, s>>>(
+              ix.text.as<uint8_t>(), n, tpb, mk, lutk, lutp, k2d, skey, ka, bc, k0, reinterpret_cast<VT*>(v), hb,
+              sbn, d_kmm, h0);
       };
       using M0 = std::integral_constant<int, 0>;
       using M1 = std::integral_constant<int, 1>;
