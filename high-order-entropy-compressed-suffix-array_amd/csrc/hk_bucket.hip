@@ -395,16 +395,24 @@ __device__ __forceinline__ void bucket_sort_item(BsShared& sh, uint2 it, const u
       reinterpret_cast<uint32_t*>(&sh.mt[0][0])[tid] = 0;   // gpre back to clean match masks
     }
     if (TRACE && d0 == 0) ts[7] = stamp();
-    auto dst = [&](int k) -> uint32_t { return sh.whist[wv][digit_of(k)] + half(rk2, k); };
+    // destinations of all items first (the base reads issue back to back, one wait), in place of
+    // the ranks; empty slots (only when cnt < BS_CAP) all write to the free slot cnt, so the
+    // exchange stores need no per-item branch
+#pragma unroll
+    for (int j = 0; j < BS_H; ++j) {
+      const uint32_t a = sh.whist[wv][digit_of(j)] + (rk2[j] & 0xFFFFu);
+      const uint32_t b = sh.whist[wv][digit_of(j + BS_H)] + (rk2[j] >> 16);
+      rk2[j] = (((vmask >> j) & 1u) ? a : cnt) | ((((vmask >> (j + BS_H)) & 1u) ? b : cnt) << 16);
+    }
+    auto dst = [&](int k) -> uint32_t { return half(rk2, k); };
     if (packprev) {
       // one exchange phase: key word (with the prev code) and original slot together
 #pragma unroll
-      for (int k = 0; k < BS_I; ++k)
-        if ((vmask >> k) & 1u) {
-          const uint32_t D = dst(k);
-          sh.buf[D] = klo[k];
-          sh.aux[D] = (uint16_t)half(ix2, k);
-        }
+      for (int k = 0; k < BS_I; ++k) {
+        const uint32_t D = dst(k);
+        sh.buf[D] = klo[k];
+        sh.aux[D] = (uint16_t)half(ix2, k);
+      }
       __syncthreads();
       for (uint32_t i = tid; i < BS_V * 256; i += BS_T) (&sh.whist[0][0])[i] = 0;
 #pragma unroll
@@ -415,7 +423,7 @@ __device__ __forceinline__ void bucket_sort_item(BsShared& sh, uint2 it, const u
     } else {
 #pragma unroll
       for (int k = 0; k < BS_I; ++k)
-        if ((vmask >> k) & 1u) buf16[dst(k)] = (uint16_t)half(ix2, k);
+        buf16[dst(k)] = (uint16_t)half(ix2, k);
       __syncthreads();
 #pragma unroll
       for (int j = 0; j < BS_H; ++j) ix2[j] = (uint32_t)buf16[s0 + 64u * j] | ((uint32_t)buf16[s0 + 64u * (j + BS_H)] << 16);
@@ -423,7 +431,7 @@ __device__ __forceinline__ void bucket_sort_item(BsShared& sh, uint2 it, const u
       if (WIDE) {
 #pragma unroll
         for (int k = 0; k < BS_I; ++k)
-          if ((vmask >> k) & 1u) sh.buf[dst(k)] = khi[k];
+          sh.buf[dst(k)] = khi[k];
         __syncthreads();
         uint32_t nh[BS_I];
 #pragma unroll
@@ -431,7 +439,7 @@ __device__ __forceinline__ void bucket_sort_item(BsShared& sh, uint2 it, const u
         __syncthreads();
 #pragma unroll
         for (int k = 0; k < BS_I; ++k)
-          if ((vmask >> k) & 1u) sh.buf[dst(k)] = klo[k];
+          sh.buf[dst(k)] = klo[k];
         __syncthreads();
         for (uint32_t i = tid; i < BS_V * 256; i += BS_T) (&sh.whist[0][0])[i] = 0;
 #pragma unroll
@@ -443,7 +451,7 @@ __device__ __forceinline__ void bucket_sort_item(BsShared& sh, uint2 it, const u
       } else {
 #pragma unroll
         for (int k = 0; k < BS_I; ++k)
-          if ((vmask >> k) & 1u) sh.buf[dst(k)] = klo[k];
+          sh.buf[dst(k)] = klo[k];
         __syncthreads();
         for (uint32_t i = tid; i < BS_V * 256; i += BS_T) (&sh.whist[0][0])[i] = 0;
 #pragma unroll
