@@ -89,7 +89,7 @@ ROOF_KERNELS = ("sa_bucket_sort", "radix_onesweep_text", "radix_onesweep")
 
 def pmc_traffic_gb(name: str) -> float | None:
     """HBM GB per launch of timer `name`'s kernel, measured with rocprofv3 PMC counters on this config
-    (tools_gpu_pmc.sh + tools_pmc_summary.py -> profiles/pmc_kernels.json; FETCH_SIZE x2 gfx950 correction)."""
+    (tools/gpu_pmc.sh + tools/pmc_summary.py -> profiles/pmc_kernels.json; FETCH_SIZE x2 gfx950 correction)."""
     p = os.path.join(ROOT, "profiles", "pmc_kernels.json")
     try:
         with open(p) as f:

@@ -1030,8 +1030,10 @@ void build_sa_bucketed(Index& ix) {
   const uint64_t n = ix.n;
   hipStream_t s = ix.stream;
   if (n >= 0xFFFFFFFFull) throw ApiError{-6, "single-GPU build supports n < 2^32 - 1"};
+  ix.have_alpha = false;   // every build recomputes the byte histogram / C (utils/utils.py:16-24)
   compute_alphabet(ix);
   ix.info.assign(8, 0);
+  ix.dbl = Index::DblState{};
   ix.sharded = false;
   ix.sa_pos64 = false;
   ix.have_sa = ix.have_bwt = ix.have_wt = false;

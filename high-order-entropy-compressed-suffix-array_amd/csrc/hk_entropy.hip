@@ -119,7 +119,12 @@ double entropy_k(Index& ix, int k) {
     return h;
   }
   if (n <= (uint64_t)k) return 0.0;                // :18-19
-  if (!ix.have_sa || ix.sharded) build_sa(ix);
+  if (ix.sharded) throw ApiError{-3, "entropy: a sharded index holds only a slice"};
+  if (!ix.have_sa) {   // the SA of the same text: an existing BWT / wavelet tree stays valid
+    const bool wt = ix.have_wt;
+    build_sa(ix);
+    ix.have_wt = wt;
+  }
   if (ix.sa_pos64) throw ApiError{-6, "entropy: 64-bit suffix arrays not supported"};
   hipStream_t s = ix.stream;
   const uint64_t m = n - (uint64_t)k;              // positions i < n - k

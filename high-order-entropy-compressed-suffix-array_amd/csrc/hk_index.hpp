@@ -100,7 +100,7 @@ struct Index {
   DevBuf big_k[2], big_v[2], big_j; // big buckets of the bucket build (sorted on the global path)
   DevBuf bk_items, bk_hist;       // bucket work items, bucket histogram
   DevBuf sel;                     // sharded build: selection masks of the slice (u16 per 16 positions)
-  DevBuf tile_a, tile_b, tile_c, tile_d;
+  DevBuf tile_a, tile_b, tile_c, tile_d, tile_e;
   DevBuf small;                // scratch for totals etc.
   DevBuf seq[2];               // WT level code sequences
   DevBuf gr_tmp[2], gr_out;    // Golomb-Rice coding of a level (per-word carries/offsets, code words)
@@ -118,6 +118,19 @@ struct Index {
   bool sharded = false;
   bool sa_pos64 = false;       // sharded slices of texts with n >= 2^32 hold u64 positions
   uint64_t shard_lo = 0, shard_hi = 0;
+  std::vector<uint64_t> shard_bounds;   // SA slice starts of every rank (+ n), from the RCCL build
+
+  // prefix doubling over the tied suffixes left by the chunk refinement (DblState): the active
+  // list act[dbl.cur] (P, J = slot in the slice, G = dense group ordinal), A suffixes in `groups`
+  // groups whose members share their first h symbols.  A sharded slice leaves this pending for
+  // the rank exchange (isa = global ISA replica, upd = (position, ISA) pairs of the last step).
+  struct DblState {
+    int cur = 0;
+    uint64_t A = 0, groups = 0, h = 0;
+    uint64_t npairs = 0;       // pairs in upd from the last step
+    bool pending = false;
+  } dbl;
+  DevBuf upd;
 
   KernelTimer timer;
   std::vector<uint64_t> info;  // build counters (see hkcsa_build_info)
@@ -172,6 +185,14 @@ int shard_sample();
 void shard_get_sa(Index& ix, uint64_t a, uint64_t b, uint64_t* out);
 void shard_get_bwt(Index& ix, uint64_t a, uint64_t b, uint8_t* out);
 void build_sa_sharded(Index& ix, const uint8_t id[128], int nranks, int rank);
+void shard_replicate(Index& ix);                                          // RCCL: full SA + BWT on every rank
+void shard_adopt(Index& ix, const uint64_t* h_sa, const uint8_t* h_bwt);  // host-assembled full SA + BWT
+// host-driven rank exchange of the sharded prefix doubling (hkcsa_shard_status ... hkcsa_shard_round)
+void shard_status(Index& ix, uint64_t st[4]);
+void shard_isa_segment_host(Index& ix, const uint64_t* h_sa, uint64_t count, uint64_t lo);
+uint64_t shard_updates(Index& ix, uint64_t* h_pairs, uint64_t cap);
+void shard_apply_host(Index& ix, const uint64_t* h_pairs, uint64_t count);
+void shard_round(Index& ix, uint64_t K);
 void comm_unique_id(uint8_t id[128]);
 
 // shared by the single-GPU and sharded builds
@@ -198,6 +219,15 @@ template <typename V>
 void refine_from_ties(Index& ix, const KeyGeom& kg, uint64_t A, bool allow_doubling);
 template <typename V>
 void refine_loop(Index& ix, const KeyGeom& kg, int cur, uint64_t A, uint64_t groups, bool allow_doubling);
+
+// Prefix doubling over the tied suffixes (hk_sa.hip).  allow_doubling = true above runs it locally
+// (single GPU: ISA from the full SA); with false, refine_loop stops after its chunk rounds with
+// ix.dbl pending and the sharded driver runs these steps around a rank exchange of ISA values.
+void dbl_isa_segment(Index& ix, const void* d_sa, uint64_t count, uint64_t lo);   // isa[sa[j]] = lo + j
+void dbl_emit_groups(Index& ix);            // upd = (P, slot of its group head) of the tied suffixes
+void dbl_apply_pairs(Index& ix, const uint64_t* d_pairs, uint64_t count);   // isa[p] = v
+void dbl_round(Index& ix, uint64_t K);      // one doubling round at offset dbl.h; dbl.h += K
+void dbl_ensure_isa(Index& ix);
 // SA/BWT of A sorted (keys, P) at slots J; ties (compared >> cs) compacted to (oP, oJ, oG)
 std::pair<uint64_t, uint64_t> refine_step_u32(Index& ix, const KeyGeom& kg, const uint64_t* keys,
                                               const uint32_t* P, const uint32_t* J, uint64_t A, int cs,

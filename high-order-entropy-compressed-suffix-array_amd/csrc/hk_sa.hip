@@ -324,49 +324,65 @@ __global__ __launch_bounds__(256) void k_refine_keys(const V* __restrict__ P, co
   }
 }
 
-// ------------------------------------------------------------- prefix doubling (u32 positions)
-__global__ __launch_bounds__(256) void k_isa_all(const uint32_t* __restrict__ sa, uint64_t n,
-                                                 uint32_t* __restrict__ isa) {
-  for (uint64_t j = (uint64_t)blockIdx.x * 256 + threadIdx.x; j < n; j += (uint64_t)gridDim.x * 256)
-    isa[sa[j]] = (uint32_t)j;
+// ------------------------------------------------------------- prefix doubling
+// ISA values are global SA slots (slice offset lo + slot in the slice).  Every member of a tied
+// group carries the slot of the group's head, so ISA is an order-consistent K-order rank:
+// isa[x] < isa[y] => suffix x < suffix y, and isa[x] == isa[y] => x and y share their first K
+// symbols, K = the smallest common-prefix length of any group still tied (on any rank).  A round
+// sorts each tied group (members sharing h >= K symbols) by ISA[p + h]: the new groups share h + K.
+template <typename V>
+__global__ __launch_bounds__(256) void k_isa_from_sa(const V* __restrict__ sa, uint64_t m, uint64_t lo,
+                                                     V* __restrict__ isa) {
+  for (uint64_t j = (uint64_t)blockIdx.x * 256 + threadIdx.x; j < m; j += (uint64_t)gridDim.x * 256)
+    isa[sa[j]] = (V)(lo + j);
 }
 
-// tied suffixes: ISA = their group start slot; G becomes the group start slot
-__global__ __launch_bounds__(256) void k_isa_active(const uint32_t* __restrict__ P, uint32_t* __restrict__ G,
-                                                    uint64_t A, const uint32_t* __restrict__ head_slot,
-                                                    uint32_t* __restrict__ isa) {
+// tied suffixes: ISA = slot of their group head; into isa directly, or as (position, ISA) pairs
+template <typename V>
+__global__ __launch_bounds__(256) void k_dbl_emit(const V* __restrict__ P, const uint32_t* __restrict__ G, uint64_t A,
+                                                  const uint32_t* __restrict__ head_slot, uint64_t lo,
+                                                  V* __restrict__ isa, uint64_t* __restrict__ pairs) {
   for (uint64_t a = (uint64_t)blockIdx.x * 256 + threadIdx.x; a < A; a += (uint64_t)gridDim.x * 256) {
-    const uint32_t s = head_slot[G[a]];
-    isa[P[a]] = s;
-    G[a] = s;
+    const uint64_t p = P[a], v = lo + head_slot[G[a]];
+    if (pairs) {
+      pairs[2 * a] = p;
+      pairs[2 * a + 1] = v;
+    } else {
+      isa[p] = (V)v;
+    }
   }
 }
 
-// doubling round keys: (group start, ISA[p+h]+1 or 0 past the end), value = position
-__global__ __launch_bounds__(256) void k_pair_keys(const uint32_t* __restrict__ P,
-                                                   const uint32_t* __restrict__ G, uint64_t A,
-                                                   const uint32_t* __restrict__ isa, uint64_t n,
-                                                   uint64_t h, uint64_t* __restrict__ keys,
-                                                   uint32_t* __restrict__ vals) {
+template <typename V>
+__global__ __launch_bounds__(256) void k_dbl_apply_pairs(const uint64_t* __restrict__ pairs, uint64_t cnt,
+                                                         V* __restrict__ isa) {
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < cnt; i += (uint64_t)gridDim.x * 256)
+    isa[pairs[2 * i]] = (V)pairs[2 * i + 1];
+}
+
+// doubling keys: (dense group ordinal << ib) | (ISA[p + h] + 1, or 0 past the end), value = position
+template <typename V>
+__global__ __launch_bounds__(256) void k_dbl_keys(const V* __restrict__ P, const uint32_t* __restrict__ G, uint64_t A,
+                                                  const V* __restrict__ isa, uint64_t n, uint64_t h, int ib,
+                                                  uint64_t* __restrict__ keys, V* __restrict__ vals) {
   for (uint64_t a = (uint64_t)blockIdx.x * 256 + threadIdx.x; a < A; a += (uint64_t)gridDim.x * 256) {
-    const uint32_t p = P[a];
+    const V p = P[a];
     const uint64_t q = (uint64_t)p + h;
     const uint64_t s = q < n ? (uint64_t)isa[q] + 1 : 0;
-    keys[a] = ((uint64_t)G[a] << 32) | s;
+    keys[a] = ((uint64_t)G[a] << ib) | s;
     vals[a] = p;
   }
 }
 
-// per tile: J of the last group head and the number of tied suffixes
-__global__ __launch_bounds__(GR_T) void k_group_stats(const uint64_t* __restrict__ keys,
-                                                      const uint32_t* __restrict__ J, uint64_t A,
-                                                      uint64_t* __restrict__ tile_last,
-                                                      uint32_t* __restrict__ tile_act) {
+// per tile of sorted doubling keys: 1 + slot of the last group head (0: none), tied suffixes, tied heads
+__global__ __launch_bounds__(GR_T) void k_dbl_stats(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ J,
+                                                    uint64_t A, uint64_t* __restrict__ tile_last,
+                                                    uint32_t* __restrict__ tile_act, uint32_t* __restrict__ tile_heads) {
   __shared__ uint64_t red[GR_T / 64];
-  __shared__ uint32_t redc[GR_T / 64];
+  __shared__ uint32_t redc[GR_T / 64], redh[GR_T / 64];
   const uint64_t base = (uint64_t)blockIdx.x * GR_TILE + (uint64_t)threadIdx.x * GR_I;
-  int64_t last = -1;
-  uint32_t act = 0;
+  uint64_t last = 0;
+  uint32_t act = 0, th = 0;
   if (base < A) {
     uint64_t prev = base > 0 ? keys[base - 1] : 0;
     uint64_t cur = keys[base];
@@ -376,46 +392,53 @@ __global__ __launch_bounds__(GR_T) void k_group_stats(const uint64_t* __restrict
       const uint64_t nxt = j + 1 < A ? keys[j + 1] : 0;
       const bool h = (j == 0) || cur != prev;
       const bool hn = (j + 1 >= A) || nxt != cur;
-      if (h) last = (int64_t)j;
+      if (h) last = (uint64_t)J[j] + 1;
       act += (h && hn) ? 0u : 1u;
+      th += (h && !hn) ? 1u : 0u;
       prev = cur;
       cur = nxt;
     }
   }
-  uint64_t lv = (uint64_t)(last + 1);
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
-    uint64_t tt = __shfl_xor(lv, o, 64);
-    lv = lv > tt ? lv : tt;
+    const uint64_t tt = __shfl_xor(last, o, 64);
+    last = last > tt ? last : tt;
     act += __shfl_xor(act, o, 64);
+    th += __shfl_xor(th, o, 64);
   }
   if ((threadIdx.x & 63) == 0) {
-    red[threadIdx.x >> 6] = lv;
+    red[threadIdx.x >> 6] = last;
     redc[threadIdx.x >> 6] = act;
+    redh[threadIdx.x >> 6] = th;
   }
   __syncthreads();
   if (threadIdx.x == 0) {
     uint64_t m = 0;
-    uint32_t c = 0;
+    uint32_t c = 0, hh = 0;
     for (int i = 0; i < GR_T / 64; ++i) {
       m = m > red[i] ? m : red[i];
       c += redc[i];
+      hh += redh[i];
     }
-    tile_last[blockIdx.x] = m ? (uint64_t)J[m - 1] : 0;
+    tile_last[blockIdx.x] = m;
     tile_act[blockIdx.x] = c;
+    tile_heads[blockIdx.x] = hh;
   }
 }
 
-// doubling round: group starts into ISA, SA/BWT entries, compaction of the still-tied suffixes
-__global__ __launch_bounds__(GR_T) void k_group_apply(
-    const uint64_t* __restrict__ keys, const uint32_t* __restrict__ P, const uint32_t* __restrict__ J,
-    uint64_t A, const uint64_t* __restrict__ carry_last, const uint64_t* __restrict__ act_off,
-    uint32_t* __restrict__ isa, uint32_t* __restrict__ sa, uint8_t* __restrict__ bwt,
-    const uint8_t* __restrict__ t, uint64_t n, uint32_t* __restrict__ oP, uint32_t* __restrict__ oJ,
-    uint32_t* __restrict__ oG) {
+// doubling round: SA / BWT entries in the slice, the new ISA of every suffix of the round (slot of
+// its new group head) into isa or as pairs, and the still-tied suffixes compacted with dense group
+// ordinals (head_slot[g] = slot of group g's head).  J is ascending (the round's slots in order).
+template <typename V>
+__global__ __launch_bounds__(GR_T) void k_dbl_apply(
+    const uint64_t* __restrict__ keys, const V* __restrict__ P, const uint32_t* __restrict__ J, uint64_t A,
+    const uint64_t* __restrict__ carry_last, const uint64_t* __restrict__ act_off,
+    const uint64_t* __restrict__ head_off, uint64_t lo, V* __restrict__ isa, uint64_t* __restrict__ pairs,
+    V* __restrict__ sa, uint8_t* __restrict__ bwt, const uint8_t* __restrict__ t, uint64_t n, V* __restrict__ oP,
+    uint32_t* __restrict__ oJ, uint32_t* __restrict__ oG, uint32_t* __restrict__ head_slot) {
   __shared__ uint64_t red[GR_T / 64];
   const uint64_t base = (uint64_t)blockIdx.x * GR_TILE + (uint64_t)threadIdx.x * GR_I;
-  uint32_t hmask = 0, amask = 0;
+  uint32_t hmask = 0, amask = 0, tmask = 0;
   uint64_t tmax = 0;
   if (base < A) {
     uint64_t prev = base > 0 ? keys[base - 1] : 0;
@@ -428,32 +451,41 @@ __global__ __launch_bounds__(GR_T) void k_group_apply(
       const bool hn = (j + 1 >= A) || nxt != cur;
       if (h) {
         hmask |= 1u << i;
-        tmax = J[j];
+        tmax = (uint64_t)J[j] + 1;
       }
       if (!(h && hn)) amask |= 1u << i;
+      if (h && !hn) tmask |= 1u << i;
       prev = cur;
       cur = nxt;
     }
   }
-  const uint64_t carry = carry_last[blockIdx.x];
   uint64_t gpre = blk_excl_max(tmax, red);
+  const uint64_t carry = carry_last[blockIdx.x];
   gpre = gpre > carry ? gpre : carry;
   uint64_t tot;
   uint64_t o = blk_excl_sum((uint64_t)__popc(amask), red, &tot) + act_off[blockIdx.x];
-  uint64_t g = gpre;
+  uint64_t og = blk_excl_sum((uint64_t)__popc(tmask), red, &tot) + head_off[blockIdx.x];
+  uint64_t g = gpre ? gpre - 1 : 0;   // slot of the current group head
   for (int i = 0; i < GR_I; ++i) {
     const uint64_t j = base + i;
     if (j >= A) break;
     const uint32_t jv = J[j];
     if (hmask & (1u << i)) g = jv;
-    const uint32_t p = P[j];
-    isa[p] = (uint32_t)g;
+    const V p = P[j];
     sa[jv] = p;
-    bwt[jv] = t[p == 0 ? n - 1 : p - 1];
+    bwt[jv] = t[p == 0 ? n - 1 : (uint64_t)p - 1];
+    const uint64_t v = lo + g;
+    if (pairs) {
+      pairs[2 * j] = (uint64_t)p;
+      pairs[2 * j + 1] = v;
+    } else {
+      isa[p] = (V)v;
+    }
     if (amask & (1u << i)) {
+      if (tmask & (1u << i)) head_slot[og++] = jv;
       oP[o] = p;
       oJ[o] = jv;
-      oG[o] = (uint32_t)g;
+      oG[o] = (uint32_t)(og - 1);
       ++o;
     }
   }
@@ -500,36 +532,82 @@ __global__ __launch_bounds__(256) void k_synth(uint8_t* __restrict__ t, uint64_t
   }
 }
 
-// one doubling grouping step over A sorted pair keys; returns the new tied count
-uint64_t group_step(Index& ix, const uint64_t* keys, const uint32_t* P, const uint32_t* J, uint64_t A,
-                    uint32_t* oP, uint32_t* oJ, uint32_t* oG) {
+int bits_of_u64(uint64_t v) {
+  int b = 0;
+  while (v) {
+    ++b;
+    v >>= 1;
+  }
+  return b;
+}
+
+// one doubling round over the active list: keys, sort, regroup; see k_dbl_apply
+template <typename V>
+void dbl_round_t(Index& ix, uint64_t K) {
+  auto& st = ix.dbl;
   hipStream_t s = ix.stream;
+  const uint64_t A = st.A;
+  const int cur = st.cur;
+  const int gbits = st.groups > 1 ? bits_of_u64(st.groups - 1) : 0;
+  const int ib = bits_of_u64(ix.n);   // ISA + 1 <= n
+  if (gbits + ib > 64) throw ApiError{-6, "prefix doubling: too many tied groups for one 64-bit key"};
+  uint64_t* kp[2] = {ix.keys[0].as<uint64_t>(), ix.keys[1].as<uint64_t>()};
+  V* vp[2] = {ix.vals[0].as<V>(), ix.vals[1].as<V>()};
+  {
+    TimedLaunch tm(ix.timer, "sa_pair_keys", (double)A * (2 * sizeof(V) + 4 + 8 + sizeof(V)));
+    k_dbl_keys<V><<<grid_for(A), 256, 0, s>>>(ix.act[cur][0].as<V>(), ix.act[cur][2].as<uint32_t>(), A,
+                                              ix.isa.as<V>(), ix.n, st.h, ib, kp[0], vp[0]);
+    HK_HIP(hipGetLastError());
+  }
+  const int sl = radix_sort_pairs<V>(ix.sw, ix.timer, kp, vp, 0, A, 0, gbits + ib, false, s);
+  ix.info[0] += ix.sw.passes_run;
+  ix.info[1] += ix.sw.passes_skipped;
   const uint64_t nt = ceil_div(A, GR_TILE);
   ix.tile_a.ensure((nt + 1) * 8);
   ix.tile_b.ensure((nt + 1) * 4);
   ix.tile_c.ensure((nt + 1) * 8);
   ix.tile_d.ensure((nt + 2) * 8);
+  DevBuf& tb2 = ix.tile_e;
+  tb2.ensure((nt + 2) * 12 + 16);
   uint64_t* tl = ix.tile_a.as<uint64_t>();
   uint32_t* ta = ix.tile_b.as<uint32_t>();
   uint64_t* cl = ix.tile_c.as<uint64_t>();
   uint64_t* ao = ix.tile_d.as<uint64_t>();
+  uint32_t* th = tb2.as<uint32_t>();
+  uint64_t* ho = reinterpret_cast<uint64_t*>(tb2.as<uint8_t>() + ((nt + 2) * 4 + 7) / 8 * 8);
   {
     TimedLaunch tm(ix.timer, "sa_group_stats", (double)A * 8);
-    k_group_stats<<<(unsigned)nt, GR_T, 0, s>>>(keys, J, A, tl, ta);
+    k_dbl_stats<<<(unsigned)nt, GR_T, 0, s>>>(kp[sl], ix.act[cur][1].as<uint32_t>(), A, tl, ta, th);
     HK_HIP(hipGetLastError());
   }
   scan_exclusive_max_u64(ix.sw, tl, cl, nt, s);
   scan_exclusive_u32_to_u64(ix.sw, ta, ao, nt, true, s);
+  scan_exclusive_u32_to_u64(ix.sw, th, ho, nt, true, s);
+  uint64_t* pairs = nullptr;
+  if (ix.sharded) {
+    ix.upd.ensure(A * 16 + 16);
+    pairs = ix.upd.as<uint64_t>();
+  }
   {
-    TimedLaunch tm(ix.timer, "sa_group_apply", (double)A * (8 + 4 + 4 + 4 + 4 + 1));
-    k_group_apply<<<(unsigned)nt, GR_T, 0, s>>>(keys, P, J, A, cl, ao, ix.isa.as<uint32_t>(), ix.sa.as<uint32_t>(),
-                                               ix.bwt.as<uint8_t>(), ix.text.as<uint8_t>(), ix.n, oP, oJ, oG);
+    TimedLaunch tm(ix.timer, "sa_group_apply", (double)A * (8 + 2 * sizeof(V) + 4 + 1 + 1 + (pairs ? 16 : sizeof(V))));
+    k_dbl_apply<V><<<(unsigned)nt, GR_T, 0, s>>>(
+        kp[sl], vp[sl], ix.act[cur][1].as<uint32_t>(), A, cl, ao, ho, ix.sharded ? ix.shard_lo : 0,
+        ix.isa.as<V>(), pairs, ix.sa.as<V>(), ix.bwt.as<uint8_t>(), ix.text.as<uint8_t>(), ix.n,
+        ix.act[cur ^ 1][0].as<V>(), ix.act[cur ^ 1][1].as<uint32_t>(), ix.act[cur ^ 1][2].as<uint32_t>(),
+        ix.head_slot.as<uint32_t>());
     HK_HIP(hipGetLastError());
   }
-  uint64_t na = 0;
-  HK_HIP(hipMemcpyAsync(&na, ao + nt, 8, hipMemcpyDeviceToHost, s));
+  uint64_t tot[2] = {0, 0};
+  HK_HIP(hipMemcpyAsync(&tot[0], ao + nt, 8, hipMemcpyDeviceToHost, s));
+  HK_HIP(hipMemcpyAsync(&tot[1], ho + nt, 8, hipMemcpyDeviceToHost, s));
   HK_HIP(hipStreamSynchronize(s));
-  return na;
+  st.npairs = pairs ? A : 0;
+  st.cur ^= 1;
+  st.A = tot[0];
+  st.groups = tot[1];
+  st.h += K;
+  ix.info.push_back(st.A);
+  ix.info[2] += 1ull << 32;
 }
 
 // one refinement grouping step (stats + scans + apply); returns (tied, groups)
@@ -677,8 +755,7 @@ void refine_loop(Index& ix, const KeyGeom& kg, int cur, uint64_t A, uint64_t gro
   uint64_t h = (uint64_t)kg.q;
   int rounds = 0;
   while (A > 0) {
-    if (++rounds > 200000) throw ApiError{-7, "suffix refinement did not converge"};
-    if (allow_doubling && rounds > kChunkRounds) break;
+    if (++rounds > kChunkRounds) break;
     int gbits = 0;
     while (gbits < 64 && (1ull << gbits) < groups) ++gbits;
     auto fits = [&](int qq) {   // G in the top gbits, chunk + nS (<= R^qq - 1 + nS) below
@@ -690,7 +767,7 @@ void refine_loop(Index& ix, const KeyGeom& kg, int cur, uint64_t A, uint64_t gro
     };
     int qn = 0;
     while (qn < 64 && fits(qn + 1)) ++qn;
-    if (qn < 1) throw ApiError{-6, "too many tied groups for one refinement key"};
+    if (qn < 1) break;   // too many groups for a chunk key: prefix doubling takes over
     {
       TimedLaunch tm(ix.timer, "sa_refine_keys", (double)A * (sizeof(V) * 2 + 4 + 8));
       k_refine_keys<V><<<grid_for(A), 256, 0, s>>>(ix.act[cur][0].as<V>(), ix.act[cur][2].as<uint32_t>(), A,
@@ -710,45 +787,29 @@ void refine_loop(Index& ix, const KeyGeom& kg, int cur, uint64_t A, uint64_t gro
     ix.info.push_back(A);
     h += (uint64_t)qn;
   }
-  ix.info[2] = (uint64_t)rounds;
+  ix.info[2] = (uint64_t)(rounds > kChunkRounds ? kChunkRounds : rounds);
+  ix.dbl = Index::DblState{};
   if (A == 0) return;
-  if constexpr (sizeof(V) == 4) {
-    // ---- prefix doubling from order h: materialise ISA once, then double
-    ix.isa.ensure(ix.n * 4 + 16);
-    {
-      TimedLaunch tm(ix.timer, "sa_isa_scatter", (double)ix.n * 8);
-      k_isa_all<<<grid_for(ix.n), 256, 0, s>>>(ix.sa.as<uint32_t>(), ix.n, ix.isa.as<uint32_t>());
-      HK_HIP(hipGetLastError());
-    }
-    k_isa_active<<<grid_for(A), 256, 0, s>>>(ix.act[cur][0].as<uint32_t>(), ix.act[cur][2].as<uint32_t>(), A,
-                                             ix.head_slot.as<uint32_t>(), ix.isa.as<uint32_t>());
-    HK_HIP(hipGetLastError());
-    int drounds = 0;
-    while (A > 0) {
-      if (++drounds > 64) throw ApiError{-7, "prefix doubling did not converge"};
-      uint32_t* P = ix.act[cur][0].as<uint32_t>();
-      uint32_t* J = ix.act[cur][1].as<uint32_t>();
-      uint32_t* G = ix.act[cur][2].as<uint32_t>();
-      {
-        TimedLaunch tm(ix.timer, "sa_pair_keys", (double)A * (4 + 4 + 4 + 8 + 4));
-        k_pair_keys<<<grid_for(A), 256, 0, s>>>(P, G, A, ix.isa.as<uint32_t>(), ix.n, h, kp[0],
-                                                reinterpret_cast<uint32_t*>(vp[0]));
-        HK_HIP(hipGetLastError());
-      }
-      uint32_t* vq[2] = {reinterpret_cast<uint32_t*>(vp[0]), reinterpret_cast<uint32_t*>(vp[1])};
-      const int sl = radix_sort_pairs<uint32_t>(ix.sw, ix.timer, kp, vq, 0, A, 0, 64, false, s);
-      ix.info[0] += ix.sw.passes_run;
-      ix.info[1] += ix.sw.passes_skipped;
-      A = group_step(ix, kp[sl], vq[sl], J, A, ix.act[cur ^ 1][0].as<uint32_t>(), ix.act[cur ^ 1][1].as<uint32_t>(),
-                     ix.act[cur ^ 1][2].as<uint32_t>());
-      cur ^= 1;
-      ix.info.push_back(A);
-      h *= 2;
-    }
-    ix.info[2] += (uint64_t)drounds << 32;
-  } else {
-    throw ApiError{-7, "prefix doubling fallback needs 32-bit positions"};
+  // ---- prefix doubling from order h over the A tied suffixes (repetitive texts)
+  ix.dbl.cur = cur;
+  ix.dbl.A = A;
+  ix.dbl.groups = groups;
+  ix.dbl.h = h;
+  ix.dbl.pending = true;
+  if (!allow_doubling) {   // sharded slice: the rank exchange drives the rounds (hk_shard.hip)
+    dbl_emit_groups(ix);
+    return;
   }
+  // single GPU: ISA of every position from the full SA, tied suffixes at their head's slot
+  dbl_ensure_isa(ix);
+  dbl_isa_segment(ix, ix.sa.p, ix.n, 0);
+  dbl_emit_groups(ix);
+  int drounds = 0;
+  while (ix.dbl.A > 0) {
+    if (++drounds > 64) throw ApiError{-7, "prefix doubling did not converge"};
+    dbl_round(ix, ix.dbl.h);
+  }
+  ix.dbl.pending = false;
 }
 
 template void refine_after_sort<uint32_t>(Index&, const KeyGeom&, int, uint64_t, bool);
@@ -761,6 +822,65 @@ std::pair<uint64_t, uint64_t> refine_step_u32(Index& ix, const KeyGeom& kg, cons
 
 template void refine_loop<uint32_t>(Index&, const KeyGeom&, int, uint64_t, uint64_t, bool);
 template void refine_loop<uint64_t>(Index&, const KeyGeom&, int, uint64_t, uint64_t, bool);
+
+// ---------------------------------------------------------------- prefix doubling steps
+void dbl_ensure_isa(Index& ix) { ix.isa.ensure(ix.n * (ix.sa_pos64 ? 8 : 4) + 16); }
+
+void dbl_isa_segment(Index& ix, const void* d_sa, uint64_t count, uint64_t lo) {
+  if (!count) return;
+  if (lo + count > ix.n) throw ApiError{-4, "ISA segment out of range"};
+  TimedLaunch tm(ix.timer, "sa_isa_scatter", (double)count * (ix.sa_pos64 ? 16 : 8));
+  if (ix.sa_pos64)
+    k_isa_from_sa<uint64_t><<<grid_for(count), 256, 0, ix.stream>>>(static_cast<const uint64_t*>(d_sa), count, lo,
+                                                                     ix.isa.as<uint64_t>());
+  else
+    k_isa_from_sa<uint32_t><<<grid_for(count), 256, 0, ix.stream>>>(static_cast<const uint32_t*>(d_sa), count, lo,
+                                                                     ix.isa.as<uint32_t>());
+  HK_HIP(hipGetLastError());
+}
+
+void dbl_emit_groups(Index& ix) {
+  auto& st = ix.dbl;
+  const uint64_t A = st.A;
+  uint64_t* pairs = nullptr;
+  if (ix.sharded) {
+    ix.upd.ensure(A * 16 + 16);
+    pairs = ix.upd.as<uint64_t>();
+  }
+  const uint64_t lo = ix.sharded ? ix.shard_lo : 0;
+  if (A) {
+    if (ix.sa_pos64)
+      k_dbl_emit<uint64_t><<<grid_for(A), 256, 0, ix.stream>>>(ix.act[st.cur][0].as<uint64_t>(),
+                                                               ix.act[st.cur][2].as<uint32_t>(), A,
+                                                               ix.head_slot.as<uint32_t>(), lo, ix.isa.as<uint64_t>(),
+                                                               pairs);
+    else
+      k_dbl_emit<uint32_t><<<grid_for(A), 256, 0, ix.stream>>>(ix.act[st.cur][0].as<uint32_t>(),
+                                                               ix.act[st.cur][2].as<uint32_t>(), A,
+                                                               ix.head_slot.as<uint32_t>(), lo, ix.isa.as<uint32_t>(),
+                                                               pairs);
+    HK_HIP(hipGetLastError());
+  }
+  st.npairs = pairs ? A : 0;
+  HK_HIP(hipStreamSynchronize(ix.stream));
+}
+
+void dbl_apply_pairs(Index& ix, const uint64_t* d_pairs, uint64_t count) {
+  if (!count) return;
+  TimedLaunch tm(ix.timer, "sa_isa_update", (double)count * (16 + (ix.sa_pos64 ? 8 : 4)));
+  if (ix.sa_pos64)
+    k_dbl_apply_pairs<uint64_t><<<grid_for(count), 256, 0, ix.stream>>>(d_pairs, count, ix.isa.as<uint64_t>());
+  else
+    k_dbl_apply_pairs<uint32_t><<<grid_for(count), 256, 0, ix.stream>>>(d_pairs, count, ix.isa.as<uint32_t>());
+  HK_HIP(hipGetLastError());
+}
+
+void dbl_round(Index& ix, uint64_t K) {
+  if (!ix.dbl.A) return;
+  if (K == 0) throw ApiError{-1, "prefix doubling: K must be positive"};
+  if (ix.sa_pos64) dbl_round_t<uint64_t>(ix, K);
+  else dbl_round_t<uint32_t>(ix, K);
+}
 
 void pack_keys(const uint8_t* d_text, uint64_t n, uint64_t lo, uint64_t count, const uint16_t* d_lut, uint64_t R,
                int q, int pb, uint64_t* d_keys, hipStream_t s, uint64_t* d_hist0) {
@@ -819,8 +939,10 @@ void build_sa(Index& ix) {
   const uint64_t n = ix.n;
   hipStream_t s = ix.stream;
   if (n >= 0xFFFFFFFFull) throw ApiError{-6, "single-GPU build supports n < 2^32 - 1"};
+  ix.have_alpha = false;   // every build recomputes the byte histogram / C (utils/utils.py:16-24)
   compute_alphabet(ix);
   ix.info.assign(4, 0);
+  ix.dbl = Index::DblState{};
   ix.sharded = false;
   ix.sa_pos64 = false;
   ix.have_sa = ix.have_bwt = ix.have_wt = false;
@@ -895,6 +1017,8 @@ void release_workspace(Index& ix) {
   ix.tile_b.release();
   ix.tile_c.release();
   ix.tile_d.release();
+  ix.tile_e.release();
+  ix.upd.release();
   ix.sw.status.release();
   ix.sw.status_tiles = 0;
   ix.sw.scan_tmp.release();

@@ -21,7 +21,9 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <algorithm>
 #include <cstring>
+#include <string>
 #include <type_traits>
 
 #include "hk_index.hpp"
@@ -672,6 +674,7 @@ void shard_build_t(Index& ix, const uint64_t* ghist, const uint64_t* gbelow, int
   ix.shard_hi = gbelow[rank + 1];
   const uint64_t m = ix.shard_hi - ix.shard_lo;
   ix.info.assign(8, 0);
+  ix.dbl = Index::DblState{};
   ix.sharded = true;
   ix.sa_pos64 = sizeof(V) == 8;
   ix.have_sa = ix.have_bwt = ix.have_wt = false;
@@ -789,7 +792,7 @@ void shard_build_t(Index& ix, const uint64_t* ghist, const uint64_t* gbelow, int
   // LDS bucket sorts over the slice's bins, unless a bucket is too big for them
   if (!global && bucket_sort_slice<V>(ix, kk, m, hb, sbn, d_h0)) {
     HK_HIP(hipStreamSynchronize(s));
-    ix.have_sa = ix.have_bwt = true;
+    ix.have_sa = ix.have_bwt = !ix.dbl.pending;   // pending: the rank exchange finishes the slice
     return;
   }
   ix.info[7] = 1;
@@ -812,8 +815,7 @@ void shard_build_t(Index& ix, const uint64_t* ghist, const uint64_t* gbelow, int
   ix.info[1] += ix.sw.passes_skipped;
   refine_after_sort<V>(ix, kk, slot, m, false);
   HK_HIP(hipStreamSynchronize(s));
-  ix.have_sa = true;
-  ix.have_bwt = true;   // BWT of the slice (bwt[j] for SA[lo + j])
+  ix.have_sa = ix.have_bwt = !ix.dbl.pending;   // BWT of the slice (bwt[j] for SA[lo + j])
 }
 
 }  // namespace
@@ -896,6 +898,153 @@ void shard_get_sa(Index& ix, uint64_t a, uint64_t b, uint64_t* out) {
 
 static ShardComm g_comm;  // one communicator per process (one process per GPU)
 
+namespace {
+
+void comm_abort() {
+  if (g_comm.comm) (void)ncclCommAbort(g_comm.comm);
+  g_comm.comm = nullptr;
+  g_comm.nranks = 0;
+  g_comm.rank = -1;
+}
+
+// an RCCL call that fails tears the communicator down (peers see their own collective fail)
+void nccl_do(ncclResult_t r, const char* what) {
+  if (r != ncclSuccess) {
+    const std::string msg = std::string(what) + ": " + ncclGetErrorString(r);
+    comm_abort();
+    throw ApiError{-8, msg};
+  }
+}
+
+// Per-rank record exchanged after every local step.  A local failure is reported through it, so
+// every rank leaves the collective sequence at the same point instead of blocking in a collective.
+struct RankStatus {
+  uint64_t lo, hi, A, h, npairs, err;
+};
+static_assert(sizeof(RankStatus) == 48, "RankStatus layout");
+
+std::vector<RankStatus> gather_status(Index& ix, const RankStatus& mine, DevBuf& buf) {
+  const int N = g_comm.nranks;
+  hipStream_t s = ix.stream;
+  buf.ensure(sizeof(RankStatus) * N + 64);
+  RankStatus* d = buf.as<RankStatus>();
+  HK_HIP(hipMemcpyAsync(d + g_comm.rank, &mine, sizeof(RankStatus), hipMemcpyHostToDevice, s));
+  {
+    TimedLaunch t(ix.timer, "rccl_allgather_status", (double)N * sizeof(RankStatus));
+    nccl_do(ncclAllGather(d + g_comm.rank, d, sizeof(RankStatus), ncclUint8, g_comm.comm, s), "ncclAllGather");
+  }
+  std::vector<RankStatus> all(N);
+  HK_HIP(hipMemcpyAsync(all.data(), d, sizeof(RankStatus) * N, hipMemcpyDeviceToHost, s));
+  HK_HIP(hipStreamSynchronize(s));
+  for (int r = 0; r < N; ++r)
+    if (all[r].err) {
+      if (r == g_comm.rank) continue;
+      throw ApiError{-8, "sharded build failed on rank " + std::to_string(r) + " (error " +
+                             std::to_string((int64_t)all[r].err) + ")"};
+    }
+  return all;
+}
+
+// Runs f; a failure becomes an error code in the status record (and the message is kept).
+template <typename F>
+uint64_t local_step(F&& f, std::string& emsg, int& ecode) {
+  try {
+    f();
+    return 0;
+  } catch (const ApiError& e) {
+    emsg = e.msg;
+    ecode = e.code;
+  } catch (const HipError& e) {
+    emsg = std::string("HIP error ") + hipGetErrorString(e.code) + " in " + e.where;
+    ecode = -2;
+    (void)hipGetLastError();
+  }
+  return (uint64_t)(int64_t)ecode;
+}
+
+constexpr uint64_t kIsaChunk = 1ull << 26;    // SA entries per rank per all-gather of the ISA build
+constexpr uint64_t kPairChunk = 1ull << 24;   // (position, ISA) pairs per rank per all-gather
+
+// In-place all-gather of per-rank ragged device arrays, CH elements of esz bytes per rank per call:
+// for each chunk, rank r's elements [off, off + cnt_r) land in gb[r*CH .. ) and visit(r, ptr, cnt,
+// off) consumes them.
+template <typename Visit>
+void ragged_allgather(Index& ix, const uint8_t* mine, const std::vector<uint64_t>& cnt, size_t esz, uint64_t CH,
+                      DevBuf& gb, const char* timer, Visit&& visit) {
+  const int N = g_comm.nranks, me = g_comm.rank;
+  hipStream_t s = ix.stream;
+  uint64_t mx = 0;
+  for (uint64_t c : cnt) mx = std::max(mx, c);
+  if (!mx) return;
+  CH = std::min(CH, mx);
+  gb.ensure((size_t)N * CH * esz + 64);
+  uint8_t* base = gb.as<uint8_t>();
+  for (uint64_t off = 0; off < mx; off += CH) {
+    const uint64_t my = cnt[me] > off ? std::min(CH, cnt[me] - off) : 0;
+    if (my) HK_HIP(hipMemcpyAsync(base + (size_t)me * CH * esz, mine + off * esz, my * esz, hipMemcpyDeviceToDevice, s));
+    {
+      TimedLaunch t(ix.timer, timer, (double)N * CH * esz);
+      nccl_do(ncclAllGather(base + (size_t)me * CH * esz, base, CH * esz, ncclUint8, g_comm.comm, s),
+              "ncclAllGather");
+    }
+    for (int r = 0; r < N; ++r) {
+      const uint64_t c = cnt[r] > off ? std::min(CH, cnt[r] - off) : 0;
+      if (c) visit(r, base + (size_t)r * CH * esz, c, off);
+    }
+  }
+}
+
+// Prefix doubling of the slices' tied suffixes with the rank exchange:
+// every rank keeps a replica of the global ISA, built from an all-gather of the SA slices and
+// refreshed after each round by an all-gather of the (position, ISA) pairs of the suffixes that
+// round re-ranked.  K = the smallest common-prefix length of any group still tied anywhere.
+void shard_doubling(Index& ix, std::vector<RankStatus> st, DevBuf& sbuf) {
+  const int N = g_comm.nranks, me = g_comm.rank;
+  const size_t V = ix.sa_pos64 ? 8 : 4;
+  DevBuf gb;
+  dbl_ensure_isa(ix);
+  {
+    std::vector<uint64_t> cnt(N);
+    for (int r = 0; r < N; ++r) cnt[r] = st[r].hi - st[r].lo;
+    ragged_allgather(ix, ix.sa.as<uint8_t>(), cnt, V, kIsaChunk, gb, "rccl_allgather_sa",
+                     [&](int r, const uint8_t* p, uint64_t c, uint64_t off) {
+                       dbl_isa_segment(ix, p, c, st[r].lo + off);
+                     });
+  }
+  for (int round = 0;; ++round) {
+    if (round > 64) throw ApiError{-7, "sharded prefix doubling did not converge"};
+    {
+      std::vector<uint64_t> cnt(N);
+      for (int r = 0; r < N; ++r) cnt[r] = st[r].npairs;
+      ragged_allgather(ix, ix.upd.as<uint8_t>(), cnt, 16, kPairChunk, gb, "rccl_allgather_pairs",
+                       [&](int, const uint8_t* p, uint64_t c, uint64_t) {
+                         dbl_apply_pairs(ix, reinterpret_cast<const uint64_t*>(p), c);
+                       });
+    }
+    uint64_t K = ~0ull;
+    for (int r = 0; r < N; ++r)
+      if (st[r].A) K = std::min(K, st[r].h);
+    std::string emsg;
+    int ecode = 0;
+    const uint64_t err = local_step([&] {
+      if (ix.dbl.A) dbl_round(ix, K);
+      else ix.dbl.npairs = 0;
+      HK_HIP(hipStreamSynchronize(ix.stream));
+    }, emsg, ecode);
+    const RankStatus mine{ix.shard_lo, ix.shard_hi, err ? 0 : ix.dbl.A, ix.dbl.h, err ? 0 : ix.dbl.npairs, err};
+    st = gather_status(ix, mine, sbuf);
+    if (err) throw ApiError{ecode, emsg};
+    uint64_t tot = 0;
+    for (int r = 0; r < N; ++r) tot += st[r].A;
+    if (!tot) break;
+  }
+  (void)me;
+  ix.dbl.pending = false;
+  ix.have_sa = ix.have_bwt = true;
+}
+
+}  // namespace
+
 void build_sa_sharded(Index& ix, const uint8_t id[128], int nranks, int rank) {
   hipStream_t s = ix.stream;
   if (!g_comm.comm || g_comm.nranks != nranks || g_comm.rank != rank || memcmp(g_comm.id, id, 128) != 0) {
@@ -909,47 +1058,194 @@ void build_sa_sharded(Index& ix, const uint8_t id[128], int nranks, int rank) {
     g_comm.rank = rank;
     memcpy(g_comm.id, id, 128);
   }
+  std::string emsg;
+  int ecode = 0;
+  // phase 1: sampled partition histogram; the extra bin carries failures (summed)
   DevBuf hist;
-  hist.ensure(SH_BUCKETS * 8 + 64);
-  shard_histogram(ix, nranks, rank, hist.as<uint64_t>());
+  hist.ensure((SH_BUCKETS + 1) * 8 + 64);
+  uint64_t err = local_step([&] {
+    ix.have_alpha = false;   // every build recomputes the byte histogram / C (utils/utils.py:16-24)
+    shard_histogram(ix, nranks, rank, hist.as<uint64_t>());
+  }, emsg, ecode);
   {
+    const uint64_t e1 = err ? 1 : 0;
+    HK_HIP(hipMemcpyAsync(hist.as<uint64_t>() + SH_BUCKETS, &e1, 8, hipMemcpyHostToDevice, s));
     TimedLaunch t(ix.timer, "rccl_allreduce_hist", (double)SH_BUCKETS * 8);
-    ncclcheck(ncclAllReduce(hist.p, hist.p, SH_BUCKETS, ncclUint64, ncclSum, g_comm.comm, s), "ncclAllReduce");
+    nccl_do(ncclAllReduce(hist.p, hist.p, SH_BUCKETS + 1, ncclUint64, ncclSum, g_comm.comm, s), "ncclAllReduce");
   }
-  std::vector<uint64_t> h(SH_BUCKETS);
-  HK_HIP(hipMemcpyAsync(h.data(), hist.p, SH_BUCKETS * 8, hipMemcpyDeviceToHost, s));
+  std::vector<uint64_t> h(SH_BUCKETS + 1);
+  HK_HIP(hipMemcpyAsync(h.data(), hist.p, (SH_BUCKETS + 1) * 8, hipMemcpyDeviceToHost, s));
   HK_HIP(hipStreamSynchronize(s));
-  // exact slice sizes: per-rank counts below every splitter, summed
-  shard_counts(ix, h.data(), nranks, rank, hist.as<uint64_t>());
+  if (err) throw ApiError{ecode, emsg};
+  if (h[SH_BUCKETS]) throw ApiError{-8, "sharded build failed on a peer rank (histogram)"};
+  // phase 2: exact slice sizes: per-rank counts below every splitter, summed (+ failure slot)
+  err = local_step([&] { shard_counts(ix, h.data(), nranks, rank, hist.as<uint64_t>()); }, emsg, ecode);
   {
-    TimedLaunch t(ix.timer, "rccl_allreduce_counts", (double)(nranks + 1) * 8);
-    ncclcheck(ncclAllReduce(hist.p, hist.p, nranks + 1, ncclUint64, ncclSum, g_comm.comm, s), "ncclAllReduce");
+    const uint64_t e1 = err ? 1 : 0;
+    HK_HIP(hipMemcpyAsync(hist.as<uint64_t>() + nranks + 1, &e1, 8, hipMemcpyHostToDevice, s));
+    TimedLaunch t(ix.timer, "rccl_allreduce_counts", (double)(nranks + 2) * 8);
+    nccl_do(ncclAllReduce(hist.p, hist.p, nranks + 2, ncclUint64, ncclSum, g_comm.comm, s), "ncclAllReduce");
   }
-  std::vector<uint64_t> below(nranks + 1);
-  HK_HIP(hipMemcpyAsync(below.data(), hist.p, (nranks + 1) * 8, hipMemcpyDeviceToHost, s));
+  std::vector<uint64_t> below(nranks + 2);
+  HK_HIP(hipMemcpyAsync(below.data(), hist.p, (nranks + 2) * 8, hipMemcpyDeviceToHost, s));
   HK_HIP(hipStreamSynchronize(s));
-  shard_build(ix, h.data(), below.data(), nranks, rank);
-  // merge: all-gather every rank's slice bounds and check that they tile [0, n)
-  DevBuf bounds;
-  bounds.ensure((size_t)nranks * 16 + 16);
-  uint64_t mine[2] = {ix.shard_lo, ix.shard_hi};
-  HK_HIP(hipMemcpyAsync(bounds.as<uint64_t>() + 2 * rank, mine, 16, hipMemcpyHostToDevice, s));
-  {
-    TimedLaunch t(ix.timer, "rccl_allgather_bounds", (double)nranks * 16);
-    ncclcheck(ncclAllGather(bounds.as<uint64_t>() + 2 * rank, bounds.p, 2, ncclUint64, g_comm.comm, s),
-              "ncclAllGather");
-  }
-  std::vector<uint64_t> all((size_t)nranks * 2);
-  HK_HIP(hipMemcpyAsync(all.data(), bounds.p, nranks * 16, hipMemcpyDeviceToHost, s));
-  HK_HIP(hipStreamSynchronize(s));
-  uint64_t expect = 0;
+  if (err) throw ApiError{ecode, emsg};
+  if (below[nranks + 1]) throw ApiError{-8, "sharded build failed on a peer rank (slice counts)"};
+  // phase 3: the slice sort; then every rank's bounds / tied count are exchanged
+  err = local_step([&] { shard_build(ix, h.data(), below.data(), nranks, rank); }, emsg, ecode);
+  DevBuf sbuf;
+  const RankStatus mine{ix.shard_lo, ix.shard_hi, err ? 0 : ix.dbl.A, ix.dbl.h, err ? 0 : ix.dbl.npairs, err};
+  const std::vector<RankStatus> st = gather_status(ix, mine, sbuf);
+  if (err) throw ApiError{ecode, emsg};
+  uint64_t expect = 0, tied = 0;
   for (int r = 0; r < nranks; ++r) {
-    if (all[2 * r] != expect) throw ApiError{-8, "shard slices do not tile the suffix array"};
-    expect = all[2 * r + 1];
+    if (st[r].lo != expect) throw ApiError{-8, "shard slices do not tile the suffix array"};
+    expect = st[r].hi;
+    tied += st[r].A;
   }
   if (expect != ix.n) throw ApiError{-8, "shard slices do not cover the suffix array"};
+  ix.shard_bounds.resize((size_t)nranks + 1);
+  for (int r = 0; r < nranks; ++r) ix.shard_bounds[r] = st[r].lo;
+  ix.shard_bounds[nranks] = ix.n;
+  // phase 4 (repetitive texts only): prefix doubling with the ISA rank exchange
+  if (tied) shard_doubling(ix, st, sbuf);
 }
 
+// Replicas for batched queries: all-gather every rank's SA slice and BWT rows, so
+// each rank holds the full SA + BWT (and then builds its own wavelet tree).
+void shard_replicate(Index& ix) {
+  if (!ix.sharded || !ix.have_sa) throw ApiError{-3, "replicate: no sharded suffix array"};
+  if (!g_comm.comm || (int)ix.shard_bounds.size() != g_comm.nranks + 1)
+    throw ApiError{-3, "replicate: no communicator of the sharded build"};
+  const int N = g_comm.nranks;
+  const uint64_t n = ix.n;
+  const size_t V = ix.sa_pos64 ? 8 : 4;
+  hipStream_t s = ix.stream;
+  std::vector<uint64_t> cnt(N);
+  for (int r = 0; r < N; ++r) cnt[r] = ix.shard_bounds[r + 1] - ix.shard_bounds[r];
+  DevBuf full_sa, full_bwt, gb;
+  full_sa.ensure(n * V + 16);
+  full_bwt.ensure(n + 64);
+  ragged_allgather(ix, ix.sa.as<uint8_t>(), cnt, V, kIsaChunk, gb, "rccl_allgather_sa",
+                   [&](int r, const uint8_t* p, uint64_t c, uint64_t off) {
+                     HK_HIP(hipMemcpyAsync(full_sa.as<uint8_t>() + (ix.shard_bounds[r] + off) * V, p, c * V,
+                                           hipMemcpyDeviceToDevice, s));
+                   });
+  ragged_allgather(ix, ix.bwt.as<uint8_t>(), cnt, 1, kIsaChunk * 8, gb, "rccl_allgather_bwt",
+                   [&](int r, const uint8_t* p, uint64_t c, uint64_t off) {
+                     HK_HIP(hipMemcpyAsync(full_bwt.as<uint8_t>() + ix.shard_bounds[r] + off, p, c,
+                                           hipMemcpyDeviceToDevice, s));
+                   });
+  HK_HIP(hipStreamSynchronize(s));
+  std::swap(ix.sa, full_sa);
+  std::swap(ix.bwt, full_bwt);
+  ix.sharded = false;
+  ix.shard_lo = 0;
+  ix.shard_hi = n;
+  ix.have_sa = ix.have_bwt = true;
+  ix.have_wt = false;
+}
+
+// Host-assembled replica (hosts running their own collectives): the full SA and BWT.
+void shard_adopt(Index& ix, const uint64_t* h_sa, const uint8_t* h_bwt) {
+  const uint64_t n = ix.n;
+  hipStream_t s = ix.stream;
+  const bool w64 = ix.sa_pos64 || n > 0xFFFFFFFFull;
+  DevBuf full_sa, full_bwt;
+  full_sa.ensure(n * (w64 ? 8 : 4) + 16);
+  full_bwt.ensure(n + 64);
+  if (w64) {
+    HK_HIP(hipMemcpyAsync(full_sa.p, h_sa, n * 8, hipMemcpyHostToDevice, s));
+  } else {
+    std::vector<uint32_t> t(n);
+    for (uint64_t i = 0; i < n; ++i) t[i] = (uint32_t)h_sa[i];
+    HK_HIP(hipMemcpyAsync(full_sa.p, t.data(), n * 4, hipMemcpyHostToDevice, s));
+    HK_HIP(hipStreamSynchronize(s));
+  }
+  HK_HIP(hipMemcpyAsync(full_bwt.p, h_bwt, n, hipMemcpyHostToDevice, s));
+  HK_HIP(hipStreamSynchronize(s));
+  std::swap(ix.sa, full_sa);
+  std::swap(ix.bwt, full_bwt);
+  ix.sa_pos64 = w64;
+  ix.sharded = false;
+  ix.shard_lo = 0;
+  ix.shard_hi = n;
+  ix.dbl = Index::DblState{};
+  ix.have_sa = ix.have_bwt = true;
+  ix.have_wt = false;
+}
+
+// ---------------------------------------------------------------- host-driven rank exchange
+void shard_status(Index& ix, uint64_t st[4]) {
+  if (!ix.sharded) throw ApiError{-3, "index is not sharded"};
+  st[0] = ix.shard_lo;
+  st[1] = ix.shard_hi;
+  st[2] = ix.dbl.A;
+  st[3] = ix.dbl.h;
+}
+
+void shard_isa_segment_host(Index& ix, const uint64_t* h_sa, uint64_t count, uint64_t lo) {
+  if (!ix.sharded || !ix.dbl.pending) throw ApiError{-3, "no pending sharded prefix doubling"};
+  if (lo > ix.n || count > ix.n - lo) throw ApiError{-4, "ISA segment out of range"};
+  if (!count) return;
+  dbl_ensure_isa(ix);
+  DevBuf tmp;
+  const size_t V = ix.sa_pos64 ? 8 : 4;
+  tmp.ensure(count * V + 16);
+  if (ix.sa_pos64) {
+    HK_HIP(hipMemcpyAsync(tmp.p, h_sa, count * 8, hipMemcpyHostToDevice, ix.stream));
+  } else {
+    std::vector<uint32_t> t(count);
+    for (uint64_t i = 0; i < count; ++i) {
+      if (h_sa[i] >= ix.n) throw ApiError{-4, "ISA segment entry out of range"};
+      t[i] = (uint32_t)h_sa[i];
+    }
+    HK_HIP(hipMemcpyAsync(tmp.p, t.data(), count * 4, hipMemcpyHostToDevice, ix.stream));
+    HK_HIP(hipStreamSynchronize(ix.stream));
+  }
+  dbl_isa_segment(ix, tmp.p, count, lo);
+  HK_HIP(hipStreamSynchronize(ix.stream));
+}
+
+uint64_t shard_updates(Index& ix, uint64_t* h_pairs, uint64_t cap) {
+  if (!ix.sharded) throw ApiError{-3, "index is not sharded"};
+  const uint64_t c = ix.dbl.npairs;
+  if (h_pairs && c) {
+    if (cap < c) throw ApiError{-4, "pair buffer too small"};
+    HK_HIP(hipMemcpyAsync(h_pairs, ix.upd.p, c * 16, hipMemcpyDeviceToHost, ix.stream));
+    HK_HIP(hipStreamSynchronize(ix.stream));
+  }
+  return c;
+}
+
+void shard_apply_host(Index& ix, const uint64_t* h_pairs, uint64_t count) {
+  if (!ix.sharded || !ix.dbl.pending) throw ApiError{-3, "no pending sharded prefix doubling"};
+  if (!count) return;
+  for (uint64_t i = 0; i < count; ++i)
+    if (h_pairs[2 * i] >= ix.n || h_pairs[2 * i + 1] >= ix.n) throw ApiError{-4, "ISA pair out of range"};
+  dbl_ensure_isa(ix);
+  DevBuf tmp;
+  tmp.ensure(count * 16 + 16);
+  HK_HIP(hipMemcpyAsync(tmp.p, h_pairs, count * 16, hipMemcpyHostToDevice, ix.stream));
+  dbl_apply_pairs(ix, tmp.as<uint64_t>(), count);
+  HK_HIP(hipStreamSynchronize(ix.stream));
+}
+
+void shard_round(Index& ix, uint64_t K) {
+  if (!ix.sharded || !ix.dbl.pending) throw ApiError{-3, "no pending sharded prefix doubling"};
+  if (!ix.dbl.A) {   // already final: nothing to sort, no pairs
+    ix.dbl.npairs = 0;
+    return;
+  }
+  if (!ix.isa.p) throw ApiError{-3, "ISA replica not loaded (hkcsa_shard_isa_segment)"};
+  if (ix.dbl.A) dbl_round(ix, K);
+  else ix.dbl.npairs = 0;
+  HK_HIP(hipStreamSynchronize(ix.stream));
+  if (!ix.dbl.A) ix.have_sa = ix.have_bwt = true;   // this slice is final (peers may still need its pairs)
+}
+
+// the last round of every rank: the host calls hkcsa_shard_round until all ranks report A = 0;
+// a rank's slice is final as soon as its own A is 0
 void comm_unique_id(uint8_t id[128]) {
   ncclUniqueId uid;
   ncclcheck(ncclGetUniqueId(&uid), "ncclGetUniqueId");

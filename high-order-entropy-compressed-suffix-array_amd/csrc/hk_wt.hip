@@ -175,7 +175,8 @@ __global__ __launch_bounds__(256) void k_rank(WtView v, const uint8_t* __restric
 
 constexpr uint64_t kSmallOcc = 32;
 
-__global__ __launch_bounds__(256) void k_locate_small(const uint32_t* __restrict__ sa,
+template <typename S>
+__global__ __launch_bounds__(256) void k_locate_small(const S* __restrict__ sa,
                                                       const int64_t* __restrict__ lr,
                                                       const uint64_t* __restrict__ oo, uint64_t P,
                                                       uint64_t* __restrict__ pos, uint64_t* big,
@@ -193,7 +194,8 @@ __global__ __launch_bounds__(256) void k_locate_small(const uint32_t* __restrict
   }
 }
 
-__global__ __launch_bounds__(256) void k_locate_big(const uint32_t* __restrict__ sa,
+template <typename S>
+__global__ __launch_bounds__(256) void k_locate_big(const S* __restrict__ sa,
                                                     const int64_t* __restrict__ lr,
                                                     const uint64_t* __restrict__ oo,
                                                     const uint64_t* __restrict__ big,
@@ -218,6 +220,7 @@ inline unsigned grid_for(uint64_t n, unsigned per = 256, unsigned cap = 16384) {
 
 void build_wt(Index& ix) {
   if (!ix.have_bwt) throw ApiError{-3, "build_wt: BWT not built"};
+  if (ix.sharded) throw ApiError{-3, "build_wt: a sharded index holds only a slice of the BWT"};
   compute_alphabet(ix);
   hipStream_t s = ix.stream;
   const uint64_t n = ix.n;
@@ -310,7 +313,7 @@ void build_wt(Index& ix) {
 
 void query_count(Index& ix, const uint8_t* d_pats, const uint64_t* d_offs, uint64_t P, int64_t* d_lr,
                  uint64_t* d_cnt) {
-  if (!ix.have_wt) throw ApiError{-3, "count: wavelet tree not built"};
+  if (!ix.have_wt || ix.sharded) throw ApiError{-3, "count: wavelet tree not built"};
   if (!P) return;
   TimedLaunch t(ix.timer, "fm_count", 0.0);
   k_count<<<grid_for(P, 256, 65535), 256, 0, ix.stream>>>(ix.view(), d_pats, d_offs, P, d_lr, d_cnt);
@@ -328,11 +331,19 @@ void query_locate_gather(Index& ix, const int64_t* d_lr, const uint64_t* d_occ_o
   unsigned long long* nbig = ix.small.as<unsigned long long>() + 512;   // byte 4096: clear of the build LUTs
   HK_HIP(hipMemsetAsync(nbig, 0, 8, s));
   TimedLaunch t(ix.timer, "fm_locate", 0.0);
-  k_locate_small<<<grid_for(P, 256, 65535), 256, 0, s>>>(ix.sa.as<uint32_t>(), d_lr, d_occ_offs, P, d_pos,
-                                                         ix.tile_c.as<uint64_t>(), nbig);
-  HK_HIP(hipGetLastError());
-  k_locate_big<<<1024, 256, 0, s>>>(ix.sa.as<uint32_t>(), d_lr, d_occ_offs, ix.tile_c.as<uint64_t>(), nbig,
-                                    d_pos);
+  if (ix.sa_pos64) {   // replicated sharded SA of a text with n >= 2^32
+    k_locate_small<uint64_t><<<grid_for(P, 256, 65535), 256, 0, s>>>(ix.sa.as<uint64_t>(), d_lr, d_occ_offs, P,
+                                                                     d_pos, ix.tile_c.as<uint64_t>(), nbig);
+    HK_HIP(hipGetLastError());
+    k_locate_big<uint64_t><<<1024, 256, 0, s>>>(ix.sa.as<uint64_t>(), d_lr, d_occ_offs, ix.tile_c.as<uint64_t>(),
+                                                nbig, d_pos);
+  } else {
+    k_locate_small<uint32_t><<<grid_for(P, 256, 65535), 256, 0, s>>>(ix.sa.as<uint32_t>(), d_lr, d_occ_offs, P,
+                                                                     d_pos, ix.tile_c.as<uint64_t>(), nbig);
+    HK_HIP(hipGetLastError());
+    k_locate_big<uint32_t><<<1024, 256, 0, s>>>(ix.sa.as<uint32_t>(), d_lr, d_occ_offs, ix.tile_c.as<uint64_t>(),
+                                                nbig, d_pos);
+  }
   HK_HIP(hipGetLastError());
 }
 

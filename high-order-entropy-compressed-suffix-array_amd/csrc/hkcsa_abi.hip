@@ -144,6 +144,7 @@ int hkcsa_build_bwt(hkcsa_index* h) {
 int hkcsa_build_wt(hkcsa_index* h) {
   return guarded([&] {
     activate(h);
+    need(!h->ix.sharded, HKCSA_E_STATE, "sharded index holds only a slice: hkcsa_shard_replicate first");
     if (h->ix.bwt_in_wt) return;   // compacted: the WT is the only copy of the BWT
     hk::build_wt(h->ix);
   });
@@ -179,6 +180,8 @@ int hkcsa_entropy(hkcsa_index* h, int k, double* out) {
   return guarded([&] {
     activate(h);
     need(out != nullptr, HKCSA_E_INVALID, "null output");
+    need(h->ix.have_text || k <= 0, HKCSA_E_STATE, "text released by hkcsa_compact");
+    need(!h->ix.sharded || k <= 0, HKCSA_E_STATE, "sharded index holds only a slice");
     *out = hk::entropy_k(h->ix, k);
   });
 }
@@ -283,6 +286,11 @@ int hkcsa_get_sa(hkcsa_index* h, uint64_t lo, uint64_t hi, uint64_t* out) {
       HK_HIP(hipStreamSynchronize(h->ix.stream));
       return;
     }
+    if (h->ix.sa_pos64) {   // replicated sharded SA of a text with n >= 2^32
+      HK_HIP(hipMemcpyAsync(out, h->ix.sa.as<uint64_t>() + lo, c * 8, hipMemcpyDeviceToHost, h->ix.stream));
+      HK_HIP(hipStreamSynchronize(h->ix.stream));
+      return;
+    }
     std::vector<uint32_t> tmp(c);
     HK_HIP(hipMemcpyAsync(tmp.data(), h->ix.sa.as<uint32_t>() + lo, c * 4, hipMemcpyDeviceToHost, h->ix.stream));
     HK_HIP(hipStreamSynchronize(h->ix.stream));
@@ -293,7 +301,7 @@ int hkcsa_get_sa(hkcsa_index* h, uint64_t lo, uint64_t hi, uint64_t* out) {
 int hkcsa_get_bwt(hkcsa_index* h, uint64_t lo, uint64_t hi, uint8_t* out) {
   return guarded([&] {
     activate(h);
-    need(h->ix.have_bwt, HKCSA_E_STATE, "BWT not built");
+    need(h->ix.have_bwt && !h->ix.sharded, HKCSA_E_STATE, "BWT not built (a sharded index holds only a slice)");
     need(lo <= hi && hi <= h->ix.n, HKCSA_E_RANGE, "BWT range out of bounds");
     if (hi == lo) return;
     need(out != nullptr, HKCSA_E_INVALID, "null output");
@@ -400,7 +408,7 @@ int hkcsa_wt_golomb(hkcsa_index* h, int depth, uint64_t nbits, uint32_t m_overri
 int hkcsa_rank(hkcsa_index* h, const uint8_t* c, const uint64_t* i, uint64_t count, uint64_t* out) {
   return guarded([&] {
     activate(h);
-    need(h->ix.have_wt, HKCSA_E_STATE, "wavelet tree not built");
+    need(h->ix.have_wt && !h->ix.sharded, HKCSA_E_STATE, "wavelet tree not built");
     if (!count) return;
     need(c && i && out, HKCSA_E_INVALID, "null argument");
     hk::DevBuf dc, di, dout;
@@ -451,6 +459,7 @@ int hkcsa_queries_count(hkcsa_index* h, hkcsa_queries* q) {
   return guarded([&] {
     activate(h);
     need(q != nullptr, HKCSA_E_INVALID, "null query set");
+    need(!h->ix.sharded, HKCSA_E_STATE, "sharded index holds only a slice");
     hk::query_count(h->ix, q->pats.as<uint8_t>(), q->offs.as<uint64_t>(), q->P, q->lr.as<int64_t>(),
                     q->cnt.as<uint64_t>());
     q->have_lr = true;
@@ -462,6 +471,7 @@ int hkcsa_queries_locate(hkcsa_index* h, hkcsa_queries* q, uint64_t* total) {
   return guarded([&] {
     activate(h);
     need(q != nullptr, HKCSA_E_INVALID, "null query set");
+    need(!h->ix.sharded, HKCSA_E_STATE, "sharded index holds only a slice");
     hipStream_t s = h->ix.stream;
     hk::query_count(h->ix, q->pats.as<uint8_t>(), q->offs.as<uint64_t>(), q->P, q->lr.as<int64_t>(),
                     q->cnt.as<uint64_t>());
@@ -544,6 +554,7 @@ int hkcsa_shard_histogram(hkcsa_index* h, int nranks, int rank, uint64_t* hist_o
     activate(h);
     need(h->ix.have_text, HKCSA_E_STATE, "text released by hkcsa_compact");
     need(hist_out != nullptr && nranks >= 1 && rank >= 0 && rank < nranks, HKCSA_E_INVALID, "bad arguments");
+    h->ix.have_alpha = false;   // phase 1 of a build: recompute the byte histogram
     const int nb = hk::shard_buckets();
     hk::DevBuf d;
     d.ensure((size_t)nb * 8);
@@ -582,7 +593,7 @@ int hkcsa_shard_build(hkcsa_index* h, const uint64_t* global_hist, const uint64_
 int hkcsa_get_shard_sa(hkcsa_index* h, uint64_t a, uint64_t b, uint64_t* out) {
   return guarded([&] {
     activate(h);
-    need(h->ix.sharded && h->ix.have_sa, HKCSA_E_STATE, "no sharded suffix array");
+    need(h->ix.sharded && (h->ix.have_sa || h->ix.dbl.pending), HKCSA_E_STATE, "no sharded suffix array");
     need(a == b || out != nullptr, HKCSA_E_INVALID, "null output");
     hk::shard_get_sa(h->ix, a, b, out);
   });
@@ -594,6 +605,61 @@ int hkcsa_get_shard_bwt(hkcsa_index* h, uint64_t a, uint64_t b, uint8_t* out) {
     need(h->ix.sharded && h->ix.have_bwt, HKCSA_E_STATE, "no sharded BWT");
     need(a == b || out != nullptr, HKCSA_E_INVALID, "null output");
     hk::shard_get_bwt(h->ix, a, b, out);
+  });
+}
+
+int hkcsa_shard_replicate(hkcsa_index* h) {
+  return guarded([&] {
+    activate(h);
+    hk::shard_replicate(h->ix);
+  });
+}
+
+int hkcsa_shard_adopt(hkcsa_index* h, const uint64_t* sa, const uint8_t* bwt) {
+  return guarded([&] {
+    activate(h);
+    need(sa && bwt, HKCSA_E_INVALID, "null argument");
+    need(h->ix.have_text, HKCSA_E_STATE, "text released by hkcsa_compact");
+    for (uint64_t i = 0; i < h->ix.n; ++i) need(sa[i] < h->ix.n, HKCSA_E_RANGE, "suffix array entry out of range");
+    hk::shard_adopt(h->ix, sa, bwt);
+  });
+}
+
+int hkcsa_shard_status(hkcsa_index* h, uint64_t st[4]) {
+  return guarded([&] {
+    need(h && st, HKCSA_E_INVALID, "null argument");
+    hk::shard_status(h->ix, st);
+  });
+}
+
+int hkcsa_shard_isa_segment(hkcsa_index* h, const uint64_t* sa, uint64_t count, uint64_t lo) {
+  return guarded([&] {
+    activate(h);
+    need(count == 0 || sa != nullptr, HKCSA_E_INVALID, "null argument");
+    hk::shard_isa_segment_host(h->ix, sa, count, lo);
+  });
+}
+
+int hkcsa_shard_updates(hkcsa_index* h, uint64_t* pairs, uint64_t cap, uint64_t* count) {
+  return guarded([&] {
+    activate(h);
+    need(count != nullptr, HKCSA_E_INVALID, "null argument");
+    *count = hk::shard_updates(h->ix, pairs, cap);
+  });
+}
+
+int hkcsa_shard_apply(hkcsa_index* h, const uint64_t* pairs, uint64_t count) {
+  return guarded([&] {
+    activate(h);
+    need(count == 0 || pairs != nullptr, HKCSA_E_INVALID, "null argument");
+    hk::shard_apply_host(h->ix, pairs, count);
+  });
+}
+
+int hkcsa_shard_round(hkcsa_index* h, uint64_t K) {
+  return guarded([&] {
+    activate(h);
+    hk::shard_round(h->ix, K);
   });
 }
 

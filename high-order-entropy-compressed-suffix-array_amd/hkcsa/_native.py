@@ -80,6 +80,13 @@ _SIGS = [
     ("hkcsa_shard_sample", C.c_int, []),
     ("hkcsa_shard_counts", C.c_int, [vp, vp, C.c_int, C.c_int, vp]),
     ("hkcsa_shard_build", C.c_int, [vp, vp, vp, C.c_int, C.c_int]),
+    ("hkcsa_shard_status", C.c_int, [vp, vp]),
+    ("hkcsa_shard_isa_segment", C.c_int, [vp, vp, C.c_uint64, C.c_uint64]),
+    ("hkcsa_shard_updates", C.c_int, [vp, vp, C.c_uint64, u64p]),
+    ("hkcsa_shard_apply", C.c_int, [vp, vp, C.c_uint64]),
+    ("hkcsa_shard_round", C.c_int, [vp, C.c_uint64]),
+    ("hkcsa_shard_replicate", C.c_int, [vp]),
+    ("hkcsa_shard_adopt", C.c_int, [vp, vp, vp]),
     ("hkcsa_key_geometry", C.c_int, [vp, C.POINTER(C.c_int), C.POINTER(C.c_int), u64p, C.POINTER(C.c_int)]),
     ("hkcsa_debug_radix_bench", C.c_int, [C.c_uint64, C.c_int, vp, C.c_int]),
     ("hkcsa_timing_enable", C.c_int, [vp, C.c_int]),

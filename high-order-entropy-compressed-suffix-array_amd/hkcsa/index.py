@@ -287,6 +287,44 @@ class DeviceIndex:
         N.check(self.lib.hkcsa_shard_range(self.h, C.byref(lo), C.byref(hi)))
         return lo.value, hi.value
 
+    def shard_status(self) -> tuple[int, int, int, int]:
+        """(lo, hi, tied suffixes left in the slice, their common-prefix length)."""
+        st = np.zeros(4, dtype=np.uint64)
+        N.check(self.lib.hkcsa_shard_status(self.h, _ptr(st)))
+        return tuple(int(x) for x in st)
+
+    def shard_isa_segment(self, sa_segment: np.ndarray, lo: int):
+        """Load ISA[sa_segment[j]] = lo + j into this rank's ISA replica (one call per rank slice)."""
+        a = np.ascontiguousarray(sa_segment, dtype=np.uint64)
+        N.check(self.lib.hkcsa_shard_isa_segment(self.h, _ptr(a) if len(a) else None, len(a), int(lo)))
+
+    def shard_updates(self) -> np.ndarray:
+        """(position, ISA) pairs of the last build / doubling step of this rank, shape (k, 2)."""
+        c = C.c_uint64(0)
+        N.check(self.lib.hkcsa_shard_updates(self.h, None, 0, C.byref(c)))
+        out = np.empty((max(1, c.value), 2), dtype=np.uint64)
+        N.check(self.lib.hkcsa_shard_updates(self.h, _ptr(out), c.value, C.byref(c)))
+        return out[:c.value]
+
+    def shard_apply(self, pairs: np.ndarray):
+        p = np.ascontiguousarray(pairs, dtype=np.uint64).reshape(-1, 2)
+        N.check(self.lib.hkcsa_shard_apply(self.h, _ptr(p) if len(p) else None, len(p)))
+
+    def shard_round(self, K: int):
+        N.check(self.lib.hkcsa_shard_round(self.h, int(K)))
+
+    def shard_replicate(self):
+        """RCCL all-gather of every rank's SA slice and BWT rows: this handle becomes a full index."""
+        N.check(self.lib.hkcsa_shard_replicate(self.h))
+
+    def shard_adopt(self, sa: np.ndarray, bwt: np.ndarray):
+        """Host-assembled replica: the full SA and BWT (hosts running their own collectives)."""
+        s = np.ascontiguousarray(sa, dtype=np.uint64)
+        b = np.ascontiguousarray(bwt, dtype=np.uint8)
+        if len(s) != self.n or len(b) != self.n:
+            raise ValueError("shard_adopt needs n SA entries and n BWT bytes")
+        N.check(self.lib.hkcsa_shard_adopt(self.h, _ptr(s), _ptr(b)))
+
     def shard_sa(self) -> np.ndarray:
         lo, hi = self.shard_range()
         out = np.empty(max(1, hi - lo), dtype=np.uint64)

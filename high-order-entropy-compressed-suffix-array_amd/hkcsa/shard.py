@@ -1,27 +1,37 @@
 """Host orchestration of the sharded suffix-array build (see csrc/hk_shard.hip).
 
 The native entry point hkcsa_build_sa_sharded does the whole exchange itself over
-RCCL.  This module is the three-phase variant for hosts that run their own
-collectives (torch.distributed over RCCL or gloo):
+RCCL.  This module is the host-driven variant for hosts that run their own
+collectives (torch.distributed over RCCL or gloo) and for ranks emulated on one GPU:
 
     h = dev.shard_histogram(N, r)            # sampled 14-bit key-prefix histogram of the block
     g = allreduce_sum(h)                     # collective 1: 16384 u64
     c = dev.shard_counts(g, N, r)            # block suffixes below each splitter
     G = allreduce_sum(c)                     # collective 2: N+1 u64 -> exact slice bounds
-    dev.shard_build(g, G, N, r)              # independent slice sort + refinement
+    dev.shard_build(g, G, N, r)              # independent slice sort + chunk refinement
+    shard_doubling(dev, r, allgather)        # repetitive texts only: prefix doubling with the
+                                             # ISA rank exchange
 
 split_buckets() restates the splitter rule of hk_shard.hip (splitters): B_r is the first
 bucket whose sampled prefix count reaches floor(S*r/N), S = the sample total; rank r
 owns buckets [B_r, B_{r+1}) and its SA slice is [G[r], G[r+1]).
+
+Prefix doubling across slices.  A slice whose tied groups survive the chunk refinement
+(long repeats / runs) stops with its groups pending (hkcsa_shard_status: A tied suffixes
+sharing their first h symbols).  Every pending rank then loads a replica of the global ISA
+from all ranks' SA slices (a tied suffix's ISA is the slot of its group head, sent as
+(position, ISA) pairs), and each round sorts its groups by ISA[p + h] at K = the smallest h
+of any pending rank, after which the re-ranked suffixes' pairs are exchanged again.
 """
 from __future__ import annotations
 
-from typing import Callable
+from typing import Callable, Sequence
 
 import numpy as np
 
 SH_BUCKETS = 1 << 14
 SH_SAMPLE = 16
+MAX_ROUNDS = 64
 
 
 def split_buckets(global_hist, nranks: int) -> list[int]:
@@ -40,13 +50,82 @@ def slice_bounds(global_below, nranks: int) -> list[tuple[int, int]]:
     return [(g[r], g[r + 1]) for r in range(nranks)]
 
 
-def sharded_build(dev, nranks: int, rank: int, allreduce_sum: Callable[[np.ndarray], np.ndarray]):
-    """Three-phase sharded SA build; returns this rank's (lo, hi) slice of the SA."""
+def _min_level(status) -> int:
+    return min(int(s[3]) for s in status if int(s[2]) > 0)
+
+
+def shard_doubling(dev, rank: int, allgather: Callable[[np.ndarray], Sequence[np.ndarray]]) -> int:
+    """Finish this rank's slice after shard_build (collective: every rank calls it).
+
+    allgather(a) returns the list of every rank's array (arrays may differ in length).
+    Returns the number of doubling rounds run (0 when no slice had ties left)."""
+    st = allgather(np.array(dev.shard_status(), dtype=np.uint64))
+    if sum(int(s[2]) for s in st) == 0:
+        return 0
+    active = int(st[rank][2]) > 0
+    segs = allgather(dev.shard_sa())
+    if active:
+        for r, seg in enumerate(segs):
+            dev.shard_isa_segment(seg, int(st[r][0]))
+    pairs = allgather(dev.shard_updates())
+    rounds = 0
+    while True:
+        if rounds >= MAX_ROUNDS:
+            raise RuntimeError("sharded prefix doubling did not converge")
+        if active:
+            for p in pairs:
+                dev.shard_apply(p)
+        K = _min_level(st)
+        if active:
+            dev.shard_round(K)
+        rounds += 1
+        st = allgather(np.array(dev.shard_status(), dtype=np.uint64))
+        if sum(int(s[2]) for s in st) == 0:
+            return rounds
+        pairs = allgather(dev.shard_updates())
+        active = int(st[rank][2]) > 0
+
+
+def emulated_doubling(devs: Sequence) -> int:
+    """shard_doubling for N ranks emulated in one process (devs[r] = rank r's handle)."""
+    st = [d.shard_status() for d in devs]
+    if sum(s[2] for s in st) == 0:
+        return 0
+    segs = [d.shard_sa() for d in devs]
+    for d, s in zip(devs, st):
+        if s[2] > 0:
+            for r, seg in enumerate(segs):
+                d.shard_isa_segment(seg, st[r][0])
+    pairs = [d.shard_updates() for d in devs]
+    rounds = 0
+    while True:
+        if rounds >= MAX_ROUNDS:
+            raise RuntimeError("sharded prefix doubling did not converge")
+        K = _min_level(st)
+        for d, s in zip(devs, st):
+            if s[2] > 0:
+                for p in pairs:
+                    d.shard_apply(p)
+        for d, s in zip(devs, st):
+            if s[2] > 0:
+                d.shard_round(K)
+        rounds += 1
+        st = [d.shard_status() for d in devs]
+        if sum(s[2] for s in st) == 0:
+            return rounds
+        pairs = [d.shard_updates() for d in devs]
+
+
+def sharded_build(dev, nranks: int, rank: int, allreduce_sum: Callable[[np.ndarray], np.ndarray],
+                  allgather: Callable[[np.ndarray], Sequence[np.ndarray]] | None = None):
+    """Host-driven sharded SA build; returns this rank's (lo, hi) slice of the SA."""
     h = dev.shard_histogram(nranks, rank)
     g = allreduce_sum(h)
     c = dev.shard_counts(g, nranks, rank)
     below = allreduce_sum(c)
     dev.shard_build(g, below, nranks, rank)
+    if allgather is not None:
+        shard_doubling(dev, rank, allgather)
     return dev.shard_range()
 
 
@@ -58,4 +137,15 @@ def torch_allreduce_sum(group=None) -> Callable[[np.ndarray], np.ndarray]:
         t = torch.from_numpy(np.asarray(h, dtype=np.int64).copy())
         dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
         return t.numpy().astype(np.uint64)
+    return f
+
+
+def torch_allgather(group=None) -> Callable[[np.ndarray], list[np.ndarray]]:
+    """Variable-length all-gather of numpy arrays over torch.distributed (gloo / RCCL host path)."""
+    import torch.distributed as dist
+
+    def f(a: np.ndarray) -> list[np.ndarray]:
+        out = [None] * dist.get_world_size(group)
+        dist.all_gather_object(out, np.asarray(a), group=group)
+        return out
     return f

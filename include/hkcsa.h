@@ -74,10 +74,16 @@ int hkcsa_create(const uint8_t* text, uint64_t n, const hkcsa_opts* o, hkcsa_ind
  * oracle/hkcsa_oracle.c:oracle_synth_text. (bench input, no reference twin) */
 int hkcsa_create_synthetic(uint64_t n, const uint8_t* alphabet, int sigma, uint64_t seed,
                            uint8_t terminator, const hkcsa_opts* o, hkcsa_index** out);
-/* Suffix array by GPU prefix doubling.  Replaces build_suffix_array
- * (csa/suffix_array.py:131-134) on T'. */
+/* Suffix array of T'.  Replaces build_suffix_array (csa/suffix_array.py:131-134).
+ * Default: keyed bucket build (LSD radix passes over the bucket bits of q-symbol
+ * suffix keys, LDS bucket sorts that write SA and BWT together, chunk refinement
+ * of tied suffixes, GPU prefix doubling over an ISA for texts whose ties persist);
+ * HKCSA_FLAG_GLOBAL_SORT: full-width LSD sort of the keys instead of bucket sorts.
+ * Recomputes the byte histogram / C array every call. */
 int hkcsa_build_sa(hkcsa_index* ix);
-/* BWT gather over SA.  Replaces bwt_transform (csa/bwt.py:3-13). */
+/* BWT of T' (bwt_transform, csa/bwt.py:3-13).  The SA build already writes the
+ * BWT in sorted order, so this is a no-op after hkcsa_build_sa; it gathers
+ * T'[SA[i]-1] only when the SA came without its BWT. */
 int hkcsa_build_bwt(hkcsa_index* ix);
 /* C array + levelwise wavelet tree over the BWT with interleaved rank lines.
  * Replaces build_count (utils/utils.py:16-24), build_occ (utils/utils.py:26-32)
@@ -177,10 +183,25 @@ int hkcsa_comm_unique_id(uint8_t id[128]);
 /* Each rank holds the same T' (created on its own device).  Ranks split the
  * final SA into contiguous rank ranges by a shared sampled key histogram (RCCL
  * all-reduce), fix the exact slice sizes with a second all-reduce of N+1 counts,
- * and sort their slice independently; the slice bounds are checked with an RCCL
- * all-gather.  After the call ix holds SA[lo:hi) (and its BWT rows). */
+ * and sort their slice independently; an RCCL all-gather of per-rank status
+ * records checks that the slices tile [0, n).  Slices still tied after the chunk
+ * refinement finish by prefix doubling with an ISA replica per rank, built by an
+ * RCCL all-gather of the SA slices and refreshed per round by an all-gather of the
+ * re-ranked suffixes' (position, ISA) pairs.  A failure on any rank makes every
+ * rank return an error (no rank is left waiting in a collective).  After the call
+ * ix holds SA[lo:hi) (and its BWT rows). */
 int hkcsa_build_sa_sharded(hkcsa_index* ix, const uint8_t id[128], int nranks, int rank);
 int hkcsa_shard_range(hkcsa_index* ix, uint64_t* lo, uint64_t* hi);
+/* Replicas for batched queries (count/locate are replicas-only):
+ * hkcsa_shard_replicate: RCCL all-gather (communicator of the last
+ *   hkcsa_build_sa_sharded) of every rank's SA slice and BWT rows; afterwards the
+ *   handle is a full index (hkcsa_build_wt, queries, hkcsa_get_sa/bwt work).
+ *   Collective: every rank calls it.  Serves EnhancedFMIndex.find / find_range
+ *   (csa/enhanced_fm_index.py:15-32) on every rank.
+ * hkcsa_shard_adopt: the same from a host-assembled full SA (n entries) and BWT
+ *   (n bytes), for hosts running their own collectives. */
+int hkcsa_shard_replicate(hkcsa_index* ix);
+int hkcsa_shard_adopt(hkcsa_index* ix, const uint64_t* sa, const uint8_t* bwt);
 /* Sharded SA slice entries SA[lo+a : lo+b) (a,b relative to the slice). */
 int hkcsa_get_shard_sa(hkcsa_index* ix, uint64_t a, uint64_t b, uint64_t* out);
 /* BWT of the slice: out[j] = T'[SA[lo+a+j]-1] (wrapping), j < b-a — the rows
@@ -203,6 +224,28 @@ int hkcsa_shard_counts(hkcsa_index* ix, const uint64_t* global_hist, int nranks,
                        uint64_t* below_out);
 int hkcsa_shard_build(hkcsa_index* ix, const uint64_t* global_hist, const uint64_t* global_below,
                       int nranks, int rank);
+/* Prefix doubling across slices, host-driven (hkcsa_build_sa_sharded runs the
+ * same steps over RCCL).  The SA must be exact for every text
+ * (csa/suffix_array.py:131-134); a slice whose tied groups survive the chunk
+ * refinement (long repeats / runs) is left pending after hkcsa_shard_build:
+ *   hkcsa_shard_status: st = {lo, hi, A = tied suffixes left, h = common-prefix
+ *     length of their groups}; A = 0 means the slice is final;
+ *   hkcsa_shard_isa_segment: ISA replica: isa[sa[j]] = lo + j for one rank's
+ *     slice (its hkcsa_get_shard_sa entries, readable while pending); call once
+ *     per rank slice on every pending rank;
+ *   hkcsa_shard_updates: the (position, ISA) pairs (2 u64 each) of this rank's
+ *     last step — the tied suffixes at their group head's slot after the build,
+ *     every re-ranked suffix after a round; NULL pairs: count only;
+ *   hkcsa_shard_apply: isa[p] = v for pairs of any rank (every rank's, own included);
+ *   hkcsa_shard_round: one doubling round: each tied group sorted by ISA[p+h],
+ *     h += K, where K = min h over the ranks with A > 0.
+ * Loop: segments -> {updates of all ranks -> apply -> round(K) -> status} until
+ * every rank reports A = 0 (hkcsa/shard.py shard_doubling). */
+int hkcsa_shard_status(hkcsa_index* ix, uint64_t st[4]);
+int hkcsa_shard_isa_segment(hkcsa_index* ix, const uint64_t* sa, uint64_t count, uint64_t lo);
+int hkcsa_shard_updates(hkcsa_index* ix, uint64_t* pairs, uint64_t cap, uint64_t* count);
+int hkcsa_shard_apply(hkcsa_index* ix, const uint64_t* pairs, uint64_t count);
+int hkcsa_shard_round(hkcsa_index* ix, uint64_t K);
 
 /* Suffix-key geometry chosen for this text (parity export for the shard tests):
  * q symbols as a radix-`radix` number above a pb-bit preceding-symbol field. */

@@ -47,18 +47,98 @@ class OracleShardDevice:
         return self.lo, self.hi
 
 
-def _worker(rank, world, port, n, q):
+class DoublingShardDevice(OracleShardDevice):
+    """Adds a CPU model of the sharded prefix-doubling steps (hk_sa.hip k_dbl_*, hk_shard.hip):
+    shard_build stops with the slice's suffixes grouped only by their first h0 symbols (members of
+    a group in scrambled order, as after the chunk refinement), and every round sorts each group by
+    ISA[p + h] from the rank's ISA replica, exactly as the GPU rounds do."""
+
+    def __init__(self, text: np.ndarray, h0: int):
+        super().__init__(text)
+        self.h0 = h0
+
+    def _share(self, a, b, h):
+        t, n = self.t, self.n
+        if a + h > n or b + h > n:
+            return a == b
+        return bytes(t[a:a + h]) == bytes(t[b:b + h])
+
+    def shard_build(self, g, below, nranks, rank):
+        super().shard_build(g, below, nranks, rank)
+        sl = [int(x) for x in self.slice]
+        groups, i = [], 0
+        while i < len(sl):
+            j = i + 1
+            while j < len(sl) and self._share(sl[i], sl[j], self.h0):
+                j += 1
+            groups.append((i, j))
+            i = j
+        self.sa = list(sl)
+        for a, b in groups:          # unspecified order inside a tied group
+            self.sa[a:b] = self.sa[a:b][::-1]
+        self.groups = [(a, b) for a, b in groups if b - a > 1]
+        self.h = self.h0
+        self.isa = None
+        self.pairs = [(self.sa[j], self.lo + a) for a, b in self.groups for j in range(a, b)]
+
+    def shard_status(self):
+        return (self.lo, self.hi, sum(b - a for a, b in self.groups), self.h)
+
+    def shard_sa(self):
+        return np.array(self.sa, dtype=np.uint64)
+
+    def shard_isa_segment(self, seg, lo):
+        if self.isa is None:
+            self.isa = np.zeros(self.n, dtype=np.int64)
+        self.isa[np.asarray(seg, dtype=np.int64)] = lo + np.arange(len(seg))
+
+    def shard_updates(self):
+        return np.array(self.pairs, dtype=np.uint64).reshape(-1, 2)
+
+    def shard_apply(self, pairs):
+        for p, v in np.asarray(pairs, dtype=np.int64).reshape(-1, 2):
+            self.isa[p] = v
+
+    def shard_round(self, K):
+        n, h = self.n, self.h
+        new_groups, self.pairs = [], []
+        for a, b in self.groups:
+            mem = sorted(self.sa[a:b], key=lambda p: int(self.isa[p + h]) + 1 if p + h < n else 0)
+            self.sa[a:b] = mem
+            key = [int(self.isa[p + h]) + 1 if p + h < n else 0 for p in mem]
+            i = 0
+            while i < len(mem):
+                j = i + 1
+                while j < len(mem) and key[j] == key[i]:
+                    j += 1
+                self.pairs += [(mem[k], self.lo + a + i) for k in range(i, j)]
+                if j - i > 1:
+                    new_groups.append((a + i, a + j))
+                i = j
+        self.groups = new_groups
+        self.h += K
+        self.slice = np.array(self.sa, dtype=np.uint64)
+
+
+def _worker(rank, world, port, n, q, kind="iid"):
     for p in (PKG, ROOT):
         sys.path.insert(0, p)
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     import torch
-    from hkcsa.shard import sharded_build, torch_allreduce_sum
+    from hkcsa.shard import sharded_build, torch_allgather, torch_allreduce_sum
     from oracle import oracle
-    text = oracle.synth_text(n, b"ACGT", seed=21)
-    dev = OracleShardDevice(text)
-    lo, hi = sharded_build(dev, world, rank, torch_allreduce_sum())
+    if kind == "iid":
+        text = oracle.synth_text(n, b"ACGT", seed=21)
+        dev = OracleShardDevice(text)
+        lo, hi = sharded_build(dev, world, rank, torch_allreduce_sum())
+    else:
+        text = np.frombuffer((b"abcab" * n)[:n - 1] + b"$", dtype=np.uint8) if kind == "periodic" else \
+            np.frombuffer(b"a" * (n - 1) + b"$", dtype=np.uint8)
+        dev = DoublingShardDevice(text, h0=3)
+        lo, hi = sharded_build(dev, world, rank, torch_allreduce_sum(), torch_allgather())
+        assert dev.shard_status()[2] == 0
     bounds = [None] * world
     dist.all_gather_object(bounds, (lo, hi))
     parts = [None] * world
@@ -79,13 +159,14 @@ def _free_port():
     return p
 
 
-@pytest.mark.parametrize("world", [2])
-def test_gloo_sharded_orchestration(world):
+@pytest.mark.parametrize("world,kind,n", [(2, "iid", 30001), (2, "periodic", 3001), (3, "run", 1501)])
+def test_gloo_sharded_orchestration(world, kind, n):
+    """iid: the three collectives of the build; periodic / run: slices left tied after the chunk
+    rounds finish by prefix doubling with the ISA rank exchange (hkcsa.shard.shard_doubling)."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    n = 30001
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, n, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n, q, kind)) for r in range(world)]
     for p in procs:
         p.start()
     bounds, ok, m, nn = q.get(timeout=120)

@@ -249,15 +249,177 @@ def test_shard_two_phase_emulated(hk, nranks, flags, alpha):
     assert np.array_equal(np.concatenate(parts), ref)
 
 
-@pytest.mark.parametrize("flags", [0, 1, 3])
-def test_shard_rccl_single_rank(hk, flags):
-    text = oracle.synth_text(200001, bytes(range(0x20, 0x7F)), seed=13)
+def _repetitive(name):
+    rng = np.random.default_rng(99)
+    if name == "periodic_64K":
+        return np.frombuffer(b"abc" * 21845 + b"$", dtype=np.uint8)
+    if name == "run_a_20K":
+        return np.frombuffer(b"a" * 20000 + b"$", dtype=np.uint8)
+    if name == "repeats_200K":
+        base = rng.integers(0, 4, size=5000).astype(np.uint8) + ord("A")
+        rep = np.tile(base, 40)
+        rep[rng.integers(0, len(rep), size=50)] = ord("T")
+        return np.concatenate([rep, [ord("$")]]).astype(np.uint8)
+    if name == "run_a_8M":     # longer than 200,000 refinement rounds x ~30 symbols
+        return np.frombuffer(b"a" * (1 << 23) + b"$", dtype=np.uint8)
+    raise KeyError(name)
+
+
+def _expected_sa(name, text):
+    if name.startswith("run_a"):   # 'a'^N '$': '$' < 'a', so SA = n-1, n-2, ..., 0
+        return np.arange(len(text) - 1, -1, -1, dtype=np.uint64)
+    return oracle.suffix_array(text)
+
+
+def _emulated_shard_build(hk, text, nranks, flags):
+    from hkcsa.shard import emulated_doubling
+    devs = [hk.DeviceIndex.from_bytes(text, device=0, flags=flags) for _ in range(nranks)]
+    g = sum(d.shard_histogram(nranks, r) for r, d in enumerate(devs))
+    below = sum(d.shard_counts(g, nranks, r) for r, d in enumerate(devs))
+    for r, d in enumerate(devs):
+        d.shard_build(g, below, nranks, r)
+    rounds = emulated_doubling(devs)
+    return devs, rounds
+
+
+@pytest.mark.parametrize("name,nranks,flags", [
+    ("periodic_64K", 2, 0), ("periodic_64K", 5, 1), ("run_a_20K", 3, 0), ("run_a_20K", 8, 1),
+    ("repeats_200K", 4, 0), ("repeats_200K", 7, 1), ("repeats_200K", 2, 3),
+    ("run_a_8M", 2, 0), ("run_a_8M", 4, 1)])
+def test_shard_doubling_emulated(hk, name, nranks, flags):
+    """Repetitive texts whose slices stay tied after the chunk rounds: prefix doubling with the ISA
+    rank exchange (hkcsa_shard_isa_segment / _updates / _apply / _round), ranks emulated on one GPU,
+    u32 and u64 positions.  Bit-exact against the oracle SA (the analytic SA for the runs)."""
+    text = _repetitive(name)
+    ref = _expected_sa(name, text)
+    devs, rounds = _emulated_shard_build(hk, text, nranks, flags)
+    assert rounds > 0, "the text should need the doubling exchange"
+    parts, bw = [], []
+    for d in devs:
+        assert d.shard_status()[2] == 0
+        parts.append(d.shard_sa())
+        bw.append(d.shard_bwt())
+    sa = np.concatenate(parts)
+    assert np.array_equal(sa, ref), name
+    assert np.array_equal(np.concatenate(bw), oracle.bwt(text, ref)), name
+    for d in devs:
+        d.close()
+
+
+@pytest.mark.parametrize("name,flags", [("dna_200K", 0), ("printable_200K", 0), ("printable_200K", 1),
+                                        ("printable_200K", 3), ("periodic_64K", 0), ("run_a_20K", 1),
+                                        ("repeats_200K", 0), ("run_a_8M", 0)])
+def test_shard_rccl_single_rank(hk, name, flags):
+    if name == "dna_200K":
+        text = oracle.synth_text(200001, b"ACGT", seed=13)
+    elif name == "printable_200K":
+        text = oracle.synth_text(200001, bytes(range(0x20, 0x7F)), seed=13)
+    else:
+        text = _repetitive(name)
     dev = hk.DeviceIndex.from_bytes(text, device=0, flags=flags)
     dev.build_sa_sharded(hk.comm_unique_id(), 1, 0)
     assert dev.shard_range() == (0, len(text))
-    sa = oracle.suffix_array(text)
+    sa = _expected_sa(name, text)
     assert np.array_equal(dev.shard_sa(), sa)
     assert np.array_equal(dev.shard_bwt(), oracle.bwt(text, sa))
+    dev.close()
+
+
+def _query_set(text, seed, count=600):
+    rng = np.random.default_rng(seed)
+    n = len(text)
+    pats = [b"", b"$", bytes(text[-3:])]
+    for _ in range(count):
+        m = int(rng.integers(1, 24))
+        st = int(rng.integers(0, max(1, n - m)))
+        pats.append(text[st:st + m].tobytes())
+    for _ in range(100):
+        pats.append(bytes(rng.choice(np.unique(text), size=int(rng.integers(1, 6)))))
+    return pats
+
+
+def _check_queries(dev, text, sa, seed):
+    fm = oracle.FM(text, sa)
+    pats = _query_set(text, seed)
+    assert np.array_equal(dev.count_ranges(pats), fm.find_range(pats))
+    offs, pos = dev.locate(pats)
+    got = [[int(x) for x in pos[offs[i]:offs[i + 1]]] for i in range(len(pats))]
+    assert got == fm.find(pats)
+
+
+@pytest.mark.parametrize("name,flags", [("dna_300K", 0), ("dna_300K", 1), ("repeats_200K", 1)])
+def test_shard_replicate_queries(hk, name, flags):
+    """Replicas for batched queries: RCCL all-gather of the SA slices and BWT rows (one rank), then
+    the wavelet tree and count / locate (u64 SA gather with flags=1) against the oracle FM index."""
+    text = oracle.synth_text(300001, b"ACGT", seed=17) if name == "dna_300K" else _repetitive(name)
+    dev = hk.DeviceIndex.from_bytes(text, device=0, flags=flags)
+    dev.build_sa_sharded(hk.comm_unique_id(), 1, 0)
+    with pytest.raises(hk.HkcsaError):
+        dev.build_wt()                      # a sharded handle holds only its slice
+    dev.shard_replicate()
+    dev.build_wt()
+    sa = oracle.suffix_array(text)
+    assert np.array_equal(dev.sa(), sa)
+    assert np.array_equal(dev.bwt(), oracle.bwt(text, sa))
+    _check_queries(dev, text, sa, seed=len(text))
+    dev.close()
+
+
+@pytest.mark.parametrize("nranks,flags", [(3, 0), (4, 1)])
+def test_shard_adopt_queries(hk, nranks, flags):
+    """Host-assembled replica after an emulated sharded build (hkcsa_shard_adopt)."""
+    text = oracle.synth_text(250001, b"ACGT", seed=19)
+    devs, _ = _emulated_shard_build(hk, text, nranks, flags)
+    sa = np.concatenate([d.shard_sa() for d in devs])
+    bwt = np.concatenate([d.shard_bwt() for d in devs])
+    ref = oracle.suffix_array(text)
+    assert np.array_equal(sa, ref)
+    dev = devs[0]
+    dev.shard_adopt(sa, bwt)
+    dev.build_wt()
+    _check_queries(dev, text, ref, seed=nranks)
+    for d in devs:
+        d.close()
+
+
+def test_sharded_handle_refuses_full_index_calls(hk):
+    """A sharded handle holds SA[lo:hi) and its BWT rows only: whole-index calls fail with
+    HKCSA_E_STATE instead of reading past the slice."""
+    text = oracle.synth_text(100001, b"ACGT", seed=23)
+    devs, _ = _emulated_shard_build(hk, text, 2, 0)
+    d = devs[1]
+    for call in (d.build_wt, lambda: d.bwt(0, 10), lambda: d.locate([b"AC"]), lambda: d.count_ranges([b"A"]),
+                 lambda: d.rank(np.array([65], np.uint8), np.array([5], np.uint64)), lambda: d.sa(0, 4),
+                 lambda: d.entropy(2)):
+        with pytest.raises(hk.HkcsaError) as e:
+            call()
+        assert e.value.code == -3
+    for x in devs:
+        x.close()
+
+
+def test_entropy_after_compact_refused(hk):
+    dev = _build(hk, oracle.synth_text(5001, b"ACGT", seed=3).tobytes())
+    h0 = dev.entropy(0)
+    dev.build_samples(4)
+    dev.compact()
+    assert dev.entropy(0) == h0
+    with pytest.raises(hk.HkcsaError) as e:
+        dev.entropy(2)
+    assert e.value.code == -3
+    dev.close()
+
+
+def test_entropy_keeps_wavelet_tree(hk):
+    text = oracle.synth_text(20001, b"ACGT", seed=5)
+    dev = hk.DeviceIndex.from_bytes(text, device=0)
+    dev.build_sa()
+    dev.build_wt()
+    e1 = dev.entropy(3)
+    dev.build_sa()          # fresh SA, then H_k rebuilds nothing and the WT stays usable
+    dev.build_wt()
+    assert dev.entropy(3) == e1
+    _check_queries(dev, text, oracle.suffix_array(text), seed=1)
     dev.close()
 
 

@@ -7,4 +7,4 @@ timeout -k 10 ${TT:-500} python -u -m pytest ${TESTS:-tests/test_gpu_parity.py} 
 rc=$?
 echo "pytest rc=$rc"; grep -cE "PASSED" gpurun_out/combo_tests.log; grep -E "FAILED|Error" gpurun_out/combo_tests.log | head -20
 if [ $rc -ne 0 ]; then tail -50 gpurun_out/combo_tests.log; exit $rc; fi
-if [ -n "$EMUL_ARGS" ]; then bash tools_gpu_emul.sh || exit $?; fi
+if [ -n "$EMUL_ARGS" ]; then bash tools/gpu_emul.sh || exit $?; fi

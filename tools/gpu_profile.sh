@@ -10,6 +10,6 @@ echo "bench ok"; cat gpurun_out/bench_default.json
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_bench -o run -- \
     python3 bench.py --no-cpu-baseline > gpurun_out/prof_bench.json 2> gpurun_out/prof_bench.err || exit $?
 echo "stats ok"
-bash tools_gpu_pmc.sh || exit $?
-timeout -k 10 400 python3 tools_shard_emulate.py --nranks 8 --ranks 0 3 7 --pos64 > gpurun_out/emul8.jsonl 2> gpurun_out/emul8.err || exit $?
+bash tools/gpu_pmc.sh || exit $?
+timeout -k 10 400 python3 tools/shard_emulate.py --nranks 8 --ranks 0 3 7 --pos64 > gpurun_out/emul8.jsonl 2> gpurun_out/emul8.err || exit $?
 cat gpurun_out/emul8.jsonl

@@ -1,6 +1,6 @@
 #!/bin/bash
 # SQ counters (issue / wait / LDS) of selected kernels during one 1 GiB bench step, one rocprofv3
-# --pmc pass per counter set.  usage: KRE="regex" [SQCMD="python3 ..."] bash tools_gpu_sqpmc.sh
+# --pmc pass per counter set.  usage: KRE="regex" [SQCMD="python3 ..."] bash tools/gpu_sqpmc.sh
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
 export TMPDIR=/tmp

@@ -11,7 +11,7 @@ if [ "${TESTS:-1}" = "1" ]; then
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 fi
 if [ "${DIAG:-1}" = "1" ]; then
-  timeout -k 10 300 python tools_radix_diag.py $((1<<30)) > gpurun_out/diag.log 2>&1
+  timeout -k 10 300 python tools/radix_diag.py $((1<<30)) > gpurun_out/diag.log 2>&1
   rc=$?; echo "diag rc=$rc"; cat gpurun_out/diag.log
   [ $rc -eq 0 ] || exit $rc
 fi

@@ -1,4 +1,4 @@
-"""Summarise the rocprofv3 PMC runs of tools_gpu_pmc.sh into profiles/pmc_kernels.json.
+"""Summarise the rocprofv3 PMC runs of tools/gpu_pmc.sh into profiles/pmc_kernels.json.
 
 HBM bytes per launch = 2 * FETCH_SIZE + WRITE_SIZE (KiB -> bytes): FETCH_SIZE is in KiB and on
 gfx950 reports half of the bytes of wide coalesced reads (MI355X_MICROARCH.md §HBM), WRITE_SIZE is
@@ -9,7 +9,7 @@ exact for streaming stores.  Per bench timer name, the n-element launches of its
 """
 import csv, json, os, sys
 
-root = os.path.dirname(os.path.abspath(__file__))
+root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 src = sys.argv[1] if len(sys.argv) > 1 else os.path.join(root, "gpurun_out")
 KERNELS = {
     "sa_bucket_sort": lambda k: "k_bucket_sort<false" in k,

@@ -1,6 +1,6 @@
 """Diagnostic: per-pass time of onesweep variants at n keys (prints one JSON line)."""
 import ctypes as C, json, sys, os
-sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "high-order-entropy-compressed-suffix-array_amd"))
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "high-order-entropy-compressed-suffix-array_amd"))
 import numpy as np
 from hkcsa import _native as N
 lib = N.load()

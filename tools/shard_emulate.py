@@ -5,7 +5,7 @@ device can play rank r of N with the two-phase API (hkcsa_shard_histogram over a
 then hkcsa_shard_build(global, N, r)).  Prints one JSON line per emulated rank with the
 slice size, wall time and the per-kernel breakdown (HIP events).
 
-  python tools_shard_emulate.py --per-rank 1073741824 --nranks 8 --ranks 0 7
+  python tools/shard_emulate.py --per-rank 1073741824 --nranks 8 --ranks 0 7
 """
 import argparse
 import json
@@ -13,7 +13,7 @@ import os
 import sys
 import time
 
-sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)),
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
                                 "high-order-entropy-compressed-suffix-array_amd"))
 from hkcsa import DeviceIndex  # noqa: E402
 
