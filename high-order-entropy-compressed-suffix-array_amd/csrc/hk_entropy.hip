@@ -105,9 +105,10 @@ double run_log_sum(Index& ix, const uint32_t* d_flags, uint64_t m, hipStream_t s
 }  // namespace
 
 double entropy_k(Index& ix, int k) {
-  if (!ix.have_text) throw ApiError{-3, "entropy: text released by compact"};
   const uint64_t n = ix.n;
   if (k < 0 || n == 0) return 0.0;
+  // H_0 needs only the byte histogram (kept after compact); H_k reads the text
+  if (!ix.have_text && (k > 0 || !ix.have_alpha)) throw ApiError{-3, "entropy: text released by compact"};
   compute_alphabet(ix);
   if (k == 0) {   // csa/high_order_entropy.py:11-16
     double h = 0;

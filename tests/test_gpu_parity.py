@@ -242,6 +242,9 @@ def test_shard_two_phase_emulated(hk, nranks, flags, alpha):
     for r, d in enumerate(devs):
         d.shard_build(g, below, nranks, r)
         assert d.shard_range() == bounds[r]
+    from hkcsa.shard import emulated_doubling
+    emulated_doubling(devs)     # skewed texts: slices whose ties outlast the chunk rounds
+    for r, d in enumerate(devs):
         parts.append(d.shard_sa())
         lo, hi = bounds[r]
         assert np.array_equal(d.shard_bwt(), ref_bwt[lo:hi]), r
