@@ -2,25 +2,37 @@
 """Headline benchmark: SA build MB/s + batched locate() patterns/s (BASELINE.json).
 
 N = 1 (default): configs[1]'s pipeline on the metric's 1 GiB sigma=4 text — one "step" is the
-  SA + BWT build of T' = 2^30 iid ACGT symbols + '$' (text resident in HBM before timing): keyed
-  suffix keys, bucket histogram, two LSD radix passes over the bucket bits (the first builds the
-  keys from the text), LDS bucket sorts that write SA and BWT, refinement of the tied suffixes.
-  After the timed steps the wavelet tree is built and 1M random 16-symbol substrings are located in
-  batches (count + SA gather), reported as locate_patterns_per_s.
-N > 1 (torchrun, one process per GPU): the sharded construction (hkcsa_build_sa_sharded: RCCL
-  all-reduce of the partition histogram and of the slice counts, independent slice sorts, RCCL
-  all-gather of the slice bounds) of an N GiB text, i.e. weak scaling at 1 GiB of suffixes per GPU;
-  value = all ranks' text MB / max-over-ranks time.
+  SA + BWT build of T' = 2^30 iid ACGT symbols + '$' (text resident in HBM before timing): byte
+  histogram / C array, keyed suffix keys, two LSD radix passes over the bucket bits (the first builds
+  the keys from the text), LDS bucket sorts that write SA and BWT, refinement of the tied suffixes.
+  After the timed steps the wavelet tree is built (warm, timed over repeats) and 1M random 16-symbol
+  substrings are located in batches (count + SA gather), reported as locate_patterns_per_s.
+  Extra legs under detail (skip with --no-legs):
+    sigma256          configs[3]: 1 GiB iid bytes (sigma=256): SA + BWT steps, 8-level WT, roofline of
+                      the radix passes and WT kernels;
+    printable_200MiB  a clearly labelled stand-in for configs[2] (english.200MB is not available
+                      offline): 200 MiB iid printable bytes (sigma=95), full build + 1M 20-symbol count().
+N > 1: one process per GPU (torchrun, or spawned here when WORLD_SIZE is unset): the sharded
+  construction (hkcsa_build_sa_sharded: RCCL all-reduce of the partition histogram and of the slice
+  counts, independent slice sorts, RCCL all-gather of per-rank status; ISA rank exchange by RCCL
+  all-gather only for texts whose ties outlast the chunk refinement).
+    default (weak):   N GiB of text on N GPUs (1 GiB of suffixes per GPU);
+    --strong:         a fixed --strong-bytes text (default 4 GiB = configs[4]) on N GPUs; at N = 1 a text
+                      with >= 2^32 suffixes is built as several slices one after another on the one GPU.
+  value = all suffixes' MB / max-over-ranks time.  After the timed steps every rank all-gathers the
+  SA slices and BWT rows (replicas), builds its wavelet tree and locates its 1/N of the patterns;
+  locate_patterns_per_s = all patterns / max-over-ranks time.
 
 The JSON line also carries:
   roofline      — the dominant kernel of the timed steps (largest summed time among the bucket
                   sort and the two radix passes) timed with HIP events on the library's stream:
                   achieved = its algorithmic bytes per launch / mean launch time, peak = 8000 GB/s
                   (MI355X HBM3E), traffic = PMC-measured HBM bytes per launch (profiles/
-                  pmc_kernels.json); the other two kernels under roofline["others"].
-  cpu_baseline  — the pure-Python restatement of the reference (oracle/ref_port.py:
-                  naive suffix sort, dense occ, dict backward search), one core, on a
-                  bounded sample (rank 0, N = 1 only).
+                  pmc_kernels.json); the other kernels under roofline["others"].
+  cpu_baseline  — the pure-Python restatement of the reference (oracle/ref_port.py: naive suffix
+                  sort, dense occ, left-spine WT, dict backward search), one core, on bounded
+                  samples (rank 0, N = 1 only): the unmodified pipeline end to end at 2^17 symbols
+                  and configs[0]'s reference stages at 1 MiB with the suffix array substituted.
 """
 from __future__ import annotations
 
@@ -28,6 +40,7 @@ import argparse
 import gc
 import json
 import os
+import socket
 import sys
 import time
 
@@ -37,21 +50,35 @@ sys.path.insert(0, ROOT)
 
 import numpy as np  # noqa: E402
 
-from hkcsa import DeviceIndex, comm_unique_id  # noqa: E402
-
 METRIC = "SA build MB/s + batched locate() patterns/s, 1 GiB text, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0
 DNA = b"ACGT"
+PRINTABLE = bytes(range(0x20, 0x7F))
+BYTES256 = bytes(range(256))
+PATTERN_WINDOW = 256 << 20   # patterns are drawn from a window of this many symbols at a seeded offset
 
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def cpu_baseline(sample_n: int, npat: int, seed: int = 3) -> dict:
-    """Reference algorithm restated in pure Python, timed on this host (1 core)."""
-    from oracle import ref_port
+# ---------------------------------------------------------------------------- CPU baseline
+def cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(sample_n: int, npat: int, c0_n: int, seed: int = 3) -> dict:
+    """Reference algorithms restated in pure Python (oracle/ref_port.py), timed on this host, 1 core."""
+    from oracle import oracle, ref_port
     rng = np.random.default_rng(seed)
+    # (1) the unmodified reference pipeline (naive suffix sort) end to end at sample_n symbols
     text = np.frombuffer(DNA, np.uint8)[rng.integers(0, 4, size=sample_n)].tobytes().decode("latin-1")
     times = []
     idx = None
@@ -69,36 +96,81 @@ def cpu_baseline(sample_n: int, npat: int, seed: int = 3) -> dict:
     for p in pats:
         idx.find(p)
     t_q = time.perf_counter() - t0
+    del idx
+    # (2) configs[0]: the reference stages at 1 MiB with the suffix array substituted (the naive
+    # sort would need ~512 GiB there); the SA comes from the oracle's C suffix sort (not timed)
+    t1 = oracle.synth_text(c0_n + 1, DNA, seed=seed + 1)
+    t1s = t1.tobytes().decode("latin-1")
+    sa = oracle.suffix_array(t1).tolist()
+    stages = {}
+    gc.collect()
+    t0 = time.perf_counter()
+    bwt = ref_port.bwt_of(t1s, sa)
+    stages["bwt_s"] = time.perf_counter() - t0
+    gc.collect()
+    t0 = time.perf_counter()
+    ref_port.left_spine_levels(bwt)
+    stages["wt_s"] = time.perf_counter() - t0
+    gc.collect()
+    t0 = time.perf_counter()
+    occ = ref_port.occ_table(bwt)
+    stages["occ_s"] = time.perf_counter() - t0
+    gc.collect()
+    t0 = time.perf_counter()
+    ref_port.count_table(t1s)
+    stages["C_s"] = time.perf_counter() - t0
+    port = ref_port.FMIndexPort.__new__(ref_port.FMIndexPort)
+    port.text, port.suffix_array, port.bwt, port.occ = t1s, sa, bwt, occ
+    port.count = ref_port.count_table(t1s)
+    st1 = rng.integers(0, len(t1s) - 16, size=npat)
+    pats1 = [t1s[s:s + 16] for s in st1]
+    gc.collect()
+    t0 = time.perf_counter()
+    for p in pats1:
+        port.find(p)
+    t_q1 = time.perf_counter() - t0
+    build1 = sum(stages.values())
     return {
         "value": round(len(tp) / 2**20 / t_build, 6),
         "unit": "MB/s",
         "cores": 1,
         "kind": "port",
         "sample": f"EnhancedFMIndex restatement (naive SA + BWT + dense occ + C) on {len(tp)} iid ACGT "
-                  f"symbols, median of 3; find() of {npat} 16-symbol substrings",
+                  f"symbols, median of 3; find() of {npat} 16-symbol substrings; plus configs[0]'s "
+                  f"stages at {c0_n + 1} symbols with the SA substituted",
         "build_s": round(t_build, 4),
         "locate_patterns_per_s": round(npat / t_q, 1),
+        "config0_1MiB": {"symbols": c0_n + 1, **{k: round(v, 4) for k, v in stages.items()},
+                         "stages_MBps": round((c0_n + 1) / 2**20 / build1, 4),
+                         "find_patterns_per_s": round(npat / t_q1, 1),
+                         "sa": "substituted (oracle C suffix sort, not timed)"},
         "host_cpus": os.cpu_count(),
+        "cpu_model": cpu_model(),
+        "note": "1 of host_cpus cores used (the reference is single-threaded pure Python)",
     }
 
 
+# ---------------------------------------------------------------------------- rooflines
 # kernels whose roofline bench.py reports: the dominant one (largest summed time) as `roofline`,
 # the others under roofline["others"]
-ROOF_KERNELS = ("sa_bucket_sort", "radix_onesweep_text", "radix_onesweep")
+ROOF_KERNELS = ("sa_bucket_sort", "radix_onesweep_text", "radix_onesweep", "byte_hist")
+WT_KERNELS = ("wt_bits", "wt_partition", "wt_map_codes")
 
 
-def pmc_traffic_gb(name: str) -> float | None:
+def pmc_traffic_gb(name: str, leg: str = "") -> float | None:
     """HBM GB per launch of timer `name`'s kernel, measured with rocprofv3 PMC counters on this config
-    (tools/gpu_pmc.sh + tools/pmc_summary.py -> profiles/pmc_kernels.json; FETCH_SIZE x2 gfx950 correction)."""
+    (tools/gpu_pmc.sh + tools/pmc_summary.py -> profiles/pmc_kernels.json; FETCH_SIZE x2 gfx950
+    correction for the wide streaming reads)."""
     p = os.path.join(ROOT, "profiles", "pmc_kernels.json")
     try:
         with open(p) as f:
-            return float(json.load(f)[name]["traffic_gb_per_launch"])
+            d = json.load(f)
+        return float((d[leg] if leg else d)[name]["traffic_gb_per_launch"])
     except Exception:
         return None
 
 
-def kernel_roofline(dev: DeviceIndex, name: str) -> dict | None:
+def kernel_roofline(dev, name: str, leg: str = "") -> dict | None:
     launches, ms, alg_bytes = dev.kernel_stats(name)
     if not launches:
         return None
@@ -106,13 +178,13 @@ def kernel_roofline(dev: DeviceIndex, name: str) -> dict | None:
     avg_s = ms / launches / 1e3
     achieved = per_launch_bytes / avg_s / 1e9
     return {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": pmc_traffic_gb(name), "kernel": name,
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": pmc_traffic_gb(name, leg), "kernel": name,
             "launches": launches, "avg_launch_ms": round(ms / launches, 4), "total_ms": round(ms, 3),
             "alg_bytes_per_launch": per_launch_bytes}
 
 
-def roofline(dev: DeviceIndex, traffic_gb: float | None) -> dict:
-    rows = [r for r in (kernel_roofline(dev, k) for k in ROOF_KERNELS) if r]
+def roofline(dev, names=ROOF_KERNELS, leg: str = "", traffic_gb: float | None = None) -> dict:
+    rows = [r for r in (kernel_roofline(dev, k, leg) for k in names) if r]
     if not rows:
         return {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None,
                 "traffic": None}
@@ -124,7 +196,7 @@ def roofline(dev: DeviceIndex, traffic_gb: float | None) -> dict:
     return dom
 
 
-def stage_breakdown(dev: DeviceIndex, names) -> dict:
+def stage_breakdown(dev, names) -> dict:
     out = {}
     for nm in names:
         l, ms, b = dev.kernel_stats(nm)
@@ -133,74 +205,99 @@ def stage_breakdown(dev: DeviceIndex, names) -> dict:
     return out
 
 
-def run_single(args) -> dict:
-    n = args.text_bytes + 1
-    dev = DeviceIndex.synthetic(n, DNA, seed=args.seed, device=0, flags=4 if args.global_sort else 0)
-    log(f"[bench] text n={n} resident on device")
-    for _ in range(args.warmup):
+BUILD_STAGES = ["byte_hist", "sa_bucket_hist", "sa_digit_hist", "sa_bin_starts", "sa_bucket_sort", "sa_big_gather",
+                "radix_onesweep_text", "radix_table_text", "radix_tile_hist", "radix_hist", "radix_onesweep",
+                "radix_onesweep_small", "sa_pack_keys", "sa_refine_stats", "sa_refine_apply", "sa_refine_keys",
+                "sa_isa_scatter", "sa_group_stats", "sa_group_apply", "sa_pair_keys", "bwt_gather"]
+SHARD_STAGES = ["shard_hist", "shard_below", "shard_select_count", "shard_pack_select", "rccl_allreduce_hist",
+                "rccl_allreduce_counts", "rccl_allgather_status", "rccl_allgather_sa", "rccl_allgather_pairs",
+                "sa_isa_update", "shard_split_join"] + BUILD_STAGES
+
+
+# ---------------------------------------------------------------------------- pattern sets
+def pattern_batch(dev, n: int, count: int, plen: int, seed: int) -> tuple[np.ndarray, np.ndarray]:
+    """count substrings of length plen drawn uniformly from a seeded window of the device text."""
+    rng = np.random.default_rng(seed)
+    win = min(n - 1, PATTERN_WINDOW)
+    w0 = int(rng.integers(0, n - win)) if n - win > 0 else 0
+    txt = dev.text(w0, w0 + win)
+    starts = rng.integers(0, win - plen, size=count).astype(np.int64)
+    data = txt[starts[:, None] + np.arange(plen)[None, :]].reshape(-1)
+    offs = np.arange(count + 1, dtype=np.uint64) * plen
+    return np.ascontiguousarray(data), offs
+
+
+def time_queries(dev, data, offs, reps: int) -> dict:
+    q = dev.queries(data=data, offs=offs)
+    P = len(offs) - 1
+    total = q.locate()
+    q.count()
+    dev.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        total = q.locate()
+    dev.synchronize()
+    t_loc = (time.perf_counter() - t0) / reps
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        q.count()
+    dev.synchronize()
+    t_cnt = (time.perf_counter() - t0) / reps
+    q.close()
+    return {"patterns": P, "plen": int(offs[1] - offs[0]) if P else 0, "occurrences": int(total),
+            "locate_s": t_loc, "count_s": t_cnt,
+            "locate_patterns_per_s": round(P / t_loc, 1), "count_patterns_per_s": round(P / t_cnt, 1)}
+
+
+def time_wt(dev, reps: int) -> float:
+    dev.build_wt()            # warm: first-call allocations happen here
+    dev.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        dev.build_wt()
+    dev.synchronize()
+    return (time.perf_counter() - t0) / reps
+
+
+# ---------------------------------------------------------------------------- single GPU
+def build_leg(alpha: bytes, n: int, steps: int, warmup: int, seed: int, flags: int = 0):
+    from hkcsa import DeviceIndex
+    dev = DeviceIndex.synthetic(n, alpha, seed=seed, device=0, flags=flags)
+    for _ in range(warmup):
         dev.build_sa()
         dev.build_bwt()
     dev.synchronize()
     dev.timing_reset()
     dev.timing(True)
-    try:
-        import torch
-        torch.cuda.synchronize()
-    except Exception:
-        pass
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        dev.build_sa()
-        dev.build_bwt()
+    for _ in range(steps):
+        dev.build_sa()          # includes the byte histogram / C array of every build
+        dev.build_bwt()         # no-op: the bucket sorts write the BWT with the SA
     dev.synchronize()
-    t1 = time.perf_counter()
-    dev.timing(False)
-    wall = t1 - t0
+    wall = time.perf_counter() - t0
+    return dev, wall
+
+
+def run_single(args) -> dict:
+    n = args.text_bytes + 1
+    alpha = {4: DNA, 95: PRINTABLE, 256: BYTES256}[args.sigma]
+    dev, wall = build_leg(alpha, n, args.steps, args.warmup, args.seed, flags=4 if args.global_sort else 0)
     value = args.steps * n / 2**20 / wall
     info = dev.build_info()
-    roof = roofline(dev, args.traffic_gb)
-    stages = stage_breakdown(dev, ["sa_bucket_hist", "sa_digit_hist", "sa_bin_starts", "sa_bucket_sort",
-                                   "sa_big_gather", "radix_onesweep_text",
-                                   "radix_table_text", "radix_tile_hist",
-                                   "radix_hist", "radix_onesweep", "radix_onesweep_small", "sa_pack_keys",
-                                   "sa_refine_stats", "sa_refine_apply", "sa_refine_keys", "sa_isa_scatter",
-                                   "sa_group_stats", "sa_group_apply", "sa_pair_keys", "bwt_gather", "byte_hist"])
-    log(f"[bench] SA+BWT {wall / args.steps * 1e3:.2f} ms/step -> {value:.1f} MB/s; info={info[:8]}")
-
-    # full build (adds the wavelet tree) and batched locate
-    t0 = time.perf_counter()
-    dev.build_wt()
-    dev.synchronize()
-    t_wt = time.perf_counter() - t0
+    leg = "" if args.sigma == 4 else f"sigma{args.sigma}"
+    roof = roofline(dev, ROOF_KERNELS, leg, args.traffic_gb)
+    stages = stage_breakdown(dev, BUILD_STAGES)
+    log(f"[bench] sigma={args.sigma} SA+BWT {wall / args.steps * 1e3:.2f} ms/step -> {value:.1f} MB/s; "
+        f"info={info[:8]}")
+    dev.timing_reset()
+    t_wt = time_wt(dev, args.wt_reps)
+    wt_roof = roofline(dev, WT_KERNELS, leg)
+    dev.timing(False)
     loc = None
     if args.patterns > 0:
-        rng = np.random.default_rng(args.seed + 1)
-        starts = np.sort(rng.integers(0, n - 1 - args.plen, size=args.patterns)).astype(np.uint64)
-        lo, hi = int(starts[0]), int(starts[-1]) + args.plen
-        txt = dev.text(lo, hi)
-        idx = (starts - lo)[:, None] + np.arange(args.plen, dtype=np.uint64)[None, :]
-        data = txt[idx].reshape(-1)
-        rng.shuffle(data.reshape(-1, args.plen))
-        offs = np.arange(args.patterns + 1, dtype=np.uint64) * args.plen
-        q = dev.queries(data=data, offs=offs)
-        q.locate()
-        dev.synchronize()
-        t0 = time.perf_counter()
-        reps = args.query_reps
-        total = 0
-        for _ in range(reps):
-            total = q.locate()
-        dev.synchronize()
-        t_loc = (time.perf_counter() - t0) / reps
-        t0 = time.perf_counter()
-        for _ in range(reps):
-            q.count()
-        dev.synchronize()
-        t_cnt = (time.perf_counter() - t0) / reps
-        loc = {"patterns": args.patterns, "plen": args.plen, "occurrences": int(total),
-               "locate_patterns_per_s": round(args.patterns / t_loc, 1),
-               "count_patterns_per_s": round(args.patterns / t_cnt, 1)}
-        q.close()
+        data, offs = pattern_batch(dev, n, args.patterns, args.plen, args.seed + 1)
+        loc = time_queries(dev, data, offs, args.query_reps)
+    dev.close()
     res = {
         "metric": METRIC,
         "value": round(value, 2),
@@ -214,33 +311,93 @@ def run_single(args) -> dict:
         "vs_baseline": None,
         "dtype": "u8",
         "data": "synthetic",
-        "config": {"workload": "1 GiB synthetic sigma=4 text: SA + BWT by the HIP bucket build (LSD "
-                               "radix passes over the bucket bits, LDS bucket sorts writing SA and BWT, "
-                               "tie refinement; configs[1] pipeline at the metric's 1 GiB), then WT + "
-                               f"1M batched {args.plen}-symbol locate()",
-                   "text_symbols": n, "sigma": 4, "positions": "u32"},
+        "config": {"workload": f"{n - 1} iid sigma={args.sigma} symbols + '$': SA + BWT by the HIP bucket "
+                               "build (byte histogram, LSD radix passes over the bucket bits, LDS bucket "
+                               "sorts writing SA and BWT, tie refinement; configs[1] pipeline at the "
+                               "metric's 1 GiB), then warm WT build + batched "
+                               f"{args.plen}-symbol locate()",
+                   "text_symbols": n, "sigma": args.sigma, "positions": "u32"},
         "roofline": roof,
         "locate_patterns_per_s": loc["locate_patterns_per_s"] if loc else None,
         "full_build_MBps": round(n / 2**20 / (wall / args.steps + t_wt), 2),
-        "detail": {"wt_build_ms": round(t_wt * 1e3, 2), "locate": loc, "stages_ms_total": stages,
-                   "build_info": info[:16]},
+        "detail": {"wt_build_ms": round(t_wt * 1e3, 3), "wt_roofline": wt_roof, "locate": loc,
+                   "pattern_source": f"uniform substrings of a {PATTERN_WINDOW >> 20} MiB window of the text",
+                   "stages_ms_total": stages, "build_info": info[:16]},
     }
-    dev.close()
     return res
 
 
+def run_extra_legs(args, res: dict):
+    """configs[3] (sigma=256, 1 GiB) and the configs[2] stand-in (sigma=95, 200 MiB)."""
+    legs = {}
+    if args.sigma != 256:
+        n = (1 << 30) + 1
+        dev, wall = build_leg(BYTES256, n, args.leg_steps, 1, args.seed + 10)
+        roof = roofline(dev, ROOF_KERNELS, "sigma256")
+        stages = stage_breakdown(dev, BUILD_STAGES)
+        dev.timing_reset()
+        t_wt = time_wt(dev, args.wt_reps)
+        wt_roof = roofline(dev, WT_KERNELS, "sigma256")
+        dev.timing(False)
+        info = dev.build_info()
+        dev.close()
+        legs["sigma256"] = {"config": "configs[3]: 1 GiB iid bytes sigma=256 + '$': SA + BWT steps, 8-level WT",
+                            "text_symbols": n, "steps": args.leg_steps,
+                            "ms_per_step": round(wall / args.leg_steps * 1e3, 3),
+                            "sa_bwt_MBps": round(args.leg_steps * n / 2**20 / wall, 2),
+                            "wt_build_ms": round(t_wt * 1e3, 3),
+                            "full_build_MBps": round(n / 2**20 / (wall / args.leg_steps + t_wt), 2),
+                            "roofline": roof, "wt_roofline": wt_roof, "stages_ms_total": stages,
+                            "build_info": info[:16]}
+        log(f"[bench] sigma256 leg: {legs['sigma256']['ms_per_step']} ms/step, WT {t_wt * 1e3:.2f} ms")
+    n = 200 * (1 << 20) + 1
+    dev, wall = build_leg(PRINTABLE, n, args.leg_steps, 1, args.seed + 20)
+    dev.timing_reset()
+    t_wt = time_wt(dev, args.wt_reps)
+    data, offs = pattern_batch(dev, n, args.patterns or 1_000_000, 20, args.seed + 21)
+    dev.timing_reset()
+    dev.timing(True)
+    qq = time_queries(dev, data, offs, args.query_reps)
+    l, ms, _ = dev.kernel_stats("fm_count")
+    dev.timing(False)
+    dev.close()
+    legs["printable_200MiB"] = {
+        "config": "stand-in for configs[2] (english.200MB absent offline: not run): 200 MiB iid printable "
+                  "bytes (sigma=95) + '$', full build + batched 20-symbol count()",
+        "text_symbols": n, "ms_per_step": round(wall / args.leg_steps * 1e3, 3),
+        "wt_build_ms": round(t_wt * 1e3, 3),
+        "full_build_MBps": round(n / 2**20 / (wall / args.leg_steps + t_wt), 2),
+        "count_patterns_per_s": qq["count_patterns_per_s"], "locate_patterns_per_s": qq["locate_patterns_per_s"],
+        "fm_count_kernel_ms": round(ms / max(1, l), 4), "patterns": qq["patterns"], "plen": 20}
+    log(f"[bench] printable leg: count {qq['count_patterns_per_s']:.3g} patterns/s")
+    res["detail"]["legs"] = legs
+
+
+# ---------------------------------------------------------------------------- sharded / multi-GPU
 def run_sharded(args, rank: int, world: int, local_rank: int) -> dict | None:
     import torch
     import torch.distributed as dist
+    from hkcsa import DeviceIndex, comm_unique_id
     torch.cuda.set_device(local_rank)
-    per = args.text_bytes
-    n = per * world + 1
-    dev = DeviceIndex.synthetic(n, DNA, seed=args.seed, device=local_rank, flags=1 if args.pos64 else 0)
+    n = (args.strong_bytes if args.strong else args.text_bytes * world) + 1
+    flags = 1 if args.pos64 else 0
+    dev = DeviceIndex.synthetic(n, DNA, seed=args.seed, device=local_rank, flags=flags)
     uid = [comm_unique_id() if rank == 0 else None]
     dist.broadcast_object_list(uid, src=0)
     uid = uid[0]
+    # slices of < 2^32 suffixes: one per rank, or several per GPU run one after another (strong, N = 1)
+    per_gpu = max(1, -(-n // (world * ((1 << 32) - (1 << 28)))))
+    if per_gpu > 1 and world > 1:
+        raise SystemExit("more than one slice per GPU is supported at N = 1 only")
+
+    def step():
+        if per_gpu == 1:
+            dev.build_sa_sharded(uid, world, rank)
+        else:
+            virtual_slices(dev, per_gpu)
+
     for _ in range(args.warmup):
-        dev.build_sa_sharded(uid, world, rank)
+        step()
     dev.synchronize()
     dev.timing_reset()
     dev.timing(True)
@@ -248,7 +405,7 @@ def run_sharded(args, rank: int, world: int, local_rank: int) -> dict | None:
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        dev.build_sa_sharded(uid, world, rank)
+        step()
     dev.synchronize()
     torch.cuda.synchronize()
     t1 = time.perf_counter()
@@ -258,20 +415,42 @@ def run_sharded(args, rank: int, world: int, local_rank: int) -> dict | None:
     dist.all_reduce(el, op=dist.ReduceOp.MAX)
     wall = float(el.item())
     lo, hi = dev.shard_range()
-    roof = roofline(dev, args.traffic_gb)
-    # the PMC summaries in profiles/ are of the single-GPU launches: not this slice's kernels
-    if args.traffic_gb is None:
+    roof = roofline(dev, ROOF_KERNELS, "", args.traffic_gb)
+    if args.traffic_gb is None:   # the PMC summaries in profiles/ are of the single-GPU launches
         roof["traffic"] = None
         for o in roof.get("others", []):
             o["traffic"] = None
-    stages = stage_breakdown(dev, ["shard_hist", "shard_below", "shard_select_count", "shard_pack_select",
-                                   "rccl_allreduce_hist", "rccl_allreduce_counts", "rccl_allgather_bounds",
-                                   "sa_bin_starts", "sa_bucket_sort", "radix_hist", "radix_onesweep",
-                                   "radix_onesweep_small", "shard_split_join", "sa_refine_stats",
-                                   "sa_refine_apply", "sa_refine_keys"])
+    stages = stage_breakdown(dev, SHARD_STAGES)
+    info = dev.build_info()[:16]
+    # ---- replicas + batched locate (patterns split P/N over the ranks)
+    loc = None
+    if args.patterns > 0 and per_gpu == 1:
+        dev.release_workspace()
+        dist.barrier()
+        t0 = time.perf_counter()
+        dev.shard_replicate()
+        dev.synchronize()
+        t_rep = time.perf_counter() - t0
+        t_wt = time_wt(dev, args.wt_reps)
+        data, offs = pattern_batch(dev, n, args.patterns, args.plen, args.seed + 1)
+        P = args.patterns
+        a, b = P * rank // world, P * (rank + 1) // world
+        mine_d = data[int(offs[a]):int(offs[b])]
+        mine_o = offs[a:b + 1] - offs[a]
+        dist.barrier()
+        qq = time_queries(dev, mine_d, mine_o, args.query_reps)
+        ts = torch.tensor([qq["locate_s"], qq["count_s"], t_rep, t_wt], dtype=torch.float64)
+        dist.all_reduce(ts, op=dist.ReduceOp.MAX)
+        occ = torch.tensor([qq["occurrences"]], dtype=torch.int64)
+        dist.all_reduce(occ)
+        loc = {"patterns": P, "plen": args.plen, "occurrences": int(occ.item()),
+               "locate_patterns_per_s": round(P / float(ts[0]), 1), "count_patterns_per_s": round(P / float(ts[1]), 1),
+               "replicate_ms": round(float(ts[2]) * 1e3, 2), "wt_build_ms": round(float(ts[3]) * 1e3, 2),
+               "split": f"P/{world} patterns per rank, max-over-ranks time"}
     res = None
     if rank == 0:
         value = args.steps * n / 2**20 / wall
+        scaling = "strong" if args.strong else "weak"
         res = {
             "metric": METRIC,
             "value": round(value, 2),
@@ -281,24 +460,40 @@ def run_sharded(args, rank: int, world: int, local_rank: int) -> dict | None:
             "warmup": args.warmup,
             "ms_per_step": round(wall / args.steps * 1e3, 3),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": scaling,
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic",
-            "config": {"workload": f"{world} GiB synthetic sigma=4 text sharded over {world} GPUs: partition "
-                                   "histogram + slice counts by RCCL all-reduce, per-rank slice selection, LSD "
-                                   "passes over the slice's bucket bits, LDS bucket sorts, tie refinement, RCCL "
-                                   "all-gather of the slice bounds", "text_symbols": n, "sigma": 4,
-                       "parallelism": f"sa-slices x{world}",
+            "config": {"workload": f"{n - 1} iid sigma=4 symbols + '$' sharded over {world} GPUs"
+                                   + (f" ({per_gpu} slices built one after another)" if per_gpu > 1 else "")
+                                   + ": partition histogram + slice counts by RCCL all-reduce, per-rank slice "
+                                   "selection, LSD passes over the slice's bucket bits, LDS bucket sorts, tie "
+                                   "refinement, RCCL all-gather of per-rank status (ISA rank exchange only for "
+                                   "ties that outlast the chunk rounds); then replicas + batched locate",
+                       "text_symbols": n, "sigma": 4, "parallelism": f"sa-slices x{world}",
                        "positions": "u64" if (n >= 2**32 - 1 or args.pos64) else "u32"},
             "roofline": roof,
-            "locate_patterns_per_s": None,
-            "detail": {"rank0_slice": [lo, hi], "stages_ms_total": stages, "build_info": dev.build_info()[:16]},
+            "locate_patterns_per_s": loc["locate_patterns_per_s"] if loc else None,
+            "detail": {"rank0_slice": [lo, hi], "slices_per_gpu": per_gpu, "locate": loc,
+                       "stages_ms_total": stages, "build_info": info},
         }
     dev.close()
     return res
 
 
+def virtual_slices(dev, k: int):
+    """One GPU builds all k slices of a sharded build one after another (host-driven phases).  Only
+    used when the text has >= 2^32 suffixes on a single GPU; the bench text is iid, so no slice is left
+    tied after its chunk rounds (checked)."""
+    g = sum(dev.shard_histogram(k, r) for r in range(k))
+    below = sum(dev.shard_counts(g, k, r) for r in range(k))
+    for r in range(k):
+        dev.shard_build(g, below, k, r)
+        if dev.shard_status()[2]:
+            raise RuntimeError("virtual slices need a text without ties left after the chunk rounds")
+
+
+# ---------------------------------------------------------------------------- launch
 def _stdout_for_result():
     """Route fd 1 to stderr for the run (RCCL / gloo print banners on stdout) and return a
     stream on the original stdout, so the result stays the only line there."""
@@ -308,47 +503,131 @@ def _stdout_for_result():
     return os.fdopen(saved, "w")
 
 
-def main():
-    result_out = _stdout_for_result()
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launch_check(rank: int, world: int) -> dict | None:
+    """--launch-check: the rendezvous and max-over-ranks reduction of a multi-GPU run, no GPU work
+    (CPU test of the launch logic, tests/test_bench_cpu.py)."""
+    import torch
+    import torch.distributed as dist
+    dist.barrier()
+    t = torch.tensor([float(rank)], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    if rank:
+        return None
+    return {"metric": METRIC, "value": None, "unit": "MB/s", "n_gpus": world, "launch_check":
+            {"world": world, "max_rank": int(t.item()), "local_rank": int(os.environ.get("LOCAL_RANK", "-1"))}}
+
+
+def _rank_entry(argv, rank, world, port, q):
+    """Spawned worker (one process per GPU): fresh interpreter, no GPU state inherited."""
+    os.environ.update({"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port), "RANK": str(rank),
+                       "WORLD_SIZE": str(world), "LOCAL_RANK": str(rank), "LOCAL_WORLD_SIZE": str(world)})
+    args = parse_args(argv)
+    import torch.distributed as dist
+    dist.init_process_group(backend="gloo")
+    try:
+        res = launch_check(rank, world) if args.launch_check else run_sharded(args, rank, world, rank)
+        if rank == 0:
+            q.put(res)
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+def spawn_ranks(argv, world: int) -> dict:
+    """--gpus N without a launcher: start N worker processes (before this process touches the GPU)."""
+    import multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank_entry, args=(argv, r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = None
+    while res is None:
+        try:
+            res = q.get(timeout=5)
+        except Exception:
+            dead = [p for p in procs if p.exitcode not in (None, 0)]
+            if dead or all(p.exitcode is not None for p in procs):
+                for p in procs:
+                    if p.exitcode is None:
+                        p.terminate()
+                raise SystemExit(f"bench: a rank failed (exit codes {[p.exitcode for p in procs]})")
+    for p in procs:
+        p.join(timeout=300)
+        if p.exitcode != 0:
+            raise SystemExit(f"bench: rank exited with {p.exitcode}")
+    return res
+
+
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--text-bytes", type=int, default=1 << 30, help="text symbols per GPU (before '$')")
+    ap.add_argument("--sigma", type=int, default=4, choices=(4, 95, 256), help="alphabet of the headline text")
     ap.add_argument("--seed", type=int, default=2)
     ap.add_argument("--patterns", type=int, default=1_000_000)
     ap.add_argument("--plen", type=int, default=16)
     ap.add_argument("--query-reps", type=int, default=5)
+    ap.add_argument("--wt-reps", type=int, default=3)
+    ap.add_argument("--leg-steps", type=int, default=3)
+    ap.add_argument("--no-legs", action="store_true", help="skip the sigma=256 and printable legs (N = 1)")
     ap.add_argument("--cpu-sample", type=int, default=1 << 17)
+    ap.add_argument("--cpu-config0", type=int, default=1 << 20)
     ap.add_argument("--cpu-patterns", type=int, default=1000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--sharded", action="store_true", help="use the sharded (multi-GPU) build even at N=1")
+    ap.add_argument("--strong", action="store_true", help="fixed text of --strong-bytes over the N GPUs")
+    ap.add_argument("--strong-bytes", type=int, default=1 << 32)
     ap.add_argument("--pos64", action="store_true", help="sharded build with 64-bit positions at any n")
     ap.add_argument("--global-sort", action="store_true",
                     help="single-GPU build by full-width LSD sort of the keys (no LDS bucket sorts)")
+    ap.add_argument("--launch-check", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--traffic-gb", type=float, default=None,
                     help="PMC-measured HBM GB per launch of the dominant kernel; default: profiles/pmc_kernels.json")
-    args = ap.parse_args()
+    return ap.parse_args(argv)
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1 or args.gpus > 1 or args.sharded:
+
+def main():
+    result_out = _stdout_for_result()
+    argv = sys.argv[1:]
+    args = parse_args(argv)
+    launched = "WORLD_SIZE" in os.environ
+    if args.gpus > 1 and not launched:
+        res = spawn_ranks(argv, args.gpus)
+    elif launched or args.gpus > 1 or args.sharded or args.strong:
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        os.environ.setdefault("MASTER_PORT", "29533")
+        os.environ.setdefault("MASTER_PORT", str(_free_port()))
         os.environ.setdefault("RANK", "0")
         os.environ.setdefault("WORLD_SIZE", "1")
         dist.init_process_group(backend="gloo")
         world = dist.get_world_size()
         rank = dist.get_rank()
-        res = run_sharded(args, rank, world, local_rank)
+        if world != args.gpus and rank == 0:
+            log(f"[bench] note: WORLD_SIZE={world} (launcher) with --gpus {args.gpus}")
+        if args.launch_check:
+            res = launch_check(rank, world)
+        else:
+            res = run_sharded(args, rank, world, int(os.environ.get("LOCAL_RANK", "0")))
         dist.barrier()
         dist.destroy_process_group()
     else:
         res = run_single(args)
+        if not args.no_legs:
+            run_extra_legs(args, res)
         if not args.no_cpu_baseline:
-            res["cpu_baseline"] = cpu_baseline(args.cpu_sample, args.cpu_patterns)
+            res["cpu_baseline"] = cpu_baseline(args.cpu_sample, args.cpu_patterns, args.cpu_config0)
     if res is not None:
         if "cpu_baseline" not in res:
             res["cpu_baseline"] = None

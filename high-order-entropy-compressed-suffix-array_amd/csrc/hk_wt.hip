@@ -274,9 +274,12 @@ void build_wt(Index& ix) {
   if (L > 0) {
     ix.seq[0].ensure(n + 64);
     ix.seq[1].ensure(n + 64);
-    k_map_codes<<<grid_for(n), 256, 0, s>>>(ix.bwt.as<uint8_t>(), n, ix.wt_code.as<int16_t>(),
-                                            ix.seq[0].as<uint8_t>());
-    HK_HIP(hipGetLastError());
+    {
+      TimedLaunch t(ix.timer, "wt_map_codes", (double)n * 2);
+      k_map_codes<<<grid_for(n), 256, 0, s>>>(ix.bwt.as<uint8_t>(), n, ix.wt_code.as<int16_t>(),
+                                              ix.seq[0].as<uint8_t>());
+      HK_HIP(hipGetLastError());
+    }
     ix.tile_b.ensure(nlines * 4 + 16);
     ix.tile_a.ensure(nlines * 8 + 16);
     int cur = 0;
