@@ -154,7 +154,7 @@ def cpu_baseline(sample_n: int, npat: int, c0_n: int, seed: int = 3) -> dict:
 # kernels whose roofline bench.py reports: the dominant one (largest summed time) as `roofline`,
 # the others under roofline["others"]
 ROOF_KERNELS = ("sa_bucket_sort", "radix_onesweep_text", "radix_onesweep", "byte_hist")
-WT_KERNELS = ("wt_bits", "wt_partition", "wt_map_codes")
+WT_KERNELS = ("wt_bits", "wt_partition")
 
 
 def pmc_traffic_gb(name: str, leg: str = "") -> float | None:

@@ -220,6 +220,210 @@ __device__ __forceinline__ void bs_load_keys(const uint64_t* __restrict__ keys, 
   for (int k = 0; k < BS_I; ++k) key[k] = sl + 64u * k < it.y ? kb[sl + 64u * k] : 0;
 }
 
+// ---- fast path: one MSD counting pass + comparison ranks inside the bins
+// The order among equal keys does not matter (they go to the tie list and are refined), so the LDS
+// sort need not be stable.  One pass bins the suffixes by the top BF_BITS of their local key with LDS
+// atomics (the returned count is a rank inside the bin, in any order); the bins hold ~2 suffixes for
+// iid text, so each suffix then counts the records of its own bin that sort below it ((remaining key
+// bits, original slot) as one u32: the slot breaks ties, so the ranks form a permutation).  Replaces
+// three stable LSD passes whose match-mask ranking and scatters spent half of their LDS cycles in bank
+// conflicts (profiles/r2_sq_counters.json).  A bin over BF_MAXBIN (skewed keys) falls back to the LSD
+// passes.
+constexpr int BF_BITS = 14;
+constexpr int BF_BINS = 1 << BF_BITS;     // 16384 u16 counters (two per u32) = 32 KiB: aliases BsShared::mt
+constexpr uint32_t BF_MAXBIN = 40;        // <= 63: the bin size and rank fields are 6 bits
+static_assert(BF_BINS * 2 == BS_W * 256 * 8, "bin counters alias the match-mask table");
+
+template <typename V, bool TRACE>
+__device__ __forceinline__ bool bucket_sort_fast(BsShared& sh, uint2 it, const uint64_t (&key)[BS_I], uint32_t vmask,
+                                                 uint32_t s0, int pbe, uint64_t symmask, uint64_t base, int lo,
+                                                 int width, int pb, int hb, const uint32_t* __restrict__ vb,
+                                                 V* __restrict__ sab, uint8_t* __restrict__ bwb,
+                                                 uint64_t* __restrict__ tie_k, V* __restrict__ tie_v,
+                                                 unsigned long long* __restrict__ tie_n, uint64_t (&ts)[8]) {
+  const uint32_t start = it.x, cnt = it.y;
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int fb = width < BF_BITS ? width : BF_BITS;
+  const int kb = width - fb;                              // key bits below the bin (<= 17)
+  const uint32_t wmask = width >= 32 ? ~0u : ((1u << width) - 1);
+  const uint32_t lowmask = (1u << kb) - 1;
+  const uint32_t pmask = (1u << pb) - 1;
+  const uint32_t himask = (1u << hb) - 1;
+  uint32_t* const H2 = reinterpret_cast<uint32_t*>(&sh.mt[0][0]);   // u16 pairs, zero on entry
+  const uint16_t* const H = reinterpret_cast<const uint16_t*>(H2);
+  uint32_t lk[BS_I], r0[BS_H];
+  // ---- 1. bin histogram; the atomic's return value is the suffix's rank inside its bin
+#pragma unroll
+  for (int k = 0; k < BS_I; ++k) {
+    const bool valid = (vmask >> k) & 1u;
+    lk[k] = (uint32_t)((((key[k] >> pbe) & symmask) - base) >> lo) & wmask;
+    uint32_t r = 0;
+    if (valid) {
+      sh.aux[s0 + 64u * k] = (uint16_t)(((uint32_t)(key[k] >> hb) & pmask) | (((uint32_t)key[k] & himask) << pb));
+      const uint32_t bin = lk[k] >> kb, sh16 = 16u * (bin & 1u);
+      r = (atomicAdd(&H2[bin >> 1], 1u << sh16) >> sh16) & 0xFFFFu;   // counts <= 18432: no carry
+    }
+    if (k < BS_H) r0[k] = r; else r0[k - BS_H] |= r << 16;
+  }
+  __syncthreads();
+  if (TRACE) ts[2] = stamp();
+  // ---- 2. exclusive scan of the 16384 counters (16 per thread) and the largest bin
+  uint32_t w8[8], tsum = 0, tmax = 0;
+  {
+    const uint4 a = reinterpret_cast<const uint4*>(H2)[2 * tid];
+    const uint4 b = reinterpret_cast<const uint4*>(H2)[2 * tid + 1];
+    w8[0] = a.x; w8[1] = a.y; w8[2] = a.z; w8[3] = a.w;
+    w8[4] = b.x; w8[5] = b.y; w8[6] = b.z; w8[7] = b.w;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const uint32_t c0 = w8[i] & 0xFFFFu, c1 = w8[i] >> 16;
+      tmax = c0 > tmax ? c0 : tmax;
+      tmax = c1 > tmax ? c1 : tmax;
+      w8[i] = tsum | ((tsum + c0) << 16);   // exclusive starts of the pair, relative to the thread
+      tsum += c0 + c1;
+    }
+  }
+  const uint32_t inc = wave_incl_sum<uint32_t>(tsum);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const uint32_t t = __shfl_xor(tmax, o, 64);
+    tmax = t > tmax ? t : tmax;
+  }
+  uint32_t* const wtot = sh.wloc;    // per-wave totals / maxima
+  if (lane == 63) wtot[wv] = inc;
+  if (lane == 0) wtot[BS_W + wv] = tmax;
+  __syncthreads();
+  uint32_t carry = 0, bmax = 0;
+#pragma unroll
+  for (int w = 0; w < BS_W; ++w) {
+    carry += (uint32_t)w < wv ? wtot[w] : 0u;
+    bmax = wtot[BS_W + w] > bmax ? wtot[BS_W + w] : bmax;
+  }
+  if (bmax > BF_MAXBIN) {   // skewed keys: the LSD passes (match-mask table back to zero)
+    __syncthreads();
+    for (uint32_t i = tid; i < BS_W * 256; i += BS_T) (&sh.mt[0][0])[i] = 0;
+    __syncthreads();
+    return false;
+  }
+  {
+    const uint32_t b0 = carry + inc - tsum;
+    const uint32_t b2 = b0 | (b0 << 16);   // starts <= 18432: no carry between the halves
+    reinterpret_cast<uint4*>(H2)[2 * tid] = make_uint4(b2 + w8[0], b2 + w8[1], b2 + w8[2], b2 + w8[3]);
+    reinterpret_cast<uint4*>(H2)[2 * tid + 1] = make_uint4(b2 + w8[4], b2 + w8[5], b2 + w8[6], b2 + w8[7]);
+  }
+  __syncthreads();
+  if (TRACE) ts[3] = stamp();
+  // the positions (coalesced, original order): in flight across the scatter and the bin ranks
+  uint32_t vv[BS_I];
+#pragma unroll
+  for (int k = 0; k < BS_I; ++k) vv[k] = ((vmask >> k) & 1u) ? vb[s0 + 64u * k] : 0u;
+  // ---- 3. records (low key bits, original slot) to their bins
+#pragma unroll
+  for (int k = 0; k < BS_I; ++k) {
+    if ((vmask >> k) & 1u) {
+      const uint32_t r = k < BS_H ? (r0[k] & 0xFFFFu) : (r0[k - BS_H] >> 16);
+      sh.buf[H[lk[k] >> kb] + r] = ((lk[k] & lowmask) << 15) | (s0 + 64u * k);
+    }
+  }
+  __syncthreads();
+  // ---- 4. rank inside the bin: records below (key, slot); equal keys are ties, the smallest slot heads
+  if (TRACE) ts[4] = stamp();
+  // Per item one register: bin start s (bits 0..14) | bin size c (15..20) | records below (21..26) |
+  // an equal key (27) | an equal key with a smaller slot (28); `my` = the item's own record.  One trip
+  // count for the wave (its largest bin); the 18 items' record reads are interleaved per step so their
+  // LDS latencies overlap.
+  uint32_t sc[BS_I], my[BS_I], cmax = 0;
+#pragma unroll
+  for (int k = 0; k < BS_I; ++k) {
+    uint32_t st = 0, c = 0;
+    if ((vmask >> k) & 1u) {
+      const uint32_t bin = lk[k] >> kb;
+      st = H[bin];
+      c = (bin + 1 < (uint32_t)BF_BINS ? H[bin + 1] : cnt) - st;
+    }
+    sc[k] = st | (c << 15);
+    my[k] = ((lk[k] & lowmask) << 15) | (s0 + 64u * k);
+    cmax = c > cmax ? c : cmax;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const uint32_t t = __shfl_xor(cmax, o, 64);
+    cmax = t > cmax ? t : cmax;
+  }
+  cmax = __builtin_amdgcn_readfirstlane(cmax);
+  for (uint32_t i = 0; i < cmax; ++i) {
+#pragma unroll
+    for (int k = 0; k < BS_I; ++k) {
+      const uint32_t c = (sc[k] >> 15) & 63u;
+      const bool in = i < c;
+      const uint32_t r = sh.buf[(sc[k] & 0x7FFFu) + (in ? i : 0u)];
+      const bool ek = in && (r >> 15) == (my[k] >> 15);
+      sc[k] = (sc[k] + (in && r < my[k] ? (1u << 21) : 0u)) | (ek && r != my[k] ? (1u << 27) : 0u) |
+              (ek && r < my[k] ? (1u << 28) : 0u);
+    }
+  }
+  if (TRACE) ts[5] = stamp();
+  uint32_t fin[BS_H], tmask = 0, hmask = 0;
+#pragma unroll
+  for (int k = 0; k < BS_I; ++k) {
+    const bool valid = (vmask >> k) & 1u;
+    const uint32_t f = valid ? (sc[k] & 0x7FFFu) + ((sc[k] >> 21) & 63u) : cnt;
+    const bool tied = valid && ((sc[k] >> 27) & 1u);
+    tmask |= (tied ? 1u : 0u) << k;
+    hmask |= (tied && !((sc[k] >> 28) & 1u) ? 1u : 0u) << k;
+    if (k < BS_H) fin[k] = f; else fin[k - BS_H] |= f << 16;
+  }
+  uint16_t pvr[BS_I];
+#pragma unroll
+  for (int k = 0; k < BS_I; ++k) pvr[k] = sh.aux[s0 + 64u * k];
+  // tie-list space: one global atomic per workgroup, each thread's ties at a block-scanned offset
+  const uint32_t nt = __popc(tmask);
+  const uint32_t tinc = wave_incl_sum<uint32_t>(nt);
+  uint32_t* const wt = reinterpret_cast<uint32_t*>(&sh.rv[0][0]);
+  if (lane == 63) wt[wv] = tinc;
+  __syncthreads();   // every record / pv read is done: buf / aux become the sorted staging planes
+  if (tid == 0) {
+    uint32_t tot = 0;
+#pragma unroll
+    for (int w = 0; w < BS_W; ++w) tot += wt[w];
+    sh.rv[1][0] = tot ? atomicAdd(tie_n, (unsigned long long)tot) : 0ull;
+  }
+  // ---- 5. stage (position, prev code) by final index
+#pragma unroll
+  for (int k = 0; k < BS_I; ++k) {
+    if ((vmask >> k) & 1u) {
+      const uint32_t f = k < BS_H ? (fin[k] & 0xFFFFu) : (fin[k - BS_H] >> 16);
+      sh.buf[f] = vv[k];
+      sh.aux[f] = pvr[k];
+    }
+  }
+  __syncthreads();
+  if (TRACE) ts[6] = stamp();
+  uint64_t tpos = sh.rv[1][0] + (tinc - nt);
+  for (uint32_t w = 0; w < wv; ++w) tpos += wt[w];
+#pragma unroll
+  for (int k = 0; k < BS_I; ++k) {
+    if ((tmask >> k) & 1u) {
+      const uint32_t f = k < BS_H ? (fin[k] & 0xFFFFu) : (fin[k - BS_H] >> 16);
+      const uint32_t pv = pvr[k];
+      tie_k[tpos] = (((uint64_t)start + f) << 1) | ((hmask >> k) & 1u);
+      tie_v[tpos] = (V)(((uint64_t)(pv >> pb) << 32) | vv[k]);
+      ++tpos;
+    }
+  }
+  // ---- 6. SA / BWT in sorted order
+#pragma unroll
+  for (int k = 0; k < BS_I; ++k) {
+    const uint32_t r = s0 + 64u * k;
+    if (r < cnt) {
+      const uint32_t pv = sh.aux[r];
+      sab[r] = (V)(((uint64_t)(pv >> pb) << 32) | sh.buf[r]);
+      bwb[r] = sh.inv[pv & pmask];
+    }
+  }
+  return true;
+}
+
 // One work item of the LDS bucket sort, its keys in `key` (slot order).
 template <bool WIDE, bool TRACE, typename V>
 __device__ __forceinline__ void bucket_sort_item(BsShared& sh, uint2 it, const uint64_t (&key)[BS_I],
@@ -573,6 +777,92 @@ __global__ __launch_bounds__(BS_T, 1) void k_bucket_sort(const uint64_t* __restr
                                    tie_v, tie_n, trace);
 }
 
+// Fast-path kernel: the same prologue (the item's sym range and varying bits), then the MSD + bin-rank
+// sort; items it cannot take (wide keys, a bin over BF_MAXBIN) are appended to `fb` for k_bucket_sort.
+template <typename V, bool TRACE>
+__global__ __launch_bounds__(BS_T, 1) void k_bucket_sort_fast(const uint64_t* __restrict__ keys,
+                                                              const uint32_t* __restrict__ vals,
+                                                              const uint2* __restrict__ items, int pb, int sb, int hb,
+                                                              uint64_t symbias, const uint8_t* __restrict__ inv,
+                                                              V* __restrict__ sa, uint8_t* __restrict__ bwt,
+                                                              uint64_t* __restrict__ tie_k, V* __restrict__ tie_v,
+                                                              unsigned long long* __restrict__ tie_n,
+                                                              uint2* __restrict__ fb, unsigned int* __restrict__ fb_n,
+                                                              uint64_t* __restrict__ trace) {
+  __shared__ BsShared sh;
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  uint64_t ts[8] = {0};
+  if (TRACE) ts[0] = stamp();
+  if (tid < 256) sh.inv[tid] = inv[tid];
+  const uint2 it = items[blockIdx.x];
+  uint64_t key[BS_I];
+  bs_load_keys(keys, it, key);
+  const uint32_t s0 = wv * BS_WSPAN + lane;
+  uint32_t vmask = 0;
+#pragma unroll
+  for (int k = 0; k < BS_I; ++k) vmask |= (s0 + 64u * k < it.y ? 1u : 0u) << k;
+
+  const uint64_t symmask = sb >= 64 ? ~0ull : ((1ull << sb) - 1);
+  const int pbe = pb + hb;
+  for (uint32_t i = tid; i < BS_W * 256; i += BS_T) (&sh.mt[0][0])[i] = 0;
+  uint64_t xmin = ~0ull;
+#pragma unroll
+  for (int k = 0; k < BS_I; ++k)
+    if ((vmask >> k) & 1u) {
+      const uint64_t x = ((key[k] >> pbe) & symmask) - symbias;
+      xmin = x < xmin ? x : xmin;
+    }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const uint64_t t = __shfl_xor(xmin, o, 64);
+    xmin = t < xmin ? t : xmin;
+  }
+  if (lane == 0) sh.rv[0][wv] = xmin;
+  __syncthreads();
+#pragma unroll
+  for (int w = 0; w < BS_W; ++w) xmin = sh.rv[0][w] < xmin ? sh.rv[0][w] : xmin;
+  const uint64_t base = symbias + xmin;
+  uint64_t vor = 0, vand = ~0ull;
+#pragma unroll
+  for (int k = 0; k < BS_I; ++k)
+    if ((vmask >> k) & 1u) {
+      const uint64_t sym = ((key[k] >> pbe) & symmask) - base;
+      vor |= sym;
+      vand &= sym;
+    }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    vor |= __shfl_xor(vor, o, 64);
+    vand &= __shfl_xor(vand, o, 64);
+  }
+  __syncthreads();
+  if (lane == 0) {
+    sh.rv[0][wv] = vor;
+    sh.rv[1][wv] = vand;
+  }
+  __syncthreads();
+  vor = 0;
+  vand = ~0ull;
+#pragma unroll
+  for (int w = 0; w < BS_W; ++w) {
+    vor |= sh.rv[0][w];
+    vand &= sh.rv[1][w];
+  }
+  const uint64_t var = vor ^ vand;
+  const int lo = var ? __builtin_ctzll(var) : 0;
+  const int width = var ? 64 - __builtin_clzll(var) - lo : 0;
+  if (TRACE) ts[1] = stamp();
+  const bool ok = width >= 1 && width <= 30 &&
+                  bucket_sort_fast<V, TRACE>(sh, it, key, vmask, s0, pbe, symmask, base, lo, width, pb, hb, vals + it.x,
+                                      sa + it.x, bwt + it.x, tie_k, tie_v, tie_n, ts);
+  if (!ok && tid == 0) fb[atomicAdd(fb_n, 1u)] = it;
+  if (TRACE) {
+    ts[7] = stamp();
+    if (tid == 0)
+      for (int i = 0; i < 8; ++i) trace[(uint64_t)blockIdx.x * 8 + i] = ts[i];
+  }
+}
+
 // ------------------------------------------------------------ 5. big buckets
 // compacted copy of the big buckets: key top D bits replaced by the big-bucket ordinal, J = slot
 __global__ __launch_bounds__(256) void k_big_gather(const uint64_t* __restrict__ keys,
@@ -638,13 +928,14 @@ inline unsigned grid_of(uint64_t n, unsigned cap = 16384) {
 
 // bucket = sym >> bsh for m suffixes whose sym fields span `span` values: the largest shift that keeps
 // the uniform-model mean bucket at <= 16.5k suffixes (one LDS sort holds 18432), with D = sb - bsh in
-// [1, 16] (bsh = sb, i.e. one bucket, when one sort holds all)
-int bucket_shift(uint64_t m, int sb, unsigned __int128 span) {
+// [1, maxD] (bsh = sb, i.e. one bucket, when one sort holds all).  maxD = 16 keeps the LSD passes over
+// the bucket bits at two; sharded slices of more than ~1.2G suffixes use up to 18 (a third pass).
+int bucket_shift(uint64_t m, int sb, unsigned __int128 span, int maxD = 16) {
   if (m <= (uint64_t)BS_CAP) return sb;
   const double l = std::log2(16500.0 * (double)span / (double)m);
   int b = (int)std::floor(l);
   b = std::min(b, sb - 1);
-  b = std::max(b, sb - 16);
+  b = std::max(b, sb - maxD);
   return std::max(b, 0);
 }
 
@@ -723,10 +1014,45 @@ uint64_t sort_bucket_items(Index& ix, const BucketPlan& plan, const uint64_t* ke
   {
     TimedLaunch t(ix.timer, "sa_bucket_sort", (double)(m - plan.big_total) * (8 + 4 + 4 + 1));
     static const bool trace = getenv("HKCSA_BS_TRACE") != nullptr;   // diagnostic phase stamps
+    // HKCSA_BS_FAST=0: the three stable LSD passes everywhere (A/B diagnostic)
+    static const int fast = getenv("HKCSA_BS_FAST") ? atoi(getenv("HKCSA_BS_FAST")) : 1;
     const unsigned grid_n = (unsigned)nn, grid_w = (unsigned)nw;
     DevBuf tbuf;
     if (trace && nn) tbuf.ensure(nn * 64 + 64);
-    if (nn) {
+    if (nn && fast) {
+      if (trace) tbuf.ensure(nn * 64 + 64);
+      ix.bk_fb.ensure(nn * sizeof(uint2) + 16);
+      unsigned int* fbn = reinterpret_cast<unsigned int*>(ix.small.as<uint8_t>() + 4352);   // small+4352: fallback count
+      HK_HIP(hipMemsetAsync(fbn, 0, 4, s));
+      if (trace)
+        k_bucket_sort_fast<V, true><<<grid_n, BS_T, 0, s>>>(
+            keys, vals, ix.bk_items.as<uint2>(), pb, sb, hb, symbias, d_inv, sa, bwt, ix.ties_k.as<uint64_t>(),
+            ix.ties_v.as<V>(), ix.ties_n.as<unsigned long long>(), ix.bk_fb.as<uint2>(), fbn, tbuf.as<uint64_t>());
+      else
+        k_bucket_sort_fast<V, false><<<grid_n, BS_T, 0, s>>>(
+            keys, vals, ix.bk_items.as<uint2>(), pb, sb, hb, symbias, d_inv, sa, bwt, ix.ties_k.as<uint64_t>(),
+            ix.ties_v.as<V>(), ix.ties_n.as<unsigned long long>(), ix.bk_fb.as<uint2>(), fbn, nullptr);
+      HK_HIP(hipGetLastError());
+      if (trace) {
+        std::vector<uint64_t> h(nn * 8);
+        HK_HIP(hipMemcpyAsync(h.data(), tbuf.p, h.size() * 8, hipMemcpyDeviceToHost, s));
+        HK_HIP(hipStreamSynchronize(s));
+        double acc[7] = {0, 0, 0, 0, 0, 0, 0};
+        for (size_t w = 0; w < nn; ++w)
+          for (int i = 0; i < 7; ++i) acc[i] += (double)(h[w * 8 + i + 1] - h[w * 8 + i]);
+        fprintf(stderr, "[bucket_sort_fast trace] %zu WGs, mean cycles: load+prologue %.0f, hist %.0f, scan %.0f, "
+                "scatter %.0f, rank %.0f, stage+ties %.0f, out %.0f\n", (size_t)nn, acc[0] / nn, acc[1] / nn,
+                acc[2] / nn, acc[3] / nn, acc[4] / nn, acc[5] / nn, acc[6] / nn);
+      }
+      unsigned int nfb = 0;
+      HK_HIP(hipMemcpyAsync(&nfb, fbn, 4, hipMemcpyDeviceToHost, s));
+      HK_HIP(hipStreamSynchronize(s));
+      ix.info[8] += nfb;   // items sorted by the LSD passes (a bin over BF_MAXBIN, or wide local keys)
+      if (nfb)
+        k_bucket_sort<false, false, V><<<nfb, BS_T, 0, s>>>(
+            keys, vals, ix.bk_fb.as<uint2>(), pb, sb, hb, symbias, d_inv, sa, bwt, ix.ties_k.as<uint64_t>(),
+            ix.ties_v.as<V>(), ix.ties_n.as<unsigned long long>(), nullptr);
+    } else if (nn) {
       if (trace && sizeof(V) == 4)
         k_bucket_sort<false, true, V><<<grid_n, BS_T, 0, s>>>(
             keys, vals, ix.bk_items.as<uint2>(), pb, sb, hb, symbias, d_inv, sa, bwt, ix.ties_k.as<uint64_t>(),
@@ -741,7 +1067,7 @@ uint64_t sort_bucket_items(Index& ix, const BucketPlan& plan, const uint64_t* ke
           keys, vals, ix.bk_items.as<uint2>() + nn, pb, sb, hb, symbias, d_inv, sa, bwt, ix.ties_k.as<uint64_t>(),
           ix.ties_v.as<V>(), ix.ties_n.as<unsigned long long>(), nullptr);
     HK_HIP(hipGetLastError());
-    if (trace && nn && sizeof(V) == 4) {
+    if (trace && nn && !fast && sizeof(V) == 4) {
       std::vector<uint64_t> h(nn * 8);
       HK_HIP(hipMemcpyAsync(h.data(), tbuf.p, h.size() * 8, hipMemcpyDeviceToHost, s));
       HK_HIP(hipStreamSynchronize(s));
@@ -939,7 +1265,7 @@ SliceBins slice_bins(uint64_t m, const KeyGeom& kg, int hb, uint64_t kmin, uint6
   b.binpos = kg.pb + hb + kg.sym_bits;
   const unsigned __int128 span = (unsigned __int128)(kmax - kmin) + 1;
   const int sbl = std::max(1, bits_of((unsigned __int128)(kmax - kmin)));   // bits of the slice's sym range
-  b.bsh = bucket_shift(m, sbl, span);
+  b.bsh = bucket_shift(m, sbl, span, 18);
   b.D = sbl - b.bsh;
   if (b.D <= 0) {
     b.D = 0;
@@ -949,10 +1275,13 @@ SliceBins slice_bins(uint64_t m, const KeyGeom& kg, int hb, uint64_t kmin, uint6
   // 2^16 bins and leaves every bucket over one sort's capacity.  Multiplicative bins (exactly 2^16
   // over the range) need 16 free key bits above the sym field.
   const double mean = (double)m / (double)(((kmax - kmin) >> b.bsh) + 1);
-  if ((mean > 16500.0 || force_mul) && b.binpos + 16 <= 64 && span > ((unsigned __int128)1 << 16)) {
-    b.mul = (uint64_t)((((unsigned __int128)1) << 80) / span);   // hi64(x * mul) < 2^16 for x < span
-    b.D = 16;
-    b.bsh = bits_of(span >> 16) + 1;
+  // multiplicative bins: 2^Dm over the range, Dm = 16 .. 18 (the fewest that keep the mean <= 16.5k)
+  int Dm = 16;
+  while (Dm < 18 && (double)m / (double)(1u << Dm) > 16500.0) ++Dm;
+  if ((mean > 16500.0 || force_mul) && b.binpos + Dm <= 64 && span > ((unsigned __int128)1 << Dm)) {
+    b.mul = (uint64_t)((((unsigned __int128)1) << (64 + Dm)) / span);   // hi64(x * mul) < 2^Dm for x < span
+    b.D = Dm;
+    b.bsh = bits_of(span >> Dm) + 1;
   }
   return b;
 }
@@ -1032,7 +1361,7 @@ void build_sa_bucketed(Index& ix) {
   if (n >= 0xFFFFFFFFull) throw ApiError{-6, "single-GPU build supports n < 2^32 - 1"};
   ix.have_alpha = false;   // every build recomputes the byte histogram / C (utils/utils.py:16-24)
   compute_alphabet(ix);
-  ix.info.assign(8, 0);
+  ix.info.assign(9, 0);
   ix.dbl = Index::DblState{};
   ix.sharded = false;
   ix.sa_pos64 = false;

@@ -87,7 +87,7 @@ struct Index {
   int wt_levels = 0;
   DevBuf wt_lines[kMaxLevels];
   uint64_t wt_nlines = 0;
-  DevBuf wt_obn, wt_rbase, wt_bit, wt_depth, wt_code, wt_C;
+  DevBuf wt_obn, wt_rbase, wt_bit, wt_depth, wt_code, wt_C, wt_lut;
   WtTables tabs;
 
   // construction workspace (kept across builds so repeated builds do not allocate)
@@ -98,7 +98,7 @@ struct Index {
   DevBuf head_slot;            // SA slot of each tied group's head (refinement -> doubling switch)
   DevBuf ties_k, ties_v, ties_n;   // unordered tie list of the bucket build (J<<1|head, P), count
   DevBuf big_k[2], big_v[2], big_j; // big buckets of the bucket build (sorted on the global path)
-  DevBuf bk_items, bk_hist;       // bucket work items, bucket histogram
+  DevBuf bk_items, bk_hist, bk_fb; // bucket work items, bucket histogram, fast-path fallback items
   DevBuf sel;                     // sharded build: selection masks of the slice (u16 per 16 positions)
   DevBuf tile_a, tile_b, tile_c, tile_d, tile_e;
   DevBuf small;                // scratch for totals etc.

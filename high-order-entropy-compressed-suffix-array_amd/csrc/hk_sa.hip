@@ -70,15 +70,30 @@ __device__ __forceinline__ uint64_t blk_excl_max(uint64_t v, uint64_t* red) {
 }
 
 // ------------------------------------------------------------- alphabet
+// Each wave keeps BHC copies of the 256 counters (lane l adds to copy l % BHC, rows 257 apart so the
+// copies of one byte sit in different banks): with one copy per wave a small alphabet (DNA: 4 bytes)
+// sent every lane's atomic to the same few addresses (79 % of the LDS cycles were conflicts,
+// profiles/r2_sq_counters.json).
+constexpr int BHC = 8;
 __global__ __launch_bounds__(256) void k_byte_hist(const uint8_t* __restrict__ t, uint64_t n,
                                                    unsigned long long* __restrict__ hist) {
-  __shared__ uint32_t h[4][256];
-  for (int i = threadIdx.x; i < 4 * 256; i += 256) (&h[0][0])[i] = 0;
+  __shared__ uint32_t h[4 * BHC * 257];
+  for (int i = threadIdx.x; i < 4 * BHC * 257; i += 256) h[i] = 0;
   __syncthreads();
-  uint32_t* mine = h[(threadIdx.x >> 6) & 3];
+  uint32_t* mine = h + ((threadIdx.x >> 6) * BHC + (threadIdx.x & (BHC - 1))) * 257;
   const uint64_t nv = n / 16;
   const uint4* t4 = reinterpret_cast<const uint4*>(t);
-  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < nv; i += (uint64_t)gridDim.x * 256) {
+  const uint64_t stride = (uint64_t)gridDim.x * 256;
+  uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  for (; i + stride < nv; i += 2 * stride) {   // two 16-byte loads in flight per lane
+    const uint4 v0 = t4[i], v1 = t4[i + stride];
+    const uint32_t w[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+#pragma unroll
+      for (int b = 0; b < 4; ++b) atomicAdd(&mine[(w[q] >> (8 * b)) & 255], 1u);
+  }
+  for (; i < nv; i += stride) {
     const uint4 v = t4[i];
     const uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
@@ -87,9 +102,11 @@ __global__ __launch_bounds__(256) void k_byte_hist(const uint8_t* __restrict__ t
       for (int b = 0; b < 4; ++b) atomicAdd(&mine[(w[q] >> (8 * b)) & 255], 1u);
   }
   if (blockIdx.x == 0)
-    for (uint64_t i = nv * 16 + threadIdx.x; i < n; i += 256) atomicAdd(&mine[t[i]], 1u);
+    for (uint64_t j = nv * 16 + threadIdx.x; j < n; j += 256) atomicAdd(&mine[t[j]], 1u);
   __syncthreads();
-  const uint32_t c = h[0][threadIdx.x] + h[1][threadIdx.x] + h[2][threadIdx.x] + h[3][threadIdx.x];
+  uint32_t c = 0;
+#pragma unroll 8
+  for (int r = 0; r < 4 * BHC; ++r) c += h[r * 257 + threadIdx.x];
   if (c) atomicAdd(&hist[threadIdx.x], (unsigned long long)c);
 }
 
@@ -941,7 +958,7 @@ void build_sa(Index& ix) {
   if (n >= 0xFFFFFFFFull) throw ApiError{-6, "single-GPU build supports n < 2^32 - 1"};
   ix.have_alpha = false;   // every build recomputes the byte histogram / C (utils/utils.py:16-24)
   compute_alphabet(ix);
-  ix.info.assign(4, 0);
+  ix.info.assign(9, 0);
   ix.dbl = Index::DblState{};
   ix.sharded = false;
   ix.sa_pos64 = false;

@@ -673,7 +673,7 @@ void shard_build_t(Index& ix, const uint64_t* ghist, const uint64_t* gbelow, int
   ix.shard_lo = gbelow[rank];
   ix.shard_hi = gbelow[rank + 1];
   const uint64_t m = ix.shard_hi - ix.shard_lo;
-  ix.info.assign(8, 0);
+  ix.info.assign(9, 0);
   ix.dbl = Index::DblState{};
   ix.sharded = true;
   ix.sa_pos64 = sizeof(V) == 8;

@@ -40,17 +40,13 @@ WtView Index::view() const {
 
 namespace {
 
-__global__ __launch_bounds__(256) void k_map_codes(const uint8_t* __restrict__ in, uint64_t n,
-                                                   const int16_t* __restrict__ code,
-                                                   uint8_t* __restrict__ out) {
-  __shared__ uint8_t L[256];
-  L[threadIdx.x] = (uint8_t)code[threadIdx.x];
-  __syncthreads();
-  for (uint64_t j = (uint64_t)blockIdx.x * 256 + threadIdx.x; j < n; j += (uint64_t)gridDim.x * 256)
-    out[j] = L[in[j]];
-}
+// Level kernels process WT_G lines (448 symbols each) per wave iteration with all their symbol loads
+// issued up front (one byte per lane per 64 symbols): the single-line form kept only 7 x 64 B in
+// flight per wave and ran latency-bound at 10-20 % of HBM bandwidth (profiles/r2_kernel_stats.csv).
+// Level 0 reads the BWT bytes themselves through a byte -> code table (no separate code-mapping pass).
+constexpr int WT_G = 4;
 
-// one wave per 448-symbol line: 7 ballots -> 7 words; word 0 later receives the ones-before count
+// one wave per WT_G lines: 7 ballots per line -> 7 words; word 0 later receives the ones-before count
 __global__ __launch_bounds__(256) void k_wt_bits(const uint8_t* __restrict__ S, uint64_t n,
                                                  const uint8_t* __restrict__ bitlut,
                                                  uint64_t* __restrict__ lines,
@@ -59,24 +55,33 @@ __global__ __launch_bounds__(256) void k_wt_bits(const uint8_t* __restrict__ S, 
   B[threadIdx.x] = bitlut[threadIdx.x];
   __syncthreads();
   const uint32_t lane = threadIdx.x & 63;
-  for (uint64_t li = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6); li < nlines;
-       li += (uint64_t)gridDim.x * 4) {
-    const uint64_t base = li * kLineBits;
-    uint64_t w[7];
-    uint32_t pop = 0;
+  for (uint64_t g = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6); g * WT_G < nlines; g += (uint64_t)gridDim.x * 4) {
+    const uint64_t base = g * WT_G * kLineBits;
+    uint8_t sym[WT_G * 7];
 #pragma unroll
-    for (int i = 0; i < 7; ++i) {
+    for (int i = 0; i < WT_G * 7; ++i) {
       const uint64_t j = base + (uint64_t)i * 64 + lane;
-      const bool bit = j < n && B[S[j]];
-      w[i] = ballot64(bit);
-      pop += (uint32_t)__popcll(w[i]);
+      sym[i] = j < n ? S[j] : 0;
     }
-    uint64_t v = 0;
 #pragma unroll
-    for (int i = 0; i < 7; ++i)
-      if (lane == (uint32_t)i + 1) v = w[i];
-    if (lane < 8) lines[li * 8 + lane] = v;
-    if (lane == 0) line_pop[li] = pop;
+    for (int q = 0; q < WT_G; ++q) {
+      const uint64_t li = g * WT_G + q;
+      if (li >= nlines) break;
+      uint64_t w[7];
+      uint32_t pop = 0;
+#pragma unroll
+      for (int i = 0; i < 7; ++i) {
+        const uint64_t j = base + (uint64_t)(q * 7 + i) * 64 + lane;
+        w[i] = ballot64(j < n && B[sym[q * 7 + i]]);
+        pop += (uint32_t)__popcll(w[i]);
+      }
+      uint64_t v = 0;
+#pragma unroll
+      for (int i = 0; i < 7; ++i)
+        if (lane == (uint32_t)i + 1) v = w[i];
+      if (lane >= 1 && lane < 8) lines[li * 8 + lane] = v;
+      if (lane == 0) line_pop[li] = pop;
+    }
   }
 }
 
@@ -97,33 +102,48 @@ __global__ void k_wt_tables(const uint64_t* __restrict__ lines, int sigma,
   }
 }
 
-// stable partition of level d's sequence into level d+1 (one wave per line)
+// stable partition of level d's sequence into level d+1 (one wave per WT_G lines); `code` maps the
+// input symbols to dense codes (level 0 reads BWT bytes) or is the identity
 __global__ __launch_bounds__(256) void k_wt_partition(const uint8_t* __restrict__ S, uint8_t* __restrict__ out,
                                                       uint64_t n, const uint64_t* __restrict__ lines,
                                                       uint64_t nlines, const uint64_t* __restrict__ obn,
-                                                      const uint64_t* __restrict__ rbase) {
+                                                      const uint64_t* __restrict__ rbase,
+                                                      const uint8_t* __restrict__ code) {
   __shared__ uint64_t OB[256], RB[256];
+  __shared__ uint8_t CODE[256];
   OB[threadIdx.x] = obn[threadIdx.x];
   RB[threadIdx.x] = rbase[threadIdx.x];
+  CODE[threadIdx.x] = code[threadIdx.x];
   __syncthreads();
   const uint32_t lane = threadIdx.x & 63;
-  for (uint64_t li0 = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6); li0 < nlines;
-       li0 += (uint64_t)gridDim.x * 4) {
-    const uint64_t li = __builtin_amdgcn_readfirstlane((uint32_t)li0);
-    const uint64_t* L = lines + li * 8;
-    uint64_t pre = L[0];
-    const uint64_t base = li * kLineBits;
+  for (uint64_t g0 = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6); g0 * WT_G < nlines;
+       g0 += (uint64_t)gridDim.x * 4) {
+    const uint64_t g = __builtin_amdgcn_readfirstlane((uint32_t)g0);
+    const uint64_t base = g * WT_G * kLineBits;
+    uint8_t sym[WT_G * 7];
 #pragma unroll
-    for (int i = 0; i < 7; ++i) {
-      const uint64_t w = L[1 + i];
+    for (int i = 0; i < WT_G * 7; ++i) {
       const uint64_t j = base + (uint64_t)i * 64 + lane;
-      if (j < n) {
-        const uint8_t c = S[j];
-        const uint64_t ob = pre + mbcnt(w);
-        const uint64_t dst = ((w >> lane) & 1ull) ? RB[c] + ob : j - ob + OB[c];
-        out[dst] = c;
+      sym[i] = j < n ? S[j] : 0;
+    }
+#pragma unroll
+    for (int q = 0; q < WT_G; ++q) {
+      const uint64_t li = g * WT_G + q;
+      if (li >= nlines) break;
+      const uint64_t* L = lines + li * 8;
+      uint64_t pre = L[0];
+#pragma unroll
+      for (int i = 0; i < 7; ++i) {
+        const uint64_t w = L[1 + i];
+        const uint64_t j = base + (uint64_t)(q * 7 + i) * 64 + lane;
+        if (j < n) {
+          const uint8_t c = CODE[sym[q * 7 + i]];
+          const uint64_t ob = pre + mbcnt(w);
+          const uint64_t dst = ((w >> lane) & 1ull) ? RB[c] + ob : j - ob + OB[c];
+          out[dst] = c;
+        }
+        pre += (uint64_t)__popcll(w);
       }
-      pre += (uint64_t)__popcll(w);
     }
   }
 }
@@ -274,23 +294,31 @@ void build_wt(Index& ix) {
   if (L > 0) {
     ix.seq[0].ensure(n + 64);
     ix.seq[1].ensure(n + 64);
-    {
-      TimedLaunch t(ix.timer, "wt_map_codes", (double)n * 2);
-      k_map_codes<<<grid_for(n), 256, 0, s>>>(ix.bwt.as<uint8_t>(), n, ix.wt_code.as<int16_t>(),
-                                              ix.seq[0].as<uint8_t>());
-      HK_HIP(hipGetLastError());
+    // level 0 reads the BWT bytes: byte -> level-0 bit and byte -> dense code tables; deeper levels
+    // read dense codes (identity code table)
+    uint8_t lut0[2][256];
+    for (int b = 0; b < 256; ++b) {
+      const int c = ix.code_of[b];
+      lut0[0][b] = c < 0 ? 0 : T.bit[0][c];
+      lut0[1][b] = (uint8_t)(c < 0 ? 0 : c);
     }
+    uint8_t ident[256];
+    for (int b = 0; b < 256; ++b) ident[b] = (uint8_t)b;
+    ix.wt_lut.ensure(3 * 256);
+    HK_HIP(hipMemcpyAsync(ix.wt_lut.p, lut0, sizeof(lut0), hipMemcpyHostToDevice, s));
+    HK_HIP(hipMemcpyAsync(ix.wt_lut.as<uint8_t>() + 512, ident, 256, hipMemcpyHostToDevice, s));
     ix.tile_b.ensure(nlines * 4 + 16);
     ix.tile_a.ensure(nlines * 8 + 16);
     int cur = 0;
-    const unsigned gl = grid_for(nlines, 4, 8192);
+    const unsigned gl = grid_for(ceil_div(nlines, WT_G), 4, 8192);
     for (int d = 0; d < L; ++d) {
       ix.wt_lines[d].ensure(nlines * 64);
       uint64_t* lines = ix.wt_lines[d].as<uint64_t>();
+      const uint8_t* in = d == 0 ? ix.bwt.as<uint8_t>() : ix.seq[cur].as<uint8_t>();
       {
         TimedLaunch t(ix.timer, "wt_bits", (double)n * (1 + 1.0 / 8));
-        k_wt_bits<<<gl, 256, 0, s>>>(ix.seq[cur].as<uint8_t>(), n, ix.wt_bit.as<uint8_t>() + d * 256, lines,
-                                     ix.tile_b.as<uint32_t>(), nlines);
+        k_wt_bits<<<gl, 256, 0, s>>>(in, n, d == 0 ? ix.wt_lut.as<uint8_t>() : ix.wt_bit.as<uint8_t>() + d * 256,
+                                     lines, ix.tile_b.as<uint32_t>(), nlines);
         HK_HIP(hipGetLastError());
       }
       scan_exclusive_u32_to_u64(ix.sw, ix.tile_b.as<uint32_t>(), ix.tile_a.as<uint64_t>(), nlines, false, s);
@@ -302,11 +330,12 @@ void build_wt(Index& ix) {
       HK_HIP(hipGetLastError());
       if (d + 1 < L) {
         TimedLaunch t(ix.timer, "wt_partition", (double)n * (1 + 1 + 1.0 / 8));
-        k_wt_partition<<<gl, 256, 0, s>>>(ix.seq[cur].as<uint8_t>(), ix.seq[cur ^ 1].as<uint8_t>(), n, lines,
-                                          nlines, ix.wt_obn.as<uint64_t>() + d * 256,
-                                          ix.wt_rbase.as<uint64_t>() + d * 256);
+        uint8_t* outp = d == 0 ? ix.seq[0].as<uint8_t>() : ix.seq[cur ^ 1].as<uint8_t>();
+        k_wt_partition<<<gl, 256, 0, s>>>(in, outp, n, lines, nlines, ix.wt_obn.as<uint64_t>() + d * 256,
+                                          ix.wt_rbase.as<uint64_t>() + d * 256,
+                                          ix.wt_lut.as<uint8_t>() + (d == 0 ? 256 : 512));
         HK_HIP(hipGetLastError());
-        cur ^= 1;
+        if (d > 0) cur ^= 1;
       }
     }
   }

@@ -267,7 +267,8 @@ int hkcsa_kernel_stats(hkcsa_index* ix, const char* name, uint64_t* launches, do
                        double* alg_bytes);
 /* Build-stage counters of the last build: [0] radix passes run, [1] skipped,
  * [2] refinement rounds (doubling rounds << 32), [3] symbols per key; bucket build:
- * [4] LDS work items, [5] big buckets, [6] suffixes in big buckets, [7] 1 = global path;
+ * [4] LDS work items, [5] big buckets, [6] suffixes in big buckets, [7] 1 = global path,
+ * [8] LDS work items sorted by the stable LSD passes instead of the MSD bin-rank fast path;
  * then tied suffixes per round (up to cap). */
 int hkcsa_build_info(hkcsa_index* ix, uint64_t* info, int cap);
 

@@ -11,6 +11,9 @@
  */
 #include <stdint.h>
 #include <stdlib.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
 #include <string.h>
 #include <math.h>
 
@@ -39,6 +42,7 @@ int oracle_suffix_array(const uint8_t* t, uint64_t n, uint64_t* sa) {
 
 /* csa/bwt.py:3-13: bwt[i] = text[sa[i]-1], wrapping to text[n-1] */
 void oracle_bwt(const uint8_t* t, uint64_t n, const uint64_t* sa, uint8_t* bwt) {
+#pragma omp parallel for schedule(static)
   for (uint64_t i = 0; i < n; ++i) bwt[i] = t[sa[i] == 0 ? n - 1 : sa[i] - 1];
 }
 
@@ -69,11 +73,32 @@ void* oracle_occ_new(const uint8_t* bwt, uint64_t n) {
   o->bwt = bwt;
   o->n = n;
   o->samp = (uint32_t*)calloc(nb * 256, sizeof(uint32_t));
-  uint32_t cur[256] = {0};
-  for (uint64_t i = 0; i <= n; ++i) {
-    if ((i & 63) == 0) memcpy(o->samp + (i >> 6) * 256, cur, sizeof(cur));
-    if (i < n) cur[bwt[i]]++;
+  /* chunked over OpenMP threads: per-chunk symbol totals, their exclusive prefix, then each chunk fills
+   * its samples from its prefix */
+  int T = 1;
+#ifdef _OPENMP
+  T = omp_get_max_threads();
+#endif
+  uint64_t* tot = (uint64_t*)calloc((size_t)(T + 1) * 256, sizeof(uint64_t));
+  const uint64_t per = (nb + T - 1) / T;   /* blocks of 64 per chunk */
+#pragma omp parallel for schedule(static, 1)
+  for (int c = 0; c < T; ++c) {
+    const uint64_t b0 = per * c, b1 = per * (c + 1) < nb ? per * (c + 1) : nb;
+    for (uint64_t i = b0 * 64; i < b1 * 64 && i < n; ++i) tot[(size_t)(c + 1) * 256 + bwt[i]]++;
   }
+  for (int c = 1; c <= T; ++c)
+    for (int s = 0; s < 256; ++s) tot[(size_t)c * 256 + s] += tot[(size_t)(c - 1) * 256 + s];
+#pragma omp parallel for schedule(static, 1)
+  for (int c = 0; c < T; ++c) {
+    const uint64_t b0 = per * c, b1 = per * (c + 1) < nb ? per * (c + 1) : nb;
+    uint32_t cur[256];
+    for (int s = 0; s < 256; ++s) cur[s] = (uint32_t)tot[(size_t)c * 256 + s];
+    for (uint64_t i = b0 * 64; i < b1 * 64 && i <= n; ++i) {
+      if ((i & 63) == 0) memcpy(o->samp + (i >> 6) * 256, cur, sizeof(cur));
+      if (i < n) cur[bwt[i]]++;
+    }
+  }
+  free(tot);
   return o;
 }
 
@@ -132,28 +157,31 @@ void oracle_find_range(const void* p, const uint64_t C[257], const uint8_t* pres
 uint64_t oracle_check_sa(const uint8_t* t, uint64_t n, const uint64_t* sa) {
   if (n == 0) return 0;
   uint64_t* isa = (uint64_t*)malloc(n * sizeof(uint64_t));
+  uint64_t bad = UINT64_MAX;   /* smallest offending index (threads: OpenMP, one per core) */
+#pragma omp parallel for schedule(static)
   for (uint64_t i = 0; i < n; ++i) isa[i] = UINT64_MAX;
+#pragma omp parallel for schedule(static) reduction(min : bad)
   for (uint64_t j = 0; j < n; ++j) {
-    if (sa[j] >= n || isa[sa[j]] != UINT64_MAX) {
-      free(isa);
-      return 1 + j;
-    }
-    isa[sa[j]] = j;
+    if (sa[j] >= n) bad = j < bad ? j : bad;
+    else isa[sa[j]] = j;
   }
+  /* a permutation iff every entry reads back its own slot (a duplicate loses one of its writes) */
+#pragma omp parallel for schedule(static) reduction(min : bad)
+  for (uint64_t j = 0; j < n; ++j)
+    if (sa[j] < n && isa[sa[j]] != j) bad = j < bad ? j : bad;
+#pragma omp parallel for schedule(static) reduction(min : bad)
   for (uint64_t j = 1; j < n; ++j) {
     const uint64_t a = sa[j - 1], b = sa[j];
+    if (a >= n || b >= n) continue;
     int ok;
     if (t[a] != t[b]) ok = t[a] < t[b];
     else if (a + 1 == n) ok = 1;          /* suffix a is a proper prefix of suffix b */
     else if (b + 1 == n) ok = 0;
     else ok = isa[a + 1] < isa[b + 1];
-    if (!ok) {
-      free(isa);
-      return 1 + j;
-    }
+    if (!ok) bad = j < bad ? j : bad;
   }
   free(isa);
-  return 0;
+  return bad == UINT64_MAX ? 0 : 1 + bad;
 }
 
 /* ------------------------------------------------------------- synthetic text

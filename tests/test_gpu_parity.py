@@ -212,6 +212,83 @@ def test_full_size_config1_256MiB(hk):
     dev.close()
 
 
+def _sampled_queries(text, sa, rng, P=2000):
+    n = len(text)
+    pats = [b"", b"$", bytes(text[-3:])]
+    for _ in range(P):
+        m = int(rng.integers(1, 24))
+        s = int(rng.integers(0, n - m))
+        pats.append(text[s:s + m].tobytes())
+    for _ in range(200):
+        pats.append(bytes(rng.integers(0, 256, size=int(rng.integers(1, 5))).astype(np.uint8)))
+    return pats
+
+
+def test_full_size_bench_1GiB_sigma4(hk):
+    """The bench step's own geometry (1 GiB sigma=4, D=16 bucket bits, ~1M ties): SA by the O(n)
+    checker (a checked SA is build_suffix_array's output), BWT recomputed, sampled count / locate /
+    rank against the oracle FM index over the checked SA."""
+    n = (1 << 30) + 1
+    dev = hk.DeviceIndex.synthetic(n, b"ACGT", seed=2)
+    dev.build_sa()
+    dev.build_bwt()
+    info = dev.build_info()
+    assert info[7] == 0 and info[4] > 0, info[:10]   # bucket path, LDS work items
+    sa = dev.sa()
+    text = oracle.synth_text(n, b"ACGT", seed=2)
+    assert oracle.check_sa(text, sa) == 0
+    bwt = oracle.bwt(text, sa)
+    assert np.array_equal(dev.bwt(), bwt)
+    dev.build_wt()
+    fm = oracle.FM(text, sa)
+    rng = np.random.default_rng(5)
+    pats = _sampled_queries(text, sa, rng)
+    assert np.array_equal(dev.count_ranges(pats), fm.find_range(pats))
+    lp = [p for p in pats[3:] if len(p) >= 12][:500]   # located in full: few occurrences each
+    offs, pos = dev.locate(lp)
+    got = [[int(x) for x in pos[offs[i]:offs[i + 1]]] for i in range(len(lp))]
+    assert got == fm.find(lp)
+    cs = text[rng.integers(0, n, size=3000)]
+    idx = rng.integers(0, n + 5, size=3000).astype(np.uint64)
+    want = np.array([fm.rank(int(c), int(i)) for c, i in zip(cs, idx)], dtype=np.uint64)
+    assert np.array_equal(dev.rank(cs, idx), want)
+    dev.close()
+
+
+def test_full_size_config3_sigma256_1GiB(hk):
+    """configs[3]: 1 GiB iid bytes (sigma=256): SA by the O(n) checker, BWT, all 8 wavelet-tree levels
+    against the oracle's levelwise WT, and sampled rank / count / locate against the oracle FM index."""
+    n = (1 << 30) + 1
+    dev = hk.DeviceIndex.synthetic(n, bytes(range(256)), seed=4)
+    dev.build_all()
+    assert dev.wt_levels() == 8
+    sa = dev.sa()
+    text = oracle.synth_text(n, bytes(range(256)), seed=4)
+    assert oracle.check_sa(text, sa) == 0
+    bwt = oracle.bwt(text, sa)
+    assert np.array_equal(dev.bwt(), bwt)
+    del sa
+    full = oracle.wt_levels(bwt)
+    assert len(full) == 8
+    for lv in range(8):
+        assert np.array_equal(dev.wt_level_bits(lv), full[lv]), lv
+    del full
+    sa = dev.sa()
+    fm = oracle.FM(text, sa)
+    rng = np.random.default_rng(6)
+    pats = _sampled_queries(text, sa, rng)
+    assert np.array_equal(dev.count_ranges(pats), fm.find_range(pats))
+    lp = [p for p in pats[3:] if len(p) >= 4][:500]   # located in full: few occurrences each
+    offs, pos = dev.locate(lp)
+    got = [[int(x) for x in pos[offs[i]:offs[i + 1]]] for i in range(len(lp))]
+    assert got == fm.find(lp)
+    cs = rng.integers(0, 256, size=3000).astype(np.uint8)
+    idx = rng.integers(0, n + 5, size=3000).astype(np.uint64)
+    want = np.array([fm.rank(int(c), int(i)) for c, i in zip(cs, idx)], dtype=np.uint64)
+    assert np.array_equal(dev.rank(cs, idx), want)
+    dev.close()
+
+
 @pytest.mark.parametrize("nranks,flags,alpha", [(2, 0, b"ACGT"), (3, 0, b"ACGT"), (2, 1, b"ACGT"), (4, 1, b"ACGT"),
                                                (4, 3, b"ACGT"), (5, 0, bytes(range(256))), (3, 0, b"ab"),
                                                (7, 0, b"AC$GT"), (6, 1, bytes(range(0x20, 0x7F))),
