@@ -220,19 +220,25 @@ __device__ __forceinline__ void bs_load_keys(const uint64_t* __restrict__ keys, 
   for (int k = 0; k < BS_I; ++k) key[k] = sl + 64u * k < it.y ? kb[sl + 64u * k] : 0;
 }
 
-// ---- fast path: one MSD counting pass + comparison ranks inside the bins
+// ---- fast path: one MSD counting pass, then the bins settled in parallel
 // The order among equal keys does not matter (they go to the tie list and are refined), so the LDS
 // sort need not be stable.  One pass bins the suffixes by the top BF_BITS of their local key with LDS
-// atomics (the returned count is a rank inside the bin, in any order); the bins hold ~2 suffixes for
-// iid text, so each suffix then counts the records of its own bin that sort below it ((remaining key
-// bits, original slot) as one u32: the slot breaks ties, so the ranks form a permutation).  Replaces
-// three stable LSD passes whose match-mask ranking and scatters spent half of their LDS cycles in bank
-// conflicts (profiles/r2_sq_counters.json).  A bin over BF_MAXBIN (skewed keys) falls back to the LSD
-// passes.
+// atomics (the returned count is a rank inside the bin, in any order) and scatters one u32 record per
+// suffix, (remaining key bits << 15 | original slot), to its bin.  The bins hold ~1.1 suffixes for iid
+// text: every thread settles 16 bins of one or two records with straight-line code (the record's final
+// index, by slot, into the u16 plane) and lists the rarer bins of 3+ records, which one thread each
+// then insertion-sorts (the slot breaks ties, so the order is total).  Equal keys are listed by final
+// index and written to the tie list from the staged planes.  Replaces three stable LSD passes whose
+// match-mask ranking and scatters spent half of their LDS cycles in bank conflicts
+// (profiles/r2_sq_counters.json).  Items with a bin over BF_MAXBIN (skewed keys), more than 30 varying
+// key bits or overflowing lists take the LSD passes (k_bucket_sort).
 constexpr int BF_BITS = 14;
 constexpr int BF_BINS = 1 << BF_BITS;     // 16384 u16 counters (two per u32) = 32 KiB: aliases BsShared::mt
-constexpr uint32_t BF_MAXBIN = 40;        // <= 63: the bin size and rank fields are 6 bits
+constexpr uint32_t BF_MAXBIN = 32;
+constexpr uint32_t BF_BIGCAP = 4096;      // bins of 3+ records (u16 bin ids in BsShared::whist, first half)
+constexpr uint32_t BF_TIECAP = 4096;      // tied records (u16 final index | head << 15, second half)
 static_assert(BF_BINS * 2 == BS_W * 256 * 8, "bin counters alias the match-mask table");
+static_assert((BF_BIGCAP + BF_TIECAP) * 2 == BS_V * 256 * 4, "bin and tie lists fill BsShared::whist");
 
 template <typename V, bool TRACE>
 __device__ __forceinline__ bool bucket_sort_fast(BsShared& sh, uint2 it, const uint64_t (&key)[BS_I], uint32_t vmask,
@@ -244,26 +250,30 @@ __device__ __forceinline__ bool bucket_sort_fast(BsShared& sh, uint2 it, const u
   const uint32_t start = it.x, cnt = it.y;
   const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int fb = width < BF_BITS ? width : BF_BITS;
-  const int kb = width - fb;                              // key bits below the bin (<= 17)
+  const int kb = width - fb;                              // key bits below the bin (<= 16)
   const uint32_t wmask = width >= 32 ? ~0u : ((1u << width) - 1);
   const uint32_t lowmask = (1u << kb) - 1;
   const uint32_t pmask = (1u << pb) - 1;
   const uint32_t himask = (1u << hb) - 1;
   uint32_t* const H2 = reinterpret_cast<uint32_t*>(&sh.mt[0][0]);   // u16 pairs, zero on entry
   const uint16_t* const H = reinterpret_cast<const uint16_t*>(H2);
-  uint32_t lk[BS_I], r0[BS_H];
+  uint16_t* const blist = reinterpret_cast<uint16_t*>(&sh.whist[0][0]);
+  uint16_t* const tlist = blist + BF_BIGCAP;
+  uint32_t* const nctr = sh.wsum;   // [0] listed bins, [1] tied records
+  uint32_t lk[BS_I], r0[BS_H], pvr[BS_H];
   // ---- 1. bin histogram; the atomic's return value is the suffix's rank inside its bin
 #pragma unroll
   for (int k = 0; k < BS_I; ++k) {
     const bool valid = (vmask >> k) & 1u;
     lk[k] = (uint32_t)((((key[k] >> pbe) & symmask) - base) >> lo) & wmask;
+    const uint32_t pv = ((uint32_t)(key[k] >> hb) & pmask) | (((uint32_t)key[k] & himask) << pb);
     uint32_t r = 0;
     if (valid) {
-      sh.aux[s0 + 64u * k] = (uint16_t)(((uint32_t)(key[k] >> hb) & pmask) | (((uint32_t)key[k] & himask) << pb));
       const uint32_t bin = lk[k] >> kb, sh16 = 16u * (bin & 1u);
       r = (atomicAdd(&H2[bin >> 1], 1u << sh16) >> sh16) & 0xFFFFu;   // counts <= 18432: no carry
     }
-    if (k < BS_H) r0[k] = r; else r0[k - BS_H] |= r << 16;
+    if (k < BS_H) { r0[k] = r; pvr[k] = pv; }
+    else { r0[k - BS_H] |= r << 16; pvr[k - BS_H] |= pv << 16; }
   }
   __syncthreads();
   if (TRACE) ts[2] = stamp();
@@ -299,25 +309,20 @@ __device__ __forceinline__ bool bucket_sort_fast(BsShared& sh, uint2 it, const u
     carry += (uint32_t)w < wv ? wtot[w] : 0u;
     bmax = wtot[BS_W + w] > bmax ? wtot[BS_W + w] : bmax;
   }
-  if (bmax > BF_MAXBIN) {   // skewed keys: the LSD passes (match-mask table back to zero)
-    __syncthreads();
-    for (uint32_t i = tid; i < BS_W * 256; i += BS_T) (&sh.mt[0][0])[i] = 0;
-    __syncthreads();
-    return false;
-  }
+  if (bmax > BF_MAXBIN) return false;   // skewed keys: the LSD passes
   {
     const uint32_t b0 = carry + inc - tsum;
     const uint32_t b2 = b0 | (b0 << 16);   // starts <= 18432: no carry between the halves
     reinterpret_cast<uint4*>(H2)[2 * tid] = make_uint4(b2 + w8[0], b2 + w8[1], b2 + w8[2], b2 + w8[3]);
     reinterpret_cast<uint4*>(H2)[2 * tid + 1] = make_uint4(b2 + w8[4], b2 + w8[5], b2 + w8[6], b2 + w8[7]);
   }
+  if (tid == 0) { nctr[0] = 0; nctr[1] = 0; }
   __syncthreads();
   if (TRACE) ts[3] = stamp();
-  // the positions (coalesced, original order): in flight across the scatter and the bin ranks
+  // ---- 3. positions (coalesced; in flight during the bin work) and records to their bins
   uint32_t vv[BS_I];
 #pragma unroll
   for (int k = 0; k < BS_I; ++k) vv[k] = ((vmask >> k) & 1u) ? vb[s0 + 64u * k] : 0u;
-  // ---- 3. records (low key bits, original slot) to their bins
 #pragma unroll
   for (int k = 0; k < BS_I; ++k) {
     if ((vmask >> k) & 1u) {
@@ -326,92 +331,110 @@ __device__ __forceinline__ bool bucket_sort_fast(BsShared& sh, uint2 it, const u
     }
   }
   __syncthreads();
-  // ---- 4. rank inside the bin: records below (key, slot); equal keys are ties, the smallest slot heads
   if (TRACE) ts[4] = stamp();
-  // Per item one register: bin start s (bits 0..14) | bin size c (15..20) | records below (21..26) |
-  // an equal key (27) | an equal key with a smaller slot (28); `my` = the item's own record.  One trip
-  // count for the wave (its largest bin); the 18 items' record reads are interleaved per step so their
-  // LDS latencies overlap.
-  uint32_t sc[BS_I], my[BS_I], cmax = 0;
+  // ---- 4. bins of one or two records settle in place: final index by slot into aux; 3+ are listed
+  uint32_t bigm = 0;
 #pragma unroll
-  for (int k = 0; k < BS_I; ++k) {
-    uint32_t st = 0, c = 0;
-    if ((vmask >> k) & 1u) {
-      const uint32_t bin = lk[k] >> kb;
-      st = H[bin];
-      c = (bin + 1 < (uint32_t)BF_BINS ? H[bin + 1] : cnt) - st;
-    }
-    sc[k] = st | (c << 15);
-    my[k] = ((lk[k] & lowmask) << 15) | (s0 + 64u * k);
-    cmax = c > cmax ? c : cmax;
-  }
+  for (int j = 0; j < BF_BINS / 2 / BS_T; ++j) {
+    const uint32_t m = tid + BS_T * j;   // bins 2m, 2m + 1
+    const uint32_t pr = H2[m];
+    const uint32_t nx = m + 1 < (uint32_t)BF_BINS / 2 ? (H2[m + 1] & 0xFFFFu) : cnt;
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    const uint32_t t = __shfl_xor(cmax, o, 64);
-    cmax = t > cmax ? t : cmax;
-  }
-  cmax = __builtin_amdgcn_readfirstlane(cmax);
-  for (uint32_t i = 0; i < cmax; ++i) {
-#pragma unroll
-    for (int k = 0; k < BS_I; ++k) {
-      const uint32_t c = (sc[k] >> 15) & 63u;
-      const bool in = i < c;
-      const uint32_t r = sh.buf[(sc[k] & 0x7FFFu) + (in ? i : 0u)];
-      const bool ek = in && (r >> 15) == (my[k] >> 15);
-      sc[k] = (sc[k] + (in && r < my[k] ? (1u << 21) : 0u)) | (ek && r != my[k] ? (1u << 27) : 0u) |
-              (ek && r < my[k] ? (1u << 28) : 0u);
+    for (int h = 0; h < 2; ++h) {
+      const uint32_t s = h ? pr >> 16 : pr & 0xFFFFu;
+      const uint32_t c = (h ? nx : pr >> 16) - s;
+      if (c == 1) {
+        sh.aux[sh.buf[s] & 0x7FFFu] = (uint16_t)s;
+      } else if (c == 2) {
+        const uint32_t x = sh.buf[s], y = sh.buf[s + 1];
+        const uint32_t a = x < y ? x : y, b = x < y ? y : x;
+        sh.aux[a & 0x7FFFu] = (uint16_t)s;
+        sh.aux[b & 0x7FFFu] = (uint16_t)(s + 1);
+        if ((x >> 15) == (y >> 15)) {   // equal keys (rare)
+          const uint32_t t = atomicAdd(&nctr[1], 2u);
+          if (t + 2 <= BF_TIECAP) {
+            tlist[t] = (uint16_t)(s | 0x8000u);
+            tlist[t + 1] = (uint16_t)(s + 1);
+          }
+        }
+      }
+      bigm |= (c >= 3 ? 1u : 0u) << (2 * j + h);
     }
   }
+  {   // wave-aggregated append of the listed bins
+    const uint32_t nb = __popc(bigm);
+    const uint32_t binc = wave_incl_sum<uint32_t>(nb);
+    uint32_t bbase = 0;
+    if (lane == 63 && binc) bbase = atomicAdd(&nctr[0], binc);
+    bbase = __shfl(bbase, 63, 64) + binc - nb;
+    while (bigm) {
+      const int q = __builtin_ctz(bigm);
+      bigm &= bigm - 1;
+      if (bbase < BF_BIGCAP) blist[bbase] = (uint16_t)(2u * (tid + BS_T * (q >> 1)) + (q & 1));
+      ++bbase;
+    }
+  }
+  __syncthreads();
   if (TRACE) ts[5] = stamp();
-  uint32_t fin[BS_H], tmask = 0, hmask = 0;
+  const uint32_t nbig = nctr[0];
+  if (nbig > BF_BIGCAP) return false;
+  // ---- 5. listed bins: one thread each sorts its records in place, assigns final indices, lists ties
+  for (uint32_t i = tid; i < nbig; i += BS_T) {
+    const uint32_t bn = blist[i];
+    const uint32_t s = H[bn], e = bn + 1 < (uint32_t)BF_BINS ? (uint32_t)H[bn + 1] : cnt;
+    for (uint32_t p = s + 1; p < e; ++p) {
+      const uint32_t x = sh.buf[p];
+      uint32_t q = p;
+      while (q > s) {
+        const uint32_t y = sh.buf[q - 1];
+        if (y < x) break;
+        sh.buf[q] = y;
+        --q;
+      }
+      sh.buf[q] = x;
+    }
+    uint32_t x = sh.buf[s], rs = s;
+    sh.aux[x & 0x7FFFu] = (uint16_t)s;
+    for (uint32_t p = s + 1; p <= e; ++p) {
+      const uint32_t y = p < e ? sh.buf[p] : ~0u;
+      if (p < e) sh.aux[y & 0x7FFFu] = (uint16_t)p;
+      if ((y >> 15) != (x >> 15)) {   // a run of equal keys ends at p (key bits < 2^16, so ~0u differs)
+        if (p - rs >= 2) {
+          const uint32_t t = atomicAdd(&nctr[1], p - rs);
+          for (uint32_t q = rs; q < p; ++q)
+            if (t + (q - rs) < BF_TIECAP) tlist[t + (q - rs)] = (uint16_t)(q | (q == rs ? 0x8000u : 0u));
+        }
+        rs = p;
+      }
+      x = y;
+    }
+  }
+  __syncthreads();
+  if (TRACE) ts[6] = stamp();
+  const uint32_t ntie = nctr[1];
+  if (ntie > BF_TIECAP) return false;
+  // tie-list space: one global atomic per workgroup; its latency overlaps the staging
+  unsigned long long tbase = 0;
+  if (tid == 0 && ntie) tbase = atomicAdd(tie_n, (unsigned long long)ntie);
+  // ---- 6. stage (position, prev code) by final index
+  uint32_t fin[BS_H];
 #pragma unroll
   for (int k = 0; k < BS_I; ++k) {
-    const bool valid = (vmask >> k) & 1u;
-    const uint32_t f = valid ? (sc[k] & 0x7FFFu) + ((sc[k] >> 21) & 63u) : cnt;
-    const bool tied = valid && ((sc[k] >> 27) & 1u);
-    tmask |= (tied ? 1u : 0u) << k;
-    hmask |= (tied && !((sc[k] >> 28) & 1u) ? 1u : 0u) << k;
+    const uint32_t f = ((vmask >> k) & 1u) ? (uint32_t)sh.aux[s0 + 64u * k] : 0u;
     if (k < BS_H) fin[k] = f; else fin[k - BS_H] |= f << 16;
   }
-  uint16_t pvr[BS_I];
-#pragma unroll
-  for (int k = 0; k < BS_I; ++k) pvr[k] = sh.aux[s0 + 64u * k];
-  // tie-list space: one global atomic per workgroup, each thread's ties at a block-scanned offset
-  const uint32_t nt = __popc(tmask);
-  const uint32_t tinc = wave_incl_sum<uint32_t>(nt);
-  uint32_t* const wt = reinterpret_cast<uint32_t*>(&sh.rv[0][0]);
-  if (lane == 63) wt[wv] = tinc;
-  __syncthreads();   // every record / pv read is done: buf / aux become the sorted staging planes
-  if (tid == 0) {
-    uint32_t tot = 0;
-#pragma unroll
-    for (int w = 0; w < BS_W; ++w) tot += wt[w];
-    sh.rv[1][0] = tot ? atomicAdd(tie_n, (unsigned long long)tot) : 0ull;
-  }
-  // ---- 5. stage (position, prev code) by final index
+  __syncthreads();
 #pragma unroll
   for (int k = 0; k < BS_I; ++k) {
     if ((vmask >> k) & 1u) {
       const uint32_t f = k < BS_H ? (fin[k] & 0xFFFFu) : (fin[k - BS_H] >> 16);
       sh.buf[f] = vv[k];
-      sh.aux[f] = pvr[k];
+      sh.aux[f] = (uint16_t)(k < BS_H ? (pvr[k] & 0xFFFFu) : (pvr[k - BS_H] >> 16));
     }
   }
+  if (tid == 0) sh.rv[1][0] = tbase;
   __syncthreads();
-  if (TRACE) ts[6] = stamp();
-  uint64_t tpos = sh.rv[1][0] + (tinc - nt);
-  for (uint32_t w = 0; w < wv; ++w) tpos += wt[w];
-#pragma unroll
-  for (int k = 0; k < BS_I; ++k) {
-    if ((tmask >> k) & 1u) {
-      const uint32_t f = k < BS_H ? (fin[k] & 0xFFFFu) : (fin[k - BS_H] >> 16);
-      const uint32_t pv = pvr[k];
-      tie_k[tpos] = (((uint64_t)start + f) << 1) | ((hmask >> k) & 1u);
-      tie_v[tpos] = (V)(((uint64_t)(pv >> pb) << 32) | vv[k]);
-      ++tpos;
-    }
-  }
-  // ---- 6. SA / BWT in sorted order
+  // ---- 7. SA / BWT in sorted order, then the tied records
 #pragma unroll
   for (int k = 0; k < BS_I; ++k) {
     const uint32_t r = s0 + 64u * k;
@@ -419,6 +442,15 @@ __device__ __forceinline__ bool bucket_sort_fast(BsShared& sh, uint2 it, const u
       const uint32_t pv = sh.aux[r];
       sab[r] = (V)(((uint64_t)(pv >> pb) << 32) | sh.buf[r]);
       bwb[r] = sh.inv[pv & pmask];
+    }
+  }
+  if (ntie) {
+    const uint64_t tb = sh.rv[1][0];
+    for (uint32_t i = tid; i < ntie; i += BS_T) {
+      const uint32_t e = tlist[i], f = e & 0x7FFFu;
+      const uint32_t pv = sh.aux[f];
+      tie_k[tb + i] = (((uint64_t)start + f) << 1) | (e >> 15);
+      tie_v[tb + i] = (V)(((uint64_t)(pv >> pb) << 32) | sh.buf[f]);
     }
   }
   return true;
@@ -1041,7 +1073,7 @@ uint64_t sort_bucket_items(Index& ix, const BucketPlan& plan, const uint64_t* ke
         for (size_t w = 0; w < nn; ++w)
           for (int i = 0; i < 7; ++i) acc[i] += (double)(h[w * 8 + i + 1] - h[w * 8 + i]);
         fprintf(stderr, "[bucket_sort_fast trace] %zu WGs, mean cycles: load+prologue %.0f, hist %.0f, scan %.0f, "
-                "scatter %.0f, rank %.0f, stage+ties %.0f, out %.0f\n", (size_t)nn, acc[0] / nn, acc[1] / nn,
+                "scatter %.0f, small bins %.0f, listed bins %.0f, stage+out %.0f\n", (size_t)nn, acc[0] / nn, acc[1] / nn,
                 acc[2] / nn, acc[3] / nn, acc[4] / nn, acc[5] / nn, acc[6] / nn);
       }
       unsigned int nfb = 0;

@@ -554,6 +554,7 @@ int radix_sort_pairs(SortWork& w, KernelTimer& tm, uint64_t* k[2], V* v[2], int 
   // HKCSA_OS_SMALL_TILES=1 restores 512 x 16 (diagnostic)
   static const bool big_tiles = getenv("HKCSA_OS_SMALL_TILES") == nullptr;
   // the text-keyed first pass keeps 512-thread tiles (its key building is heavier per tile)
+  static const bool text_big = getenv("HKCSA_OS_TEXT_T") && atoi(getenv("HKCSA_OS_TEXT_T")) == 1024;
   const uint64_t tile_elems = small ? 256 * OS_I : OS_TILE;
   const uint64_t big_elems = 1024 * OS_I;
   const uint64_t tiles = ceil_div(n, tile_elems);
@@ -621,6 +622,11 @@ int radix_sort_pairs(SortWork& w, KernelTimer& tm, uint64_t* k[2], V* v[2], int 
       if (from_text) {
         if (small)
           k_onesweep<V, 256, OS_I, 0, 4, true><<<(unsigned)tiles, 256, 0, s>>>(
+              nullptr, nullptr, k[nxt], v[nxt], n, (uint32_t)(bit_lo + 8 * p), w.offs.as<uint64_t>() + p * 256,
+              w.status.as<uint64_t>(), w.counters.as<uint32_t>() + p, w.epoch, w.err.as<uint32_t>(), 1,
+              has_next ? bit_lo + 8 * (p + 1) : -1, w.hpart.as<unsigned long long>(), *src);
+        else if (src->g.lb == 2 && text_big)   // DNA, 1024-thread tiles (A/B: HKCSA_OS_TEXT_T=1024)
+          k_onesweep<V, 1024, OS_I, 0, 4, true, 2><<<(unsigned)ceil_div(n, big_elems), 1024, 0, s>>>(
               nullptr, nullptr, k[nxt], v[nxt], n, (uint32_t)(bit_lo + 8 * p), w.offs.as<uint64_t>() + p * 256,
               w.status.as<uint64_t>(), w.counters.as<uint32_t>() + p, w.epoch, w.err.as<uint32_t>(), 1,
               has_next ? bit_lo + 8 * (p + 1) : -1, w.hpart.as<unsigned long long>(), *src);

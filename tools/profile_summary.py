@@ -29,13 +29,13 @@ LEGS = ["sigma4", "sigma256", "printable_200MiB"]
 
 # bench timer name -> kernel-name predicate (the n-sized launches are the largest grids)
 TIMERS = {
-    "sa_bucket_sort": lambda k: "k_bucket_sort<false" in k,
-    "radix_onesweep_text": lambda k: "k_onesweep<" in k and ", true>" in k,
-    "radix_onesweep": lambda k: "k_onesweep<" in k and ", false>" in k,
+    # k_onesweep<V, T, I, MODE, LBW, FT, LB>: FT = the text pass (keys built from the text)
+    "sa_bucket_sort": lambda k: "k_bucket_sort_fast<" in k or "k_bucket_sort<false" in k,
+    "radix_onesweep_text": lambda k: "k_onesweep<" in k and ", true, " in k,
+    "radix_onesweep": lambda k: "k_onesweep<" in k and ", false, " in k,
     "byte_hist": lambda k: "k_byte_hist" in k,
     "wt_bits": lambda k: "k_wt_bits" in k,
     "wt_partition": lambda k: "k_wt_partition" in k,
-    "wt_map_codes": lambda k: "k_map_codes" in k,
     "sa_digit_hist": lambda k: "k_bucket_hist" in k,
     "fm_count": lambda k: "k_count" in k,
 }
