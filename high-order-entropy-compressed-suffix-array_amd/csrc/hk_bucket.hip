@@ -334,31 +334,35 @@ __device__ __forceinline__ bool bucket_sort_fast(BsShared& sh, uint2 it, const u
   if (TRACE) ts[4] = stamp();
   // ---- 4. bins of one or two records settle in place: final index by slot into aux; 3+ are listed
   uint32_t bigm = 0;
+  {
+    uint32_t pr[BF_BINS / 2 / BS_T], nx[BF_BINS / 2 / BS_T];
 #pragma unroll
-  for (int j = 0; j < BF_BINS / 2 / BS_T; ++j) {
-    const uint32_t m = tid + BS_T * j;   // bins 2m, 2m + 1
-    const uint32_t pr = H2[m];
-    const uint32_t nx = m + 1 < (uint32_t)BF_BINS / 2 ? (H2[m + 1] & 0xFFFFu) : cnt;
+    for (int j = 0; j < BF_BINS / 2 / BS_T; ++j) {
+      const uint32_t m = tid + BS_T * j;   // bins 2m, 2m + 1
+      pr[j] = H2[m];
+      nx[j] = m + 1 < (uint32_t)BF_BINS / 2 ? (H2[m + 1] & 0xFFFFu) : cnt;
+    }
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const uint32_t s = h ? pr >> 16 : pr & 0xFFFFu;
-      const uint32_t c = (h ? nx : pr >> 16) - s;
-      if (c == 1) {
-        sh.aux[sh.buf[s] & 0x7FFFu] = (uint16_t)s;
-      } else if (c == 2) {
-        const uint32_t x = sh.buf[s], y = sh.buf[s + 1];
+    for (int j = 0; j < BF_BINS / 2 / BS_T; ++j) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {   // branch-free: the loads of all 16 bins issue together
+        const uint32_t s = h ? pr[j] >> 16 : pr[j] & 0xFFFFu;
+        const uint32_t c = (h ? nx[j] : pr[j] >> 16) - s;
+        const bool some = c - 1u < 2u, two = c == 2;
+        const uint32_t x = some ? sh.buf[s] : 0u;
+        const uint32_t y = two ? sh.buf[s + 1] : x;
         const uint32_t a = x < y ? x : y, b = x < y ? y : x;
-        sh.aux[a & 0x7FFFu] = (uint16_t)s;
-        sh.aux[b & 0x7FFFu] = (uint16_t)(s + 1);
-        if ((x >> 15) == (y >> 15)) {   // equal keys (rare)
+        if (some) sh.aux[a & 0x7FFFu] = (uint16_t)s;
+        if (two) sh.aux[b & 0x7FFFu] = (uint16_t)(s + 1);
+        if (two && (x >> 15) == (y >> 15)) {   // equal keys (rare)
           const uint32_t t = atomicAdd(&nctr[1], 2u);
           if (t + 2 <= BF_TIECAP) {
             tlist[t] = (uint16_t)(s | 0x8000u);
             tlist[t + 1] = (uint16_t)(s + 1);
           }
         }
+        bigm |= (c >= 3 ? 1u : 0u) << (2 * j + h);
       }
-      bigm |= (c >= 3 ? 1u : 0u) << (2 * j + h);
     }
   }
   {   // wave-aggregated append of the listed bins
@@ -378,10 +382,37 @@ __device__ __forceinline__ bool bucket_sort_fast(BsShared& sh, uint2 it, const u
   if (TRACE) ts[5] = stamp();
   const uint32_t nbig = nctr[0];
   if (nbig > BF_BIGCAP) return false;
-  // ---- 5. listed bins: one thread each sorts its records in place, assigns final indices, lists ties
+  // ---- 5. listed bins, one thread each: up to 8 records ranked in registers (all loads in flight
+  // together), larger bins insertion-sorted in place; final indices by slot, equal keys listed
   for (uint32_t i = tid; i < nbig; i += BS_T) {
     const uint32_t bn = blist[i];
     const uint32_t s = H[bn], e = bn + 1 < (uint32_t)BF_BINS ? (uint32_t)H[bn + 1] : cnt;
+    const uint32_t c = e - s;
+    if (c <= 8) {
+      uint32_t r[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) r[q] = (uint32_t)q < c ? sh.buf[s + q] : ~0u;   // key bits < 2^16: pads rank last
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        uint32_t below = 0, eq = 0, eqb = 0;
+#pragma unroll
+        for (int o = 0; o < 8; ++o) {
+          if (o == q) continue;
+          const bool e15 = (r[o] >> 15) == (r[q] >> 15);
+          below += r[o] < r[q] ? 1u : 0u;
+          eq |= e15 ? 1u : 0u;
+          eqb |= (e15 && r[o] < r[q]) ? 1u : 0u;
+        }
+        if ((uint32_t)q < c) {
+          sh.aux[r[q] & 0x7FFFu] = (uint16_t)(s + below);
+          if (eq) {   // equal keys (rare); the smallest slot heads the group
+            const uint32_t t = atomicAdd(&nctr[1], 1u);
+            if (t < BF_TIECAP) tlist[t] = (uint16_t)((s + below) | (eqb ? 0u : 0x8000u));
+          }
+        }
+      }
+      continue;
+    }
     for (uint32_t p = s + 1; p < e; ++p) {
       const uint32_t x = sh.buf[p];
       uint32_t q = p;
