@@ -142,6 +142,243 @@ __global__ __launch_bounds__(BH_T, 1) void k_bucket_hist(const uint8_t* __restri
   }
 }
 
+// ------------------------------------------------------------ 1b. cursor partition
+// The bucket grouping needs no stable passes: the LDS bucket sort orders every bucket completely
+// and equal keys are refined, so the order inside a bucket is free.  Two scatter passes whose
+// destinations are reserved from global cursors therefore replace the two stable onesweep passes:
+// no decoupled lookback (2.2 ms of a 7.3 ms 1 GiB pass, tools/radix_diag.py: 512x16 tiles with and
+// without it) and one LDS atomic per suffix for its rank instead of the match-mask ranking.
+//   pre-pass  k_bucket_hist_spans: the 2^D bucket counts of every workgroup span (u32 partials,
+//             reduced by k_bucket_reduce) and the span's counts of pass A's digit (bucket >> sA);
+//   pass A    k_cpart<true>: keys from the text, scattered by the bucket's top digit; cursors per
+//             (span, digit), started at the digit's start plus the earlier spans' counts;
+//   pass B    k_cpart<false> (D > 8): tiles inside one top-digit region, scattered by the bucket's
+//             low 8 bits; cursors per bucket, started at the bucket starts.
+// Each tile reserves its digit runs with one global atomic per digit (issued before its keys are
+// staged; the result is first needed for the write-out).
+__global__ __launch_bounds__(BH_T, 1) void k_bucket_hist_spans(const uint8_t* __restrict__ t, uint64_t n,
+                                                               const uint16_t* __restrict__ lutk,
+                                                               const uint64_t* __restrict__ skey, KeyedArgs g,
+                                                               int bsh, int D, int sA, uint32_t* __restrict__ part,
+                                                               unsigned long long* __restrict__ drain,
+                                                               uint32_t* __restrict__ spanc, uint64_t span) {
+  __shared__ uint32_t H[32768];   // u16 pairs (drained at 0x8000, as k_bucket_hist)
+  __shared__ uint32_t M[256];     // pass A digit counts of this span
+  __shared__ uint16_t L[256];
+  __shared__ uint64_t SK[72];
+  const uint32_t tid = threadIdx.x;
+  for (uint32_t i = tid; i < 32768; i += BH_T) H[i] = 0;
+  if (tid < 256) {
+    M[tid] = 0;
+    L[tid] = lutk[tid];
+  }
+  if (tid < 72) SK[tid] = skey[tid];
+  __syncthreads();
+  auto add = [&](uint32_t b) {
+    const uint32_t sh = 16u * (b & 1u);
+    const uint32_t old = atomicAdd(&H[b >> 1], 1u << sh);
+    if (((old >> sh) & 0xFFFFu) == 0x7FFFu) {
+      atomicSub(&H[b >> 1], 0x8000u << sh);
+      atomicAdd(&drain[b], 0x8000ull);
+      atomicAdd(&M[b >> sA], 0x8000u);
+    }
+  };
+  const uint64_t lim = n < g.s_start ? n : g.s_start;   // positions with a text window
+  const uint64_t lo = (uint64_t)blockIdx.x * span;
+  const uint64_t hi = lo + span < n ? lo + span : n;
+  const int lb = 31 - __clz((uint32_t)g.Rk);
+  const uint32_t bmask = (1u << D) - 1;
+  uint4 w0 = make_uint4(0, 0, 0, 0), w1 = w0;
+  if (lo + (uint64_t)tid * BH_PER < hi) {
+    const uint4* src = reinterpret_cast<const uint4*>(t + lo + (uint64_t)tid * BH_PER);
+    w0 = src[0];
+    w1 = src[1];
+  }
+  for (uint64_t base = lo; base < hi; base += BH_TILE) {
+    const uint64_t p0 = base + (uint64_t)tid * BH_PER;
+    const uint32_t wd[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+    if (p0 + BH_TILE < hi) {   // next iteration's bytes in flight
+      const uint4* src = reinterpret_cast<const uint4*>(t + p0 + BH_TILE);
+      w0 = src[0];
+      w1 = src[1];
+    }
+    const uint64_t lim2 = lim < hi ? lim : hi;
+    if (p0 < lim2) {
+      uint32_t b = 0;
+#pragma unroll
+      for (int i = 0; i < 2 * BH_PER - 1; ++i) {
+        b = ((b << lb) | (L[(wd[i >> 2] >> (8 * (i & 3))) & 255u] & 255u)) & bmask;
+        const int j = i - (g.hq - 1);
+        if (j >= 0 && j < BH_PER && p0 + j < lim2) add(b);
+      }
+    }
+    for (uint64_t p = p0 > lim ? p0 : lim; p < p0 + BH_PER && p < hi; ++p) add((uint32_t)(SK[p - g.s_start] >> bsh));
+  }
+  __syncthreads();
+  const uint32_t nb = 1u << D, np = (nb + 1) / 2;
+  uint2* const pw = reinterpret_cast<uint2*>(part + (uint64_t)blockIdx.x * (np * 2));
+  for (uint32_t i = tid; i < np; i += BH_T) pw[i] = make_uint2(H[i] & 0xFFFFu, H[i] >> 16);
+  // pass A digit counts: contiguous pairs per thread, one LDS add per digit run
+  const uint32_t per = (np + BH_T - 1) / BH_T;
+  uint32_t acc = 0, cd = 0;
+  for (uint32_t i = tid * per; i < np && i < tid * per + per; ++i) {
+    const uint32_t v = H[i];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const uint32_t d = (2 * i + h) >> sA;
+      if (d != cd) {
+        if (acc) atomicAdd(&M[cd], acc);
+        acc = 0;
+        cd = d;
+      }
+      acc += h ? v >> 16 : v & 0xFFFFu;
+    }
+  }
+  if (acc) atomicAdd(&M[cd], acc);
+  __syncthreads();
+  if (tid < 256) spanc[(uint64_t)blockIdx.x * 256 + tid] = M[tid];
+}
+
+// hist[b] = drained counts + the spans' partial counts of bucket b
+__global__ __launch_bounds__(256) void k_bucket_reduce(const uint32_t* __restrict__ part,
+                                                       const unsigned long long* __restrict__ drain, uint32_t nspan,
+                                                       uint32_t stride, uint32_t nb, uint64_t* __restrict__ hist) {
+  const uint32_t b = blockIdx.x * 256 + threadIdx.x;
+  if (b >= nb) return;
+  uint64_t s = drain[b];
+#pragma unroll 8
+  for (uint32_t w = 0; w < nspan; ++w) s += part[(uint64_t)w * stride + b];
+  hist[b] = s;
+}
+
+constexpr int CP_T = 512;
+constexpr int CP_I = 16;
+constexpr int CP_TILE = CP_T * CP_I;   // 8192 suffixes per tile
+
+struct CpShared {
+  union {
+    uint64_t keys[CP_TILE];
+    uint32_t vals[CP_TILE];
+    uint16_t codes[CP_TILE + kCodePad];   // pass A: the tile's text codes ...
+    struct {                              // ... or packed codes and raw bytes (radix 2^lb)
+      uint32_t pk[(CP_TILE + 64) / 4 + 4];
+      uint8_t raw[CP_TILE + 64];
+    } ft;
+  } stage;
+  uint64_t gb[256];    // destination of the digit's run minus its tile start
+  uint32_t cnt[256];   // digit counts (ranks by LDS atomics)
+  uint32_t tst[256];   // tile-local exclusive digit starts
+  uint32_t wsum[4];
+  uint32_t prev0;
+  uint16_t L[256], LP[256];
+  uint64_t SK[72];
+};
+
+// One tile: ranks by LDS atomics (any order inside a digit), one cursor reservation per digit,
+// keys then values staged in digit order and written as runs.  FT: the tile is text positions
+// [blockIdx.x * CP_TILE, ...) and builds its keys (values = positions), cursor row = its span's;
+// else tiles[blockIdx.x] = {start lo, start hi, count, region} and the row is the region's.
+template <bool FT, int LB>
+__global__ __launch_bounds__(CP_T, 2) void k_cpart(const uint64_t* __restrict__ kin, const uint32_t* __restrict__ vin,
+                                                   uint64_t* __restrict__ kout, uint32_t* __restrict__ vout,
+                                                   uint64_t n, int shift, unsigned long long* __restrict__ cur,
+                                                   const uint4* __restrict__ tiles, uint64_t span, TextKeySrc src) {
+  constexpr int WSPAN = CP_I * 64;
+  __shared__ CpShared sh;
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  uint64_t tbase;
+  uint32_t tn;
+  unsigned long long* row;
+  if (FT) {
+    // workgroups b, b + 8, ... (one XCD when blocks are dealt round-robin, which only speed relies
+    // on) take the spans g, g + 8, ... in order: the runs a cursor row hands out back to back are
+    // written from one L2, which merges them into whole lines
+    const uint32_t per = (uint32_t)(span / CP_TILE), g = blockIdx.x & 7u, k = blockIdx.x >> 3;
+    const uint64_t tile = (uint64_t)(g + 8u * (k / per)) * per + k % per;
+    tbase = tile * CP_TILE;
+    if (tbase >= n) return;   // past the last span (whole workgroup, before any barrier)
+    tn = (uint32_t)(n - tbase < (uint64_t)CP_TILE ? n - tbase : CP_TILE);
+    row = cur + (tbase / span) * 256;
+  } else {
+    const uint4 ti = tiles[blockIdx.x];
+    tbase = (uint64_t)ti.x | ((uint64_t)ti.y << 32);
+    tn = ti.z;
+    if (tn == 0) return;   // padding of a shorter XCD list
+    row = cur + (uint64_t)ti.w * 256;
+  }
+  if (tid < 256) sh.cnt[tid] = 0;
+  const uint32_t s0 = wv * WSPAN + lane;   // item k of this thread is tile slot s0 + 64 k
+  uint64_t key[CP_I];
+  uint32_t val[CP_I];
+  if (FT) {
+    if (tid < 256) {
+      sh.L[tid] = src.lutk[tid];
+      sh.LP[tid] = src.lutp[tid];
+    }
+    if (tid < 72) sh.SK[tid] = src.skey[tid];
+    __syncthreads();
+    text_keys<CP_T, CP_I, LB>(key, src, n, tbase, tbase + (uint64_t)wv * WSPAN, lane, sh.stage.codes,
+                              sh.stage.ft.pk, sh.stage.ft.raw, &sh.prev0, sh.L, sh.LP, sh.SK);
+#pragma unroll
+    for (int k = 0; k < CP_I; ++k) val[k] = (uint32_t)(tbase + s0 + 64u * k);
+  } else {
+#pragma unroll
+    for (int k = 0; k < CP_I; ++k) key[k] = s0 + 64u * k < tn ? kin[tbase + s0 + 64u * k] : ~0ull;
+#pragma unroll
+    for (int k = 0; k < CP_I; ++k) val[k] = s0 + 64u * k < tn ? vin[tbase + s0 + 64u * k] : 0u;
+  }
+  __syncthreads();   // counters zeroed; the text staging is read
+  uint32_t rk[CP_I];
+#pragma unroll
+  for (int k = 0; k < CP_I; ++k) {
+    const uint32_t d = (uint32_t)(key[k] >> shift) & 255u;
+    const uint32_t r = s0 + 64u * k < tn ? atomicAdd(&sh.cnt[d], 1u) : 0u;
+    rk[k] = r | (d << 16);
+  }
+  __syncthreads();
+  unsigned long long g = 0;
+  uint32_t c = 0, inc = 0;
+  if (tid < 256) {
+    c = sh.cnt[tid];
+    if (c) g = atomicAdd(&row[tid], (unsigned long long)c);   // the digit run's destination
+    inc = wave_incl_sum<uint32_t>(c);
+    if (lane == 63) sh.wsum[wv] = inc;
+  }
+  __syncthreads();
+  if (tid < 256) {
+    uint32_t carry = 0;
+    for (uint32_t w = 0; w < wv; ++w) carry += sh.wsum[w];
+    sh.tst[tid] = carry + inc - c;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < CP_I; ++k)
+    if (s0 + 64u * k < tn) sh.stage.keys[sh.tst[rk[k] >> 16] + (rk[k] & 0xFFFFu)] = key[k];
+  if (tid < 256) sh.gb[tid] = g - sh.tst[tid];   // first use of the reservation
+  __syncthreads();
+  uint32_t dg[CP_I / 4] = {};
+#pragma unroll
+  for (int i = 0; i < CP_I; ++i) {
+    const uint32_t s = (uint32_t)i * CP_T + tid;
+    if (s < tn) {
+      const uint64_t kk = sh.stage.keys[s];
+      const uint32_t d = (uint32_t)(kk >> shift) & 255u;
+      dg[i >> 2] |= d << (8 * (i & 3));
+      kout[sh.gb[d] + s] = kk;
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < CP_I; ++k)
+    if (s0 + 64u * k < tn) sh.stage.vals[sh.tst[rk[k] >> 16] + (rk[k] & 0xFFFFu)] = val[k];
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < CP_I; ++i) {
+    const uint32_t s = (uint32_t)i * CP_T + tid;
+    if (s < tn) vout[sh.gb[(dg[i >> 2] >> (8 * (i & 3))) & 255u] + s] = sh.stage.vals[s];
+  }
+}
+
 // ------------------------------------------------------------ 2. keys
 constexpr int PKK_TILE = 4096;
 __global__ __launch_bounds__(256) void k_pack_keyed(const uint8_t* __restrict__ t, uint64_t n,
@@ -1417,6 +1654,121 @@ template bool bucket_sort_slice<uint32_t>(Index&, const KeyGeom&, uint64_t, int,
 template bool bucket_sort_slice<uint64_t>(Index&, const KeyGeom&, uint64_t, int, const SliceBins&,
                                           const uint64_t*);
 
+// ---------------------------------------------------------------- cursor partition (host)
+// Groups the suffixes by bucket (section 1b): pre-pass counts, cursors on the host, pass A (and
+// pass B when D > 8).  Leaves the bucket counts in `hist`; returns the key/value slot holding the
+// grouped pairs.
+int cursor_partition(Index& ix, const KeyGeom& kg, const TextKeySrc& tks, uint64_t* kp[2], uint32_t* vp[2],
+                     std::vector<uint64_t>& hist) {
+  const uint64_t n = ix.n;
+  hipStream_t s = ix.stream;
+  const int D = kg.bucket_bits, sb = kg.sym_bits, pb = kg.pb, bsh = sb - D;
+  const int sA = D > 8 ? 8 : 0;   // pass A digit = bucket >> sA
+  const uint32_t nb = 1u << D, ndA = 1u << (D - sA);
+  const uint64_t span = ceil_div(ceil_div(n, (uint64_t)BH_TILE), 256) * BH_TILE;   // one workgroup per CU
+  const uint32_t nspan = (uint32_t)ceil_div(n, span);
+  const uint32_t stride = nb;
+  ix.cp_part.ensure((uint64_t)nspan * stride * 4 + (uint64_t)nspan * 256 * 4 + 16);
+  ix.bk_hist.ensure((uint64_t)nb * 16 + 16);
+  uint32_t* d_part = ix.cp_part.as<uint32_t>();
+  uint32_t* d_spanc = d_part + (uint64_t)nspan * stride;
+  unsigned long long* d_drain = ix.bk_hist.as<unsigned long long>();
+  uint64_t* d_hist = ix.bk_hist.as<uint64_t>() + nb;
+  HK_HIP(hipMemsetAsync(d_drain, 0, (uint64_t)nb * 8, s));
+  {
+    TimedLaunch t(ix.timer, "sa_bucket_hist", (double)n);
+    k_bucket_hist_spans<<<nspan, BH_T, 0, s>>>(tks.text, n, tks.lutk, tks.skey, tks.g, bsh, D, sA, d_part, d_drain,
+                                               d_spanc, span);
+    HK_HIP(hipGetLastError());
+    k_bucket_reduce<<<(nb + 255) / 256, 256, 0, s>>>(d_part, d_drain, nspan, stride, nb, d_hist);
+    HK_HIP(hipGetLastError());
+  }
+  hist.assign(nb, 0);
+  std::vector<uint32_t> spanc((uint64_t)nspan * 256);
+  HK_HIP(hipMemcpyAsync(hist.data(), d_hist, (uint64_t)nb * 8, hipMemcpyDeviceToHost, s));
+  HK_HIP(hipMemcpyAsync(spanc.data(), d_spanc, spanc.size() * 4, hipMemcpyDeviceToHost, s));
+  HK_HIP(hipStreamSynchronize(s));
+  // cursors: pass A per (span, digit), pass B per bucket
+  std::vector<uint64_t> totA(ndA, 0), cur((uint64_t)nspan * 256 + (D > 8 ? nb : 0), 0);
+  for (uint32_t w = 0; w < nspan; ++w)
+    for (uint32_t d = 0; d < ndA; ++d) totA[d] += spanc[(uint64_t)w * 256 + d];
+  uint64_t acc = 0, hsum = 0;
+  for (uint32_t b = 0; b < nb; ++b) hsum += hist[b];
+  std::vector<uint64_t> startA(ndA + 1, 0);
+  for (uint32_t d = 0; d < ndA; ++d) {
+    startA[d] = acc;
+    acc += totA[d];
+  }
+  startA[ndA] = acc;
+  if (acc != n || hsum != n) throw ApiError{-7, "cursor partition: bucket counts do not cover the text"};
+  for (uint32_t d = 0; d < ndA; ++d) {
+    uint64_t run = startA[d];
+    for (uint32_t w = 0; w < nspan; ++w) {
+      cur[(uint64_t)w * 256 + d] = run;
+      run += spanc[(uint64_t)w * 256 + d];
+    }
+  }
+  std::vector<uint4> tiles;
+  if (D > 8) {
+    uint64_t* cb = cur.data() + (uint64_t)nspan * 256;
+    uint64_t run = 0;
+    for (uint32_t b = 0; b < nb; ++b) {
+      cb[b] = run;
+      run += hist[b];
+    }
+    // regions dealt to 8 lists (largest first, to the lightest list); list g's tiles go to blocks
+    // g, g + 8, ... so that one XCD works through one region's cursor row at a time (see k_cpart)
+    std::vector<uint32_t> order(ndA);
+    for (uint32_t d = 0; d < ndA; ++d) order[d] = d;
+    std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return totA[a] > totA[b]; });
+    std::vector<std::vector<uint4>> lists(8);
+    std::vector<uint64_t> load(8, 0);
+    for (uint32_t d : order) {
+      if (!totA[d]) continue;
+      const int g = (int)(std::min_element(load.begin(), load.end()) - load.begin());
+      for (uint64_t p = startA[d]; p < startA[d + 1]; p += CP_TILE) {
+        const uint64_t c = std::min<uint64_t>(CP_TILE, startA[d + 1] - p);
+        lists[g].push_back(make_uint4((uint32_t)p, (uint32_t)(p >> 32), (uint32_t)c, d));
+        load[g] += 1;
+      }
+    }
+    size_t maxl = 0;
+    for (auto& l : lists) maxl = std::max(maxl, l.size());
+    tiles.assign(maxl * 8, make_uint4(0, 0, 0, 0));
+    for (int g = 0; g < 8; ++g)
+      for (size_t k = 0; k < lists[g].size(); ++k) tiles[k * 8 + g] = lists[g][k];
+  }
+  ix.cp_cur.ensure(cur.size() * 8 + 16);
+  HK_HIP(hipMemcpy(ix.cp_cur.p, cur.data(), cur.size() * 8, hipMemcpyHostToDevice));
+  if (!tiles.empty()) {
+    ix.cp_tiles.ensure(tiles.size() * sizeof(uint4) + 16);
+    HK_HIP(hipMemcpy(ix.cp_tiles.p, tiles.data(), tiles.size() * sizeof(uint4), hipMemcpyHostToDevice));
+  }
+  unsigned long long* d_curA = ix.cp_cur.as<unsigned long long>();
+  const int outA = D > 8 ? 1 : 0;
+  {
+    TimedLaunch t(ix.timer, "radix_part_text", (double)n * (1 + 8 + 4));
+    const unsigned grid = (unsigned)(8 * ceil_div(nspan, 8u) * (span / CP_TILE));
+    if (tks.g.lb == 2)
+      k_cpart<true, 2><<<grid, CP_T, 0, s>>>(nullptr, nullptr, kp[outA], vp[outA], n, pb + bsh + sA, d_curA,
+                                             nullptr, span, tks);
+    else
+      k_cpart<true, 0><<<grid, CP_T, 0, s>>>(nullptr, nullptr, kp[outA], vp[outA], n, pb + bsh + sA, d_curA,
+                                             nullptr, span, tks);
+    HK_HIP(hipGetLastError());
+  }
+  ix.info[0] += 1;
+  if (D > 8) {
+    TimedLaunch t(ix.timer, "radix_part", (double)n * 2 * (8 + 4));
+    k_cpart<false, 0><<<(unsigned)tiles.size(), CP_T, 0, s>>>(kp[1], vp[1], kp[0], vp[0], n, pb + bsh,
+                                                             d_curA + (uint64_t)nspan * 256,
+                                                             ix.cp_tiles.as<uint4>(), 0, TextKeySrc{});
+    HK_HIP(hipGetLastError());
+    ix.info[0] += 1;
+  }
+  return 0;
+}
+
 // ---------------------------------------------------------------- driver
 void build_sa_bucketed(Index& ix) {
   const uint64_t n = ix.n;
@@ -1463,8 +1815,14 @@ void build_sa_bucketed(Index& ix) {
   const uint32_t nbins = 1u << D;
   std::vector<uint64_t> hist(nbins, 0);
   uint64_t* d_h0 = reinterpret_cast<uint64_t*>(ix.small.as<uint8_t>() + 5120);
-  const bool late_hist = D > 0 && ka.hq > 0;
-  if (late_hist) {
+  // whole-symbol buckets: the lookback-free cursor partition (HKCSA_CURSOR=0: the stable onesweep
+  // passes with the late bucket histogram, for A/B)
+  static const bool cursor_env = !getenv("HKCSA_CURSOR") || atoi(getenv("HKCSA_CURSOR")) != 0;
+  const bool use_cp = cursor_env && D > 0 && ka.hq > 0 && D <= 16;
+  const bool late_hist = D > 0 && ka.hq > 0 && !use_cp;
+  if (use_cp) {
+    // counted with the partition below
+  } else if (late_hist) {
     HK_HIP(hipMemsetAsync(d_h0, 0, 256 * 8, s));
     TimedLaunch t(ix.timer, "sa_digit_hist", (double)n);
     const uint64_t tiles = ceil_div(n, (uint64_t)BH_TILE);
@@ -1500,7 +1858,10 @@ void build_sa_bucketed(Index& ix) {
   const TextKeySrc tks{ix.text.as<uint8_t>(), n, d_lutk, d_lutp, d_skey, ka};
   int slot = 0;
   bool sorted_by_bucket = false;
-  if (late_hist) {
+  if (use_cp) {
+    slot = cursor_partition(ix, kg, tks, kp, vp, hist);
+    sorted_by_bucket = true;
+  } else if (late_hist) {
     // ---- LSD passes over the bucket bits (the first builds the keys from the text), then the
     // bucket counts from the sorted keys
     slot = radix_sort_pairs<uint32_t>(ix.sw, ix.timer, kp, vp, 0, n, pb + bsh, pb + sb, true, s, d_h0, &tks);

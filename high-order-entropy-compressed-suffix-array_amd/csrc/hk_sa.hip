@@ -1036,6 +1036,9 @@ void release_workspace(Index& ix) {
   ix.tile_d.release();
   ix.tile_e.release();
   ix.upd.release();
+  ix.cp_part.release();
+  ix.cp_cur.release();
+  ix.cp_tiles.release();
   ix.sw.status.release();
   ix.sw.status_tiles = 0;
   ix.sw.scan_tmp.release();

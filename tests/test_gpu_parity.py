@@ -508,11 +508,14 @@ def test_timing_stats(hk):
     dev.timing(True)
     dev.build_sa()
     dev.synchronize()
-    # < 2^24 keys: the small-sort variants; the first pass builds the keys from the text
-    l, ms, b = dev.kernel_stats("radix_onesweep_text_small")
+    # whole-symbol buckets: the cursor partition (pre-pass counts, pass A builds the keys from the
+    # text, pass B when the bucket has more than 8 bits), no onesweep pass over the text
+    l, ms, b = dev.kernel_stats("sa_bucket_hist")
     assert l == 1 and ms > 0 and b > 0
-    l, ms, b = dev.kernel_stats("radix_onesweep_small")
-    assert l >= 1 and ms > 0 and b > 0
+    l, ms, b = dev.kernel_stats("radix_part_text")
+    assert l == 1 and ms > 0 and b > 0
+    assert dev.kernel_stats("radix_part")[0] <= 1
+    assert dev.kernel_stats("radix_onesweep_text_small")[0] == 0
     l, ms, b = dev.kernel_stats("sa_bucket_sort")
     assert l == 1 and ms > 0 and b > 0
     assert dev.kernel_stats("sa_pack_keys")[0] == 0

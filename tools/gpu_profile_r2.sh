@@ -20,7 +20,7 @@ i=0
 for set in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_LDS SQ_INSTS_VALU SQ_WAIT_INST_LDS SQ_WAVES" \
            "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_BUSY_CYCLES SQ_INSTS_VMEM_WR GRBM_GUI_ACTIVE"; do
   i=$((i+1))
-  timeout -k 10 300 rocprofv3 --pmc $set --kernel-include-regex "k_synth|bucket_sort|onesweep|byte_hist|wt_" --output-format csv \
+  timeout -k 10 300 rocprofv3 --pmc $set --kernel-include-regex "k_synth|bucket_sort|onesweep|cpart|bucket_hist|byte_hist|wt_" --output-format csv \
       -d gpurun_out/${TAG}_sq_$i -o run -- $B > gpurun_out/${TAG}_sq_$i.log 2>&1 || { echo "sq $i rc=$?"; tail -5 gpurun_out/${TAG}_sq_$i.log; exit 1; }
   echo "sq set $i ok"
 done

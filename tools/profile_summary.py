@@ -36,7 +36,10 @@ TIMERS = {
     "byte_hist": lambda k: "k_byte_hist" in k,
     "wt_bits": lambda k: "k_wt_bits" in k,
     "wt_partition": lambda k: "k_wt_partition" in k,
-    "sa_digit_hist": lambda k: "k_bucket_hist" in k,
+    "radix_part_text": lambda k: "k_cpart<true" in k,
+    "radix_part": lambda k: "k_cpart<false" in k,
+    "sa_bucket_hist": lambda k: "k_bucket_hist_spans" in k,
+    "sa_digit_hist": lambda k: "k_bucket_hist<" in k,
     "fm_count": lambda k: "k_count" in k,
 }
 
@@ -73,9 +76,10 @@ def stats_csv(trace, path):
 def pmc_rows(path):
     rows = list(csv.DictReader(open(path)))
     rows.sort(key=lambda r: int(r["Dispatch_Id"]))
-    leg, out = -1, []
+    leg, out, seen = -1, [], set()
     for r in rows:
-        if "k_synth" in r["Kernel_Name"]:
+        if "k_synth" in r["Kernel_Name"] and r["Dispatch_Id"] not in seen:   # one row per counter
+            seen.add(r["Dispatch_Id"])
             leg += 1
         r["leg"] = max(leg, 0)
         out.append(r)
