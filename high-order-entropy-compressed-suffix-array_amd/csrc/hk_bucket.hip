@@ -251,6 +251,68 @@ __global__ __launch_bounds__(256) void k_bucket_reduce(const uint32_t* __restric
   hist[b] = s;
 }
 
+// Cursors of both passes from the counts (one workgroup): pass B's per bucket = the bucket starts,
+// pass A's per (span, digit) = the digit's start + the earlier spans' counts; also the digit
+// totals and starts (region bounds of pass B) for the host and pass B.
+__global__ __launch_bounds__(1024) void k_cp_cursors(const uint64_t* __restrict__ hist, const uint32_t* __restrict__ spanc,
+                                                     uint32_t nspan, uint32_t nb, uint32_t ndA,
+                                                     unsigned long long* __restrict__ curA,
+                                                     unsigned long long* __restrict__ curB,
+                                                     uint64_t* __restrict__ totA, uint64_t* __restrict__ startA) {
+  __shared__ uint64_t ws[16];
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  // pass B: exclusive scan of the bucket counts, `per` consecutive buckets per thread
+  if (curB) {
+    const uint32_t per = (nb + 1023) / 1024, b0 = tid * per;
+    uint64_t sum = 0;
+    for (uint32_t b = b0; b < b0 + per && b < nb; ++b) sum += hist[b];
+    const uint64_t inc = wave_incl_sum<uint64_t>(sum);
+    if (lane == 63) ws[wv] = inc;
+    __syncthreads();
+    uint64_t run = inc - sum;
+    for (uint32_t w = 0; w < wv; ++w) run += ws[w];
+    for (uint32_t b = b0; b < b0 + per && b < nb; ++b) {
+      curB[b] = run;
+      run += hist[b];
+    }
+    __syncthreads();
+  }
+  // pass A: digit totals, their starts, then the per-span cursors; digit d = tid & 255, span
+  // quarter q = tid >> 8 (the quarters' partial sums meet in LDS)
+  __shared__ uint64_t qs[4][256], st[256];
+  const uint32_t d = tid & 255u, q = tid >> 8, qper = (nspan + 3) / 4, w0 = q * qper < nspan ? q * qper : nspan;
+  const uint32_t w1 = w0 + qper < nspan ? w0 + qper : nspan;
+  uint64_t part = 0;
+  if (d < ndA)
+    for (uint32_t w = w0; w < w1; ++w) part += spanc[(uint64_t)w * 256 + d];
+  qs[q][d] = part;
+  __syncthreads();
+  uint64_t tot = 0;
+  if (tid < 256) tot = qs[0][tid] + qs[1][tid] + qs[2][tid] + qs[3][tid];
+  const uint64_t inc = wave_incl_sum<uint64_t>(tot);
+  if (lane == 63 && wv < 4) ws[wv] = inc;
+  __syncthreads();
+  if (tid < 256) {
+    uint64_t run = inc - tot;
+    for (uint32_t w = 0; w < wv; ++w) run += ws[w];
+    st[tid] = run;
+    if (tid < ndA) {
+      totA[tid] = tot;
+      startA[tid] = run;
+      if (tid == ndA - 1) startA[ndA] = run + tot;
+    }
+  }
+  __syncthreads();
+  if (d < ndA) {
+    uint64_t run = st[d];
+    for (uint32_t qq = 0; qq < q; ++qq) run += qs[qq][d];
+    for (uint32_t w = w0; w < w1; ++w) {
+      curA[(uint64_t)w * 256 + d] = run;
+      run += spanc[(uint64_t)w * 256 + d];
+    }
+  }
+}
+
 constexpr int CP_T = 512;
 constexpr int CP_I = 16;
 constexpr int CP_TILE = CP_T * CP_I;   // 8192 suffixes per tile
@@ -277,12 +339,14 @@ struct CpShared {
 // One tile: ranks by LDS atomics (any order inside a digit), one cursor reservation per digit,
 // keys then values staged in digit order and written as runs.  FT: the tile is text positions
 // [blockIdx.x * CP_TILE, ...) and builds its keys (values = positions), cursor row = its span's;
-// else tiles[blockIdx.x] = {start lo, start hi, count, region} and the row is the region's.
+// else a tile of one region (from the XCD-group region table) and the row is the region's.
 template <bool FT, int LB>
 __global__ __launch_bounds__(CP_T, 2) void k_cpart(const uint64_t* __restrict__ kin, const uint32_t* __restrict__ vin,
                                                    uint64_t* __restrict__ kout, uint32_t* __restrict__ vout,
                                                    uint64_t n, int shift, unsigned long long* __restrict__ cur,
-                                                   const uint4* __restrict__ tiles, uint64_t span, TextKeySrc src) {
+                                                   const uint32_t* __restrict__ gtab,
+                                                   const uint64_t* __restrict__ startA, uint64_t span,
+                                                   TextKeySrc src) {
   constexpr int WSPAN = CP_I * 64;
   __shared__ CpShared sh;
   const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -300,11 +364,38 @@ __global__ __launch_bounds__(CP_T, 2) void k_cpart(const uint64_t* __restrict__ 
     tn = (uint32_t)(n - tbase < (uint64_t)CP_TILE ? n - tbase : CP_TILE);
     row = cur + (tbase / span) * 256;
   } else {
-    const uint4 ti = tiles[blockIdx.x];
-    tbase = (uint64_t)ti.x | ((uint64_t)ti.y << 32);
-    tn = ti.z;
-    if (tn == 0) return;   // padding of a shorter XCD list
-    row = cur + (uint64_t)ti.w * 256;
+    // region table: gtab[g] = first entry of XCD group g (gtab[8] = end), entries {region, first
+    // tile}; workgroup b is tile b >> 3 of group b & 7 (see cursor_partition)
+    uint32_t* const T2 = reinterpret_cast<uint32_t*>(&sh.stage);   // the table (<= 9 + 512 words), one round trip
+    for (uint32_t i = tid; i < 9 + 2 * 256; i += CP_T) T2[i] = gtab[i];
+    __syncthreads();
+    if (tid == 0) {
+      const uint32_t g = blockIdx.x & 7u, k = blockIdx.x >> 3;
+      uint32_t lo = T2[g], hi = T2[g + 1];   // last entry with first tile <= k
+      uint32_t d = ~0u, k0 = 0;
+      if (lo < hi && T2[9 + 2 * lo + 1] <= k) {
+        while (hi - lo > 1) {
+          const uint32_t mid = (lo + hi) / 2;
+          if (T2[9 + 2 * mid + 1] <= k) lo = mid; else hi = mid;
+        }
+        d = T2[9 + 2 * lo];
+        k0 = T2[9 + 2 * lo + 1];
+      }
+      uint64_t tb = 0, tl = 0;
+      if (d != ~0u) {
+        tb = startA[d] + (uint64_t)(k - k0) * CP_TILE;
+        tl = tb < startA[d + 1] ? startA[d + 1] - tb : 0;
+      }
+      sh.gb[0] = tb;
+      sh.gb[1] = tl < (uint64_t)CP_TILE ? tl : (uint64_t)CP_TILE;
+      sh.gb[2] = d;
+    }
+    __syncthreads();
+    tbase = sh.gb[0];
+    tn = (uint32_t)sh.gb[1];
+    if (tn == 0) return;   // past the end of a shorter group (whole workgroup)
+    row = cur + sh.gb[2] * 256;
+    __syncthreads();   // gb is reused below
   }
   if (tid < 256) sh.cnt[tid] = 0;
   const uint32_t s0 = wv * WSPAN + lane;   // item k of this thread is tile slot s0 + 64 k
@@ -1655,9 +1746,11 @@ template bool bucket_sort_slice<uint64_t>(Index&, const KeyGeom&, uint64_t, int,
                                           const uint64_t*);
 
 // ---------------------------------------------------------------- cursor partition (host)
-// Groups the suffixes by bucket (section 1b): pre-pass counts, cursors on the host, pass A (and
-// pass B when D > 8).  Leaves the bucket counts in `hist`; returns the key/value slot holding the
-// grouped pairs.
+// Groups the suffixes by bucket (section 1b): pre-pass counts and cursors on the device, pass A
+// launched at once; the bucket counts and digit totals come back behind an event while pass A
+// runs (the host deals the pass-B regions to XCD groups and the caller plans the bucket items
+// meanwhile), then pass B (D > 8).  Leaves the bucket counts in `hist`; returns the slot holding
+// the grouped pairs.
 int cursor_partition(Index& ix, const KeyGeom& kg, const TextKeySrc& tks, uint64_t* kp[2], uint32_t* vp[2],
                      std::vector<uint64_t>& hist) {
   const uint64_t n = ix.n;
@@ -1670,10 +1763,21 @@ int cursor_partition(Index& ix, const KeyGeom& kg, const TextKeySrc& tks, uint64
   const uint32_t stride = nb;
   ix.cp_part.ensure((uint64_t)nspan * stride * 4 + (uint64_t)nspan * 256 * 4 + 16);
   ix.bk_hist.ensure((uint64_t)nb * 16 + 16);
+  ix.cp_cur.ensure(((uint64_t)nspan * 256 + nb + 2 * 257 + 16) * 8);
+  ix.cp_tiles.ensure((9 + 2 * 256 + 16) * 4);
+  ix.cp_host.ensure((uint64_t)nb * 8 + 2 * 257 * 8 + (9 + 2 * 256) * 4 + 64);
   uint32_t* d_part = ix.cp_part.as<uint32_t>();
   uint32_t* d_spanc = d_part + (uint64_t)nspan * stride;
   unsigned long long* d_drain = ix.bk_hist.as<unsigned long long>();
   uint64_t* d_hist = ix.bk_hist.as<uint64_t>() + nb;
+  unsigned long long* d_curA = ix.cp_cur.as<unsigned long long>();
+  unsigned long long* d_curB = d_curA + (uint64_t)nspan * 256;
+  uint64_t* d_totA = reinterpret_cast<uint64_t*>(d_curB + nb);
+  uint64_t* d_startA = d_totA + 257;
+  uint32_t* d_gtab = ix.cp_tiles.as<uint32_t>();
+  uint64_t* h_hist = ix.cp_host.as<uint64_t>();
+  uint64_t* h_totA = h_hist + nb;   // totA[257] then startA[257]
+  uint32_t* h_gtab = reinterpret_cast<uint32_t*>(h_totA + 2 * 257);
   HK_HIP(hipMemsetAsync(d_drain, 0, (uint64_t)nb * 8, s));
   {
     TimedLaunch t(ix.timer, "sa_bucket_hist", (double)n);
@@ -1682,87 +1786,71 @@ int cursor_partition(Index& ix, const KeyGeom& kg, const TextKeySrc& tks, uint64
     HK_HIP(hipGetLastError());
     k_bucket_reduce<<<(nb + 255) / 256, 256, 0, s>>>(d_part, d_drain, nspan, stride, nb, d_hist);
     HK_HIP(hipGetLastError());
+    k_cp_cursors<<<1, 1024, 0, s>>>(d_hist, d_spanc, nspan, nb, ndA, d_curA, D > 8 ? d_curB : nullptr, d_totA,
+                                    d_startA);
+    HK_HIP(hipGetLastError());
   }
-  hist.assign(nb, 0);
-  std::vector<uint32_t> spanc((uint64_t)nspan * 256);
-  HK_HIP(hipMemcpyAsync(hist.data(), d_hist, (uint64_t)nb * 8, hipMemcpyDeviceToHost, s));
-  HK_HIP(hipMemcpyAsync(spanc.data(), d_spanc, spanc.size() * 4, hipMemcpyDeviceToHost, s));
-  HK_HIP(hipStreamSynchronize(s));
-  // cursors: pass A per (span, digit), pass B per bucket
-  std::vector<uint64_t> totA(ndA, 0), cur((uint64_t)nspan * 256 + (D > 8 ? nb : 0), 0);
-  for (uint32_t w = 0; w < nspan; ++w)
-    for (uint32_t d = 0; d < ndA; ++d) totA[d] += spanc[(uint64_t)w * 256 + d];
-  uint64_t acc = 0, hsum = 0;
-  for (uint32_t b = 0; b < nb; ++b) hsum += hist[b];
-  std::vector<uint64_t> startA(ndA + 1, 0);
-  for (uint32_t d = 0; d < ndA; ++d) {
-    startA[d] = acc;
-    acc += totA[d];
-  }
-  startA[ndA] = acc;
-  if (acc != n || hsum != n) throw ApiError{-7, "cursor partition: bucket counts do not cover the text"};
-  for (uint32_t d = 0; d < ndA; ++d) {
-    uint64_t run = startA[d];
-    for (uint32_t w = 0; w < nspan; ++w) {
-      cur[(uint64_t)w * 256 + d] = run;
-      run += spanc[(uint64_t)w * 256 + d];
-    }
-  }
-  std::vector<uint4> tiles;
-  if (D > 8) {
-    uint64_t* cb = cur.data() + (uint64_t)nspan * 256;
-    uint64_t run = 0;
-    for (uint32_t b = 0; b < nb; ++b) {
-      cb[b] = run;
-      run += hist[b];
-    }
-    // regions dealt to 8 lists (largest first, to the lightest list); list g's tiles go to blocks
-    // g, g + 8, ... so that one XCD works through one region's cursor row at a time (see k_cpart)
-    std::vector<uint32_t> order(ndA);
-    for (uint32_t d = 0; d < ndA; ++d) order[d] = d;
-    std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return totA[a] > totA[b]; });
-    std::vector<std::vector<uint4>> lists(8);
-    std::vector<uint64_t> load(8, 0);
-    for (uint32_t d : order) {
-      if (!totA[d]) continue;
-      const int g = (int)(std::min_element(load.begin(), load.end()) - load.begin());
-      for (uint64_t p = startA[d]; p < startA[d + 1]; p += CP_TILE) {
-        const uint64_t c = std::min<uint64_t>(CP_TILE, startA[d + 1] - p);
-        lists[g].push_back(make_uint4((uint32_t)p, (uint32_t)(p >> 32), (uint32_t)c, d));
-        load[g] += 1;
-      }
-    }
-    size_t maxl = 0;
-    for (auto& l : lists) maxl = std::max(maxl, l.size());
-    tiles.assign(maxl * 8, make_uint4(0, 0, 0, 0));
-    for (int g = 0; g < 8; ++g)
-      for (size_t k = 0; k < lists[g].size(); ++k) tiles[k * 8 + g] = lists[g][k];
-  }
-  ix.cp_cur.ensure(cur.size() * 8 + 16);
-  HK_HIP(hipMemcpy(ix.cp_cur.p, cur.data(), cur.size() * 8, hipMemcpyHostToDevice));
-  if (!tiles.empty()) {
-    ix.cp_tiles.ensure(tiles.size() * sizeof(uint4) + 16);
-    HK_HIP(hipMemcpy(ix.cp_tiles.p, tiles.data(), tiles.size() * sizeof(uint4), hipMemcpyHostToDevice));
-  }
-  unsigned long long* d_curA = ix.cp_cur.as<unsigned long long>();
+  HK_HIP(hipMemcpyAsync(h_hist, d_hist, (uint64_t)nb * 8, hipMemcpyDeviceToHost, s));
+  HK_HIP(hipMemcpyAsync(h_totA, d_totA, 2 * 257 * 8, hipMemcpyDeviceToHost, s));
+  hipEvent_t ev;
+  HK_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+  HK_HIP(hipEventRecord(ev, s));
   const int outA = D > 8 ? 1 : 0;
   {
     TimedLaunch t(ix.timer, "radix_part_text", (double)n * (1 + 8 + 4));
     const unsigned grid = (unsigned)(8 * ceil_div(nspan, 8u) * (span / CP_TILE));
     if (tks.g.lb == 2)
       k_cpart<true, 2><<<grid, CP_T, 0, s>>>(nullptr, nullptr, kp[outA], vp[outA], n, pb + bsh + sA, d_curA,
-                                             nullptr, span, tks);
+                                             nullptr, nullptr, span, tks);
     else
       k_cpart<true, 0><<<grid, CP_T, 0, s>>>(nullptr, nullptr, kp[outA], vp[outA], n, pb + bsh + sA, d_curA,
-                                             nullptr, span, tks);
+                                             nullptr, nullptr, span, tks);
     HK_HIP(hipGetLastError());
   }
   ix.info[0] += 1;
+  const hipError_t we = hipEventSynchronize(ev);   // the counts, not pass A
+  (void)hipEventDestroy(ev);
+  HK_HIP(we);
+  hist.assign(h_hist, h_hist + nb);
+  const uint64_t* totA = h_totA;
+  uint64_t tsum = 0, hsum = 0;
+  for (uint32_t d = 0; d < ndA; ++d) tsum += totA[d];
+  for (uint32_t b = 0; b < nb; ++b) hsum += hist[b];
+  if (tsum != n || hsum != n) throw ApiError{-7, "cursor partition: bucket counts do not cover the text"};
   if (D > 8) {
+    // regions dealt to 8 XCD groups (largest first, to the group with the fewest tiles); group g's
+    // tiles go to workgroups g, g + 8, ... so that one XCD works through one region's cursor row at a
+    // time and its L2 merges the runs the row hands out back to back (blocks are dealt round-robin
+    // over the XCDs: a speed assumption only)
+    std::vector<uint32_t> order;
+    for (uint32_t d = 0; d < ndA; ++d)
+      if (totA[d]) order.push_back(d);
+    std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return totA[a] > totA[b]; });
+    std::vector<std::vector<uint32_t>> grp(8);
+    uint64_t load[8] = {0};
+    for (uint32_t d : order) {
+      const int g = (int)(std::min_element(load, load + 8) - load);
+      grp[g].push_back(d);
+      load[g] += ceil_div(totA[d], (uint64_t)CP_TILE);
+    }
+    uint32_t e = 0;
+    uint64_t maxl = 0;
+    for (int g = 0; g < 8; ++g) {
+      h_gtab[g] = e;
+      uint32_t k0 = 0;
+      for (uint32_t d : grp[g]) {
+        h_gtab[9 + 2 * e] = d;
+        h_gtab[9 + 2 * e + 1] = k0;
+        k0 += (uint32_t)ceil_div(totA[d], (uint64_t)CP_TILE);
+        ++e;
+      }
+      maxl = std::max<uint64_t>(maxl, k0);
+    }
+    h_gtab[8] = e;
+    HK_HIP(hipMemcpyAsync(d_gtab, h_gtab, (9 + 2 * e) * 4, hipMemcpyHostToDevice, s));
     TimedLaunch t(ix.timer, "radix_part", (double)n * 2 * (8 + 4));
-    k_cpart<false, 0><<<(unsigned)tiles.size(), CP_T, 0, s>>>(kp[1], vp[1], kp[0], vp[0], n, pb + bsh,
-                                                             d_curA + (uint64_t)nspan * 256,
-                                                             ix.cp_tiles.as<uint4>(), 0, TextKeySrc{});
+    k_cpart<false, 0><<<(unsigned)(8 * maxl), CP_T, 0, s>>>(kp[1], vp[1], kp[0], vp[0], n, pb + bsh, d_curB, d_gtab,
+                                                           d_startA, 0, TextKeySrc{});
     HK_HIP(hipGetLastError());
     ix.info[0] += 1;
   }

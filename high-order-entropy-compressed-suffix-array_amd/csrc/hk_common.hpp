@@ -114,6 +114,33 @@ struct DevBuf {
   template <typename T> T* as() const { return static_cast<T*>(p); }
 };
 
+// grow-only pinned host buffer (asynchronous copies in both directions)
+struct HostBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+  HostBuf() = default;
+  HostBuf(const HostBuf&) = delete;
+  HostBuf& operator=(const HostBuf&) = delete;
+  ~HostBuf() { release(); }
+  void release() {
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    bytes = 0;
+  }
+  void ensure(size_t nbytes) {
+    if (nbytes <= bytes && p) return;
+    release();
+    size_t b = nbytes ? nbytes : 16;
+    if (hipHostMalloc(&p, b, hipHostMallocDefault) != hipSuccess) {
+      p = nullptr;
+      (void)hipGetLastError();
+      throw ApiError{-5, "hipHostMalloc of " + std::to_string(b) + " bytes failed"};
+    }
+    bytes = b;
+  }
+  template <typename T> T* as() const { return static_cast<T*>(p); }
+};
+
 // ----------------------------------------------------- timing registry
 struct KernelTimer {
   struct Pending { std::string name; hipEvent_t a, b; double bytes; };

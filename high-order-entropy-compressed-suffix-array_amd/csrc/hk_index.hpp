@@ -100,6 +100,7 @@ struct Index {
   DevBuf big_k[2], big_v[2], big_j; // big buckets of the bucket build (sorted on the global path)
   DevBuf bk_items, bk_hist, bk_fb; // bucket work items, bucket histogram, fast-path fallback items
   DevBuf cp_part, cp_cur, cp_tiles; // cursor partition: per-span counts, destination cursors, pass-B tiles
+  HostBuf cp_host;                  // ... and its pinned host side (bucket counts, region table)
   DevBuf sel;                     // sharded build: selection masks of the slice (u16 per 16 positions)
   DevBuf tile_a, tile_b, tile_c, tile_d, tile_e;
   DevBuf small;                // scratch for totals etc.

@@ -585,22 +585,42 @@ int radix_sort_pairs(SortWork& w, KernelTimer& tm, uint64_t* k[2], V* v[2], int 
     HK_HIP(hipGetLastError());
   };
   if (src && (!d_hist0 || !vals_iota)) throw ApiError{-1, "radix_sort_pairs: text keys need hist0 and iota values"};
-  if (d_hist0) HK_HIP(hipMemcpyAsync(hist, d_hist0, 256 * 8, hipMemcpyDeviceToDevice, s));
-  else digit_hist(0);
+  // small sorts (refinement rounds): every digit's histogram and offsets from one read of the keys
+  // and one host round trip, then the passes back to back (no per-pass readback)
+  const bool upfront = small && !d_hist0;
+  if (upfront) {
+    HK_HIP(hipMemsetAsync(hist, 0, (uint64_t)np * 256 * 8, s));
+    {
+      TimedLaunch t(tm, "radix_hist", (double)n * 8);
+      unsigned g = (unsigned)std::min<uint64_t>(ceil_div(n, HG_PER_BLOCK), 2048);
+      k_digit_hist<<<g, HG_T, 0, s>>>(k[cur], n, bit_lo, np, reinterpret_cast<unsigned long long*>(hist), kbias);
+      HK_HIP(hipGetLastError());
+    }
+    k_hist_offsets<<<np, 256, 0, s>>>(hist, w.offs.as<uint64_t>());
+    HK_HIP(hipGetLastError());
+    HK_HIP(hipMemcpyAsync(w.h_hist, hist, (uint64_t)np * 256 * 8, hipMemcpyDeviceToHost, s));
+    HK_HIP(hipStreamSynchronize(s));
+  } else if (d_hist0) {
+    HK_HIP(hipMemcpyAsync(hist, d_hist0, 256 * 8, hipMemcpyDeviceToDevice, s));
+  } else {
+    digit_hist(0);
+  }
 
   bool iota_pending = vals_iota;
   for (int p = 0; p < np; ++p) {
     // the digit's histogram is complete here: offsets + single-bucket (skippable) check
-    k_hist_offsets<<<1, 256, 0, s>>>(hist + p * 256, w.offs.as<uint64_t>() + p * 256);
-    HK_HIP(hipGetLastError());
-    HK_HIP(hipMemcpyAsync(w.h_hist + p * 256, hist + p * 256, 256 * 8, hipMemcpyDeviceToHost, s));
-    HK_HIP(hipStreamSynchronize(s));
+    if (!upfront) {
+      k_hist_offsets<<<1, 256, 0, s>>>(hist + p * 256, w.offs.as<uint64_t>() + p * 256);
+      HK_HIP(hipGetLastError());
+      HK_HIP(hipMemcpyAsync(w.h_hist + p * 256, hist + p * 256, 256 * 8, hipMemcpyDeviceToHost, s));
+      HK_HIP(hipStreamSynchronize(s));
+    }
     bool trivial = false;
     for (int d = 0; d < 256; ++d)
       if (w.h_hist[p * 256 + d] == n) trivial = true;
     const bool from_text = src && p == 0;   // builds the keys: never skipped
     if (from_text) trivial = false;
-    const bool has_next = p + 1 < np;
+    const bool has_next = p + 1 < np && !upfront;   // upfront: no next-digit histogram in the pass
     if (trivial) {
       w.passes_skipped++;
       if (has_next) digit_hist(p + 1);
