@@ -18,6 +18,9 @@
 //   with obn = ones before the node, rbase = node start + zeros in node - obn (per level/code
 //   tables in LDS).
 
+#include <algorithm>
+#include <vector>
+
 #include "hk_index.hpp"
 #include "hk_wtq.hpp"
 
@@ -40,48 +43,63 @@ WtView Index::view() const {
 
 namespace {
 
-// Level kernels process WT_G lines (448 symbols each) per wave iteration with all their symbol loads
-// issued up front (one byte per lane per 64 symbols): the single-line form kept only 7 x 64 B in
-// flight per wave and ran latency-bound at 10-20 % of HBM bandwidth (profiles/r2_kernel_stats.csv).
-// Level 0 reads the BWT bytes themselves through a byte -> code table (no separate code-mapping pass).
-constexpr int WT_G = 4;
+// Level kernels: every lane reads 16 consecutive symbols with one 16-B load, so a wave reads 1 KiB
+// per instruction (the byte-per-lane forms moved 64 B per instruction and ran at 18-26 % of HBM,
+// profiles/r2b_sq_counters.json).  16 rank lines hold 16 x 448 = 7 x 1024 symbols, so 7 loads per
+// lane cover 16 whole lines, and every 64-bit data word is the 16-bit slices of 4 adjacent lanes.
+// Per level one u16 table maps the input symbol (BWT byte at level 0, dense code below) to
+// bit << 15 | node << 8 | code (a depth-d node index is < 2^d <= 128).
+constexpr int WT_V = 16;   // lines per wave group
 
-// one wave per WT_G lines: 7 ballots per line -> 7 words; word 0 later receives the ones-before count
+__device__ __forceinline__ uint32_t byte_of(const uint4& v, int i) {
+  const uint32_t w = i < 4 ? v.x : i < 8 ? v.y : i < 12 ? v.z : v.w;
+  return (w >> (8 * (i & 3))) & 255u;
+}
+
+// one wave per WT_V lines: data words from lane slices, line popcounts (word 0 later receives the
+// ones-before count)
 __global__ __launch_bounds__(256) void k_wt_bits(const uint8_t* __restrict__ S, uint64_t n,
-                                                 const uint8_t* __restrict__ bitlut,
-                                                 uint64_t* __restrict__ lines,
+                                                 const uint16_t* __restrict__ lut, uint64_t* __restrict__ lines,
                                                  uint32_t* __restrict__ line_pop, uint64_t nlines) {
-  __shared__ uint8_t B[256];
-  B[threadIdx.x] = bitlut[threadIdx.x];
+  __shared__ uint16_t LU[256];
+  __shared__ uint8_t Q[4][7 * WT_V];   // popcount of every data word of the group
+  LU[threadIdx.x] = lut[threadIdx.x];
   __syncthreads();
-  const uint32_t lane = threadIdx.x & 63;
-  for (uint64_t g = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6); g * WT_G < nlines; g += (uint64_t)gridDim.x * 4) {
-    const uint64_t base = g * WT_G * kLineBits;
-    uint8_t sym[WT_G * 7];
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const uint64_t ngroups = (nlines + WT_V - 1) / WT_V;
+  for (uint64_t g = (uint64_t)blockIdx.x * 4 + wv; g < ngroups; g += (uint64_t)gridDim.x * 4) {
+    const uint64_t base = g * WT_V * kLineBits;
+    uint4 v[7];
 #pragma unroll
-    for (int i = 0; i < WT_G * 7; ++i) {
-      const uint64_t j = base + (uint64_t)i * 64 + lane;
-      sym[i] = j < n ? S[j] : 0;
+    for (int it = 0; it < 7; ++it) {
+      const uint64_t j = base + (uint64_t)it * 1024 + lane * 16u;
+      v[it] = j < n ? *reinterpret_cast<const uint4*>(S + j) : make_uint4(0, 0, 0, 0);   // 64 pad bytes past n
     }
 #pragma unroll
-    for (int q = 0; q < WT_G; ++q) {
-      const uint64_t li = g * WT_G + q;
-      if (li >= nlines) break;
-      uint64_t w[7];
+    for (int it = 0; it < 7; ++it) {
+      const uint64_t j = base + (uint64_t)it * 1024 + lane * 16u;
+      uint32_t bits = 0;
+#pragma unroll
+      for (int i = 0; i < 16; ++i)
+        bits |= ((j + i < n ? (uint32_t)LU[byte_of(v[it], i)] >> 15 : 0u) & 1u) << i;
+      const uint64_t w = (uint64_t)bits | ((uint64_t)__shfl_down(bits, 1, 64) << 16) |
+                         ((uint64_t)__shfl_down(bits, 2, 64) << 32) | ((uint64_t)__shfl_down(bits, 3, 64) << 48);
+      if ((lane & 3u) == 0) {
+        const uint32_t q = it * 16 + (lane >> 2);   // data word of the group, line q / 7
+        const uint64_t li = g * WT_V + q / 7;
+        if (li < nlines) lines[li * 8 + 1 + q % 7] = w;
+        Q[wv][q] = (uint8_t)__popcll(w);
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    if (lane < WT_V) {
+      const uint64_t li = g * WT_V + lane;
       uint32_t pop = 0;
 #pragma unroll
-      for (int i = 0; i < 7; ++i) {
-        const uint64_t j = base + (uint64_t)(q * 7 + i) * 64 + lane;
-        w[i] = ballot64(j < n && B[sym[q * 7 + i]]);
-        pop += (uint32_t)__popcll(w[i]);
-      }
-      uint64_t v = 0;
-#pragma unroll
-      for (int i = 0; i < 7; ++i)
-        if (lane == (uint32_t)i + 1) v = w[i];
-      if (lane >= 1 && lane < 8) lines[li * 8 + lane] = v;
-      if (lane == 0) line_pop[li] = pop;
+      for (int k = 0; k < 7; ++k) pop += Q[wv][lane * 7 + k];
+      if (li < nlines) line_pop[li] = pop;
     }
+    __builtin_amdgcn_wave_barrier();
   }
 }
 
@@ -102,50 +120,151 @@ __global__ void k_wt_tables(const uint64_t* __restrict__ lines, int sigma,
   }
 }
 
-// stable partition of level d's sequence into level d+1 (one wave per WT_G lines); `code` maps the
-// input symbols to dense codes (level 0 reads BWT bytes) or is the identity
+// stable partition of level d's sequence into level d+1.  Each wave takes a contiguous run of
+// 1024-symbol spans; a span's ones-before come from its line (count word + the data words before
+// it) and a wave scan.  Spans inside one node (all but the <= 2^d listed in `bspan`) extend two
+// contiguous output runs (zeros, ones): their bytes are staged in LDS at the destination's offset
+// mod 16, whole aligned 16-B chunks are written as they fill and the partial last chunk is carried
+// to the next span, so bytes are stored one at a time only where a run starts or ends.  A span
+// across a node boundary ends both runs and scatters its bytes.  VALU per span was the limit of the
+// byte-edge form (722 wave-instructions per span, tools/gpu_pmc_kernel.sh).
+struct WtRun {
+  uint64_t rd;     // destination of staging byte 0 (16-aligned)
+  uint32_t fill;   // staged bytes [own0, fill) not yet written
+  uint32_t own0;   // first owned staging byte of the run's first chunk
+  bool live;
+};
+
+__device__ __forceinline__ void wt_run_flush(WtRun& r, const uint8_t* st, uint8_t* __restrict__ out, uint32_t lane) {
+  if (r.live && lane < 16 && lane >= r.own0 && lane < r.fill) out[r.rd + lane] = st[lane];
+  r.live = false;
+}
+
 __global__ __launch_bounds__(256) void k_wt_partition(const uint8_t* __restrict__ S, uint8_t* __restrict__ out,
                                                       uint64_t n, const uint64_t* __restrict__ lines,
-                                                      uint64_t nlines, const uint64_t* __restrict__ obn,
+                                                      const uint64_t* __restrict__ obn,
                                                       const uint64_t* __restrict__ rbase,
-                                                      const uint8_t* __restrict__ code) {
+                                                      const uint16_t* __restrict__ lut,
+                                                      const uint64_t* __restrict__ bspan, uint32_t nbspan,
+                                                      int translate) {
   __shared__ uint64_t OB[256], RB[256];
-  __shared__ uint8_t CODE[256];
+  __shared__ uint16_t LU[256];
+  __shared__ uint64_t BS[256];
+  __shared__ __attribute__((aligned(16))) uint8_t ST[4][2][1024 + 48];
   OB[threadIdx.x] = obn[threadIdx.x];
   RB[threadIdx.x] = rbase[threadIdx.x];
-  CODE[threadIdx.x] = code[threadIdx.x];
+  LU[threadIdx.x] = lut[threadIdx.x];
+  BS[threadIdx.x] = threadIdx.x < nbspan ? bspan[threadIdx.x] : ~0ull;
   __syncthreads();
-  const uint32_t lane = threadIdx.x & 63;
-  for (uint64_t g0 = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6); g0 * WT_G < nlines;
-       g0 += (uint64_t)gridDim.x * 4) {
-    const uint64_t g = __builtin_amdgcn_readfirstlane((uint32_t)g0);
-    const uint64_t base = g * WT_G * kLineBits;
-    uint8_t sym[WT_G * 7];
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const uint64_t nspans = (n + 1023) / 1024, nw = (uint64_t)gridDim.x * 4;
+  const uint64_t per = (nspans + nw - 1) / nw, gw = (uint64_t)blockIdx.x * 4 + wv;
+  const uint64_t t0 = gw * per, t1 = t0 + per < nspans ? t0 + per : nspans;
+  WtRun run[2] = {{0, 0, 0, false}, {0, 0, 0, false}};
+  uint32_t bi = 0;   // boundary spans below t
+  while (bi < nbspan && BS[bi] < t0) ++bi;
+  for (uint64_t t = t0; t < t1; ++t) {
+    const uint64_t base = t * 1024, j0 = base + lane * 16u;
+    const uint4 v = j0 < n ? *reinterpret_cast<const uint4*>(S + j0) : make_uint4(0, 0, 0, 0);
+    const uint64_t li0 = base / kLineBits;
+    const uint32_t wi0 = (uint32_t)(base - li0 * kLineBits) / 64;
+    uint64_t part = 0;
+    if (lane < wi0) part = (uint64_t)__popcll(lines[li0 * 8 + 1 + lane]);
+    else if (lane == 7) part = lines[li0 * 8];
+    const uint64_t onesbase = wave_sum<uint64_t>(part);
+    const uint32_t nv = j0 >= n ? 0u : (n - j0 >= 16 ? 16u : (uint32_t)(n - j0));
+    const uint32_t valid = nv == 16 ? 0xFFFFu : (1u << nv) - 1;
+    uint32_t bits = 0;
+    uint32_t cw[4] = {v.x, v.y, v.z, v.w};
+    if (translate) {   // level 0: BWT bytes -> dense codes
 #pragma unroll
-    for (int i = 0; i < WT_G * 7; ++i) {
-      const uint64_t j = base + (uint64_t)i * 64 + lane;
-      sym[i] = j < n ? S[j] : 0;
-    }
+      for (int k = 0; k < 4; ++k) {
+        uint32_t o = 0;
 #pragma unroll
-    for (int q = 0; q < WT_G; ++q) {
-      const uint64_t li = g * WT_G + q;
-      if (li >= nlines) break;
-      const uint64_t* L = lines + li * 8;
-      uint64_t pre = L[0];
-#pragma unroll
-      for (int i = 0; i < 7; ++i) {
-        const uint64_t w = L[1 + i];
-        const uint64_t j = base + (uint64_t)(q * 7 + i) * 64 + lane;
-        if (j < n) {
-          const uint8_t c = CODE[sym[q * 7 + i]];
-          const uint64_t ob = pre + mbcnt(w);
-          const uint64_t dst = ((w >> lane) & 1ull) ? RB[c] + ob : j - ob + OB[c];
-          out[dst] = c;
+        for (int i = 0; i < 4; ++i) {
+          const uint32_t e = LU[(cw[k] >> (8 * i)) & 255u];
+          bits |= (e >> 15) << (4 * k + i);
+          o |= (e & 255u) << (8 * i);
         }
-        pre += (uint64_t)__popcll(w);
+        cw[k] = o;
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) bits |= ((uint32_t)LU[(cw[i >> 2] >> (8 * (i & 3))) & 255u] >> 15) << i;
+    }
+    bits &= valid;
+    const uint32_t ones = __popc(bits), nz = nv - ones;
+    const uint32_t oinc = wave_incl_sum<uint32_t>(ones), zinc = wave_incl_sum<uint32_t>(nz);
+    const uint32_t opre = oinc - ones, zpre = zinc - nz;
+    const uint32_t c0 = (uint32_t)__shfl(cw[0] & 255u, 0, 64);   // code of the span's first symbol
+    const bool boundary = bi < nbspan && BS[bi] == t;
+    if (boundary) ++bi;
+    if (!boundary) {
+      const uint32_t tot[2] = {(uint32_t)__shfl(zinc, 63, 64), (uint32_t)__shfl(oinc, 63, 64)};
+      const uint64_t dst[2] = {base - onesbase + OB[c0], RB[c0] + onesbase};
+      uint32_t at[2];
+#pragma unroll
+      for (int r = 0; r < 2; ++r) {
+        WtRun& R = run[r];
+        if (!R.live || R.rd + R.fill != dst[r]) {   // a new run (first span, or after a boundary)
+          wt_run_flush(R, ST[wv][r], out, lane);
+          R.rd = dst[r] & ~15ull;
+          R.fill = R.own0 = (uint32_t)(dst[r] & 15u);
+          R.live = true;
+        }
+        at[r] = R.fill;
+      }
+      uint32_t zk = at[0] + zpre, ok = at[1] + opre;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        if ((valid >> i) & 1u) {
+          const uint8_t c = (uint8_t)(cw[i >> 2] >> (8 * (i & 3)));
+          if ((bits >> i) & 1u) ST[wv][1][ok++] = c; else ST[wv][0][zk++] = c;
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int r = 0; r < 2; ++r) {
+        WtRun& R = run[r];
+        const uint32_t end = R.fill + tot[r], full = end / 16;
+        uint8_t* st = ST[wv][r];
+        for (uint32_t ch = lane; ch < full; ch += 64) {
+          const uint4 q = *reinterpret_cast<const uint4*>(st + ch * 16);
+          if (ch == 0 && R.own0) {
+#pragma unroll
+            for (int b = 0; b < 16; ++b)
+              if ((uint32_t)b >= R.own0) out[R.rd + b] = (uint8_t)byte_of(q, b);
+          } else {
+            *reinterpret_cast<uint4*>(out + R.rd + ch * 16) = q;
+          }
+        }
+        if (full) {
+          R.own0 = 0;
+          R.rd += (uint64_t)full * 16;
+          __builtin_amdgcn_wave_barrier();
+          if (lane == 0) *reinterpret_cast<uint4*>(st) = *reinterpret_cast<const uint4*>(st + full * 16);
+        }
+        R.fill = end - full * 16;
+      }
+      __builtin_amdgcn_wave_barrier();
+    } else {
+      wt_run_flush(run[0], ST[wv][0], out, lane);
+      wt_run_flush(run[1], ST[wv][1], out, lane);
+      uint64_t ob = onesbase + opre;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        if ((valid >> i) & 1u) {
+          const uint8_t c = (uint8_t)(cw[i >> 2] >> (8 * (i & 3)));
+          const uint64_t j = j0 + i;
+          if ((bits >> i) & 1u) out[RB[c] + ob++] = c;
+          else out[j - ob + OB[c]] = c;
+        }
       }
     }
   }
+  __builtin_amdgcn_wave_barrier();
+  wt_run_flush(run[0], ST[wv][0], out, lane);
+  wt_run_flush(run[1], ST[wv][1], out, lane);
 }
 
 __global__ __launch_bounds__(256) void k_wt_extract(const uint64_t* __restrict__ lines, uint64_t nwords,
@@ -294,31 +413,52 @@ void build_wt(Index& ix) {
   if (L > 0) {
     ix.seq[0].ensure(n + 64);
     ix.seq[1].ensure(n + 64);
-    // level 0 reads the BWT bytes: byte -> level-0 bit and byte -> dense code tables; deeper levels
-    // read dense codes (identity code table)
-    uint8_t lut0[2][256];
-    for (int b = 0; b < 256; ++b) {
-      const int c = ix.code_of[b];
-      lut0[0][b] = c < 0 ? 0 : T.bit[0][c];
-      lut0[1][b] = (uint8_t)(c < 0 ? 0 : c);
+    // per level: input symbol (BWT byte at level 0, dense code below) -> bit << 15 | node << 8 | code
+    uint16_t lut[kMaxLevels][256];
+    for (int d = 0; d < L; ++d) {
+      uint16_t node_of[256] = {0};
+      int nd = -1;
+      for (int c = 0; c < sigma; ++c) {
+        if (c == 0 || T.start[d][c] != T.start[d][c - 1]) ++nd;
+        node_of[c] = (uint16_t)nd;
+      }
+      if (nd >= 128) throw ApiError{-6, "build_wt: more than 128 nodes on a level"};
+      for (int x = 0; x < 256; ++x) {
+        const int c = d == 0 ? ix.code_of[x] : (x < sigma ? x : -1);
+        lut[d][x] = c < 0 ? 0 : (uint16_t)((T.bit[d][c] << 15) | (node_of[c] << 8) | c);
+      }
     }
-    uint8_t ident[256];
-    for (int b = 0; b < 256; ++b) ident[b] = (uint8_t)b;
-    ix.wt_lut.ensure(3 * 256);
-    HK_HIP(hipMemcpyAsync(ix.wt_lut.p, lut0, sizeof(lut0), hipMemcpyHostToDevice, s));
-    HK_HIP(hipMemcpyAsync(ix.wt_lut.as<uint8_t>() + 512, ident, 256, hipMemcpyHostToDevice, s));
+    ix.wt_lut.ensure(sizeof(lut));
+    HK_HIP(hipMemcpyAsync(ix.wt_lut.p, lut, (size_t)L * 512, hipMemcpyHostToDevice, s));
     ix.tile_b.ensure(nlines * 4 + 16);
     ix.tile_a.ensure(nlines * 8 + 16);
+    // per level, the 1024-symbol spans holding a node start (k_wt_partition scatters those bytewise);
+    // copied once, read after the synchronize at the end of the build
+    std::vector<uint64_t> bsp((size_t)kMaxLevels * 256, 0);
+    uint32_t nbsp[kMaxLevels] = {0};
+    for (int d = 0; d < L; ++d) {
+      std::vector<uint64_t> v;
+      for (int c = 1; c < sigma; ++c)
+        if (T.start[d][c] != T.start[d][c - 1] && T.start[d][c] % 1024 && T.start[d][c] < n)
+          v.push_back(T.start[d][c] / 1024);
+      std::sort(v.begin(), v.end());
+      v.erase(std::unique(v.begin(), v.end()), v.end());
+      if (v.size() > 256) throw ApiError{-6, "build_wt: more than 256 node boundaries on a level"};
+      std::copy(v.begin(), v.end(), bsp.begin() + (size_t)d * 256);
+      nbsp[d] = (uint32_t)v.size();
+    }
+    ix.tile_d.ensure(bsp.size() * 8);
+    HK_HIP(hipMemcpyAsync(ix.tile_d.p, bsp.data(), bsp.size() * 8, hipMemcpyHostToDevice, s));
     int cur = 0;
-    const unsigned gl = grid_for(ceil_div(nlines, WT_G), 4, 8192);
+    const unsigned gb = grid_for(ceil_div(nlines, WT_V), 4, 8192), gp = grid_for(ceil_div(n, 1024), 4, 8192);
     for (int d = 0; d < L; ++d) {
       ix.wt_lines[d].ensure(nlines * 64);
       uint64_t* lines = ix.wt_lines[d].as<uint64_t>();
       const uint8_t* in = d == 0 ? ix.bwt.as<uint8_t>() : ix.seq[cur].as<uint8_t>();
       {
         TimedLaunch t(ix.timer, "wt_bits", (double)n * (1 + 1.0 / 8));
-        k_wt_bits<<<gl, 256, 0, s>>>(in, n, d == 0 ? ix.wt_lut.as<uint8_t>() : ix.wt_bit.as<uint8_t>() + d * 256,
-                                     lines, ix.tile_b.as<uint32_t>(), nlines);
+        k_wt_bits<<<gb, 256, 0, s>>>(in, n, ix.wt_lut.as<uint16_t>() + d * 256, lines, ix.tile_b.as<uint32_t>(),
+                                     nlines);
         HK_HIP(hipGetLastError());
       }
       scan_exclusive_u32_to_u64(ix.sw, ix.tile_b.as<uint32_t>(), ix.tile_a.as<uint64_t>(), nlines, false, s);
@@ -331,9 +471,9 @@ void build_wt(Index& ix) {
       if (d + 1 < L) {
         TimedLaunch t(ix.timer, "wt_partition", (double)n * (1 + 1 + 1.0 / 8));
         uint8_t* outp = d == 0 ? ix.seq[0].as<uint8_t>() : ix.seq[cur ^ 1].as<uint8_t>();
-        k_wt_partition<<<gl, 256, 0, s>>>(in, outp, n, lines, nlines, ix.wt_obn.as<uint64_t>() + d * 256,
-                                          ix.wt_rbase.as<uint64_t>() + d * 256,
-                                          ix.wt_lut.as<uint8_t>() + (d == 0 ? 256 : 512));
+        k_wt_partition<<<gp, 256, 0, s>>>(in, outp, n, lines, ix.wt_obn.as<uint64_t>() + d * 256,
+                                          ix.wt_rbase.as<uint64_t>() + d * 256, ix.wt_lut.as<uint16_t>() + d * 256,
+                                          ix.tile_d.as<uint64_t>() + d * 256, nbsp[d], d == 0 ? 1 : 0);
         HK_HIP(hipGetLastError());
         if (d > 0) cur ^= 1;
       }
