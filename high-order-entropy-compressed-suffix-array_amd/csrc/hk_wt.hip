@@ -19,6 +19,8 @@
 //   tables in LDS).
 
 #include <algorithm>
+#include <cstdlib>
+#include <cstring>
 #include <vector>
 
 #include "hk_index.hpp"
@@ -56,11 +58,40 @@ __device__ __forceinline__ uint32_t byte_of(const uint4& v, int i) {
   return (w >> (8 * (i & 3))) & 255u;
 }
 
+// Small alphabets (sigma <= 8, every byte < 128): four symbols per VALU step.  Level 0 maps BWT
+// bytes to dense codes by per-byte threshold compares on whole words (code = number of code-start
+// bytes <= the byte; bit 7 of (byte | 0x80) - t is byte >= t, no borrow between bytes); the level's
+// bit of each code comes from an 8-entry byte table by v_perm_b32, and one multiply gathers the
+// four 0/1 bytes into 4 bits (b0 | b1 << 1 | b2 << 2 | b3 << 3 at bits 24..27).
+struct WtSmall {
+  uint32_t lut_lo, lut_hi;   // bit of codes 0..3 / 4..7, one byte each
+  uint32_t thr[7];           // code-start byte of codes 1..7, replicated to the 4 bytes
+  int nthr;                  // sigma - 1 at level 0, 0 below (the input is already codes)
+};
+
+__device__ __forceinline__ uint32_t small_codes(uint32_t x, const WtSmall& a) {
+  if (!a.nthr) return x;
+  const uint32_t xo = x | 0x80808080u;
+  uint32_t c = 0;
+#pragma unroll
+  for (int k = 0; k < 7; ++k)
+    if (k < a.nthr) c += ((xo - a.thr[k]) & 0x80808080u) >> 7;
+  return c;
+}
+
+// (bytes past n are arbitrary: a selector of 8..15 yields 0x00 / 0xFF / sign bytes, so every byte is
+// cut to its bit 0 before the multiply, or its carries would reach the neighbours' bits)
+__device__ __forceinline__ uint32_t small_bits4(uint32_t codes, const WtSmall& a) {
+  const uint32_t b = __builtin_amdgcn_perm(a.lut_hi, a.lut_lo, codes) & 0x01010101u;
+  return ((b * 0x01020408u) >> 24) & 15u;
+}
+
 // one wave per WT_V lines: data words from lane slices, line popcounts (word 0 later receives the
 // ones-before count)
+template <bool SMALL>
 __global__ __launch_bounds__(256) void k_wt_bits(const uint8_t* __restrict__ S, uint64_t n,
                                                  const uint16_t* __restrict__ lut, uint64_t* __restrict__ lines,
-                                                 uint32_t* __restrict__ line_pop, uint64_t nlines) {
+                                                 uint32_t* __restrict__ line_pop, uint64_t nlines, WtSmall sa) {
   __shared__ uint16_t LU[256];
   __shared__ uint8_t Q[4][7 * WT_V];   // popcount of every data word of the group
   LU[threadIdx.x] = lut[threadIdx.x];
@@ -79,9 +110,16 @@ __global__ __launch_bounds__(256) void k_wt_bits(const uint8_t* __restrict__ S, 
     for (int it = 0; it < 7; ++it) {
       const uint64_t j = base + (uint64_t)it * 1024 + lane * 16u;
       uint32_t bits = 0;
+      if (SMALL) {
+        const uint32_t w4[4] = {v[it].x, v[it].y, v[it].z, v[it].w};
 #pragma unroll
-      for (int i = 0; i < 16; ++i)
-        bits |= ((j + i < n ? (uint32_t)LU[byte_of(v[it], i)] >> 15 : 0u) & 1u) << i;
+        for (int k = 0; k < 4; ++k) bits |= small_bits4(small_codes(w4[k], sa), sa) << (4 * k);
+        if (j + 16 > n) bits &= j >= n ? 0u : (1u << (uint32_t)(n - j)) - 1;
+      } else {
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+          bits |= ((j + i < n ? (uint32_t)LU[byte_of(v[it], i)] >> 15 : 0u) & 1u) << i;
+      }
       const uint64_t w = (uint64_t)bits | ((uint64_t)__shfl_down(bits, 1, 64) << 16) |
                          ((uint64_t)__shfl_down(bits, 2, 64) << 32) | ((uint64_t)__shfl_down(bits, 3, 64) << 48);
       if ((lane & 3u) == 0) {
@@ -140,13 +178,14 @@ __device__ __forceinline__ void wt_run_flush(WtRun& r, const uint8_t* st, uint8_
   r.live = false;
 }
 
+template <bool SMALL>
 __global__ __launch_bounds__(256) void k_wt_partition(const uint8_t* __restrict__ S, uint8_t* __restrict__ out,
                                                       uint64_t n, const uint64_t* __restrict__ lines,
                                                       const uint64_t* __restrict__ obn,
                                                       const uint64_t* __restrict__ rbase,
                                                       const uint16_t* __restrict__ lut,
                                                       const uint64_t* __restrict__ bspan, uint32_t nbspan,
-                                                      int translate) {
+                                                      int translate, WtSmall sa) {
   __shared__ uint64_t OB[256], RB[256];
   __shared__ uint16_t LU[256];
   __shared__ uint64_t BS[256];
@@ -176,7 +215,13 @@ __global__ __launch_bounds__(256) void k_wt_partition(const uint8_t* __restrict_
     const uint32_t valid = nv == 16 ? 0xFFFFu : (1u << nv) - 1;
     uint32_t bits = 0;
     uint32_t cw[4] = {v.x, v.y, v.z, v.w};
-    if (translate) {   // level 0: BWT bytes -> dense codes
+    if (SMALL) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        cw[k] = small_codes(cw[k], sa);
+        bits |= small_bits4(cw[k], sa) << (4 * k);
+      }
+    } else if (translate) {   // level 0: BWT bytes -> dense codes
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         uint32_t o = 0;
@@ -409,12 +454,15 @@ void build_wt(Index& ix) {
                         hipMemcpyHostToDevice, s));
 
   const uint64_t nlines = n / kLineBits + 1;
+  // host sources of asynchronous copies: alive until the synchronize at the end of the build
+  std::vector<uint16_t> lutv((size_t)kMaxLevels * 256, 0);
+  uint16_t (*lut)[256] = reinterpret_cast<uint16_t (*)[256]>(lutv.data());
+  std::vector<uint64_t> bsp((size_t)kMaxLevels * 256, 0);
   ix.wt_nlines = nlines;
   if (L > 0) {
     ix.seq[0].ensure(n + 64);
     ix.seq[1].ensure(n + 64);
     // per level: input symbol (BWT byte at level 0, dense code below) -> bit << 15 | node << 8 | code
-    uint16_t lut[kMaxLevels][256];
     for (int d = 0; d < L; ++d) {
       uint16_t node_of[256] = {0};
       int nd = -1;
@@ -428,13 +476,33 @@ void build_wt(Index& ix) {
         lut[d][x] = c < 0 ? 0 : (uint16_t)((T.bit[d][c] << 15) | (node_of[c] << 8) | c);
       }
     }
-    ix.wt_lut.ensure(sizeof(lut));
-    HK_HIP(hipMemcpyAsync(ix.wt_lut.p, lut, (size_t)L * 512, hipMemcpyHostToDevice, s));
+    ix.wt_lut.ensure(lutv.size() * 2);
+    HK_HIP(hipMemcpyAsync(ix.wt_lut.p, lutv.data(), (size_t)L * 512, hipMemcpyHostToDevice, s));
+    // small alphabets: the SWAR level kernels (HKCSA_WT_SMALL=0 keeps the table path, for A/B)
+    static const bool small_env = !getenv("HKCSA_WT_SMALL") || atoi(getenv("HKCSA_WT_SMALL")) != 0;
+    bool small = small_env && sigma <= 8;
+    int byte_of_code[8] = {0};
+    for (int b = 0; b < 256; ++b)
+      if (ix.code_of[b] >= 0) {
+        if (b >= 128) small = false;
+        else if (ix.code_of[b] < 8) byte_of_code[ix.code_of[b]] = b;
+      }
+    WtSmall sml[kMaxLevels];
+    memset(sml, 0, sizeof(sml));
+    for (int d = 0; d < L && small; ++d) {
+      for (int c = 0; c < sigma; ++c) {
+        const uint32_t bit = T.bit[d][c];
+        if (c < 4) sml[d].lut_lo |= bit << (8 * c); else sml[d].lut_hi |= bit << (8 * (c - 4));
+      }
+      if (d == 0) {
+        sml[d].nthr = sigma - 1;
+        for (int k = 1; k < sigma; ++k) sml[d].thr[k - 1] = 0x01010101u * (uint32_t)byte_of_code[k];
+      }
+    }
     ix.tile_b.ensure(nlines * 4 + 16);
     ix.tile_a.ensure(nlines * 8 + 16);
     // per level, the 1024-symbol spans holding a node start (k_wt_partition scatters those bytewise);
     // copied once, read after the synchronize at the end of the build
-    std::vector<uint64_t> bsp((size_t)kMaxLevels * 256, 0);
     uint32_t nbsp[kMaxLevels] = {0};
     for (int d = 0; d < L; ++d) {
       std::vector<uint64_t> v;
@@ -457,8 +525,12 @@ void build_wt(Index& ix) {
       const uint8_t* in = d == 0 ? ix.bwt.as<uint8_t>() : ix.seq[cur].as<uint8_t>();
       {
         TimedLaunch t(ix.timer, "wt_bits", (double)n * (1 + 1.0 / 8));
-        k_wt_bits<<<gb, 256, 0, s>>>(in, n, ix.wt_lut.as<uint16_t>() + d * 256, lines, ix.tile_b.as<uint32_t>(),
-                                     nlines);
+        if (small)
+          k_wt_bits<true><<<gb, 256, 0, s>>>(in, n, ix.wt_lut.as<uint16_t>() + d * 256, lines,
+                                             ix.tile_b.as<uint32_t>(), nlines, sml[d]);
+        else
+          k_wt_bits<false><<<gb, 256, 0, s>>>(in, n, ix.wt_lut.as<uint16_t>() + d * 256, lines,
+                                              ix.tile_b.as<uint32_t>(), nlines, sml[d]);
         HK_HIP(hipGetLastError());
       }
       scan_exclusive_u32_to_u64(ix.sw, ix.tile_b.as<uint32_t>(), ix.tile_a.as<uint64_t>(), nlines, false, s);
@@ -471,9 +543,16 @@ void build_wt(Index& ix) {
       if (d + 1 < L) {
         TimedLaunch t(ix.timer, "wt_partition", (double)n * (1 + 1 + 1.0 / 8));
         uint8_t* outp = d == 0 ? ix.seq[0].as<uint8_t>() : ix.seq[cur ^ 1].as<uint8_t>();
-        k_wt_partition<<<gp, 256, 0, s>>>(in, outp, n, lines, ix.wt_obn.as<uint64_t>() + d * 256,
-                                          ix.wt_rbase.as<uint64_t>() + d * 256, ix.wt_lut.as<uint16_t>() + d * 256,
-                                          ix.tile_d.as<uint64_t>() + d * 256, nbsp[d], d == 0 ? 1 : 0);
+        if (small)
+          k_wt_partition<true><<<gp, 256, 0, s>>>(in, outp, n, lines, ix.wt_obn.as<uint64_t>() + d * 256,
+                                                  ix.wt_rbase.as<uint64_t>() + d * 256,
+                                                  ix.wt_lut.as<uint16_t>() + d * 256, ix.tile_d.as<uint64_t>() + d * 256,
+                                                  nbsp[d], d == 0 ? 1 : 0, sml[d]);
+        else
+          k_wt_partition<false><<<gp, 256, 0, s>>>(in, outp, n, lines, ix.wt_obn.as<uint64_t>() + d * 256,
+                                                   ix.wt_rbase.as<uint64_t>() + d * 256,
+                                                   ix.wt_lut.as<uint16_t>() + d * 256,
+                                                   ix.tile_d.as<uint64_t>() + d * 256, nbsp[d], d == 0 ? 1 : 0, sml[d]);
         HK_HIP(hipGetLastError());
         if (d > 0) cur ^= 1;
       }
