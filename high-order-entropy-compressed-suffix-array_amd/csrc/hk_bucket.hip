@@ -1669,7 +1669,10 @@ SliceBins slice_bins(uint64_t m, const KeyGeom& kg, int hb, uint64_t kmin, uint6
   // multiplicative bins: 2^Dm over the range, Dm = 16 .. 18 (the fewest that keep the mean <= 16.5k)
   int Dm = 16;
   while (Dm < 18 && (double)m / (double)(1u << Dm) > 16500.0) ++Dm;
-  if ((mean > 16500.0 || force_mul) && b.binpos + Dm <= 64 && span > ((unsigned __int128)1 << Dm)) {
+  // also when the shift bins need more 8-bit passes than Dm multiplicative bins (a 17-bit shift bin
+  // over a range just past a power of two costs a whole third pass for one bit)
+  const bool fewer_passes = (b.D + 7) / 8 > (Dm + 7) / 8;
+  if ((mean > 16500.0 || force_mul || fewer_passes) && b.binpos + Dm <= 64 && span > ((unsigned __int128)1 << Dm)) {
     b.mul = (uint64_t)((((unsigned __int128)1) << (64 + Dm)) / span);   // hi64(x * mul) < 2^Dm for x < span
     b.D = Dm;
     b.bsh = bits_of(span >> Dm) + 1;

@@ -140,6 +140,8 @@ struct Index {
   WtView view() const;
 };
 
+void byte_hist_range(Index& ix, uint64_t lo, uint64_t hi, unsigned long long* d_out);
+void set_alphabet(Index& ix, const uint64_t* h);
 void compute_alphabet(Index& ix);
 void build_sa(Index& ix);
 void build_bwt(Index& ix);

@@ -918,19 +918,19 @@ void synth_text(uint8_t* d_text, uint64_t n, const uint8_t* alphabet, int sigma,
   HK_HIP(hipGetLastError());
 }
 
-void compute_alphabet(Index& ix) {
-  if (ix.have_alpha) return;
+// byte counts of T'[lo, hi) (lo a multiple of 16) into d_out[256] (u64)
+void byte_hist_range(Index& ix, uint64_t lo, uint64_t hi, unsigned long long* d_out) {
   hipStream_t s = ix.stream;
-  ix.small.ensure(8192);
-  HK_HIP(hipMemsetAsync(ix.small.p, 0, 256 * 8, s));
-  {
-    TimedLaunch t(ix.timer, "byte_hist", (double)ix.n);
-    k_byte_hist<<<grid_for(ix.n / 16 + 1, 256, 2048), 256, 0, s>>>(ix.text.as<uint8_t>(), ix.n,
-                                                                   ix.small.as<unsigned long long>());
-    HK_HIP(hipGetLastError());
-  }
-  HK_HIP(hipMemcpyAsync(ix.byte_hist, ix.small.p, 256 * 8, hipMemcpyDeviceToHost, s));
-  HK_HIP(hipStreamSynchronize(s));
+  HK_HIP(hipMemsetAsync(d_out, 0, 256 * 8, s));
+  if (hi <= lo) return;
+  TimedLaunch t(ix.timer, "byte_hist", (double)(hi - lo));
+  k_byte_hist<<<grid_for((hi - lo) / 16 + 1, 256, 2048), 256, 0, s>>>(ix.text.as<uint8_t>() + lo, hi - lo, d_out);
+  HK_HIP(hipGetLastError());
+}
+
+// alphabet, C over bytes and dense codes from the byte histogram (utils/utils.py:16-24)
+void set_alphabet(Index& ix, const uint64_t* h) {
+  for (int b = 0; b < 256; ++b) ix.byte_hist[b] = h[b];
   ix.sigma = 0;
   uint64_t acc = 0;
   for (int b = 0; b < 256; ++b) {
@@ -946,6 +946,17 @@ void compute_alphabet(Index& ix) {
   ix.Cbyte[256] = acc;
   ix.Ccode[ix.sigma] = acc;
   ix.have_alpha = true;
+}
+
+void compute_alphabet(Index& ix) {
+  if (ix.have_alpha) return;
+  hipStream_t s = ix.stream;
+  ix.small.ensure(8192);
+  byte_hist_range(ix, 0, ix.n, ix.small.as<unsigned long long>());
+  uint64_t h[256];
+  HK_HIP(hipMemcpyAsync(h, ix.small.p, 256 * 8, hipMemcpyDeviceToHost, s));
+  HK_HIP(hipStreamSynchronize(s));
+  set_alphabet(ix, h);
 }
 
 void build_sa(Index& ix) {

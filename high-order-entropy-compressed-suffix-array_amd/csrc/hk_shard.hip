@@ -1060,13 +1060,34 @@ void build_sa_sharded(Index& ix, const uint8_t id[128], int nranks, int rank) {
   }
   std::string emsg;
   int ecode = 0;
-  // phase 1: sampled partition histogram; the extra bin carries failures (summed)
   DevBuf hist;
   hist.ensure((SH_BUCKETS + 1) * 8 + 64);
+  // phase 0: every build recomputes the byte histogram / C (utils/utils.py:16-24): each rank counts
+  // its 16-aligned block of T' and an all-reduce sums them (+ a failure slot), so no rank reads
+  // all of T' for it
   uint64_t err = local_step([&] {
-    ix.have_alpha = false;   // every build recomputes the byte histogram / C (utils/utils.py:16-24)
-    shard_histogram(ix, nranks, rank, hist.as<uint64_t>());
+    const uint64_t b0 = rank ? ((uint64_t)((__uint128_t)ix.n * (uint64_t)rank / (uint64_t)nranks) & ~15ull) : 0;
+    const uint64_t b1 = rank + 1 < nranks
+                            ? ((uint64_t)((__uint128_t)ix.n * (uint64_t)(rank + 1) / (uint64_t)nranks) & ~15ull)
+                            : ix.n;
+    byte_hist_range(ix, b0, b1, hist.as<unsigned long long>());
   }, emsg, ecode);
+  {
+    const uint64_t e1 = err ? 1 : 0;
+    HK_HIP(hipMemcpyAsync(hist.as<uint64_t>() + 256, &e1, 8, hipMemcpyHostToDevice, s));
+    TimedLaunch t(ix.timer, "rccl_allreduce_bytes", 257.0 * 8);
+    nccl_do(ncclAllReduce(hist.p, hist.p, 257, ncclUint64, ncclSum, g_comm.comm, s), "ncclAllReduce");
+  }
+  {
+    std::vector<uint64_t> bh(257);
+    HK_HIP(hipMemcpyAsync(bh.data(), hist.p, 257 * 8, hipMemcpyDeviceToHost, s));
+    HK_HIP(hipStreamSynchronize(s));
+    if (err) throw ApiError{ecode, emsg};
+    if (bh[256]) throw ApiError{-8, "sharded build failed on a peer rank (byte histogram)"};
+    set_alphabet(ix, bh.data());
+  }
+  // phase 1: sampled partition histogram; the extra bin carries failures (summed)
+  err = local_step([&] { shard_histogram(ix, nranks, rank, hist.as<uint64_t>()); }, emsg, ecode);
   {
     const uint64_t e1 = err ? 1 : 0;
     HK_HIP(hipMemcpyAsync(hist.as<uint64_t>() + SH_BUCKETS, &e1, 8, hipMemcpyHostToDevice, s));
