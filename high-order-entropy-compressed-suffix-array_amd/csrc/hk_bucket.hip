@@ -1773,6 +1773,10 @@ int cursor_partition(Index& ix, const KeyGeom& kg, const TextKeySrc& tks, uint64
   uint32_t* d_spanc = d_part + (uint64_t)nspan * stride;
   unsigned long long* d_drain = ix.bk_hist.as<unsigned long long>();
   uint64_t* d_hist = ix.bk_hist.as<uint64_t>() + nb;
+  static const bool addr_dbg = getenv("HKCSA_CP_ADDR") != nullptr;   // diagnostic: buffer placement
+  if (addr_dbg)
+    fprintf(stderr, "[cp addr] k0 %p k1 %p v0 %p v1 %p text %p\n", (void*)kp[0], (void*)kp[1], (void*)vp[0],
+            (void*)vp[1], (void*)tks.text);
   unsigned long long* d_curA = ix.cp_cur.as<unsigned long long>();
   unsigned long long* d_curB = d_curA + (uint64_t)nspan * 256;
   uint64_t* d_totA = reinterpret_cast<uint64_t*>(d_curB + nb);
