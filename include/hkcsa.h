@@ -75,9 +75,11 @@ int hkcsa_create(const uint8_t* text, uint64_t n, const hkcsa_opts* o, hkcsa_ind
 int hkcsa_create_synthetic(uint64_t n, const uint8_t* alphabet, int sigma, uint64_t seed,
                            uint8_t terminator, const hkcsa_opts* o, hkcsa_index** out);
 /* Suffix array of T'.  Replaces build_suffix_array (csa/suffix_array.py:131-134).
- * Default: keyed bucket build (LSD radix passes over the bucket bits of q-symbol
- * suffix keys, LDS bucket sorts that write SA and BWT together, chunk refinement
- * of tied suffixes, GPU prefix doubling over an ISA for texts whose ties persist);
+ * Default: keyed bucket build (q-symbol suffix keys grouped by bucket with two
+ * lookback-free scatter passes whose destinations come from per-span cursors — or
+ * two stable LSD passes when the alphabet has no whole-symbol buckets — LDS bucket
+ * sorts that write SA and BWT together, chunk refinement of tied suffixes, GPU
+ * prefix doubling over an ISA for texts whose ties persist);
  * HKCSA_FLAG_GLOBAL_SORT: full-width LSD sort of the keys instead of bucket sorts.
  * Recomputes the byte histogram / C array every call. */
 int hkcsa_build_sa(hkcsa_index* ix);
@@ -265,10 +267,10 @@ int hkcsa_timing_reset(hkcsa_index* ix);
  * alg_bytes is the algorithmic byte count summed over launches. */
 int hkcsa_kernel_stats(hkcsa_index* ix, const char* name, uint64_t* launches, double* total_ms,
                        double* alg_bytes);
-/* Build-stage counters of the last build: [0] radix passes run, [1] skipped,
+/* Build-stage counters of the last build: [0] radix / cursor scatter passes run, [1] skipped,
  * [2] refinement rounds (doubling rounds << 32), [3] symbols per key; bucket build:
  * [4] LDS work items, [5] big buckets, [6] suffixes in big buckets, [7] 1 = global path,
- * [8] LDS work items sorted by the stable LSD passes instead of the MSD bin-rank fast path;
+ * [8] LDS work items sorted by the stable LSD passes instead of the MSD bin fast path;
  * then tied suffixes per round (up to cap). */
 int hkcsa_build_info(hkcsa_index* ix, uint64_t* info, int cap);
 
