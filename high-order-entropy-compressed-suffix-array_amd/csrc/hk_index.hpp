@@ -140,6 +140,7 @@ struct Index {
   WtView view() const;
 };
 
+void sa_to_host_u64(Index& ix, uint64_t lo, uint64_t c, uint64_t* out);
 void byte_hist_range(Index& ix, uint64_t lo, uint64_t hi, unsigned long long* d_out);
 void set_alphabet(Index& ix, const uint64_t* h);
 void compute_alphabet(Index& ix);

@@ -22,6 +22,8 @@
 
 #include <cmath>
 
+#include <algorithm>
+
 #include "hk_index.hpp"
 #include "hk_keys.hpp"
 
@@ -916,6 +918,27 @@ void synth_text(uint8_t* d_text, uint64_t n, const uint8_t* alphabet, int sigma,
   for (int i = 0; i < sigma; ++i) al.s[i] = alphabet[i];
   k_synth<<<grid_for(n), 256, 0, s>>>(d_text, n, al, sigma, seed, terminator);
   HK_HIP(hipGetLastError());
+}
+
+__global__ __launch_bounds__(256) void k_widen_u32(const uint32_t* __restrict__ in, uint64_t* __restrict__ out,
+                                                   uint64_t n) {
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) out[i] = in[i];
+}
+
+// SA[lo, lo + c) as u64 into a host buffer: widened on the GPU in 32M-entry chunks (device staging),
+// each chunk copied straight into the caller's buffer (no host-side conversion pass)
+void sa_to_host_u64(Index& ix, uint64_t lo, uint64_t c, uint64_t* out) {
+  hipStream_t s = ix.stream;
+  constexpr uint64_t CH = 1ull << 25;
+  DevBuf tmp;
+  tmp.ensure(std::min<uint64_t>(c, CH) * 8);
+  for (uint64_t o = 0; o < c; o += CH) {
+    const uint64_t k = std::min<uint64_t>(CH, c - o);
+    k_widen_u32<<<grid_for(k, 256, 8192), 256, 0, s>>>(ix.sa.as<uint32_t>() + lo + o, tmp.as<uint64_t>(), k);
+    HK_HIP(hipGetLastError());
+    HK_HIP(hipMemcpyAsync(out + o, tmp.p, k * 8, hipMemcpyDeviceToHost, s));
+    HK_HIP(hipStreamSynchronize(s));
+  }
 }
 
 // byte counts of T'[lo, hi) (lo a multiple of 16) into d_out[256] (u64)

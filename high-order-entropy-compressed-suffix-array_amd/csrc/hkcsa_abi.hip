@@ -291,10 +291,7 @@ int hkcsa_get_sa(hkcsa_index* h, uint64_t lo, uint64_t hi, uint64_t* out) {
       HK_HIP(hipStreamSynchronize(h->ix.stream));
       return;
     }
-    std::vector<uint32_t> tmp(c);
-    HK_HIP(hipMemcpyAsync(tmp.data(), h->ix.sa.as<uint32_t>() + lo, c * 4, hipMemcpyDeviceToHost, h->ix.stream));
-    HK_HIP(hipStreamSynchronize(h->ix.stream));
-    for (uint64_t i = 0; i < c; ++i) out[i] = tmp[i];
+    hk::sa_to_host_u64(h->ix, lo, c, out);
   });
 }
 

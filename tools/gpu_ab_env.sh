@@ -12,7 +12,7 @@ i=0
 for v in "$@"; do
   i=$((i+1))
   [ "$v" = "-" ] && v=""
-  env $v timeout -k 10 300 python3 bench.py --steps 10 --warmup 2 --no-legs --no-cpu-baseline ${BARGS} > gpurun_out/abv_$i.json 2> gpurun_out/abv_$i.err || { echo "variant $i failed"; tail gpurun_out/abv_$i.err; exit 1; }
+  env $v timeout -k 10 300 python3 bench.py --steps 10 --warmup 2 --no-legs --no-cpu-baseline ${BARGS} --no-pcie > gpurun_out/abv_$i.json 2> gpurun_out/abv_$i.err || { echo "variant $i failed"; tail gpurun_out/abv_$i.err; exit 1; }
   python3 - "$v" gpurun_out/abv_$i.json <<'PY'
 import json, sys
 d = json.load(open(sys.argv[2])); r = d['roofline']

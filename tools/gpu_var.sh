@@ -3,7 +3,7 @@
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
 for i in $(seq 1 ${R:-6}); do
-  HKCSA_CP_ADDR=1 timeout -k 10 200 python3 bench.py --steps 6 --warmup 1 --no-legs --no-cpu-baseline --patterns 0 > gpurun_out/var_$i.json 2> gpurun_out/var_$i.err || exit 1
+  HKCSA_CP_ADDR=1 timeout -k 10 200 python3 bench.py --steps 6 --warmup 1 --no-legs --no-cpu-baseline --patterns 0 --no-pcie > gpurun_out/var_$i.json 2> gpurun_out/var_$i.err || exit 1
   python3 - "$i" <<'PY'
 import json, sys
 i = sys.argv[1]
