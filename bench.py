@@ -153,8 +153,8 @@ def cpu_baseline(sample_n: int, npat: int, c0_n: int, seed: int = 3) -> dict:
 # ---------------------------------------------------------------------------- rooflines
 # kernels whose roofline bench.py reports: the dominant one (largest summed time) as `roofline`,
 # the others under roofline["others"]
-ROOF_KERNELS = ("sa_bucket_sort", "radix_part_text", "radix_part", "radix_onesweep_text", "radix_onesweep",
-                "byte_hist")
+ROOF_KERNELS = ("sa_bucket_sort", "radix_part_text", "radix_part", "radix_part_keys", "radix_onesweep_text",
+                "radix_onesweep", "byte_hist")
 WT_KERNELS = ("wt_bits", "wt_partition")
 
 
@@ -206,7 +206,8 @@ def stage_breakdown(dev, names) -> dict:
     return out
 
 
-BUILD_STAGES = ["byte_hist", "sa_bucket_hist", "radix_part_text", "radix_part", "sa_digit_hist", "sa_bin_starts",
+BUILD_STAGES = ["byte_hist", "sa_bucket_hist", "radix_part_text", "radix_part_keys", "radix_part", "sa_digit_hist",
+                "sa_bin_starts",
                 "sa_bucket_sort", "sa_big_gather", "radix_onesweep_text", "radix_table_text", "radix_tile_hist", "radix_hist", "radix_onesweep",
                 "radix_onesweep_small", "sa_pack_keys", "sa_refine_stats", "sa_refine_apply", "sa_refine_keys",
                 "sa_isa_scatter", "sa_group_stats", "sa_group_apply", "sa_pair_keys", "bwt_gather"]

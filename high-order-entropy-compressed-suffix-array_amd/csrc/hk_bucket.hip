@@ -156,6 +156,35 @@ __global__ __launch_bounds__(BH_T, 1) void k_bucket_hist(const uint8_t* __restri
 //             low 8 bits; cursors per bucket, started at the bucket starts.
 // Each tile reserves its digit runs with one global atomic per digit (issued before its keys are
 // staged; the result is first needed for the write-out).
+// end of a span pre-pass: the span's 2^D counts as plain u32 stores (reduced by k_bucket_reduce)
+// and its counts of pass A's digit (bucket >> sA, incl. the drained parts already in M)
+__device__ __forceinline__ void hist_spans_flush(const uint32_t* H, uint32_t* M, int D, int sA,
+                                                 uint32_t* __restrict__ part, uint32_t* __restrict__ spanc) {
+  const uint32_t tid = threadIdx.x;
+  const uint32_t nb = 1u << D, np = (nb + 1) / 2;
+  uint2* const pw = reinterpret_cast<uint2*>(part + (uint64_t)blockIdx.x * (np * 2));
+  for (uint32_t i = tid; i < np; i += BH_T) pw[i] = make_uint2(H[i] & 0xFFFFu, H[i] >> 16);
+  // pass A digit counts: contiguous pairs per thread, one LDS add per digit run
+  const uint32_t per = (np + BH_T - 1) / BH_T;
+  uint32_t acc = 0, cd = 0;
+  for (uint32_t i = tid * per; i < np && i < tid * per + per; ++i) {
+    const uint32_t v = H[i];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const uint32_t d = (2 * i + h) >> sA;
+      if (d != cd) {
+        if (acc) atomicAdd(&M[cd], acc);
+        acc = 0;
+        cd = d;
+      }
+      acc += h ? v >> 16 : v & 0xFFFFu;
+    }
+  }
+  if (acc) atomicAdd(&M[cd], acc);
+  __syncthreads();
+  if (tid < 256) spanc[(uint64_t)blockIdx.x * 256 + tid] = M[tid];
+}
+
 __global__ __launch_bounds__(BH_T, 1) void k_bucket_hist_spans(const uint8_t* __restrict__ t, uint64_t n,
                                                                const uint16_t* __restrict__ lutk,
                                                                const uint64_t* __restrict__ skey, KeyedArgs g,
@@ -215,28 +244,50 @@ __global__ __launch_bounds__(BH_T, 1) void k_bucket_hist_spans(const uint8_t* __
     for (uint64_t p = p0 > lim ? p0 : lim; p < p0 + BH_PER && p < hi; ++p) add((uint32_t)(SK[p - g.s_start] >> bsh));
   }
   __syncthreads();
-  const uint32_t nb = 1u << D, np = (nb + 1) / 2;
-  uint2* const pw = reinterpret_cast<uint2*>(part + (uint64_t)blockIdx.x * (np * 2));
-  for (uint32_t i = tid; i < np; i += BH_T) pw[i] = make_uint2(H[i] & 0xFFFFu, H[i] >> 16);
-  // pass A digit counts: contiguous pairs per thread, one LDS add per digit run
-  const uint32_t per = (np + BH_T - 1) / BH_T;
-  uint32_t acc = 0, cd = 0;
-  for (uint32_t i = tid * per; i < np && i < tid * per + per; ++i) {
-    const uint32_t v = H[i];
+  hist_spans_flush(H, M, D, sA, part, spanc);
+}
+
+// the pre-pass over the packed keys of a sharded slice: bin = ((key - kbias) >> shift) & (2^D - 1)
+__global__ __launch_bounds__(BH_T, 1) void k_key_hist_spans(const uint64_t* __restrict__ keys, uint64_t m, int shift,
+                                                            uint64_t kbias, int D, int sA, uint32_t* __restrict__ part,
+                                                            unsigned long long* __restrict__ drain,
+                                                            uint32_t* __restrict__ spanc, uint64_t span) {
+  __shared__ uint32_t H[32768];
+  __shared__ uint32_t M[256];
+  const uint32_t tid = threadIdx.x;
+  for (uint32_t i = tid; i < 32768; i += BH_T) H[i] = 0;
+  if (tid < 256) M[tid] = 0;
+  __syncthreads();
+  const uint32_t bmask = (1u << D) - 1;
+  auto add = [&](uint64_t k) {
+    const uint32_t b = (uint32_t)((k - kbias) >> shift) & bmask;
+    const uint32_t sh = 16u * (b & 1u);
+    const uint32_t old = atomicAdd(&H[b >> 1], 1u << sh);
+    if (((old >> sh) & 0xFFFFu) == 0x7FFFu) {
+      atomicSub(&H[b >> 1], 0x8000u << sh);
+      atomicAdd(&drain[b], 0x8000ull);
+      atomicAdd(&M[b >> sA], 0x8000u);
+    }
+  };
+  const uint64_t lo = (uint64_t)blockIdx.x * span;
+  const uint64_t hi = lo + span < m ? lo + span : m;
+  for (uint64_t base = lo; base < hi; base += (uint64_t)BH_T * 8) {   // four 16-B loads in flight
+    ulonglong2 v[4];
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const uint32_t d = (2 * i + h) >> sA;
-      if (d != cd) {
-        if (acc) atomicAdd(&M[cd], acc);
-        acc = 0;
-        cd = d;
-      }
-      acc += h ? v >> 16 : v & 0xFFFFu;
+    for (int u = 0; u < 4; ++u) {
+      const uint64_t p = base + ((uint64_t)u * BH_T + tid) * 2;
+      v[u] = p + 1 < hi ? *reinterpret_cast<const ulonglong2*>(keys + p)
+                        : make_ulonglong2(p < hi ? keys[p] : 0ull, 0ull);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const uint64_t p = base + ((uint64_t)u * BH_T + tid) * 2;
+      if (p < hi) add(v[u].x);
+      if (p + 1 < hi) add(v[u].y);
     }
   }
-  if (acc) atomicAdd(&M[cd], acc);
   __syncthreads();
-  if (tid < 256) spanc[(uint64_t)blockIdx.x * 256 + tid] = M[tid];
+  hist_spans_flush(H, M, D, sA, part, spanc);
 }
 
 // hist[b] = drained counts + the spans' partial counts of bucket b
@@ -340,20 +391,24 @@ struct CpShared {
 // keys then values staged in digit order and written as runs.  FT: the tile is text positions
 // [blockIdx.x * CP_TILE, ...) and builds its keys (values = positions), cursor row = its span's;
 // else a tile of one region (from the XCD-group region table) and the row is the region's.
-template <bool FT, int LB>
+// MODE 0: pass A over the text (builds the keys); 1: pass A over packed keys (a sharded slice's);
+// 2: pass B over one region per tile.  digit = ((key - kbias) >> shift) & 255.
+template <int MODE, int LB>
 __global__ __launch_bounds__(CP_T, 2) void k_cpart(const uint64_t* __restrict__ kin, const uint32_t* __restrict__ vin,
                                                    uint64_t* __restrict__ kout, uint32_t* __restrict__ vout,
-                                                   uint64_t n, int shift, unsigned long long* __restrict__ cur,
+                                                   uint64_t n, int shift, uint64_t kbias,
+                                                   unsigned long long* __restrict__ cur,
                                                    const uint32_t* __restrict__ gtab,
                                                    const uint64_t* __restrict__ startA, uint64_t span,
                                                    TextKeySrc src) {
   constexpr int WSPAN = CP_I * 64;
+  constexpr bool FT = MODE == 0;
   __shared__ CpShared sh;
   const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   uint64_t tbase;
   uint32_t tn;
   unsigned long long* row;
-  if (FT) {
+  if (MODE <= 1) {
     // workgroups b, b + 8, ... (one XCD when blocks are dealt round-robin, which only speed relies
     // on) take the spans g, g + 8, ... in order: the runs a cursor row hands out back to back are
     // written from one L2, which merges them into whole lines
@@ -422,7 +477,7 @@ __global__ __launch_bounds__(CP_T, 2) void k_cpart(const uint64_t* __restrict__ 
   uint32_t rk[CP_I];
 #pragma unroll
   for (int k = 0; k < CP_I; ++k) {
-    const uint32_t d = (uint32_t)(key[k] >> shift) & 255u;
+    const uint32_t d = (uint32_t)((key[k] - kbias) >> shift) & 255u;
     const uint32_t r = s0 + 64u * k < tn ? atomicAdd(&sh.cnt[d], 1u) : 0u;
     rk[k] = r | (d << 16);
   }
@@ -453,7 +508,7 @@ __global__ __launch_bounds__(CP_T, 2) void k_cpart(const uint64_t* __restrict__ 
     const uint32_t s = (uint32_t)i * CP_T + tid;
     if (s < tn) {
       const uint64_t kk = sh.stage.keys[s];
-      const uint32_t d = (uint32_t)(kk >> shift) & 255u;
+      const uint32_t d = (uint32_t)((kk - kbias) >> shift) & 255u;
       dg[i >> 2] |= d << (8 * (i & 3));
       kout[sh.gb[d] + s] = kk;
     }
@@ -1680,6 +1735,15 @@ SliceBins slice_bins(uint64_t m, const KeyGeom& kg, int hb, uint64_t kmin, uint6
   return b;
 }
 
+int cursor_partition(Index& ix, uint64_t n, int D, int bitlo, uint64_t kbias, const TextKeySrc* tks, uint64_t* kp[2],
+                     uint32_t* vp[2], std::vector<uint64_t>& hist);
+
+// the cursor partition groups buckets wherever D <= 16 (HKCSA_CURSOR=0: the stable onesweep passes)
+static bool cursor_enabled() {
+  static const bool on = !getenv("HKCSA_CURSOR") || atoi(getenv("HKCSA_CURSOR")) != 0;
+  return on;
+}
+
 template <typename V>
 bool bucket_sort_slice(Index& ix, const KeyGeom& kg, uint64_t m, int hb, const SliceBins& bins, const uint64_t* d_h0) {
   hipStream_t s = ix.stream;
@@ -1695,21 +1759,26 @@ bool bucket_sort_slice(Index& ix, const KeyGeom& kg, uint64_t m, int hb, const S
     // (key - kmin << pbe) above bsh
     const uint64_t kbias = bins.mul ? 0 : bins.kmin << pbe;
     const int shift = bins.mul ? bins.binpos : pbe + bins.bsh;
-    slot = radix_sort_pairs<uint32_t>(ix.sw, ix.timer, kp, vp, 0, m, shift, shift + D, false, s, d_h0, nullptr,
-                                      kbias);
-    ix.info[0] += ix.sw.passes_run;
-    ix.info[1] += ix.sw.passes_skipped;
-    ix.bk_hist.ensure((uint64_t)(nbins + 1) * 8);
-    {
-      TimedLaunch t(ix.timer, "sa_bin_starts", (double)(nbins + 1) * 8);
-      k_bin_starts<<<(nbins + 1 + 255) / 256, 256, 0, s>>>(kp[slot], m, kbias, shift, nbins,
-                                                          ix.bk_hist.as<uint64_t>());
-      HK_HIP(hipGetLastError());
+    if (cursor_enabled() && D <= 16) {
+      // bin counts from the packed keys, then the two lookback-free cursor passes
+      slot = cursor_partition(ix, m, D, shift, kbias, nullptr, kp, vp, hist);
+    } else {
+      slot = radix_sort_pairs<uint32_t>(ix.sw, ix.timer, kp, vp, 0, m, shift, shift + D, false, s, d_h0, nullptr,
+                                        kbias);
+      ix.info[0] += ix.sw.passes_run;
+      ix.info[1] += ix.sw.passes_skipped;
+      ix.bk_hist.ensure((uint64_t)(nbins + 1) * 8);
+      {
+        TimedLaunch t(ix.timer, "sa_bin_starts", (double)(nbins + 1) * 8);
+        k_bin_starts<<<(nbins + 1 + 255) / 256, 256, 0, s>>>(kp[slot], m, kbias, shift, nbins,
+                                                            ix.bk_hist.as<uint64_t>());
+        HK_HIP(hipGetLastError());
+      }
+      std::vector<uint64_t> st(nbins + 1);
+      HK_HIP(hipMemcpyAsync(st.data(), ix.bk_hist.p, (uint64_t)(nbins + 1) * 8, hipMemcpyDeviceToHost, s));
+      HK_HIP(hipStreamSynchronize(s));
+      for (uint32_t b = 0; b < nbins; ++b) hist[b] = st[b + 1] - st[b];
     }
-    std::vector<uint64_t> st(nbins + 1);
-    HK_HIP(hipMemcpyAsync(st.data(), ix.bk_hist.p, (uint64_t)(nbins + 1) * 8, hipMemcpyDeviceToHost, s));
-    HK_HIP(hipStreamSynchronize(s));
-    for (uint32_t b = 0; b < nbins; ++b) hist[b] = st[b + 1] - st[b];
   } else {
     hist[0] = m;
   }
@@ -1749,16 +1818,15 @@ template bool bucket_sort_slice<uint64_t>(Index&, const KeyGeom&, uint64_t, int,
                                           const uint64_t*);
 
 // ---------------------------------------------------------------- cursor partition (host)
-// Groups the suffixes by bucket (section 1b): pre-pass counts and cursors on the device, pass A
+// Groups n suffixes by bucket (section 1b): pre-pass counts and cursors on the device, pass A
 // launched at once; the bucket counts and digit totals come back behind an event while pass A
 // runs (the host deals the pass-B regions to XCD groups and the caller plans the bucket items
-// meanwhile), then pass B (D > 8).  Leaves the bucket counts in `hist`; returns the slot holding
-// the grouped pairs.
-int cursor_partition(Index& ix, const KeyGeom& kg, const TextKeySrc& tks, uint64_t* kp[2], uint32_t* vp[2],
-                     std::vector<uint64_t>& hist) {
-  const uint64_t n = ix.n;
+// meanwhile), then pass B (D > 8).  bucket = ((key - kbias) >> bitlo) & (2^D - 1).  With `tks` the
+// keys are built from the text (single GPU); without, they are the packed keys in kp[0] / vp[0]
+// (a sharded slice).  Leaves the bucket counts in `hist`; returns the slot holding the grouped pairs.
+int cursor_partition(Index& ix, uint64_t n, int D, int bitlo, uint64_t kbias, const TextKeySrc* tks, uint64_t* kp[2],
+                     uint32_t* vp[2], std::vector<uint64_t>& hist) {
   hipStream_t s = ix.stream;
-  const int D = kg.bucket_bits, sb = kg.sym_bits, pb = kg.pb, bsh = sb - D;
   const int sA = D > 8 ? 8 : 0;   // pass A digit = bucket >> sA
   const uint32_t nb = 1u << D, ndA = 1u << (D - sA);
   const uint64_t span = ceil_div(ceil_div(n, (uint64_t)BH_TILE), 256) * BH_TILE;   // one workgroup per CU
@@ -1775,8 +1843,7 @@ int cursor_partition(Index& ix, const KeyGeom& kg, const TextKeySrc& tks, uint64
   uint64_t* d_hist = ix.bk_hist.as<uint64_t>() + nb;
   static const bool addr_dbg = getenv("HKCSA_CP_ADDR") != nullptr;   // diagnostic: buffer placement
   if (addr_dbg)
-    fprintf(stderr, "[cp addr] k0 %p k1 %p v0 %p v1 %p text %p\n", (void*)kp[0], (void*)kp[1], (void*)vp[0],
-            (void*)vp[1], (void*)tks.text);
+    fprintf(stderr, "[cp addr] k0 %p k1 %p v0 %p v1 %p\n", (void*)kp[0], (void*)kp[1], (void*)vp[0], (void*)vp[1]);
   unsigned long long* d_curA = ix.cp_cur.as<unsigned long long>();
   unsigned long long* d_curB = d_curA + (uint64_t)nspan * 256;
   uint64_t* d_totA = reinterpret_cast<uint64_t*>(d_curB + nb);
@@ -1787,9 +1854,12 @@ int cursor_partition(Index& ix, const KeyGeom& kg, const TextKeySrc& tks, uint64
   uint32_t* h_gtab = reinterpret_cast<uint32_t*>(h_totA + 2 * 257);
   HK_HIP(hipMemsetAsync(d_drain, 0, (uint64_t)nb * 8, s));
   {
-    TimedLaunch t(ix.timer, "sa_bucket_hist", (double)n);
-    k_bucket_hist_spans<<<nspan, BH_T, 0, s>>>(tks.text, n, tks.lutk, tks.skey, tks.g, bsh, D, sA, d_part, d_drain,
-                                               d_spanc, span);
+    TimedLaunch t(ix.timer, "sa_bucket_hist", (double)n * (tks ? 1 : 8));
+    if (tks)
+      k_bucket_hist_spans<<<nspan, BH_T, 0, s>>>(tks->text, n, tks->lutk, tks->skey, tks->g, bitlo - tks->g.pb, D, sA,
+                                                 d_part, d_drain, d_spanc, span);
+    else
+      k_key_hist_spans<<<nspan, BH_T, 0, s>>>(kp[0], n, bitlo, kbias, D, sA, d_part, d_drain, d_spanc, span);
     HK_HIP(hipGetLastError());
     k_bucket_reduce<<<(nb + 255) / 256, 256, 0, s>>>(d_part, d_drain, nspan, stride, nb, d_hist);
     HK_HIP(hipGetLastError());
@@ -1802,16 +1872,20 @@ int cursor_partition(Index& ix, const KeyGeom& kg, const TextKeySrc& tks, uint64
   hipEvent_t ev;
   HK_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
   HK_HIP(hipEventRecord(ev, s));
-  const int outA = D > 8 ? 1 : 0;
+  // pass A: text -> slot D > 8 ? 1 : 0; packed keys: slot 0 -> 1
+  const int outA = tks ? (D > 8 ? 1 : 0) : 1;
   {
-    TimedLaunch t(ix.timer, "radix_part_text", (double)n * (1 + 8 + 4));
+    TimedLaunch t(ix.timer, tks ? "radix_part_text" : "radix_part_keys", (double)n * (tks ? 1 + 8 + 4 : 2 * (8 + 4)));
     const unsigned grid = (unsigned)(8 * ceil_div(nspan, 8u) * (span / CP_TILE));
-    if (tks.g.lb == 2)
-      k_cpart<true, 2><<<grid, CP_T, 0, s>>>(nullptr, nullptr, kp[outA], vp[outA], n, pb + bsh + sA, d_curA,
-                                             nullptr, nullptr, span, tks);
+    if (!tks)
+      k_cpart<1, 0><<<grid, CP_T, 0, s>>>(kp[0], vp[0], kp[1], vp[1], n, bitlo + sA, kbias, d_curA, nullptr, nullptr,
+                                          span, TextKeySrc{});
+    else if (tks->g.lb == 2)
+      k_cpart<0, 2><<<grid, CP_T, 0, s>>>(nullptr, nullptr, kp[outA], vp[outA], n, bitlo + sA, 0, d_curA, nullptr,
+                                          nullptr, span, *tks);
     else
-      k_cpart<true, 0><<<grid, CP_T, 0, s>>>(nullptr, nullptr, kp[outA], vp[outA], n, pb + bsh + sA, d_curA,
-                                             nullptr, nullptr, span, tks);
+      k_cpart<0, 0><<<grid, CP_T, 0, s>>>(nullptr, nullptr, kp[outA], vp[outA], n, bitlo + sA, 0, d_curA, nullptr,
+                                          nullptr, span, *tks);
     HK_HIP(hipGetLastError());
   }
   ix.info[0] += 1;
@@ -1856,12 +1930,13 @@ int cursor_partition(Index& ix, const KeyGeom& kg, const TextKeySrc& tks, uint64
     h_gtab[8] = e;
     HK_HIP(hipMemcpyAsync(d_gtab, h_gtab, (9 + 2 * e) * 4, hipMemcpyHostToDevice, s));
     TimedLaunch t(ix.timer, "radix_part", (double)n * 2 * (8 + 4));
-    k_cpart<false, 0><<<(unsigned)(8 * maxl), CP_T, 0, s>>>(kp[1], vp[1], kp[0], vp[0], n, pb + bsh, d_curB, d_gtab,
-                                                           d_startA, 0, TextKeySrc{});
+    k_cpart<2, 0><<<(unsigned)(8 * maxl), CP_T, 0, s>>>(kp[1], vp[1], kp[0], vp[0], n, bitlo, kbias, d_curB, d_gtab,
+                                                       d_startA, 0, TextKeySrc{});
     HK_HIP(hipGetLastError());
     ix.info[0] += 1;
+    return 0;
   }
-  return 0;
+  return outA;
 }
 
 // ---------------------------------------------------------------- driver
@@ -1912,8 +1987,7 @@ void build_sa_bucketed(Index& ix) {
   uint64_t* d_h0 = reinterpret_cast<uint64_t*>(ix.small.as<uint8_t>() + 5120);
   // whole-symbol buckets: the lookback-free cursor partition (HKCSA_CURSOR=0: the stable onesweep
   // passes with the late bucket histogram, for A/B)
-  static const bool cursor_env = !getenv("HKCSA_CURSOR") || atoi(getenv("HKCSA_CURSOR")) != 0;
-  const bool use_cp = cursor_env && D > 0 && ka.hq > 0 && D <= 16;
+  const bool use_cp = cursor_enabled() && D > 0 && ka.hq > 0 && D <= 16;
   const bool late_hist = D > 0 && ka.hq > 0 && !use_cp;
   if (use_cp) {
     // counted with the partition below
@@ -1954,7 +2028,7 @@ void build_sa_bucketed(Index& ix) {
   int slot = 0;
   bool sorted_by_bucket = false;
   if (use_cp) {
-    slot = cursor_partition(ix, kg, tks, kp, vp, hist);
+    slot = cursor_partition(ix, n, D, pb + bsh, 0, &tks, kp, vp, hist);
     sorted_by_bucket = true;
   } else if (late_hist) {
     // ---- LSD passes over the bucket bits (the first builds the keys from the text), then the
