@@ -624,9 +624,10 @@ static_assert(BF_BINS * 2 == BS_W * 256 * 8, "bin counters alias the match-mask 
 static_assert((BF_BIGCAP + BF_TIECAP) * 2 == BS_V * 256 * 4, "bin and tie lists fill BsShared::whist");
 
 template <typename V, bool TRACE>
-__device__ __forceinline__ bool bucket_sort_fast(BsShared& sh, uint2 it, const uint64_t (&key)[BS_I], uint32_t vmask,
-                                                 uint32_t s0, int pbe, uint64_t symmask, uint64_t base, int lo,
-                                                 int width, int pb, int hb, const uint32_t* __restrict__ vb,
+__device__ __forceinline__ bool bucket_sort_fast(BsShared& sh, uint2 it, const uint64_t (&xs)[BS_I],
+                                                 const uint32_t (&pvr)[BS_H], uint32_t vmask, uint32_t s0,
+                                                 uint64_t xmin, int lo, int width, int pb,
+                                                 const uint32_t* __restrict__ vb,
                                                  V* __restrict__ sab, uint8_t* __restrict__ bwb,
                                                  uint64_t* __restrict__ tie_k, V* __restrict__ tie_v,
                                                  unsigned long long* __restrict__ tie_n, uint64_t (&ts)[8]) {
@@ -637,26 +638,23 @@ __device__ __forceinline__ bool bucket_sort_fast(BsShared& sh, uint2 it, const u
   const uint32_t wmask = width >= 32 ? ~0u : ((1u << width) - 1);
   const uint32_t lowmask = (1u << kb) - 1;
   const uint32_t pmask = (1u << pb) - 1;
-  const uint32_t himask = (1u << hb) - 1;
   uint32_t* const H2 = reinterpret_cast<uint32_t*>(&sh.mt[0][0]);   // u16 pairs, zero on entry
   const uint16_t* const H = reinterpret_cast<const uint16_t*>(H2);
   uint16_t* const blist = reinterpret_cast<uint16_t*>(&sh.whist[0][0]);
   uint16_t* const tlist = blist + BF_BIGCAP;
   uint32_t* const nctr = sh.wsum;   // [0] listed bins, [1] tied records
-  uint32_t lk[BS_I], r0[BS_H], pvr[BS_H];
+  uint32_t lk[BS_I], r0[BS_H];
   // ---- 1. bin histogram; the atomic's return value is the suffix's rank inside its bin
 #pragma unroll
   for (int k = 0; k < BS_I; ++k) {
     const bool valid = (vmask >> k) & 1u;
-    lk[k] = (uint32_t)((((key[k] >> pbe) & symmask) - base) >> lo) & wmask;
-    const uint32_t pv = ((uint32_t)(key[k] >> hb) & pmask) | (((uint32_t)key[k] & himask) << pb);
+    lk[k] = (uint32_t)((xs[k] - xmin) >> lo) & wmask;
     uint32_t r = 0;
     if (valid) {
       const uint32_t bin = lk[k] >> kb, sh16 = 16u * (bin & 1u);
       r = (atomicAdd(&H2[bin >> 1], 1u << sh16) >> sh16) & 0xFFFFu;   // counts <= 18432: no carry
     }
-    if (k < BS_H) { r0[k] = r; pvr[k] = pv; }
-    else { r0[k - BS_H] |= r << 16; pvr[k - BS_H] |= pv << 16; }
+    if (k < BS_H) r0[k] = r; else r0[k - BS_H] |= r << 16;
   }
   __syncthreads();
   if (TRACE) ts[2] = stamp();
@@ -1251,56 +1249,57 @@ __global__ __launch_bounds__(BS_T, 1) void k_bucket_sort_fast(const uint64_t* __
   const uint64_t symmask = sb >= 64 ? ~0ull : ((1ull << sb) - 1);
   const int pbe = pb + hb;
   for (uint32_t i = tid; i < BS_W * 256; i += BS_T) (&sh.mt[0][0])[i] = 0;
-  uint64_t xmin = ~0ull;
+  // the sym fields once (key -> sym - symbias in place, the BWT code / position bits to pvr), then one
+  // reduction of min, max, or, and: the low varying bit of the values is that of the values relative
+  // to the minimum, and the relative width is bits((max - min) >> lo)
+  const uint32_t pmask = (1u << pb) - 1, himask = (1u << hb) - 1;
+  uint32_t pvr[BS_H];
+  uint64_t xmin = ~0ull, xmax = 0, vor = 0, vand = ~0ull;
 #pragma unroll
-  for (int k = 0; k < BS_I; ++k)
+  for (int k = 0; k < BS_I; ++k) {
+    const uint32_t pv = ((uint32_t)(key[k] >> hb) & pmask) | (((uint32_t)key[k] & himask) << pb);
+    if (k < BS_H) pvr[k] = pv; else pvr[k - BS_H] |= pv << 16;
+    const uint64_t x = ((key[k] >> pbe) & symmask) - symbias;
+    key[k] = x;
     if ((vmask >> k) & 1u) {
-      const uint64_t x = ((key[k] >> pbe) & symmask) - symbias;
       xmin = x < xmin ? x : xmin;
+      xmax = x > xmax ? x : xmax;
+      vor |= x;
+      vand &= x;
     }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    const uint64_t t = __shfl_xor(xmin, o, 64);
-    xmin = t < xmin ? t : xmin;
   }
-  if (lane == 0) sh.rv[0][wv] = xmin;
-  __syncthreads();
-#pragma unroll
-  for (int w = 0; w < BS_W; ++w) xmin = sh.rv[0][w] < xmin ? sh.rv[0][w] : xmin;
-  const uint64_t base = symbias + xmin;
-  uint64_t vor = 0, vand = ~0ull;
-#pragma unroll
-  for (int k = 0; k < BS_I; ++k)
-    if ((vmask >> k) & 1u) {
-      const uint64_t sym = ((key[k] >> pbe) & symmask) - base;
-      vor |= sym;
-      vand &= sym;
-    }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
+    const uint64_t a0 = __shfl_xor(xmin, o, 64), a1 = __shfl_xor(xmax, o, 64);
+    xmin = a0 < xmin ? a0 : xmin;
+    xmax = a1 > xmax ? a1 : xmax;
     vor |= __shfl_xor(vor, o, 64);
     vand &= __shfl_xor(vand, o, 64);
   }
-  __syncthreads();
+  uint64_t* const red = reinterpret_cast<uint64_t*>(&sh.whist[0][0]);   // [4][BS_W], free until the lists
   if (lane == 0) {
-    sh.rv[0][wv] = vor;
-    sh.rv[1][wv] = vand;
+    red[wv] = xmin;
+    red[BS_W + wv] = xmax;
+    red[2 * BS_W + wv] = vor;
+    red[3 * BS_W + wv] = vand;
   }
   __syncthreads();
-  vor = 0;
-  vand = ~0ull;
 #pragma unroll
   for (int w = 0; w < BS_W; ++w) {
-    vor |= sh.rv[0][w];
-    vand &= sh.rv[1][w];
+    xmin = red[w] < xmin ? red[w] : xmin;
+    xmax = red[BS_W + w] > xmax ? red[BS_W + w] : xmax;
+    vor |= red[2 * BS_W + w];
+    vand &= red[3 * BS_W + w];
   }
   const uint64_t var = vor ^ vand;
   const int lo = var ? __builtin_ctzll(var) : 0;
-  const int width = var ? 64 - __builtin_clzll(var) - lo : 0;
+  const uint64_t span = (xmax - xmin) >> lo;
+  const int width = var ? 64 - __builtin_clzll(span) : 0;
   if (TRACE) ts[1] = stamp();
+  // (every thread has read the reduction before the fast path reuses whist: its first barrier)
   const bool ok = width >= 1 && width <= 30 &&
-                  bucket_sort_fast<V, TRACE>(sh, it, key, vmask, s0, pbe, symmask, base, lo, width, pb, hb, vals + it.x,
-                                      sa + it.x, bwt + it.x, tie_k, tie_v, tie_n, ts);
+                  bucket_sort_fast<V, TRACE>(sh, it, key, pvr, vmask, s0, xmin, lo, width, pb, vals + it.x,
+                                             sa + it.x, bwt + it.x, tie_k, tie_v, tie_n, ts);
   if (!ok && tid == 0) fb[atomicAdd(fb_n, 1u)] = it;
   if (TRACE) {
     ts[7] = stamp();
