@@ -25,6 +25,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <type_traits>
 
 #include "hk_index.hpp"
 #include "hk_keys.hpp"
@@ -157,27 +158,35 @@ __global__ __launch_bounds__(BH_T, 1) void k_bucket_hist(const uint8_t* __restri
 // Each tile reserves its digit runs with one global atomic per digit (issued before its keys are
 // staged; the result is first needed for the write-out).
 // end of a span pre-pass: the span's 2^D counts as plain u32 stores (reduced by k_bucket_reduce)
-// and its counts of pass A's digit (bucket >> sA, incl. the drained parts already in M)
+// and its counts of pass A's digit (bucket >> sA, incl. the drained parts already in M).  CB = bits
+// per LDS counter (16: two per word, 2^D <= 65536; 8: four per word, 2^D <= 131072).
+template <int CB>
 __device__ __forceinline__ void hist_spans_flush(const uint32_t* H, uint32_t* M, int D, int sA,
                                                  uint32_t* __restrict__ part, uint32_t* __restrict__ spanc) {
+  constexpr int CPW = 32 / CB;
+  constexpr uint32_t CM = (1u << CB) - 1;
   const uint32_t tid = threadIdx.x;
-  const uint32_t nb = 1u << D, np = (nb + 1) / 2;
-  uint2* const pw = reinterpret_cast<uint2*>(part + (uint64_t)blockIdx.x * (np * 2));
-  for (uint32_t i = tid; i < np; i += BH_T) pw[i] = make_uint2(H[i] & 0xFFFFu, H[i] >> 16);
-  // pass A digit counts: contiguous pairs per thread, one LDS add per digit run
+  const uint32_t nb = 1u << D, np = (nb + CPW - 1) / CPW;
+  uint32_t* const pw = part + (uint64_t)blockIdx.x * (np * CPW);
+  for (uint32_t i = tid; i < np; i += BH_T) {
+    const uint32_t v = H[i];
+    if (CPW == 2) reinterpret_cast<uint2*>(pw)[i] = make_uint2(v & CM, v >> 16);
+    else reinterpret_cast<uint4*>(pw)[i] = make_uint4(v & CM, (v >> 8) & CM, (v >> 16) & CM, v >> 24);
+  }
+  // pass A digit counts: contiguous words per thread, one LDS add per digit run
   const uint32_t per = (np + BH_T - 1) / BH_T;
   uint32_t acc = 0, cd = 0;
   for (uint32_t i = tid * per; i < np && i < tid * per + per; ++i) {
     const uint32_t v = H[i];
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const uint32_t d = (2 * i + h) >> sA;
+    for (int h = 0; h < CPW; ++h) {
+      const uint32_t d = (CPW * i + h) >> sA;
       if (d != cd) {
         if (acc) atomicAdd(&M[cd], acc);
         acc = 0;
         cd = d;
       }
-      acc += h ? v >> 16 : v & 0xFFFFu;
+      acc += (v >> (CB * h)) & CM;
     }
   }
   if (acc) atomicAdd(&M[cd], acc);
@@ -185,13 +194,17 @@ __device__ __forceinline__ void hist_spans_flush(const uint32_t* H, uint32_t* M,
   if (tid < 256) spanc[(uint64_t)blockIdx.x * 256 + tid] = M[tid];
 }
 
+template <int CB>
 __global__ __launch_bounds__(BH_T, 1) void k_bucket_hist_spans(const uint8_t* __restrict__ t, uint64_t n,
                                                                const uint16_t* __restrict__ lutk,
                                                                const uint64_t* __restrict__ skey, KeyedArgs g,
                                                                int bsh, int D, int sA, uint32_t* __restrict__ part,
                                                                unsigned long long* __restrict__ drain,
                                                                uint32_t* __restrict__ spanc, uint64_t span) {
-  __shared__ uint32_t H[32768];   // u16 pairs (drained at 0x8000, as k_bucket_hist)
+  // CB-bit counters packed in 32768 words (drained at half range, as k_bucket_hist)
+  constexpr int CPW = 32 / CB;
+  constexpr uint32_t HALF = 1u << (CB - 1);
+  __shared__ uint32_t H[32768];
   __shared__ uint32_t M[256];     // pass A digit counts of this span
   __shared__ uint16_t L[256];
   __shared__ uint64_t SK[72];
@@ -204,19 +217,21 @@ __global__ __launch_bounds__(BH_T, 1) void k_bucket_hist_spans(const uint8_t* __
   if (tid < 72) SK[tid] = skey[tid];
   __syncthreads();
   auto add = [&](uint32_t b) {
-    const uint32_t sh = 16u * (b & 1u);
-    const uint32_t old = atomicAdd(&H[b >> 1], 1u << sh);
-    if (((old >> sh) & 0xFFFFu) == 0x7FFFu) {
-      atomicSub(&H[b >> 1], 0x8000u << sh);
-      atomicAdd(&drain[b], 0x8000ull);
-      atomicAdd(&M[b >> sA], 0x8000u);
+    const uint32_t sh = CB * (b % CPW);
+    const uint32_t old = atomicAdd(&H[b / CPW], 1u << sh);
+    if (((old >> sh) & ((1u << CB) - 1)) == HALF - 1) {
+      atomicSub(&H[b / CPW], HALF << sh);
+      atomicAdd(&drain[b], (unsigned long long)HALF);
+      atomicAdd(&M[b >> sA], HALF);
     }
   };
   const uint64_t lim = n < g.s_start ? n : g.s_start;   // positions with a text window
   const uint64_t lo = (uint64_t)blockIdx.x * span;
   const uint64_t hi = lo + span < n ? lo + span : n;
   const int lb = 31 - __clz((uint32_t)g.Rk);
-  const uint32_t bmask = (1u << D) - 1;
+  // the window of hq symbols (hq * lb <= 32 bits); the bucket is its top D bits
+  const int wbits = g.hq * lb, wdrop = wbits - D;
+  const uint32_t bmask = wbits >= 32 ? ~0u : (1u << wbits) - 1;
   uint4 w0 = make_uint4(0, 0, 0, 0), w1 = w0;
   if (lo + (uint64_t)tid * BH_PER < hi) {
     const uint4* src = reinterpret_cast<const uint4*>(t + lo + (uint64_t)tid * BH_PER);
@@ -238,13 +253,13 @@ __global__ __launch_bounds__(BH_T, 1) void k_bucket_hist_spans(const uint8_t* __
       for (int i = 0; i < 2 * BH_PER - 1; ++i) {
         b = ((b << lb) | (L[(wd[i >> 2] >> (8 * (i & 3))) & 255u] & 255u)) & bmask;
         const int j = i - (g.hq - 1);
-        if (j >= 0 && j < BH_PER && p0 + j < lim2) add(b);
+        if (j >= 0 && j < BH_PER && p0 + j < lim2) add(b >> wdrop);
       }
     }
     for (uint64_t p = p0 > lim ? p0 : lim; p < p0 + BH_PER && p < hi; ++p) add((uint32_t)(SK[p - g.s_start] >> bsh));
   }
   __syncthreads();
-  hist_spans_flush(H, M, D, sA, part, spanc);
+  hist_spans_flush<CB>(H, M, D, sA, part, spanc);
 }
 
 // the pre-pass over the packed keys of a sharded slice: bin = ((key - kbias) >> shift) & (2^D - 1)
@@ -287,7 +302,7 @@ __global__ __launch_bounds__(BH_T, 1) void k_key_hist_spans(const uint64_t* __re
     }
   }
   __syncthreads();
-  hist_spans_flush(H, M, D, sA, part, spanc);
+  hist_spans_flush<16>(H, M, D, sA, part, spanc);
 }
 
 // hist[b] = drained counts + the spans' partial counts of bucket b
@@ -368,20 +383,21 @@ constexpr int CP_T = 512;
 constexpr int CP_I = 16;
 constexpr int CP_TILE = CP_T * CP_I;   // 8192 suffixes per tile
 
+template <int NB, int T = CP_T>
 struct CpShared {
   union {
-    uint64_t keys[CP_TILE];
-    uint32_t vals[CP_TILE];
-    uint16_t codes[CP_TILE + kCodePad];   // pass A: the tile's text codes ...
-    struct {                              // ... or packed codes and raw bytes (radix 2^lb)
-      uint32_t pk[(CP_TILE + 64) / 4 + 4];
-      uint8_t raw[CP_TILE + 64];
+    uint64_t keys[T * CP_I];
+    uint32_t vals[T * CP_I];
+    uint16_t codes[T * CP_I + kCodePad];   // pass A: the tile's text codes ...
+    struct {                               // ... or packed codes and raw bytes (radix 2^lb)
+      uint32_t pk[(T * CP_I + 64) / 4 + 4];
+      uint8_t raw[T * CP_I + 64];
     } ft;
   } stage;
-  uint64_t gb[256];    // destination of the digit's run minus its tile start
-  uint32_t cnt[256];   // digit counts (ranks by LDS atomics)
-  uint32_t tst[256];   // tile-local exclusive digit starts
-  uint32_t wsum[4];
+  uint64_t gb[NB];     // destination of the digit's run minus its tile start
+  uint32_t cnt[NB];    // digit counts (ranks by LDS atomics)
+  uint32_t tst[NB];    // tile-local exclusive digit starts
+  uint32_t wsum[NB / 64];
   uint32_t prev0;
   uint16_t L[256], LP[256];
   uint64_t SK[72];
@@ -393,8 +409,8 @@ struct CpShared {
 // else a tile of one region (from the XCD-group region table) and the row is the region's.
 // MODE 0: pass A over the text (builds the keys); 1: pass A over packed keys (a sharded slice's);
 // 2: pass B over one region per tile.  digit = ((key - kbias) >> shift) & 255.
-template <int MODE, int LB>
-__global__ __launch_bounds__(CP_T, 2) void k_cpart(const uint64_t* __restrict__ kin, const uint32_t* __restrict__ vin,
+template <int MODE, int LB, int NB = 256, int T = CP_T>
+__global__ __launch_bounds__(T, T == 1024 ? 1 : 2) void k_cpart(const uint64_t* __restrict__ kin, const uint32_t* __restrict__ vin,
                                                    uint64_t* __restrict__ kout, uint32_t* __restrict__ vout,
                                                    uint64_t n, int shift, uint64_t kbias,
                                                    unsigned long long* __restrict__ cur,
@@ -403,7 +419,10 @@ __global__ __launch_bounds__(CP_T, 2) void k_cpart(const uint64_t* __restrict__ 
                                                    TextKeySrc src) {
   constexpr int WSPAN = CP_I * 64;
   constexpr bool FT = MODE == 0;
-  __shared__ CpShared sh;
+  static_assert(NB == 256 || NB == 512, "digits per pass");
+  constexpr uint32_t DM = NB - 1;
+  constexpr int TILE = T * CP_I;
+  __shared__ CpShared<NB, T> sh;
   const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   uint64_t tbase;
   uint32_t tn;
@@ -412,17 +431,17 @@ __global__ __launch_bounds__(CP_T, 2) void k_cpart(const uint64_t* __restrict__ 
     // workgroups b, b + 8, ... (one XCD when blocks are dealt round-robin, which only speed relies
     // on) take the spans g, g + 8, ... in order: the runs a cursor row hands out back to back are
     // written from one L2, which merges them into whole lines
-    const uint32_t per = (uint32_t)(span / CP_TILE), g = blockIdx.x & 7u, k = blockIdx.x >> 3;
+    const uint32_t per = (uint32_t)(span / TILE), g = blockIdx.x & 7u, k = blockIdx.x >> 3;
     const uint64_t tile = (uint64_t)(g + 8u * (k / per)) * per + k % per;
-    tbase = tile * CP_TILE;
+    tbase = tile * TILE;
     if (tbase >= n) return;   // past the last span (whole workgroup, before any barrier)
-    tn = (uint32_t)(n - tbase < (uint64_t)CP_TILE ? n - tbase : CP_TILE);
+    tn = (uint32_t)(n - tbase < (uint64_t)TILE ? n - tbase : TILE);
     row = cur + (tbase / span) * 256;
   } else {
     // region table: gtab[g] = first entry of XCD group g (gtab[8] = end), entries {region, first
     // tile}; workgroup b is tile b >> 3 of group b & 7 (see cursor_partition)
     uint32_t* const T2 = reinterpret_cast<uint32_t*>(&sh.stage);   // the table (<= 9 + 512 words), one round trip
-    for (uint32_t i = tid; i < 9 + 2 * 256; i += CP_T) T2[i] = gtab[i];
+    for (uint32_t i = tid; i < 9 + 2 * 256; i += T) T2[i] = gtab[i];
     __syncthreads();
     if (tid == 0) {
       const uint32_t g = blockIdx.x & 7u, k = blockIdx.x >> 3;
@@ -438,21 +457,21 @@ __global__ __launch_bounds__(CP_T, 2) void k_cpart(const uint64_t* __restrict__ 
       }
       uint64_t tb = 0, tl = 0;
       if (d != ~0u) {
-        tb = startA[d] + (uint64_t)(k - k0) * CP_TILE;
+        tb = startA[d] + (uint64_t)(k - k0) * TILE;
         tl = tb < startA[d + 1] ? startA[d + 1] - tb : 0;
       }
       sh.gb[0] = tb;
-      sh.gb[1] = tl < (uint64_t)CP_TILE ? tl : (uint64_t)CP_TILE;
+      sh.gb[1] = tl < (uint64_t)TILE ? tl : (uint64_t)TILE;
       sh.gb[2] = d;
     }
     __syncthreads();
     tbase = sh.gb[0];
     tn = (uint32_t)sh.gb[1];
     if (tn == 0) return;   // past the end of a shorter group (whole workgroup)
-    row = cur + sh.gb[2] * 256;
+    row = cur + sh.gb[2] * NB;
     __syncthreads();   // gb is reused below
   }
-  if (tid < 256) sh.cnt[tid] = 0;
+  if (tid < NB) sh.cnt[tid] = 0;
   const uint32_t s0 = wv * WSPAN + lane;   // item k of this thread is tile slot s0 + 64 k
   uint64_t key[CP_I];
   uint32_t val[CP_I];
@@ -463,7 +482,7 @@ __global__ __launch_bounds__(CP_T, 2) void k_cpart(const uint64_t* __restrict__ 
     }
     if (tid < 72) sh.SK[tid] = src.skey[tid];
     __syncthreads();
-    text_keys<CP_T, CP_I, LB>(key, src, n, tbase, tbase + (uint64_t)wv * WSPAN, lane, sh.stage.codes,
+    text_keys<T, CP_I, LB>(key, src, n, tbase, tbase + (uint64_t)wv * WSPAN, lane, sh.stage.codes,
                               sh.stage.ft.pk, sh.stage.ft.raw, &sh.prev0, sh.L, sh.LP, sh.SK);
 #pragma unroll
     for (int k = 0; k < CP_I; ++k) val[k] = (uint32_t)(tbase + s0 + 64u * k);
@@ -477,21 +496,21 @@ __global__ __launch_bounds__(CP_T, 2) void k_cpart(const uint64_t* __restrict__ 
   uint32_t rk[CP_I];
 #pragma unroll
   for (int k = 0; k < CP_I; ++k) {
-    const uint32_t d = (uint32_t)((key[k] - kbias) >> shift) & 255u;
+    const uint32_t d = (uint32_t)((key[k] - kbias) >> shift) & DM;
     const uint32_t r = s0 + 64u * k < tn ? atomicAdd(&sh.cnt[d], 1u) : 0u;
     rk[k] = r | (d << 16);
   }
   __syncthreads();
   unsigned long long g = 0;
   uint32_t c = 0, inc = 0;
-  if (tid < 256) {
+  if (tid < NB) {
     c = sh.cnt[tid];
     if (c) g = atomicAdd(&row[tid], (unsigned long long)c);   // the digit run's destination
     inc = wave_incl_sum<uint32_t>(c);
     if (lane == 63) sh.wsum[wv] = inc;
   }
   __syncthreads();
-  if (tid < 256) {
+  if (tid < NB) {
     uint32_t carry = 0;
     for (uint32_t w = 0; w < wv; ++w) carry += sh.wsum[w];
     sh.tst[tid] = carry + inc - c;
@@ -500,16 +519,16 @@ __global__ __launch_bounds__(CP_T, 2) void k_cpart(const uint64_t* __restrict__ 
 #pragma unroll
   for (int k = 0; k < CP_I; ++k)
     if (s0 + 64u * k < tn) sh.stage.keys[sh.tst[rk[k] >> 16] + (rk[k] & 0xFFFFu)] = key[k];
-  if (tid < 256) sh.gb[tid] = g - sh.tst[tid];   // first use of the reservation
+  if (tid < NB) sh.gb[tid] = g - sh.tst[tid];   // first use of the reservation
   __syncthreads();
-  uint32_t dg[CP_I / 4] = {};
+  uint32_t dg[CP_I / 2] = {};   // digits of the staged slots, two per register
 #pragma unroll
   for (int i = 0; i < CP_I; ++i) {
-    const uint32_t s = (uint32_t)i * CP_T + tid;
+    const uint32_t s = (uint32_t)i * T + tid;
     if (s < tn) {
       const uint64_t kk = sh.stage.keys[s];
-      const uint32_t d = (uint32_t)((kk - kbias) >> shift) & 255u;
-      dg[i >> 2] |= d << (8 * (i & 3));
+      const uint32_t d = (uint32_t)((kk - kbias) >> shift) & DM;
+      dg[i >> 1] |= d << (16 * (i & 1));
       kout[sh.gb[d] + s] = kk;
     }
   }
@@ -520,8 +539,8 @@ __global__ __launch_bounds__(CP_T, 2) void k_cpart(const uint64_t* __restrict__ 
   __syncthreads();
 #pragma unroll
   for (int i = 0; i < CP_I; ++i) {
-    const uint32_t s = (uint32_t)i * CP_T + tid;
-    if (s < tn) vout[sh.gb[(dg[i >> 2] >> (8 * (i & 3))) & 255u] + s] = sh.stage.vals[s];
+    const uint32_t s = (uint32_t)i * T + tid;
+    if (s < tn) vout[sh.gb[(dg[i >> 1] >> (16 * (i & 1))) & DM] + s] = sh.stage.vals[s];
   }
 }
 
@@ -565,18 +584,20 @@ constexpr int BS_CAP = BS_T * BS_I;   // 18432 suffixes per workgroup
 constexpr int BS_WSPAN = BS_I * 64;
 constexpr int BS_V = BS_W;            // per-wave digit histograms, in element order
 
-struct BsShared {
-  uint32_t buf[BS_CAP];          // u32 plane: local key exchange; positions at the end
-  uint16_t aux[BS_CAP];          // u16 plane: original-slot exchange (prev codes packed in the key),
+template <int T>
+struct BsSharedT {
+  uint32_t buf[T * BS_I];        // u32 plane: local key exchange; positions at the end
+  uint16_t aux[T * BS_I];        // u16 plane: original-slot exchange (prev codes packed in the key),
                                  // or the prev codes by original slot (when they do not fit the key)
-  uint64_t mt[BS_W][256];        // per-wave match masks (lanes holding a digit), zero between items;
+  uint64_t mt[T / 64][256];      // per-wave match masks (lanes holding a digit), zero between items;
                                  // mt[0..1] double as the scan's per-group prefixes
-  uint32_t whist[BS_V][256];     // digit counts per wave -> destination base per wave
+  uint32_t whist[T / 64][256];   // digit counts per wave -> destination base per wave
   uint32_t wloc[256];            // scan: wave-local exclusive digit start
   uint32_t wsum[4];
-  uint64_t rv[2][BS_W];
+  uint64_t rv[2][T / 64];
   uint8_t inv[256];
 };
+using BsShared = BsSharedT<BS_T>;   // the LSD passes (k_bucket_sort) always run 1024-thread items
 
 // diagnostic stamps (TRACE): shader-clock time at the phase boundaries
 __device__ __forceinline__ uint64_t stamp() {
@@ -615,22 +636,26 @@ __device__ __forceinline__ void bs_load_keys(const uint64_t* __restrict__ keys, 
 // match-mask ranking and scatters spent half of their LDS cycles in bank conflicts
 // (profiles/r2_sq_counters.json).  Items with a bin over BF_MAXBIN (skewed keys), more than 30 varying
 // key bits or overflowing lists take the LSD passes (k_bucket_sort).
-constexpr int BF_BITS = 14;
-constexpr int BF_BINS = 1 << BF_BITS;     // 16384 u16 counters (two per u32) = 32 KiB: aliases BsShared::mt
+// Workgroups of T = 1024 (18 432-suffix items, 14-bit bins, one per CU) or 512 threads (9216-suffix
+// items of 2^17 buckets, 13-bit bins, ~80 KiB of LDS: two per CU, so one item's key loads overlap
+// the other's LDS phases).  Bins hold ~1.1 suffixes either way.
+template <int T> constexpr int bf_bits() { return T == 1024 ? 14 : 13; }
 constexpr uint32_t BF_MAXBIN = 32;
-constexpr uint32_t BF_BIGCAP = 4096;      // bins of 3+ records (u16 bin ids in BsShared::whist, first half)
-constexpr uint32_t BF_TIECAP = 4096;      // tied records (u16 final index | head << 15, second half)
-static_assert(BF_BINS * 2 == BS_W * 256 * 8, "bin counters alias the match-mask table");
-static_assert((BF_BIGCAP + BF_TIECAP) * 2 == BS_V * 256 * 4, "bin and tie lists fill BsShared::whist");
 
-template <typename V, bool TRACE>
-__device__ __forceinline__ bool bucket_sort_fast(BsShared& sh, uint2 it, const uint64_t (&xs)[BS_I],
+template <typename V, bool TRACE, int T>
+__device__ __forceinline__ bool bucket_sort_fast(BsSharedT<T>& sh, uint2 it, const uint64_t (&xs)[BS_I],
                                                  const uint32_t (&pvr)[BS_H], uint32_t vmask, uint32_t s0,
                                                  uint64_t xmin, int lo, int width, int pb,
                                                  const uint32_t* __restrict__ vb,
                                                  V* __restrict__ sab, uint8_t* __restrict__ bwb,
                                                  uint64_t* __restrict__ tie_k, V* __restrict__ tie_v,
                                                  unsigned long long* __restrict__ tie_n, uint64_t (&ts)[8]) {
+  constexpr int BF_BITS = bf_bits<T>(), BF_BINS = 1 << BF_BITS;   // u16 counters, two per u32: alias mt
+  constexpr uint32_t BF_BIGCAP = 4u * T;   // bins of 3+ records (u16 bin ids in whist, first half)
+  constexpr uint32_t BF_TIECAP = 4u * T;   // tied records (u16 final index | head << 15, second half)
+  static_assert(BF_BINS * 2 == (T / 64) * 256 * 8, "bin counters alias the match-mask table");
+  static_assert((BF_BIGCAP + BF_TIECAP) * 2 == (T / 64) * 256 * 4, "bin and tie lists fill whist");
+  static_assert(BF_BINS / T == 16, "16 bin counters per thread");
   const uint32_t start = it.x, cnt = it.y;
   const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int fb = width < BF_BITS ? width : BF_BITS;
@@ -682,13 +707,13 @@ __device__ __forceinline__ bool bucket_sort_fast(BsShared& sh, uint2 it, const u
   }
   uint32_t* const wtot = sh.wloc;    // per-wave totals / maxima
   if (lane == 63) wtot[wv] = inc;
-  if (lane == 0) wtot[BS_W + wv] = tmax;
+  if (lane == 0) wtot[(T / 64) + wv] = tmax;
   __syncthreads();
   uint32_t carry = 0, bmax = 0;
 #pragma unroll
-  for (int w = 0; w < BS_W; ++w) {
+  for (int w = 0; w < (T / 64); ++w) {
     carry += (uint32_t)w < wv ? wtot[w] : 0u;
-    bmax = wtot[BS_W + w] > bmax ? wtot[BS_W + w] : bmax;
+    bmax = wtot[(T / 64) + w] > bmax ? wtot[(T / 64) + w] : bmax;
   }
   if (bmax > BF_MAXBIN) return false;   // skewed keys: the LSD passes
   {
@@ -716,15 +741,15 @@ __device__ __forceinline__ bool bucket_sort_fast(BsShared& sh, uint2 it, const u
   // ---- 4. bins of one or two records settle in place: final index by slot into aux; 3+ are listed
   uint32_t bigm = 0;
   {
-    uint32_t pr[BF_BINS / 2 / BS_T], nx[BF_BINS / 2 / BS_T];
+    uint32_t pr[BF_BINS / 2 / T], nx[BF_BINS / 2 / T];
 #pragma unroll
-    for (int j = 0; j < BF_BINS / 2 / BS_T; ++j) {
-      const uint32_t m = tid + BS_T * j;   // bins 2m, 2m + 1
+    for (int j = 0; j < BF_BINS / 2 / T; ++j) {
+      const uint32_t m = tid + T * j;   // bins 2m, 2m + 1
       pr[j] = H2[m];
       nx[j] = m + 1 < (uint32_t)BF_BINS / 2 ? (H2[m + 1] & 0xFFFFu) : cnt;
     }
 #pragma unroll
-    for (int j = 0; j < BF_BINS / 2 / BS_T; ++j) {
+    for (int j = 0; j < BF_BINS / 2 / T; ++j) {
 #pragma unroll
       for (int h = 0; h < 2; ++h) {   // branch-free: the loads of all 16 bins issue together
         const uint32_t s = h ? pr[j] >> 16 : pr[j] & 0xFFFFu;
@@ -755,7 +780,7 @@ __device__ __forceinline__ bool bucket_sort_fast(BsShared& sh, uint2 it, const u
     while (bigm) {
       const int q = __builtin_ctz(bigm);
       bigm &= bigm - 1;
-      if (bbase < BF_BIGCAP) blist[bbase] = (uint16_t)(2u * (tid + BS_T * (q >> 1)) + (q & 1));
+      if (bbase < BF_BIGCAP) blist[bbase] = (uint16_t)(2u * (tid + T * (q >> 1)) + (q & 1));
       ++bbase;
     }
   }
@@ -765,7 +790,7 @@ __device__ __forceinline__ bool bucket_sort_fast(BsShared& sh, uint2 it, const u
   if (nbig > BF_BIGCAP) return false;
   // ---- 5. listed bins, one thread each: up to 8 records ranked in registers (all loads in flight
   // together), larger bins insertion-sorted in place; final indices by slot, equal keys listed
-  for (uint32_t i = tid; i < nbig; i += BS_T) {
+  for (uint32_t i = tid; i < nbig; i += T) {
     const uint32_t bn = blist[i];
     const uint32_t s = H[bn], e = bn + 1 < (uint32_t)BF_BINS ? (uint32_t)H[bn + 1] : cnt;
     const uint32_t c = e - s;
@@ -858,7 +883,7 @@ __device__ __forceinline__ bool bucket_sort_fast(BsShared& sh, uint2 it, const u
   }
   if (ntie) {
     const uint64_t tb = sh.rv[1][0];
-    for (uint32_t i = tid; i < ntie; i += BS_T) {
+    for (uint32_t i = tid; i < ntie; i += T) {
       const uint32_t e = tlist[i], f = e & 0x7FFFu;
       const uint32_t pv = sh.aux[f];
       tie_k[tb + i] = (((uint64_t)start + f) << 1) | (e >> 15);
@@ -1223,8 +1248,8 @@ __global__ __launch_bounds__(BS_T, 1) void k_bucket_sort(const uint64_t* __restr
 
 // Fast-path kernel: the same prologue (the item's sym range and varying bits), then the MSD + bin-rank
 // sort; items it cannot take (wide keys, a bin over BF_MAXBIN) are appended to `fb` for k_bucket_sort.
-template <typename V, bool TRACE>
-__global__ __launch_bounds__(BS_T, 1) void k_bucket_sort_fast(const uint64_t* __restrict__ keys,
+template <typename V, bool TRACE, int T>
+__global__ __launch_bounds__(T, T == 1024 ? 1 : 4) void k_bucket_sort_fast(const uint64_t* __restrict__ keys,
                                                               const uint32_t* __restrict__ vals,
                                                               const uint2* __restrict__ items, int pb, int sb, int hb,
                                                               uint64_t symbias, const uint8_t* __restrict__ inv,
@@ -1233,7 +1258,7 @@ __global__ __launch_bounds__(BS_T, 1) void k_bucket_sort_fast(const uint64_t* __
                                                               unsigned long long* __restrict__ tie_n,
                                                               uint2* __restrict__ fb, unsigned int* __restrict__ fb_n,
                                                               uint64_t* __restrict__ trace) {
-  __shared__ BsShared sh;
+  __shared__ BsSharedT<T> sh;
   const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   uint64_t ts[8] = {0};
   if (TRACE) ts[0] = stamp();
@@ -1248,7 +1273,7 @@ __global__ __launch_bounds__(BS_T, 1) void k_bucket_sort_fast(const uint64_t* __
 
   const uint64_t symmask = sb >= 64 ? ~0ull : ((1ull << sb) - 1);
   const int pbe = pb + hb;
-  for (uint32_t i = tid; i < BS_W * 256; i += BS_T) (&sh.mt[0][0])[i] = 0;
+  for (uint32_t i = tid; i < (T / 64) * 256; i += T) (&sh.mt[0][0])[i] = 0;
   // the sym fields once (key -> sym - symbias in place, the BWT code / position bits to pvr), then one
   // reduction of min, max, or, and: the low varying bit of the values is that of the values relative
   // to the minimum, and the relative width is bits((max - min) >> lo)
@@ -1276,20 +1301,20 @@ __global__ __launch_bounds__(BS_T, 1) void k_bucket_sort_fast(const uint64_t* __
     vor |= __shfl_xor(vor, o, 64);
     vand &= __shfl_xor(vand, o, 64);
   }
-  uint64_t* const red = reinterpret_cast<uint64_t*>(&sh.whist[0][0]);   // [4][BS_W], free until the lists
+  uint64_t* const red = reinterpret_cast<uint64_t*>(&sh.whist[0][0]);   // [4][(T / 64)], free until the lists
   if (lane == 0) {
     red[wv] = xmin;
-    red[BS_W + wv] = xmax;
-    red[2 * BS_W + wv] = vor;
-    red[3 * BS_W + wv] = vand;
+    red[(T / 64) + wv] = xmax;
+    red[2 * (T / 64) + wv] = vor;
+    red[3 * (T / 64) + wv] = vand;
   }
   __syncthreads();
 #pragma unroll
-  for (int w = 0; w < BS_W; ++w) {
+  for (int w = 0; w < (T / 64); ++w) {
     xmin = red[w] < xmin ? red[w] : xmin;
-    xmax = red[BS_W + w] > xmax ? red[BS_W + w] : xmax;
-    vor |= red[2 * BS_W + w];
-    vand &= red[3 * BS_W + w];
+    xmax = red[(T / 64) + w] > xmax ? red[(T / 64) + w] : xmax;
+    vor |= red[2 * (T / 64) + w];
+    vand &= red[3 * (T / 64) + w];
   }
   const uint64_t var = vor ^ vand;
   const int lo = var ? __builtin_ctzll(var) : 0;
@@ -1298,7 +1323,7 @@ __global__ __launch_bounds__(BS_T, 1) void k_bucket_sort_fast(const uint64_t* __
   if (TRACE) ts[1] = stamp();
   // (every thread has read the reduction before the fast path reuses whist: its first barrier)
   const bool ok = width >= 1 && width <= 30 &&
-                  bucket_sort_fast<V, TRACE>(sh, it, key, pvr, vmask, s0, xmin, lo, width, pb, vals + it.x,
+                  bucket_sort_fast<V, TRACE, T>(sh, it, key, pvr, vmask, s0, xmin, lo, width, pb, vals + it.x,
                                              sa + it.x, bwt + it.x, tie_k, tie_v, tie_n, ts);
   if (!ok && tid == 0) fb[atomicAdd(fb_n, 1u)] = it;
   if (TRACE) {
@@ -1401,10 +1426,12 @@ struct BucketPlan {
   std::vector<uint2> items_n, items_w;       // {start, count}: narrow / wide local keys
   std::vector<uint64_t> big_start, big_cstart;
   uint64_t big_total = 0;
+  uint64_t cap = BS_CAP;                     // suffixes per item: 18 432, or 9216 (512-thread fast sorts)
 };
 
-BucketPlan plan_buckets(const std::vector<uint64_t>& hist, int bsh) {
+BucketPlan plan_buckets(const std::vector<uint64_t>& hist, int bsh, uint64_t cap) {
   BucketPlan pl;
+  pl.cap = cap;
   const bool wide_geom = bsh > 32;
   uint64_t off = 0, istart = 0, icnt = 0;
   uint32_t ib0 = 0;
@@ -1418,14 +1445,14 @@ BucketPlan plan_buckets(const std::vector<uint64_t>& hist, int bsh) {
   for (uint32_t b = 0; b < (uint32_t)hist.size(); ++b) {
     const uint64_t c = hist[b];
     if (!c) continue;
-    if (c > (uint64_t)BS_CAP) {
+    if (c > cap) {
       flush(prev_b);
       pl.big_cstart.push_back(pl.big_total);
       pl.big_start.push_back(off);
       pl.big_total += c;
     } else {
       const bool keep_narrow = !wide_geom && icnt && bsh + (32 - __builtin_clz(b ^ ib0)) > 32;
-      if (icnt && (icnt + c > (uint64_t)BS_CAP || keep_narrow)) flush(prev_b);
+      if (icnt && (icnt + c > cap || keep_narrow)) flush(prev_b);
       if (!icnt) {
         istart = off;
         ib0 = b;
@@ -1469,14 +1496,23 @@ uint64_t sort_bucket_items(Index& ix, const BucketPlan& plan, const uint64_t* ke
       ix.bk_fb.ensure(nn * sizeof(uint2) + 16);
       unsigned int* fbn = reinterpret_cast<unsigned int*>(ix.small.as<uint8_t>() + 4352);   // small+4352: fallback count
       HK_HIP(hipMemsetAsync(fbn, 0, 4, s));
-      if (trace)
-        k_bucket_sort_fast<V, true><<<grid_n, BS_T, 0, s>>>(
+      auto launch = [&](auto ttag, auto trtag) {
+        constexpr int T = decltype(ttag)::value;
+        constexpr bool TR = decltype(trtag)::value;
+        k_bucket_sort_fast<V, TR, T><<<grid_n, T, 0, s>>>(
             keys, vals, ix.bk_items.as<uint2>(), pb, sb, hb, symbias, d_inv, sa, bwt, ix.ties_k.as<uint64_t>(),
-            ix.ties_v.as<V>(), ix.ties_n.as<unsigned long long>(), ix.bk_fb.as<uint2>(), fbn, tbuf.as<uint64_t>());
-      else
-        k_bucket_sort_fast<V, false><<<grid_n, BS_T, 0, s>>>(
-            keys, vals, ix.bk_items.as<uint2>(), pb, sb, hb, symbias, d_inv, sa, bwt, ix.ties_k.as<uint64_t>(),
-            ix.ties_v.as<V>(), ix.ties_n.as<unsigned long long>(), ix.bk_fb.as<uint2>(), fbn, nullptr);
+            ix.ties_v.as<V>(), ix.ties_n.as<unsigned long long>(), ix.bk_fb.as<uint2>(), fbn,
+            TR ? tbuf.as<uint64_t>() : nullptr);
+      };
+      using T512 = std::integral_constant<int, 512>;
+      using T1024 = std::integral_constant<int, 1024>;
+      using TrOn = std::integral_constant<bool, true>;
+      using TrOff = std::integral_constant<bool, false>;
+      if (plan.cap <= (uint64_t)512 * BS_I) {
+        if (trace) launch(T512{}, TrOn{}); else launch(T512{}, TrOff{});
+      } else {
+        if (trace) launch(T1024{}, TrOn{}); else launch(T1024{}, TrOff{});
+      }
       HK_HIP(hipGetLastError());
       if (trace) {
         std::vector<uint64_t> h(nn * 8);
@@ -1781,7 +1817,7 @@ bool bucket_sort_slice(Index& ix, const KeyGeom& kg, uint64_t m, int hb, const S
   } else {
     hist[0] = m;
   }
-  const BucketPlan plan = plan_buckets(hist, bins.bsh);
+  const BucketPlan plan = plan_buckets(hist, bins.bsh, BS_CAP);
   ix.info[4] = plan.items_n.size() + plan.items_w.size();
   ix.info[5] = plan.big_start.size();
   ix.info[6] = plan.big_total;
@@ -1826,7 +1862,9 @@ template bool bucket_sort_slice<uint64_t>(Index&, const KeyGeom&, uint64_t, int,
 int cursor_partition(Index& ix, uint64_t n, int D, int bitlo, uint64_t kbias, const TextKeySrc* tks, uint64_t* kp[2],
                      uint32_t* vp[2], std::vector<uint64_t>& hist) {
   hipStream_t s = ix.stream;
-  const int sA = D > 8 ? 8 : 0;   // pass A digit = bucket >> sA
+  if (D > 17 || (!tks && D > 16)) throw ApiError{-1, "cursor partition: too many bucket bits"};
+  // pass A digit = bucket >> sA (its top 8 bits, all of it for D <= 8); pass B digit = the low sA bits
+  const int sA = D > 16 ? D - 8 : (D > 8 ? 8 : 0);
   const uint32_t nb = 1u << D, ndA = 1u << (D - sA);
   const uint64_t span = ceil_div(ceil_div(n, (uint64_t)BH_TILE), 256) * BH_TILE;   // one workgroup per CU
   const uint32_t nspan = (uint32_t)ceil_div(n, span);
@@ -1854,9 +1892,12 @@ int cursor_partition(Index& ix, uint64_t n, int D, int bitlo, uint64_t kbias, co
   HK_HIP(hipMemsetAsync(d_drain, 0, (uint64_t)nb * 8, s));
   {
     TimedLaunch t(ix.timer, "sa_bucket_hist", (double)n * (tks ? 1 : 8));
-    if (tks)
-      k_bucket_hist_spans<<<nspan, BH_T, 0, s>>>(tks->text, n, tks->lutk, tks->skey, tks->g, bitlo - tks->g.pb, D, sA,
-                                                 d_part, d_drain, d_spanc, span);
+    if (tks && D > 16)   // 2^17 buckets: u8 counters (drained at 128)
+      k_bucket_hist_spans<8><<<nspan, BH_T, 0, s>>>(tks->text, n, tks->lutk, tks->skey, tks->g, bitlo - tks->g.pb, D,
+                                                    sA, d_part, d_drain, d_spanc, span);
+    else if (tks)
+      k_bucket_hist_spans<16><<<nspan, BH_T, 0, s>>>(tks->text, n, tks->lutk, tks->skey, tks->g, bitlo - tks->g.pb, D,
+                                                     sA, d_part, d_drain, d_spanc, span);
     else
       k_key_hist_spans<<<nspan, BH_T, 0, s>>>(kp[0], n, bitlo, kbias, D, sA, d_part, d_drain, d_spanc, span);
     HK_HIP(hipGetLastError());
@@ -1913,6 +1954,9 @@ int cursor_partition(Index& ix, uint64_t n, int D, int bitlo, uint64_t kbias, co
       grp[g].push_back(d);
       load[g] += ceil_div(totA[d], (uint64_t)CP_TILE);
     }
+    // 9-bit digits: 1024-thread tiles (twice the run length per digit)
+    static const bool big_b = !getenv("HKCSA_CP_B1024") || atoi(getenv("HKCSA_CP_B1024")) != 0;
+    const uint64_t btile = sA > 8 && big_b ? 1024 * CP_I : CP_TILE;
     uint32_t e = 0;
     uint64_t maxl = 0;
     for (int g = 0; g < 8; ++g) {
@@ -1921,7 +1965,7 @@ int cursor_partition(Index& ix, uint64_t n, int D, int bitlo, uint64_t kbias, co
       for (uint32_t d : grp[g]) {
         h_gtab[9 + 2 * e] = d;
         h_gtab[9 + 2 * e + 1] = k0;
-        k0 += (uint32_t)ceil_div(totA[d], (uint64_t)CP_TILE);
+        k0 += (uint32_t)ceil_div(totA[d], btile);
         ++e;
       }
       maxl = std::max<uint64_t>(maxl, k0);
@@ -1929,8 +1973,15 @@ int cursor_partition(Index& ix, uint64_t n, int D, int bitlo, uint64_t kbias, co
     h_gtab[8] = e;
     HK_HIP(hipMemcpyAsync(d_gtab, h_gtab, (9 + 2 * e) * 4, hipMemcpyHostToDevice, s));
     TimedLaunch t(ix.timer, "radix_part", (double)n * 2 * (8 + 4));
-    k_cpart<2, 0><<<(unsigned)(8 * maxl), CP_T, 0, s>>>(kp[1], vp[1], kp[0], vp[0], n, bitlo, kbias, d_curB, d_gtab,
-                                                       d_startA, 0, TextKeySrc{});
+    if (sA > 8 && btile > CP_TILE)
+      k_cpart<2, 0, 512, 1024><<<(unsigned)(8 * maxl), 1024, 0, s>>>(kp[1], vp[1], kp[0], vp[0], n, bitlo, kbias,
+                                                                      d_curB, d_gtab, d_startA, 0, TextKeySrc{});
+    else if (sA > 8)
+      k_cpart<2, 0, 512><<<(unsigned)(8 * maxl), CP_T, 0, s>>>(kp[1], vp[1], kp[0], vp[0], n, bitlo, kbias, d_curB,
+                                                              d_gtab, d_startA, 0, TextKeySrc{});
+    else
+      k_cpart<2, 0><<<(unsigned)(8 * maxl), CP_T, 0, s>>>(kp[1], vp[1], kp[0], vp[0], n, bitlo, kbias, d_curB, d_gtab,
+                                                         d_startA, 0, TextKeySrc{});
     HK_HIP(hipGetLastError());
     ix.info[0] += 1;
     return 0;
@@ -1962,21 +2013,35 @@ void build_sa_bucketed(Index& ix) {
   const KeyGeom kg = key_geometry_keyed(ix);
   upload_geometry(ix, kg);
   ix.info[3] = (uint64_t)kg.q;
-  const int D = kg.bucket_bits, sb = kg.sym_bits, pb = kg.pb;
-  const int bsh = sb - D;
+  int D = kg.bucket_bits;
+  const int sb = kg.sym_bits, pb = kg.pb;
   const uint8_t* small = ix.small.as<uint8_t>();
   const uint16_t* d_lutp = reinterpret_cast<const uint16_t*>(small + 4608);
   const uint16_t* d_lutk = reinterpret_cast<const uint16_t*>(small + 2560);
   const uint64_t* d_skey = reinterpret_cast<const uint64_t*>(small + 3584);
   const KeyChunks kch = key_chunks(kg.Rk, kg.q);
   KeyedArgs ka{kg.Rk, kch.Rck, kch.Rlast, kg.s_start, kg.q, kch.ck, kg.pb, 0};
+  // half items: one more bucket bit and 9216-suffix items sorted by 512-thread workgroups, two per
+  // CU (the cursor pre-pass takes ceil((D + 1) / lb) symbols and drops the excess low bits);
+  // HKCSA_HALF_ITEMS=0 keeps 18 432-suffix items (A/B)
+  static const bool half_env = !getenv("HKCSA_HALF_ITEMS") || atoi(getenv("HKCSA_HALF_ITEMS")) != 0;
+  int item_T = 1024;
   {
     // first hq symbols are exactly the top D bits when Rk = 2^k, k | D and no short key exceeds Rk^q - 1
     const int lb = (kg.Rk & (kg.Rk - 1)) == 0 ? __builtin_ctzll(kg.Rk) : 0;
-    if (lb && D > 0 && D % lb == 0 && sb == lb * kg.q) ka.hq = D / lb;
+    const bool whole = lb && sb == lb * kg.q;
+    const int hq1 = lb ? (D + 1 + lb - 1) / lb : 0;
+    if (half_env && cursor_enabled() && whole && D > 0 && D + 1 <= 17 && D + 1 <= sb && hq1 * lb <= 32 && hq1 <= 16) {
+      D += 1;
+      ka.hq = hq1;
+      item_T = 512;
+    } else if (whole && D > 0 && D % lb == 0) {
+      ka.hq = D / lb;
+    }
     // packed bit windows need whole codes per 32-bit word: lb in {1, 2, 4, 8}
-    if (lb && 32 % lb == 0 && sb == lb * kg.q) ka.lb = lb;
+    if (lb && 32 % lb == 0 && whole) ka.lb = lb;
   }
+  const int bsh = sb - D;
 
   // ---- 1. bucket histogram.  Radix 2^k with whole-symbol buckets: only the first LSD pass's digit
   // histogram is taken from the text now; the bucket counts come from the sorted keys after the
@@ -1986,7 +2051,7 @@ void build_sa_bucketed(Index& ix) {
   uint64_t* d_h0 = reinterpret_cast<uint64_t*>(ix.small.as<uint8_t>() + 5120);
   // whole-symbol buckets: the lookback-free cursor partition (HKCSA_CURSOR=0: the stable onesweep
   // passes with the late bucket histogram, for A/B)
-  const bool use_cp = cursor_enabled() && D > 0 && ka.hq > 0 && D <= 16;
+  const bool use_cp = cursor_enabled() && D > 0 && ka.hq > 0 && D <= 17;
   const bool late_hist = D > 0 && ka.hq > 0 && !use_cp;
   if (use_cp) {
     // counted with the partition below
@@ -2050,7 +2115,7 @@ void build_sa_bucketed(Index& ix) {
   }
 
   // ---- 2. work items (whole buckets, packed while they fit) and big buckets
-  const BucketPlan plan = plan_buckets(hist, bsh);
+  const BucketPlan plan = plan_buckets(hist, bsh, item_T == 512 ? (uint64_t)512 * BS_I : (uint64_t)BS_CAP);
   const std::vector<uint2>& items_n = plan.items_n;
   const std::vector<uint2>& items_w = plan.items_w;
   const std::vector<uint64_t>& big_start = plan.big_start;
