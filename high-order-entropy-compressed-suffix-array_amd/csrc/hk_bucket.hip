@@ -41,6 +41,7 @@ constexpr int BH_T = 1024;
 constexpr int BH_PER = 16;                  // consecutive positions per thread (radix-2^k path)
 constexpr int BH_TILE = BH_T * BH_PER;      // 16384 positions per iteration = 2 radix tiles
 constexpr int BH_STAGE = 4096;              // staged positions per iteration of the generic path
+constexpr uint32_t CP_NAM = 512;           // cursor partition: pass A digit rows (<= 9-bit digits)
 
 __device__ __forceinline__ void bh_add(uint32_t* H, uint32_t b, unsigned long long* __restrict__ hist) {
   const uint32_t sh = 16u * (b & 1u);
@@ -143,6 +144,24 @@ __global__ __launch_bounds__(BH_T, 1) void k_bucket_hist(const uint8_t* __restri
   }
 }
 
+// Packed records of the single-GPU cursor partition (k_cpart PK, the PK item sorts): one u64 per
+// suffix, (key bits below pass A's 9-bit digit) << pbits | position.  Their prev field is the keyed
+// code (pb2 bits) when the terminal is unkeyed (tcode >= 0, the dense code of the terminal, which
+// precedes only suffix 0): the BWT byte of position 0 is the terminal, every other code maps back
+// as code + (code >= tcode).
+struct PkGeom {
+  int pbits = 0, pb = 0, pb2 = 0, tcode = -1;
+};
+
+// a record's key bits below the pass A digit in the full (pb-bit prev) layout
+__device__ __forceinline__ uint64_t pk_full_low(uint64_t rec, const PkGeom& g) {
+  const uint64_t kr = rec >> g.pbits;
+  const uint64_t pos = rec & ((1ull << g.pbits) - 1);
+  uint32_t pf = (uint32_t)kr & ((1u << g.pb2) - 1);
+  if (g.tcode >= 0) pf = pos == 0 ? (uint32_t)g.tcode : pf + (pf >= (uint32_t)g.tcode ? 1u : 0u);
+  return ((kr >> g.pb2) << g.pb) | pf;
+}
+
 // ------------------------------------------------------------ 1b. cursor partition
 // The bucket grouping needs no stable passes: the LDS bucket sort orders every bucket completely
 // and equal keys are refined, so the order inside a bucket is free.  Two scatter passes whose
@@ -157,17 +176,20 @@ __global__ __launch_bounds__(BH_T, 1) void k_bucket_hist(const uint8_t* __restri
 //             low 8 bits; cursors per bucket, started at the bucket starts.
 // Each tile reserves its digit runs with one global atomic per digit (issued before its keys are
 // staged; the result is first needed for the write-out).
-// end of a span pre-pass: the span's 2^D counts as plain u32 stores (reduced by k_bucket_reduce)
+// end of a span pre-pass: the span's bucket counts as plain u32 stores (reduced by k_bucket_reduce)
 // and its counts of pass A's digit (bucket >> sA, incl. the drained parts already in M).  CB = bits
-// per LDS counter (16: two per word, 2^D <= 65536; 8: four per word, 2^D <= 131072).
+// per LDS counter (16: two per word, 2^D <= 65536; 8: four per word, 2^D <= 131072).  The LDS
+// counters hold buckets [boff, boff + nbl) of the 2^D (boff > 0: the second half of an exact
+// two-run count, whose digit counts add to the first run's).
 template <int CB>
-__device__ __forceinline__ void hist_spans_flush(const uint32_t* H, uint32_t* M, int D, int sA,
-                                                 uint32_t* __restrict__ part, uint32_t* __restrict__ spanc) {
+__device__ __forceinline__ void hist_spans_flush(const uint32_t* H, uint32_t* M, uint32_t nbl, uint32_t boff,
+                                                 uint32_t stride, int sA, uint32_t* __restrict__ part,
+                                                 uint32_t* __restrict__ spanc) {
   constexpr int CPW = 32 / CB;
   constexpr uint32_t CM = (1u << CB) - 1;
   const uint32_t tid = threadIdx.x;
-  const uint32_t nb = 1u << D, np = (nb + CPW - 1) / CPW;
-  uint32_t* const pw = part + (uint64_t)blockIdx.x * (np * CPW);
+  const uint32_t np = (nbl + CPW - 1) / CPW;
+  uint32_t* const pw = part + (uint64_t)blockIdx.x * stride + boff;
   for (uint32_t i = tid; i < np; i += BH_T) {
     const uint32_t v = H[i];
     if (CPW == 2) reinterpret_cast<uint2*>(pw)[i] = make_uint2(v & CM, v >> 16);
@@ -180,7 +202,7 @@ __device__ __forceinline__ void hist_spans_flush(const uint32_t* H, uint32_t* M,
     const uint32_t v = H[i];
 #pragma unroll
     for (int h = 0; h < CPW; ++h) {
-      const uint32_t d = (CPW * i + h) >> sA;
+      const uint32_t d = (boff + CPW * i + h) >> sA;
       if (d != cd) {
         if (acc) atomicAdd(&M[cd], acc);
         acc = 0;
@@ -191,36 +213,49 @@ __device__ __forceinline__ void hist_spans_flush(const uint32_t* H, uint32_t* M,
   }
   if (acc) atomicAdd(&M[cd], acc);
   __syncthreads();
-  if (tid < 256) spanc[(uint64_t)blockIdx.x * 256 + tid] = M[tid];
+  if (tid < CP_NAM) {
+    uint32_t* const sc = spanc + (uint64_t)blockIdx.x * CP_NAM + tid;
+    *sc = (boff ? *sc : 0u) + M[tid];
+  }
 }
 
-template <int CB>
+// CB = 8 (2^17 buckets): a byte drained at 128 can still pass 255 when ~128+ increments to one
+// bucket land before the drain (every thread inside one long run of a symbol); any increment that
+// sees a byte at >= 224 raises *ovf, pass A then skips itself and the host recounts exactly with two
+// CB = 16 runs over the bucket halves (HB = 0, 1: only buckets with b >> 16 == HB; HB = -1: all).
+template <int CB, int HB = -1>
 __global__ __launch_bounds__(BH_T, 1) void k_bucket_hist_spans(const uint8_t* __restrict__ t, uint64_t n,
                                                                const uint16_t* __restrict__ lutk,
                                                                const uint64_t* __restrict__ skey, KeyedArgs g,
                                                                int bsh, int D, int sA, uint32_t* __restrict__ part,
                                                                unsigned long long* __restrict__ drain,
-                                                               uint32_t* __restrict__ spanc, uint64_t span) {
+                                                               uint32_t* __restrict__ spanc, uint64_t span,
+                                                               unsigned long long* __restrict__ ovf) {
+  constexpr int hb = HB;
   // CB-bit counters packed in 32768 words (drained at half range, as k_bucket_hist)
   constexpr int CPW = 32 / CB;
   constexpr uint32_t HALF = 1u << (CB - 1);
+  const uint32_t boff = hb > 0 ? 65536u : 0u;
+  bool bad = false;
   __shared__ uint32_t H[32768];
-  __shared__ uint32_t M[256];     // pass A digit counts of this span
+  __shared__ uint32_t M[CP_NAM];  // pass A digit counts of this span
   __shared__ uint16_t L[256];
   __shared__ uint64_t SK[72];
   const uint32_t tid = threadIdx.x;
   for (uint32_t i = tid; i < 32768; i += BH_T) H[i] = 0;
-  if (tid < 256) {
-    M[tid] = 0;
-    L[tid] = lutk[tid];
-  }
+  if (tid < CP_NAM) M[tid] = 0;
+  if (tid < 256) L[tid] = lutk[tid];
   if (tid < 72) SK[tid] = skey[tid];
   __syncthreads();
   auto add = [&](uint32_t b) {
-    const uint32_t sh = CB * (b % CPW);
-    const uint32_t old = atomicAdd(&H[b / CPW], 1u << sh);
-    if (((old >> sh) & ((1u << CB) - 1)) == HALF - 1) {
-      atomicSub(&H[b / CPW], HALF << sh);
+    if (hb >= 0 && (b >> 16) != (uint32_t)hb) return;
+    const uint32_t bl = b - boff;
+    const uint32_t sh = CB * (bl % CPW);
+    const uint32_t old = atomicAdd(&H[bl / CPW], 1u << sh);
+    const uint32_t ob = (old >> sh) & ((1u << CB) - 1);
+    if (CB == 8) bad |= ob >= 224u;
+    if (ob == HALF - 1) {
+      atomicSub(&H[bl / CPW], HALF << sh);
       atomicAdd(&drain[b], (unsigned long long)HALF);
       atomicAdd(&M[b >> sA], HALF);
     }
@@ -258,8 +293,10 @@ __global__ __launch_bounds__(BH_T, 1) void k_bucket_hist_spans(const uint8_t* __
     }
     for (uint64_t p = p0 > lim ? p0 : lim; p < p0 + BH_PER && p < hi; ++p) add((uint32_t)(SK[p - g.s_start] >> bsh));
   }
+  if (CB == 8 && bad) atomicOr(ovf, 1ull);
   __syncthreads();
-  hist_spans_flush<CB>(H, M, D, sA, part, spanc);
+  const uint32_t nbl = hb >= 0 ? 65536u : 1u << D;
+  hist_spans_flush<CB>(H, M, nbl, boff, 1u << D, sA, part, spanc);
 }
 
 // the pre-pass over the packed keys of a sharded slice: bin = ((key - kbias) >> shift) & (2^D - 1)
@@ -268,10 +305,10 @@ __global__ __launch_bounds__(BH_T, 1) void k_key_hist_spans(const uint64_t* __re
                                                             unsigned long long* __restrict__ drain,
                                                             uint32_t* __restrict__ spanc, uint64_t span) {
   __shared__ uint32_t H[32768];
-  __shared__ uint32_t M[256];
+  __shared__ uint32_t M[CP_NAM];
   const uint32_t tid = threadIdx.x;
   for (uint32_t i = tid; i < 32768; i += BH_T) H[i] = 0;
-  if (tid < 256) M[tid] = 0;
+  if (tid < CP_NAM) M[tid] = 0;
   __syncthreads();
   const uint32_t bmask = (1u << D) - 1;
   auto add = [&](uint64_t k) {
@@ -302,7 +339,7 @@ __global__ __launch_bounds__(BH_T, 1) void k_key_hist_spans(const uint64_t* __re
     }
   }
   __syncthreads();
-  hist_spans_flush<16>(H, M, D, sA, part, spanc);
+  hist_spans_flush<16>(H, M, 1u << D, 0, 1u << D, sA, part, spanc);
 }
 
 // hist[b] = drained counts + the spans' partial counts of bucket b
@@ -317,65 +354,89 @@ __global__ __launch_bounds__(256) void k_bucket_reduce(const uint32_t* __restric
   hist[b] = s;
 }
 
-// Cursors of both passes from the counts (one workgroup): pass B's per bucket = the bucket starts,
-// pass A's per (span, digit) = the digit's start + the earlier spans' counts; also the digit
-// totals and starts (region bounds of pass B) for the host and pass B.
+// Cursors of both passes from the counts, in two small kernels over blocks of 64 digits x 16
+// span groups (one workgroup scanning every span of every digit took 0.25-0.5 ms of serial loads):
+// k_cp_colsum: per digit, the span groups' partial sums (exclusive over groups) and the digit total;
+// k_cp_cursors: every block scans the digit totals (digit starts; block 0 publishes them as the
+// region bounds of pass B), then each (digit, group) thread walks its spans: pass A's cursor of
+// (span, digit) = the digit's start + the earlier spans' counts.  The last block instead scans the
+// bucket counts into pass B's cursors (the bucket starts).
+constexpr uint32_t CP_DB = 64, CP_NG = 16;   // digits per block, span groups
+
+__global__ __launch_bounds__(1024) void k_cp_colsum(const uint32_t* __restrict__ spanc, uint32_t nspan, uint32_t ndA,
+                                                    uint64_t* __restrict__ gpre, uint64_t* __restrict__ totA) {
+  __shared__ uint64_t ps[CP_NG][CP_DB];
+  const uint32_t tid = threadIdx.x, dl = tid % CP_DB, g = tid / CP_DB, d = blockIdx.x * CP_DB + dl;
+  const uint32_t per = (nspan + CP_NG - 1) / CP_NG, w0 = g * per < nspan ? g * per : nspan;
+  const uint32_t w1 = w0 + per < nspan ? w0 + per : nspan;
+  uint64_t part = 0;
+  if (d < ndA) {
+#pragma unroll 8
+    for (uint32_t w = w0; w < w1; ++w) part += spanc[(uint64_t)w * CP_NAM + d];
+  }
+  ps[g][dl] = part;
+  __syncthreads();
+  if (g == 0 && d < ndA) {
+    uint64_t run = 0;
+    for (uint32_t q = 0; q < CP_NG; ++q) {
+      gpre[(uint64_t)q * CP_NAM + d] = run;
+      run += ps[q][dl];
+    }
+    totA[d] = run;
+  }
+}
+
 __global__ __launch_bounds__(1024) void k_cp_cursors(const uint64_t* __restrict__ hist, const uint32_t* __restrict__ spanc,
-                                                     uint32_t nspan, uint32_t nb, uint32_t ndA,
-                                                     unsigned long long* __restrict__ curA,
+                                                     const uint64_t* __restrict__ gpre, uint32_t nspan, uint32_t nb,
+                                                     uint32_t ndA, unsigned long long* __restrict__ curA,
                                                      unsigned long long* __restrict__ curB,
-                                                     uint64_t* __restrict__ totA, uint64_t* __restrict__ startA) {
+                                                     const uint64_t* __restrict__ totA, uint64_t* __restrict__ startA) {
   __shared__ uint64_t ws[16];
+  __shared__ uint64_t st[CP_NAM];
   const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  // pass B: exclusive scan of the bucket counts, `per` consecutive buckets per thread
-  if (curB) {
+  const uint32_t nblkA = (ndA + CP_DB - 1) / CP_DB;
+  if (blockIdx.x == nblkA) {
+    // pass B: exclusive scan of the bucket counts, `per` consecutive buckets per thread
     const uint32_t per = (nb + 1023) / 1024, b0 = tid * per;
     uint64_t sum = 0;
+#pragma unroll 8
     for (uint32_t b = b0; b < b0 + per && b < nb; ++b) sum += hist[b];
     const uint64_t inc = wave_incl_sum<uint64_t>(sum);
     if (lane == 63) ws[wv] = inc;
     __syncthreads();
     uint64_t run = inc - sum;
     for (uint32_t w = 0; w < wv; ++w) run += ws[w];
+#pragma unroll 8
     for (uint32_t b = b0; b < b0 + per && b < nb; ++b) {
       curB[b] = run;
       run += hist[b];
     }
-    __syncthreads();
+    return;
   }
-  // pass A: digit totals, their starts, then the per-span cursors; digit d = tid & 255, span
-  // quarter q = tid >> 8 (the quarters' partial sums meet in LDS)
-  __shared__ uint64_t qs[4][256], st[256];
-  const uint32_t d = tid & 255u, q = tid >> 8, qper = (nspan + 3) / 4, w0 = q * qper < nspan ? q * qper : nspan;
-  const uint32_t w1 = w0 + qper < nspan ? w0 + qper : nspan;
-  uint64_t part = 0;
-  if (d < ndA)
-    for (uint32_t w = w0; w < w1; ++w) part += spanc[(uint64_t)w * 256 + d];
-  qs[q][d] = part;
-  __syncthreads();
-  uint64_t tot = 0;
-  if (tid < 256) tot = qs[0][tid] + qs[1][tid] + qs[2][tid] + qs[3][tid];
+  // digit starts (every block; ndA <= CP_NAM, one value per thread of the first CP_NAM)
+  const uint64_t tot = tid < ndA ? totA[tid] : 0;
   const uint64_t inc = wave_incl_sum<uint64_t>(tot);
-  if (lane == 63 && wv < 4) ws[wv] = inc;
+  if (lane == 63 && wv < CP_NAM / 64) ws[wv] = inc;
   __syncthreads();
-  if (tid < 256) {
+  if (tid < CP_NAM) {
     uint64_t run = inc - tot;
     for (uint32_t w = 0; w < wv; ++w) run += ws[w];
     st[tid] = run;
-    if (tid < ndA) {
-      totA[tid] = tot;
+    if (blockIdx.x == 0 && tid < ndA) {
       startA[tid] = run;
       if (tid == ndA - 1) startA[ndA] = run + tot;
     }
   }
   __syncthreads();
-  if (d < ndA) {
-    uint64_t run = st[d];
-    for (uint32_t qq = 0; qq < q; ++qq) run += qs[qq][d];
-    for (uint32_t w = w0; w < w1; ++w) {
-      curA[(uint64_t)w * 256 + d] = run;
-      run += spanc[(uint64_t)w * 256 + d];
-    }
+  const uint32_t dl = tid % CP_DB, g = tid / CP_DB, d = blockIdx.x * CP_DB + dl;
+  if (d >= ndA) return;
+  const uint32_t per = (nspan + CP_NG - 1) / CP_NG, w0 = g * per < nspan ? g * per : nspan;
+  const uint32_t w1 = w0 + per < nspan ? w0 + per : nspan;
+  uint64_t run = st[d] + gpre[(uint64_t)g * CP_NAM + d];
+#pragma unroll 8
+  for (uint32_t w = w0; w < w1; ++w) {
+    curA[(uint64_t)w * CP_NAM + d] = run;
+    run += spanc[(uint64_t)w * CP_NAM + d];
   }
 }
 
@@ -383,7 +444,7 @@ constexpr int CP_T = 512;
 constexpr int CP_I = 16;
 constexpr int CP_TILE = CP_T * CP_I;   // 8192 suffixes per tile
 
-template <int NB, int T = CP_T>
+template <int NB, int T = CP_T, bool SD = false>
 struct CpShared {
   union {
     uint64_t keys[T * CP_I];
@@ -394,6 +455,7 @@ struct CpShared {
       uint8_t raw[T * CP_I + 64];
     } ft;
   } stage;
+  uint8_t sd[SD ? T * CP_I : 4];   // packed pass A: low 8 bits of each staged slot's digit
   uint64_t gb[NB];     // destination of the digit's run minus its tile start
   uint32_t cnt[NB];    // digit counts (ranks by LDS atomics)
   uint32_t tst[NB];    // tile-local exclusive digit starts
@@ -408,22 +470,30 @@ struct CpShared {
 // [blockIdx.x * CP_TILE, ...) and builds its keys (values = positions), cursor row = its span's;
 // else a tile of one region (from the XCD-group region table) and the row is the region's.
 // MODE 0: pass A over the text (builds the keys); 1: pass A over packed keys (a sharded slice's);
-// 2: pass B over one region per tile.  digit = ((key - kbias) >> shift) & 255.
-template <int MODE, int LB, int NB = 256, int T = CP_T>
+// 2: pass B over one region per tile.  digit = ((key - kbias) >> shift) & (NB - 1).
+// PK (packed records, single GPU): one u64 per suffix, (key bits below pass A's digit) << pbits |
+// position, instead of a key and a value plane.  Pass A (NB = 512) packs after ranking and stages
+// each slot's digit (low 8 bits in sd, the 9th from the slot's side of digit 256's start); pass B
+// (NB = 256, shift counts the position bits) moves the records unchanged.
+template <int MODE, int LB, int NB = 256, int T = CP_T, bool PK = false>
 __global__ __launch_bounds__(T, T == 1024 ? 1 : 2) void k_cpart(const uint64_t* __restrict__ kin, const uint32_t* __restrict__ vin,
                                                    uint64_t* __restrict__ kout, uint32_t* __restrict__ vout,
                                                    uint64_t n, int shift, uint64_t kbias,
                                                    unsigned long long* __restrict__ cur,
                                                    const uint32_t* __restrict__ gtab,
                                                    const uint64_t* __restrict__ startA, uint64_t span,
-                                                   TextKeySrc src) {
+                                                   TextKeySrc src, int pbits = 0,
+                                                   const unsigned long long* __restrict__ skip = nullptr) {
   constexpr int WSPAN = CP_I * 64;
   constexpr bool FT = MODE == 0;
+  constexpr bool SD = PK && MODE == 0;
   static_assert(NB == 256 || NB == 512, "digits per pass");
+  static_assert(!PK || MODE == 2 || (MODE == 0 && NB == 512), "packed records: pass A over 9-bit digits");
   constexpr uint32_t DM = NB - 1;
   constexpr int TILE = T * CP_I;
-  __shared__ CpShared<NB, T> sh;
+  __shared__ CpShared<NB, T, SD> sh;
   const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  if (MODE == 0 && skip && *skip) return;   // the pre-pass counts overflowed: recounted, then relaunched
   uint64_t tbase;
   uint32_t tn;
   unsigned long long* row;
@@ -436,12 +506,12 @@ __global__ __launch_bounds__(T, T == 1024 ? 1 : 2) void k_cpart(const uint64_t* 
     tbase = tile * TILE;
     if (tbase >= n) return;   // past the last span (whole workgroup, before any barrier)
     tn = (uint32_t)(n - tbase < (uint64_t)TILE ? n - tbase : TILE);
-    row = cur + (tbase / span) * 256;
+    row = cur + (tbase / span) * CP_NAM;
   } else {
     // region table: gtab[g] = first entry of XCD group g (gtab[8] = end), entries {region, first
     // tile}; workgroup b is tile b >> 3 of group b & 7 (see cursor_partition)
-    uint32_t* const T2 = reinterpret_cast<uint32_t*>(&sh.stage);   // the table (<= 9 + 512 words), one round trip
-    for (uint32_t i = tid; i < 9 + 2 * 256; i += T) T2[i] = gtab[i];
+    uint32_t* const T2 = reinterpret_cast<uint32_t*>(&sh.stage);   // the table (<= 9 + 2 * CP_NAM words)
+    for (uint32_t i = tid; i < 9 + 2 * CP_NAM; i += T) T2[i] = gtab[i];
     __syncthreads();
     if (tid == 0) {
       const uint32_t g = blockIdx.x & 7u, k = blockIdx.x >> 3;
@@ -489,8 +559,10 @@ __global__ __launch_bounds__(T, T == 1024 ? 1 : 2) void k_cpart(const uint64_t* 
   } else {
 #pragma unroll
     for (int k = 0; k < CP_I; ++k) key[k] = s0 + 64u * k < tn ? kin[tbase + s0 + 64u * k] : ~0ull;
+    if (!PK) {
 #pragma unroll
-    for (int k = 0; k < CP_I; ++k) val[k] = s0 + 64u * k < tn ? vin[tbase + s0 + 64u * k] : 0u;
+      for (int k = 0; k < CP_I; ++k) val[k] = s0 + 64u * k < tn ? vin[tbase + s0 + 64u * k] : 0u;
+    }
   }
   __syncthreads();   // counters zeroed; the text staging is read
   uint32_t rk[CP_I];
@@ -499,6 +571,11 @@ __global__ __launch_bounds__(T, T == 1024 ? 1 : 2) void k_cpart(const uint64_t* 
     const uint32_t d = (uint32_t)((key[k] - kbias) >> shift) & DM;
     const uint32_t r = s0 + 64u * k < tn ? atomicAdd(&sh.cnt[d], 1u) : 0u;
     rk[k] = r | (d << 16);
+  }
+  if (SD) {   // the record: key bits below the digit, then the position
+    const uint64_t klmask = (1ull << shift) - 1;
+#pragma unroll
+    for (int k = 0; k < CP_I; ++k) key[k] = ((key[k] & klmask) << pbits) | val[k];
   }
   __syncthreads();
   unsigned long long g = 0;
@@ -518,20 +595,26 @@ __global__ __launch_bounds__(T, T == 1024 ? 1 : 2) void k_cpart(const uint64_t* 
   __syncthreads();
 #pragma unroll
   for (int k = 0; k < CP_I; ++k)
-    if (s0 + 64u * k < tn) sh.stage.keys[sh.tst[rk[k] >> 16] + (rk[k] & 0xFFFFu)] = key[k];
+    if (s0 + 64u * k < tn) {
+      const uint32_t f = sh.tst[rk[k] >> 16] + (rk[k] & 0xFFFFu);
+      sh.stage.keys[f] = key[k];
+      if (SD) sh.sd[f] = (uint8_t)(rk[k] >> 16);
+    }
   if (tid < NB) sh.gb[tid] = g - sh.tst[tid];   // first use of the reservation
   __syncthreads();
   uint32_t dg[CP_I / 2] = {};   // digits of the staged slots, two per register
+  const uint32_t hi256 = SD ? sh.tst[256] : 0u;   // staged slots >= hi256 hold digits >= 256
 #pragma unroll
   for (int i = 0; i < CP_I; ++i) {
     const uint32_t s = (uint32_t)i * T + tid;
     if (s < tn) {
       const uint64_t kk = sh.stage.keys[s];
-      const uint32_t d = (uint32_t)((kk - kbias) >> shift) & DM;
-      dg[i >> 1] |= d << (16 * (i & 1));
+      const uint32_t d = SD ? (uint32_t)sh.sd[s] | (s >= hi256 ? 256u : 0u) : (uint32_t)((kk - kbias) >> shift) & DM;
+      if (!PK) dg[i >> 1] |= d << (16 * (i & 1));
       kout[sh.gb[d] + s] = kk;
     }
   }
+  if (PK) return;
   __syncthreads();
 #pragma unroll
   for (int k = 0; k < CP_I; ++k)
@@ -642,11 +725,13 @@ __device__ __forceinline__ void bs_load_keys(const uint64_t* __restrict__ keys, 
 template <int T> constexpr int bf_bits() { return T == 1024 ? 14 : 13; }
 constexpr uint32_t BF_MAXBIN = 32;
 
-template <typename V, bool TRACE, int T>
+// PK: xs holds the packed records (sym = record >> xsh, position = the low pbits bits) and the
+// positions come from them instead of a value plane.
+template <typename V, bool TRACE, int T, bool PK = false>
 __device__ __forceinline__ bool bucket_sort_fast(BsSharedT<T>& sh, uint2 it, const uint64_t (&xs)[BS_I],
                                                  const uint32_t (&pvr)[BS_H], uint32_t vmask, uint32_t s0,
-                                                 uint64_t xmin, int lo, int width, int pb,
-                                                 const uint32_t* __restrict__ vb,
+                                                 uint64_t xmin, int lo, int width, int pb, int xsh, int pbits,
+                                                 int term, const uint32_t* __restrict__ vb,
                                                  V* __restrict__ sab, uint8_t* __restrict__ bwb,
                                                  uint64_t* __restrict__ tie_k, V* __restrict__ tie_v,
                                                  unsigned long long* __restrict__ tie_n, uint64_t (&ts)[8]) {
@@ -668,12 +753,15 @@ __device__ __forceinline__ bool bucket_sort_fast(BsSharedT<T>& sh, uint2 it, con
   uint16_t* const blist = reinterpret_cast<uint16_t*>(&sh.whist[0][0]);
   uint16_t* const tlist = blist + BF_BIGCAP;
   uint32_t* const nctr = sh.wsum;   // [0] listed bins, [1] tied records
-  uint32_t lk[BS_I], r0[BS_H];
+  uint32_t lk[BS_I], r0[BS_H], vv[BS_I];
   // ---- 1. bin histogram; the atomic's return value is the suffix's rank inside its bin
 #pragma unroll
   for (int k = 0; k < BS_I; ++k) {
     const bool valid = (vmask >> k) & 1u;
-    lk[k] = (uint32_t)((xs[k] - xmin) >> lo) & wmask;
+    lk[k] = (uint32_t)(((PK ? xs[k] >> xsh : xs[k]) - xmin) >> lo) & wmask;
+    // packed: the position waits in the u32 plane by slot (free until the records' scatter), so no
+    // register holds it across the histogram and the scan
+    if (PK) sh.buf[s0 + 64u * k] = (uint32_t)xs[k] & (uint32_t)((1ull << pbits) - 1);
     uint32_t r = 0;
     if (valid) {
       const uint32_t bin = lk[k] >> kb, sh16 = 16u * (bin & 1u);
@@ -726,9 +814,14 @@ __device__ __forceinline__ bool bucket_sort_fast(BsSharedT<T>& sh, uint2 it, con
   __syncthreads();
   if (TRACE) ts[3] = stamp();
   // ---- 3. positions (coalesced; in flight during the bin work) and records to their bins
-  uint32_t vv[BS_I];
+  if (PK) {   // packed: from the u32 plane (phase 1), before the records overwrite it
 #pragma unroll
-  for (int k = 0; k < BS_I; ++k) vv[k] = ((vmask >> k) & 1u) ? vb[s0 + 64u * k] : 0u;
+    for (int k = 0; k < BS_I; ++k) vv[k] = sh.buf[s0 + 64u * k];
+    __syncthreads();
+  } else {
+#pragma unroll
+    for (int k = 0; k < BS_I; ++k) vv[k] = ((vmask >> k) & 1u) ? vb[s0 + 64u * k] : 0u;
+  }
 #pragma unroll
   for (int k = 0; k < BS_I; ++k) {
     if ((vmask >> k) & 1u) {
@@ -876,9 +969,9 @@ __device__ __forceinline__ bool bucket_sort_fast(BsSharedT<T>& sh, uint2 it, con
   for (int k = 0; k < BS_I; ++k) {
     const uint32_t r = s0 + 64u * k;
     if (r < cnt) {
-      const uint32_t pv = sh.aux[r];
-      sab[r] = (V)(((uint64_t)(pv >> pb) << 32) | sh.buf[r]);
-      bwb[r] = sh.inv[pv & pmask];
+      const uint32_t pv = sh.aux[r], pos = sh.buf[r];
+      sab[r] = (V)(((uint64_t)(pv >> pb) << 32) | pos);
+      bwb[r] = PK && pos == 0 && term >= 0 ? (uint8_t)term : sh.inv[pv & pmask];
     }
   }
   if (ntie) {
@@ -1248,7 +1341,7 @@ __global__ __launch_bounds__(BS_T, 1) void k_bucket_sort(const uint64_t* __restr
 
 // Fast-path kernel: the same prologue (the item's sym range and varying bits), then the MSD + bin-rank
 // sort; items it cannot take (wide keys, a bin over BF_MAXBIN) are appended to `fb` for k_bucket_sort.
-template <typename V, bool TRACE, int T>
+template <typename V, bool TRACE, int T, bool PK = false>
 __global__ __launch_bounds__(T, T == 1024 ? 1 : 4) void k_bucket_sort_fast(const uint64_t* __restrict__ keys,
                                                               const uint32_t* __restrict__ vals,
                                                               const uint2* __restrict__ items, int pb, int sb, int hb,
@@ -1257,12 +1350,17 @@ __global__ __launch_bounds__(T, T == 1024 ? 1 : 4) void k_bucket_sort_fast(const
                                                               uint64_t* __restrict__ tie_k, V* __restrict__ tie_v,
                                                               unsigned long long* __restrict__ tie_n,
                                                               uint2* __restrict__ fb, unsigned int* __restrict__ fb_n,
-                                                              uint64_t* __restrict__ trace) {
+                                                              uint64_t* __restrict__ trace, PkGeom pg) {
   __shared__ BsSharedT<T> sh;
   const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   uint64_t ts[8] = {0};
   if (TRACE) ts[0] = stamp();
-  if (tid < 256) sh.inv[tid] = inv[tid];
+  // packed records with keyed prev codes: code c is dense code c + (c >= tcode), position 0's is the terminal
+  const bool remap = PK && pg.tcode >= 0;
+  if (tid < 256) sh.inv[tid] = inv[remap && tid >= (uint32_t)pg.tcode ? tid + 1 : tid];   // inv holds 512 entries
+  const int term = remap ? (int)inv[pg.tcode] : -1;
+  const int pbits = PK ? pg.pbits : 0;
+  pb = PK ? pg.pb2 : pb;
   const uint2 it = items[blockIdx.x];
   uint64_t key[BS_I];
   bs_load_keys(keys, it, key);
@@ -1282,10 +1380,11 @@ __global__ __launch_bounds__(T, T == 1024 ? 1 : 4) void k_bucket_sort_fast(const
   uint64_t xmin = ~0ull, xmax = 0, vor = 0, vand = ~0ull;
 #pragma unroll
   for (int k = 0; k < BS_I; ++k) {
-    const uint32_t pv = ((uint32_t)(key[k] >> hb) & pmask) | (((uint32_t)key[k] & himask) << pb);
+    const uint64_t kl = PK ? key[k] >> pbits : key[k];   // packed: the record stays (positions)
+    const uint32_t pv = ((uint32_t)(kl >> hb) & pmask) | (((uint32_t)kl & himask) << pb);
     if (k < BS_H) pvr[k] = pv; else pvr[k - BS_H] |= pv << 16;
-    const uint64_t x = ((key[k] >> pbe) & symmask) - symbias;
-    key[k] = x;
+    const uint64_t x = ((kl >> pbe) & symmask) - symbias;
+    if (!PK) key[k] = x;
     if ((vmask >> k) & 1u) {
       xmin = x < xmin ? x : xmin;
       xmax = x > xmax ? x : xmax;
@@ -1323,7 +1422,8 @@ __global__ __launch_bounds__(T, T == 1024 ? 1 : 4) void k_bucket_sort_fast(const
   if (TRACE) ts[1] = stamp();
   // (every thread has read the reduction before the fast path reuses whist: its first barrier)
   const bool ok = width >= 1 && width <= 30 &&
-                  bucket_sort_fast<V, TRACE, T>(sh, it, key, pvr, vmask, s0, xmin, lo, width, pb, vals + it.x,
+                  bucket_sort_fast<V, TRACE, T, PK>(sh, it, key, pvr, vmask, s0, xmin, lo, width, pb, pbits + pbe,
+                                                    pbits, term, vals + it.x,
                                              sa + it.x, bwt + it.x, tie_k, tie_v, tie_n, ts);
   if (!ok && tid == 0) fb[atomicAdd(fb_n, 1u)] = it;
   if (TRACE) {
@@ -1334,13 +1434,15 @@ __global__ __launch_bounds__(T, T == 1024 ? 1 : 4) void k_bucket_sort_fast(const
 }
 
 // ------------------------------------------------------------ 5. big buckets
-// compacted copy of the big buckets: key top D bits replaced by the big-bucket ordinal, J = slot
+// compacted copy of the big buckets: key top D bits replaced by the big-bucket ordinal, J = slot;
+// pbits > 0: packed records (key bits << pbits | position, section 1b), no value plane
 __global__ __launch_bounds__(256) void k_big_gather(const uint64_t* __restrict__ keys,
                                                     const uint32_t* __restrict__ vals,
                                                     const uint64_t* __restrict__ bstart,
                                                     const uint64_t* __restrict__ cstart, uint32_t nbig,
                                                     uint64_t total, int lowbits, uint64_t* __restrict__ ok,
-                                                    uint32_t* __restrict__ ov, uint32_t* __restrict__ oj) {
+                                                    uint32_t* __restrict__ ov, uint32_t* __restrict__ oj,
+                                                    PkGeom pg) {
   for (uint64_t a = (uint64_t)blockIdx.x * 256 + threadIdx.x; a < total; a += (uint64_t)gridDim.x * 256) {
     uint32_t lo = 0, hi = nbig;   // last g with cstart[g] <= a
     while (hi - lo > 1) {
@@ -1348,10 +1450,37 @@ __global__ __launch_bounds__(256) void k_big_gather(const uint64_t* __restrict__
       if (cstart[mid] <= a) lo = mid; else hi = mid;
     }
     const uint64_t src = bstart[lo] + (a - cstart[lo]);
-    const uint64_t k = keys[src];
+    const uint64_t r = keys[src], k = pg.pbits ? pk_full_low(r, pg) : r;
     ok[a] = ((uint64_t)lo << lowbits) | (lowbits ? (k & ((1ull << lowbits) - 1)) : 0);
-    ov[a] = vals[src];
+    ov[a] = pg.pbits ? (uint32_t)(r & ((1ull << pg.pbits) - 1)) : vals[src];
     oj[a] = (uint32_t)src;
+  }
+}
+
+// packed records back to (key, position) planes for the paths that take full keys (the LSD item
+// sorts, the global path): items[i] = {start, count}; the region (pass A digit) of index j is the last
+// r with startA[r] <= j, and the key is region << klw | the record's key bits in the full layout
+__global__ __launch_bounds__(256) void k_unpack_items(const uint64_t* __restrict__ rec, const uint2* __restrict__ items,
+                                                      uint32_t nitems, const uint64_t* __restrict__ startA,
+                                                      uint32_t ndA, PkGeom pg, int klw, uint64_t* __restrict__ kout,
+                                                      uint32_t* __restrict__ vout) {
+  __shared__ uint64_t S[CP_NAM + 1];
+  for (uint32_t i = threadIdx.x; i <= ndA; i += 256) S[i] = startA[i];
+  __syncthreads();
+  const uint64_t pmask = (1ull << pg.pbits) - 1;
+  for (uint32_t i = blockIdx.x; i < nitems; i += gridDim.x) {
+    const uint2 it = items[i];
+    for (uint32_t a = threadIdx.x; a < it.y; a += 256) {
+      const uint64_t j = (uint64_t)it.x + a;
+      uint32_t lo = 0, hi = ndA;   // S[lo] <= j < S[hi]
+      while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (S[mid] <= j) lo = mid; else hi = mid;
+      }
+      const uint64_t r = rec[j];
+      kout[j] = ((uint64_t)lo << klw) | pk_full_low(r, pg);
+      vout[j] = (uint32_t)(r & pmask);
+    }
   }
 }
 
@@ -1429,7 +1558,8 @@ struct BucketPlan {
   uint64_t cap = BS_CAP;                     // suffixes per item: 18 432, or 9216 (512-thread fast sorts)
 };
 
-BucketPlan plan_buckets(const std::vector<uint64_t>& hist, int bsh, uint64_t cap) {
+// split_sh < 32: no item spans two values of bucket >> split_sh (packed records: pass A regions)
+BucketPlan plan_buckets(const std::vector<uint64_t>& hist, int bsh, uint64_t cap, int split_sh = 32) {
   BucketPlan pl;
   pl.cap = cap;
   const bool wide_geom = bsh > 32;
@@ -1452,7 +1582,8 @@ BucketPlan plan_buckets(const std::vector<uint64_t>& hist, int bsh, uint64_t cap
       pl.big_total += c;
     } else {
       const bool keep_narrow = !wide_geom && icnt && bsh + (32 - __builtin_clz(b ^ ib0)) > 32;
-      if (icnt && (icnt + c > cap || keep_narrow)) flush(prev_b);
+      const bool region = split_sh < 32 && (b >> split_sh) != (ib0 >> split_sh);
+      if (icnt && (icnt + c > cap || keep_narrow || region)) flush(prev_b);
       if (!icnt) {
         istart = off;
         ib0 = b;
@@ -1466,12 +1597,37 @@ BucketPlan plan_buckets(const std::vector<uint64_t>& hist, int bsh, uint64_t cap
   return pl;
 }
 
-// Launches the LDS sorts of the plan's work items over the bucket-grouped (keys, vals); writes
-// sa / bwt in sorted order and appends the tied suffixes to ix.ties_*; returns the tie count.
+// the cursor partition's packed records (section 1b): record = key bits below the pass A digit
+// (klw of them) << pbits | position; the items that need full keys are unpacked to (kfull, vfull)
+struct PackedRecs {
+  PkGeom g;                           // g.pbits > 0: packed
+  int klw = 0;                        // key bits below pass A's digit, full layout
+  uint16_t lutp2[256];                // byte -> prev code of the records (keyed code when g.tcode >= 0)
+  const uint64_t* startA = nullptr;   // region starts (ndA + 1)
+  uint32_t ndA = 0;
+  uint64_t* kfull = nullptr;
+  uint32_t* vfull = nullptr;
+};
+
+void unpack_items(Index& ix, const PackedRecs& pk, const uint64_t* rec, const uint2* d_items, uint32_t nitems) {
+  if (!nitems) return;
+  k_unpack_items<<<std::min<uint32_t>(nitems, 4096), 256, 0, ix.stream>>>(rec, d_items, nitems, pk.startA, pk.ndA,
+                                                                         pk.g, pk.klw, pk.kfull, pk.vfull);
+  HK_HIP(hipGetLastError());
+}
+
+// Launches the LDS sorts of the plan's work items over the bucket-grouped (keys, vals) or packed
+// records (pk); writes sa / bwt in sorted order and appends the tied suffixes to ix.ties_*; returns
+// the tie count.
 template <typename V>
 uint64_t sort_bucket_items(Index& ix, const BucketPlan& plan, const uint64_t* keys, const uint32_t* vals, uint64_t m,
-                           int pb, int sb, int hb, uint64_t symbias, V* sa, uint8_t* bwt) {
+                           int pb, int sb, int hb, uint64_t symbias, V* sa, uint8_t* bwt,
+                           const PackedRecs* pk = nullptr) {
   hipStream_t s = ix.stream;
+  if (pk && (hb || symbias || sizeof(V) != 4)) throw ApiError{-1, "packed records: single-GPU keys only"};
+  // the LSD item sorts read full keys: packed items are unpacked to (kfull, vfull) first
+  const uint64_t* lkeys = pk ? pk->kfull : keys;
+  const uint32_t* lvals = pk ? pk->vfull : vals;
   const uint8_t* d_inv = ix.small.as<uint8_t>() + 3072;
   ix.ties_k.ensure(m * 8 + 16);
   ix.ties_v.ensure(m * sizeof(V) + 16);
@@ -1484,7 +1640,7 @@ uint64_t sort_bucket_items(Index& ix, const BucketPlan& plan, const uint64_t* ke
     HK_HIP(hipMemcpyAsync(ix.bk_items.as<uint2>() + nn, plan.items_w.data(), nw * sizeof(uint2),
                           hipMemcpyHostToDevice, s));
   {
-    TimedLaunch t(ix.timer, "sa_bucket_sort", (double)(m - plan.big_total) * (8 + 4 + 4 + 1));
+    TimedLaunch t(ix.timer, "sa_bucket_sort", (double)(m - plan.big_total) * (pk ? 8 + 4 + 1 : 8 + 4 + 4 + 1));
     static const bool trace = getenv("HKCSA_BS_TRACE") != nullptr;   // diagnostic phase stamps
     // HKCSA_BS_FAST=0: the three stable LSD passes everywhere (A/B diagnostic)
     static const int fast = getenv("HKCSA_BS_FAST") ? atoi(getenv("HKCSA_BS_FAST")) : 1;
@@ -1499,10 +1655,19 @@ uint64_t sort_bucket_items(Index& ix, const BucketPlan& plan, const uint64_t* ke
       auto launch = [&](auto ttag, auto trtag) {
         constexpr int T = decltype(ttag)::value;
         constexpr bool TR = decltype(trtag)::value;
+        if constexpr (std::is_same<V, uint32_t>::value) {
+          if (pk) {
+            k_bucket_sort_fast<V, TR, T, true><<<grid_n, T, 0, s>>>(
+                keys, pk->vfull, ix.bk_items.as<uint2>(), pb, sb, hb, symbias, d_inv, sa, bwt,
+                ix.ties_k.as<uint64_t>(), ix.ties_v.as<V>(), ix.ties_n.as<unsigned long long>(), ix.bk_fb.as<uint2>(),
+                fbn, TR ? tbuf.as<uint64_t>() : nullptr, pk->g);
+            return;
+          }
+        }
         k_bucket_sort_fast<V, TR, T><<<grid_n, T, 0, s>>>(
             keys, vals, ix.bk_items.as<uint2>(), pb, sb, hb, symbias, d_inv, sa, bwt, ix.ties_k.as<uint64_t>(),
             ix.ties_v.as<V>(), ix.ties_n.as<unsigned long long>(), ix.bk_fb.as<uint2>(), fbn,
-            TR ? tbuf.as<uint64_t>() : nullptr);
+            TR ? tbuf.as<uint64_t>() : nullptr, PkGeom{});
       };
       using T512 = std::integral_constant<int, 512>;
       using T1024 = std::integral_constant<int, 1024>;
@@ -1529,24 +1694,29 @@ uint64_t sort_bucket_items(Index& ix, const BucketPlan& plan, const uint64_t* ke
       HK_HIP(hipMemcpyAsync(&nfb, fbn, 4, hipMemcpyDeviceToHost, s));
       HK_HIP(hipStreamSynchronize(s));
       ix.info[8] += nfb;   // items sorted by the LSD passes (a bin over BF_MAXBIN, or wide local keys)
-      if (nfb)
+      if (nfb) {
+        if (pk) unpack_items(ix, *pk, keys, ix.bk_fb.as<uint2>(), nfb);
         k_bucket_sort<false, false, V><<<nfb, BS_T, 0, s>>>(
-            keys, vals, ix.bk_fb.as<uint2>(), pb, sb, hb, symbias, d_inv, sa, bwt, ix.ties_k.as<uint64_t>(),
+            lkeys, lvals, ix.bk_fb.as<uint2>(), pb, sb, hb, symbias, d_inv, sa, bwt, ix.ties_k.as<uint64_t>(),
             ix.ties_v.as<V>(), ix.ties_n.as<unsigned long long>(), nullptr);
+      }
     } else if (nn) {
+      if (pk) unpack_items(ix, *pk, keys, ix.bk_items.as<uint2>(), (uint32_t)nn);
       if (trace && sizeof(V) == 4)
         k_bucket_sort<false, true, V><<<grid_n, BS_T, 0, s>>>(
-            keys, vals, ix.bk_items.as<uint2>(), pb, sb, hb, symbias, d_inv, sa, bwt, ix.ties_k.as<uint64_t>(),
+            lkeys, lvals, ix.bk_items.as<uint2>(), pb, sb, hb, symbias, d_inv, sa, bwt, ix.ties_k.as<uint64_t>(),
             ix.ties_v.as<V>(), ix.ties_n.as<unsigned long long>(), tbuf.as<uint64_t>());
       else
         k_bucket_sort<false, false, V><<<grid_n, BS_T, 0, s>>>(
-            keys, vals, ix.bk_items.as<uint2>(), pb, sb, hb, symbias, d_inv, sa, bwt, ix.ties_k.as<uint64_t>(),
+            lkeys, lvals, ix.bk_items.as<uint2>(), pb, sb, hb, symbias, d_inv, sa, bwt, ix.ties_k.as<uint64_t>(),
             ix.ties_v.as<V>(), ix.ties_n.as<unsigned long long>(), nullptr);
     }
-    if (nw)
+    if (nw) {
+      if (pk) unpack_items(ix, *pk, keys, ix.bk_items.as<uint2>() + nn, (uint32_t)nw);
       k_bucket_sort<true, false, V><<<grid_w, BS_T, 0, s>>>(
-          keys, vals, ix.bk_items.as<uint2>() + nn, pb, sb, hb, symbias, d_inv, sa, bwt, ix.ties_k.as<uint64_t>(),
+          lkeys, lvals, ix.bk_items.as<uint2>() + nn, pb, sb, hb, symbias, d_inv, sa, bwt, ix.ties_k.as<uint64_t>(),
           ix.ties_v.as<V>(), ix.ties_n.as<unsigned long long>(), nullptr);
+    }
     HK_HIP(hipGetLastError());
     if (trace && nn && !fast && sizeof(V) == 4) {
       std::vector<uint64_t> h(nn * 8);
@@ -1621,6 +1791,7 @@ KeyGeom key_geometry_keyed(Index& ix, int reserve) {
     codek[b] = Rk++;
   }
   if (!unkeyed) m_term = 0;
+  g.tcode = unkeyed ? (int)g.lutp[term] : -1;
   g.Rk = (uint64_t)std::max(Rk, 2);
   for (int b = 0; b < 256; ++b) g.lutk[b] = (uint16_t)(codek[b] | (b << 8));
   {
@@ -1686,6 +1857,7 @@ KeyGeom key_geometry_keyed(Index& ix, int reserve) {
     }
   }
   if (g.q == 0) throw ApiError{-6, "keyed geometry: no symbol count fits a 64-bit key"};
+  if (ix.flags & kFlagMaxBuckets) g.bucket_bits = std::min(16, g.sym_bits);   // the 1 GiB pipeline at any n
   shorts(g.q, g.skey, g.s_start, nullptr);
   g.nS = (uint32_t)(n - g.s_start);
   // exact order of the short suffixes (bytes compare like Python str over latin-1 code points)
@@ -1771,7 +1943,7 @@ SliceBins slice_bins(uint64_t m, const KeyGeom& kg, int hb, uint64_t kmin, uint6
 }
 
 int cursor_partition(Index& ix, uint64_t n, int D, int bitlo, uint64_t kbias, const TextKeySrc* tks, uint64_t* kp[2],
-                     uint32_t* vp[2], std::vector<uint64_t>& hist);
+                     uint32_t* vp[2], std::vector<uint64_t>& hist, PackedRecs* pk = nullptr);
 
 // the cursor partition groups buckets wherever D <= 16 (HKCSA_CURSOR=0: the stable onesweep passes)
 static bool cursor_enabled() {
@@ -1859,21 +2031,32 @@ template bool bucket_sort_slice<uint64_t>(Index&, const KeyGeom&, uint64_t, int,
 // meanwhile), then pass B (D > 8).  bucket = ((key - kbias) >> bitlo) & (2^D - 1).  With `tks` the
 // keys are built from the text (single GPU); without, they are the packed keys in kp[0] / vp[0]
 // (a sharded slice).  Leaves the bucket counts in `hist`; returns the slot holding the grouped pairs.
+// pk (pk->pbits > 0, text keys, D = 17): packed records, pass A over the top 9 bucket bits with
+// 1024-thread tiles, pass B over the low 8 (k_cpart PK); the records land in kp[0] and pk gets the
+// region starts for unpacking.
 int cursor_partition(Index& ix, uint64_t n, int D, int bitlo, uint64_t kbias, const TextKeySrc* tks, uint64_t* kp[2],
-                     uint32_t* vp[2], std::vector<uint64_t>& hist) {
+                     uint32_t* vp[2], std::vector<uint64_t>& hist, PackedRecs* pk) {
   hipStream_t s = ix.stream;
   if (D > 17 || (!tks && D > 16)) throw ApiError{-1, "cursor partition: too many bucket bits"};
-  // pass A digit = bucket >> sA (its top 8 bits, all of it for D <= 8); pass B digit = the low sA bits
-  const int sA = D > 16 ? D - 8 : (D > 8 ? 8 : 0);
+  const bool packed = pk && pk->g.pbits > 0;
+  // packed: pass A builds the keys with the records' prev field (pb2 bits), so below the bucket
+  // there are bitlo2 = bitlo - pb + pb2 bits
+  const int bitlo2 = packed ? bitlo - pk->g.pb + pk->g.pb2 : bitlo;
+  if (packed && (!tks || D != 17 || kbias || bitlo2 + 8 + pk->g.pbits > 64 || tks->g.pb != pk->g.pb))
+    throw ApiError{-1, "cursor partition: packed records need 17 text bucket bits"};
+  // pass A digit = bucket >> sA (its top 8 bits, all of it for D <= 8; 9 bits for packed records);
+  // pass B digit = the low sA bits
+  const int sA = packed ? D - 9 : (D > 16 ? D - 8 : (D > 8 ? 8 : 0));
   const uint32_t nb = 1u << D, ndA = 1u << (D - sA);
   const uint64_t span = ceil_div(ceil_div(n, (uint64_t)BH_TILE), 256) * BH_TILE;   // one workgroup per CU
   const uint32_t nspan = (uint32_t)ceil_div(n, span);
   const uint32_t stride = nb;
-  ix.cp_part.ensure((uint64_t)nspan * stride * 4 + (uint64_t)nspan * 256 * 4 + 16);
+  ix.cp_part.ensure((uint64_t)nspan * stride * 4 + (uint64_t)nspan * CP_NAM * 4 + 16);
   ix.bk_hist.ensure((uint64_t)nb * 16 + 16);
-  ix.cp_cur.ensure(((uint64_t)nspan * 256 + nb + 2 * 257 + 16) * 8);
-  ix.cp_tiles.ensure((9 + 2 * 256 + 16) * 4);
-  ix.cp_host.ensure((uint64_t)nb * 8 + 2 * 257 * 8 + (9 + 2 * 256) * 4 + 64);
+  ix.cp_cur.ensure(((uint64_t)nspan * CP_NAM + nb + 2 * (CP_NAM + 1) + 16 + (uint64_t)CP_NG * CP_NAM) * 8);
+  constexpr uint64_t kLp2Off = (9 + 2 * CP_NAM + 16) * 4;   // packed: the records' prev-code table
+  ix.cp_tiles.ensure(kLp2Off + 512);
+  ix.cp_host.ensure((uint64_t)nb * 8 + 2 * (CP_NAM + 1) * 8 + (9 + 2 * CP_NAM) * 4 + 64);
   uint32_t* d_part = ix.cp_part.as<uint32_t>();
   uint32_t* d_spanc = d_part + (uint64_t)nspan * stride;
   unsigned long long* d_drain = ix.bk_hist.as<unsigned long long>();
@@ -1882,56 +2065,106 @@ int cursor_partition(Index& ix, uint64_t n, int D, int bitlo, uint64_t kbias, co
   if (addr_dbg)
     fprintf(stderr, "[cp addr] k0 %p k1 %p v0 %p v1 %p\n", (void*)kp[0], (void*)kp[1], (void*)vp[0], (void*)vp[1]);
   unsigned long long* d_curA = ix.cp_cur.as<unsigned long long>();
-  unsigned long long* d_curB = d_curA + (uint64_t)nspan * 256;
+  unsigned long long* d_curB = d_curA + (uint64_t)nspan * CP_NAM;
   uint64_t* d_totA = reinterpret_cast<uint64_t*>(d_curB + nb);
-  uint64_t* d_startA = d_totA + 257;
+  uint64_t* d_startA = d_totA + (CP_NAM + 1);
   uint32_t* d_gtab = ix.cp_tiles.as<uint32_t>();
   uint64_t* h_hist = ix.cp_host.as<uint64_t>();
-  uint64_t* h_totA = h_hist + nb;   // totA[257] then startA[257]
-  uint32_t* h_gtab = reinterpret_cast<uint32_t*>(h_totA + 2 * 257);
-  HK_HIP(hipMemsetAsync(d_drain, 0, (uint64_t)nb * 8, s));
-  {
-    TimedLaunch t(ix.timer, "sa_bucket_hist", (double)n * (tks ? 1 : 8));
-    if (tks && D > 16)   // 2^17 buckets: u8 counters (drained at 128)
+  uint64_t* h_totA = h_hist + nb;   // totA[CP_NAM + 1] then startA[CP_NAM + 1]
+  uint32_t* h_gtab = reinterpret_cast<uint32_t*>(h_totA + 2 * (CP_NAM + 1) + 1);   // after the overflow flag
+  unsigned long long* d_ovf = reinterpret_cast<unsigned long long*>(d_totA + 2 * (CP_NAM + 1));
+  uint64_t* d_gpre = d_totA + 2 * (CP_NAM + 1) + 16;   // [CP_NG][CP_NAM] span-group prefixes
+  const uint64_t* h_ovf = h_totA + 2 * (CP_NAM + 1);
+  TextKeySrc tks2{};
+  if (packed) {
+    pk->startA = d_startA;
+    pk->ndA = ndA;
+    pk->klw = bitlo + sA;
+    uint16_t* d_lp2 = reinterpret_cast<uint16_t*>(ix.cp_tiles.as<uint8_t>() + kLp2Off);
+    HK_HIP(hipMemcpyAsync(d_lp2, pk->lutp2, 512, hipMemcpyHostToDevice, s));   // pk outlives the stream's use
+    tks2 = *tks;
+    tks2.lutp = d_lp2;
+    tks2.g.pb = pk->g.pb2;
+  }
+  // pre-pass (exact: 2^17 buckets as two u16 runs over the bucket halves, after a u8 overflow)
+  auto prepass = [&](bool exact) {
+    HK_HIP(hipMemsetAsync(d_drain, 0, (uint64_t)nb * 8, s));
+    HK_HIP(hipMemsetAsync(d_ovf, 0, 8, s));
+    TimedLaunch t(ix.timer, "sa_bucket_hist", (double)n * (tks ? (exact ? 2 : 1) : 8));
+    if (tks && D > 16 && !exact) {   // 2^17 buckets: u8 counters (drained at 128)
       k_bucket_hist_spans<8><<<nspan, BH_T, 0, s>>>(tks->text, n, tks->lutk, tks->skey, tks->g, bitlo - tks->g.pb, D,
-                                                    sA, d_part, d_drain, d_spanc, span);
-    else if (tks)
-      k_bucket_hist_spans<16><<<nspan, BH_T, 0, s>>>(tks->text, n, tks->lutk, tks->skey, tks->g, bitlo - tks->g.pb, D,
-                                                     sA, d_part, d_drain, d_spanc, span);
-    else
+                                                    sA, d_part, d_drain, d_spanc, span, d_ovf);
+    } else if (tks) {
+      if (D > 16) {
+        k_bucket_hist_spans<16, 0><<<nspan, BH_T, 0, s>>>(tks->text, n, tks->lutk, tks->skey, tks->g,
+                                                          bitlo - tks->g.pb, D, sA, d_part, d_drain, d_spanc, span,
+                                                          d_ovf);
+        k_bucket_hist_spans<16, 1><<<nspan, BH_T, 0, s>>>(tks->text, n, tks->lutk, tks->skey, tks->g,
+                                                          bitlo - tks->g.pb, D, sA, d_part, d_drain, d_spanc, span,
+                                                          d_ovf);
+      } else {
+        k_bucket_hist_spans<16><<<nspan, BH_T, 0, s>>>(tks->text, n, tks->lutk, tks->skey, tks->g, bitlo - tks->g.pb,
+                                                       D, sA, d_part, d_drain, d_spanc, span, d_ovf);
+      }
+    } else {
       k_key_hist_spans<<<nspan, BH_T, 0, s>>>(kp[0], n, bitlo, kbias, D, sA, d_part, d_drain, d_spanc, span);
+    }
     HK_HIP(hipGetLastError());
     k_bucket_reduce<<<(nb + 255) / 256, 256, 0, s>>>(d_part, d_drain, nspan, stride, nb, d_hist);
     HK_HIP(hipGetLastError());
-    k_cp_cursors<<<1, 1024, 0, s>>>(d_hist, d_spanc, nspan, nb, ndA, d_curA, D > 8 ? d_curB : nullptr, d_totA,
-                                    d_startA);
+    const uint32_t nblkA = (ndA + CP_DB - 1) / CP_DB;
+    k_cp_colsum<<<nblkA, 1024, 0, s>>>(d_spanc, nspan, ndA, d_gpre, d_totA);
     HK_HIP(hipGetLastError());
-  }
-  HK_HIP(hipMemcpyAsync(h_hist, d_hist, (uint64_t)nb * 8, hipMemcpyDeviceToHost, s));
-  HK_HIP(hipMemcpyAsync(h_totA, d_totA, 2 * 257 * 8, hipMemcpyDeviceToHost, s));
-  hipEvent_t ev;
-  HK_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-  HK_HIP(hipEventRecord(ev, s));
-  // pass A: text -> slot D > 8 ? 1 : 0; packed keys: slot 0 -> 1
+    k_cp_cursors<<<nblkA + (D > 8 ? 1 : 0), 1024, 0, s>>>(d_hist, d_spanc, d_gpre, nspan, nb, ndA, d_curA,
+                                                          D > 8 ? d_curB : nullptr, d_totA, d_startA);
+    HK_HIP(hipGetLastError());
+  };
+  // pass A: text -> slot D > 8 ? 1 : 0; packed keys: slot 0 -> 1.  A text pass skips itself when the
+  // pre-pass flagged an overflow
   const int outA = tks ? (D > 8 ? 1 : 0) : 1;
-  {
-    TimedLaunch t(ix.timer, tks ? "radix_part_text" : "radix_part_keys", (double)n * (tks ? 1 + 8 + 4 : 2 * (8 + 4)));
+  auto passA = [&]() {
+    TimedLaunch t(ix.timer, tks ? "radix_part_text" : "radix_part_keys",
+                  (double)n * (packed ? 1 + 8 : tks ? 1 + 8 + 4 : 2 * (8 + 4)));
     const unsigned grid = (unsigned)(8 * ceil_div(nspan, 8u) * (span / CP_TILE));
-    if (!tks)
+    const unsigned grid_pk = (unsigned)(8 * ceil_div(nspan, 8u) * (span / (1024 * CP_I)));
+    if (packed && tks->g.lb == 2)
+      k_cpart<0, 2, 512, 1024, true><<<grid_pk, 1024, 0, s>>>(nullptr, nullptr, kp[outA], nullptr, n, bitlo2 + sA, 0,
+                                                             d_curA, nullptr, nullptr, span, tks2, pk->g.pbits, d_ovf);
+    else if (packed)
+      k_cpart<0, 0, 512, 1024, true><<<grid_pk, 1024, 0, s>>>(nullptr, nullptr, kp[outA], nullptr, n, bitlo2 + sA, 0,
+                                                             d_curA, nullptr, nullptr, span, tks2, pk->g.pbits, d_ovf);
+    else if (!tks)
       k_cpart<1, 0><<<grid, CP_T, 0, s>>>(kp[0], vp[0], kp[1], vp[1], n, bitlo + sA, kbias, d_curA, nullptr, nullptr,
                                           span, TextKeySrc{});
     else if (tks->g.lb == 2)
       k_cpart<0, 2><<<grid, CP_T, 0, s>>>(nullptr, nullptr, kp[outA], vp[outA], n, bitlo + sA, 0, d_curA, nullptr,
-                                          nullptr, span, *tks);
+                                          nullptr, span, *tks, 0, d_ovf);
     else
       k_cpart<0, 0><<<grid, CP_T, 0, s>>>(nullptr, nullptr, kp[outA], vp[outA], n, bitlo + sA, 0, d_curA, nullptr,
-                                          nullptr, span, *tks);
+                                          nullptr, span, *tks, 0, d_ovf);
     HK_HIP(hipGetLastError());
+    ix.info[0] += 1;
+  };
+  // the counts come back behind an event while pass A runs
+  auto counts_then_passA = [&]() {
+    HK_HIP(hipMemcpyAsync(h_hist, d_hist, (uint64_t)nb * 8, hipMemcpyDeviceToHost, s));
+    HK_HIP(hipMemcpyAsync(h_totA, d_totA, (2 * (CP_NAM + 1) + 1) * 8, hipMemcpyDeviceToHost, s));
+    hipEvent_t ev;
+    HK_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    HK_HIP(hipEventRecord(ev, s));
+    passA();
+    const hipError_t we = hipEventSynchronize(ev);   // the counts, not pass A
+    (void)hipEventDestroy(ev);
+    HK_HIP(we);
+  };
+  prepass(false);
+  counts_then_passA();
+  if (*h_ovf) {   // u8 counters overflowed (long runs of one bucket): exact recount, pass A again
+    ix.info[0] -= 1;
+    prepass(true);
+    counts_then_passA();
+    if (*h_ovf) throw ApiError{-7, "cursor partition: exact recount flagged an overflow"};
   }
-  ix.info[0] += 1;
-  const hipError_t we = hipEventSynchronize(ev);   // the counts, not pass A
-  (void)hipEventDestroy(ev);
-  HK_HIP(we);
   hist.assign(h_hist, h_hist + nb);
   const uint64_t* totA = h_totA;
   uint64_t tsum = 0, hsum = 0;
@@ -1972,8 +2205,12 @@ int cursor_partition(Index& ix, uint64_t n, int D, int bitlo, uint64_t kbias, co
     }
     h_gtab[8] = e;
     HK_HIP(hipMemcpyAsync(d_gtab, h_gtab, (9 + 2 * e) * 4, hipMemcpyHostToDevice, s));
-    TimedLaunch t(ix.timer, "radix_part", (double)n * 2 * (8 + 4));
-    if (sA > 8 && btile > CP_TILE)
+    TimedLaunch t(ix.timer, "radix_part", (double)n * 2 * (packed ? 8 : 8 + 4));
+    if (packed)
+      k_cpart<2, 0, 256, CP_T, true><<<(unsigned)(8 * maxl), CP_T, 0, s>>>(kp[1], nullptr, kp[0], nullptr, n,
+                                                                          bitlo2 + pk->g.pbits, 0, d_curB, d_gtab,
+                                                                          d_startA, 0, TextKeySrc{}, pk->g.pbits);
+    else if (sA > 8 && btile > CP_TILE)
       k_cpart<2, 0, 512, 1024><<<(unsigned)(8 * maxl), 1024, 0, s>>>(kp[1], vp[1], kp[0], vp[0], n, bitlo, kbias,
                                                                       d_curB, d_gtab, d_startA, 0, TextKeySrc{});
     else if (sA > 8)
@@ -2091,9 +2328,36 @@ void build_sa_bucketed(Index& ix) {
   const TextKeySrc tks{ix.text.as<uint8_t>(), n, d_lutk, d_lutp, d_skey, ka};
   int slot = 0;
   bool sorted_by_bucket = false;
+  // packed records (section 1b): one u64 per suffix through both passes and the item sorts when the
+  // key bits below pass A's 9-bit digit and the position bits fit 64 (1 GiB DNA: 33 + 31);
+  // HKCSA_PACKED=0 keeps the key and position planes (A/B)
+  static const bool pk_env = !getenv("HKCSA_PACKED") || atoi(getenv("HKCSA_PACKED")) != 0;
+  PackedRecs pkr;
+  {
+    const int posb = 64 - __builtin_clzll(n - 1);
+    // prev field of the records: the keyed code when the terminal is unkeyed (bits(Rk - 1))
+    int pb2 = pb;
+    if (kg.tcode >= 0) {
+      pb2 = 1;
+      while ((1ull << pb2) < kg.Rk) ++pb2;
+      pb2 = std::min(pb2, pb);
+    }
+    if (pk_env && use_cp && D == 17 && pb2 + bsh + 8 + posb <= 64) {
+      pkr.g.pbits = posb;
+      pkr.g.pb = pb;
+      pkr.g.pb2 = pb2;
+      pkr.g.tcode = pb2 < pb ? kg.tcode : -1;
+      for (int b = 0; b < 256; ++b)
+        pkr.lutp2[b] = pkr.g.tcode < 0 ? kg.lutp[b] : (kg.kflag[b] ? kg.kdig[b] : 0);
+      pkr.kfull = kp[1];
+      pkr.vfull = vp[1];
+    }
+  }
+  const bool packed = pkr.g.pbits > 0;
   if (use_cp) {
-    slot = cursor_partition(ix, n, D, pb + bsh, 0, &tks, kp, vp, hist);
+    slot = cursor_partition(ix, n, D, pb + bsh, 0, &tks, kp, vp, hist, packed ? &pkr : nullptr);
     sorted_by_bucket = true;
+    if (packed) ix.info[7] |= 2;
   } else if (late_hist) {
     // ---- LSD passes over the bucket bits (the first builds the keys from the text), then the
     // bucket counts from the sorted keys
@@ -2115,7 +2379,8 @@ void build_sa_bucketed(Index& ix) {
   }
 
   // ---- 2. work items (whole buckets, packed while they fit) and big buckets
-  const BucketPlan plan = plan_buckets(hist, bsh, item_T == 512 ? (uint64_t)512 * BS_I : (uint64_t)BS_CAP);
+  const BucketPlan plan = plan_buckets(hist, bsh, item_T == 512 ? (uint64_t)512 * BS_I : (uint64_t)BS_CAP,
+                                       packed ? 8 : 32);
   const std::vector<uint2>& items_n = plan.items_n;
   const std::vector<uint2>& items_w = plan.items_w;
   const std::vector<uint64_t>& big_start = plan.big_start;
@@ -2135,7 +2400,15 @@ void build_sa_bucketed(Index& ix) {
   if (big_total > n / 2) {
     // skewed text: the global path (full LSD radix sort + refinement from the keys)
     int gs;
-    if (sorted_by_bucket) {
+    if (packed) {   // full keys into slot 1 first
+      std::vector<uint2> ch;
+      for (uint64_t a = 0; a < n; a += 65536) ch.push_back(make_uint2((uint32_t)a, (uint32_t)std::min<uint64_t>(65536, n - a)));
+      ix.bk_items.ensure(ch.size() * sizeof(uint2) + 16);
+      HK_HIP(hipMemcpyAsync(ix.bk_items.p, ch.data(), ch.size() * sizeof(uint2), hipMemcpyHostToDevice, s));
+      unpack_items(ix, pkr, kp[slot], ix.bk_items.as<uint2>(), (uint32_t)ch.size());
+      HK_HIP(hipStreamSynchronize(s));   // ch is freed at the end of this block
+      gs = radix_sort_pairs<uint32_t>(ix.sw, ix.timer, kp, vp, 1, n, pb, pb + sb, false, s);
+    } else if (sorted_by_bucket) {
       gs = radix_sort_pairs<uint32_t>(ix.sw, ix.timer, kp, vp, slot, n, pb, pb + sb, false, s);
     } else {
       pack();
@@ -2146,7 +2419,7 @@ void build_sa_bucketed(Index& ix) {
     ix.info[1] += ix.sw.passes_skipped;
     std::swap(ix.sa, ix.vals[slot]);
     ix.vals[slot].ensure(n * 4 + 16);
-    ix.info[7] = 1;
+    ix.info[7] |= 1;
     refine_after_sort<uint32_t>(ix, kg, slot, n, true);
     HK_HIP(hipStreamSynchronize(s));
     ix.have_sa = ix.have_bwt = true;
@@ -2174,7 +2447,7 @@ void build_sa_bucketed(Index& ix) {
 
   // ---- 4. LDS sorts of the buckets
   uint64_t ntie = sort_bucket_items<uint32_t>(ix, plan, kp[slot], vp[slot], n, pb, sb, 0, 0, ix.sa.as<uint32_t>(),
-                                              ix.bwt.as<uint8_t>());
+                                              ix.bwt.as<uint8_t>(), packed ? &pkr : nullptr);
 
   // ---- 5. big buckets on the global path
   if (big_total) {
@@ -2196,7 +2469,7 @@ void build_sa_bucketed(Index& ix) {
       k_big_gather<<<grid_of(big_total), 256, 0, s>>>(kp[slot], vp[slot], ix.tile_a.as<uint64_t>(),
                                                      ix.tile_c.as<uint64_t>(), nbig, big_total, lowbits,
                                                      ix.big_k[0].as<uint64_t>(), ix.big_v[0].as<uint32_t>(),
-                                                     ix.big_j.as<uint32_t>());
+                                                     ix.big_j.as<uint32_t>(), pkr.g);
       HK_HIP(hipGetLastError());
     }
     uint64_t* bk[2] = {ix.big_k[0].as<uint64_t>(), ix.big_k[1].as<uint64_t>()};

@@ -13,6 +13,7 @@ constexpr uint32_t kFlagPos64 = 1u;   // hkcsa_opts.flags: 64-bit positions in s
 constexpr uint32_t kFlagNoSplit = 2u; // ... and sort them as whole u64 values (no split low/high halves)
 constexpr uint32_t kFlagGlobalSort = 4u; // full LSD sort of the keys (no bucket sorts)
 constexpr uint32_t kFlagMulBins = 8u;    // sharded slices: force multiplicative bucket bins
+constexpr uint32_t kFlagMaxBuckets = 16u; // single GPU: the most bucket bits at any n (diagnostic)
 constexpr int kLineBits = 448;   // 7 data words per 64-B rank line (word 0 = ones before the line)
 
 struct WtTables {                // per level, per dense code (host mirror of the device tables)
@@ -47,6 +48,7 @@ struct KeyGeom {
   uint16_t kdig[256];        // byte -> number of keyed bytes below it (its keyed code when keyed)
   uint8_t kflag[256];        // byte -> 1 when keyed
   uint16_t k2d[256];         // keyed code -> dense code (the prev field of a keyed byte)
+  int tcode = -1;            // dense code of the unkeyed terminal (-1: none); it precedes only suffix 0
 };
 int mixed_radix_bits(uint64_t R, int q);   // bits of R^q - 1 (65 when it does not fit 64 bits)
 

@@ -78,6 +78,7 @@ class QuerySet:
 FLAG_POS64 = 1   # HKCSA_FLAG_POS64: 64-bit positions in sharded builds at any n
 FLAG_GLOBAL_SORT = 4   # HKCSA_FLAG_GLOBAL_SORT: build by full-width LSD sort (no bucket sorts)
 FLAG_MUL_BINS = 8      # HKCSA_FLAG_MUL_BINS: sharded slices use multiplicative bucket bins (diagnostic)
+FLAG_MAX_BUCKETS = 16  # HKCSA_FLAG_MAX_BUCKETS: single GPU, the most bucket bits at any n (diagnostic)
 
 
 class DeviceIndex:

@@ -51,6 +51,8 @@ typedef struct hkcsa_queries hkcsa_queries;
                                   /* top-bit passes + LDS bucket sorts); single GPU and slices */
 #define HKCSA_FLAG_MUL_BINS 8u /* sharded slices: multiplicative bucket bins even where the  */
                                /* shift bins would do (diagnostic; chosen automatically)    */
+#define HKCSA_FLAG_MAX_BUCKETS 16u /* single GPU: 2^16 buckets (2^17 with half items) at any n, */
+                                   /* so small texts take the 1 GiB pipeline (diagnostic)       */
 
 typedef struct hkcsa_opts {
   int32_t device;   /* HIP device ordinal (-1 = current)                 */
@@ -269,7 +271,8 @@ int hkcsa_kernel_stats(hkcsa_index* ix, const char* name, uint64_t* launches, do
                        double* alg_bytes);
 /* Build-stage counters of the last build: [0] radix / cursor scatter passes run, [1] skipped,
  * [2] refinement rounds (doubling rounds << 32), [3] symbols per key; bucket build:
- * [4] LDS work items, [5] big buckets, [6] suffixes in big buckets, [7] 1 = global path,
+ * [4] LDS work items, [5] big buckets, [6] suffixes in big buckets, [7] bit 0 = global path,
+ * bit 1 = packed records (one u64 of key bits and position per suffix through the partition),
  * [8] LDS work items sorted by the stable LSD passes instead of the MSD bin fast path;
  * then tied suffixes per round (up to cap). */
 int hkcsa_build_info(hkcsa_index* ix, uint64_t* info, int cap);

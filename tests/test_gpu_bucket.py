@@ -12,6 +12,7 @@ from oracle import oracle
 pytestmark = pytest.mark.gpu
 
 GLOBAL_SORT = 4
+MAX_BUCKETS = 16   # 2^17 buckets at any n: the 1 GiB pipeline (half items, packed records)
 
 
 @pytest.fixture(scope="module")
@@ -40,6 +41,7 @@ def _cases():
     # terminal above every symbol, in the middle, and not unique
     yield "term_top", np.concatenate([_rand(300000, b"abc", 25), [ord("~")]]).astype(np.uint8)
     yield "term_mid", np.concatenate([_rand(300000, b"az", 26), [ord("m")]]).astype(np.uint8)
+    yield "term_mid4", np.concatenate([_rand(300000, b"acgt", 35), [ord("m")]]).astype(np.uint8)
     yield "term_repeated", np.concatenate([_rand(300000, b"$AC", 27), [ord("$")]]).astype(np.uint8)
     yield "term_lowest_byte", np.concatenate([_rand(100000, b"\x01\x02\x03", 28), [0]]).astype(np.uint8)
     # skewed binary: wide local keys and big buckets (most suffixes start with a's)
@@ -58,7 +60,7 @@ def _cases():
     yield "all_same_70", np.frombuffer(b"q" * 70, dtype=np.uint8)
 
 
-@pytest.mark.parametrize("flags", [0, GLOBAL_SORT])
+@pytest.mark.parametrize("flags", [0, GLOBAL_SORT, MAX_BUCKETS])
 @pytest.mark.parametrize("name,text", list(_cases()))
 def test_bucket_build_vs_oracle(hk, name, text, flags):
     dev = hk.DeviceIndex.from_bytes(text.tobytes(), device=0, flags=flags)
@@ -74,6 +76,10 @@ def test_bucket_build_vs_oracle(hk, name, text, flags):
         assert info[7] == 0 and info[4] > 0 and info[5] == 0, (name, info[:8])
     if flags == 0 and name == "dna_run_2M":
         assert info[7] == 0 and info[5] >= 1, (name, info[:8])
+    if flags == MAX_BUCKETS and name in ("dna_4M", "dna_run_2M", "term_mid4", "radix16_1M"):
+        # packed records (bit 1) with the prev field re-coded without the terminal ('$' lowest in
+        # dna_*, 'm' inside the alphabet in term_mid4)
+        assert info[7] & 2, (name, info[:8])
     dev.close()
 
 

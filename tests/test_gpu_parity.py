@@ -233,7 +233,7 @@ def test_full_size_bench_1GiB_sigma4(hk):
     dev.build_sa()
     dev.build_bwt()
     info = dev.build_info()
-    assert info[7] == 0 and info[4] > 0, info[:10]   # bucket path, LDS work items
+    assert info[7] == 2 and info[4] > 0, info[:10]   # bucket path with packed records, LDS work items
     sa = dev.sa()
     text = oracle.synth_text(n, b"ACGT", seed=2)
     assert oracle.check_sa(text, sa) == 0

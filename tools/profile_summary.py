@@ -36,8 +36,10 @@ TIMERS = {
     "byte_hist": lambda k: "k_byte_hist" in k,
     "wt_bits": lambda k: "k_wt_bits" in k,
     "wt_partition": lambda k: "k_wt_partition" in k,
-    "radix_part_text": lambda k: "k_cpart<true" in k,
-    "radix_part": lambda k: "k_cpart<false" in k,
+    # k_cpart<MODE, LB, NB, T>: MODE 0 = pass A from the text, 1 = pass A from packed keys, 2 = pass B
+    "radix_part_text": lambda k: "k_cpart<0," in k,
+    "radix_part_keys": lambda k: "k_cpart<1," in k,
+    "radix_part": lambda k: "k_cpart<2," in k,
     "sa_bucket_hist": lambda k: "k_bucket_hist_spans" in k,
     "sa_digit_hist": lambda k: "k_bucket_hist<" in k,
     "fm_count": lambda k: "k_count" in k,
