@@ -456,7 +456,9 @@ struct CpShared {
     } ft;
   } stage;
   uint8_t sd[SD ? T * CP_I : 4];   // packed pass A: low 8 bits of each staged slot's digit
-  uint64_t gb[NB];     // destination of the digit's run minus its tile start
+  // destination of the digit's run minus its tile start (packed pass A: u32, single GPU n < 2^32,
+  // so that 512-thread tiles fit two workgroups per CU)
+  std::conditional_t<SD, uint32_t, uint64_t> gb[NB];
   uint32_t cnt[NB];    // digit counts (ranks by LDS atomics)
   uint32_t tst[NB];    // tile-local exclusive digit starts
   uint32_t wsum[NB / 64];
@@ -600,7 +602,7 @@ __global__ __launch_bounds__(T, T == 1024 ? 1 : 2) void k_cpart(const uint64_t* 
       sh.stage.keys[f] = key[k];
       if (SD) sh.sd[f] = (uint8_t)(rk[k] >> 16);
     }
-  if (tid < NB) sh.gb[tid] = g - sh.tst[tid];   // first use of the reservation
+  if (tid < NB) sh.gb[tid] = (std::remove_reference_t<decltype(sh.gb[0])>)(g - sh.tst[tid]);   // first use of the reservation
   __syncthreads();
   uint32_t dg[CP_I / 2] = {};   // digits of the staged slots, two per register
   const uint32_t hi256 = SD ? sh.tst[256] : 0u;   // staged slots >= hi256 hold digits >= 256
@@ -611,7 +613,8 @@ __global__ __launch_bounds__(T, T == 1024 ? 1 : 2) void k_cpart(const uint64_t* 
       const uint64_t kk = sh.stage.keys[s];
       const uint32_t d = SD ? (uint32_t)sh.sd[s] | (s >= hi256 ? 256u : 0u) : (uint32_t)((kk - kbias) >> shift) & DM;
       if (!PK) dg[i >> 1] |= d << (16 * (i & 1));
-      kout[sh.gb[d] + s] = kk;
+      if (SD) kout[(uint32_t)(sh.gb[d] + s)] = kk;
+      else kout[sh.gb[d] + s] = kk;
     }
   }
   if (PK) return;
@@ -2126,13 +2129,21 @@ int cursor_partition(Index& ix, uint64_t n, int D, int bitlo, uint64_t kbias, co
     TimedLaunch t(ix.timer, tks ? "radix_part_text" : "radix_part_keys",
                   (double)n * (packed ? 1 + 8 : tks ? 1 + 8 + 4 : 2 * (8 + 4)));
     const unsigned grid = (unsigned)(8 * ceil_div(nspan, 8u) * (span / CP_TILE));
+    // packed: 512-thread tiles, two workgroups per CU (HKCSA_PK_A1024=1: 1024-thread tiles, one per CU)
+    static const bool a1024 = getenv("HKCSA_PK_A1024") && atoi(getenv("HKCSA_PK_A1024")) != 0;
     const unsigned grid_pk = (unsigned)(8 * ceil_div(nspan, 8u) * (span / (1024 * CP_I)));
-    if (packed && tks->g.lb == 2)
+    if (packed && a1024 && tks->g.lb == 2)
       k_cpart<0, 2, 512, 1024, true><<<grid_pk, 1024, 0, s>>>(nullptr, nullptr, kp[outA], nullptr, n, bitlo2 + sA, 0,
                                                              d_curA, nullptr, nullptr, span, tks2, pk->g.pbits, d_ovf);
-    else if (packed)
+    else if (packed && a1024)
       k_cpart<0, 0, 512, 1024, true><<<grid_pk, 1024, 0, s>>>(nullptr, nullptr, kp[outA], nullptr, n, bitlo2 + sA, 0,
                                                              d_curA, nullptr, nullptr, span, tks2, pk->g.pbits, d_ovf);
+    else if (packed && tks->g.lb == 2)
+      k_cpart<0, 2, 512, CP_T, true><<<grid, CP_T, 0, s>>>(nullptr, nullptr, kp[outA], nullptr, n, bitlo2 + sA, 0,
+                                                          d_curA, nullptr, nullptr, span, tks2, pk->g.pbits, d_ovf);
+    else if (packed)
+      k_cpart<0, 0, 512, CP_T, true><<<grid, CP_T, 0, s>>>(nullptr, nullptr, kp[outA], nullptr, n, bitlo2 + sA, 0,
+                                                          d_curA, nullptr, nullptr, span, tks2, pk->g.pbits, d_ovf);
     else if (!tks)
       k_cpart<1, 0><<<grid, CP_T, 0, s>>>(kp[0], vp[0], kp[1], vp[1], n, bitlo + sA, kbias, d_curA, nullptr, nullptr,
                                           span, TextKeySrc{});
