@@ -730,7 +730,7 @@ constexpr uint32_t BF_MAXBIN = 32;
 
 // PK: xs holds the packed records (sym = record >> xsh, position = the low pbits bits) and the
 // positions come from them instead of a value plane.
-template <typename V, bool TRACE, int T, bool PK = false>
+template <typename V, bool TRACE, int T, bool PK = false, bool X32 = false>
 __device__ __forceinline__ bool bucket_sort_fast(BsSharedT<T>& sh, uint2 it, const uint64_t (&xs)[BS_I],
                                                  const uint32_t (&pvr)[BS_H], uint32_t vmask, uint32_t s0,
                                                  uint64_t xmin, int lo, int width, int pb, int xsh, int pbits,
@@ -761,7 +761,10 @@ __device__ __forceinline__ bool bucket_sort_fast(BsSharedT<T>& sh, uint2 it, con
 #pragma unroll
   for (int k = 0; k < BS_I; ++k) {
     const bool valid = (vmask >> k) & 1u;
-    lk[k] = (uint32_t)(((PK ? xs[k] >> xsh : xs[k]) - xmin) >> lo) & wmask;
+    if (X32)
+      lk[k] = (((uint32_t)(xs[k] >> 32) >> (xsh - 32)) - (uint32_t)xmin) >> lo & wmask;
+    else
+      lk[k] = (uint32_t)(((PK ? xs[k] >> xsh : xs[k]) - xmin) >> lo) & wmask;
     // packed: the position waits in the u32 plane by slot (free until the records' scatter), so no
     // register holds it across the histogram and the scan
     if (PK) sh.buf[s0 + 64u * k] = (uint32_t)xs[k] & (uint32_t)((1ull << pbits) - 1);
@@ -1344,7 +1347,9 @@ __global__ __launch_bounds__(BS_T, 1) void k_bucket_sort(const uint64_t* __restr
 
 // Fast-path kernel: the same prologue (the item's sym range and varying bits), then the MSD + bin-rank
 // sort; items it cannot take (wide keys, a bin over BF_MAXBIN) are appended to `fb` for k_bucket_sort.
-template <typename V, bool TRACE, int T, bool PK = false>
+// X32 (packed records whose sym field starts at bit >= 32): the sym is the record's high word shifted,
+// so the prologue and the local keys work in 32-bit arithmetic.
+template <typename V, bool TRACE, int T, bool PK = false, bool X32 = false>
 __global__ __launch_bounds__(T, T == 1024 ? 1 : 4) void k_bucket_sort_fast(const uint64_t* __restrict__ keys,
                                                               const uint32_t* __restrict__ vals,
                                                               const uint2* __restrict__ items, int pb, int sb, int hb,
@@ -1377,18 +1382,34 @@ __global__ __launch_bounds__(T, T == 1024 ? 1 : 4) void k_bucket_sort_fast(const
   for (uint32_t i = tid; i < (T / 64) * 256; i += T) (&sh.mt[0][0])[i] = 0;
   // the sym fields once (key -> sym - symbias in place, the BWT code / position bits to pvr), then one
   // reduction of min, max, or, and: the low varying bit of the values is that of the values relative
-  // to the minimum, and the relative width is bits((max - min) >> lo)
+  // to the minimum, and the relative width is bits((max - min) >> lo).  Branch-free over the item's
+  // end (neutral values) for X32, so no record's fields wait in scratch across a masked block.
+  using XT = std::conditional_t<X32, uint32_t, uint64_t>;
+  const int xsh = pbits + pbe;   // packed: the sym field's first bit in the record
   const uint32_t pmask = (1u << pb) - 1, himask = (1u << hb) - 1;
   uint32_t pvr[BS_H];
-  uint64_t xmin = ~0ull, xmax = 0, vor = 0, vand = ~0ull;
+  XT xmin = (XT)~0ull, xmax = 0, vor = 0, vand = (XT)~0ull;
 #pragma unroll
   for (int k = 0; k < BS_I; ++k) {
-    const uint64_t kl = PK ? key[k] >> pbits : key[k];   // packed: the record stays (positions)
-    const uint32_t pv = ((uint32_t)(kl >> hb) & pmask) | (((uint32_t)kl & himask) << pb);
+    const bool valid = (vmask >> k) & 1u;
+    uint32_t pv;
+    XT x;
+    if (X32) {
+      pv = (uint32_t)(key[k] >> pbits) & pmask;   // hb = 0, symbias = 0
+      x = (XT)((uint32_t)(key[k] >> 32) >> (xsh - 32));
+    } else {
+      const uint64_t kl = PK ? key[k] >> pbits : key[k];   // packed: the record stays (positions)
+      pv = ((uint32_t)(kl >> hb) & pmask) | (((uint32_t)kl & himask) << pb);
+      x = (XT)(((kl >> pbe) & symmask) - symbias);
+      if (!PK) key[k] = x;
+    }
     if (k < BS_H) pvr[k] = pv; else pvr[k - BS_H] |= pv << 16;
-    const uint64_t x = ((kl >> pbe) & symmask) - symbias;
-    if (!PK) key[k] = x;
-    if ((vmask >> k) & 1u) {
+    if (X32) {   // selects: no masked block (the 64-bit variants keep less live with the branch)
+      xmin = valid && x < xmin ? x : xmin;
+      xmax = valid && x > xmax ? x : xmax;
+      vor |= valid ? x : (XT)0;
+      vand &= valid ? x : (XT)~0ull;
+    } else if (valid) {
       xmin = x < xmin ? x : xmin;
       xmax = x > xmax ? x : xmax;
       vor |= x;
@@ -1397,13 +1418,13 @@ __global__ __launch_bounds__(T, T == 1024 ? 1 : 4) void k_bucket_sort_fast(const
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
-    const uint64_t a0 = __shfl_xor(xmin, o, 64), a1 = __shfl_xor(xmax, o, 64);
+    const XT a0 = __shfl_xor(xmin, o, 64), a1 = __shfl_xor(xmax, o, 64);
     xmin = a0 < xmin ? a0 : xmin;
     xmax = a1 > xmax ? a1 : xmax;
     vor |= __shfl_xor(vor, o, 64);
     vand &= __shfl_xor(vand, o, 64);
   }
-  uint64_t* const red = reinterpret_cast<uint64_t*>(&sh.whist[0][0]);   // [4][(T / 64)], free until the lists
+  XT* const red = reinterpret_cast<XT*>(&sh.whist[0][0]);   // [4][(T / 64)], free until the lists
   if (lane == 0) {
     red[wv] = xmin;
     red[(T / 64) + wv] = xmax;
@@ -1418,15 +1439,15 @@ __global__ __launch_bounds__(T, T == 1024 ? 1 : 4) void k_bucket_sort_fast(const
     vor |= red[2 * (T / 64) + w];
     vand &= red[3 * (T / 64) + w];
   }
-  const uint64_t var = vor ^ vand;
+  const uint64_t var = (uint64_t)(vor ^ vand);
   const int lo = var ? __builtin_ctzll(var) : 0;
-  const uint64_t span = (xmax - xmin) >> lo;
+  const uint64_t span = (uint64_t)(xmax - xmin) >> lo;
   const int width = var ? 64 - __builtin_clzll(span) : 0;
   if (TRACE) ts[1] = stamp();
   // (every thread has read the reduction before the fast path reuses whist: its first barrier)
   const bool ok = width >= 1 && width <= 30 &&
-                  bucket_sort_fast<V, TRACE, T, PK>(sh, it, key, pvr, vmask, s0, xmin, lo, width, pb, pbits + pbe,
-                                                    pbits, term, vals + it.x,
+                  bucket_sort_fast<V, TRACE, T, PK, X32>(sh, it, key, pvr, vmask, s0, (uint64_t)xmin, lo, width, pb,
+                                                         xsh, pbits, term, vals + it.x,
                                              sa + it.x, bwt + it.x, tie_k, tie_v, tie_n, ts);
   if (!ok && tid == 0) fb[atomicAdd(fb_n, 1u)] = it;
   if (TRACE) {
@@ -1659,6 +1680,13 @@ uint64_t sort_bucket_items(Index& ix, const BucketPlan& plan, const uint64_t* ke
         constexpr int T = decltype(ttag)::value;
         constexpr bool TR = decltype(trtag)::value;
         if constexpr (std::is_same<V, uint32_t>::value) {
+          if (pk && pk->g.pbits + pk->g.pb2 >= 32) {   // sym fields in the records' high words
+            k_bucket_sort_fast<V, TR, T, true, true><<<grid_n, T, 0, s>>>(
+                keys, pk->vfull, ix.bk_items.as<uint2>(), pb, sb, hb, symbias, d_inv, sa, bwt,
+                ix.ties_k.as<uint64_t>(), ix.ties_v.as<V>(), ix.ties_n.as<unsigned long long>(), ix.bk_fb.as<uint2>(),
+                fbn, TR ? tbuf.as<uint64_t>() : nullptr, pk->g);
+            return;
+          }
           if (pk) {
             k_bucket_sort_fast<V, TR, T, true><<<grid_n, T, 0, s>>>(
                 keys, pk->vfull, ix.bk_items.as<uint2>(), pb, sb, hb, symbias, d_inv, sa, bwt,
