@@ -329,6 +329,23 @@ def test_shard_two_phase_emulated(hk, nranks, flags, alpha):
     assert np.array_equal(np.concatenate(parts), ref)
 
 
+@pytest.mark.parametrize("n,nranks,flags,alpha", [((24 << 20) + 1, 3, 0, b"ACGT"), ((24 << 20) + 1, 2, 1, b"ACGT"),
+                                                  ((24 << 20) + 1, 4, 8, b"ACGT"), ((12 << 20) + 1, 2, 0, bytes(range(256)))],
+                         ids=["dna24M-3", "dna24M-2-pos64", "dna24M-4-mul", "bytes12M-2"])
+def test_shard_large_slices(hk, n, nranks, flags, alpha):
+    """Slices of millions of suffixes, so the slice's cursor partition runs both passes (more than 2^8
+    bins) as at the bench sizes: the concatenated slices checked by the O(n) SA checker and against the
+    oracle BWT; flags=1 64-bit positions, flags=8 multiplicative bins."""
+    text = oracle.synth_text(n, alpha, seed=31 + nranks)
+    devs, _ = _emulated_shard_build(hk, text, nranks, flags)
+    sa = np.concatenate([d.shard_sa() for d in devs])
+    assert oracle.check_sa(text, sa) == 0
+    assert np.array_equal(np.concatenate([d.shard_bwt() for d in devs]), oracle.bwt(text, sa))
+    assert max(d.build_info()[4] for d in devs) > 256   # bucket items: more than pass A's 256 digits
+    for d in devs:
+        d.close()
+
+
 def _repetitive(name):
     rng = np.random.default_rng(99)
     if name == "periodic_64K":
