@@ -104,6 +104,8 @@ struct Index {
   DevBuf cp_part, cp_cur, cp_tiles; // cursor partition: per-span counts, destination cursors, pass-B tiles
   HostBuf cp_host;                  // ... and its pinned host side (bucket counts, region table)
   DevBuf sel;                     // sharded build: selection masks of the slice (u16 per 16 positions)
+  DevBuf kmer;                    // count: backward-search state of every K-symbol string (build_wt)
+  int kmer_k = 0;
   DevBuf tile_a, tile_b, tile_c, tile_d, tile_e;
   DevBuf small;                // scratch for totals etc.
   DevBuf seq[2];               // WT level code sequences

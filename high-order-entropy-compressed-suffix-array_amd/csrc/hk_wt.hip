@@ -319,17 +319,38 @@ __global__ __launch_bounds__(256) void k_wt_extract(const uint64_t* __restrict__
 }
 
 // ------------------------------------------------------------ queries
+// Batched backward search, one lane per pattern (csa/enhanced_fm_index.py:21-32): the state (xl, xr)
+// is the half-open row range, a symbol outside the alphabet or an empty range ends the search.  With
+// a k-mer table (K > 0) the last K symbols of a pattern take one lookup of the state they lead to
+// from the full range (k_kmer_table: the same LF steps, so identical results) instead of K steps.
+template <int NC>
 __global__ __launch_bounds__(256) void k_count(WtView v, const uint8_t* __restrict__ pats,
                                                const uint64_t* __restrict__ offs, uint64_t P,
-                                               int64_t* __restrict__ lr, uint64_t* __restrict__ cnt) {
-  __shared__ QShared q;
+                                               int64_t* __restrict__ lr, uint64_t* __restrict__ cnt,
+                                               const ulonglong2* __restrict__ kmer, int K) {
+  __shared__ QSharedT<NC> q;
   load_qshared(q, v);
   for (uint64_t p = (uint64_t)blockIdx.x * 256 + threadIdx.x; p < P; p += (uint64_t)gridDim.x * 256) {
     const uint64_t s = offs[p];
     uint64_t k = offs[p + 1];
     uint64_t xl = 0, xr = v.n;
     bool ok = true;
-    while (k > s) {
+    if (K > 0 && k - s >= (uint64_t)K) {
+      uint32_t idx = 0;
+      for (int j = 0; j < K; ++j) {
+        const int c = q.code[pats[k - K + j]];
+        ok &= c >= 0;
+        idx = idx * (uint32_t)v.sigma + (uint32_t)(c < 0 ? 0 : c);
+      }
+      k -= K;
+      if (ok) {
+        const ulonglong2 e = kmer[idx];
+        xl = e.x;
+        xr = e.y;
+        ok = xl < xr;
+      }
+    }
+    while (ok && k > s) {
       --k;
       const int c = q.code[pats[k]];
       if (c < 0) { ok = false; break; }
@@ -339,6 +360,26 @@ __global__ __launch_bounds__(256) void k_count(WtView v, const uint8_t* __restri
     lr[2 * p] = ok ? (int64_t)xl : -1;
     lr[2 * p + 1] = ok ? (int64_t)xr - 1 : -1;
     if (cnt) cnt[p] = ok ? xr - xl : 0;
+  }
+}
+
+// k-mer table: entry idx (the codes c_0 .. c_{K-1} of a K-symbol string, c_0 most significant in
+// radix sigma) = the state after the backward search of that string from the full range; an empty
+// state is stored as (1, 0)
+template <int NC>
+__global__ __launch_bounds__(256) void k_kmer_table(WtView v, int K, uint64_t total, ulonglong2* __restrict__ tab) {
+  __shared__ QSharedT<NC> q;
+  load_qshared(q, v);
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (uint64_t)gridDim.x * 256) {
+    uint64_t xl = 0, xr = v.n, x = i;
+    bool ok = true;
+    for (int j = 0; j < K; ++j) {   // the last symbol (least significant digit) first
+      const int c = (int)(x % (uint64_t)v.sigma);
+      x /= (uint64_t)v.sigma;
+      lf_pair(q, c, xl, xr);
+      if (xl >= xr) { ok = false; break; }
+    }
+    tab[i] = ok ? make_ulonglong2(xl, xr) : make_ulonglong2(1, 0);
   }
 }
 
@@ -558,6 +599,28 @@ void build_wt(Index& ix) {
       }
     }
   }
+  // k-mer table for the batched count: K = the most symbols with sigma^K <= 2^19 entries (6 MiB of
+  // (l, r) pairs, cache-resident), at most 12 (HKCSA_KMER=0: no table, for A/B)
+  static const bool kmer_env = !getenv("HKCSA_KMER") || atoi(getenv("HKCSA_KMER")) != 0;
+  ix.kmer_k = 0;
+  if (kmer_env && L > 0 && sigma >= 2) {
+    int K = 0;
+    uint64_t tot = 1;
+    while (K < 12 && tot * (uint64_t)sigma <= (1ull << 19)) {
+      tot *= (uint64_t)sigma;
+      ++K;
+    }
+    if (K >= 2) {
+      ix.kmer.ensure(tot * 16 + 16);
+      TimedLaunch t(ix.timer, "fm_kmer_table", (double)tot * 16);
+      if (sigma <= 16)
+        k_kmer_table<16><<<grid_for(tot, 256, 8192), 256, 0, s>>>(ix.view(), K, tot, ix.kmer.as<ulonglong2>());
+      else
+        k_kmer_table<256><<<grid_for(tot, 256, 8192), 256, 0, s>>>(ix.view(), K, tot, ix.kmer.as<ulonglong2>());
+      HK_HIP(hipGetLastError());
+      ix.kmer_k = K;
+    }
+  }
   HK_HIP(hipStreamSynchronize(s));
   ix.have_wt = true;
 }
@@ -567,7 +630,13 @@ void query_count(Index& ix, const uint8_t* d_pats, const uint64_t* d_offs, uint6
   if (!ix.have_wt || ix.sharded) throw ApiError{-3, "count: wavelet tree not built"};
   if (!P) return;
   TimedLaunch t(ix.timer, "fm_count", 0.0);
-  k_count<<<grid_for(P, 256, 65535), 256, 0, ix.stream>>>(ix.view(), d_pats, d_offs, P, d_lr, d_cnt);
+  const ulonglong2* km = ix.kmer_k ? ix.kmer.as<ulonglong2>() : nullptr;
+  if (ix.sigma <= 16)
+    k_count<16><<<grid_for(P, 256, 65535), 256, 0, ix.stream>>>(ix.view(), d_pats, d_offs, P, d_lr, d_cnt, km,
+                                                                 ix.kmer_k);
+  else
+    k_count<256><<<grid_for(P, 256, 65535), 256, 0, ix.stream>>>(ix.view(), d_pats, d_offs, P, d_lr, d_cnt, km,
+                                                                  ix.kmer_k);
   HK_HIP(hipGetLastError());
 }
 

@@ -46,32 +46,38 @@ __device__ __forceinline__ uint64_t rank1_bit(const uint64_t* __restrict__ lines
   return r;
 }
 
-struct QShared {
-  uint64_t obn[kMaxLevels][256];
-  uint64_t rbase[kMaxLevels][256];
-  uint8_t bit[kMaxLevels][256];
-  uint8_t depth[256];
+// Per-level / per-code walk tables in LDS for NC codes (256: any alphabet; 16: sigma <= 16, ~1 KiB
+// instead of ~38 KiB, so the query kernels keep more waves in flight).
+template <int NC>
+struct QSharedT {
+  uint64_t obn[kMaxLevels][NC];
+  uint64_t rbase[kMaxLevels][NC];
+  uint8_t bit[kMaxLevels][NC];
+  uint8_t depth[NC];
   int16_t code[256];
   const uint64_t* lines[kMaxLevels];
 };
+using QShared = QSharedT<256>;
 
-__device__ __forceinline__ void load_qshared(QShared& q, const WtView& v) {
+template <int NC>
+__device__ __forceinline__ void load_qshared(QSharedT<NC>& q, const WtView& v) {
   const int t = threadIdx.x;  // blockDim == 256
-  q.depth[t] = v.depth[t];
   q.code[t] = v.code[t];
+  if (t < NC) q.depth[t] = v.depth[t];
   for (int d = 0; d < v.levels; ++d) {
-    if (t < v.sigma) {
+    if (t < v.sigma && t < NC) {
       q.obn[d][t] = v.obn[d * 256 + t];
       q.rbase[d][t] = v.rbase[d * 256 + t];
     }
-    q.bit[d][t] = v.bit[d * 256 + t];
+    if (t < NC) q.bit[d][t] = v.bit[d * 256 + t];
   }
   if (t < kMaxLevels) q.lines[t] = v.lines[t];
   __syncthreads();
 }
 
 // LF step of the pair (xl, xr) for code c: returns the leaf positions
-__device__ __forceinline__ void lf_pair(const QShared& q, int c, uint64_t& xl, uint64_t& xr) {
+template <class Q>
+__device__ __forceinline__ void lf_pair(const Q& q, int c, uint64_t& xl, uint64_t& xr) {
   const int dep = q.depth[c];
   for (int d = 0; d < dep; ++d) {
     const uint64_t* L = q.lines[d];
@@ -92,7 +98,8 @@ __device__ __forceinline__ void lf_pair(const QShared& q, int c, uint64_t& xl, u
 // LF of row x without knowing its symbol: walk down following the bits (the node's first code
 // lo stands for every code of the node in the per-code tables).  Returns the leaf position
 // C[c] + occ(c, x) and the dense code c = BWT[x].
-__device__ __forceinline__ uint64_t lf_access(const QShared& q, int sigma, uint64_t x, int& code) {
+template <class Q>
+__device__ __forceinline__ uint64_t lf_access(const Q& q, int sigma, uint64_t x, int& code) {
   int lo = 0, hi = sigma;
   for (int d = 0; hi - lo > 1; ++d) {
     const int mid = lo + (hi - lo) / 2;
