@@ -2,7 +2,7 @@
 //
 // Every rank holds the same T' (≤ 288 GB HBM each makes replication cheap) and owns one
 // contiguous range of the FINAL suffix array:
-//   1. each rank histograms the 14-bit key prefix of every 16th position of its block; one RCCL
+//   1. each rank histograms the 14-bit key prefix of every 64th position of its block; one RCCL
 //      all-reduce gives the sampled global histogram, from which all ranks derive the same
 //      splitter buckets B_1 < ... < B_{N-1};
 //   2. each rank counts, over its block, the suffixes below every splitter (a register-only byte
@@ -35,7 +35,7 @@ namespace {
 constexpr int SH_BUCKET_BITS = 14;
 constexpr int SH_BUCKETS = 1 << SH_BUCKET_BITS;
 constexpr int PS_TILE = 4096;
-constexpr int SH_SAMPLE = 16;   // histogram sample stride (splitters need balance, not exact counts)
+constexpr int SH_SAMPLE = 64;   // histogram sample stride (splitters need balance, not exact counts)
 
 struct ShardComm {  // one RCCL communicator per process (one process per GPU)
   ncclComm_t comm = nullptr;

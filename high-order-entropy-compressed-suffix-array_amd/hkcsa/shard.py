@@ -30,7 +30,7 @@ from typing import Callable, Sequence
 import numpy as np
 
 SH_BUCKETS = 1 << 14
-SH_SAMPLE = 16
+SH_SAMPLE = 64
 MAX_ROUNDS = 64
 
 

@@ -334,7 +334,7 @@ static uint64_t shard_bucket(const uint8_t* t, uint64_t n, uint64_t p, const uin
   return key >> bsh;
 }
 
-/* Sampled key-prefix histogram of positions p in [lo, hi) with p % 16 == 0 (hk_shard.hip,
+/* Sampled key-prefix histogram of positions p in [lo, hi) with p % 64 == 0 (hk_shard.hip,
  * SH_SAMPLE): the splitters only need balance; exact slice sizes come from oracle_shard_below. */
 void oracle_shard_hist(const uint8_t* t, uint64_t n, uint64_t lo, uint64_t hi, uint64_t* hist /* 16384 */) {
   uint16_t code[256];
@@ -344,7 +344,7 @@ void oracle_shard_hist(const uint8_t* t, uint64_t n, uint64_t lo, uint64_t hi, u
   int bsh = kb - 14;
   if (bsh < 0) bsh = 0;
   memset(hist, 0, 16384 * sizeof(uint64_t));
-  for (uint64_t p = (lo + 15) / 16 * 16; p < hi; p += 16) hist[shard_bucket(t, n, p, code, q, pb, R, bsh)]++;
+  for (uint64_t p = (lo + 63) / 64 * 64; p < hi; p += 64) hist[shard_bucket(t, n, p, code, q, pb, R, bsh)]++;
 }
 
 /* below[j] = #{p in [lo, hi) : bucket(p) < B[j]} for j < nb */

@@ -75,7 +75,7 @@ def test_slice_bounds_tile_the_sa(nranks):
     from hkcsa.shard import split_buckets
     t = oracle.synth_text(20000, b"ACGT", seed=4)
     h = oracle.shard_hist(t, 0, len(t))
-    assert int(h.sum()) == (len(t) + 15) // 16
+    assert int(h.sum()) == (len(t) + 63) // 64
     B = split_buckets(h, nranks)
     below = sum(oracle.shard_below(t, len(t) * r // nranks, len(t) * (r + 1) // nranks, B) for r in range(nranks))
     assert np.array_equal(below, oracle.shard_below(t, 0, len(t), B))
