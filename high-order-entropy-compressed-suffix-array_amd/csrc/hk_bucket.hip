@@ -2184,16 +2184,22 @@ int cursor_partition(Index& ix, uint64_t n, int D, int bitlo, uint64_t kbias, co
     HK_HIP(hipGetLastError());
     ix.info[0] += 1;
   };
-  // the counts come back behind an event while pass A runs
+  // the counts come back on the auxiliary stream while pass A runs (pass A does not wait for the
+  // copies; the host waits for them alone)
+  if (!ix.aux_stream) HK_HIP(hipStreamCreateWithFlags(&ix.aux_stream, hipStreamNonBlocking));
   auto counts_then_passA = [&]() {
-    HK_HIP(hipMemcpyAsync(h_hist, d_hist, (uint64_t)nb * 8, hipMemcpyDeviceToHost, s));
-    HK_HIP(hipMemcpyAsync(h_totA, d_totA, (2 * (CP_NAM + 1) + 1) * 8, hipMemcpyDeviceToHost, s));
-    hipEvent_t ev;
-    HK_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-    HK_HIP(hipEventRecord(ev, s));
+    hipEvent_t ev_pre, ev_cnt;
+    HK_HIP(hipEventCreateWithFlags(&ev_pre, hipEventDisableTiming));
+    HK_HIP(hipEventCreateWithFlags(&ev_cnt, hipEventDisableTiming));
+    HK_HIP(hipEventRecord(ev_pre, s));
+    HK_HIP(hipStreamWaitEvent(ix.aux_stream, ev_pre, 0));
+    HK_HIP(hipMemcpyAsync(h_hist, d_hist, (uint64_t)nb * 8, hipMemcpyDeviceToHost, ix.aux_stream));
+    HK_HIP(hipMemcpyAsync(h_totA, d_totA, (2 * (CP_NAM + 1) + 1) * 8, hipMemcpyDeviceToHost, ix.aux_stream));
+    HK_HIP(hipEventRecord(ev_cnt, ix.aux_stream));
     passA();
-    const hipError_t we = hipEventSynchronize(ev);   // the counts, not pass A
-    (void)hipEventDestroy(ev);
+    const hipError_t we = hipEventSynchronize(ev_cnt);   // the counts, not pass A
+    (void)hipEventDestroy(ev_pre);
+    (void)hipEventDestroy(ev_cnt);
     HK_HIP(we);
   };
   prepass(false);

@@ -148,6 +148,7 @@ struct KernelTimer {
   bool enabled = false;
   std::vector<Pending> pending;
   std::vector<std::pair<std::string, Stat>> stats;
+  std::vector<hipEvent_t> pool;   // resolved events, reused: no event creation on the launch path
   hipStream_t stream = nullptr;
 
   Stat& stat(const std::string& n) {
@@ -155,12 +156,21 @@ struct KernelTimer {
     stats.emplace_back(n, Stat{});
     return stats.back().second;
   }
+  // timing events need no system-scope release (the host reads only their timestamps)
+  hipEvent_t get() {
+    hipEvent_t e = nullptr;
+    if (!pool.empty()) {
+      e = pool.back();
+      pool.pop_back();
+    } else {
+      HK_HIP(hipEventCreateWithFlags(&e, hipEventDisableSystemFence));
+    }
+    return e;
+  }
   // returns the event to record after the launch (or nullptr when disabled)
   hipEvent_t begin(const std::string& name, double bytes) {
     if (!enabled) return nullptr;
-    Pending pd{name, nullptr, nullptr, bytes};
-    HK_HIP(hipEventCreate(&pd.a));
-    HK_HIP(hipEventCreate(&pd.b));
+    Pending pd{name, get(), get(), bytes};
     HK_HIP(hipEventRecord(pd.a, stream));
     pending.push_back(pd);
     return pd.b;
@@ -177,14 +187,15 @@ struct KernelTimer {
       s.launches++;
       s.ms += ms;
       s.bytes += pd.bytes;
-      (void)hipEventDestroy(pd.a);
-      (void)hipEventDestroy(pd.b);
+      pool.push_back(pd.a);
+      pool.push_back(pd.b);
     }
     pending.clear();
   }
   void reset() { resolve(); stats.clear(); }
   ~KernelTimer() {
     for (auto& pd : pending) { (void)hipEventDestroy(pd.a); (void)hipEventDestroy(pd.b); }
+    for (hipEvent_t e : pool) (void)hipEventDestroy(e);
   }
 };
 

@@ -70,6 +70,7 @@ struct Index {
   int device = 0;
   uint32_t flags = 0;          // hkcsa_opts.flags
   hipStream_t stream = nullptr;
+  hipStream_t aux_stream = nullptr;   // read-backs that overlap the main stream (cursor partition counts)
   uint64_t n = 0;
   DevBuf text;                 // T' (n bytes + 64 pad)
 

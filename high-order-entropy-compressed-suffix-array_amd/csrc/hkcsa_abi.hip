@@ -221,9 +221,11 @@ void hkcsa_free(hkcsa_index* h) {
   if (!h) return;
   (void)hipSetDevice(h->ix.device);
   (void)hipStreamSynchronize(h->ix.stream);
-  hipStream_t s = h->ix.stream;
+  if (h->ix.aux_stream) (void)hipStreamSynchronize(h->ix.aux_stream);
+  hipStream_t s = h->ix.stream, a = h->ix.aux_stream;
   delete h;
   if (s) (void)hipStreamDestroy(s);
+  if (a) (void)hipStreamDestroy(a);
 }
 
 int hkcsa_bwt_gather(const uint8_t* text, uint64_t n, const uint64_t* sa, uint8_t* out) {
