@@ -107,6 +107,9 @@ struct Index {
   DevBuf sel;                     // sharded build: selection masks of the slice (u16 per 16 positions)
   DevBuf kmer;                    // count: backward-search state of every K-symbol string (build_wt)
   int kmer_k = 0;
+  DevBuf occ_lines, occ_sb;       // count: flat occ directory of the BWT (sigma <= 8, build_wt)
+  bool occ_ok = false;
+  uint64_t occ_nsb = 0;
   DevBuf tile_a, tile_b, tile_c, tile_d, tile_e;
   DevBuf small;                // scratch for totals etc.
   DevBuf seq[2];               // WT level code sequences

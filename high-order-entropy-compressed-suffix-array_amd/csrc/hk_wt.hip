@@ -319,16 +319,111 @@ __global__ __launch_bounds__(256) void k_wt_extract(const uint64_t* __restrict__
 }
 
 // ------------------------------------------------------------ queries
+// ------------------------------------------------------------ flat occ directory (sigma <= 8)
+// The reference's find_range takes occ(c, i) from its dense occ table (utils/utils.py:26-32,
+// csa/enhanced_fm_index.py:34-40).  For small alphabets the batched count reads the same values from
+// a directory of the BWT instead of walking the wavelet tree: 64-B lines of OC_S = 128 symbols, each
+// 8 u16 counts (occurrences of every code before the line, relative to its superblock of 256 lines)
+// and the codes as 3 bit-planes of 128 bits; per superblock 8 u64 counts.  occ(c, x) = superblock
+// count + line count + popcount of the codes equal to c below x in the line: one 64-B line per rank
+// (the WT needs one per level), 0.5 B per symbol.
+constexpr int OC_S = 128, OC_LPS = 256;
+
+// one workgroup per superblock, 32 lines per round: 8 threads per line, 16 symbols each (one 16-byte
+// load: the wave's loads are contiguous), whose plane bits are assembled in LDS with the line's
+// counts; exclusive counts inside the superblock, superblock totals per code (scanned afterwards)
+__global__ __launch_bounds__(256) void k_occ_lines(const uint8_t* __restrict__ bwt, uint64_t n,
+                                                   const int16_t* __restrict__ code, uint64_t nlines,
+                                                   uint4* __restrict__ lines, uint64_t* __restrict__ sbt) {
+  __shared__ int16_t CD[256];
+  __shared__ uint4 img[32 * 4];
+  __shared__ uint32_t lc[32][8];
+  __shared__ uint32_t carry[8], tot[8];
+  const uint32_t tid = threadIdx.x, ln = tid >> 3, j = tid & 7;
+  CD[tid] = code[tid];
+  if (tid < 8) carry[tid] = 0;
+  __syncthreads();
+  uint16_t* const img16 = reinterpret_cast<uint16_t*>(img);
+  for (int it = 0; it < OC_LPS / 32; ++it) {
+    const uint64_t l0 = (uint64_t)blockIdx.x * OC_LPS + (uint64_t)it * 32;
+    if (l0 >= nlines) break;   // uniform
+    const uint64_t li = l0 + ln, p = li * OC_S + 16 * j;
+    // bytes past n: code 0 (after every queried position; the BWT holds n + 64 bytes)
+    const uint4 v = li < nlines && p < n ? *reinterpret_cast<const uint4*>(bwt + p) : make_uint4(0, 0, 0, 0);
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    uint32_t pq[3] = {0, 0, 0};
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int c = p + i < n ? CD[(w[i >> 2] >> (8 * (i & 3))) & 255u] : 0;
+#pragma unroll
+      for (int q = 0; q < 3; ++q) pq[q] |= (uint32_t)((c >> q) & 1) << i;
+    }
+    // counts of the 8 codes in these 16 symbols (pairwise plane products), one byte each, summed over
+    // the line's 8 threads (<= 128 per byte, no carry)
+    const uint32_t n0 = ~pq[0] & 0xFFFFu, n1 = ~pq[1] & 0xFFFFu, n2 = ~pq[2] & 0xFFFFu;
+    const uint32_t a[4] = {n0 & n1, pq[0] & n1, n0 & pq[1], pq[0] & pq[1]};
+    uint64_t cb = 0;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) cb |= (uint64_t)__popc(a[c & 3] & ((c & 4) ? pq[2] : n2)) << (8 * c);
+    cb += __shfl_xor(cb, 1, 64);
+    cb += __shfl_xor(cb, 2, 64);
+    cb += __shfl_xor(cb, 4, 64);
+    lc[ln][j] = (uint32_t)(cb >> (8 * j)) & 255u;   // this line's count of code j
+#pragma unroll
+    for (int q = 0; q < 3; ++q) img16[ln * 32 + 8 * (1 + q) + j] = (uint16_t)pq[q];
+    __syncthreads();
+    {   // thread (code tid >> 5, line tid & 31): the code's occurrences before the line (32-lane scan)
+      const uint32_t c8 = tid >> 5, l32 = tid & 31u, v0 = lc[l32][c8];
+      uint32_t inc = v0;
+#pragma unroll
+      for (int d = 1; d < 32; d <<= 1) {
+        const uint32_t t = __shfl_up(inc, d, 32);
+        inc += l32 >= (uint32_t)d ? t : 0u;
+      }
+      img16[l32 * 32 + c8] = (uint16_t)(carry[c8] + inc - v0);
+      if (l32 == 31) tot[c8] = inc;
+    }
+    __syncthreads();
+    if (tid < 8) carry[tid] += tot[tid];
+    if (tid < 128 && l0 + (tid >> 2) < nlines) lines[l0 * 4 + tid] = img[tid];
+    __syncthreads();
+  }
+  if (tid < 8) sbt[(uint64_t)tid * gridDim.x + blockIdx.x] = carry[tid];   // [code][superblock]
+}
+
+__device__ __forceinline__ uint64_t occ_rank(const uint4* __restrict__ lines, const uint64_t* __restrict__ sb,
+                                             uint64_t nsb, int c, uint64_t x) {
+  const uint64_t li = x >> 7;
+  const uint32_t off = (uint32_t)x & 127u;
+  const uint4* L = lines + li * 4;
+  const uint4 h = L[0], a = L[1], b = L[2], d = L[3];
+  const uint32_t hw = c < 4 ? (c < 2 ? h.x : h.y) : (c < 6 ? h.z : h.w);
+  const uint32_t cnt = (hw >> (16 * (c & 1))) & 0xFFFFu;
+  const uint64_t p00 = ((uint64_t)a.y << 32) | a.x, p01 = ((uint64_t)a.w << 32) | a.z;
+  const uint64_t p10 = ((uint64_t)b.y << 32) | b.x, p11 = ((uint64_t)b.w << 32) | b.z;
+  const uint64_t p20 = ((uint64_t)d.y << 32) | d.x, p21 = ((uint64_t)d.w << 32) | d.z;
+  uint64_t m0 = ((c & 1) ? p00 : ~p00) & ((c & 2) ? p10 : ~p10) & ((c & 4) ? p20 : ~p20);
+  uint64_t m1 = ((c & 1) ? p01 : ~p01) & ((c & 2) ? p11 : ~p11) & ((c & 4) ? p21 : ~p21);
+  m0 &= off >= 64 ? ~0ull : ((1ull << off) - 1ull);
+  m1 &= off > 64 ? ((1ull << (off - 64)) - 1ull) : 0ull;
+  return sb[(uint64_t)c * nsb + (li >> 8)] + cnt + (uint64_t)(__popcll(m0) + __popcll(m1));
+}
+
 // Batched backward search, one lane per pattern (csa/enhanced_fm_index.py:21-32): the state (xl, xr)
 // is the half-open row range, a symbol outside the alphabet or an empty range ends the search.  With
 // a k-mer table (K > 0) the last K symbols of a pattern take one lookup of the state they lead to
 // from the full range (k_kmer_table: the same LF steps, so identical results) instead of K steps.
-template <int NC>
+// FLAT (sigma <= 8): the LF steps read the flat occ directory (one line per rank) instead of the WT.
+template <int NC, bool FLAT = false>
 __global__ __launch_bounds__(256) void k_count(WtView v, const uint8_t* __restrict__ pats,
                                                const uint64_t* __restrict__ offs, uint64_t P,
                                                int64_t* __restrict__ lr, uint64_t* __restrict__ cnt,
-                                               const ulonglong2* __restrict__ kmer, int K) {
+                                               const ulonglong2* __restrict__ kmer, int K,
+                                               const uint4* __restrict__ ol = nullptr,
+                                               const uint64_t* __restrict__ osb = nullptr, uint64_t onsb = 0) {
   __shared__ QSharedT<NC> q;
+  __shared__ uint64_t CC[8];
+  if (FLAT && threadIdx.x < 8) CC[threadIdx.x] = threadIdx.x < (unsigned)v.sigma ? v.Ccode[threadIdx.x] : 0;
   load_qshared(q, v);
   for (uint64_t p = (uint64_t)blockIdx.x * 256 + threadIdx.x; p < P; p += (uint64_t)gridDim.x * 256) {
     const uint64_t s = offs[p];
@@ -354,7 +449,12 @@ __global__ __launch_bounds__(256) void k_count(WtView v, const uint8_t* __restri
       --k;
       const int c = q.code[pats[k]];
       if (c < 0) { ok = false; break; }
-      lf_pair(q, c, xl, xr);
+      if (FLAT) {
+        xl = CC[c] + occ_rank(ol, osb, onsb, c, xl);
+        xr = CC[c] + occ_rank(ol, osb, onsb, c, xr);
+      } else {
+        lf_pair(q, c, xl, xr);
+      }
       if (xl >= xr) { ok = false; break; }
     }
     lr[2 * p] = ok ? (int64_t)xl : -1;
@@ -621,6 +721,23 @@ void build_wt(Index& ix) {
       ix.kmer_k = K;
     }
   }
+  // flat occ directory for the batched count (sigma <= 8; HKCSA_OCC=0: WT walks, for A/B)
+  static const bool occ_env = !getenv("HKCSA_OCC") || atoi(getenv("HKCSA_OCC")) != 0;
+  ix.occ_ok = false;
+  if (occ_env && sigma >= 2 && sigma <= 8) {
+    const uint64_t nl = n / OC_S + 1, nsb = ceil_div(nl, (uint64_t)OC_LPS);
+    ix.occ_lines.ensure(nl * 64 + 64);
+    ix.occ_sb.ensure(nsb * 64 + 64);   // [8 codes][nsb]
+    TimedLaunch t(ix.timer, "fm_occ_lines", (double)n * (1 + 0.5));
+    k_occ_lines<<<(unsigned)nsb, 256, 0, s>>>(ix.bwt.as<uint8_t>(), n, ix.wt_code.as<int16_t>(), nl,
+                                             ix.occ_lines.as<uint4>(), ix.occ_sb.as<uint64_t>());
+    HK_HIP(hipGetLastError());
+    for (int c = 0; c < 8; ++c)   // per code, the superblocks' exclusive prefix (in place)
+      scan_exclusive_u64(ix.sw, ix.occ_sb.as<uint64_t>() + (uint64_t)c * nsb, ix.occ_sb.as<uint64_t>() + (uint64_t)c * nsb,
+                         nsb, false, s);
+    ix.occ_nsb = nsb;
+    ix.occ_ok = true;
+  }
   HK_HIP(hipStreamSynchronize(s));
   ix.have_wt = true;
 }
@@ -631,7 +748,11 @@ void query_count(Index& ix, const uint8_t* d_pats, const uint64_t* d_offs, uint6
   if (!P) return;
   TimedLaunch t(ix.timer, "fm_count", 0.0);
   const ulonglong2* km = ix.kmer_k ? ix.kmer.as<ulonglong2>() : nullptr;
-  if (ix.sigma <= 16)
+  if (ix.occ_ok)
+    k_count<16, true><<<grid_for(P, 256, 65535), 256, 0, ix.stream>>>(ix.view(), d_pats, d_offs, P, d_lr, d_cnt, km,
+                                                                       ix.kmer_k, ix.occ_lines.as<uint4>(),
+                                                                       ix.occ_sb.as<uint64_t>(), ix.occ_nsb);
+  else if (ix.sigma <= 16)
     k_count<16><<<grid_for(P, 256, 65535), 256, 0, ix.stream>>>(ix.view(), d_pats, d_offs, P, d_lr, d_cnt, km,
                                                                  ix.kmer_k);
   else
