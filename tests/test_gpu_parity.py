@@ -289,6 +289,65 @@ def test_full_size_config3_sigma256_1GiB(hk):
     dev.close()
 
 
+def test_wt_and_count_beyond_4gib(hk):
+    """n > 2^32, as in the replicated index every rank builds after an N >= 4 sharded build: the WT
+    rank against host prefix counts (streamed), and the batched count (k-mer table + flat occ
+    directory) against a host backward search driven by the WT rank (csa/enhanced_fm_index.py:21-40).
+    The sequence itself stands in for the BWT (hkcsa_use_text_as_bwt)."""
+    n = (1 << 32) + (1 << 28) + 1
+    dev = hk.DeviceIndex.synthetic(n, b"ACGT", seed=77)
+    dev.use_text_as_bwt()
+    dev.build_wt()
+    rng = np.random.default_rng(7)
+    idx = np.concatenate([rng.integers(0, n + 1, size=40), [0, (1 << 32) - 1, 1 << 32, (1 << 32) + 1, n - 1, n]])
+    idx = np.sort(idx.astype(np.uint64))
+    syms = np.frombuffer(b"$ACGTx", dtype=np.uint8)
+    want = np.zeros((len(idx), len(syms)), dtype=np.uint64)
+    run = np.zeros(256, dtype=np.uint64)
+    chunk, lo, j = 1 << 28, 0, 0
+    while lo < n and j < len(idx):
+        hi = min(n, lo + chunk)
+        part = dev.text(lo, hi)
+        while j < len(idx) and int(idx[j]) <= hi:
+            k = int(idx[j]) - lo
+            want[j] = (run + np.bincount(part[:k], minlength=256).astype(np.uint64))[syms]
+            j += 1
+        run += np.bincount(part, minlength=256).astype(np.uint64)
+        lo = hi
+    cs = np.repeat(syms[None, :], len(idx), axis=0).reshape(-1)
+    got = dev.rank(cs, np.repeat(idx, len(syms))).reshape(len(idx), len(syms))
+    assert np.array_equal(got, want)
+    # batched count vs the step-by-step search over the WT rank
+    tail = dev.text(n - (1 << 20), n)
+    pats = [tail[s:s + m].tobytes() for s, m in zip(rng.integers(0, len(tail) - 24, size=300),
+                                                  rng.integers(1, 22, size=300))]
+    pats += [bytes(rng.choice(np.frombuffer(b"ACGT", np.uint8), size=m)) for m in (8, 9, 12, 16, 20)]
+    pats += [b"", b"$", b"ACGTx", b"T" * 12]
+    C = dev.C()
+    P = len(pats)
+    lo_ = np.zeros(P, dtype=np.int64)
+    hi_ = np.full(P, n - 1, dtype=np.int64)
+    alive = np.ones(P, dtype=bool)
+    for k in range(max(len(p) for p in pats)):
+        sel = np.array([alive[i] and len(pats[i]) > k for i in range(P)])
+        if not sel.any():
+            break
+        ii = np.nonzero(sel)[0]
+        c = np.array([pats[i][len(pats[i]) - 1 - k] for i in ii], dtype=np.uint8)
+        rl = dev.rank(c, lo_[ii].astype(np.uint64)).astype(np.int64)
+        rr = dev.rank(c, (hi_[ii] + 1).astype(np.uint64)).astype(np.int64)
+        cb = C[c].astype(np.int64)
+        present = np.isin(c, np.frombuffer(b"$ACGT", np.uint8))
+        nl = np.where(present, cb + rl, 0)
+        nr = np.where(present, cb + rr - 1, -1)
+        dead = nl > nr
+        lo_[ii], hi_[ii] = nl, nr
+        alive[ii[dead]] = False
+    exp = np.stack([np.where(alive, lo_, -1), np.where(alive, hi_, -1)], axis=1)
+    assert np.array_equal(dev.count_ranges(pats), exp)
+    dev.close()
+
+
 @pytest.mark.parametrize("nranks,flags,alpha", [(2, 0, b"ACGT"), (3, 0, b"ACGT"), (2, 1, b"ACGT"), (4, 1, b"ACGT"),
                                                (4, 3, b"ACGT"), (5, 0, bytes(range(256))), (3, 0, b"ab"),
                                                (7, 0, b"AC$GT"), (6, 1, bytes(range(0x20, 0x7F))),
