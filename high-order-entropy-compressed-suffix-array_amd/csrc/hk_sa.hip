@@ -343,6 +343,63 @@ __global__ __launch_bounds__(256) void k_refine_keys(const V* __restrict__ P, co
   }
 }
 
+// Segmented sort of a refinement round's keys: the tied suffixes are listed group by group (G
+// ascending, each group contiguous) and only the order inside a group matters, so the thread of a
+// group's head sorts a group of <= SEG_MAX members in registers (bitonic network over 16, padded with
+// ~0 keys) in place; a larger group raises *big and the round takes the global radix sort instead.
+// Equal keys may swap (they stay tied, and their slots are reassigned by the next round).
+constexpr int SEG_MAX = 16;
+
+template <typename V>
+__global__ __launch_bounds__(256) void k_seg_sort16(uint64_t* __restrict__ keys, V* __restrict__ vals,
+                                                    const uint32_t* __restrict__ G, uint64_t A,
+                                                    unsigned int* __restrict__ big) {
+  for (uint64_t a = (uint64_t)blockIdx.x * 256 + threadIdx.x; a < A; a += (uint64_t)gridDim.x * 256) {
+    const uint32_t g = G[a];
+    if (a > 0 && G[a - 1] == g) continue;   // not a head
+    uint32_t sz = 1;
+    while (sz <= SEG_MAX && a + sz < A && G[a + sz] == g) ++sz;
+    if (sz > SEG_MAX) {
+      atomicOr(big, 1u);
+      continue;
+    }
+    if (sz == 1) continue;
+    uint64_t k[SEG_MAX];
+    V v[SEG_MAX];
+#pragma unroll
+    for (int i = 0; i < SEG_MAX; ++i) {
+      k[i] = (uint32_t)i < sz ? keys[a + i] : ~0ull;
+      v[i] = (uint32_t)i < sz ? vals[a + i] : (V)0;
+    }
+#pragma unroll
+    for (int size = 2; size <= SEG_MAX; size <<= 1) {
+#pragma unroll
+      for (int stride = size >> 1; stride > 0; stride >>= 1) {
+#pragma unroll
+        for (int i = 0; i < SEG_MAX; ++i) {
+          const int j = i ^ stride;
+          if (j > i) {
+            const bool up = (i & size) == 0;
+            const bool sw = up ? k[i] > k[j] : k[i] < k[j];
+            const uint64_t ki = k[i], kj = k[j];
+            const V vi = v[i], vj = v[j];
+            k[i] = sw ? kj : ki;
+            k[j] = sw ? ki : kj;
+            v[i] = sw ? vj : vi;
+            v[j] = sw ? vi : vj;
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < SEG_MAX; ++i)
+      if ((uint32_t)i < sz) {
+        keys[a + i] = k[i];
+        vals[a + i] = v[i];
+      }
+  }
+}
+
 // ------------------------------------------------------------- prefix doubling
 // ISA values are global SA slots (slice offset lo + slot in the slice).  Every member of a tied
 // group carries the slot of the group's head, so ISA is an order-consistent K-order rank:
@@ -794,9 +851,28 @@ void refine_loop(Index& ix, const KeyGeom& kg, int cur, uint64_t A, uint64_t gro
                                                    vp[0], s_start, nS, d_srank);
       HK_HIP(hipGetLastError());
     }
-    const int sl = radix_sort_pairs<V>(ix.sw, ix.timer, kp, vp, 0, A, 0, 64, false, s);
-    ix.info[0] += ix.sw.passes_run;
-    ix.info[1] += ix.sw.passes_skipped;
+    // groups of <= SEG_MAX members sorted in place; the global radix sort only when a group is larger
+    // (HKCSA_SEGSORT=0: always the radix sort, for A/B)
+    static const bool seg_env = !getenv("HKCSA_SEGSORT") || atoi(getenv("HKCSA_SEGSORT")) != 0;
+    int sl = -1;
+    if (seg_env) {
+      unsigned int* d_big = reinterpret_cast<unsigned int*>(ix.small.as<uint8_t>() + 4356);   // small+4356: flag
+      unsigned int h_big = 0;
+      HK_HIP(hipMemsetAsync(d_big, 0, 4, s));
+      {
+        TimedLaunch tm(ix.timer, "sa_refine_segsort", (double)A * (2 * 8 + 2 * sizeof(V) + 4));
+        k_seg_sort16<V><<<grid_for(A), 256, 0, s>>>(kp[0], vp[0], ix.act[cur][2].as<uint32_t>(), A, d_big);
+        HK_HIP(hipGetLastError());
+      }
+      HK_HIP(hipMemcpyAsync(&h_big, d_big, 4, hipMemcpyDeviceToHost, s));
+      HK_HIP(hipStreamSynchronize(s));
+      if (!h_big) sl = 0;
+    }
+    if (sl < 0) {
+      sl = radix_sort_pairs<V>(ix.sw, ix.timer, kp, vp, 0, A, 0, 64, false, s);
+      ix.info[0] += ix.sw.passes_run;
+      ix.info[1] += ix.sw.passes_skipped;
+    }
     auto r = refine_step<V>(ix, kg, kp[sl], vp[sl], ix.act[cur][1].as<uint32_t>(), A, 0, false, true,
                             ix.act[cur ^ 1][0].as<V>(), ix.act[cur ^ 1][1].as<uint32_t>(),
                             ix.act[cur ^ 1][2].as<uint32_t>(), ix.head_slot.as<uint32_t>());

@@ -1,26 +1,10 @@
 #!/bin/bash
-# A/B of bench.py (1 GiB sigma=4, SA+BWT steps) under environment variants: each argument is one
-# variant ("VAR=1 VAR2=x" or "-" for none).  TESTS=1 runs the GPU suite first; TRACE=1 adds the
-# bucket-sort phase stamps of each variant.
-cd "$GRAFT_REPO_ROOT" || exit 1
-mkdir -p gpurun_out
-if [ -n "$TESTS" ]; then
-  timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/gputest.log 2>&1 || { tail -40 gpurun_out/gputest.log; exit 1; }
-  tail -2 gpurun_out/gputest.log
-fi
-i=0
-for v in "$@"; do
-  i=$((i+1))
-  [ "$v" = "-" ] && v=""
-  env $v timeout -k 10 300 python3 bench.py --steps 10 --warmup 2 --no-legs --no-cpu-baseline ${BARGS} --no-pcie > gpurun_out/abv_$i.json 2> gpurun_out/abv_$i.err || { echo "variant $i failed"; tail gpurun_out/abv_$i.err; exit 1; }
-  python3 - "$v" gpurun_out/abv_$i.json <<'PY'
-import json, sys
-d = json.load(open(sys.argv[2])); r = d['roofline']
-st = {k: v['ms'] / v['launches'] for k, v in d['detail']['stages_ms_total'].items()}
-print(f"[{sys.argv[1] or 'default'}] {d['ms_per_step']} ms/step", {k: round(v, 3) for k, v in st.items() if v > 0.2},
-      "wt", d['detail']['wt_build_ms'], "loc/s", d['locate_patterns_per_s'])
-PY
-  if [ -n "$TRACE" ]; then
-    env $v HKCSA_BS_TRACE=1 timeout -k 10 300 python3 bench.py --steps 1 --warmup 0 --no-legs --no-cpu-baseline --patterns 0 ${BARGS} 2>&1 >/dev/null | grep trace
-  fi
+# Parity (everything but the sharded cases unless K is set), then the 1 GiB bench with an env toggle
+# on / off twice: AB_VAR=NAME.
+cd "$GRAFT_REPO_ROOT" && mkdir -p gpurun_out && export TMPDIR=/tmp
+timeout -k 10 500 python -u -m pytest tests/test_gpu_bucket.py tests/test_gpu_parity.py tests/test_gpu_dropin.py -m gpu -x -q --timeout 160 --timeout-method thread -k "${K:-not shard}" > gpurun_out/ab_tests.log 2>&1 || { tail -30 gpurun_out/ab_tests.log; exit 1; }
+tail -2 gpurun_out/ab_tests.log
+for v in 1 0 1 0; do
+  env $AB_VAR=$v timeout -k 10 300 python3 bench.py --steps 10 --warmup 2 --no-legs --no-cpu-baseline --no-pcie > gpurun_out/ab_$v.json 2> gpurun_out/ab_$v.err || { tail -5 gpurun_out/ab_$v.err; exit 1; }
+  python3 -c "import json; d=json.load(open('gpurun_out/ab_$v.json')); st=d['detail']['stages_ms_total']; print('$AB_VAR=$v', d['ms_per_step'], {k: round(v['ms']/d['steps'],3) for k, v in st.items() if not k.startswith('radix_part') and k not in ('sa_bucket_sort','byte_hist','sa_bucket_hist')})"
 done
