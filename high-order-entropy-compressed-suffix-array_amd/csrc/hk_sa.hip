@@ -72,44 +72,48 @@ __device__ __forceinline__ uint64_t blk_excl_max(uint64_t v, uint64_t* red) {
 }
 
 // ------------------------------------------------------------- alphabet
-// Each wave keeps BHC copies of the 256 counters (lane l adds to copy l % BHC, rows 257 apart so the
-// copies of one byte sit in different banks): with one copy per wave a small alphabet (DNA: 4 bytes)
-// sent every lane's atomic to the same few addresses (79 % of the LDS cycles were conflicts,
-// profiles/r2_sq_counters.json).
-constexpr int BHC = 8;
+// One counter copy per lane index (64 per workgroup, shared by the 4 waves' lanes of that index), u16
+// pairs with rows 129 words apart, so the lanes adding the same byte hit 64 different banks: no
+// contention at all (8 copies per wave left 77 % of the LDS cycles in conflicts for DNA,
+// profiles/r2c_sq_counters.json).  The grid keeps every copy below 2^16 (byte_hist_range).
+constexpr int BH_ROW = 129;
 __global__ __launch_bounds__(256) void k_byte_hist(const uint8_t* __restrict__ t, uint64_t n,
                                                    unsigned long long* __restrict__ hist) {
-  __shared__ uint32_t h[4 * BHC * 257];
-  for (int i = threadIdx.x; i < 4 * BHC * 257; i += 256) h[i] = 0;
+  __shared__ uint32_t h[64 * BH_ROW];
+  for (int i = threadIdx.x; i < 64 * BH_ROW; i += 256) h[i] = 0;
   __syncthreads();
-  uint32_t* mine = h + ((threadIdx.x >> 6) * BHC + (threadIdx.x & (BHC - 1))) * 257;
+  uint32_t* mine = h + (threadIdx.x & 63) * BH_ROW;
+  auto add4 = [&](uint32_t w) {
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      const uint32_t x = (w >> (8 * b)) & 255u;
+      atomicAdd(&mine[x >> 1], 1u << (16 * (x & 1u)));
+    }
+  };
   const uint64_t nv = n / 16;
   const uint4* t4 = reinterpret_cast<const uint4*>(t);
   const uint64_t stride = (uint64_t)gridDim.x * 256;
   uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
   for (; i + stride < nv; i += 2 * stride) {   // two 16-byte loads in flight per lane
     const uint4 v0 = t4[i], v1 = t4[i + stride];
-    const uint32_t w[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
-#pragma unroll
-    for (int q = 0; q < 8; ++q)
-#pragma unroll
-      for (int b = 0; b < 4; ++b) atomicAdd(&mine[(w[q] >> (8 * b)) & 255], 1u);
+    add4(v0.x); add4(v0.y); add4(v0.z); add4(v0.w);
+    add4(v1.x); add4(v1.y); add4(v1.z); add4(v1.w);
   }
   for (; i < nv; i += stride) {
     const uint4 v = t4[i];
-    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-#pragma unroll
-      for (int b = 0; b < 4; ++b) atomicAdd(&mine[(w[q] >> (8 * b)) & 255], 1u);
+    add4(v.x); add4(v.y); add4(v.z); add4(v.w);
   }
   if (blockIdx.x == 0)
-    for (uint64_t j = nv * 16 + threadIdx.x; j < n; j += 256) atomicAdd(&mine[t[j]], 1u);
+    for (uint64_t j = nv * 16 + threadIdx.x; j < n; j += 256) {
+      const uint32_t x = t[j];
+      atomicAdd(&mine[x >> 1], 1u << (16 * (x & 1u)));
+    }
   __syncthreads();
+  const uint32_t b = threadIdx.x, sh = 16u * (b & 1u);
   uint32_t c = 0;
 #pragma unroll 8
-  for (int r = 0; r < 4 * BHC; ++r) c += h[r * 257 + threadIdx.x];
-  if (c) atomicAdd(&hist[threadIdx.x], (unsigned long long)c);
+  for (int r = 0; r < 64; ++r) c += (h[r * BH_ROW + (b >> 1)] >> sh) & 0xFFFFu;
+  if (c) atomicAdd(&hist[b], (unsigned long long)c);
 }
 
 // ------------------------------------------------------------- keys
@@ -1023,7 +1027,10 @@ void byte_hist_range(Index& ix, uint64_t lo, uint64_t hi, unsigned long long* d_
   HK_HIP(hipMemsetAsync(d_out, 0, 256 * 8, s));
   if (hi <= lo) return;
   TimedLaunch t(ix.timer, "byte_hist", (double)(hi - lo));
-  k_byte_hist<<<grid_for((hi - lo) / 16 + 1, 256, 2048), 256, 0, s>>>(ix.text.as<uint8_t>() + lo, hi - lo, d_out);
+  // every counter copy (4 lanes of the workgroup) stays below 2^16: <= 8192 bytes per lane
+  const uint64_t cap = std::max<uint64_t>(2048, ceil_div(hi - lo, (uint64_t)256 * 8192));
+  k_byte_hist<<<(unsigned)std::min<uint64_t>(ceil_div((hi - lo) / 16 + 1, (uint64_t)256), cap), 256, 0, s>>>(
+      ix.text.as<uint8_t>() + lo, hi - lo, d_out);
   HK_HIP(hipGetLastError());
 }
 
