@@ -782,19 +782,26 @@ KeyGeom key_geometry(Index& ix, bool with_prev) {
 // device copies of the LUTs: small+2048 = lut (u16[256]), small+3072 = inv (u8[512])
 void upload_geometry(Index& ix, const KeyGeom& kg) {
   ix.small.ensure(8192);
-  HK_HIP(hipMemcpyAsync(ix.small.as<uint8_t>() + 2048, kg.lut, 512, hipMemcpyHostToDevice, ix.stream));
-  HK_HIP(hipMemcpyAsync(ix.small.as<uint8_t>() + 3072, kg.inv, 512, hipMemcpyHostToDevice, ix.stream));
   if (kg.keyed) {   // small+2560 = lutk, +4608 = lutp (u16[256]), +3584 = skey (u64[72]), +7168 = srank (u32[72])
-    HK_HIP(hipMemcpyAsync(ix.small.as<uint8_t>() + 2560, kg.lutk, 512, hipMemcpyHostToDevice, ix.stream));
-    HK_HIP(hipMemcpyAsync(ix.small.as<uint8_t>() + 4608, kg.lutp, 512, hipMemcpyHostToDevice, ix.stream));
-    HK_HIP(hipMemcpyAsync(ix.small.as<uint8_t>() + 3584, kg.skey, sizeof(kg.skey), hipMemcpyHostToDevice,
-                          ix.stream));
-    HK_HIP(hipMemcpyAsync(ix.small.as<uint8_t>() + 7168, kg.srank, sizeof(kg.srank), hipMemcpyHostToDevice,
-                          ix.stream));
-    HK_HIP(hipMemcpyAsync(ix.small.as<uint8_t>() + 7456, kg.k2d, sizeof(kg.k2d), hipMemcpyHostToDevice,
-                          ix.stream));   // +7456 = k2d (u16[256])
+    // +7456 = k2d (u16[256]); the ranges in between (4096: locate / fallback counters, 5120: digit
+    // histogram) are reset by their users before use.  Staged in pinned memory: one upload.
+    ix.small_host.ensure(8192);
+    uint8_t* hs = ix.small_host.as<uint8_t>();
+    memcpy(hs + 2048, kg.lut, 512);
+    memcpy(hs + 3072, kg.inv, 512);
+    memcpy(hs + 2560, kg.lutk, 512);
+    memcpy(hs + 4608, kg.lutp, 512);
+    memcpy(hs + 3584, kg.skey, sizeof(kg.skey));
+    memcpy(hs + 7168, kg.srank, sizeof(kg.srank));
+    memcpy(hs + 7456, kg.k2d, sizeof(kg.k2d));
+    static_assert(7456 + sizeof(kg.k2d) <= 8192, "geometry tables fit the small buffer");
+    HK_HIP(hipMemcpyAsync(ix.small.as<uint8_t>() + 2048, hs + 2048, 7456 + sizeof(kg.k2d) - 2048,
+                          hipMemcpyHostToDevice, ix.stream));
+  } else {
+    HK_HIP(hipMemcpyAsync(ix.small.as<uint8_t>() + 2048, kg.lut, 512, hipMemcpyHostToDevice, ix.stream));
+    HK_HIP(hipMemcpyAsync(ix.small.as<uint8_t>() + 3072, kg.inv, 512, hipMemcpyHostToDevice, ix.stream));
   }
-  HK_HIP(hipStreamSynchronize(ix.stream));   // kg may be a host temporary
+  HK_HIP(hipStreamSynchronize(ix.stream));   // kg may be a host temporary; the staging is reused
 }
 
 template <typename V>
