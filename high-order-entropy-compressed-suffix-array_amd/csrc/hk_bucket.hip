@@ -1808,9 +1808,12 @@ KeyGeom key_geometry_keyed(Index& ix, int reserve) {
 
   // the last bytes of T' (short suffixes)
   const uint64_t nt = std::min<uint64_t>(n, 70);
-  uint8_t tail[72] = {0};
-  HK_HIP(hipMemcpyAsync(tail, ix.text.as<uint8_t>() + (n - nt), nt, hipMemcpyDeviceToHost, ix.stream));
-  HK_HIP(hipStreamSynchronize(ix.stream));
+  if (!ix.tail_valid) {   // alphabet set without compute_alphabet (sharded all-reduce): read it here
+    HK_HIP(hipMemcpyAsync(ix.tail, ix.text.as<uint8_t>() + (n - nt), nt, hipMemcpyDeviceToHost, ix.stream));
+    HK_HIP(hipStreamSynchronize(ix.stream));
+    ix.tail_valid = true;
+  }
+  const uint8_t* tail = ix.tail;
   const uint8_t term = tail[nt - 1];
   const bool unkeyed = ix.byte_hist[term] == 1 && ix.sigma >= 2;
   int codek[256];

@@ -77,6 +77,8 @@ struct Index {
   // alphabet
   bool have_alpha = false;
   uint64_t byte_hist[256] = {0};
+  uint8_t tail[72] = {0};      // the last min(n, 70) bytes of T' (short-suffix keys), read with the histogram
+  bool tail_valid = false;
   int sigma = 0;
   uint8_t syms[256] = {0};
   int16_t code_of[256];

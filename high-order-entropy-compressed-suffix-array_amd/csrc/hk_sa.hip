@@ -1068,7 +1068,11 @@ void compute_alphabet(Index& ix) {
   byte_hist_range(ix, 0, ix.n, ix.small.as<unsigned long long>());
   uint64_t h[256];
   HK_HIP(hipMemcpyAsync(h, ix.small.p, 256 * 8, hipMemcpyDeviceToHost, s));
+  // the text's last bytes (the keyed geometry's short suffixes) in the same round trip
+  const uint64_t nt = std::min<uint64_t>(ix.n, 70);
+  if (nt) HK_HIP(hipMemcpyAsync(ix.tail, ix.text.as<uint8_t>() + (ix.n - nt), nt, hipMemcpyDeviceToHost, s));
   HK_HIP(hipStreamSynchronize(s));
+  ix.tail_valid = nt > 0;
   set_alphabet(ix, h);
 }
 
