@@ -699,14 +699,15 @@ void build_wt(Index& ix) {
       }
     }
   }
-  // k-mer table for the batched count: K = the most symbols with sigma^K <= 2^19 entries (6 MiB of
-  // (l, r) pairs, cache-resident), at most 12 (HKCSA_KMER=0: no table, for A/B)
+  // k-mer table for the batched count: K = the most symbols with sigma^K <= 2^20 entries (<= 16 MiB
+  // of (l, r) pairs, MALL-resident; DNA + '$': K = 8, printable: 3, bytes: 2), at most 12
+  // (HKCSA_KMER=0: no table, for A/B)
   static const bool kmer_env = !getenv("HKCSA_KMER") || atoi(getenv("HKCSA_KMER")) != 0;
   ix.kmer_k = 0;
   if (kmer_env && L > 0 && sigma >= 2) {
     int K = 0;
     uint64_t tot = 1;
-    while (K < 12 && tot * (uint64_t)sigma <= (1ull << 19)) {
+    while (K < 12 && tot * (uint64_t)sigma <= (1ull << 20)) {
       tot *= (uint64_t)sigma;
       ++K;
     }
