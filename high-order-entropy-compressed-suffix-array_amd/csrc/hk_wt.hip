@@ -466,9 +466,13 @@ __global__ __launch_bounds__(256) void k_count(WtView v, const uint8_t* __restri
 // k-mer table: entry idx (the codes c_0 .. c_{K-1} of a K-symbol string, c_0 most significant in
 // radix sigma) = the state after the backward search of that string from the full range; an empty
 // state is stored as (1, 0)
-template <int NC>
-__global__ __launch_bounds__(256) void k_kmer_table(WtView v, int K, uint64_t total, ulonglong2* __restrict__ tab) {
+template <int NC, bool FLAT = false>
+__global__ __launch_bounds__(256) void k_kmer_table(WtView v, int K, uint64_t total, ulonglong2* __restrict__ tab,
+                                                    const uint4* __restrict__ ol = nullptr,
+                                                    const uint64_t* __restrict__ osb = nullptr, uint64_t onsb = 0) {
   __shared__ QSharedT<NC> q;
+  __shared__ uint64_t CC[8];
+  if (FLAT && threadIdx.x < 8) CC[threadIdx.x] = threadIdx.x < (unsigned)v.sigma ? v.Ccode[threadIdx.x] : 0;
   load_qshared(q, v);
   for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (uint64_t)gridDim.x * 256) {
     uint64_t xl = 0, xr = v.n, x = i;
@@ -476,7 +480,12 @@ __global__ __launch_bounds__(256) void k_kmer_table(WtView v, int K, uint64_t to
     for (int j = 0; j < K; ++j) {   // the last symbol (least significant digit) first
       const int c = (int)(x % (uint64_t)v.sigma);
       x /= (uint64_t)v.sigma;
-      lf_pair(q, c, xl, xr);
+      if (FLAT) {
+        xl = CC[c] + occ_rank(ol, osb, onsb, c, xl);
+        xr = CC[c] + occ_rank(ol, osb, onsb, c, xr);
+      } else {
+        lf_pair(q, c, xl, xr);
+      }
       if (xl >= xr) { ok = false; break; }
     }
     tab[i] = ok ? make_ulonglong2(xl, xr) : make_ulonglong2(1, 0);
@@ -699,29 +708,6 @@ void build_wt(Index& ix) {
       }
     }
   }
-  // k-mer table for the batched count: K = the most symbols with sigma^K <= 2^20 entries (<= 16 MiB
-  // of (l, r) pairs, MALL-resident; DNA + '$': K = 8, printable: 3, bytes: 2), at most 12
-  // (HKCSA_KMER=0: no table, for A/B)
-  static const bool kmer_env = !getenv("HKCSA_KMER") || atoi(getenv("HKCSA_KMER")) != 0;
-  ix.kmer_k = 0;
-  if (kmer_env && L > 0 && sigma >= 2) {
-    int K = 0;
-    uint64_t tot = 1;
-    while (K < 12 && tot * (uint64_t)sigma <= (1ull << 20)) {
-      tot *= (uint64_t)sigma;
-      ++K;
-    }
-    if (K >= 2) {
-      ix.kmer.ensure(tot * 16 + 16);
-      TimedLaunch t(ix.timer, "fm_kmer_table", (double)tot * 16);
-      if (sigma <= 16)
-        k_kmer_table<16><<<grid_for(tot, 256, 8192), 256, 0, s>>>(ix.view(), K, tot, ix.kmer.as<ulonglong2>());
-      else
-        k_kmer_table<256><<<grid_for(tot, 256, 8192), 256, 0, s>>>(ix.view(), K, tot, ix.kmer.as<ulonglong2>());
-      HK_HIP(hipGetLastError());
-      ix.kmer_k = K;
-    }
-  }
   // flat occ directory for the batched count (sigma <= 8; HKCSA_OCC=0: WT walks, for A/B)
   static const bool occ_env = !getenv("HKCSA_OCC") || atoi(getenv("HKCSA_OCC")) != 0;
   ix.occ_ok = false;
@@ -738,6 +724,34 @@ void build_wt(Index& ix) {
                          nsb, false, s);
     ix.occ_nsb = nsb;
     ix.occ_ok = true;
+  }
+  // k-mer table for the batched count: K = the most symbols with sigma^K <= 2^20 entries (<= 16 MiB
+  // of (l, r) pairs, MALL-resident; DNA + '$': K = 8, printable: 3, bytes: 2), at most 12
+  // (HKCSA_KMER=0: no table, for A/B)
+  static const bool kmer_env = !getenv("HKCSA_KMER") || atoi(getenv("HKCSA_KMER")) != 0;
+  ix.kmer_k = 0;
+  if (kmer_env && L > 0 && sigma >= 2) {
+    int K = 0;
+    uint64_t tot = 1;
+    const uint64_t cap = ix.occ_ok ? (1ull << 21) : (1ull << 20);   // the directory builds it cheaply
+    while (K < 12 && tot * (uint64_t)sigma <= cap) {
+      tot *= (uint64_t)sigma;
+      ++K;
+    }
+    if (K >= 2) {
+      ix.kmer.ensure(tot * 16 + 16);
+      TimedLaunch t(ix.timer, "fm_kmer_table", (double)tot * 16);
+      if (ix.occ_ok)
+        k_kmer_table<16, true><<<grid_for(tot, 256, 8192), 256, 0, s>>>(ix.view(), K, tot, ix.kmer.as<ulonglong2>(),
+                                                                       ix.occ_lines.as<uint4>(),
+                                                                       ix.occ_sb.as<uint64_t>(), ix.occ_nsb);
+      else if (sigma <= 16)
+        k_kmer_table<16><<<grid_for(tot, 256, 8192), 256, 0, s>>>(ix.view(), K, tot, ix.kmer.as<ulonglong2>());
+      else
+        k_kmer_table<256><<<grid_for(tot, 256, 8192), 256, 0, s>>>(ix.view(), K, tot, ix.kmer.as<ulonglong2>());
+      HK_HIP(hipGetLastError());
+      ix.kmer_k = K;
+    }
   }
   HK_HIP(hipStreamSynchronize(s));
   ix.have_wt = true;

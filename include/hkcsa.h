@@ -93,7 +93,7 @@ int hkcsa_build_bwt(hkcsa_index* ix);
  * Replaces build_count (utils/utils.py:16-24), build_occ (utils/utils.py:26-32)
  * as the rank structure, and WaveletTree.build_tree (csa/wavelet_tree.py:72-100).
  * Also builds the batched count's accelerators: the backward-search state of every
- * K-symbol string (sigma^K <= 2^20) and, for sigma <= 8, a flat occ directory of the
+ * K-symbol string (sigma^K <= 2^20, 2^21 for sigma <= 8) and, for sigma <= 8, a flat occ directory of the
  * BWT (one 64-B line per 128 symbols); both give results identical to the WT walk. */
 int hkcsa_build_wt(hkcsa_index* ix);
 /* SA + BWT + WT in one call (EnhancedFMIndex.__init__, csa/enhanced_fm_index.py:8-13). */
