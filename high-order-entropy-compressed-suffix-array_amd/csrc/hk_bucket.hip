@@ -477,7 +477,7 @@ struct CpShared {
 // position, instead of a key and a value plane.  Pass A (NB = 512) packs after ranking and stages
 // each slot's digit (low 8 bits in sd, the 9th from the slot's side of digit 256's start); pass B
 // (NB = 256, shift counts the position bits) moves the records unchanged.
-template <int MODE, int LB, int NB = 256, int T = CP_T, bool PK = false>
+template <int MODE, int LB, int NB = 256, int T = CP_T, bool PK = false, bool CS = true>
 __global__ __launch_bounds__(T, T == 1024 ? 1 : 2) void k_cpart(const uint64_t* __restrict__ kin, const uint32_t* __restrict__ vin,
                                                    uint64_t* __restrict__ kout, uint32_t* __restrict__ vout,
                                                    uint64_t n, int shift, uint64_t kbias,
@@ -544,7 +544,10 @@ __global__ __launch_bounds__(T, T == 1024 ? 1 : 2) void k_cpart(const uint64_t* 
     __syncthreads();   // gb is reused below
   }
   if (tid < NB) sh.cnt[tid] = 0;
-  const uint32_t s0 = wv * WSPAN + lane;   // item k of this thread is tile slot s0 + 64 k
+  const uint32_t s0 = wv * WSPAN + lane;   // item k of this thread is tile slot s0 + 64 k ...
+  // ... or, packed pass A over radix-2^2 codes (HKCSA_CONSEC=0: lane-strided), slot 16 tid + k
+  constexpr bool CONSEC = CS && MODE == 0 && PK && LB == 2 && CP_I == 16;
+  const uint32_t c0 = CONSEC ? 16u * tid : s0, cst = CONSEC ? 1u : 64u;
   uint64_t key[CP_I];
   uint32_t val[CP_I];
   if (FT) {
@@ -554,10 +557,13 @@ __global__ __launch_bounds__(T, T == 1024 ? 1 : 2) void k_cpart(const uint64_t* 
     }
     if (tid < 72) sh.SK[tid] = src.skey[tid];
     __syncthreads();
-    text_keys<T, CP_I, LB>(key, src, n, tbase, tbase + (uint64_t)wv * WSPAN, lane, sh.stage.codes,
-                              sh.stage.ft.pk, sh.stage.ft.raw, &sh.prev0, sh.L, sh.LP, sh.SK);
+    if constexpr (CONSEC)
+      text_keys_consec2<T>(key, src, n, tbase, sh.stage.ft.pk, &sh.prev0, sh.L, sh.LP, sh.SK);
+    else
+      text_keys<T, CP_I, LB>(key, src, n, tbase, tbase + (uint64_t)wv * WSPAN, lane, sh.stage.codes,
+                             sh.stage.ft.pk, sh.stage.ft.raw, &sh.prev0, sh.L, sh.LP, sh.SK);
 #pragma unroll
-    for (int k = 0; k < CP_I; ++k) val[k] = (uint32_t)(tbase + s0 + 64u * k);
+    for (int k = 0; k < CP_I; ++k) val[k] = (uint32_t)(tbase + c0 + cst * k);
   } else {
 #pragma unroll
     for (int k = 0; k < CP_I; ++k) key[k] = s0 + 64u * k < tn ? kin[tbase + s0 + 64u * k] : ~0ull;
@@ -571,7 +577,7 @@ __global__ __launch_bounds__(T, T == 1024 ? 1 : 2) void k_cpart(const uint64_t* 
 #pragma unroll
   for (int k = 0; k < CP_I; ++k) {
     const uint32_t d = (uint32_t)((key[k] - kbias) >> shift) & DM;
-    const uint32_t r = s0 + 64u * k < tn ? atomicAdd(&sh.cnt[d], 1u) : 0u;
+    const uint32_t r = c0 + cst * k < tn ? atomicAdd(&sh.cnt[d], 1u) : 0u;
     rk[k] = r | (d << 16);
   }
   if (SD) {   // the record: key bits below the digit, then the position
@@ -597,7 +603,7 @@ __global__ __launch_bounds__(T, T == 1024 ? 1 : 2) void k_cpart(const uint64_t* 
   __syncthreads();
 #pragma unroll
   for (int k = 0; k < CP_I; ++k)
-    if (s0 + 64u * k < tn) {
+    if (c0 + cst * k < tn) {
       const uint32_t f = sh.tst[rk[k] >> 16] + (rk[k] & 0xFFFFu);
       sh.stage.keys[f] = key[k];
       if (SD) sh.sd[f] = (uint8_t)(rk[k] >> 16);
@@ -621,7 +627,7 @@ __global__ __launch_bounds__(T, T == 1024 ? 1 : 2) void k_cpart(const uint64_t* 
   __syncthreads();
 #pragma unroll
   for (int k = 0; k < CP_I; ++k)
-    if (s0 + 64u * k < tn) sh.stage.vals[sh.tst[rk[k] >> 16] + (rk[k] & 0xFFFFu)] = val[k];
+    if (c0 + cst * k < tn) sh.stage.vals[sh.tst[rk[k] >> 16] + (rk[k] & 0xFFFFu)] = val[k];
   __syncthreads();
 #pragma unroll
   for (int i = 0; i < CP_I; ++i) {
@@ -2162,6 +2168,8 @@ int cursor_partition(Index& ix, uint64_t n, int D, int bitlo, uint64_t kbias, co
     const unsigned grid = (unsigned)(8 * ceil_div(nspan, 8u) * (span / CP_TILE));
     // packed: 512-thread tiles, two workgroups per CU (HKCSA_PK_A1024=1: 1024-thread tiles, one per CU)
     static const bool a1024 = getenv("HKCSA_PK_A1024") && atoi(getenv("HKCSA_PK_A1024")) != 0;
+    // consecutive positions per thread in the packed radix-2^2 pass A (HKCSA_CONSEC=0: lane-strided)
+    static const bool consec = !getenv("HKCSA_CONSEC") || atoi(getenv("HKCSA_CONSEC")) != 0;
     const unsigned grid_pk = (unsigned)(8 * ceil_div(nspan, 8u) * (span / (1024 * CP_I)));
     if (packed && a1024 && tks->g.lb == 2)
       k_cpart<0, 2, 512, 1024, true><<<grid_pk, 1024, 0, s>>>(nullptr, nullptr, kp[outA], nullptr, n, bitlo2 + sA, 0,
@@ -2169,9 +2177,13 @@ int cursor_partition(Index& ix, uint64_t n, int D, int bitlo, uint64_t kbias, co
     else if (packed && a1024)
       k_cpart<0, 0, 512, 1024, true><<<grid_pk, 1024, 0, s>>>(nullptr, nullptr, kp[outA], nullptr, n, bitlo2 + sA, 0,
                                                              d_curA, nullptr, nullptr, span, tks2, pk->g.pbits, d_ovf);
-    else if (packed && tks->g.lb == 2)
+    else if (packed && tks->g.lb == 2 && consec)
       k_cpart<0, 2, 512, CP_T, true><<<grid, CP_T, 0, s>>>(nullptr, nullptr, kp[outA], nullptr, n, bitlo2 + sA, 0,
                                                           d_curA, nullptr, nullptr, span, tks2, pk->g.pbits, d_ovf);
+    else if (packed && tks->g.lb == 2)
+      k_cpart<0, 2, 512, CP_T, true, false><<<grid, CP_T, 0, s>>>(nullptr, nullptr, kp[outA], nullptr, n,
+                                                                 bitlo2 + sA, 0, d_curA, nullptr, nullptr, span, tks2,
+                                                                 pk->g.pbits, d_ovf);
     else if (packed)
       k_cpart<0, 0, 512, CP_T, true><<<grid, CP_T, 0, s>>>(nullptr, nullptr, kp[outA], nullptr, n, bitlo2 + sA, 0,
                                                           d_curA, nullptr, nullptr, span, tks2, pk->g.pbits, d_ovf);

@@ -334,4 +334,55 @@ __device__ __forceinline__ void text_keys(uint64_t (&key)[I], const TextKeySrc& 
   }
 }
 
+// Pass A of the packed-record build (radix 2^2 codes, 16 items per thread): item k of thread tid is
+// position tbase + 16 tid + k, so the thread's 16 windows and prev codes all come from the three packed
+// words at its own 16 symbols (plus the word before) with compile-time shifts: 4 LDS reads per thread
+// instead of 5 per key (text_keys' lane-strided items need a fresh 3-word window, a raw byte and a
+// table lookup each).  The prev field is the keyed code straight from the stream (the packed records'
+// prev code: the unique terminal, code 0 in both, precedes only position 0), LP only for the byte
+// before the tile.
+template <int T>
+__device__ __forceinline__ void text_keys_consec2(uint64_t (&key)[16], const TextKeySrc& src, uint64_t n,
+                                                  uint64_t tbase, uint32_t* pk, uint32_t* prev0,
+                                                  const uint16_t* L, const uint16_t* LP, const uint64_t* SK) {
+  constexpr int TILE = T * 16;
+  const uint32_t tid = threadIdx.x;
+  if (tid == 0) *prev0 = src.text[tbase == 0 ? n - 1 : tbase - 1];
+  for (uint32_t c = tid; c < (uint32_t)(TILE + 64) / 32; c += T) {
+    const uint64_t p0 = tbase + 32ull * c;
+    uint4 a = make_uint4(0, 0, 0, 0), b = a;
+    if (p0 < n) {   // T' has 64 readable pad bytes; positions past n only feed short suffixes
+      const uint4* q4 = reinterpret_cast<const uint4*>(src.text + p0);
+      a = q4[0];
+      b = q4[1];
+    }
+    const uint32_t w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+#pragma unroll
+    for (int o = 0; o < 2; ++o) {
+      uint32_t word = 0;
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        const int i = o * 16 + u;
+        word = (word << 2) | (L[(w[i >> 2] >> (8 * (i & 3))) & 255u] & 255u);
+      }
+      pk[c * 2 + o] = word;
+    }
+  }
+  __syncthreads();
+  const uint32_t a = pk[tid], b = pk[tid + 1], c = pk[tid + 2];
+  const uint32_t pw = tid ? pk[tid - 1] : 0u;
+  const uint64_t hi = ((uint64_t)a << 32) | b;
+  const int kbits = src.g.q * 2;
+  const uint64_t j0 = tbase + 16ull * tid;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const uint64_t j = j0 + k;
+    const uint64_t win = k ? (hi << (2 * k)) | (c >> (32 - 2 * k)) : hi;
+    uint64_t sym = kbits >= 64 ? win : win >> (64 - kbits);
+    if (j >= src.g.s_start) sym = j < n ? SK[j - src.g.s_start] : 0;
+    const uint32_t pc = k ? (a >> (32 - 2 * k)) & 3u : (tid ? pw & 3u : LP[*prev0]);
+    key[k] = j < n ? (sym << src.g.pb) | pc : ~0ull;
+  }
+}
+
 }  // namespace hk
