@@ -223,7 +223,10 @@ __device__ __forceinline__ void hist_spans_flush(const uint32_t* H, uint32_t* M,
 // bucket land before the drain (every thread inside one long run of a symbol); any increment that
 // sees a byte at >= 224 raises *ovf, pass A then skips itself and the host recounts exactly with two
 // CB = 16 runs over the bucket halves (HB = 0, 1: only buckets with b >> 16 == HB; HB = -1: all).
-template <int CB, int HB = -1>
+// LBQ/HQ > 0: the code width and window length fixed at compile time (= log2 g.Rk and g.hq; DNA
+// 2/9, bytes 8/3): only the BH_PER + HQ - 1 codes a thread's windows use are mapped, no per-code
+// window tests.
+template <int CB, int HB = -1, int LBQ = 0, int HQ = 0>
 __global__ __launch_bounds__(BH_T, 1) void k_bucket_hist_spans(const uint8_t* __restrict__ t, uint64_t n,
                                                                const uint16_t* __restrict__ lutk,
                                                                const uint64_t* __restrict__ skey, KeyedArgs g,
@@ -263,9 +266,12 @@ __global__ __launch_bounds__(BH_T, 1) void k_bucket_hist_spans(const uint8_t* __
   const uint64_t lim = n < g.s_start ? n : g.s_start;   // positions with a text window
   const uint64_t lo = (uint64_t)blockIdx.x * span;
   const uint64_t hi = lo + span < n ? lo + span : n;
-  const int lb = 31 - __clz((uint32_t)g.Rk);
+  const int lb = LBQ ? LBQ : 31 - __clz((uint32_t)g.Rk);
+  const int hq = HQ ? HQ : g.hq;
+  constexpr int NI = HQ ? BH_PER + HQ - 1 : 2 * BH_PER - 1;
+  static_assert(NI <= 2 * BH_PER, "window past the thread's 32 bytes");
   // the window of hq symbols (hq * lb <= 32 bits); the bucket is its top D bits
-  const int wbits = g.hq * lb, wdrop = wbits - D;
+  const int wbits = hq * lb, wdrop = wbits - D;
   const uint32_t bmask = wbits >= 32 ? ~0u : (1u << wbits) - 1;
   uint4 w0 = make_uint4(0, 0, 0, 0), w1 = w0;
   if (lo + (uint64_t)tid * BH_PER < hi) {
@@ -283,12 +289,13 @@ __global__ __launch_bounds__(BH_T, 1) void k_bucket_hist_spans(const uint8_t* __
     }
     const uint64_t lim2 = lim < hi ? lim : hi;
     if (p0 < lim2) {
+      const bool full = p0 + BH_PER <= lim2;
       uint32_t b = 0;
 #pragma unroll
-      for (int i = 0; i < 2 * BH_PER - 1; ++i) {
+      for (int i = 0; i < NI; ++i) {
         b = ((b << lb) | (L[(wd[i >> 2] >> (8 * (i & 3))) & 255u] & 255u)) & bmask;
-        const int j = i - (g.hq - 1);
-        if (j >= 0 && j < BH_PER && p0 + j < lim2) add(b >> wdrop);
+        const int j = i - (hq - 1);
+        if (j >= 0 && j < BH_PER && (full || p0 + j < lim2)) add(b >> wdrop);
       }
     }
     for (uint64_t p = p0 > lim ? p0 : lim; p < p0 + BH_PER && p < hi; ++p) add((uint32_t)(SK[p - g.s_start] >> bsh));
@@ -2127,13 +2134,20 @@ int cursor_partition(Index& ix, uint64_t n, int D, int bitlo, uint64_t kbias, co
     tks2.g.pb = pk->g.pb2;
   }
   // pre-pass (exact: 2^17 buckets as two u16 runs over the bucket halves, after a u8 overflow)
+  // pre-pass with the code width and window fixed at compile time (HKCSA_HIST_FIXED=0: runtime)
+  static const bool hist_fixed = !getenv("HKCSA_HIST_FIXED") || atoi(getenv("HKCSA_HIST_FIXED")) != 0;
+  auto hist_fixed_enabled = [] { return hist_fixed; };
   auto prepass = [&](bool exact) {
     HK_HIP(hipMemsetAsync(d_drain, 0, (uint64_t)nb * 8, s));
     HK_HIP(hipMemsetAsync(d_ovf, 0, 8, s));
     TimedLaunch t(ix.timer, "sa_bucket_hist", (double)n * (tks ? (exact ? 2 : 1) : 8));
     if (tks && D > 16 && !exact) {   // 2^17 buckets: u8 counters (drained at 128)
-      k_bucket_hist_spans<8><<<nspan, BH_T, 0, s>>>(tks->text, n, tks->lutk, tks->skey, tks->g, bitlo - tks->g.pb, D,
-                                                    sA, d_part, d_drain, d_spanc, span, d_ovf);
+      const int lbk = 31 - __builtin_clz((uint32_t)tks->g.Rk);
+      auto kern = k_bucket_hist_spans<8>;
+      if (hist_fixed_enabled() && lbk == 2 && tks->g.hq == 9) kern = k_bucket_hist_spans<8, -1, 2, 9>;
+      else if (hist_fixed_enabled() && lbk == 8 && tks->g.hq == 3) kern = k_bucket_hist_spans<8, -1, 8, 3>;
+      kern<<<nspan, BH_T, 0, s>>>(tks->text, n, tks->lutk, tks->skey, tks->g, bitlo - tks->g.pb, D, sA, d_part,
+                                  d_drain, d_spanc, span, d_ovf);
     } else if (tks) {
       if (D > 16) {
         k_bucket_hist_spans<16, 0><<<nspan, BH_T, 0, s>>>(tks->text, n, tks->lutk, tks->skey, tks->g,
