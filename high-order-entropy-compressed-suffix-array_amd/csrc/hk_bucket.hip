@@ -1672,10 +1672,17 @@ uint64_t sort_bucket_items(Index& ix, const BucketPlan& plan, const uint64_t* ke
   HK_HIP(hipMemsetAsync(ix.ties_n.p, 0, 8, s));
   const uint64_t nn = plan.items_n.size(), nw = plan.items_w.size();
   ix.bk_items.ensure((nn + nw) * sizeof(uint2) + 16);
-  if (nn) HK_HIP(hipMemcpyAsync(ix.bk_items.p, plan.items_n.data(), nn * sizeof(uint2), hipMemcpyHostToDevice, s));
-  if (nw)
-    HK_HIP(hipMemcpyAsync(ix.bk_items.as<uint2>() + nn, plan.items_w.data(), nw * sizeof(uint2),
-                          hipMemcpyHostToDevice, s));
+  if (nn + nw) {
+    // pinned staging: the copy is queued behind the partition passes without holding the host (the
+    // ~37 us DMA of ~1 MB of items still runs between pass B and the sort).  The same copy on the
+    // auxiliary stream, under pass B, was slower: passes A and B lost 0.1-0.15 ms each beside it.
+    // The previous call's copy is complete (this function ends with a stream synchronize).
+    ix.items_host.ensure((nn + nw) * sizeof(uint2));
+    uint2* const hi = ix.items_host.as<uint2>();
+    if (nn) memcpy(hi, plan.items_n.data(), nn * sizeof(uint2));
+    if (nw) memcpy(hi + nn, plan.items_w.data(), nw * sizeof(uint2));
+    HK_HIP(hipMemcpyAsync(ix.bk_items.p, hi, (nn + nw) * sizeof(uint2), hipMemcpyHostToDevice, s));
+  }
   {
     TimedLaunch t(ix.timer, "sa_bucket_sort", (double)(m - plan.big_total) * (pk ? 8 + 4 + 1 : 8 + 4 + 4 + 1));
     static const bool trace = getenv("HKCSA_BS_TRACE") != nullptr;   // diagnostic phase stamps

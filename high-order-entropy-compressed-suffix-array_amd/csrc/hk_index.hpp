@@ -115,6 +115,7 @@ struct Index {
   DevBuf tile_a, tile_b, tile_c, tile_d, tile_e;
   DevBuf small;                // scratch for totals etc.
   HostBuf small_host;          // pinned staging of the geometry tables (one upload per geometry)
+  HostBuf items_host;          // pinned staging of the bucket-sort work items
   DevBuf seq[2];               // WT level code sequences
   DevBuf gr_tmp[2], gr_out;    // Golomb-Rice coding of a level (per-word carries/offsets, code words)
 
