@@ -259,13 +259,17 @@ __global__ __launch_bounds__(256) void k_wt_partition(const uint8_t* __restrict_
         }
         at[r] = R.fill;
       }
+      // one byte store per symbol: the two staging runs are adjacent, so the destination is
+      // zeros' slot zk or (1024 + 48) + ones' slot ok
       uint32_t zk = at[0] + zpre, ok = at[1] + opre;
+      uint8_t* const st0 = ST[wv][0];
+      constexpr uint32_t kRun1 = (uint32_t)(sizeof(ST[0][0]));
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
-        if ((valid >> i) & 1u) {
-          const uint8_t c = (uint8_t)(cw[i >> 2] >> (8 * (i & 3)));
-          if ((bits >> i) & 1u) ST[wv][1][ok++] = c; else ST[wv][0][zk++] = c;
-        }
+        const uint32_t b = (bits >> i) & 1u;
+        if ((valid >> i) & 1u) st0[b ? kRun1 + ok : zk] = (uint8_t)(cw[i >> 2] >> (8 * (i & 3)));
+        ok += b;
+        zk += ((valid >> i) & 1u) - b;
       }
       __builtin_amdgcn_wave_barrier();
 #pragma unroll
