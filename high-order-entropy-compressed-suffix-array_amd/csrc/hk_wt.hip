@@ -264,12 +264,22 @@ __global__ __launch_bounds__(256) void k_wt_partition(const uint8_t* __restrict_
       uint32_t zk = at[0] + zpre, ok = at[1] + opre;
       uint8_t* const st0 = ST[wv][0];
       constexpr uint32_t kRun1 = (uint32_t)(sizeof(ST[0][0]));
+      if (base + 1024 <= n) {   // a full span: every lane's 16 symbols are valid, no store guard
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const uint32_t b = (bits >> i) & 1u;
-        if ((valid >> i) & 1u) st0[b ? kRun1 + ok : zk] = (uint8_t)(cw[i >> 2] >> (8 * (i & 3)));
-        ok += b;
-        zk += ((valid >> i) & 1u) - b;
+        for (int i = 0; i < 16; ++i) {
+          const uint32_t b = (bits >> i) & 1u;
+          st0[b ? kRun1 + ok : zk] = (uint8_t)(cw[i >> 2] >> (8 * (i & 3)));
+          ok += b;
+          zk += 1u - b;
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const uint32_t b = (bits >> i) & 1u;
+          if ((valid >> i) & 1u) st0[b ? kRun1 + ok : zk] = (uint8_t)(cw[i >> 2] >> (8 * (i & 3)));
+          ok += b;
+          zk += ((valid >> i) & 1u) - b;
+        }
       }
       __builtin_amdgcn_wave_barrier();
 #pragma unroll
