@@ -117,8 +117,8 @@ __global__ __launch_bounds__(256) void k_wt_bits(const uint8_t* __restrict__ S, 
         if (j + 16 > n) bits &= j >= n ? 0u : (1u << (uint32_t)(n - j)) - 1;
       } else {
 #pragma unroll
-        for (int i = 0; i < 16; ++i)
-          bits |= ((j + i < n ? (uint32_t)LU[byte_of(v[it], i)] >> 15 : 0u) & 1u) << i;
+        for (int i = 0; i < 16; ++i) bits |= (((uint32_t)LU[byte_of(v[it], i)] >> 15) & 1u) << i;
+        if (j + 16 > n) bits &= j >= n ? 0u : (1u << (uint32_t)(n - j)) - 1;   // the text's last chunk
       }
       const uint64_t w = (uint64_t)bits | ((uint64_t)__shfl_down(bits, 1, 64) << 16) |
                          ((uint64_t)__shfl_down(bits, 2, 64) << 32) | ((uint64_t)__shfl_down(bits, 3, 64) << 48);
