@@ -153,8 +153,8 @@ def cpu_baseline(sample_n: int, npat: int, c0_n: int, seed: int = 3) -> dict:
 # ---------------------------------------------------------------------------- rooflines
 # kernels whose roofline bench.py reports: the dominant one (largest summed time) as `roofline`,
 # the others under roofline["others"]
-ROOF_KERNELS = ("sa_bucket_sort", "radix_part_text", "radix_part", "radix_part_keys", "radix_onesweep_text",
-                "radix_onesweep", "byte_hist")
+ROOF_KERNELS = ("sa_bucket_sort", "radix_part_text", "radix_part", "radix_part_keys", "shard_slice_part",
+                "radix_onesweep_text", "radix_onesweep", "byte_hist")
 WT_KERNELS = ("wt_bits", "wt_partition")
 
 
@@ -211,7 +211,8 @@ BUILD_STAGES = ["byte_hist", "sa_bucket_hist", "radix_part_text", "radix_part_ke
                 "sa_bucket_sort", "sa_big_gather", "radix_onesweep_text", "radix_table_text", "radix_tile_hist", "radix_hist", "radix_onesweep",
                 "radix_onesweep_small", "sa_pack_keys", "sa_refine_stats", "sa_refine_apply", "sa_refine_keys", "sa_refine_segsort",
                 "sa_isa_scatter", "sa_group_stats", "sa_group_apply", "sa_pair_keys", "bwt_gather"]
-SHARD_STAGES = ["shard_hist", "shard_below", "shard_select_count", "shard_pack_select", "rccl_allreduce_bytes",
+SHARD_STAGES = ["shard_hist", "shard_below", "shard_slice_hist", "shard_slice_part", "shard_select_count",
+                "shard_pack_select", "rccl_allreduce_bytes",
                 "rccl_allreduce_hist",
                 "rccl_allreduce_counts", "rccl_allgather_status", "rccl_allgather_sa", "rccl_allgather_pairs",
                 "sa_isa_update", "shard_split_join"] + BUILD_STAGES
@@ -416,8 +417,9 @@ def run_sharded(args, rank: int, world: int, local_rank: int) -> dict | None:
     uid = [comm_unique_id() if rank == 0 else None]
     dist.broadcast_object_list(uid, src=0)
     uid = uid[0]
-    # slices of < 2^32 suffixes: one per rank, or several per GPU run one after another (strong, N = 1)
-    per_gpu = max(1, -(-n // (world * ((1 << 32) - (1 << 28)))))
+    # one slice per rank; a text of >= 2^32 suffixes on one GPU (strong, N = 1) is built as slices of
+    # ~1 GiB one after another (the geometry of every weak-scaling rank)
+    per_gpu = slices_per_gpu(n, world)
     if per_gpu > 1 and world > 1:
         raise SystemExit("more than one slice per GPU is supported at N = 1 only")
 
@@ -512,16 +514,26 @@ def run_sharded(args, rank: int, world: int, local_rank: int) -> dict | None:
     return res
 
 
-def virtual_slices(dev, k: int):
+def slices_per_gpu(n: int, world: int) -> int:
+    """1, or at N = 1 for a text with >= 2^32 suffixes, slices of about 2^30 suffixes."""
+    if world > 1 or n < (1 << 32) - 1:
+        return 1
+    return max(2, int(round(n / (1 << 30))))
+
+
+def virtual_slices(dev, k: int, on_slice=None):
     """One GPU builds all k slices of a sharded build one after another (host-driven phases).  Only
     used when the text has >= 2^32 suffixes on a single GPU; the bench text is iid, so no slice is left
-    tied after its chunk rounds (checked)."""
+    tied after its chunk rounds (checked).  on_slice(r) runs after slice r is built (parity tests read
+    the slice there)."""
     g = sum(dev.shard_histogram(k, r) for r in range(k))
     below = sum(dev.shard_counts(g, k, r) for r in range(k))
     for r in range(k):
         dev.shard_build(g, below, k, r)
         if dev.shard_status()[2]:
             raise RuntimeError("virtual slices need a text without ties left after the chunk rounds")
+        if on_slice is not None:
+            on_slice(r)
 
 
 # ---------------------------------------------------------------------------- launch

@@ -149,8 +149,9 @@ __global__ __launch_bounds__(BH_T, 1) void k_bucket_hist(const uint8_t* __restri
 // code (pb2 bits) when the terminal is unkeyed (tcode >= 0, the dense code of the terminal, which
 // precedes only suffix 0): the BWT byte of position 0 is the terminal, every other code maps back
 // as code + (code >= tcode).
+// phb: position bits above 32 (sharded slices of texts with >= 2^32 suffixes, u64 SA entries).
 struct PkGeom {
-  int pbits = 0, pb = 0, pb2 = 0, tcode = -1;
+  int pbits = 0, pb = 0, pb2 = 0, tcode = -1, phb = 0;
 };
 
 // a record's key bits below the pass A digit in the full (pb-bit prev) layout
@@ -643,6 +644,401 @@ __global__ __launch_bounds__(T, T == 1024 ? 1 : 2) void k_cpart(const uint64_t* 
   }
 }
 
+// ------------------------------------------------------------ 1c. sharded slices (keyed coarse splitters)
+// A slice of a sharded build owns every suffix whose keyed sym field lies in [base << bsh, (base + nb)
+// << bsh): its bin is (sym >> bsh) - base < nb.  With a whole-symbol keyed radix 2^lb, sym >> bsh is the
+// first DB = sb - bsh bits of the sym field: a window of hq symbols with its low wdrop bits dropped, so
+// the bin comes from the text exactly as the single-GPU cursor pre-pass computes its bucket.  The
+// selection is therefore fused into the cursor partition: the pre-pass counts only the slice's suffixes
+// (per span: bins and pass A digits), and pass A scans the whole text, keeps the slice's suffixes and
+// scatters them by digit - no selection masks, no key planes in position order, no third pass.
+// Every rank scans all of T' twice, so for radix 2^2 (DNA) both scans run in registers: a byte maps to
+// its keyed code through an 8-entry byte table indexed by 3 bits of the byte (one v_perm_b32 per four
+// bytes; the host picks the bit field that separates the keyed bytes), a multiply packs four codes,
+// and each position's window is one v_alignbit of the packed words (REG kernels).
+struct SliceSel {
+  uint32_t base = 0, nb = 0;   // first global bin of the slice, bins in the slice
+  int bsh = 0, DB = 0;         // sym bits below a bin; sym bits above them
+  int hq = 0, wdrop = 0;       // window of hq symbols (hq * lb bits), low wdrop bits dropped
+  uint32_t g = 1;              // sub-tiles of CP_TILE positions per unit (pass A workgroup)
+  int sA = 0;                  // pass B digit bits (the pass A digit = bin >> sA)
+  int pbits = 0, pb2 = 0;      // packed records: position bits, prev-code bits (0: key / value planes)
+  int pbe = 0;                 // key planes: prev + position-high bits below the relative sym field
+  uint32_t tl = 0, th = 0;     // REG: keyed code of byte b = byte ((b >> ps) & 7) of {th, tl}
+  int ps = -1;                 // REG: the byte's bit field (-1: no 3-bit field separates the keyed bytes)
+};
+
+constexpr uint32_t SL_SUB = 8192;   // positions per sub-tile (= CP_TILE)
+
+// keyed codes (radix 2^2) of 16 text bytes, packed MSB-first (first byte in bits 31..30)
+__device__ __forceinline__ uint32_t pack16_2(const uint4& v, const SliceSel& sl) {
+  auto p8 = [&](uint32_t w) -> uint32_t {
+    const uint32_t c = __builtin_amdgcn_perm(sl.th, sl.tl, (w >> sl.ps) & 0x07070707u);   // 4 codes, a byte each
+    return (c * 0x40100401u) >> 24;   // c0 << 6 | c1 << 4 | c2 << 2 | c3 (the partial products never overlap)
+  };
+  return (p8(v.x) << 24) | (p8(v.y) << 16) | (p8(v.z) << 8) | p8(v.w);
+}
+
+// the 32 code bits from position k of the packed stream w0:w1 (k compile-time after unrolling)
+__device__ __forceinline__ uint32_t win32(uint32_t w0, uint32_t w1, int k) {
+  return k ? __builtin_amdgcn_alignbit(w0, w1, 32 - 2 * k) : w0;
+}
+
+// Pre-pass of a slice: for every text span (one workgroup), the slice's bin counts (CB-bit LDS counters
+// as k_bucket_hist_spans) and its pass A digit counts.  REG: radix 2^2 in registers; else the LDS code
+// table (LBQ / HQ compile-time when given).
+template <int CB, int HB = -1, int LBQ = 0, int HQ = 0, bool REG = false>
+__global__ __launch_bounds__(BH_T, 1) void k_slice_hist_spans(const uint8_t* __restrict__ t, uint64_t n,
+                                                              const uint16_t* __restrict__ lutk,
+                                                              const uint64_t* __restrict__ skey, KeyedArgs g,
+                                                              SliceSel sl, int D, uint32_t* __restrict__ part,
+                                                              unsigned long long* __restrict__ drain,
+                                                              uint32_t* __restrict__ spanc, uint64_t span,
+                                                              unsigned long long* __restrict__ ovf) {
+  constexpr int hb = HB;
+  constexpr uint32_t HALF = 1u << (CB - 1);
+  constexpr int CPW = 32 / CB;
+  const uint32_t boff = hb > 0 ? 65536u : 0u;
+  const int sA = sl.sA;
+  bool bad = false;
+  __shared__ uint32_t H[32768];
+  __shared__ uint32_t M[CP_NAM];
+  __shared__ uint16_t L[256];
+  __shared__ uint64_t SK[72];
+  const uint32_t tid = threadIdx.x;
+  for (uint32_t i = tid; i < 32768; i += BH_T) H[i] = 0;
+  if (tid < CP_NAM) M[tid] = 0;
+  if (tid < 256) L[tid] = lutk[tid];
+  if (tid < 72) SK[tid] = skey[tid];
+  __syncthreads();
+  auto add = [&](uint32_t b) {   // b: the slice bin, < sl.nb
+    if (hb >= 0 && (b >> 16) != (uint32_t)hb) return;
+    const uint32_t bl = b - boff;
+    const uint32_t sh = CB * (bl % CPW);
+    const uint32_t old = atomicAdd(&H[bl / CPW], 1u << sh);
+    const uint32_t ob = (old >> sh) & ((1u << CB) - 1);
+    if (CB == 8) bad |= ob >= 224u;
+    if (ob == HALF - 1) {
+      atomicSub(&H[bl / CPW], HALF << sh);
+      atomicAdd(&drain[b], (unsigned long long)HALF);
+      atomicAdd(&M[b >> sA], HALF);
+    }
+  };
+  const uint64_t lim = n < g.s_start ? n : g.s_start;   // positions with a text window
+  const uint64_t lo = (uint64_t)blockIdx.x * span;
+  const uint64_t hi = lo + span < n ? lo + span : n;
+  const int lb = LBQ ? LBQ : 31 - __clz((uint32_t)g.Rk);
+  const int hq = HQ ? HQ : sl.hq;
+  constexpr int NI = HQ ? BH_PER + HQ - 1 : 2 * BH_PER - 1;
+  static_assert(NI <= 2 * BH_PER, "window past the thread's 32 bytes");
+  const int wbits = hq * lb, wdrop = sl.wdrop, dsh = 32 - sl.DB;
+  const uint32_t bmask = wbits >= 32 ? ~0u : (1u << wbits) - 1;
+  uint4 w0 = make_uint4(0, 0, 0, 0), w1 = w0;
+  if (lo + (uint64_t)tid * BH_PER < hi) {
+    const uint4* src = reinterpret_cast<const uint4*>(t + lo + (uint64_t)tid * BH_PER);
+    w0 = src[0];
+    w1 = src[1];
+  }
+  for (uint64_t base = lo; base < hi; base += BH_TILE) {
+    const uint64_t p0 = base + (uint64_t)tid * BH_PER;
+    const uint4 a = w0, b4 = w1;
+    if (p0 + BH_TILE < hi) {   // next iteration's bytes in flight
+      const uint4* src = reinterpret_cast<const uint4*>(t + p0 + BH_TILE);
+      w0 = src[0];
+      w1 = src[1];
+    }
+    const uint64_t lim2 = lim < hi ? lim : hi;
+    if (p0 < lim2) {
+      const bool full = p0 + BH_PER <= lim2;
+      if constexpr (REG) {
+        const uint32_t c0 = pack16_2(a, sl), c1 = pack16_2(b4, sl);
+#pragma unroll
+        for (int k = 0; k < BH_PER; ++k) {
+          const uint32_t bin = (win32(c0, c1, k) >> dsh) - sl.base;
+          if (bin < sl.nb && (full || p0 + k < lim2)) add(bin);
+        }
+      } else {
+        const uint32_t wd[8] = {a.x, a.y, a.z, a.w, b4.x, b4.y, b4.z, b4.w};
+        uint32_t b = 0;
+#pragma unroll
+        for (int i = 0; i < NI; ++i) {
+          b = ((b << lb) | (L[(wd[i >> 2] >> (8 * (i & 3))) & 255u] & 255u)) & bmask;
+          const int j = i - (hq - 1);
+          if (j >= 0 && j < BH_PER && (full || p0 + j < lim2)) {
+            const uint32_t bin = (b >> wdrop) - sl.base;
+            if (bin < sl.nb) add(bin);
+          }
+        }
+      }
+    }
+    for (uint64_t p = p0 > lim ? p0 : lim; p < p0 + BH_PER && p < hi; ++p) {
+      const uint32_t bin = (uint32_t)(SK[p - g.s_start] >> sl.bsh) - sl.base;
+      if (bin < sl.nb) add(bin);
+    }
+  }
+  if (CB == 8 && bad) atomicOr(ovf, 1ull);
+  __syncthreads();
+  const uint32_t nbl = hb >= 0 ? 65536u : 1u << D;
+  hist_spans_flush<CB>(H, M, nbl, boff, 1u << D, sA, part, spanc);
+}
+
+// Pass A of a slice: workgroup = one unit (g sub-tiles of CP_TILE positions of one span).  Round 1
+// counts the unit's kept suffixes per pass A digit (LDS atomics, nothing staged); when they fit one
+// tile (<= CP_TILE, iid text: g is ~0.9 of the text / slice ratio) the runs are reserved at once and
+// round 2 keys the unit again, staging every kept suffix straight at its final slot; a denser unit
+// (non-iid text) takes each sub-tile as a tile of its own (rank, reserve, stage, write).  PK: packed
+// records ((sym - (base << bsh)) & the bits below the pass A digit, prev code, position), one u64
+// each; else keys (sym - (base << bsh)) << pbe | prev << hb | position >> 32 and u32 values.
+// REG (radix 2^2, packed records): keys in registers from the thread's 16 consecutive positions
+// (three 16-B loads and the word before; prev codes from the stream).  Else CONSEC (radix 2^2, packed):
+// text_keys_consec2 over the LDS-staged sub-tile; else lane-strided text_keys.
+template <bool CONSEC>
+struct SlText {   // one sub-tile's text staging (text_keys: packed codes + raw bytes)
+  uint32_t pk[(CP_TILE + 64) / 4 + 4];
+  uint8_t raw[CP_TILE + 64];
+};
+template <>
+struct SlText<true> {   // radix 2^2, consecutive items (text_keys_consec2): packed codes only
+  uint32_t pk[(CP_TILE + 64) / 16 + 4];
+};
+
+template <int LB, bool PK, bool REG>
+struct SlShared {
+  uint64_t keys[CP_TILE];           // records / keys by final slot
+  uint32_t vals[PK ? 1 : CP_TILE];  // key planes: low position bits by final slot
+  uint8_t sd[CP_TILE];              // low 8 bits of each staged slot's digit
+  SlText<LB == 2 && PK> tx[REG ? 0 : 1];
+  uint32_t tg[CP_NAM];   // tile-local exclusive digit starts, then the runs' destinations minus them
+  uint32_t cnt[CP_NAM];
+  uint32_t wsum[CP_NAM / 64];
+  uint32_t prev0;
+  uint16_t L[256], LP[256];
+  uint64_t SK[72];
+};
+
+template <int LB, bool PK, bool REG = false>
+__global__ __launch_bounds__(CP_T, 2) void k_slice_cpart(uint64_t* __restrict__ kout, uint32_t* __restrict__ vout,
+                                                         uint64_t n, unsigned long long* __restrict__ cur,
+                                                         uint64_t span, TextKeySrc src, SliceSel sl,
+                                                         const unsigned long long* __restrict__ skip,
+                                                         uint64_t mcap) {
+  constexpr int T = CP_T;
+  static_assert(!REG || (LB == 2 && PK), "register keys: radix 2^2 packed records");
+  // consecutive items take their prev codes from the keyed code stream: packed records only (a key
+  // plane's prev field is the dense code)
+  constexpr bool CONSEC = LB == 2 && PK;
+  __shared__ SlShared<LB, PK, REG> sh;
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  if (skip && *skip) return;   // the pre-pass counters overflowed: recounted, then relaunched
+  const uint64_t U = (uint64_t)SL_SUB * sl.g;
+  // XCD groups as k_cpart: workgroups b, b + 8, ... take consecutive units of one span
+  const uint32_t per = (uint32_t)(span / U), gx = blockIdx.x & 7u, k8 = blockIdx.x >> 3;
+  const uint64_t unit = (uint64_t)(gx + 8u * (k8 / per)) * per + k8 % per;
+  const uint64_t ubase = unit * U;
+  if (ubase >= n) return;   // past the last span (whole workgroup, before any barrier)
+  unsigned long long* const row = cur + (ubase / span) * CP_NAM;
+  if (tid < 256) {
+    sh.L[tid] = src.lutk[tid];
+    sh.LP[tid] = src.lutp[tid];
+  }
+  if (tid < 72) sh.SK[tid] = src.skey[tid];
+  sh.cnt[tid] = 0;
+  __syncthreads();
+  const uint64_t lim = n < src.g.s_start ? n : src.g.s_start;
+  const uint64_t kmask_lo = (1ull << (sl.bsh + sl.sA)) - 1;   // record: the bits below the pass A digit
+  const uint64_t sbase = (uint64_t)sl.base << sl.bsh;
+  const int kpb = src.g.pb;                                    // prev bits of the keys
+  const uint64_t pmk = (1ull << kpb) - 1;
+  const int hbk = PK ? 0 : sl.pbe - kpb;                       // key planes: position-high bits
+  const int dsh = 32 - sl.DB, kbits = 2 * src.g.q;
+  const uint32_t nsub = (uint32_t)((n - ubase < U ? n - ubase : U) + SL_SUB - 1) / SL_SUB;
+  uint64_t key[CP_I];
+  uint32_t rk[CP_I];
+  auto keys_of = [&](uint64_t tb) {
+    __syncthreads();   // the previous sub-tile's staging has been read
+    if constexpr (REG) {
+      // no staging: this thread's 16 consecutive positions from three 16-B loads (T' has 64 pad bytes)
+      const uint64_t p0 = tb + 16ull * tid;
+      if (p0 >= n) {
+#pragma unroll
+        for (int k = 0; k < CP_I; ++k) key[k] = ~0ull;
+        return;
+      }
+      const uint4* q4 = reinterpret_cast<const uint4*>(src.text + p0);
+      const uint32_t c0 = pack16_2(q4[0], sl), c1 = pack16_2(q4[1], sl), c2 = pack16_2(q4[2], sl);
+      uint32_t pc;   // prev code of position p0: the records' code of T'[p0 - 1] (T'[n - 1] for p0 = 0)
+      if (p0) {
+        const uint32_t pw = reinterpret_cast<const uint32_t*>(src.text + p0)[-1] >> 24;
+        pc = __builtin_amdgcn_perm(sl.th, sl.tl, (pw >> sl.ps) & 7u) & 3u;
+      } else {
+        pc = sh.LP[src.text[n - 1]];
+      }
+#pragma unroll
+      for (int k = 0; k < CP_I; ++k) {
+        const uint64_t j = p0 + k;
+        const uint64_t win = ((uint64_t)win32(c0, c1, k) << 32) | win32(c1, c2, k);
+        uint64_t sym = kbits >= 64 ? win : win >> (64 - kbits);
+        if (j >= src.g.s_start) sym = j < n ? sh.SK[j - src.g.s_start] : 0;
+        const uint32_t prv = k ? (c0 >> (32 - 2 * k)) & 3u : pc;
+        key[k] = j < n ? (sym << kpb) | prv : ~0ull;
+      }
+    } else if constexpr (CONSEC) {
+      text_keys_consec2<T>(key, src, n, tb, sh.tx[0].pk, &sh.prev0, sh.L, sh.LP, sh.SK);
+    } else {
+      text_keys<T, CP_I, LB>(key, src, n, tb, tb + (uint64_t)wv * (CP_I * 64), lane, nullptr, sh.tx[0].pk,
+                             sh.tx[0].raw, &sh.prev0, sh.L, sh.LP, sh.SK);
+    }
+  };
+  auto pos_of = [&](uint64_t tb, int k) -> uint64_t {
+    return (REG || CONSEC) ? tb + 16ull * tid + (uint64_t)k : tb + (uint64_t)wv * (CP_I * 64) + 64ull * k + lane;
+  };
+  // the kept suffix's record / key and its pass A digit (~0u: not in the slice)
+  auto record = [&](uint64_t j, uint64_t kk, uint64_t& out) -> uint32_t {
+    if (j >= n) return ~0u;
+    const uint64_t sym = kk >> kpb;
+    const uint32_t bin = (uint32_t)(sym >> sl.bsh) - sl.base;
+    if (bin >= sl.nb) return ~0u;
+    const uint64_t x = sym - sbase;
+    if (PK) out = ((((x & kmask_lo) << sl.pb2) | (kk & pmk)) << sl.pbits) | j;
+    else out = (x << sl.pbe) | ((kk & pmk) << hbk) | (hbk ? j >> 32 : 0ull);
+    return bin >> sl.sA;
+  };
+  auto write_out = [&](uint32_t cnt_tile, uint32_t hi256) {
+    for (int i = 0; i < CP_I; ++i) {
+      const uint32_t s = (uint32_t)i * T + tid;
+      if (s < cnt_tile) {
+        const uint32_t d = (uint32_t)sh.sd[s] | (s >= hi256 ? 256u : 0u);
+        const uint32_t o = sh.tg[d] + s;   // u32 arithmetic: tg = destination - tile start (mod 2^32)
+        if (o < mcap) {   // guard: counts that disagree with the pre-pass fail the host's check, not memory
+          kout[o] = sh.keys[s];
+          if constexpr (!PK) vout[o] = sh.vals[s];
+        }
+      }
+    }
+  };
+  // ---- round 1: the unit's kept suffixes per digit
+  for (uint32_t st = 0; st < nsub; ++st) {
+    const uint64_t tb = ubase + (uint64_t)st * SL_SUB;
+    if constexpr (REG) {   // bins only, from two 16-B loads
+      const uint64_t p0 = tb + 16ull * tid;
+      if (p0 < n) {
+        const uint4* q4 = reinterpret_cast<const uint4*>(src.text + p0);
+        const uint32_t c0 = pack16_2(q4[0], sl), c1 = pack16_2(q4[1], sl);
+        const bool full = p0 + 16 <= lim;
+#pragma unroll
+        for (int k = 0; k < CP_I; ++k) {
+          const uint32_t bin = (win32(c0, c1, k) >> dsh) - sl.base;
+          if (bin < sl.nb && (full || p0 + k < lim)) atomicAdd(&sh.cnt[bin >> sl.sA], 1u);
+        }
+        for (uint64_t j = p0 > lim ? p0 : lim; j < p0 + 16 && j < n; ++j) {   // short suffixes
+          const uint32_t bin = (uint32_t)(sh.SK[j - src.g.s_start] >> sl.bsh) - sl.base;
+          if (bin < sl.nb) atomicAdd(&sh.cnt[bin >> sl.sA], 1u);
+        }
+      }
+    } else {
+      keys_of(tb);
+#pragma unroll
+      for (int k = 0; k < CP_I; ++k) {
+        uint64_t rec = 0;
+        const uint32_t d = record(pos_of(tb, k), key[k], rec);
+        if (d != ~0u) atomicAdd(&sh.cnt[d], 1u);
+      }
+    }
+  }
+  __syncthreads();
+  const uint32_t cu = sh.cnt[tid];
+  uint32_t total = 0;
+  {
+    const uint32_t inc = wave_incl_sum<uint32_t>(cu);
+    if (lane == 63) sh.wsum[wv] = inc;
+    __syncthreads();
+    uint32_t carry = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < T / 64; ++w) {
+      carry += w < wv ? sh.wsum[w] : 0u;
+      total += sh.wsum[w];
+    }
+    sh.tg[tid] = carry + inc - cu;
+    sh.cnt[tid] = 0;   // every thread read its own count above
+  }
+  const bool fast = total <= (uint32_t)CP_TILE;
+  if (fast) {
+    // the unit's runs reserved now (the result is first needed at the write-out)
+    const unsigned long long resv = cu ? atomicAdd(&row[tid], (unsigned long long)cu) : 0ull;
+    __syncthreads();
+    for (uint32_t st = 0; st < nsub; ++st) {
+      const uint64_t tb = ubase + (uint64_t)st * SL_SUB;
+      keys_of(tb);
+#pragma unroll
+      for (int k = 0; k < CP_I; ++k) {
+        const uint64_t j = pos_of(tb, k);
+        uint64_t rec = 0;
+        const uint32_t d = record(j, key[k], rec);
+        if (d != ~0u) {
+          uint32_t f = sh.tg[d] + atomicAdd(&sh.cnt[d], 1u);
+          f = f < (uint32_t)CP_TILE ? f : (uint32_t)CP_TILE - 1;   // (only a count mismatch overruns)
+          sh.keys[f] = rec;
+          sh.sd[f] = (uint8_t)d;
+          if constexpr (!PK) sh.vals[f] = (uint32_t)j;
+        }
+      }
+    }
+    __syncthreads();
+    const uint32_t hi256 = sh.tg[256];   // staged slots >= hi256 hold digits >= 256
+    const uint32_t gbv = (uint32_t)(resv - sh.tg[tid]);
+    __syncthreads();
+    sh.tg[tid] = gbv;
+    __syncthreads();
+    write_out(total, hi256);
+    return;
+  }
+  // dense unit: every sub-tile is a tile of its own
+  for (uint32_t st = 0; st < nsub; ++st) {
+    const uint64_t tb = ubase + (uint64_t)st * SL_SUB;
+    keys_of(tb);   // (barrier first: the previous tile's write-out has read sh)
+    sh.cnt[tid] = 0;
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < CP_I; ++k) {
+      const uint64_t j = pos_of(tb, k);
+      uint64_t rec = 0;
+      const uint32_t d = record(j, key[k], rec);
+      key[k] = rec;
+      rk[k] = d == ~0u ? ~0u : (atomicAdd(&sh.cnt[d], 1u) | (d << 16));
+    }
+    __syncthreads();
+    const uint32_t c = sh.cnt[tid];
+    const unsigned long long g = c ? atomicAdd(&row[tid], (unsigned long long)c) : 0ull;
+    const uint32_t inc = wave_incl_sum<uint32_t>(c);
+    if (lane == 63) sh.wsum[wv] = inc;
+    __syncthreads();
+    uint32_t carry = 0, tot = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < T / 64; ++w) {
+      carry += w < wv ? sh.wsum[w] : 0u;
+      tot += sh.wsum[w];
+    }
+    sh.tg[tid] = carry + inc - c;
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < CP_I; ++k)
+      if (rk[k] != ~0u) {
+        const uint32_t d = rk[k] >> 16;
+        const uint32_t f = sh.tg[d] + (rk[k] & 0xFFFFu);
+        sh.keys[f] = key[k];
+        sh.sd[f] = (uint8_t)d;
+        if constexpr (!PK) sh.vals[f] = (uint32_t)pos_of(tb, k);
+      }
+    __syncthreads();
+    const uint32_t hi256 = sh.tg[256];
+    const uint32_t gbv = (uint32_t)(g - sh.tg[tid]);
+    __syncthreads();
+    sh.tg[tid] = gbv;
+    __syncthreads();
+    write_out(tot, hi256);
+  }
+}
+
 // ------------------------------------------------------------ 2. keys
 constexpr int PKK_TILE = 4096;
 __global__ __launch_bounds__(256) void k_pack_keyed(const uint8_t* __restrict__ t, uint64_t n,
@@ -990,7 +1386,7 @@ __device__ __forceinline__ bool bucket_sort_fast(BsSharedT<T>& sh, uint2 it, con
     if (r < cnt) {
       const uint32_t pv = sh.aux[r], pos = sh.buf[r];
       sab[r] = (V)(((uint64_t)(pv >> pb) << 32) | pos);
-      bwb[r] = PK && pos == 0 && term >= 0 ? (uint8_t)term : sh.inv[pv & pmask];
+      bwb[r] = PK && pos == 0 && (pv >> pb) == 0 && term >= 0 ? (uint8_t)term : sh.inv[pv & pmask];
     }
   }
   if (ntie) {
@@ -1409,6 +1805,8 @@ __global__ __launch_bounds__(T, T == 1024 ? 1 : 4) void k_bucket_sort_fast(const
     XT x;
     if (X32) {
       pv = (uint32_t)(key[k] >> pbits) & pmask;   // hb = 0, symbias = 0
+      // u64 positions: their bits above 32 ride with the prev code (SA / tie values reassemble them)
+      if (sizeof(V) == 8) pv |= ((uint32_t)(key[k] >> 32) & ((1u << pg.phb) - 1)) << pb;
       x = (XT)((uint32_t)(key[k] >> 32) >> (xsh - 32));
     } else {
       const uint64_t kl = PK ? key[k] >> pbits : key[k];   // packed: the record stays (positions)
@@ -1497,10 +1895,12 @@ __global__ __launch_bounds__(256) void k_big_gather(const uint64_t* __restrict__
 // packed records back to (key, position) planes for the paths that take full keys (the LSD item
 // sorts, the global path): items[i] = {start, count}; the region (pass A digit) of index j is the last
 // r with startA[r] <= j, and the key is region << klw | the record's key bits in the full layout
+// uhb > 0 (u64 positions): the position's bits above 32 go below the key (the hb layout of the key
+// planes), the low 32 to vout
 __global__ __launch_bounds__(256) void k_unpack_items(const uint64_t* __restrict__ rec, const uint2* __restrict__ items,
                                                       uint32_t nitems, const uint64_t* __restrict__ startA,
                                                       uint32_t ndA, PkGeom pg, int klw, uint64_t* __restrict__ kout,
-                                                      uint32_t* __restrict__ vout) {
+                                                      uint32_t* __restrict__ vout, int uhb = 0) {
   __shared__ uint64_t S[CP_NAM + 1];
   for (uint32_t i = threadIdx.x; i <= ndA; i += 256) S[i] = startA[i];
   __syncthreads();
@@ -1515,9 +1915,21 @@ __global__ __launch_bounds__(256) void k_unpack_items(const uint64_t* __restrict
         if (S[mid] <= j) lo = mid; else hi = mid;
       }
       const uint64_t r = rec[j];
-      kout[j] = ((uint64_t)lo << klw) | pk_full_low(r, pg);
+      const uint64_t k = ((uint64_t)lo << klw) | pk_full_low(r, pg);
+      kout[j] = uhb ? (k << uhb) | ((r & pmask) >> 32) : k;
       vout[j] = (uint32_t)(r & pmask);
     }
+  }
+}
+
+// key planes with hb position bits below the key -> u64 SA entries (high bits | low 32) and bare keys
+__global__ __launch_bounds__(256) void k_split_join_keys(uint64_t* __restrict__ keys, const uint32_t* __restrict__ lo32,
+                                                         uint64_t m, int hb, uint64_t* __restrict__ sa) {
+  const uint64_t mask = (1ull << hb) - 1;
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < m; i += (uint64_t)gridDim.x * 256) {
+    const uint64_t k = keys[i];
+    sa[i] = ((k & mask) << 32) | lo32[i];
+    keys[i] = k >> hb;
   }
 }
 
@@ -1644,12 +2056,13 @@ struct PackedRecs {
   uint32_t ndA = 0;
   uint64_t* kfull = nullptr;
   uint32_t* vfull = nullptr;
+  int uhb = 0;                        // u64 positions: hb of the unpacked key layout
 };
 
 void unpack_items(Index& ix, const PackedRecs& pk, const uint64_t* rec, const uint2* d_items, uint32_t nitems) {
   if (!nitems) return;
   k_unpack_items<<<std::min<uint32_t>(nitems, 4096), 256, 0, ix.stream>>>(rec, d_items, nitems, pk.startA, pk.ndA,
-                                                                         pk.g, pk.klw, pk.kfull, pk.vfull);
+                                                                         pk.g, pk.klw, pk.kfull, pk.vfull, pk.uhb);
   HK_HIP(hipGetLastError());
 }
 
@@ -1661,10 +2074,13 @@ uint64_t sort_bucket_items(Index& ix, const BucketPlan& plan, const uint64_t* ke
                            int pb, int sb, int hb, uint64_t symbias, V* sa, uint8_t* bwt,
                            const PackedRecs* pk = nullptr) {
   hipStream_t s = ix.stream;
-  if (pk && (hb || symbias || sizeof(V) != 4)) throw ApiError{-1, "packed records: single-GPU keys only"};
-  // the LSD item sorts read full keys: packed items are unpacked to (kfull, vfull) first
+  if (pk && (hb || symbias)) throw ApiError{-1, "packed records: no key-plane position bits or sym bias"};
+  if (pk && sizeof(V) == 4 && (pk->g.phb || pk->uhb)) throw ApiError{-1, "packed records: u64 positions need a u64 SA"};
+  // the LSD item sorts read full keys: packed items are unpacked to (kfull, vfull) first (with the
+  // position's high bits below the key for u64 positions)
   const uint64_t* lkeys = pk ? pk->kfull : keys;
   const uint32_t* lvals = pk ? pk->vfull : vals;
+  const int lhb = pk ? pk->uhb : hb;
   const uint8_t* d_inv = ix.small.as<uint8_t>() + 3072;
   ix.ties_k.ensure(m * 8 + 16);
   ix.ties_v.ensure(m * sizeof(V) + 16);
@@ -1699,21 +2115,19 @@ uint64_t sort_bucket_items(Index& ix, const BucketPlan& plan, const uint64_t* ke
       auto launch = [&](auto ttag, auto trtag) {
         constexpr int T = decltype(ttag)::value;
         constexpr bool TR = decltype(trtag)::value;
-        if constexpr (std::is_same<V, uint32_t>::value) {
-          if (pk && pk->g.pbits + pk->g.pb2 >= 32) {   // sym fields in the records' high words
-            k_bucket_sort_fast<V, TR, T, true, true><<<grid_n, T, 0, s>>>(
-                keys, pk->vfull, ix.bk_items.as<uint2>(), pb, sb, hb, symbias, d_inv, sa, bwt,
-                ix.ties_k.as<uint64_t>(), ix.ties_v.as<V>(), ix.ties_n.as<unsigned long long>(), ix.bk_fb.as<uint2>(),
-                fbn, TR ? tbuf.as<uint64_t>() : nullptr, pk->g);
-            return;
-          }
-          if (pk) {
-            k_bucket_sort_fast<V, TR, T, true><<<grid_n, T, 0, s>>>(
-                keys, pk->vfull, ix.bk_items.as<uint2>(), pb, sb, hb, symbias, d_inv, sa, bwt,
-                ix.ties_k.as<uint64_t>(), ix.ties_v.as<V>(), ix.ties_n.as<unsigned long long>(), ix.bk_fb.as<uint2>(),
-                fbn, TR ? tbuf.as<uint64_t>() : nullptr, pk->g);
-            return;
-          }
+        if (pk && pk->g.pbits + pk->g.pb2 >= 32) {   // sym fields in the records' high words
+          k_bucket_sort_fast<V, TR, T, true, true><<<grid_n, T, 0, s>>>(
+              keys, pk->vfull, ix.bk_items.as<uint2>(), pb, sb, hb, symbias, d_inv, sa, bwt,
+              ix.ties_k.as<uint64_t>(), ix.ties_v.as<V>(), ix.ties_n.as<unsigned long long>(), ix.bk_fb.as<uint2>(),
+              fbn, TR ? tbuf.as<uint64_t>() : nullptr, pk->g);
+          return;
+        }
+        if (pk) {
+          k_bucket_sort_fast<V, TR, T, true><<<grid_n, T, 0, s>>>(
+              keys, pk->vfull, ix.bk_items.as<uint2>(), pb, sb, hb, symbias, d_inv, sa, bwt,
+              ix.ties_k.as<uint64_t>(), ix.ties_v.as<V>(), ix.ties_n.as<unsigned long long>(), ix.bk_fb.as<uint2>(),
+              fbn, TR ? tbuf.as<uint64_t>() : nullptr, pk->g);
+          return;
         }
         k_bucket_sort_fast<V, TR, T><<<grid_n, T, 0, s>>>(
             keys, vals, ix.bk_items.as<uint2>(), pb, sb, hb, symbias, d_inv, sa, bwt, ix.ties_k.as<uint64_t>(),
@@ -1748,24 +2162,24 @@ uint64_t sort_bucket_items(Index& ix, const BucketPlan& plan, const uint64_t* ke
       if (nfb) {
         if (pk) unpack_items(ix, *pk, keys, ix.bk_fb.as<uint2>(), nfb);
         k_bucket_sort<false, false, V><<<nfb, BS_T, 0, s>>>(
-            lkeys, lvals, ix.bk_fb.as<uint2>(), pb, sb, hb, symbias, d_inv, sa, bwt, ix.ties_k.as<uint64_t>(),
+            lkeys, lvals, ix.bk_fb.as<uint2>(), pb, sb, lhb, symbias, d_inv, sa, bwt, ix.ties_k.as<uint64_t>(),
             ix.ties_v.as<V>(), ix.ties_n.as<unsigned long long>(), nullptr);
       }
     } else if (nn) {
       if (pk) unpack_items(ix, *pk, keys, ix.bk_items.as<uint2>(), (uint32_t)nn);
       if (trace && sizeof(V) == 4)
         k_bucket_sort<false, true, V><<<grid_n, BS_T, 0, s>>>(
-            lkeys, lvals, ix.bk_items.as<uint2>(), pb, sb, hb, symbias, d_inv, sa, bwt, ix.ties_k.as<uint64_t>(),
+            lkeys, lvals, ix.bk_items.as<uint2>(), pb, sb, lhb, symbias, d_inv, sa, bwt, ix.ties_k.as<uint64_t>(),
             ix.ties_v.as<V>(), ix.ties_n.as<unsigned long long>(), tbuf.as<uint64_t>());
       else
         k_bucket_sort<false, false, V><<<grid_n, BS_T, 0, s>>>(
-            lkeys, lvals, ix.bk_items.as<uint2>(), pb, sb, hb, symbias, d_inv, sa, bwt, ix.ties_k.as<uint64_t>(),
+            lkeys, lvals, ix.bk_items.as<uint2>(), pb, sb, lhb, symbias, d_inv, sa, bwt, ix.ties_k.as<uint64_t>(),
             ix.ties_v.as<V>(), ix.ties_n.as<unsigned long long>(), nullptr);
     }
     if (nw) {
       if (pk) unpack_items(ix, *pk, keys, ix.bk_items.as<uint2>() + nn, (uint32_t)nw);
       k_bucket_sort<true, false, V><<<grid_w, BS_T, 0, s>>>(
-          lkeys, lvals, ix.bk_items.as<uint2>() + nn, pb, sb, hb, symbias, d_inv, sa, bwt, ix.ties_k.as<uint64_t>(),
+          lkeys, lvals, ix.bk_items.as<uint2>() + nn, pb, sb, lhb, symbias, d_inv, sa, bwt, ix.ties_k.as<uint64_t>(),
           ix.ties_v.as<V>(), ix.ties_n.as<unsigned long long>(), nullptr);
     }
     HK_HIP(hipGetLastError());
@@ -1809,7 +2223,7 @@ __global__ __launch_bounds__(256) void k_bin_starts(const uint64_t* __restrict__
 }  // namespace
 
 // ---------------------------------------------------------------- geometry
-KeyGeom key_geometry_keyed(Index& ix, int reserve) {
+KeyGeom key_geometry_keyed(Index& ix, int reserve, int min_q, int max_sb) {
   compute_alphabet(ix);
   const uint64_t n = ix.n;
   KeyGeom g{};
@@ -1895,11 +2309,11 @@ KeyGeom key_geometry_keyed(Index& ix, int reserve) {
   // iid collision rate sum(p_c^2)^q of the keyed symbols.
   auto ties = [&](int q) { return std::min((double)n, (double)n * (double)n * std::pow(p2, (double)q)); };
   double best = 1e300;
-  for (int q = 1; q <= 64; ++q) {
+  for (int q = std::max(1, min_q); q <= 64; ++q) {
     uint64_t ss;
     unsigned __int128 span = 0;
     const int sb = shorts(q, nullptr, ss, &span);
-    if (sb == 99 || g.pb + sb + reserve > 64) break;
+    if (sb == 99 || g.pb + sb + reserve > 64 || sb > max_sb) break;
     const int bs = shift_for(sb, span);
     const double passes = (double)((bs + 7) / 8) * (bs > 32 ? 1.3 : 1.0);
     const double cost = passes + 13.0 * ties(q) / (double)n;
@@ -2079,6 +2493,41 @@ template bool bucket_sort_slice<uint64_t>(Index&, const KeyGeom&, uint64_t, int,
                                           const uint64_t*);
 
 // ---------------------------------------------------------------- cursor partition (host)
+// Pass B's region table: the top-digit regions dealt to 8 XCD groups (largest first, to the group with
+// the fewest tiles); group g's tiles go to workgroups g, g + 8, ... so that one XCD works through one
+// region's cursor row at a time and its L2 merges the runs the row hands out back to back (blocks are
+// dealt round-robin over the XCDs: a speed assumption only).  Returns the most tiles of any group.
+static uint64_t deal_regions(Index& ix, const uint64_t* totA, uint32_t ndA, uint64_t btile, uint32_t* h_gtab,
+                             uint32_t* d_gtab) {
+  std::vector<uint32_t> order;
+  for (uint32_t d = 0; d < ndA; ++d)
+    if (totA[d]) order.push_back(d);
+  std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return totA[a] > totA[b]; });
+  std::vector<std::vector<uint32_t>> grp(8);
+  uint64_t load[8] = {0};
+  for (uint32_t d : order) {
+    const int g = (int)(std::min_element(load, load + 8) - load);
+    grp[g].push_back(d);
+    load[g] += ceil_div(totA[d], (uint64_t)CP_TILE);
+  }
+  uint32_t e = 0;
+  uint64_t maxl = 0;
+  for (int g = 0; g < 8; ++g) {
+    h_gtab[g] = e;
+    uint32_t k0 = 0;
+    for (uint32_t d : grp[g]) {
+      h_gtab[9 + 2 * e] = d;
+      h_gtab[9 + 2 * e + 1] = k0;
+      k0 += (uint32_t)ceil_div(totA[d], btile);
+      ++e;
+    }
+    maxl = std::max<uint64_t>(maxl, k0);
+  }
+  h_gtab[8] = e;
+  HK_HIP(hipMemcpyAsync(d_gtab, h_gtab, (9 + 2 * e) * 4, hipMemcpyHostToDevice, ix.stream));
+  return maxl;
+}
+
 // Groups n suffixes by bucket (section 1b): pre-pass counts and cursors on the device, pass A
 // launched at once; the bucket counts and digit totals come back behind an event while pass A
 // runs (the host deals the pass-B regions to XCD groups and the caller plans the bucket items
@@ -2253,39 +2702,10 @@ int cursor_partition(Index& ix, uint64_t n, int D, int bitlo, uint64_t kbias, co
   for (uint32_t b = 0; b < nb; ++b) hsum += hist[b];
   if (tsum != n || hsum != n) throw ApiError{-7, "cursor partition: bucket counts do not cover the text"};
   if (D > 8) {
-    // regions dealt to 8 XCD groups (largest first, to the group with the fewest tiles); group g's
-    // tiles go to workgroups g, g + 8, ... so that one XCD works through one region's cursor row at a
-    // time and its L2 merges the runs the row hands out back to back (blocks are dealt round-robin
-    // over the XCDs: a speed assumption only)
-    std::vector<uint32_t> order;
-    for (uint32_t d = 0; d < ndA; ++d)
-      if (totA[d]) order.push_back(d);
-    std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return totA[a] > totA[b]; });
-    std::vector<std::vector<uint32_t>> grp(8);
-    uint64_t load[8] = {0};
-    for (uint32_t d : order) {
-      const int g = (int)(std::min_element(load, load + 8) - load);
-      grp[g].push_back(d);
-      load[g] += ceil_div(totA[d], (uint64_t)CP_TILE);
-    }
     // 9-bit digits: 1024-thread tiles (twice the run length per digit)
     static const bool big_b = !getenv("HKCSA_CP_B1024") || atoi(getenv("HKCSA_CP_B1024")) != 0;
     const uint64_t btile = sA > 8 && big_b ? 1024 * CP_I : CP_TILE;
-    uint32_t e = 0;
-    uint64_t maxl = 0;
-    for (int g = 0; g < 8; ++g) {
-      h_gtab[g] = e;
-      uint32_t k0 = 0;
-      for (uint32_t d : grp[g]) {
-        h_gtab[9 + 2 * e] = d;
-        h_gtab[9 + 2 * e + 1] = k0;
-        k0 += (uint32_t)ceil_div(totA[d], btile);
-        ++e;
-      }
-      maxl = std::max<uint64_t>(maxl, k0);
-    }
-    h_gtab[8] = e;
-    HK_HIP(hipMemcpyAsync(d_gtab, h_gtab, (9 + 2 * e) * 4, hipMemcpyHostToDevice, s));
+    const uint64_t maxl = deal_regions(ix, totA, ndA, btile, h_gtab, d_gtab);
     TimedLaunch t(ix.timer, "radix_part", (double)n * 2 * (packed ? 8 : 8 + 4));
     if (packed)
       k_cpart<2, 0, 256, CP_T, true><<<(unsigned)(8 * maxl), CP_T, 0, s>>>(kp[1], nullptr, kp[0], nullptr, n,
@@ -2306,6 +2726,473 @@ int cursor_partition(Index& ix, uint64_t n, int D, int bitlo, uint64_t kbias, co
   }
   return outA;
 }
+
+// ---------------------------------------------------------------- sharded slices, keyed scheme (host)
+namespace {
+
+// Exact histogram of the coarse keyed bucket (the top 16 bits of the sym field: the first 16 / lb
+// symbols, radix 2^lb) of the positions [lo, hi) (lo a multiple of 16): one span per workgroup, u16
+// counter pairs drained at 2^15 (bh_add), per-span partials reduced by k_bucket_reduce.
+__global__ __launch_bounds__(BH_T, 1) void k_coarse_hist(const uint8_t* __restrict__ t, uint64_t n, uint64_t lo,
+                                                         uint64_t hi, const uint16_t* __restrict__ lutk,
+                                                         const uint64_t* __restrict__ skey, KeyedArgs g, int hq,
+                                                         int bsh16, uint64_t span, uint32_t* __restrict__ part,
+                                                         unsigned long long* __restrict__ drain) {
+  __shared__ uint32_t H[32768];
+  __shared__ uint16_t L[256];
+  __shared__ uint64_t SK[72];
+  const uint32_t tid = threadIdx.x;
+  for (uint32_t i = tid; i < 32768; i += BH_T) H[i] = 0;
+  if (tid < 256) L[tid] = lutk[tid];
+  if (tid < 72) SK[tid] = skey[tid];
+  __syncthreads();
+  const uint64_t a = lo + (uint64_t)blockIdx.x * span;
+  const uint64_t b = a + span < hi ? a + span : hi;
+  const uint64_t lim = n < g.s_start ? n : g.s_start;
+  const int lb = 31 - __clz((uint32_t)g.Rk);
+  for (uint64_t base = a; base < b; base += BH_TILE) {
+    const uint64_t p0 = base + (uint64_t)tid * BH_PER;
+    if (p0 >= b) continue;
+    const uint4* src = reinterpret_cast<const uint4*>(t + p0);   // T' has 64 readable pad bytes
+    const uint4 w0 = src[0], w1 = src[1];
+    const uint32_t wd[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+    const uint64_t lim2 = lim < b ? lim : b;
+    if (p0 < lim2) {
+      uint32_t w = 0;
+#pragma unroll
+      for (int i = 0; i < 2 * BH_PER - 1; ++i) {
+        w = (w << lb) | (L[(wd[i >> 2] >> (8 * (i & 3))) & 255u] & 255u);
+        const int j = i - (hq - 1);
+        if (j >= 0 && j < BH_PER && p0 + j < lim2) bh_add(H, w & 0xFFFFu, drain);
+      }
+    }
+    for (uint64_t p = p0 > lim ? p0 : lim; p < p0 + BH_PER && p < b; ++p)
+      bh_add(H, (uint32_t)(SK[p - g.s_start] >> bsh16), drain);
+  }
+  __syncthreads();
+  uint2* const pw = reinterpret_cast<uint2*>(part + (uint64_t)blockIdx.x * 65536);
+  for (uint32_t i = tid; i < 32768; i += BH_T) {
+    const uint32_t v = H[i];
+    pw[i] = make_uint2(v & 0xFFFFu, v >> 16);
+  }
+}
+
+int coarse_lb(const KeyGeom& kg) {
+  const uint64_t R = kg.Rk;
+  if (R != 2 && R != 4 && R != 16 && R != 256) return 0;
+  return __builtin_ctzll(R);
+}
+
+}  // namespace
+
+// lb of the keyed coarse scheme (whole-symbol keyed radix 2^lb, lb in {1, 2, 4, 8}), 0 when it does not apply
+int shard_keyed_lb(Index& ix) {
+  const KeyGeom kg = key_geometry_keyed(ix);
+  return coarse_lb(kg);
+}
+
+void shard_coarse_hist(Index& ix, uint64_t lo, uint64_t hi, uint64_t* d_hist) {
+  hipStream_t s = ix.stream;
+  const KeyGeom kg0 = key_geometry_keyed(ix);
+  const int lb = coarse_lb(kg0);
+  if (!lb) throw ApiError{-1, "keyed coarse histogram: alphabet without a whole-symbol keyed radix"};
+  const KeyGeom kg = key_geometry_keyed(ix, 0, 16 / lb);   // q >= 16 / lb: the coarse bucket is q-independent
+  upload_geometry(ix, kg);
+  const uint8_t* small = ix.small.as<uint8_t>();
+  const KeyChunks kch = key_chunks(kg.Rk, kg.q);
+  const KeyedArgs ka{kg.Rk, kch.Rck, kch.Rlast, kg.s_start, kg.q, kch.ck, kg.pb, 0, lb};
+  HK_HIP(hipMemsetAsync(d_hist, 0, 65536 * 8, s));
+  if (hi <= lo) return;
+  if (lo % 16) throw ApiError{-1, "coarse histogram: block start not 16-aligned"};
+  const uint64_t span = ceil_div(ceil_div(hi - lo, (uint64_t)BH_TILE), 256) * BH_TILE;
+  const uint32_t nspan = (uint32_t)ceil_div(hi - lo, span);
+  ix.cp_part.ensure((uint64_t)nspan * 65536 * 4 + 16);
+  ix.bk_hist.ensure(65536 * 8 + 16);
+  unsigned long long* d_drain = ix.bk_hist.as<unsigned long long>();
+  HK_HIP(hipMemsetAsync(d_drain, 0, 65536 * 8, s));
+  TimedLaunch t(ix.timer, "shard_hist", (double)(hi - lo));
+  k_coarse_hist<<<nspan, BH_T, 0, s>>>(ix.text.as<uint8_t>(), ix.n, lo, hi,
+                                       reinterpret_cast<const uint16_t*>(small + 2560),
+                                       reinterpret_cast<const uint64_t*>(small + 3584), ka, 16 / lb, kg.sym_bits - 16,
+                                       span, ix.cp_part.as<uint32_t>(), d_drain);
+  HK_HIP(hipGetLastError());
+  k_bucket_reduce<<<65536 / 256, 256, 0, s>>>(ix.cp_part.as<uint32_t>(), d_drain, nspan, 65536, 65536, d_hist);
+  HK_HIP(hipGetLastError());
+}
+
+namespace {
+
+struct SlicePlan {
+  KeyGeom kk;
+  SliceSel sl;
+  int D = 0, lb = 0, pb = 0, hb = 0;   // hb: key planes' position-high bits (u64 SA)
+  bool packed = false;
+  bool reg = false;   // radix 2^2 packed records with a perm-table byte field: the register kernels
+  PkGeom pg;
+  int uhb = 0;
+};
+
+// Geometry of the slice of coarse buckets [c_lo, c_hi): f = the most extra bin bits with at most 2^17
+// bins (k << f) and a pre-pass window of <= 16 symbols; packed records when the bits below the pass A
+// digit, the prev code and the position fit one u64 (q capped for that), else key / value planes.
+SlicePlan plan_slice(Index& ix, uint32_t c_lo, uint32_t c_hi, bool u64pos) {
+  SlicePlan P;
+  const KeyGeom kg0 = key_geometry_keyed(ix);
+  P.lb = coarse_lb(kg0);
+  if (!P.lb) throw ApiError{-1, "slice plan: no whole-symbol keyed radix"};
+  const int lb = P.lb;
+  const uint64_t n = ix.n;
+  const int pbits = n > 1 ? 64 - __builtin_clzll(n - 1) : 1;
+  P.hb = 0;
+  if (u64pos) {
+    P.hb = 1;
+    while (((n - 1) >> 32) >> P.hb) ++P.hb;
+  }
+  const uint32_t k = c_hi - c_lo;
+  auto geom_f = [&](int sb, int& f) {   // the pre-pass window: <= 16 symbols of <= 32 bits
+    f = 0;
+    while ((uint64_t)k << (f + 1) <= (1u << 17) && 16 + f + 1 <= sb) {
+      const int hq = (16 + f + 1 + lb - 1) / lb;
+      if (hq > 16 || hq * lb > 32) break;
+      ++f;
+    }
+  };
+  int pb2 = kg0.pb;
+  if (kg0.tcode >= 0) {
+    pb2 = 1;
+    while ((1ull << pb2) < kg0.Rk) ++pb2;
+    pb2 = std::min(pb2, kg0.pb);
+  }
+  // HKCSA_SLICE_PACKED=0: key / value planes (A/B)
+  static const bool pk_env = !getenv("HKCSA_SLICE_PACKED") || atoi(getenv("HKCSA_SLICE_PACKED")) != 0;
+  // the fallback key planes of packed records keep >= 1 position bit below the key for a u64 SA
+  const int uhb = u64pos ? std::max(1, pbits - 32) : 0;
+  bool packed = pk_env;
+  KeyGeom kk;
+  int f = 0;
+  if (packed) {
+    // bsh + 8 + pb2 + pbits <= 64 with bsh = sb - (16 + f): sb <= 56 - pb2 - pbits + 16 + f
+    kk = key_geometry_keyed(ix, uhb, 16 / lb);
+    for (int it = 0; it < 4 && packed; ++it) {
+      geom_f(kk.sym_bits, f);
+      const int bound = 56 - pb2 - pbits + 16 + f;
+      if (kk.sym_bits <= bound) break;
+      if (bound < 16 + f || bound < lb * (16 / lb)) {
+        packed = false;
+        break;
+      }
+      kk = key_geometry_keyed(ix, uhb, 16 / lb, bound);
+    }
+    if (packed) {
+      geom_f(kk.sym_bits, f);
+      if (kk.sym_bits - (16 + f) + 8 + pb2 + pbits > 64) packed = false;
+    }
+  }
+  if (!packed) {
+    kk = key_geometry_keyed(ix, P.hb, 16 / lb);
+    geom_f(kk.sym_bits, f);
+  }
+  P.kk = kk;
+  P.packed = packed;
+  P.pb = kk.pb;
+  SliceSel& sl = P.sl;
+  sl.DB = 16 + f;
+  sl.bsh = kk.sym_bits - sl.DB;
+  sl.base = c_lo << f;
+  sl.nb = k << f;
+  sl.hq = (sl.DB + lb - 1) / lb;
+  sl.wdrop = sl.hq * lb - sl.DB;
+  P.D = 1;
+  while ((1u << P.D) < sl.nb) ++P.D;
+  sl.sA = P.D > 8 ? 8 : 0;
+  if (packed) {
+    sl.pbits = pbits;
+    sl.pb2 = pb2;
+    P.pg.pbits = pbits;
+    P.pg.pb = kk.pb;
+    P.pg.pb2 = pb2;
+    P.pg.tcode = pb2 < kk.pb ? kk.tcode : -1;
+    P.pg.phb = std::max(0, pbits - 32);
+    P.uhb = uhb;
+  } else {
+    sl.pbe = kk.pb + P.hb;
+  }
+  // register kernels (radix 2^2, packed): a 3-bit field of the byte that separates the keyed bytes
+  // indexes an 8-entry table of their codes (every byte the scans key is keyed: the unkeyed terminal
+  // only ends short suffixes, which take their boundary keys)
+  static const bool reg_env = !getenv("HKCSA_SLICE_REG") || atoi(getenv("HKCSA_SLICE_REG")) != 0;
+  if (reg_env && packed && lb == 2) {
+    for (int ps = 0; ps <= 5 && !P.reg; ++ps) {
+      uint8_t tab[8] = {0};
+      bool used[8] = {false}, ok = true;
+      for (int b = 0; b < 256 && ok; ++b) {
+        if (!kk.kflag[b]) continue;
+        const int idx = (b >> ps) & 7;
+        ok = !used[idx];
+        used[idx] = true;
+        tab[idx] = (uint8_t)kk.kdig[b];
+      }
+      if (!ok) continue;
+      P.reg = true;
+      sl.ps = ps;
+      sl.tl = (uint32_t)tab[0] | (uint32_t)tab[1] << 8 | (uint32_t)tab[2] << 16 | (uint32_t)tab[3] << 24;
+      sl.th = (uint32_t)tab[4] | (uint32_t)tab[5] << 8 | (uint32_t)tab[6] << 16 | (uint32_t)tab[7] << 24;
+    }
+  }
+  return P;
+}
+
+}  // namespace
+
+// The slice's cursor partition (section 1c): pre-pass over the whole text counting the slice's bins
+// (and its units' pass A digits), cursors, fused pass A from the text, pass B.  Records / key planes
+// end in slot 0 (D > 8) or 1; hist gets the bin counts.
+static int cursor_partition_slice(Index& ix, const SlicePlan& P, const TextKeySrc& tks, uint64_t m, uint64_t* kp[2],
+                                  uint32_t* vp[2], std::vector<uint64_t>& hist, PackedRecs& pkr) {
+  hipStream_t s = ix.stream;
+  const uint64_t n = ix.n;
+  const SliceSel& sl = P.sl;
+  const int D = P.D, sA = sl.sA;
+  const uint32_t nb2 = 1u << D, ndA = 1u << (D - sA);
+  const uint64_t U = (uint64_t)SL_SUB * sl.g;
+  const uint64_t Lq = sl.g % 2 ? 2 * U : U;   // lcm(BH_TILE, U)
+  const uint64_t span = ceil_div(ceil_div(n, Lq), 256) * Lq;
+  const uint32_t nspan = (uint32_t)ceil_div(n, span);
+  ix.cp_part.ensure((uint64_t)nspan * nb2 * 4 + (uint64_t)nspan * CP_NAM * 4 + 16);
+  ix.bk_hist.ensure((uint64_t)nb2 * 16 + 16);
+  ix.cp_cur.ensure(((uint64_t)nspan * CP_NAM + nb2 + 2 * (CP_NAM + 1) + 16 + (uint64_t)CP_NG * CP_NAM) * 8);
+  constexpr uint64_t kLp2Off = (9 + 2 * CP_NAM + 16) * 4;
+  ix.cp_tiles.ensure(kLp2Off + 512);
+  ix.cp_host.ensure((uint64_t)nb2 * 8 + 2 * (CP_NAM + 1) * 8 + (9 + 2 * CP_NAM) * 4 + 64);
+  uint32_t* d_part = ix.cp_part.as<uint32_t>();
+  uint32_t* d_spanc = d_part + (uint64_t)nspan * nb2;
+  unsigned long long* d_drain = ix.bk_hist.as<unsigned long long>();
+  uint64_t* d_hist = ix.bk_hist.as<uint64_t>() + nb2;
+  unsigned long long* d_curA = ix.cp_cur.as<unsigned long long>();
+  unsigned long long* d_curB = d_curA + (uint64_t)nspan * CP_NAM;
+  uint64_t* d_totA = reinterpret_cast<uint64_t*>(d_curB + nb2);
+  uint64_t* d_startA = d_totA + (CP_NAM + 1);
+  unsigned long long* d_ovf = reinterpret_cast<unsigned long long*>(d_totA + 2 * (CP_NAM + 1));
+  uint64_t* d_gpre = d_totA + 2 * (CP_NAM + 1) + 16;
+  uint32_t* d_gtab = ix.cp_tiles.as<uint32_t>();
+  uint64_t* h_hist = ix.cp_host.as<uint64_t>();
+  uint64_t* h_totA = h_hist + nb2;
+  uint32_t* h_gtab = reinterpret_cast<uint32_t*>(h_totA + 2 * (CP_NAM + 1) + 1);
+  const uint64_t* h_ovf = h_totA + 2 * (CP_NAM + 1);
+  TextKeySrc tks2 = tks;
+  if (P.packed) {
+    uint16_t* d_lp2 = reinterpret_cast<uint16_t*>(ix.cp_tiles.as<uint8_t>() + kLp2Off);
+    HK_HIP(hipMemcpyAsync(d_lp2, pkr.lutp2, 512, hipMemcpyHostToDevice, s));
+    tks2.lutp = d_lp2;
+    tks2.g.pb = P.pg.pb2;
+    pkr.startA = d_startA;
+    pkr.ndA = ndA;
+    pkr.klw = P.pb + sl.bsh + sA;
+  }
+  auto prepass = [&](bool exact) {
+    HK_HIP(hipMemsetAsync(d_drain, 0, (uint64_t)nb2 * 8, s));
+    HK_HIP(hipMemsetAsync(d_ovf, 0, 8, s));
+    TimedLaunch t(ix.timer, "shard_slice_hist", (double)n * (exact ? 2 : 1));
+    const KeyedArgs& g = tks.g;
+    const bool reg = P.reg;
+    if (D > 16 && !exact) {
+      auto kern = k_slice_hist_spans<8>;
+      if (reg) kern = k_slice_hist_spans<8, -1, 2, 0, true>;
+      else if (P.lb == 2 && sl.hq == 9) kern = k_slice_hist_spans<8, -1, 2, 9>;
+      else if (P.lb == 2 && sl.hq == 10) kern = k_slice_hist_spans<8, -1, 2, 10>;
+      kern<<<nspan, BH_T, 0, s>>>(tks.text, n, tks.lutk, tks.skey, g, sl, D, d_part, d_drain, d_spanc, span, d_ovf);
+    } else if (D > 16) {
+      auto k0 = reg ? k_slice_hist_spans<16, 0, 2, 0, true> : k_slice_hist_spans<16, 0>;
+      auto k1 = reg ? k_slice_hist_spans<16, 1, 2, 0, true> : k_slice_hist_spans<16, 1>;
+      k0<<<nspan, BH_T, 0, s>>>(tks.text, n, tks.lutk, tks.skey, g, sl, D, d_part, d_drain, d_spanc, span, d_ovf);
+      k1<<<nspan, BH_T, 0, s>>>(tks.text, n, tks.lutk, tks.skey, g, sl, D, d_part, d_drain, d_spanc, span, d_ovf);
+    } else {
+      auto kern = k_slice_hist_spans<16>;
+      if (reg) kern = k_slice_hist_spans<16, -1, 2, 0, true>;
+      else if (P.lb == 2 && sl.hq == 9) kern = k_slice_hist_spans<16, -1, 2, 9>;
+      else if (P.lb == 2 && sl.hq == 10) kern = k_slice_hist_spans<16, -1, 2, 10>;
+      kern<<<nspan, BH_T, 0, s>>>(tks.text, n, tks.lutk, tks.skey, g, sl, D, d_part, d_drain, d_spanc, span, d_ovf);
+    }
+    HK_HIP(hipGetLastError());
+    k_bucket_reduce<<<(nb2 + 255) / 256, 256, 0, s>>>(d_part, d_drain, nspan, nb2, nb2, d_hist);
+    HK_HIP(hipGetLastError());
+    const uint32_t nblkA = (ndA + CP_DB - 1) / CP_DB;
+    k_cp_colsum<<<nblkA, 1024, 0, s>>>(d_spanc, nspan, ndA, d_gpre, d_totA);
+    HK_HIP(hipGetLastError());
+    k_cp_cursors<<<nblkA + (sA ? 1 : 0), 1024, 0, s>>>(d_hist, d_spanc, d_gpre, nspan, nb2, ndA, d_curA,
+                                                       sA ? d_curB : nullptr, d_totA, d_startA);
+    HK_HIP(hipGetLastError());
+  };
+  const int outA = sA ? 1 : 0;
+  auto passA = [&]() {
+    TimedLaunch t(ix.timer, "shard_slice_part", (double)n + (double)m * (P.packed ? 8 : 8 + 4));
+    const unsigned grid = (unsigned)(8 * ceil_div(nspan, 8u) * (span / U));
+    void* vo = P.packed ? nullptr : (void*)vp[outA];
+    const unsigned long long* skip = D > 16 ? d_ovf : nullptr;
+    if (P.reg)
+      k_slice_cpart<2, true, true><<<grid, CP_T, 0, s>>>(kp[outA], nullptr, n, d_curA, span, tks2, sl, skip, m);
+    else if (P.packed && P.lb == 2)
+      k_slice_cpart<2, true><<<grid, CP_T, 0, s>>>(kp[outA], nullptr, n, d_curA, span, tks2, sl, skip, m);
+    else if (P.packed && P.lb == 1)
+      k_slice_cpart<1, true><<<grid, CP_T, 0, s>>>(kp[outA], nullptr, n, d_curA, span, tks2, sl, skip, m);
+    else if (P.packed && P.lb == 4)
+      k_slice_cpart<4, true><<<grid, CP_T, 0, s>>>(kp[outA], nullptr, n, d_curA, span, tks2, sl, skip, m);
+    else if (P.packed)
+      k_slice_cpart<8, true><<<grid, CP_T, 0, s>>>(kp[outA], nullptr, n, d_curA, span, tks2, sl, skip, m);
+    else if (P.lb == 1)
+      k_slice_cpart<1, false><<<grid, CP_T, 0, s>>>(kp[outA], (uint32_t*)vo, n, d_curA, span, tks2, sl, skip, m);
+    else if (P.lb == 2)
+      k_slice_cpart<2, false><<<grid, CP_T, 0, s>>>(kp[outA], (uint32_t*)vo, n, d_curA, span, tks2, sl, skip, m);
+    else if (P.lb == 4)
+      k_slice_cpart<4, false><<<grid, CP_T, 0, s>>>(kp[outA], (uint32_t*)vo, n, d_curA, span, tks2, sl, skip, m);
+    else
+      k_slice_cpart<8, false><<<grid, CP_T, 0, s>>>(kp[outA], (uint32_t*)vo, n, d_curA, span, tks2, sl, skip, m);
+    HK_HIP(hipGetLastError());
+    ix.info[0] += 1;
+  };
+  if (!ix.aux_stream) HK_HIP(hipStreamCreateWithFlags(&ix.aux_stream, hipStreamNonBlocking));
+  auto counts_then_passA = [&]() {
+    hipEvent_t ev_pre, ev_cnt;
+    HK_HIP(hipEventCreateWithFlags(&ev_pre, hipEventDisableTiming));
+    HK_HIP(hipEventCreateWithFlags(&ev_cnt, hipEventDisableTiming));
+    HK_HIP(hipEventRecord(ev_pre, s));
+    HK_HIP(hipStreamWaitEvent(ix.aux_stream, ev_pre, 0));
+    HK_HIP(hipMemcpyAsync(h_hist, d_hist, (uint64_t)nb2 * 8, hipMemcpyDeviceToHost, ix.aux_stream));
+    HK_HIP(hipMemcpyAsync(h_totA, d_totA, (2 * (CP_NAM + 1) + 1) * 8, hipMemcpyDeviceToHost, ix.aux_stream));
+    HK_HIP(hipEventRecord(ev_cnt, ix.aux_stream));
+    passA();
+    const hipError_t we = hipEventSynchronize(ev_cnt);
+    (void)hipEventDestroy(ev_pre);
+    (void)hipEventDestroy(ev_cnt);
+    HK_HIP(we);
+  };
+  prepass(false);
+  counts_then_passA();
+  if (D > 16 && *h_ovf) {   // u8 counters overflowed: exact recount, pass A again
+    ix.info[0] -= 1;
+    prepass(true);
+    counts_then_passA();
+  }
+  hist.assign(h_hist, h_hist + nb2);
+  uint64_t tsum = 0, hsum = 0;
+  for (uint32_t d = 0; d < ndA; ++d) tsum += h_totA[d];
+  for (uint32_t b = 0; b < nb2; ++b) hsum += hist[b];
+  if (tsum != m || hsum != m) throw ApiError{-7, "slice partition: bin counts do not match the slice size"};
+  if (!sA) return outA;
+  const uint64_t maxl = deal_regions(ix, h_totA, ndA, CP_TILE, h_gtab, d_gtab);
+  TimedLaunch t(ix.timer, "radix_part", (double)m * 2 * (P.packed ? 8 : 8 + 4));
+  if (P.packed)
+    k_cpart<2, 0, 256, CP_T, true><<<(unsigned)(8 * maxl), CP_T, 0, s>>>(
+        kp[1], nullptr, kp[0], nullptr, m, P.pg.pbits + P.pg.pb2 + sl.bsh, 0, d_curB, d_gtab, d_startA, 0,
+        TextKeySrc{}, P.pg.pbits);
+  else
+    k_cpart<2, 0><<<(unsigned)(8 * maxl), CP_T, 0, s>>>(kp[1], vp[1], kp[0], vp[0], m, sl.pbe + sl.bsh, 0, d_curB,
+                                                       d_gtab, d_startA, 0, TextKeySrc{});
+  HK_HIP(hipGetLastError());
+  ix.info[0] += 1;
+  return 0;
+}
+
+// One sharded slice under the keyed coarse scheme: the coarse buckets [c_lo, c_hi), m suffixes.
+template <typename V>
+void build_slice_keyed(Index& ix, uint32_t c_lo, uint32_t c_hi, uint64_t m) {
+  hipStream_t s = ix.stream;
+  const uint64_t n = ix.n;
+  SlicePlan P = plan_slice(ix, c_lo, c_hi, sizeof(V) == 8);
+  const KeyGeom& kk = P.kk;
+  upload_geometry(ix, kk);
+  ix.info[3] = (uint64_t)kk.q;
+  ix.info[7] |= 4 | (P.packed ? 2 : 0);
+  // units: ~0.9 of the slice density per sub-tile keeps the kept suffixes of a unit within one tile
+  {
+    const double ratio = m ? (double)n / (double)m : 1.0;
+    uint32_t g = (uint32_t)std::floor(0.9 * ratio);
+    if (g < 1) g = 1;
+    if (g > 64) g = 64;
+    P.sl.g = g;
+  }
+  const uint8_t* small = ix.small.as<uint8_t>();
+  const KeyChunks kch = key_chunks(kk.Rk, kk.q);
+  KeyedArgs ka{kk.Rk, kch.Rck, kch.Rlast, kk.s_start, kk.q, kch.ck, kk.pb, 0, P.lb};
+  const TextKeySrc tks{ix.text.as<uint8_t>(), n, reinterpret_cast<const uint16_t*>(small + 2560),
+                       reinterpret_cast<const uint16_t*>(small + 4608), reinterpret_cast<const uint64_t*>(small + 3584),
+                       ka};
+  for (int i = 0; i < 2; ++i) {
+    ix.keys[i].ensure(m * 8 + 16);
+    ix.vals[i].ensure(m * sizeof(V) + 16);   // u32 here; the tie refinement sorts V values in them
+  }
+  uint64_t* kp[2] = {ix.keys[0].as<uint64_t>(), ix.keys[1].as<uint64_t>()};
+  uint32_t* vp[2] = {ix.vals[0].as<uint32_t>(), ix.vals[1].as<uint32_t>()};
+  PackedRecs pkr;
+  if (P.packed) {
+    pkr.g = P.pg;
+    for (int b = 0; b < 256; ++b) pkr.lutp2[b] = pkr.g.tcode < 0 ? kk.lutp[b] : (kk.kflag[b] ? kk.kdig[b] : 0);
+    pkr.kfull = kp[1];
+    pkr.vfull = vp[1];
+    pkr.uhb = P.uhb;
+  }
+  std::vector<uint64_t> hist;
+  const int slot = cursor_partition_slice(ix, P, tks, m, kp, vp, hist, pkr);
+  const int sbx = P.sl.bsh + P.D;   // bits of the slice-relative sym field
+  const int lhb = P.packed ? P.uhb : P.hb;
+  uint64_t hmax = 0;
+  for (uint64_t c : hist) hmax = std::max(hmax, c);
+  const uint64_t cap = hmax <= (uint64_t)512 * BS_I ? (uint64_t)512 * BS_I : (uint64_t)BS_CAP;
+  const BucketPlan plan = plan_buckets(hist, P.sl.bsh, cap, P.packed ? P.sl.sA : 32);
+  ix.info[4] = plan.items_n.size() + plan.items_w.size();
+  ix.info[5] = plan.big_start.size();
+  ix.info[6] = plan.big_total;
+  static const bool dbg = getenv("HKCSA_SHARD_DEBUG") != nullptr;
+  if (dbg)
+    fprintf(stderr, "[slice-k] m=%llu q=%d sb=%d f=%d bsh=%d D=%d nb=%u g=%u packed=%d pbits=%d hmax=%llu items=%zu big=%zu\n",
+            (unsigned long long)m, kk.q, kk.sym_bits, P.sl.DB - 16, P.sl.bsh, P.D, P.sl.nb, P.sl.g, P.packed ? 1 : 0,
+            P.sl.pbits, (unsigned long long)hmax, plan.items_n.size() + plan.items_w.size(), plan.big_start.size());
+  ix.bwt.ensure(m + 64);
+  if (!plan.big_total && !(ix.flags & kFlagGlobalSort)) {
+    const uint64_t ntie = sort_bucket_items<V>(ix, plan, kp[slot], vp[slot], m, P.pb, sbx, P.packed ? 0 : P.hb, 0,
+                                               ix.sa.as<V>(), ix.bwt.as<uint8_t>(), P.packed ? &pkr : nullptr);
+    ix.info.push_back(ntie);
+    refine_from_ties<V>(ix, kk, ntie, false);
+    return;
+  }
+  // big buckets (skewed text) or HKCSA_FLAG_GLOBAL_SORT: full LSD sort of the slice's keys
+  ix.info[7] |= 1;
+  int ks = slot;
+  if (P.packed) {   // key planes first (slot 1; each record's region found in the pass A starts)
+    std::vector<uint2> ch;
+    for (uint64_t a = 0; a < m; a += 65536)
+      ch.push_back(make_uint2((uint32_t)a, (uint32_t)std::min<uint64_t>(65536, m - a)));
+    if (!ch.empty()) {
+      ix.bk_items.ensure(ch.size() * sizeof(uint2) + 16);
+      HK_HIP(hipMemcpyAsync(ix.bk_items.p, ch.data(), ch.size() * sizeof(uint2), hipMemcpyHostToDevice, s));
+      unpack_items(ix, pkr, kp[slot], ix.bk_items.as<uint2>(), (uint32_t)ch.size());
+    }
+    HK_HIP(hipStreamSynchronize(s));   // ch is freed at the end of this block
+    ks = 1;
+  }
+  const int pbe = P.pb + lhb;
+  if (lhb) {
+    const int sl2 = radix_sort_pairs<uint32_t>(ix.sw, ix.timer, kp, vp, ks, m, pbe, pbe + sbx, false, s);
+    ix.info[0] += ix.sw.passes_run;
+    ix.info[1] += ix.sw.passes_skipped;
+    TimedLaunch t(ix.timer, "shard_split_join", (double)m * (8 + 4 + 8 + 8));
+    k_split_join_keys<<<grid_of(m), 256, 0, s>>>(kp[sl2], vp[sl2], m, lhb, ix.sa.as<uint64_t>());
+    HK_HIP(hipGetLastError());
+    refine_after_sort<V>(ix, kk, sl2, m, false);
+  } else {
+    V* vq[2] = {reinterpret_cast<V*>(vp[0]), reinterpret_cast<V*>(vp[1])};
+    if (sizeof(V) == 8) throw ApiError{-1, "slice: u64 positions need split position bits"};
+    const int sl2 = radix_sort_pairs<V>(ix.sw, ix.timer, kp, vq, ks, m, P.pb, P.pb + sbx, false, s);
+    ix.info[0] += ix.sw.passes_run;
+    ix.info[1] += ix.sw.passes_skipped;
+    std::swap(ix.sa, ix.vals[sl2]);
+    ix.vals[sl2].ensure(m * sizeof(V) + 16);
+    refine_after_sort<V>(ix, kk, sl2, m, false);
+  }
+}
+
+template void build_slice_keyed<uint32_t>(Index&, uint32_t, uint32_t, uint64_t);
+template void build_slice_keyed<uint64_t>(Index&, uint32_t, uint32_t, uint64_t);
 
 // ---------------------------------------------------------------- driver
 void build_sa_bucketed(Index& ix) {

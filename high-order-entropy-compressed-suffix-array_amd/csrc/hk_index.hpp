@@ -214,7 +214,8 @@ void comm_unique_id(uint8_t id[128]);
 
 // shared by the single-GPU and sharded builds
 KeyGeom key_geometry(Index& ix, bool with_prev);
-KeyGeom key_geometry_keyed(Index& ix, int reserve = 0);   // keyed layout; reserve = low key bits kept free
+// keyed layout; reserve = low key bits kept free; q >= min_q, sym bits <= max_sb (sharded slices)
+KeyGeom key_geometry_keyed(Index& ix, int reserve = 0, int min_q = 1, int max_sb = 64);
 void build_sa_bucketed(Index& ix);       // single-GPU SA + BWT: 2 LSD passes + LDS bucket sorts
 // Bucket bins of one slice's sym fields, all within [kmin, kmax]: shift bins (sym - kmin) >> bsh, or
 // multiplicative bins hi64((sym - kmin) * mul) (exactly 2^16 over the range, stored in the key at
@@ -231,6 +232,15 @@ SliceBins slice_bins(uint64_t m, const KeyGeom& kg, int hb, uint64_t kmin, uint6
 // a bucket exceeds one LDS sort.
 template <typename V>
 bool bucket_sort_slice(Index& ix, const KeyGeom& kg, uint64_t m, int hb, const SliceBins& bins, const uint64_t* d_h0);
+// Keyed coarse scheme of the sharded build (texts whose keyed radix is 2^lb, lb in {1, 2, 4, 8}): the
+// partition bucket of a suffix is the top 16 bits of its keyed sym field (its first 16 / lb symbols).
+int shard_keyed_lb(Index& ix);                                               // lb, 0: scheme not applicable
+bool shard_keyed(Index& ix);                                                 // the keyed scheme applies
+void shard_coarse_hist(Index& ix, uint64_t lo, uint64_t hi, uint64_t* d_hist);   // exact, 65536 bins, [lo, hi)
+// SA + BWT of the slice of coarse buckets [c_lo, c_hi) (m suffixes): fused selection + cursor partition
+// over the whole text, LDS bucket sorts, tie refinement (ties outlasting the chunk rounds left pending)
+template <typename V>
+void build_slice_keyed(Index& ix, uint32_t c_lo, uint32_t c_hi, uint64_t m);
 // tie list (J << 1 | head, P) of m entries in (k, v) -> refinement loop (from symbol offset h)
 template <typename V>
 void refine_from_ties(Index& ix, const KeyGeom& kg, uint64_t A, bool allow_doubling);

@@ -1165,6 +1165,7 @@ void release_workspace(Index& ix) {
   ix.tile_e.release();
   ix.upd.release();
   ix.cp_part.release();
+  ix.sel.release();
   ix.cp_cur.release();
   ix.cp_tiles.release();
   ix.sw.status.release();

@@ -1,21 +1,31 @@
 // hk_shard.hip — suffix-array construction sharded over the GPUs of one node.
 //
 // Every rank holds the same T' (≤ 288 GB HBM each makes replication cheap) and owns one
-// contiguous range of the FINAL suffix array:
-//   1. each rank histograms the 14-bit key prefix of every 64th position of its block; one RCCL
-//      all-reduce gives the sampled global histogram, from which all ranks derive the same
-//      splitter buckets B_1 < ... < B_{N-1};
+// contiguous range of the FINAL suffix array.  Two partition schemes, chosen from the alphabet
+// (identically on every rank):
+//
+// Keyed coarse scheme (whole-symbol keyed radix 2^lb: DNA, binary, 16 or 256 symbols):
+//   1. each rank counts, exactly, the coarse bucket (the top 16 bits of the keyed sym field = the
+//      first 16 / lb symbols) of every suffix of its block; ONE RCCL all-reduce of the 65536 counts
+//      gives every rank the exact global histogram, hence identical splitters C_r and exact slice
+//      bounds (no second counting pass);
+//   2. each rank builds its slice with the single-GPU pipeline fused with the selection
+//      (hk_bucket.hip §1c): a pre-pass over T' counts the slice's bins, pass A scans T', keeps the
+//      slice's suffixes and scatters packed records by digit, then pass B, the LDS bucket sorts and
+//      the tie refinement.
+// Partition-key scheme (any other alphabet):
+//   1. each rank histograms the 14-bit radix-(sigma+1) key prefix of every 64th position of its
+//      block; an RCCL all-reduce gives the sampled global histogram and the splitter buckets;
 //   2. each rank counts, over its block, the suffixes below every splitter (a register-only byte
 //      pre-test against the splitters' prefix images); a second all-reduce of N+1 counts gives
 //      the exact slice bounds [lo, hi) of every rank;
 //   3. each rank scans all of T' and keeps the suffixes whose bucket it owns (count + scan +
 //      write, reading T' twice, writing only its ~n/N pairs);
-//   4. it radix-sorts its slice by the q-symbol key and refines tied groups by sorting on
-//      (dense group ordinal, next symbols of the suffix) read straight from the replicated
-//      text — no rank exchange is needed because every comparison stays inside one slice;
-//   5. an RCCL all-gather of the slice bounds checks that the slices tile [0, n).
-// Positions are 64-bit when n ≥ 2^32 (the 4 GiB + 1 config); they are sorted as u32 low halves
-// with the high bits parked below the key.
+//   4. it sorts its slice by the q-symbol key and refines tied groups by sorting on
+//      (dense group ordinal, next symbols of the suffix) read straight from the replicated text.
+// Both: an RCCL all-gather of per-rank status records checks that the slices tile [0, n); groups
+// still tied after the chunk rounds finish by prefix doubling with an ISA rank exchange.
+// Positions are 64-bit when n ≥ 2^32 (the 4 GiB + 1 config).
 
 #include <rccl/rccl.h>
 
@@ -34,6 +44,7 @@ namespace {
 
 constexpr int SH_BUCKET_BITS = 14;
 constexpr int SH_BUCKETS = 1 << SH_BUCKET_BITS;
+constexpr int SH_KBUCKETS = 65536;   // keyed coarse scheme: the top 16 sym bits (hkcsa_shard_buckets())
 constexpr int PS_TILE = 4096;
 constexpr int SH_SAMPLE = 64;   // histogram sample stride (splitters need balance, not exact counts)
 
@@ -603,17 +614,31 @@ BelowImg below_img(const PrefixImages& pi, const BucketGeom& g, uint32_t B) {
   return im;
 }
 
-// splitter buckets B_0 = 0 < ... < B_N = SH_BUCKETS from the sampled global histogram
-std::vector<uint32_t> splitters(const uint64_t* ghist, int nranks) {
-  std::vector<uint64_t> cum(SH_BUCKETS + 1, 0);
-  for (int i = 0; i < SH_BUCKETS; ++i) cum[i + 1] = cum[i] + ghist[i];
-  const uint64_t tot = cum[SH_BUCKETS];
+// splitter buckets B_0 = 0 < ... < B_N = nb from a global histogram of nb bins: B_r = the smallest B
+// with cum[B] >= floor(total * r / N).  aligned (keyed scheme): when N divides nb and the equal-width
+// splitters B_r = r * nb / N leave no slice 2 % above total / N, those are taken instead (iid text: a
+// slice of exactly 2^k coarse buckets gets 2^17 bins, where a balanced 2^k + 1 would get half as many).
+// hkcsa/shard.py split_buckets restates this rule.
+std::vector<uint32_t> splitters(const uint64_t* ghist, int nranks, int nb = SH_BUCKETS, bool aligned = false) {
+  std::vector<uint64_t> cum(nb + 1, 0);
+  for (int i = 0; i < nb; ++i) cum[i + 1] = cum[i] + ghist[i];
+  const uint64_t tot = cum[nb];
   std::vector<uint32_t> B(nranks + 1);
+  if (aligned && nb % nranks == 0) {
+    bool ok = true;
+    const uint64_t cap = tot / (uint64_t)nranks + tot / (uint64_t)nranks / 50;
+    for (int r = 0; r < nranks && ok; ++r)
+      ok = cum[(uint64_t)nb * (r + 1) / nranks] - cum[(uint64_t)nb * r / nranks] <= cap;
+    if (ok) {
+      for (int r = 0; r <= nranks; ++r) B[r] = (uint32_t)((uint64_t)nb * r / nranks);
+      return B;
+    }
+  }
   for (int r = 0; r <= nranks; ++r) {
     if (r == 0) { B[r] = 0; continue; }
-    if (r == nranks) { B[r] = SH_BUCKETS; continue; }
+    if (r == nranks) { B[r] = (uint32_t)nb; continue; }
     const uint64_t target = (uint64_t)((__uint128_t)tot * (uint64_t)r / (uint64_t)nranks);
-    uint32_t lo = 0, hi = SH_BUCKETS;
+    uint32_t lo = 0, hi = (uint32_t)nb;
     while (lo < hi) {  // smallest B with cum[B] >= target
       const uint32_t mid = (lo + hi) / 2;
       if (cum[mid] >= target) hi = mid; else lo = mid + 1;
@@ -621,6 +646,14 @@ std::vector<uint32_t> splitters(const uint64_t* ghist, int nranks) {
     B[r] = lo;
   }
   return B;
+}
+
+// rank r's block of T' for the per-rank histograms: 16-aligned starts (the last block ends at n)
+std::pair<uint64_t, uint64_t> block_of(uint64_t n, int nranks, int rank) {
+  const uint64_t b0 = rank ? ((uint64_t)((__uint128_t)n * (uint64_t)rank / (uint64_t)nranks) & ~15ull) : 0;
+  const uint64_t b1 =
+      rank + 1 < nranks ? ((uint64_t)((__uint128_t)n * (uint64_t)(rank + 1) / (uint64_t)nranks) & ~15ull) : n;
+  return {b0, b1};
 }
 
 // Bounds of the keyed sym fields of the suffixes whose partition bucket lies in [blo, bhi), from
@@ -818,15 +851,53 @@ void shard_build_t(Index& ix, const uint64_t* ghist, const uint64_t* gbelow, int
   ix.have_sa = ix.have_bwt = !ix.dbl.pending;   // BWT of the slice (bwt[j] for SA[lo + j])
 }
 
+// Keyed coarse scheme: rank r owns the coarse buckets [C_r, C_{r+1}) (splitters of the exact global
+// histogram) and its SA slice is [cum(C_r), cum(C_{r+1})).  gbelow (hkcsa_shard_build's global counts)
+// must agree with the histogram.
+template <typename V>
+void shard_build_keyed(Index& ix, const uint64_t* ghist, const uint64_t* gbelow, int nranks, int rank) {
+  const uint64_t n = ix.n;
+  const std::vector<uint32_t> B = splitters(ghist, nranks, SH_KBUCKETS, true);
+  std::vector<uint64_t> cum(SH_KBUCKETS + 1, 0);
+  for (int c = 0; c < SH_KBUCKETS; ++c) cum[c + 1] = cum[c] + ghist[c];
+  if (cum[SH_KBUCKETS] != n) throw ApiError{-7, "keyed coarse histogram does not count every suffix"};
+  for (int r = 0; r <= nranks; ++r)
+    if (gbelow[r] != cum[B[r]]) throw ApiError{-7, "global splitter counts disagree with the coarse histogram"};
+  ix.shard_lo = cum[B[rank]];
+  ix.shard_hi = cum[B[rank + 1]];
+  const uint64_t m = ix.shard_hi - ix.shard_lo;
+  ix.info.assign(9, 0);
+  ix.dbl = Index::DblState{};
+  ix.sharded = true;
+  ix.sa_pos64 = sizeof(V) == 8;
+  ix.have_sa = ix.have_bwt = ix.have_wt = false;
+  ix.sa.ensure(m * sizeof(V) + 16);
+  ix.bwt.ensure(m + 64);
+  if (!m) {
+    ix.have_sa = ix.have_bwt = true;
+    return;
+  }
+  build_slice_keyed<V>(ix, B[rank], B[rank + 1], m);
+  HK_HIP(hipStreamSynchronize(ix.stream));
+  ix.have_sa = ix.have_bwt = !ix.dbl.pending;   // pending: the rank exchange finishes the slice
+}
+
 }  // namespace
 
+bool shard_keyed(Index& ix) { return shard_keyed_lb(ix) > 0; }
+
 void shard_histogram(Index& ix, int nranks, int rank, uint64_t* d_hist) {
+  if (shard_keyed(ix)) {   // exact coarse histogram of the 16-aligned block
+    const auto b = block_of(ix.n, nranks, rank);
+    shard_coarse_hist(ix, b.first, b.second, d_hist);
+    return;
+  }
   KeyGeom kg = partition_geometry(ix);
   hipStream_t s = ix.stream;
   const uint64_t lo = (uint64_t)((__uint128_t)ix.n * (uint64_t)rank / (uint64_t)nranks);
   const uint64_t hi = (uint64_t)((__uint128_t)ix.n * (uint64_t)(rank + 1) / (uint64_t)nranks);
   upload_geometry(ix, kg);
-  HK_HIP(hipMemsetAsync(d_hist, 0, SH_BUCKETS * 8, s));
+  HK_HIP(hipMemsetAsync(d_hist, 0, SH_KBUCKETS * 8, s));
   if (hi > lo) {
     TimedLaunch t(ix.timer, "shard_hist", (double)(hi - lo) / SH_SAMPLE * (kg.q + 1));
     k_shard_hist<<<grid_for((hi - lo) / SH_SAMPLE + 1, 256, 512), 256, 0, s>>>(
@@ -838,6 +909,25 @@ void shard_histogram(Index& ix, int nranks, int rank, uint64_t* d_hist) {
 
 void shard_counts(Index& ix, const uint64_t* h_global_hist, int nranks, int rank, uint64_t* d_below) {
   if (nranks > SH_MAX_RANKS) throw ApiError{-2, "at most 64 ranks"};
+  if (shard_keyed(ix)) {   // the block's exact coarse counts, summed below every splitter
+    const std::vector<uint32_t> B = splitters(h_global_hist, nranks, SH_KBUCKETS, true);
+    const auto b = block_of(ix.n, nranks, rank);
+    DevBuf d;
+    d.ensure(SH_KBUCKETS * 8);
+    shard_coarse_hist(ix, b.first, b.second, d.as<uint64_t>());
+    std::vector<uint64_t> bh(SH_KBUCKETS), below(nranks + 1, 0);
+    HK_HIP(hipMemcpyAsync(bh.data(), d.p, SH_KBUCKETS * 8, hipMemcpyDeviceToHost, ix.stream));
+    HK_HIP(hipStreamSynchronize(ix.stream));
+    uint64_t acc = 0;
+    uint32_t c = 0;
+    for (int r = 0; r <= nranks; ++r) {
+      while (c < B[r]) acc += bh[c++];
+      below[r] = acc;
+    }
+    HK_HIP(hipMemcpyAsync(d_below, below.data(), (nranks + 1) * 8, hipMemcpyHostToDevice, ix.stream));
+    HK_HIP(hipStreamSynchronize(ix.stream));
+    return;
+  }
   KeyGeom kg = partition_geometry(ix);
   hipStream_t s = ix.stream;
   const uint64_t lo = (uint64_t)((__uint128_t)ix.n * (uint64_t)rank / (uint64_t)nranks);
@@ -863,13 +953,17 @@ void shard_counts(Index& ix, const uint64_t* h_global_hist, int nranks, int rank
 }
 
 void shard_build(Index& ix, const uint64_t* h_global_hist, const uint64_t* h_global_below, int nranks, int rank) {
-  if (ix.n > 0xFFFFFFFEull || (ix.flags & kFlagPos64))
-    shard_build_t<uint64_t>(ix, h_global_hist, h_global_below, nranks, rank);
-  else
-    shard_build_t<uint32_t>(ix, h_global_hist, h_global_below, nranks, rank);
+  const bool keyed = shard_keyed(ix);
+  if (ix.n > 0xFFFFFFFEull || (ix.flags & kFlagPos64)) {
+    if (keyed) shard_build_keyed<uint64_t>(ix, h_global_hist, h_global_below, nranks, rank);
+    else shard_build_t<uint64_t>(ix, h_global_hist, h_global_below, nranks, rank);
+  } else {
+    if (keyed) shard_build_keyed<uint32_t>(ix, h_global_hist, h_global_below, nranks, rank);
+    else shard_build_t<uint32_t>(ix, h_global_hist, h_global_below, nranks, rank);
+  }
 }
 
-int shard_buckets() { return SH_BUCKETS; }
+int shard_buckets() { return SH_KBUCKETS; }
 int shard_sample() { return SH_SAMPLE; }
 
 void shard_get_bwt(Index& ix, uint64_t a, uint64_t b, uint8_t* out) {
@@ -888,10 +982,7 @@ void shard_get_sa(Index& ix, uint64_t a, uint64_t b, uint64_t* out) {
   if (ix.sa_pos64) {
     HK_HIP(hipMemcpyAsync(out, ix.sa.as<uint64_t>() + a, (b - a) * 8, hipMemcpyDeviceToHost, s));
   } else {
-    std::vector<uint32_t> tmp(b - a);
-    HK_HIP(hipMemcpyAsync(tmp.data(), ix.sa.as<uint32_t>() + a, (b - a) * 4, hipMemcpyDeviceToHost, s));
-    HK_HIP(hipStreamSynchronize(s));
-    for (uint64_t i = 0; i < b - a; ++i) out[i] = tmp[i];
+    sa_to_host_u64(ix, a, b - a, out);   // widened on the GPU in chunks, straight into `out`
   }
   HK_HIP(hipStreamSynchronize(s));
 }
@@ -998,11 +1089,10 @@ void ragged_allgather(Index& ix, const uint8_t* mine, const std::vector<uint64_t
 // every rank keeps a replica of the global ISA, built from an all-gather of the SA slices and
 // refreshed after each round by an all-gather of the (position, ISA) pairs of the suffixes that
 // round re-ranked.  K = the smallest common-prefix length of any group still tied anywhere.
-void shard_doubling(Index& ix, std::vector<RankStatus> st, DevBuf& sbuf) {
+// agreed: set while the error being thrown is known to every rank (a status exchange reported it)
+void shard_doubling_rounds(Index& ix, std::vector<RankStatus> st, DevBuf& sbuf, DevBuf& gb, bool& agreed) {
   const int N = g_comm.nranks, me = g_comm.rank;
   const size_t V = ix.sa_pos64 ? 8 : 4;
-  DevBuf gb;
-  dbl_ensure_isa(ix);
   {
     std::vector<uint64_t> cnt(N);
     for (int r = 0; r < N; ++r) cnt[r] = st[r].hi - st[r].lo;
@@ -1032,8 +1122,10 @@ void shard_doubling(Index& ix, std::vector<RankStatus> st, DevBuf& sbuf) {
       HK_HIP(hipStreamSynchronize(ix.stream));
     }, emsg, ecode);
     const RankStatus mine{ix.shard_lo, ix.shard_hi, err ? 0 : ix.dbl.A, ix.dbl.h, err ? 0 : ix.dbl.npairs, err};
+    agreed = true;   // a peer's failure is thrown by gather_status itself, after the exchange
     st = gather_status(ix, mine, sbuf);
     if (err) throw ApiError{ecode, emsg};
+    agreed = false;
     uint64_t tot = 0;
     for (int r = 0; r < N; ++r) tot += st[r].A;
     if (!tot) break;
@@ -1041,6 +1133,36 @@ void shard_doubling(Index& ix, std::vector<RankStatus> st, DevBuf& sbuf) {
   (void)me;
   ix.dbl.pending = false;
   ix.have_sa = ix.have_bwt = true;
+}
+
+
+// The allocations a rank can fail on (the ISA replica, the gather staging) run first, under local_step,
+// and one status exchange makes every rank leave together before any all-gather; a failure after that
+// (a launch inside a gather's visit) aborts the communicator so that peers see their collective fail.
+void shard_doubling(Index& ix, std::vector<RankStatus> st, DevBuf& sbuf) {
+  const int N = g_comm.nranks, me = g_comm.rank;
+  const size_t V = ix.sa_pos64 ? 8 : 4;
+  DevBuf gb;
+  {
+    uint64_t mx = 1;
+    for (int r = 0; r < N; ++r) mx = std::max(mx, st[r].hi - st[r].lo);
+    std::string emsg;
+    int ecode = 0;
+    const uint64_t err = local_step([&] {
+      dbl_ensure_isa(ix);
+      gb.ensure(std::max((size_t)N * std::min(kIsaChunk, mx) * V, (size_t)N * kPairChunk * 16) + 64);
+    }, emsg, ecode);
+    const RankStatus mine{ix.shard_lo, ix.shard_hi, st[me].A, st[me].h, st[me].npairs, err};
+    st = gather_status(ix, mine, sbuf);
+    if (err) throw ApiError{ecode, emsg};
+  }
+  bool agreed = false;
+  try {
+    shard_doubling_rounds(ix, st, sbuf, gb, agreed);
+  } catch (...) {
+    if (!agreed) comm_abort();
+    throw;
+  }
 }
 
 }  // namespace
@@ -1061,16 +1183,13 @@ void build_sa_sharded(Index& ix, const uint8_t id[128], int nranks, int rank) {
   std::string emsg;
   int ecode = 0;
   DevBuf hist;
-  hist.ensure((SH_BUCKETS + 1) * 8 + 64);
+  hist.ensure((SH_KBUCKETS + 1) * 8 + 64);
   // phase 0: every build recomputes the byte histogram / C (utils/utils.py:16-24): each rank counts
   // its 16-aligned block of T' and an all-reduce sums them (+ a failure slot), so no rank reads
   // all of T' for it
   uint64_t err = local_step([&] {
-    const uint64_t b0 = rank ? ((uint64_t)((__uint128_t)ix.n * (uint64_t)rank / (uint64_t)nranks) & ~15ull) : 0;
-    const uint64_t b1 = rank + 1 < nranks
-                            ? ((uint64_t)((__uint128_t)ix.n * (uint64_t)(rank + 1) / (uint64_t)nranks) & ~15ull)
-                            : ix.n;
-    byte_hist_range(ix, b0, b1, hist.as<unsigned long long>());
+    const auto b = block_of(ix.n, nranks, rank);
+    byte_hist_range(ix, b.first, b.second, hist.as<unsigned long long>());
   }, emsg, ecode);
   {
     const uint64_t e1 = err ? 1 : 0;
@@ -1086,32 +1205,51 @@ void build_sa_sharded(Index& ix, const uint8_t id[128], int nranks, int rank) {
     if (bh[256]) throw ApiError{-8, "sharded build failed on a peer rank (byte histogram)"};
     set_alphabet(ix, bh.data());
   }
-  // phase 1: sampled partition histogram; the extra bin carries failures (summed)
-  err = local_step([&] { shard_histogram(ix, nranks, rank, hist.as<uint64_t>()); }, emsg, ecode);
+  // phase 1: partition histogram (keyed scheme: exact coarse counts of the block; else the sampled
+  // partition-key histogram); the extra bin carries failures (summed)
+  bool keyed = false;
+  err = local_step([&] {
+    keyed = shard_keyed(ix);
+    shard_histogram(ix, nranks, rank, hist.as<uint64_t>());
+  }, emsg, ecode);
+  // every rank reduces the same count whatever its scheme decision (a failed rank could not know it);
+  // the partition-key scheme leaves the bins past SH_BUCKETS zero
+  const int nbh = SH_KBUCKETS;
   {
     const uint64_t e1 = err ? 1 : 0;
-    HK_HIP(hipMemcpyAsync(hist.as<uint64_t>() + SH_BUCKETS, &e1, 8, hipMemcpyHostToDevice, s));
-    TimedLaunch t(ix.timer, "rccl_allreduce_hist", (double)SH_BUCKETS * 8);
-    nccl_do(ncclAllReduce(hist.p, hist.p, SH_BUCKETS + 1, ncclUint64, ncclSum, g_comm.comm, s), "ncclAllReduce");
+    HK_HIP(hipMemcpyAsync(hist.as<uint64_t>() + nbh, &e1, 8, hipMemcpyHostToDevice, s));
+    TimedLaunch t(ix.timer, "rccl_allreduce_hist", (double)nbh * 8);
+    nccl_do(ncclAllReduce(hist.p, hist.p, nbh + 1, ncclUint64, ncclSum, g_comm.comm, s), "ncclAllReduce");
   }
-  std::vector<uint64_t> h(SH_BUCKETS + 1);
-  HK_HIP(hipMemcpyAsync(h.data(), hist.p, (SH_BUCKETS + 1) * 8, hipMemcpyDeviceToHost, s));
+  std::vector<uint64_t> h(SH_KBUCKETS + 1, 0);
+  HK_HIP(hipMemcpyAsync(h.data(), hist.p, (nbh + 1) * 8, hipMemcpyDeviceToHost, s));
   HK_HIP(hipStreamSynchronize(s));
   if (err) throw ApiError{ecode, emsg};
-  if (h[SH_BUCKETS]) throw ApiError{-8, "sharded build failed on a peer rank (histogram)"};
-  // phase 2: exact slice sizes: per-rank counts below every splitter, summed (+ failure slot)
-  err = local_step([&] { shard_counts(ix, h.data(), nranks, rank, hist.as<uint64_t>()); }, emsg, ecode);
-  {
-    const uint64_t e1 = err ? 1 : 0;
-    HK_HIP(hipMemcpyAsync(hist.as<uint64_t>() + nranks + 1, &e1, 8, hipMemcpyHostToDevice, s));
-    TimedLaunch t(ix.timer, "rccl_allreduce_counts", (double)(nranks + 2) * 8);
-    nccl_do(ncclAllReduce(hist.p, hist.p, nranks + 2, ncclUint64, ncclSum, g_comm.comm, s), "ncclAllReduce");
+  if (h[nbh]) throw ApiError{-8, "sharded build failed on a peer rank (histogram)"};
+  std::vector<uint64_t> below(nranks + 2, 0);
+  if (keyed) {
+    // exact counts: the slice bounds follow from the histogram itself (no second collective)
+    const std::vector<uint32_t> B = splitters(h.data(), nranks, SH_KBUCKETS, true);
+    uint64_t acc = 0;
+    uint32_t c = 0;
+    for (int r = 0; r <= nranks; ++r) {
+      while (c < B[r]) acc += h[c++];
+      below[r] = acc;
+    }
+  } else {
+    // phase 2: exact slice sizes: per-rank counts below every splitter, summed (+ failure slot)
+    err = local_step([&] { shard_counts(ix, h.data(), nranks, rank, hist.as<uint64_t>()); }, emsg, ecode);
+    {
+      const uint64_t e1 = err ? 1 : 0;
+      HK_HIP(hipMemcpyAsync(hist.as<uint64_t>() + nranks + 1, &e1, 8, hipMemcpyHostToDevice, s));
+      TimedLaunch t(ix.timer, "rccl_allreduce_counts", (double)(nranks + 2) * 8);
+      nccl_do(ncclAllReduce(hist.p, hist.p, nranks + 2, ncclUint64, ncclSum, g_comm.comm, s), "ncclAllReduce");
+    }
+    HK_HIP(hipMemcpyAsync(below.data(), hist.p, (nranks + 2) * 8, hipMemcpyDeviceToHost, s));
+    HK_HIP(hipStreamSynchronize(s));
+    if (err) throw ApiError{ecode, emsg};
+    if (below[nranks + 1]) throw ApiError{-8, "sharded build failed on a peer rank (slice counts)"};
   }
-  std::vector<uint64_t> below(nranks + 2);
-  HK_HIP(hipMemcpyAsync(below.data(), hist.p, (nranks + 2) * 8, hipMemcpyDeviceToHost, s));
-  HK_HIP(hipStreamSynchronize(s));
-  if (err) throw ApiError{ecode, emsg};
-  if (below[nranks + 1]) throw ApiError{-8, "sharded build failed on a peer rank (slice counts)"};
   // phase 3: the slice sort; then every rank's bounds / tied count are exchanged
   err = local_step([&] { shard_build(ix, h.data(), below.data(), nranks, rank); }, emsg, ecode);
   DevBuf sbuf;
@@ -1143,21 +1281,41 @@ void shard_replicate(Index& ix) {
   const size_t V = ix.sa_pos64 ? 8 : 4;
   hipStream_t s = ix.stream;
   std::vector<uint64_t> cnt(N);
-  for (int r = 0; r < N; ++r) cnt[r] = ix.shard_bounds[r + 1] - ix.shard_bounds[r];
-  DevBuf full_sa, full_bwt, gb;
-  full_sa.ensure(n * V + 16);
-  full_bwt.ensure(n + 64);
-  ragged_allgather(ix, ix.sa.as<uint8_t>(), cnt, V, kIsaChunk, gb, "rccl_allgather_sa",
-                   [&](int r, const uint8_t* p, uint64_t c, uint64_t off) {
-                     HK_HIP(hipMemcpyAsync(full_sa.as<uint8_t>() + (ix.shard_bounds[r] + off) * V, p, c * V,
-                                           hipMemcpyDeviceToDevice, s));
-                   });
-  ragged_allgather(ix, ix.bwt.as<uint8_t>(), cnt, 1, kIsaChunk * 8, gb, "rccl_allgather_bwt",
-                   [&](int r, const uint8_t* p, uint64_t c, uint64_t off) {
-                     HK_HIP(hipMemcpyAsync(full_bwt.as<uint8_t>() + ix.shard_bounds[r] + off, p, c,
-                                           hipMemcpyDeviceToDevice, s));
-                   });
-  HK_HIP(hipStreamSynchronize(s));
+  uint64_t mx = 1;
+  for (int r = 0; r < N; ++r) {
+    cnt[r] = ix.shard_bounds[r + 1] - ix.shard_bounds[r];
+    mx = std::max(mx, cnt[r]);
+  }
+  DevBuf full_sa, full_bwt, gb, sbuf;
+  // the allocations first, then one status exchange: every rank leaves together if any failed
+  {
+    std::string emsg;
+    int ecode = 0;
+    const uint64_t err = local_step([&] {
+      full_sa.ensure(n * V + 16);
+      full_bwt.ensure(n + 64);
+      gb.ensure((size_t)N * std::max(std::min(kIsaChunk, mx) * V, std::min(kIsaChunk * 8, mx)) + 64);
+    }, emsg, ecode);
+    const RankStatus mine{ix.shard_lo, ix.shard_hi, 0, 0, 0, err};
+    (void)gather_status(ix, mine, sbuf);
+    if (err) throw ApiError{ecode, emsg};
+  }
+  try {
+    ragged_allgather(ix, ix.sa.as<uint8_t>(), cnt, V, kIsaChunk, gb, "rccl_allgather_sa",
+                     [&](int r, const uint8_t* p, uint64_t c, uint64_t off) {
+                       HK_HIP(hipMemcpyAsync(full_sa.as<uint8_t>() + (ix.shard_bounds[r] + off) * V, p, c * V,
+                                             hipMemcpyDeviceToDevice, s));
+                     });
+    ragged_allgather(ix, ix.bwt.as<uint8_t>(), cnt, 1, kIsaChunk * 8, gb, "rccl_allgather_bwt",
+                     [&](int r, const uint8_t* p, uint64_t c, uint64_t off) {
+                       HK_HIP(hipMemcpyAsync(full_bwt.as<uint8_t>() + ix.shard_bounds[r] + off, p, c,
+                                             hipMemcpyDeviceToDevice, s));
+                     });
+    HK_HIP(hipStreamSynchronize(s));
+  } catch (...) {
+    comm_abort();   // a peer may be waiting in the next all-gather
+    throw;
+  }
   std::swap(ix.sa, full_sa);
   std::swap(ix.bwt, full_bwt);
   ix.sharded = false;
@@ -1167,10 +1325,35 @@ void shard_replicate(Index& ix) {
   ix.have_wt = false;
 }
 
-// Host-assembled replica (hosts running their own collectives): the full SA and BWT.
+namespace {
+// adopted replica check: every entry < n and seen once (a bitmap, one atomic OR each; n entries, so
+// no duplicate means a permutation) and bwt[i] == T'[sa[i] - 1] (wrapping, csa/bwt.py:8-11); flags:
+// bit 0 out of range / duplicate, bit 1 BWT mismatch
+template <typename V>
+__global__ __launch_bounds__(256) void k_adopt_check(const V* __restrict__ sa, const uint8_t* __restrict__ bwt,
+                                                     const uint8_t* __restrict__ t, uint64_t n,
+                                                     uint32_t* __restrict__ seen, unsigned int* __restrict__ flag) {
+  uint32_t f = 0;
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
+    const uint64_t p = sa[i];
+    if (p >= n) {
+      f |= 1u;
+      continue;
+    }
+    const uint32_t bit = 1u << (p & 31);
+    if (atomicOr(&seen[p >> 5], bit) & bit) f |= 1u;
+    if (bwt[i] != t[p ? p - 1 : n - 1]) f |= 2u;
+  }
+  if (f) atomicOr(flag, f);
+}
+}  // namespace
+
+// Host-assembled replica (hosts running their own collectives): the full SA and BWT, checked on the
+// GPU (a permutation of [0, n) whose BWT rows match the text) before it replaces the slice.
 void shard_adopt(Index& ix, const uint64_t* h_sa, const uint8_t* h_bwt) {
   const uint64_t n = ix.n;
   hipStream_t s = ix.stream;
+  if (!ix.sharded) throw ApiError{-3, "adopt: the handle holds no sharded build"};
   const bool w64 = ix.sa_pos64 || n > 0xFFFFFFFFull;
   DevBuf full_sa, full_bwt;
   full_sa.ensure(n * (w64 ? 8 : 4) + 16);
@@ -1184,7 +1367,26 @@ void shard_adopt(Index& ix, const uint64_t* h_sa, const uint8_t* h_bwt) {
     HK_HIP(hipStreamSynchronize(s));
   }
   HK_HIP(hipMemcpyAsync(full_bwt.p, h_bwt, n, hipMemcpyHostToDevice, s));
-  HK_HIP(hipStreamSynchronize(s));
+  {
+    DevBuf seen;
+    seen.ensure((n / 32 + 1) * 4 + 16);
+    HK_HIP(hipMemsetAsync(seen.p, 0, (n / 32 + 1) * 4 + 16, s));
+    unsigned int* d_flag = reinterpret_cast<unsigned int*>(seen.as<uint8_t>() + (n / 32 + 1) * 4);
+    if (w64)
+      k_adopt_check<uint64_t><<<grid_for(n, 256, 8192), 256, 0, s>>>(full_sa.as<uint64_t>(), full_bwt.as<uint8_t>(),
+                                                                      ix.text.as<uint8_t>(), n, seen.as<uint32_t>(),
+                                                                      d_flag);
+    else
+      k_adopt_check<uint32_t><<<grid_for(n, 256, 8192), 256, 0, s>>>(full_sa.as<uint32_t>(), full_bwt.as<uint8_t>(),
+                                                                      ix.text.as<uint8_t>(), n, seen.as<uint32_t>(),
+                                                                      d_flag);
+    HK_HIP(hipGetLastError());
+    unsigned int flag = 0;
+    HK_HIP(hipMemcpyAsync(&flag, d_flag, 4, hipMemcpyDeviceToHost, s));
+    HK_HIP(hipStreamSynchronize(s));
+    if (flag & 1u) throw ApiError{-4, "adopt: the suffix array is not a permutation of [0, n)"};
+    if (flag & 2u) throw ApiError{-4, "adopt: BWT rows do not match T'[SA - 1]"};
+  }
   std::swap(ix.sa, full_sa);
   std::swap(ix.bwt, full_bwt);
   ix.sa_pos64 = w64;
@@ -1253,8 +1455,8 @@ void shard_apply_host(Index& ix, const uint64_t* h_pairs, uint64_t count) {
 }
 
 void shard_round(Index& ix, uint64_t K) {
-  if (!ix.sharded || !ix.dbl.pending) throw ApiError{-3, "no pending sharded prefix doubling"};
-  if (!ix.dbl.A) {   // already final: nothing to sort, no pairs
+  if (!ix.sharded) throw ApiError{-3, "index is not sharded"};
+  if (!ix.dbl.pending || !ix.dbl.A) {   // final (or never tied): nothing to sort, no pairs to re-send
     ix.dbl.npairs = 0;
     return;
   }

@@ -548,6 +548,16 @@ int hkcsa_comm_unique_id(uint8_t id[128]) {
 int hkcsa_shard_buckets(void) { return hk::shard_buckets(); }
 int hkcsa_shard_sample(void) { return hk::shard_sample(); }
 
+int hkcsa_shard_scheme(hkcsa_index* h, int* scheme) {
+  return guarded([&] {
+    activate(h);
+    need(scheme != nullptr, HKCSA_E_INVALID, "null output");
+    need(h->ix.have_text, HKCSA_E_STATE, "text released by hkcsa_compact");
+    h->ix.have_alpha = false;
+    *scheme = hk::shard_keyed(h->ix) ? 1 : 0;
+  });
+}
+
 int hkcsa_shard_histogram(hkcsa_index* h, int nranks, int rank, uint64_t* hist_out) {
   return guarded([&] {
     activate(h);
@@ -619,8 +629,8 @@ int hkcsa_shard_adopt(hkcsa_index* h, const uint64_t* sa, const uint8_t* bwt) {
     activate(h);
     need(sa && bwt, HKCSA_E_INVALID, "null argument");
     need(h->ix.have_text, HKCSA_E_STATE, "text released by hkcsa_compact");
-    for (uint64_t i = 0; i < h->ix.n; ++i) need(sa[i] < h->ix.n, HKCSA_E_RANGE, "suffix array entry out of range");
-    hk::shard_adopt(h->ix, sa, bwt);
+    need(h->ix.sharded, HKCSA_E_STATE, "adopt: the handle holds no sharded build");
+    hk::shard_adopt(h->ix, sa, bwt);   // checks the replica on the GPU (permutation, BWT rows)
   });
 }
 

@@ -78,6 +78,7 @@ _SIGS = [
     ("hkcsa_shard_buckets", C.c_int, []),
     ("hkcsa_shard_histogram", C.c_int, [vp, C.c_int, C.c_int, vp]),
     ("hkcsa_shard_sample", C.c_int, []),
+    ("hkcsa_shard_scheme", C.c_int, [vp, C.POINTER(C.c_int)]),
     ("hkcsa_shard_counts", C.c_int, [vp, vp, C.c_int, C.c_int, vp]),
     ("hkcsa_shard_build", C.c_int, [vp, vp, vp, C.c_int, C.c_int]),
     ("hkcsa_shard_status", C.c_int, [vp, vp]),

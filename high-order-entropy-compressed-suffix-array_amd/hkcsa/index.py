@@ -267,6 +267,12 @@ class DeviceIndex:
         b = np.frombuffer(uid, dtype=np.uint8)
         N.check(self.lib.hkcsa_build_sa_sharded(self.h, _ptr(b), nranks, rank))
 
+    def shard_scheme(self) -> int:
+        """1: keyed coarse partition (exact 65536-bin histogram), 0: sampled partition key."""
+        s = C.c_int(0)
+        N.check(self.lib.hkcsa_shard_scheme(self.h, C.byref(s)))
+        return s.value
+
     def shard_histogram(self, nranks: int, rank: int) -> np.ndarray:
         out = np.empty(self.lib.hkcsa_shard_buckets(), dtype=np.uint64)
         N.check(self.lib.hkcsa_shard_histogram(self.h, nranks, rank, _ptr(out)))
@@ -326,16 +332,26 @@ class DeviceIndex:
             raise ValueError("shard_adopt needs n SA entries and n BWT bytes")
         N.check(self.lib.hkcsa_shard_adopt(self.h, _ptr(s), _ptr(b)))
 
-    def shard_sa(self) -> np.ndarray:
+    def shard_sa(self, out: np.ndarray | None = None) -> np.ndarray:
+        """SA[lo:hi) of this rank (u64); `out` (a contiguous u64 array of hi - lo entries) is filled in
+        place when given."""
         lo, hi = self.shard_range()
-        out = np.empty(max(1, hi - lo), dtype=np.uint64)
-        N.check(self.lib.hkcsa_get_shard_sa(self.h, 0, hi - lo, _ptr(out)))
+        if out is None:
+            out = np.empty(max(1, hi - lo), dtype=np.uint64)
+        elif out.dtype != np.uint64 or not out.flags.c_contiguous or len(out) != hi - lo:
+            raise ValueError("shard_sa: out must be a contiguous u64 array of the slice's length")
+        if hi > lo:
+            N.check(self.lib.hkcsa_get_shard_sa(self.h, 0, hi - lo, _ptr(out)))
         return out[:hi - lo]
 
-    def shard_bwt(self) -> np.ndarray:
+    def shard_bwt(self, out: np.ndarray | None = None) -> np.ndarray:
         lo, hi = self.shard_range()
-        out = np.empty(max(1, hi - lo), dtype=np.uint8)
-        N.check(self.lib.hkcsa_get_shard_bwt(self.h, 0, hi - lo, _ptr(out)))
+        if out is None:
+            out = np.empty(max(1, hi - lo), dtype=np.uint8)
+        elif out.dtype != np.uint8 or not out.flags.c_contiguous or len(out) != hi - lo:
+            raise ValueError("shard_bwt: out must be a contiguous u8 array of the slice's length")
+        if hi > lo:
+            N.check(self.lib.hkcsa_get_shard_bwt(self.h, 0, hi - lo, _ptr(out)))
         return out[:hi - lo]
 
     # ------------------------------------------------------------ timing

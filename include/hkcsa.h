@@ -215,10 +215,21 @@ int hkcsa_get_shard_sa(hkcsa_index* ix, uint64_t a, uint64_t b, uint64_t* out);
  * bwt_transform (csa/bwt.py:4-9) emits for this rank's SA range. */
 int hkcsa_get_shard_bwt(hkcsa_index* ix, uint64_t a, uint64_t b, uint8_t* out);
 /* The same construction in three host-visible phases, for hosts that do their own
- * collectives (and for single-GPU tests of the partitioning).  Rank r's block is
- * the positions [n*r/N, n*(r+1)/N):
- *   hkcsa_shard_histogram: key-prefix histogram (hkcsa_shard_buckets() bins) of the
- *     block's positions p with p % hkcsa_shard_sample() == 0;
+ * collectives (and for single-GPU tests of the partitioning).  Two partition schemes,
+ * chosen from the alphabet (hkcsa_shard_scheme):
+ *   1 (keyed coarse: the keyed radix is 2^lb, lb in {1,2,4,8} — DNA, binary, 16 or 256
+ *     symbols): the bucket of a suffix is the top 16 bits of its keyed sym field (its
+ *     first 16/lb symbols); rank r's block is [n*r/N, n*(r+1)/N) with 16-aligned starts
+ *     and hkcsa_shard_histogram counts EVERY suffix of it (exact), so the global
+ *     histogram alone fixes the slices (hkcsa_build_sa_sharded skips the counts phase);
+ *     the splitters are equal-width (r * 65536 / N) when N divides 65536 and no such slice
+ *     is 2 % above n/N, else balanced (below);
+ *   0 (partition key, any other alphabet): the bucket is the top 14 bits of a radix-(sigma+1)
+ *     key over the positions p % hkcsa_shard_sample() == 0 of [n*r/N, n*(r+1)/N); bins past
+ *     16384 stay 0; balanced splitters.
+ * Balanced splitters: B_r = the smallest bucket with cum(B_r) >= floor(S*r/N), S = the
+ * histogram total (hkcsa/shard.py split_buckets).
+ *   hkcsa_shard_histogram: the block's histogram (hkcsa_shard_buckets() = 65536 bins);
  *   hkcsa_shard_counts: with G = the element-wise sum of every rank's histogram,
  *     below_out[j] (j = 0..N) = #suffixes of the block whose bucket is below
  *     splitter j (splitters derived from G; below_out[0] = 0);
@@ -226,6 +237,7 @@ int hkcsa_get_shard_bwt(hkcsa_index* ix, uint64_t a, uint64_t b, uint8_t* out);
  *     sum of every rank's below_out (lo, hi = its entries r and r+1). */
 int hkcsa_shard_buckets(void);
 int hkcsa_shard_sample(void);
+int hkcsa_shard_scheme(hkcsa_index* ix, int* scheme);   /* 1 keyed coarse, 0 partition key */
 int hkcsa_shard_histogram(hkcsa_index* ix, int nranks, int rank, uint64_t* hist_out);
 int hkcsa_shard_counts(hkcsa_index* ix, const uint64_t* global_hist, int nranks, int rank,
                        uint64_t* below_out);

@@ -195,6 +195,7 @@ static uint64_t splitmix64(uint64_t x) {
 
 void oracle_synth_text(uint64_t n, const uint8_t* alpha, int sigma, uint64_t seed, uint8_t term, uint8_t* out) {
   const uint64_t key = seed * 0xD1B54A32D192ED03ull;
+#pragma omp parallel for schedule(static)
   for (uint64_t i = 0; i < n; ++i) {
     if (i + 1 == n) out[i] = term;
     else out[i] = alpha[(uint32_t)(splitmix64(key ^ i) >> 32) % (uint32_t)sigma];
@@ -334,29 +335,105 @@ static uint64_t shard_bucket(const uint8_t* t, uint64_t n, uint64_t p, const uin
   return key >> bsh;
 }
 
-/* Sampled key-prefix histogram of positions p in [lo, hi) with p % 64 == 0 (hk_shard.hip,
- * SH_SAMPLE): the splitters only need balance; exact slice sizes come from oracle_shard_below. */
-void oracle_shard_hist(const uint8_t* t, uint64_t n, uint64_t lo, uint64_t hi, uint64_t* hist /* 16384 */) {
+/* Keyed coarse scheme of the sharded build (hk_bucket.hip key_geometry_keyed, shard_coarse_hist):
+ * the keyed alphabet is every byte present except a terminal T[n-1] that occurs exactly once (when
+ * at least two bytes are present); a keyed byte's digit is the number of keyed bytes below it.  The
+ * scheme applies when the keyed radix Rk = max(#keyed, 2) is 2^lb with lb in {1, 2, 4, 8}.  The coarse
+ * bucket of suffix p is the first H = 16 / lb digits of its digit string as one radix-Rk number: the
+ * digits of T[p..] up to the unkeyed terminal or the end of the text, then one digit (the number of
+ * keyed bytes below the terminal, or 0 when the text just ends), then zeros.  Returns lb (0: the
+ * sampled partition key below applies instead). */
+int oracle_shard_scheme(const uint8_t* t, uint64_t n, uint16_t dig[256], int* unkeyed_term, int* mterm) {
+  uint64_t h[256] = {0};
+  for (uint64_t i = 0; i < n; ++i) h[t[i]]++;
+  int sigma = 0;
+  for (int c = 0; c < 256; ++c) sigma += h[c] != 0;
+  const int term = n ? t[n - 1] : -1;
+  const int unk = n && h[term] == 1 && sigma >= 2;
+  int rk = 0, below = 0;
+  for (int c = 0; c < 256; ++c) {
+    const int keyed = h[c] && !(unk && c == term);
+    dig[c] = (uint16_t)rk;
+    if (unk && c < term && keyed) ++below;
+    rk += keyed;
+  }
+  if (rk < 2) rk = 2;
+  *unkeyed_term = unk ? term : -1;
+  *mterm = unk ? below : 0;
+  switch (rk) {
+    case 2: return 1;
+    case 4: return 2;
+    case 16: return 4;
+    case 256: return 8;
+    default: return 0;
+  }
+}
+
+static uint32_t coarse_bucket(const uint8_t* t, uint64_t n, uint64_t p, const uint16_t* dig, int lb, int uterm,
+                              int mterm) {
+  const int H = 16 / lb;
+  uint32_t v = 0;
+  int i = 0, done = 0;
+  for (; i < H && !done; ++i) {
+    const uint64_t j = p + (uint64_t)i;
+    uint32_t d;
+    if (j >= n) {
+      d = 0;
+      done = 1;
+    } else if ((int)t[j] == uterm && j == n - 1) {
+      d = (uint32_t)mterm;
+      done = 1;
+    } else {
+      d = dig[t[j]];
+    }
+    v = (v << lb) | d;
+  }
+  for (; i < H; ++i) v <<= lb;
+  return v;
+}
+
+/* Sharded partition histogram of the positions [lo, hi): keyed scheme: the exact coarse histogram
+ * (65536 bins); else the sampled key-prefix histogram of the positions p % 64 == 0 (hk_shard.hip,
+ * SH_SAMPLE) in the first 16384 bins: the splitters only need balance; exact slice sizes come from
+ * oracle_shard_below. */
+void oracle_shard_hist(const uint8_t* t, uint64_t n, uint64_t lo, uint64_t hi, uint64_t* hist /* 65536 */) {
+  memset(hist, 0, 65536 * sizeof(uint64_t));
+  uint16_t dig[256];
+  int uterm, mterm;
+  const int lb = oracle_shard_scheme(t, n, dig, &uterm, &mterm);
+  if (lb) {
+    for (uint64_t p = lo; p < hi; ++p) hist[coarse_bucket(t, n, p, dig, lb, uterm, mterm)]++;
+    return;
+  }
   uint16_t code[256];
   int q, pb, kb;
   uint64_t R;
   partition_geometry(t, n, &q, &pb, &R, &kb, code);
   int bsh = kb - 14;
   if (bsh < 0) bsh = 0;
-  memset(hist, 0, 16384 * sizeof(uint64_t));
   for (uint64_t p = (lo + 63) / 64 * 64; p < hi; p += 64) hist[shard_bucket(t, n, p, code, q, pb, R, bsh)]++;
 }
 
-/* below[j] = #{p in [lo, hi) : bucket(p) < B[j]} for j < nb */
+/* below[j] = #{p in [lo, hi) : bucket(p) < B[j]} for j < nb (the scheme's bucket) */
 void oracle_shard_below(const uint8_t* t, uint64_t n, uint64_t lo, uint64_t hi, const uint32_t* B, int nb,
                         uint64_t* below) {
+  for (int j = 0; j < nb; ++j) below[j] = 0;
+  uint16_t dig[256];
+  int uterm, mterm;
+  const int lb = oracle_shard_scheme(t, n, dig, &uterm, &mterm);
+  if (lb) {
+    for (uint64_t p = lo; p < hi; ++p) {
+      const uint32_t b = coarse_bucket(t, n, p, dig, lb, uterm, mterm);
+      for (int j = 0; j < nb; ++j) below[j] += b < B[j];
+    }
+    return;
+  }
   uint16_t code[256];
   int q, pb, kb;
   uint64_t R;
   partition_geometry(t, n, &q, &pb, &R, &kb, code);
   int bsh = kb - 14;
   if (bsh < 0) bsh = 0;
-  for (int j = 0; j < nb; ++j) below[j] = 0;
   for (uint64_t p = lo; p < hi; ++p) {
     const uint64_t b = shard_bucket(t, n, p, code, q, pb, R, bsh);
     for (int j = 0; j < nb; ++j) below[j] += b < B[j];

@@ -54,6 +54,8 @@ def lib():
         L.oracle_wt_levels.restype = C.c_int
         L.oracle_shard_hist.argtypes = [vp, u64, u64, u64, vp]
         L.oracle_shard_below.argtypes = [vp, u64, u64, u64, vp, C.c_int, vp]
+        L.oracle_shard_scheme.argtypes = [vp, u64, vp, vp, vp]
+        L.oracle_shard_scheme.restype = C.c_int
         L.oracle_key_geometry.argtypes = [vp, u64, vp, vp, vp, vp, vp]
         L.oracle_golomb.argtypes = [vp, u64, C.c_uint32, vp]
         L.oracle_golomb.restype = u64
@@ -117,15 +119,24 @@ def wt_levels(seq) -> np.ndarray:
     return bits[:L, :len(s)].copy()
 
 
-def shard_hist(t, lo: int, hi: int) -> np.ndarray:
+def shard_scheme(t) -> int:
+    """lb of the keyed coarse partition (exact 16-bit sym-prefix histogram), 0: the sampled key."""
     t = _u8(t)
-    h = np.zeros(16384, dtype=np.uint64)
+    dig = np.zeros(256, dtype=np.uint16)
+    ut, mt = C.c_int(0), C.c_int(0)
+    return int(lib().oracle_shard_scheme(_p(t) if len(t) else None, len(t), _p(dig), C.byref(ut), C.byref(mt)))
+
+
+def shard_hist(t, lo: int, hi: int) -> np.ndarray:
+    """The sharded build's partition histogram of [lo, hi) (65536 bins; see oracle_shard_hist)."""
+    t = _u8(t)
+    h = np.zeros(65536, dtype=np.uint64)
     lib().oracle_shard_hist(_p(t), len(t), lo, hi, _p(h))
     return h
 
 
 def shard_below(t, lo: int, hi: int, splitters) -> np.ndarray:
-    """#positions p in [lo, hi) whose 14-bit key bucket is below each splitter."""
+    """#positions p in [lo, hi) whose partition bucket is below each splitter."""
     t = _u8(t)
     B = np.ascontiguousarray(splitters, dtype=np.uint32)
     out = np.zeros(len(B), dtype=np.uint64)

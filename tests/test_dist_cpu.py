@@ -35,7 +35,7 @@ class OracleShardDevice:
     def shard_counts(self, g, nranks, rank):
         from hkcsa.shard import split_buckets
         lo, hi = self.n * rank // nranks, self.n * (rank + 1) // nranks
-        return self.o.shard_below(self.t, lo, hi, split_buckets(g, nranks))
+        return self.o.shard_below(self.t, lo, hi, split_buckets(g, nranks, aligned=self.o.shard_scheme(self.t) > 0))
 
     def shard_build(self, g, below, nranks, rank):
         from hkcsa.shard import slice_bounds
@@ -45,6 +45,9 @@ class OracleShardDevice:
 
     def shard_range(self):
         return self.lo, self.hi
+
+    def shard_status(self):
+        return (self.lo, self.hi, 0, 0)   # the oracle slice is final
 
 
 class DoublingShardDevice(OracleShardDevice):
@@ -157,6 +160,17 @@ def _free_port():
     p = s.getsockname()[1]
     s.close()
     return p
+
+
+def test_sharded_build_without_allgather_refuses_tied_slice():
+    """A slice left tied after the chunk rounds needs the rank exchange: sharded_build without an
+    allgather raises instead of returning the slice in tied order."""
+    from hkcsa.shard import sharded_build
+    from oracle import oracle  # noqa: F401 (stand-in device uses it)
+    text = np.frombuffer(b"a" * 400 + b"$", dtype=np.uint8)
+    dev = DoublingShardDevice(text, h0=3)
+    with pytest.raises(RuntimeError, match="allgather"):
+        sharded_build(dev, 1, 0, lambda h: h)
 
 
 @pytest.mark.parametrize("world,kind,n", [(2, "iid", 30001), (2, "periodic", 3001), (3, "run", 1501)])

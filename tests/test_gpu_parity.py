@@ -359,17 +359,23 @@ def test_shard_two_phase_emulated(hk, nranks, flags, alpha):
     """Ranks emulated on one GPU; flags=1 forces the 64-bit position kernels (n >= 2^32 path: split
     u32 sort values), flags=3 the whole-u64 value sort, flags=4 the global sort of each slice instead
     of its LDS bucket sorts, flags=8 multiplicative bucket bins; the skewed alphabets give slices
-    whose big buckets take the global path.
-    Alphabets cover the byte-image pre-test thresholds for radix 3 .. 257."""
+    whose big buckets take the global path.  Keyed coarse scheme (radix 2^lb: ACGT, ab, bytes) and
+    the partition-key scheme (AC$GT, printable, aaa..ab) against the oracle's restatement of each;
+    the partition-key alphabets cover the byte-image pre-test thresholds for radix 3 .. 257."""
     text = oracle.synth_text(400001, alpha, seed=12 + nranks)
     ref = oracle.suffix_array(text)
     ref_bwt = oracle.bwt(text, ref)
     devs = [hk.DeviceIndex.from_bytes(text, device=0, flags=flags) for _ in range(nranks)]
+    scheme = devs[0].shard_scheme()
+    assert scheme == (1 if oracle.shard_scheme(text) else 0)
     g = sum(d.shard_histogram(nranks, r) for r, d in enumerate(devs))
-    assert int(g.sum()) == (len(text) + 63) // 64          # every 64th position (hkcsa_shard_sample)
+    if scheme:   # keyed coarse buckets: every suffix counted
+        assert int(g.sum()) == len(text)
+    else:        # partition key: every 64th position (hkcsa_shard_sample)
+        assert int(g.sum()) == (len(text) + 63) // 64
     assert np.array_equal(g, oracle.shard_hist(text, 0, len(text)))
     from hkcsa.shard import slice_bounds, split_buckets
-    B = split_buckets(g, nranks)
+    B = split_buckets(g, nranks, aligned=bool(scheme))
     below = sum(d.shard_counts(g, nranks, r) for r, d in enumerate(devs))
     assert np.array_equal(below, oracle.shard_below(text, 0, len(text), B))
     assert int(below[-1]) == len(text)

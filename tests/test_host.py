@@ -69,17 +69,25 @@ def test_golomb_m_matches_kat(kat):
             assert GolombRiceEncoder(bits).m == kat[word]["wt_bwt_m"]
 
 
-@pytest.mark.parametrize("nranks", [1, 2, 3, 8])
-def test_slice_bounds_tile_the_sa(nranks):
-    """Sampled histogram -> splitters -> exact below-counts -> slices tile [0, n) near n/N each."""
+@pytest.mark.parametrize("nranks,alpha", [(1, b"ACGT"), (2, b"ACGT"), (3, b"ACGT"), (8, b"ACGT"),
+                                          (2, b"AC$GT"), (3, bytes(range(0x20, 0x7F))), (8, b"AC$GT")])
+def test_slice_bounds_tile_the_sa(nranks, alpha):
+    """Partition histogram -> splitters -> exact below-counts -> slices tile [0, n) near n/N each.
+    ACGT (+ the unique '$'): keyed radix 4, the exact coarse histogram; '$' inside the text / printable
+    bytes: the sampled partition key."""
     from hkcsa.shard import split_buckets
-    t = oracle.synth_text(20000, b"ACGT", seed=4)
+    t = oracle.synth_text(20000, alpha, seed=4)
+    keyed = oracle.shard_scheme(t) > 0
+    assert keyed == (alpha == b"ACGT")
     h = oracle.shard_hist(t, 0, len(t))
-    assert int(h.sum()) == (len(t) + 63) // 64
-    B = split_buckets(h, nranks)
+    assert int(h.sum()) == (len(t) if keyed else (len(t) + 63) // 64)
+    B = split_buckets(h, nranks, aligned=keyed)
     below = sum(oracle.shard_below(t, len(t) * r // nranks, len(t) * (r + 1) // nranks, B) for r in range(nranks))
     assert np.array_equal(below, oracle.shard_below(t, 0, len(t), B))
     b = slice_bounds(below, nranks)
+    if keyed:   # exact histogram: the bounds are its prefix sums at the splitters
+        cum = np.concatenate(([0], np.cumsum(h)))
+        assert [int(cum[x]) for x in B] == [int(x) for x in below]
     assert b[0][0] == 0 and b[-1][1] == len(t)
     for (lo, hi), (lo2, _) in zip(b, b[1:]):
         assert hi == lo2 and lo <= hi

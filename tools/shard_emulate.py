@@ -17,7 +17,8 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(
                                 "high-order-entropy-compressed-suffix-array_amd"))
 from hkcsa import DeviceIndex  # noqa: E402
 
-STAGES = ["shard_select_count", "shard_pack_select", "sa_bucket_hist", "radix_part_keys", "radix_part",
+STAGES = ["shard_hist", "shard_slice_hist", "shard_slice_part", "shard_select_count", "shard_pack_select",
+          "sa_bucket_hist", "radix_part_keys", "radix_part",
           "sa_bin_starts", "sa_bucket_sort", "radix_hist",
           "radix_onesweep", "radix_onesweep_small", "shard_split_join", "sa_refine_stats", "sa_refine_apply",
           "sa_refine_keys"]
