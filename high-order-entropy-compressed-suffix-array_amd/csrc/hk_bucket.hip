@@ -733,19 +733,31 @@ __global__ __launch_bounds__(BH_T, 1) void k_slice_hist_spans(const uint8_t* __r
   static_assert(NI <= 2 * BH_PER, "window past the thread's 32 bytes");
   const int wbits = hq * lb, wdrop = sl.wdrop, dsh = 32 - sl.DB;
   const uint32_t bmask = wbits >= 32 ? ~0u : (1u << wbits) - 1;
-  uint4 w0 = make_uint4(0, 0, 0, 0), w1 = w0;
-  if (lo + (uint64_t)tid * BH_PER < hi) {
-    const uint4* src = reinterpret_cast<const uint4*>(t + lo + (uint64_t)tid * BH_PER);
-    w0 = src[0];
-    w1 = src[1];
+  // the next PF iterations' bytes in flight (one iteration ahead left the scan latency-bound at ~1.4 TB/s)
+  constexpr int PF = REG ? 3 : 1;
+  uint4 f0[PF], f1[PF];
+#pragma unroll
+  for (int u = 0; u < PF; ++u) {
+    f0[u] = f1[u] = make_uint4(0, 0, 0, 0);
+    const uint64_t pu = lo + (uint64_t)u * BH_TILE + (uint64_t)tid * BH_PER;
+    if (pu < hi) {
+      const uint4* src = reinterpret_cast<const uint4*>(t + pu);
+      f0[u] = src[0];
+      f1[u] = src[1];
+    }
   }
   for (uint64_t base = lo; base < hi; base += BH_TILE) {
     const uint64_t p0 = base + (uint64_t)tid * BH_PER;
-    const uint4 a = w0, b4 = w1;
-    if (p0 + BH_TILE < hi) {   // next iteration's bytes in flight
-      const uint4* src = reinterpret_cast<const uint4*>(t + p0 + BH_TILE);
-      w0 = src[0];
-      w1 = src[1];
+    const uint4 a = f0[0], b4 = f1[0];
+#pragma unroll
+    for (int u = 0; u + 1 < PF; ++u) {
+      f0[u] = f0[u + 1];
+      f1[u] = f1[u + 1];
+    }
+    if (p0 + PF * BH_TILE < hi) {
+      const uint4* src = reinterpret_cast<const uint4*>(t + p0 + PF * BH_TILE);
+      f0[PF - 1] = src[0];
+      f1[PF - 1] = src[1];
     }
     const uint64_t lim2 = lim < hi ? lim : hi;
     if (p0 < lim2) {
@@ -1034,6 +1046,206 @@ __global__ __launch_bounds__(CP_T, 2) void k_slice_cpart(uint64_t* __restrict__ 
     const uint32_t gbv = (uint32_t)(g - sh.tg[tid]);
     __syncthreads();
     sh.tg[tid] = gbv;
+    __syncthreads();
+    write_out(tot, hi256);
+  }
+}
+
+// Pass A of a slice, radix 2^2 packed records, all in registers (g <= SL_G sub-tiles per unit): every
+// text load of the unit is issued up front (three 16-B loads and the word before per thread and
+// sub-tile), the packed codes and the kept-position masks stay in registers between round 1 (bins ->
+// digit counts) and round 2, which keys only the kept positions (a bit loop: ~1/N of the 16 per
+// sub-tile) and stages them at their final slots.  Each sub-tile of a unit denser than one tile is
+// ranked, reserved and written on its own (non-iid text), as in k_slice_cpart.
+constexpr int SL_G = 8;
+
+__global__ __launch_bounds__(CP_T, 4) void k_slice_cpart_reg(uint64_t* __restrict__ kout, uint64_t n,
+                                                             unsigned long long* __restrict__ cur, uint64_t span,
+                                                             TextKeySrc src, SliceSel sl,
+                                                             const unsigned long long* __restrict__ skip,
+                                                             uint64_t mcap) {
+  constexpr int T = CP_T;
+  __shared__ uint64_t keys[CP_TILE];
+  __shared__ uint8_t sdg[CP_TILE];
+  __shared__ uint32_t tg[CP_NAM], cnt[CP_NAM], wsum[CP_NAM / 64];
+  __shared__ uint16_t LP[256];
+  __shared__ uint64_t SK[72];
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  if (skip && *skip) return;   // the pre-pass counters overflowed: recounted, then relaunched
+  const uint64_t U = (uint64_t)SL_SUB * sl.g;
+  const uint32_t per = (uint32_t)(span / U), gx = blockIdx.x & 7u, k8 = blockIdx.x >> 3;
+  const uint64_t unit = (uint64_t)(gx + 8u * (k8 / per)) * per + k8 % per;
+  const uint64_t ubase = unit * U;
+  if (ubase >= n) return;   // past the last span (whole workgroup, before any barrier)
+  unsigned long long* const row = cur + (ubase / span) * CP_NAM;
+  const uint32_t nsub = (uint32_t)((n - ubase < U ? n - ubase : U) + SL_SUB - 1) / SL_SUB;
+  if (tid < 256) LP[tid] = src.lutp[tid];
+  if (tid < 72) SK[tid] = src.skey[tid];
+  cnt[tid] = 0;
+  __syncthreads();
+  const uint64_t lim = n < src.g.s_start ? n : src.g.s_start;
+  const uint64_t kmask_lo = (1ull << (sl.bsh + sl.sA)) - 1;
+  const uint64_t sbase = (uint64_t)sl.base << sl.bsh;
+  const int kbits = 2 * src.g.q, dsh = 32 - sl.DB;
+  const uint64_t tmask = kbits >= 64 ? ~0ull : (1ull << kbits) - 1;
+  // ---- round 1: packed codes, kept-position masks, digit counts.  The unit's loads go out in two
+  // batches of SL_G / 2 sub-tiles (all of them at once held ~190 VGPRs: 2 waves per SIMD)
+  constexpr int SB = SL_G / 2;
+  uint32_t c[SL_G][3], msk[SL_G], pcs = 0;
+  uint4 q[SB][3];
+  uint32_t pw[SB];
+#pragma unroll
+  for (int st = 0; st < SL_G; ++st) {
+    if (st % SB == 0) {
+#pragma unroll
+      for (int u = 0; u < SB; ++u) {
+        const uint64_t pu = ubase + (uint64_t)(st + u) * SL_SUB + 16ull * tid;
+        q[u][0] = q[u][1] = q[u][2] = make_uint4(0, 0, 0, 0);
+        pw[u] = 0;
+        if ((uint32_t)(st + u) < nsub && pu < n) {   // T' has 64 readable pad bytes
+          const uint4* q4 = reinterpret_cast<const uint4*>(src.text + pu);
+          q[u][0] = q4[0];
+          q[u][1] = q4[1];
+          q[u][2] = q4[2];
+          if (pu) pw[u] = reinterpret_cast<const uint32_t*>(src.text + pu)[-1];
+        }
+      }
+    }
+    msk[st] = 0;
+    c[st][0] = pack16_2(q[st % SB][0], sl);
+    c[st][1] = pack16_2(q[st % SB][1], sl);
+    c[st][2] = pack16_2(q[st % SB][2], sl);
+    const uint64_t p0 = ubase + (uint64_t)st * SL_SUB + 16ull * tid;
+    if ((uint32_t)st >= nsub || p0 >= n) continue;
+    // prev code of p0: the records' code of T'[p0 - 1] (T'[n - 1] for p0 = 0)
+    const uint32_t pb = pw[st % SB] >> 24;
+    const uint32_t pc = p0 ? __builtin_amdgcn_perm(sl.th, sl.tl, (pb >> sl.ps) & 7u) & 3u : (uint32_t)LP[src.text[n - 1]];
+    pcs |= pc << (2 * st);
+    const bool full = p0 + 16 <= lim;
+    uint32_t m = 0;
+#pragma unroll
+    for (int k = 0; k < CP_I; ++k) {
+      const uint32_t bin = (win32(c[st][0], c[st][1], k) >> dsh) - sl.base;
+      if (bin < sl.nb && (full || p0 + k < lim)) {
+        m |= 1u << k;
+        atomicAdd(&cnt[bin >> sl.sA], 1u);
+      }
+    }
+    for (uint64_t j = p0 > lim ? p0 : lim; j < p0 + 16 && j < n; ++j) {   // short suffixes: boundary keys
+      const uint32_t bin = (uint32_t)(SK[j - src.g.s_start] >> sl.bsh) - sl.base;
+      if (bin < sl.nb) {
+        m |= 1u << (uint32_t)(j - p0);
+        atomicAdd(&cnt[bin >> sl.sA], 1u);
+      }
+    }
+    msk[st] = m;
+  }
+  // the record of kept position k of sub-tile st (runtime k) and its pass A digit
+  auto record_at = [&](int st, int k, uint64_t& rec) -> uint32_t {
+    const uint64_t j = ubase + (uint64_t)st * SL_SUB + 16ull * tid + (uint64_t)k;
+    const int sh = 32 - 2 * k;   // 2..32
+    const uint64_t s01 = ((uint64_t)c[st][0] << 32) | c[st][1], s12 = ((uint64_t)c[st][1] << 32) | c[st][2];
+    const uint64_t win = ((uint64_t)(uint32_t)(s01 >> sh) << 32) | (uint32_t)(s12 >> sh);
+    uint64_t sym = kbits >= 64 ? win : (win >> (64 - kbits)) & tmask;
+    if (j >= src.g.s_start) sym = SK[j - src.g.s_start];
+    const uint32_t prv = (uint32_t)(((((uint64_t)((pcs >> (2 * st)) & 3u)) << 32) | c[st][0]) >> sh) & 3u;
+    const uint32_t bin = (uint32_t)(sym >> sl.bsh) - sl.base;
+    const uint64_t x = sym - sbase;
+    rec = ((((x & kmask_lo) << sl.pb2) | prv) << sl.pbits) | j;
+    return bin >> sl.sA;
+  };
+  __syncthreads();
+  const uint32_t cu = cnt[tid];
+  uint32_t total = 0;
+  {
+    const uint32_t inc = wave_incl_sum<uint32_t>(cu);
+    if (lane == 63) wsum[wv] = inc;
+    __syncthreads();
+    uint32_t carry = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < T / 64; ++w) {
+      carry += w < wv ? wsum[w] : 0u;
+      total += wsum[w];
+    }
+    tg[tid] = carry + inc - cu;
+    cnt[tid] = 0;
+  }
+  auto write_out = [&](uint32_t cnt_tile, uint32_t hi256) {
+    for (int i = 0; i < CP_I; ++i) {
+      const uint32_t s = (uint32_t)i * T + tid;
+      if (s < cnt_tile) {
+        const uint32_t d = (uint32_t)sdg[s] | (s >= hi256 ? 256u : 0u);
+        const uint32_t o = tg[d] + s;   // u32: tg = destination - tile start (mod 2^32)
+        if (o < mcap) kout[o] = keys[s];
+      }
+    }
+  };
+  if (total <= (uint32_t)CP_TILE) {
+    const unsigned long long resv = cu ? atomicAdd(&row[tid], (unsigned long long)cu) : 0ull;
+    __syncthreads();
+    // ---- round 2: key and stage the kept positions only
+#pragma unroll
+    for (int st = 0; st < SL_G; ++st) {
+      uint32_t m = msk[st];
+      while (m) {
+        const int k = __builtin_ctz(m);
+        m &= m - 1;
+        uint64_t rec;
+        const uint32_t d = record_at(st, k, rec);
+        uint32_t f = tg[d] + atomicAdd(&cnt[d], 1u);
+        f = f < (uint32_t)CP_TILE ? f : (uint32_t)CP_TILE - 1;   // (only a count mismatch overruns)
+        keys[f] = rec;
+        sdg[f] = (uint8_t)d;
+      }
+    }
+    __syncthreads();
+    const uint32_t hi256 = tg[256];
+    const uint32_t gbv = (uint32_t)(resv - tg[tid]);
+    __syncthreads();
+    tg[tid] = gbv;
+    __syncthreads();
+    write_out(total, hi256);
+    return;
+  }
+  // dense unit: each sub-tile counted, reserved, staged and written on its own (ranks by a second
+  // round of atomics, as the fast path: no per-position rank registers)
+#pragma unroll
+  for (int st = 0; st < SL_G; ++st) {   // (unrolled: c[st] / msk[st] stay register-resident)
+    if ((uint32_t)st >= nsub) break;   // uniform
+    __syncthreads();   // the previous write-out has read keys / tg; counters free
+    cnt[tid] = 0;
+    __syncthreads();
+    for (uint32_t m = msk[st]; m; m &= m - 1) {
+      uint64_t rec;
+      atomicAdd(&cnt[record_at(st, __builtin_ctz(m), rec)], 1u);
+    }
+    __syncthreads();
+    const uint32_t cc = cnt[tid];
+    const unsigned long long g = cc ? atomicAdd(&row[tid], (unsigned long long)cc) : 0ull;
+    const uint32_t inc = wave_incl_sum<uint32_t>(cc);
+    if (lane == 63) wsum[wv] = inc;
+    __syncthreads();
+    uint32_t carry = 0, tot = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < T / 64; ++w) {
+      carry += w < wv ? wsum[w] : 0u;
+      tot += wsum[w];
+    }
+    tg[tid] = carry + inc - cc;
+    cnt[tid] = 0;
+    __syncthreads();
+    for (uint32_t m = msk[st]; m; m &= m - 1) {
+      uint64_t rec;
+      const uint32_t d = record_at(st, __builtin_ctz(m), rec);
+      const uint32_t f = tg[d] + atomicAdd(&cnt[d], 1u);
+      keys[f] = rec;
+      sdg[f] = (uint8_t)d;
+    }
+    __syncthreads();
+    const uint32_t hi256 = tg[256];
+    const uint32_t gbv = (uint32_t)(g - tg[tid]);
+    __syncthreads();
+    tg[tid] = gbv;
     __syncthreads();
     write_out(tot, hi256);
   }
@@ -3030,7 +3242,7 @@ static int cursor_partition_slice(Index& ix, const SlicePlan& P, const TextKeySr
     void* vo = P.packed ? nullptr : (void*)vp[outA];
     const unsigned long long* skip = D > 16 ? d_ovf : nullptr;
     if (P.reg)
-      k_slice_cpart<2, true, true><<<grid, CP_T, 0, s>>>(kp[outA], nullptr, n, d_curA, span, tks2, sl, skip, m);
+      k_slice_cpart_reg<<<grid, CP_T, 0, s>>>(kp[outA], n, d_curA, span, tks2, sl, skip, m);
     else if (P.packed && P.lb == 2)
       k_slice_cpart<2, true><<<grid, CP_T, 0, s>>>(kp[outA], nullptr, n, d_curA, span, tks2, sl, skip, m);
     else if (P.packed && P.lb == 1)
@@ -3108,7 +3320,7 @@ void build_slice_keyed(Index& ix, uint32_t c_lo, uint32_t c_hi, uint64_t m) {
     const double ratio = m ? (double)n / (double)m : 1.0;
     uint32_t g = (uint32_t)std::floor(0.9 * ratio);
     if (g < 1) g = 1;
-    if (g > 64) g = 64;
+    if (g > (P.reg ? (uint32_t)SL_G : 64u)) g = P.reg ? (uint32_t)SL_G : 64u;   // register kernel: <= SL_G
     P.sl.g = g;
   }
   const uint8_t* small = ix.small.as<uint8_t>();

@@ -354,7 +354,8 @@ def test_wt_and_count_beyond_4gib(hk):
                                                (3, 3, bytes(range(256))), (3, 4, b"ACGT"), (2, 5, b"ACGT"),
                                                (3, 0, b"aaaaaaaaaaaaaaab"), (2, 1, b"aaaaaaaab"),
                                                (3, 8, b"ACGT"), (2, 9, bytes(range(0x20, 0x7F))),
-                                               (4, 8, b"aaaaaaaab")])
+                                               (4, 8, b"aaaaaaaab"), (4, 0, bytes([1, 2, 0x41, 0x42])),
+                                               (3, 1, bytes([1, 2, 0x41, 0x42]))])
 def test_shard_two_phase_emulated(hk, nranks, flags, alpha):
     """Ranks emulated on one GPU; flags=1 forces the 64-bit position kernels (n >= 2^32 path: split
     u32 sort values), flags=3 the whole-u64 value sort, flags=4 the global sort of each slice instead
@@ -407,6 +408,27 @@ def test_shard_large_slices(hk, n, nranks, flags, alpha):
     assert oracle.check_sa(text, sa) == 0
     assert np.array_equal(np.concatenate([d.shard_bwt() for d in devs]), oracle.bwt(text, sa))
     assert max(d.build_info()[4] for d in devs) > 256   # bucket items: more than pass A's 256 digits
+    for d in devs:
+        d.close()
+
+
+@pytest.mark.parametrize("nranks,flags", [(4, 0), (8, 1), (3, 4)])
+def test_shard_keyed_dense_units(hk, nranks, flags):
+    """DNA with a long run and a periodic stretch: the run's suffixes all fall in one slice, so that
+    slice's pass A units hold more kept suffixes than one tile (each sub-tile then ranked and written
+    on its own), its buckets exceed one LDS sort (the slice's global path) and its ties outlast the
+    chunk rounds (prefix doubling with the rank exchange).  flags 4: the global sort everywhere."""
+    rng = np.random.default_rng(nranks)
+    dna = np.frombuffer(b"ACGT", dtype=np.uint8)
+    text = np.concatenate([dna[rng.integers(0, 4, 600_000)], np.full(200_000, ord("A"), np.uint8),
+                           dna[rng.integers(0, 4, 600_000)], np.frombuffer(b"CA" * 100_000, np.uint8),
+                           [ord("$")]]).astype(np.uint8)
+    ref = oracle.suffix_array(text)
+    devs, _ = _emulated_shard_build(hk, text, nranks, flags)
+    assert devs[0].shard_scheme() == 1
+    parts = [d.shard_sa() for d in devs]
+    assert np.array_equal(np.concatenate(parts), ref)
+    assert np.array_equal(np.concatenate([d.shard_bwt() for d in devs]), oracle.bwt(text, ref))
     for d in devs:
         d.close()
 

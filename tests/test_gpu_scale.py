@@ -112,5 +112,8 @@ def test_printable_200MiB_count_20sym(hk):
     fm = oracle.FM(text, sa)
     got = dev.count_ranges(pats)
     assert np.array_equal(got, fm.find_range(pats))
-    assert (got[:20000, 0] >= 0).all()
+    # substrings are found (the printable alphabet holds '$': patterns with it follow the reference's
+    # wrapped-row quirk, csa/bwt.py:9-10, so only '$'-free ones must occur)
+    plain = np.array([b"$" not in p for p in pats[:20000]])
+    assert (got[:20000, 0][plain] >= 0).all()
     dev.close()
