@@ -422,12 +422,13 @@ def run_sharded(args, rank: int, world: int, local_rank: int) -> dict | None:
     per_gpu = slices_per_gpu(n, world)
     if per_gpu > 1 and world > 1:
         raise SystemExit("more than one slice per GPU is supported at N = 1 only")
+    keyed = dev.shard_scheme() == 1 if per_gpu > 1 else None
 
     def step():
         if per_gpu == 1:
             dev.build_sa_sharded(uid, world, rank)
         else:
-            virtual_slices(dev, per_gpu)
+            virtual_slices(dev, per_gpu, keyed=keyed)
 
     for _ in range(args.warmup):
         step()
@@ -521,13 +522,23 @@ def slices_per_gpu(n: int, world: int) -> int:
     return max(2, int(round(n / (1 << 30))))
 
 
-def virtual_slices(dev, k: int, on_slice=None):
+def virtual_slices(dev, k: int, on_slice=None, keyed=None):
     """One GPU builds all k slices of a sharded build one after another (host-driven phases).  Only
     used when the text has >= 2^32 suffixes on a single GPU; the bench text is iid, so no slice is left
     tied after its chunk rounds (checked).  on_slice(r) runs after slice r is built (parity tests read
-    the slice there)."""
-    g = sum(dev.shard_histogram(k, r) for r in range(k))
-    below = sum(dev.shard_counts(g, k, r) for r in range(k))
+    the slice there).  Keyed coarse scheme (keyed=True, dev.shard_scheme() == 1): the exact histogram
+    of the whole text is the global one, so the slice bounds are its prefix sums at the splitters (the
+    rule of build_sa_sharded's keyed phase 1) and no per-slice block is counted again."""
+    from hkcsa.shard import split_buckets
+    if keyed is None:
+        keyed = dev.shard_scheme() == 1
+    if keyed:
+        g = dev.shard_histogram(1, 0)
+        cum = np.concatenate(([0], np.cumsum(g, dtype=np.uint64)))
+        below = np.array([cum[b] for b in split_buckets(g, k, aligned=True)], dtype=np.uint64)
+    else:
+        g = sum(dev.shard_histogram(k, r) for r in range(k))
+        below = sum(dev.shard_counts(g, k, r) for r in range(k))
     for r in range(k):
         dev.shard_build(g, below, k, r)
         if dev.shard_status()[2]:

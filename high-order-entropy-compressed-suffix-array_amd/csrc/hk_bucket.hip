@@ -185,7 +185,7 @@ __device__ __forceinline__ uint64_t pk_full_low(uint64_t rec, const PkGeom& g) {
 template <int CB>
 __device__ __forceinline__ void hist_spans_flush(const uint32_t* H, uint32_t* M, uint32_t nbl, uint32_t boff,
                                                  uint32_t stride, int sA, uint32_t* __restrict__ part,
-                                                 uint32_t* __restrict__ spanc) {
+                                                 uint32_t* __restrict__ spanc, uint32_t* fsum = nullptr) {
   constexpr int CPW = 32 / CB;
   constexpr uint32_t CM = (1u << CB) - 1;
   const uint32_t tid = threadIdx.x;
@@ -198,7 +198,7 @@ __device__ __forceinline__ void hist_spans_flush(const uint32_t* H, uint32_t* M,
   }
   // pass A digit counts: contiguous words per thread, one LDS add per digit run
   const uint32_t per = (np + BH_T - 1) / BH_T;
-  uint32_t acc = 0, cd = 0;
+  uint32_t acc = 0, cd = 0, fs = 0;
   for (uint32_t i = tid * per; i < np && i < tid * per + per; ++i) {
     const uint32_t v = H[i];
 #pragma unroll
@@ -206,6 +206,7 @@ __device__ __forceinline__ void hist_spans_flush(const uint32_t* H, uint32_t* M,
       const uint32_t d = (boff + CPW * i + h) >> sA;
       if (d != cd) {
         if (acc) atomicAdd(&M[cd], acc);
+        fs += acc;
         acc = 0;
         cd = d;
       }
@@ -213,6 +214,7 @@ __device__ __forceinline__ void hist_spans_flush(const uint32_t* H, uint32_t* M,
     }
   }
   if (acc) atomicAdd(&M[cd], acc);
+  if (fsum && fs + acc) atomicAdd(fsum, fs + acc);
   __syncthreads();
   if (tid < CP_NAM) {
     uint32_t* const sc = spanc + (uint64_t)blockIdx.x * CP_NAM + tid;
@@ -664,6 +666,8 @@ struct SliceSel {
   int sA = 0;                  // pass B digit bits (the pass A digit = bin >> sA)
   int pbits = 0, pb2 = 0;      // packed records: position bits, prev-code bits (0: key / value planes)
   int pbe = 0;                 // key planes: prev + position-high bits below the relative sym field
+  uint32_t wb = 0, wn1 = 0;    // REG: base << (32 - DB), (nb << (32 - DB)) - 1: a 32-bit window w is
+                               // in the slice iff w - wb <= wn1 (its bin: (w - wb) >> (32 - DB))
   uint32_t tl = 0, th = 0;     // REG: keyed code of byte b = byte ((b >> ps) & 7) of {th, tl}
   int ps = -1;                 // REG: the byte's bit field (-1: no 3-bit field separates the keyed bytes)
 };
@@ -705,13 +709,25 @@ __global__ __launch_bounds__(BH_T, 1) void k_slice_hist_spans(const uint8_t* __r
   __shared__ uint32_t M[CP_NAM];
   __shared__ uint16_t L[256];
   __shared__ uint64_t SK[72];
+  __shared__ uint32_t KT[2];   // NODRAIN: adds, counter fields
   const uint32_t tid = threadIdx.x;
   for (uint32_t i = tid; i < 32768; i += BH_T) H[i] = 0;
   if (tid < CP_NAM) M[tid] = 0;
   if (tid < 256) L[tid] = lutk[tid];
   if (tid < 72) SK[tid] = skey[tid];
+  if (tid < 2) KT[tid] = 0;
   __syncthreads();
+  // REG, CB = 8: no drains.  Plain LDS adds (no returned value to wait for) and a count of the adds;
+  // a byte that wrapped carries into its neighbour (or off the word), so the span's counter fields
+  // then sum to less than the adds: the flush compares the two and raises *ovf (exact recount).
+  constexpr bool NODRAIN = REG && CB == 8;
+  uint32_t kc = 0;
   auto add = [&](uint32_t b) {   // b: the slice bin, < sl.nb
+    if constexpr (NODRAIN) {
+      atomicAdd(&H[b >> 2], 1u << (8 * (b & 3)));
+      ++kc;
+      return;
+    }
     if (hb >= 0 && (b >> 16) != (uint32_t)hb) return;
     const uint32_t bl = b - boff;
     const uint32_t sh = CB * (bl % CPW);
@@ -764,10 +780,18 @@ __global__ __launch_bounds__(BH_T, 1) void k_slice_hist_spans(const uint8_t* __r
       const bool full = p0 + BH_PER <= lim2;
       if constexpr (REG) {
         const uint32_t c0 = pack16_2(a, sl), c1 = pack16_2(b4, sl);
+        if (full) {   // (split so the full body carries no per-position 64-bit bound test)
 #pragma unroll
-        for (int k = 0; k < BH_PER; ++k) {
-          const uint32_t bin = (win32(c0, c1, k) >> dsh) - sl.base;
-          if (bin < sl.nb && (full || p0 + k < lim2)) add(bin);
+          for (int k = 0; k < BH_PER; ++k) {
+            const uint32_t w = win32(c0, c1, k) - sl.wb;
+            if (w <= sl.wn1) add(w >> dsh);
+          }
+        } else {
+#pragma unroll
+          for (int k = 0; k < BH_PER; ++k) {
+            const uint32_t w = win32(c0, c1, k) - sl.wb;
+            if (w <= sl.wn1 && p0 + k < lim2) add(w >> dsh);
+          }
         }
       } else {
         const uint32_t wd[8] = {a.x, a.y, a.z, a.w, b4.x, b4.y, b4.z, b4.w};
@@ -789,9 +813,17 @@ __global__ __launch_bounds__(BH_T, 1) void k_slice_hist_spans(const uint8_t* __r
     }
   }
   if (CB == 8 && bad) atomicOr(ovf, 1ull);
+  if (NODRAIN) {
+    const uint32_t wk = wave_incl_sum<uint32_t>(kc);
+    if ((tid & 63) == 63 && wk) atomicAdd(&KT[0], wk);
+  }
   __syncthreads();
   const uint32_t nbl = hb >= 0 ? 65536u : 1u << D;
-  hist_spans_flush<CB>(H, M, nbl, boff, 1u << D, sA, part, spanc);
+  hist_spans_flush<CB>(H, M, nbl, boff, 1u << D, sA, part, spanc, NODRAIN ? &KT[1] : nullptr);
+  if (NODRAIN) {
+    __syncthreads();
+    if (tid == 0 && KT[0] != KT[1]) atomicOr(ovf, 1ull);
+  }
 }
 
 // Pass A of a slice: workgroup = one unit (g sub-tiles of CP_TILE positions of one span).  Round 1
@@ -1084,10 +1116,8 @@ __global__ __launch_bounds__(CP_T, 4) void k_slice_cpart_reg(uint64_t* __restric
   cnt[tid] = 0;
   __syncthreads();
   const uint64_t lim = n < src.g.s_start ? n : src.g.s_start;
-  const uint64_t kmask_lo = (1ull << (sl.bsh + sl.sA)) - 1;
   const uint64_t sbase = (uint64_t)sl.base << sl.bsh;
   const int kbits = 2 * src.g.q, dsh = 32 - sl.DB;
-  const uint64_t tmask = kbits >= 64 ? ~0ull : (1ull << kbits) - 1;
   // ---- round 1: packed codes, kept-position masks, digit counts.  The unit's loads go out in two
   // batches of SL_G / 2 sub-tiles (all of them at once held ~190 VGPRs: 2 waves per SIMD)
   constexpr int SB = SL_G / 2;
@@ -1123,12 +1153,24 @@ __global__ __launch_bounds__(CP_T, 4) void k_slice_cpart_reg(uint64_t* __restric
     pcs |= pc << (2 * st);
     const bool full = p0 + 16 <= lim;
     uint32_t m = 0;
+    const int dA = dsh + sl.sA;
+    if (full) {
 #pragma unroll
-    for (int k = 0; k < CP_I; ++k) {
-      const uint32_t bin = (win32(c[st][0], c[st][1], k) >> dsh) - sl.base;
-      if (bin < sl.nb && (full || p0 + k < lim)) {
-        m |= 1u << k;
-        atomicAdd(&cnt[bin >> sl.sA], 1u);
+      for (int k = 0; k < CP_I; ++k) {
+        const uint32_t w = win32(c[st][0], c[st][1], k) - sl.wb;
+        if (w <= sl.wn1) {
+          m |= 1u << k;
+          atomicAdd(&cnt[w >> dA], 1u);
+        }
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < CP_I; ++k) {
+        const uint32_t w = win32(c[st][0], c[st][1], k) - sl.wb;
+        if (w <= sl.wn1 && p0 + k < lim) {
+          m |= 1u << k;
+          atomicAdd(&cnt[w >> dA], 1u);
+        }
       }
     }
     for (uint64_t j = p0 > lim ? p0 : lim; j < p0 + 16 && j < n; ++j) {   // short suffixes: boundary keys
@@ -1141,18 +1183,19 @@ __global__ __launch_bounds__(CP_T, 4) void k_slice_cpart_reg(uint64_t* __restric
     msk[st] = m;
   }
   // the record of kept position k of sub-tile st (runtime k) and its pass A digit
+  // (the 64-bit window minus the slice base at its sym field: its top kbits are sym - sbase, whose
+  // low Z bits go to the record and whose bits above them are the pass A digit)
+  const int Z = sl.bsh + sl.sA, pz = sl.pb2 + sl.pbits;
+  const uint64_t wS = sbase << (64 - kbits);
   auto record_at = [&](int st, int k, uint64_t& rec) -> uint32_t {
     const uint64_t j = ubase + (uint64_t)st * SL_SUB + 16ull * tid + (uint64_t)k;
     const int sh = 32 - 2 * k;   // 2..32
     const uint64_t s01 = ((uint64_t)c[st][0] << 32) | c[st][1], s12 = ((uint64_t)c[st][1] << 32) | c[st][2];
-    const uint64_t win = ((uint64_t)(uint32_t)(s01 >> sh) << 32) | (uint32_t)(s12 >> sh);
-    uint64_t sym = kbits >= 64 ? win : (win >> (64 - kbits)) & tmask;
-    if (j >= src.g.s_start) sym = SK[j - src.g.s_start];
+    uint64_t wr = (((uint64_t)(uint32_t)(s01 >> sh) << 32) | (uint32_t)(s12 >> sh)) - wS;
+    if (j >= src.g.s_start) wr = (SK[j - src.g.s_start] - sbase) << (64 - kbits);
     const uint32_t prv = (uint32_t)(((((uint64_t)((pcs >> (2 * st)) & 3u)) << 32) | c[st][0]) >> sh) & 3u;
-    const uint32_t bin = (uint32_t)(sym >> sl.bsh) - sl.base;
-    const uint64_t x = sym - sbase;
-    rec = ((((x & kmask_lo) << sl.pb2) | prv) << sl.pbits) | j;
-    return bin >> sl.sA;
+    rec = (((wr << (kbits - Z)) >> (64 - Z)) << pz) | ((uint64_t)prv << sl.pbits) | j;
+    return (uint32_t)(wr >> (64 - kbits + Z));
   };
   __syncthreads();
   const uint32_t cu = cnt[tid];
@@ -1187,15 +1230,25 @@ __global__ __launch_bounds__(CP_T, 4) void k_slice_cpart_reg(uint64_t* __restric
 #pragma unroll
     for (int st = 0; st < SL_G; ++st) {
       uint32_t m = msk[st];
-      while (m) {
+      while (m) {   // two kept positions a trip: their slot atomics in flight together
         const int k = __builtin_ctz(m);
         m &= m - 1;
-        uint64_t rec;
+        const bool two = m != 0;
+        const int k2 = two ? __builtin_ctz(m) : k;
+        m &= m - 1;
+        uint64_t rec, rec2;
         const uint32_t d = record_at(st, k, rec);
+        const uint32_t d2 = record_at(st, k2, rec2);
         uint32_t f = tg[d] + atomicAdd(&cnt[d], 1u);
+        uint32_t f2 = two ? tg[d2] + atomicAdd(&cnt[d2], 1u) : 0u;
         f = f < (uint32_t)CP_TILE ? f : (uint32_t)CP_TILE - 1;   // (only a count mismatch overruns)
         keys[f] = rec;
         sdg[f] = (uint8_t)d;
+        if (two) {
+          f2 = f2 < (uint32_t)CP_TILE ? f2 : (uint32_t)CP_TILE - 1;
+          keys[f2] = rec2;
+          sdg[f2] = (uint8_t)d2;
+        }
       }
     }
     __syncthreads();
@@ -3114,6 +3167,8 @@ SlicePlan plan_slice(Index& ix, uint32_t c_lo, uint32_t c_hi, bool u64pos) {
   sl.nb = k << f;
   sl.hq = (sl.DB + lb - 1) / lb;
   sl.wdrop = sl.hq * lb - sl.DB;
+  sl.wb = sl.base << (32 - sl.DB);
+  sl.wn1 = (uint32_t)(((uint64_t)sl.nb << (32 - sl.DB)) - 1);
   P.D = 1;
   while ((1u << P.D) < sl.nb) ++P.D;
   sl.sA = P.D > 8 ? 8 : 0;
@@ -3282,6 +3337,7 @@ static int cursor_partition_slice(Index& ix, const SlicePlan& P, const TextKeySr
   counts_then_passA();
   if (D > 16 && *h_ovf) {   // u8 counters overflowed: exact recount, pass A again
     ix.info[0] -= 1;
+    if (ix.info.size() > 7) ix.info[7] |= 8;
     prepass(true);
     counts_then_passA();
   }
@@ -3356,9 +3412,10 @@ void build_slice_keyed(Index& ix, uint32_t c_lo, uint32_t c_hi, uint64_t m) {
   ix.info[6] = plan.big_total;
   static const bool dbg = getenv("HKCSA_SHARD_DEBUG") != nullptr;
   if (dbg)
-    fprintf(stderr, "[slice-k] m=%llu q=%d sb=%d f=%d bsh=%d D=%d nb=%u g=%u packed=%d pbits=%d hmax=%llu items=%zu big=%zu\n",
+    fprintf(stderr, "[slice-k] m=%llu q=%d sb=%d f=%d bsh=%d D=%d nb=%u g=%u packed=%d pbits=%d hmax=%llu items=%zu big=%zu recount=%d\n",
             (unsigned long long)m, kk.q, kk.sym_bits, P.sl.DB - 16, P.sl.bsh, P.D, P.sl.nb, P.sl.g, P.packed ? 1 : 0,
-            P.sl.pbits, (unsigned long long)hmax, plan.items_n.size() + plan.items_w.size(), plan.big_start.size());
+            P.sl.pbits, (unsigned long long)hmax, plan.items_n.size() + plan.items_w.size(), plan.big_start.size(),
+            (int)(ix.info[7] >> 3 & 1));
   ix.bwt.ensure(m + 64);
   if (!plan.big_total && !(ix.flags & kFlagGlobalSort)) {
     const uint64_t ntie = sort_bucket_items<V>(ix, plan, kp[slot], vp[slot], m, P.pb, sbx, P.packed ? 0 : P.hb, 0,
