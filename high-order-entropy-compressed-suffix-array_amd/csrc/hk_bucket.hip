@@ -749,33 +749,22 @@ __global__ __launch_bounds__(BH_T, 1) void k_slice_hist_spans(const uint8_t* __r
   static_assert(NI <= 2 * BH_PER, "window past the thread's 32 bytes");
   const int wbits = hq * lb, wdrop = sl.wdrop, dsh = 32 - sl.DB;
   const uint32_t bmask = wbits >= 32 ? ~0u : (1u << wbits) - 1;
-  // the next PF iterations' bytes in flight (one iteration ahead left the scan latency-bound at ~1.4 TB/s)
-  constexpr int PF = REG ? 3 : 1;
+  // PF iterations' bytes in flight: slot u's registers are consumed, then reloaded with the bytes PF
+  // iterations ahead (a rotating prefetch makes the compiler copy the new registers at the back edge,
+  // which waits for the loads just issued)
+  // (the loads are unconditional, a position past the span reads the span's first bytes instead: a
+  // load under a branch leaves the wait-count pass no exact count, so it waits for all of them)
+  constexpr int PF = REG ? 4 : 2;
   uint4 f0[PF], f1[PF];
+  auto fetch = [&](uint64_t p, uint4& x0, uint4& x1) {
+    const uint4* src = reinterpret_cast<const uint4*>(t + (p < hi ? p : lo));
+    x0 = src[0];
+    x1 = src[1];
+  };
 #pragma unroll
-  for (int u = 0; u < PF; ++u) {
-    f0[u] = f1[u] = make_uint4(0, 0, 0, 0);
-    const uint64_t pu = lo + (uint64_t)u * BH_TILE + (uint64_t)tid * BH_PER;
-    if (pu < hi) {
-      const uint4* src = reinterpret_cast<const uint4*>(t + pu);
-      f0[u] = src[0];
-      f1[u] = src[1];
-    }
-  }
-  for (uint64_t base = lo; base < hi; base += BH_TILE) {
-    const uint64_t p0 = base + (uint64_t)tid * BH_PER;
-    const uint4 a = f0[0], b4 = f1[0];
-#pragma unroll
-    for (int u = 0; u + 1 < PF; ++u) {
-      f0[u] = f0[u + 1];
-      f1[u] = f1[u + 1];
-    }
-    if (p0 + PF * BH_TILE < hi) {
-      const uint4* src = reinterpret_cast<const uint4*>(t + p0 + PF * BH_TILE);
-      f0[PF - 1] = src[0];
-      f1[PF - 1] = src[1];
-    }
-    const uint64_t lim2 = lim < hi ? lim : hi;
+  for (int u = 0; u < PF; ++u) fetch(lo + (uint64_t)u * BH_TILE + (uint64_t)tid * BH_PER, f0[u], f1[u]);
+  const uint64_t lim2 = lim < hi ? lim : hi;
+  auto step = [&](uint64_t p0, const uint4 a, const uint4 b4) {
     if (p0 < lim2) {
       const bool full = p0 + BH_PER <= lim2;
       if constexpr (REG) {
@@ -810,6 +799,16 @@ __global__ __launch_bounds__(BH_T, 1) void k_slice_hist_spans(const uint8_t* __r
     for (uint64_t p = p0 > lim ? p0 : lim; p < p0 + BH_PER && p < hi; ++p) {
       const uint32_t bin = (uint32_t)(SK[p - g.s_start] >> sl.bsh) - sl.base;
       if (bin < sl.nb) add(bin);
+    }
+  };
+  for (uint64_t base = lo; base < hi; base += PF * BH_TILE) {
+#pragma unroll
+    for (int u = 0; u < PF; ++u) {
+      const uint64_t bu = base + (uint64_t)u * BH_TILE;
+      if (bu >= hi) break;   // uniform
+      const uint64_t p0 = bu + (uint64_t)tid * BH_PER;
+      step(p0, f0[u], f1[u]);
+      fetch(p0 + PF * BH_TILE, f0[u], f1[u]);
     }
   }
   if (CB == 8 && bad) atomicOr(ovf, 1ull);
@@ -2322,6 +2321,8 @@ struct PackedRecs {
   uint64_t* kfull = nullptr;
   uint32_t* vfull = nullptr;
   int uhb = 0;                        // u64 positions: hb of the unpacked key layout
+  bool reg = false;                   // radix 2^2 with a perm table: the register pre-pass (rsl)
+  SliceSel rsl;                       // ... as a slice of every bucket
 };
 
 void unpack_items(Index& ix, const PackedRecs& pk, const uint64_t* rec, const uint2* d_items, uint32_t nitems) {
@@ -2864,11 +2865,17 @@ int cursor_partition(Index& ix, uint64_t n, int D, int bitlo, uint64_t kbias, co
     TimedLaunch t(ix.timer, "sa_bucket_hist", (double)n * (tks ? (exact ? 2 : 1) : 8));
     if (tks && D > 16 && !exact) {   // 2^17 buckets: u8 counters (drained at 128)
       const int lbk = 31 - __builtin_clz((uint32_t)tks->g.Rk);
-      auto kern = k_bucket_hist_spans<8>;
-      if (hist_fixed_enabled() && lbk == 2 && tks->g.hq == 9) kern = k_bucket_hist_spans<8, -1, 2, 9>;
-      else if (hist_fixed_enabled() && lbk == 8 && tks->g.hq == 3) kern = k_bucket_hist_spans<8, -1, 8, 3>;
-      kern<<<nspan, BH_T, 0, s>>>(tks->text, n, tks->lutk, tks->skey, tks->g, bitlo - tks->g.pb, D, sA, d_part,
-                                  d_drain, d_spanc, span, d_ovf);
+      if (packed && pk->reg) {   // register scan, undrained u8 counters (checked; exact recount on a wrap)
+        k_slice_hist_spans<8, -1, 2, 0, true><<<nspan, BH_T, 0, s>>>(tks->text, n, tks->lutk, tks->skey, tks->g,
+                                                                     pk->rsl, D, d_part, d_drain, d_spanc, span,
+                                                                     d_ovf);
+      } else {
+        auto kern = k_bucket_hist_spans<8>;
+        if (hist_fixed_enabled() && lbk == 2 && tks->g.hq == 9) kern = k_bucket_hist_spans<8, -1, 2, 9>;
+        else if (hist_fixed_enabled() && lbk == 8 && tks->g.hq == 3) kern = k_bucket_hist_spans<8, -1, 8, 3>;
+        kern<<<nspan, BH_T, 0, s>>>(tks->text, n, tks->lutk, tks->skey, tks->g, bitlo - tks->g.pb, D, sA, d_part,
+                                    d_drain, d_spanc, span, d_ovf);
+      }
     } else if (tks) {
       if (D > 16) {
         k_bucket_hist_spans<16, 0><<<nspan, BH_T, 0, s>>>(tks->text, n, tks->lutk, tks->skey, tks->g,
@@ -3097,6 +3104,32 @@ struct SlicePlan {
   int uhb = 0;
 };
 
+}  // namespace
+
+// Register-scan tables (radix 2^2 keyed codes): the 3-bit field (b >> ps) & 7 of a byte that separates
+// the keyed bytes indexes an 8-entry table of their codes; false when no field separates them
+static bool reg_tables(const KeyGeom& kk, SliceSel& sl) {
+  for (int ps = 0; ps <= 5; ++ps) {
+    uint8_t tab[8] = {0};
+    bool used[8] = {false}, ok = true;
+    for (int b = 0; b < 256 && ok; ++b) {
+      if (!kk.kflag[b]) continue;
+      const int idx = (b >> ps) & 7;
+      ok = !used[idx];
+      used[idx] = true;
+      tab[idx] = (uint8_t)kk.kdig[b];
+    }
+    if (!ok) continue;
+    sl.ps = ps;
+    sl.tl = (uint32_t)tab[0] | (uint32_t)tab[1] << 8 | (uint32_t)tab[2] << 16 | (uint32_t)tab[3] << 24;
+    sl.th = (uint32_t)tab[4] | (uint32_t)tab[5] << 8 | (uint32_t)tab[6] << 16 | (uint32_t)tab[7] << 24;
+    return true;
+  }
+  return false;
+}
+
+namespace {
+
 // Geometry of the slice of coarse buckets [c_lo, c_hi): f = the most extra bin bits with at most 2^17
 // bins (k << f) and a pre-pass window of <= 16 symbols; packed records when the bits below the pass A
 // digit, the prev code and the position fit one u64 (q capped for that), else key / value planes.
@@ -3188,24 +3221,7 @@ SlicePlan plan_slice(Index& ix, uint32_t c_lo, uint32_t c_hi, bool u64pos) {
   // indexes an 8-entry table of their codes (every byte the scans key is keyed: the unkeyed terminal
   // only ends short suffixes, which take their boundary keys)
   static const bool reg_env = !getenv("HKCSA_SLICE_REG") || atoi(getenv("HKCSA_SLICE_REG")) != 0;
-  if (reg_env && packed && lb == 2) {
-    for (int ps = 0; ps <= 5 && !P.reg; ++ps) {
-      uint8_t tab[8] = {0};
-      bool used[8] = {false}, ok = true;
-      for (int b = 0; b < 256 && ok; ++b) {
-        if (!kk.kflag[b]) continue;
-        const int idx = (b >> ps) & 7;
-        ok = !used[idx];
-        used[idx] = true;
-        tab[idx] = (uint8_t)kk.kdig[b];
-      }
-      if (!ok) continue;
-      P.reg = true;
-      sl.ps = ps;
-      sl.tl = (uint32_t)tab[0] | (uint32_t)tab[1] << 8 | (uint32_t)tab[2] << 16 | (uint32_t)tab[3] << 24;
-      sl.th = (uint32_t)tab[4] | (uint32_t)tab[5] << 8 | (uint32_t)tab[6] << 16 | (uint32_t)tab[7] << 24;
-    }
-  }
+  if (reg_env && packed && lb == 2) P.reg = reg_tables(kk, sl);
   return P;
 }
 
@@ -3588,6 +3604,19 @@ void build_sa_bucketed(Index& ix) {
         pkr.lutp2[b] = pkr.g.tcode < 0 ? kg.lutp[b] : (kg.kflag[b] ? kg.kdig[b] : 0);
       pkr.kfull = kp[1];
       pkr.vfull = vp[1];
+      // radix 2^2: the register pre-pass over all 2^17 buckets (HKCSA_HIST_REG=0: the LDS-table scan)
+      static const bool hreg = !getenv("HKCSA_HIST_REG") || atoi(getenv("HKCSA_HIST_REG")) != 0;
+      SliceSel& r = pkr.rsl;
+      if (hreg && tks.g.lb == 2 && reg_tables(kg, r)) {
+        r.base = 0;
+        r.nb = 1u << 17;
+        r.DB = 17;
+        r.bsh = bsh;
+        r.sA = 8;
+        r.wb = 0;
+        r.wn1 = ~0u;
+        pkr.reg = true;
+      }
     }
   }
   const bool packed = pkr.g.pbits > 0;

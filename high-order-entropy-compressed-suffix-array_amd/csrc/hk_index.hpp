@@ -112,6 +112,12 @@ struct Index {
   DevBuf occ_lines, occ_sb;       // count: flat occ directory of the BWT (sigma <= 8, build_wt)
   bool occ_ok = false;
   uint64_t occ_nsb = 0;
+  // count: two-level 16-ary occ directory (8 < sigma <= 256, build_wt): level 0 = the BWT's WT node
+  // at depth nib_g, level 1 = the WT's depth-nib_g sequence as code - node start; tables in nib_tab
+  DevBuf nib_lines[2], nib_sb[2], nib_tab;
+  bool nib_ok = false;
+  int nib_g = 0;
+  uint64_t nib_nsb = 0;
   DevBuf tile_a, tile_b, tile_c, tile_d, tile_e;
   DevBuf small;                // scratch for totals etc.
   HostBuf small_host;          // pinned staging of the geometry tables (one upload per geometry)
