@@ -323,10 +323,12 @@ def run_single(args) -> dict:
     t_wt = time_wt(dev, args.wt_reps)
     wt_roof = roofline(dev, WT_KERNELS, leg)
     dev.timing(False)
-    loc = None
+    loc = eps = None
     if args.patterns > 0:
         data, offs = pattern_batch(dev, n, args.patterns, args.plen, args.seed + 1)
         loc = time_queries(dev, data, offs, args.query_reps)
+        if args.eps:
+            eps = epsilon_leg(dev, n, data, offs, args.query_reps, loc)
     dev.close()
     pcie = pcie_inclusive(n, alpha, args.seed + 7) if args.pcie else None
     res = {
@@ -354,9 +356,43 @@ def run_single(args) -> dict:
         "full_build_MBps": round(n / 2**20 / (wall / args.steps + t_wt), 2),
         "detail": {"wt_build_ms": round(t_wt * 1e3, 3), "wt_roofline": wt_roof, "locate": loc,
                    "pattern_source": f"uniform substrings of a {PATTERN_WINDOW >> 20} MiB window of the text",
-                   "stages_ms_total": stages, "build_info": info[:16], "pcie_inclusive": pcie},
+                   "stages_ms_total": stages, "build_info": info[:16], "pcie_inclusive": pcie,
+                   "epsilon": eps},
     }
     return res
+
+
+def epsilon_leg(dev, n: int, data, offs, reps: int, full: dict) -> dict:
+    """CompressedSuffixArray(text, epsilon=0.5)'s compact mode on the bench index (tests/benchmark.py:25,
+    32,47): SA/ISA samples every ceil(log2(n) ** 0.5) positions + compact (the SA, BWT and text leave
+    HBM), timed once, then the same patterns located by LF walks over the wavelet tree (identical
+    answers: tests/test_gpu_parity.py test_sampled_*).  Runs last: the index keeps only samples."""
+    from csa.csa import sample_rate
+    rate = sample_rate(n, 0.5)
+    dev.synchronize()
+    dev.timing_reset()
+    dev.timing(True)
+    t0 = time.perf_counter()
+    dev.build_samples(rate)
+    dev.compact()
+    dev.synchronize()
+    t_s = time.perf_counter() - t0
+    smp_ms = {k: round(dev.kernel_stats(k)[1], 3) for k in ("smp_mark", "smp_fill", "smp_fix")}
+    sp = dev.space()
+    dev.timing_reset()
+    qq = time_queries(dev, data, offs, reps)
+    l, ms, _ = dev.kernel_stats("fm_locate_sampled")
+    dev.timing(False)
+    if qq["occurrences"] != full["occurrences"]:
+        raise RuntimeError("sampled locate disagrees with the full-SA locate")
+    log(f"[bench] epsilon=0.5 (rate {rate}): samples+compact {t_s * 1e3:.2f} ms, "
+        f"locate {qq['locate_patterns_per_s']:.3g} patterns/s")
+    return {"epsilon": 0.5, "sample_rate": rate, "samples_compact_ms": round(t_s * 1e3, 3),
+            "sample_kernels_ms": smp_ms, "space_bytes": sp,
+            "locate_patterns_per_s": qq["locate_patterns_per_s"], "count_patterns_per_s": qq["count_patterns_per_s"],
+            "locate_sampled_kernel_ms": round(ms / max(1, l), 4), "occurrences": qq["occurrences"],
+            "patterns": qq["patterns"], "plen": qq["plen"],
+            "vs_full_sa_locate": round(qq["locate_patterns_per_s"] / full["locate_patterns_per_s"], 4)}
 
 
 def run_extra_legs(args, res: dict):
@@ -640,6 +676,8 @@ def parse_args(argv=None):
     ap.add_argument("--cpu-config0", type=int, default=1 << 20)
     ap.add_argument("--cpu-patterns", type=int, default=1000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-eps", dest="eps", action="store_false",
+                    help="skip the epsilon=0.5 compact-mode leg (samples + LF-walk locate) at N = 1")
     ap.add_argument("--no-pcie", dest="pcie", action="store_false",
                     help="skip the host-buffer (PCIe-inclusive) build after the timed steps")
     ap.add_argument("--sharded", action="store_true", help="use the sharded (multi-GPU) build even at N=1")

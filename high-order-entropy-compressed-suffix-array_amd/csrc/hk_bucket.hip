@@ -2464,10 +2464,10 @@ uint64_t sort_bucket_items(Index& ix, const BucketPlan& plan, const uint64_t* ke
               acc[6] / nn, acc[2] / nn, acc[3] / nn, acc[4] / nn);
     }
   }
-  uint64_t ntie = 0;
-  HK_HIP(hipMemcpyAsync(&ntie, ix.ties_n.p, 8, hipMemcpyDeviceToHost, s));
+  uint64_t* const h = ix.rb();
+  HK_HIP(hipMemcpyAsync(h, ix.ties_n.p, 8, hipMemcpyDeviceToHost, s));
   HK_HIP(hipStreamSynchronize(s));
-  return ntie;
+  return h[0];
 }
 
 // starts[b] = first index of bin b in keys sorted by bin = ((key - kbias) >> shift) & (nbins - 1)
@@ -2635,9 +2635,10 @@ void refine_from_ties(Index& ix, const KeyGeom& kg, uint64_t A, bool allow_doubl
   scan_exclusive_u32_to_u64(ix.sw, GH, hx, A, true, s);
   k_tie_groups<<<grid_of(A), 256, 0, s>>>(hx, J, A, GH, ix.head_slot.as<uint32_t>());
   HK_HIP(hipGetLastError());
-  uint64_t groups = 0;
-  HK_HIP(hipMemcpyAsync(&groups, hx + A, 8, hipMemcpyDeviceToHost, s));
+  uint64_t* const hg = ix.rb();
+  HK_HIP(hipMemcpyAsync(hg, hx + A, 8, hipMemcpyDeviceToHost, s));
   HK_HIP(hipStreamSynchronize(s));
+  const uint64_t groups = hg[0];
   refine_loop<V>(ix, kg, 0, A, groups, allow_doubling);
 }
 

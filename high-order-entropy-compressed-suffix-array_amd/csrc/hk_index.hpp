@@ -122,6 +122,12 @@ struct Index {
   DevBuf small;                // scratch for totals etc.
   HostBuf small_host;          // pinned staging of the geometry tables (one upload per geometry)
   HostBuf items_host;          // pinned staging of the bucket-sort work items
+  HostBuf rb_host;             // pinned landing slots of the build's small read-backs (counts, totals)
+  uint64_t* rb(int k = 4) {    // k u64 slots
+    rb_host.ensure(64);
+    (void)k;
+    return static_cast<uint64_t*>(rb_host.p);
+  }
   DevBuf seq[2];               // WT level code sequences
   DevBuf gr_tmp[2], gr_out;    // Golomb-Rice coding of a level (per-word carries/offsets, code words)
 
@@ -132,6 +138,7 @@ struct Index {
   uint32_t smp_rate = 0;
   uint64_t smp_count = 0, smp_fixn = 0;
   int smp_cstar = 0;
+  bool smp_w64 = false;        // 8-byte samples (the SA was u64)
   DevBuf smp_mark, smp_sa, smp_isa, smp_fix, smp_inv;
 
   // sharded construction

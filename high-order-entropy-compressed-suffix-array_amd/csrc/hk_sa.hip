@@ -677,7 +677,7 @@ void dbl_round_t(Index& ix, uint64_t K) {
         ix.head_slot.as<uint32_t>());
     HK_HIP(hipGetLastError());
   }
-  uint64_t tot[2] = {0, 0};
+  uint64_t* const tot = ix.rb();   // pinned: the copies land without a staging hop
   HK_HIP(hipMemcpyAsync(&tot[0], ao + nt, 8, hipMemcpyDeviceToHost, s));
   HK_HIP(hipMemcpyAsync(&tot[1], ho + nt, 8, hipMemcpyDeviceToHost, s));
   HK_HIP(hipStreamSynchronize(s));
@@ -722,7 +722,7 @@ std::pair<uint64_t, uint64_t> refine_step(Index& ix, const KeyGeom& kg, const ui
           bwt, inv, 0, ix.text.as<uint8_t>(), ix.n, oP, oJ, oG, head_slot);
     HK_HIP(hipGetLastError());
   }
-  uint64_t tot[2];
+  uint64_t* const tot = ix.rb();
   HK_HIP(hipMemcpyAsync(&tot[0], ix.tile_a.as<uint64_t>() + nt, 8, hipMemcpyDeviceToHost, s));
   HK_HIP(hipMemcpyAsync(&tot[1], ix.tile_d.as<uint64_t>() + nt, 8, hipMemcpyDeviceToHost, s));
   HK_HIP(hipStreamSynchronize(s));

@@ -8,6 +8,8 @@
 //   samp_sa     SA[i] of the marked rows, in row order               4 · ceil(n/s) bytes
 //   samp_isa    row of text position k·s                             4 · ceil(n/s) bytes
 //   fix         the true LF of the rows whose BWT symbol is c* = T'[n-1]   4 · occ(c*) bytes
+// (4-byte words while n < 2^32; a replicated index of a text with >= 2^32 suffixes, whose SA is u64,
+// keeps 8-byte samples: every kernel below is templated on the word W)
 //
 // Why `fix`: BWT[row of SA=0] wraps to T'[n-1] (csa/bwt.py:8-11), so the c*-rows of the BWT are
 // the suffixes preceded by c* plus the wrapped row.  For every other symbol c, C[c] + occ(c, i)
@@ -20,6 +22,8 @@
 //   extract(i,j): one lane per sample interval [k·s, (k+1)·s): start at the row of (k+1)·s (the
 //                 row of 0 for the interval ending at n) and emit BWT[row] = T'[p-1] while
 //                 stepping row = LF(row).
+#include <type_traits>
+
 #include "hk_index.hpp"
 #include "hk_wtq.hpp"
 
@@ -32,7 +36,8 @@ inline unsigned grid_for(uint64_t n, unsigned per = 256, unsigned cap = 16384) {
 }
 
 // one wave per 448-row line: 7 ballots of (SA[j] % s == 0)
-__global__ __launch_bounds__(256) void k_smp_bits(const uint32_t* __restrict__ sa, uint64_t n, uint32_t s,
+template <typename W>
+__global__ __launch_bounds__(256) void k_smp_bits(const W* __restrict__ sa, uint64_t n, uint32_t s,
                                                   uint64_t* __restrict__ lines, uint32_t* __restrict__ line_pop,
                                                   uint64_t nlines) {
   const uint32_t lane = threadIdx.x & 63;
@@ -62,21 +67,23 @@ __global__ __launch_bounds__(256) void k_smp_fill_lines(uint64_t* __restrict__ l
     lines[li * 8] = excl[li];
 }
 
-__global__ __launch_bounds__(256) void k_smp_fill(const uint32_t* __restrict__ sa, uint64_t n, uint32_t s,
-                                                  const uint64_t* __restrict__ mark, uint32_t* __restrict__ ssa,
-                                                  uint32_t* __restrict__ sisa) {
+template <typename W>
+__global__ __launch_bounds__(256) void k_smp_fill(const W* __restrict__ sa, uint64_t n, uint32_t s,
+                                                  const uint64_t* __restrict__ mark, W* __restrict__ ssa,
+                                                  W* __restrict__ sisa) {
   for (uint64_t j = (uint64_t)blockIdx.x * 256 + threadIdx.x; j < n; j += (uint64_t)gridDim.x * 256) {
-    const uint32_t p = sa[j];
+    const W p = sa[j];
     if (p % s) continue;
     ssa[rank1(mark, j)] = p;
-    sisa[p / s] = (uint32_t)j;
+    sisa[p / s] = (W)j;
   }
 }
 
 // c*-rows i: tmp[SA[i]] = occ(c*, i) (their order among the c*-rows)
-__global__ __launch_bounds__(256) void k_fix_a(WtView v, const uint32_t* __restrict__ sa,
+template <typename W>
+__global__ __launch_bounds__(256) void k_fix_a(WtView v, const W* __restrict__ sa,
                                                const uint8_t* __restrict__ bwt, uint8_t cstar_byte, int cstar,
-                                               uint32_t* __restrict__ tmp) {
+                                               W* __restrict__ tmp) {
   __shared__ QShared q;
   load_qshared(q, v);
   const uint64_t n = v.n;
@@ -84,40 +91,44 @@ __global__ __launch_bounds__(256) void k_fix_a(WtView v, const uint32_t* __restr
     if (bwt[i] != cstar_byte) continue;
     uint64_t x = i, y = i;
     lf_pair(q, cstar, x, y);
-    tmp[sa[i]] = (uint32_t)(x - v.Ccode[cstar]);
+    tmp[sa[i]] = (W)(x - v.Ccode[cstar]);
   }
 }
 
 // rows j of the c* bucket: the c*-row whose suffix is SA[j]+1 (cyclically) has true LF j
-__global__ __launch_bounds__(256) void k_fix_b(const uint32_t* __restrict__ sa, uint64_t n, uint64_t b0, uint64_t cnt,
-                                               const uint32_t* __restrict__ tmp, uint32_t* __restrict__ fix) {
+template <typename W>
+__global__ __launch_bounds__(256) void k_fix_b(const W* __restrict__ sa, uint64_t n, uint64_t b0, uint64_t cnt,
+                                               const W* __restrict__ tmp, W* __restrict__ fix) {
   for (uint64_t k = (uint64_t)blockIdx.x * 256 + threadIdx.x; k < cnt; k += (uint64_t)gridDim.x * 256) {
     const uint64_t j = b0 + k;
     uint64_t p = (uint64_t)sa[j] + 1;
     if (p == n) p = 0;
-    fix[tmp[p]] = (uint32_t)j;
+    fix[tmp[p]] = (W)j;
   }
 }
 
+template <typename W>
 struct SmpView {
   const uint64_t* mark;
-  const uint32_t* ssa;
-  const uint32_t* sisa;
-  const uint32_t* fix;
+  const W* ssa;
+  const W* sisa;
+  const W* fix;
   uint64_t cbase;   // C[c*] (first row of the c* bucket)
   int cstar;
   uint32_t s;
 };
 
 // exact cyclic LF (row of suffix SA[x]-1) and the BWT code of row x
-__device__ __forceinline__ uint64_t lf_exact(const QShared& q, const WtView& v, const SmpView& m, uint64_t x,
+template <typename W>
+__device__ __forceinline__ uint64_t lf_exact(const QShared& q, const WtView& v, const SmpView<W>& m, uint64_t x,
                                              int& code) {
   uint64_t y = lf_access(q, v.sigma, x, code);
   if (code == m.cstar) y = m.fix[y - m.cbase];
   return y;
 }
 
-__device__ __forceinline__ uint64_t sa_of_row(const QShared& q, const WtView& v, const SmpView& m, uint64_t x) {
+template <typename W>
+__device__ __forceinline__ uint64_t sa_of_row(const QShared& q, const WtView& v, const SmpView<W>& m, uint64_t x) {
   uint64_t k = 0;
   for (;;) {
     uint32_t b;
@@ -131,7 +142,8 @@ __device__ __forceinline__ uint64_t sa_of_row(const QShared& q, const WtView& v,
 
 constexpr uint64_t kSmallOcc = 32;
 
-__global__ __launch_bounds__(256) void k_locate_smp_small(WtView v, SmpView m, const int64_t* __restrict__ lr,
+template <typename W>
+__global__ __launch_bounds__(256) void k_locate_smp_small(WtView v, SmpView<W> m, const int64_t* __restrict__ lr,
                                                           const uint64_t* __restrict__ oo, uint64_t P,
                                                           uint64_t* __restrict__ pos, uint64_t* big,
                                                           unsigned long long* nbig) {
@@ -150,7 +162,8 @@ __global__ __launch_bounds__(256) void k_locate_smp_small(WtView v, SmpView m, c
   }
 }
 
-__global__ __launch_bounds__(256) void k_locate_smp_big(WtView v, SmpView m, const int64_t* __restrict__ lr,
+template <typename W>
+__global__ __launch_bounds__(256) void k_locate_smp_big(WtView v, SmpView<W> m, const int64_t* __restrict__ lr,
                                                         const uint64_t* __restrict__ oo,
                                                         const uint64_t* __restrict__ big,
                                                         const unsigned long long* __restrict__ nbig,
@@ -168,7 +181,8 @@ __global__ __launch_bounds__(256) void k_locate_smp_big(WtView v, SmpView m, con
 }
 
 // SA[lo + t] for t < count (full-array export in compressed mode)
-__global__ __launch_bounds__(256) void k_sa_range_smp(WtView v, SmpView m, uint64_t lo, uint64_t count,
+template <typename W>
+__global__ __launch_bounds__(256) void k_sa_range_smp(WtView v, SmpView<W> m, uint64_t lo, uint64_t count,
                                                       uint64_t* __restrict__ out) {
   __shared__ QShared q;
   load_qshared(q, v);
@@ -189,7 +203,8 @@ __global__ __launch_bounds__(256) void k_bwt_range(WtView v, uint64_t lo, uint64
 }
 
 // T'[i:j): one lane per sample interval
-__global__ __launch_bounds__(256) void k_extract_smp(WtView v, SmpView m, uint64_t i, uint64_t j,
+template <typename W>
+__global__ __launch_bounds__(256) void k_extract_smp(WtView v, SmpView<W> m, uint64_t i, uint64_t j,
                                                      const uint8_t* __restrict__ inv, uint8_t* __restrict__ out) {
   __shared__ QShared q;
   load_qshared(q, v);
@@ -209,41 +224,37 @@ __global__ __launch_bounds__(256) void k_extract_smp(WtView v, SmpView m, uint64
   }
 }
 
-}  // namespace
-
-SmpView smp_view(const Index& ix) {
-  return SmpView{ix.smp_mark.as<uint64_t>(), ix.smp_sa.as<uint32_t>(), ix.smp_isa.as<uint32_t>(),
-                 ix.smp_fix.as<uint32_t>(), ix.Ccode[ix.smp_cstar], ix.smp_cstar, ix.smp_rate};
+template <typename W>
+SmpView<W> smp_view(const Index& ix) {
+  return SmpView<W>{ix.smp_mark.as<uint64_t>(), ix.smp_sa.as<W>(), ix.smp_isa.as<W>(), ix.smp_fix.as<W>(),
+                    ix.Ccode[ix.smp_cstar], ix.smp_cstar, ix.smp_rate};
 }
 
-void build_samples(Index& ix, uint32_t rate) {
-  if (rate == 0) throw ApiError{-2, "sample rate must be positive"};
-  if (!ix.have_sa || ix.sharded || ix.sa_pos64) throw ApiError{-3, "samples: single-GPU suffix array not built"};
-  if (!ix.have_bwt || !ix.have_text) throw ApiError{-3, "samples: BWT not built"};
-  if (!ix.have_wt) build_wt(ix);
+template <typename W>
+void build_samples_t(Index& ix, uint32_t rate) {
   hipStream_t s = ix.stream;
   const uint64_t n = ix.n;
   const uint64_t nlines = n / kLineBits + 1;
-  const uint32_t* sa = ix.sa.as<uint32_t>();
+  const W* sa = ix.sa.as<W>();
   ix.smp_mark.ensure(nlines * 64);
   ix.tile_b.ensure(nlines * 4 + 16);
   ix.tile_a.ensure(nlines * 8 + 16);
   {
-    TimedLaunch t(ix.timer, "smp_mark", (double)n * 4 + (double)nlines * 64);
-    k_smp_bits<<<grid_for(nlines, 4, 8192), 256, 0, s>>>(sa, n, rate, ix.smp_mark.as<uint64_t>(),
-                                                         ix.tile_b.as<uint32_t>(), nlines);
+    TimedLaunch t(ix.timer, "smp_mark", (double)n * sizeof(W) + (double)nlines * 64);
+    k_smp_bits<W><<<grid_for(nlines, 4, 8192), 256, 0, s>>>(sa, n, rate, ix.smp_mark.as<uint64_t>(),
+                                                            ix.tile_b.as<uint32_t>(), nlines);
     HK_HIP(hipGetLastError());
   }
   scan_exclusive_u32_to_u64(ix.sw, ix.tile_b.as<uint32_t>(), ix.tile_a.as<uint64_t>(), nlines, false, s);
   k_smp_fill_lines<<<grid_for(nlines), 256, 0, s>>>(ix.smp_mark.as<uint64_t>(), ix.tile_a.as<uint64_t>(), nlines);
   HK_HIP(hipGetLastError());
   const uint64_t ns = ceil_div(n, rate);   // positions 0, s, 2s, ... < n
-  ix.smp_sa.ensure(ns * 4 + 16);
-  ix.smp_isa.ensure(ns * 4 + 16);
+  ix.smp_sa.ensure(ns * sizeof(W) + 16);
+  ix.smp_isa.ensure(ns * sizeof(W) + 16);
   {
-    TimedLaunch t(ix.timer, "smp_fill", (double)n * 4 + (double)ns * 8);
-    k_smp_fill<<<grid_for(n), 256, 0, s>>>(sa, n, rate, ix.smp_mark.as<uint64_t>(), ix.smp_sa.as<uint32_t>(),
-                                           ix.smp_isa.as<uint32_t>());
+    TimedLaunch t(ix.timer, "smp_fill", (double)n * sizeof(W) + (double)ns * 2 * sizeof(W));
+    k_smp_fill<W><<<grid_for(n), 256, 0, s>>>(sa, n, rate, ix.smp_mark.as<uint64_t>(), ix.smp_sa.as<W>(),
+                                              ix.smp_isa.as<W>());
     HK_HIP(hipGetLastError());
   }
   // exact LF of the c*-rows
@@ -252,15 +263,14 @@ void build_samples(Index& ix, uint32_t rate) {
   HK_HIP(hipStreamSynchronize(s));
   const int cstar = ix.code_of[last];
   const uint64_t cnt = ix.Ccode[cstar + 1] - ix.Ccode[cstar];
-  ix.smp_fix.ensure(cnt * 4 + 16);
-  ix.isa.ensure(n * 4 + 16);   // scratch: tmp[SA[i]] for the c*-rows
+  ix.smp_fix.ensure(cnt * sizeof(W) + 16);
+  ix.isa.ensure(n * sizeof(W) + 16);   // scratch: tmp[SA[i]] for the c*-rows
   {
-    TimedLaunch t(ix.timer, "smp_fix", (double)n * 5 + (double)cnt * 16);
-    k_fix_a<<<grid_for(n, 256, 8192), 256, 0, s>>>(ix.view(), sa, ix.bwt.as<uint8_t>(), last, cstar,
-                                                   ix.isa.as<uint32_t>());
+    TimedLaunch t(ix.timer, "smp_fix", (double)n * (1 + sizeof(W)) + (double)cnt * 4 * sizeof(W));
+    k_fix_a<W><<<grid_for(n, 256, 8192), 256, 0, s>>>(ix.view(), sa, ix.bwt.as<uint8_t>(), last, cstar,
+                                                      ix.isa.as<W>());
     HK_HIP(hipGetLastError());
-    k_fix_b<<<grid_for(cnt), 256, 0, s>>>(sa, n, ix.Ccode[cstar], cnt, ix.isa.as<uint32_t>(),
-                                          ix.smp_fix.as<uint32_t>());
+    k_fix_b<W><<<grid_for(cnt), 256, 0, s>>>(sa, n, ix.Ccode[cstar], cnt, ix.isa.as<W>(), ix.smp_fix.as<W>());
     HK_HIP(hipGetLastError());
   }
   ix.smp_inv.ensure(256);
@@ -270,7 +280,21 @@ void build_samples(Index& ix, uint32_t rate) {
   ix.smp_count = ns;
   ix.smp_fixn = cnt;
   ix.smp_cstar = cstar;
+  ix.smp_w64 = sizeof(W) == 8;
   ix.have_samples = true;
+}
+
+}  // namespace
+
+// A replicated sharded index (shard_replicate: the whole u64 SA on every rank) samples like a single-GPU
+// one; a slice-only sharded index has no whole SA to sample.
+void build_samples(Index& ix, uint32_t rate) {
+  if (rate == 0) throw ApiError{-2, "sample rate must be positive"};
+  if (!ix.have_sa || ix.sharded) throw ApiError{-3, "samples: whole suffix array not built (a slice-only sharded index)"};
+  if (!ix.have_bwt || !ix.have_text) throw ApiError{-3, "samples: BWT not built"};
+  if (!ix.have_wt) build_wt(ix);
+  if (ix.sa_pos64) build_samples_t<uint64_t>(ix, rate);
+  else build_samples_t<uint32_t>(ix, rate);
 }
 
 void compact(Index& ix) {
@@ -294,18 +318,27 @@ void sampled_locate_gather(Index& ix, const int64_t* d_lr, const uint64_t* d_occ
   unsigned long long* nbig = ix.small.as<unsigned long long>() + 520;
   HK_HIP(hipMemsetAsync(nbig, 0, 8, s));
   TimedLaunch t(ix.timer, "fm_locate_sampled", 0.0);
-  const SmpView m = smp_view(ix);
-  k_locate_smp_small<<<grid_for(P, 256, 65535), 256, 0, s>>>(ix.view(), m, d_lr, d_occ_offs, P, d_pos,
-                                                             ix.tile_c.as<uint64_t>(), nbig);
-  HK_HIP(hipGetLastError());
-  k_locate_smp_big<<<1024, 256, 0, s>>>(ix.view(), m, d_lr, d_occ_offs, ix.tile_c.as<uint64_t>(), nbig, d_pos);
-  HK_HIP(hipGetLastError());
+  auto run = [&](auto m) {
+    using W = std::remove_const_t<std::remove_pointer_t<decltype(m.ssa)>>;
+    k_locate_smp_small<W><<<grid_for(P, 256, 65535), 256, 0, s>>>(ix.view(), m, d_lr, d_occ_offs, P, d_pos,
+                                                                  ix.tile_c.as<uint64_t>(), nbig);
+    HK_HIP(hipGetLastError());
+    k_locate_smp_big<W><<<1024, 256, 0, s>>>(ix.view(), m, d_lr, d_occ_offs, ix.tile_c.as<uint64_t>(), nbig, d_pos);
+    HK_HIP(hipGetLastError());
+  };
+  if (ix.smp_w64) run(smp_view<uint64_t>(ix));
+  else run(smp_view<uint32_t>(ix));
 }
 
 void sampled_sa_range(Index& ix, uint64_t lo, uint64_t count, uint64_t* d_out) {
   if (!ix.have_samples) throw ApiError{-3, "no suffix array and no samples"};
   if (!count) return;
-  k_sa_range_smp<<<grid_for(count, 256, 65535), 256, 0, ix.stream>>>(ix.view(), smp_view(ix), lo, count, d_out);
+  if (ix.smp_w64)
+    k_sa_range_smp<uint64_t><<<grid_for(count, 256, 65535), 256, 0, ix.stream>>>(ix.view(), smp_view<uint64_t>(ix), lo,
+                                                                                 count, d_out);
+  else
+    k_sa_range_smp<uint32_t><<<grid_for(count, 256, 65535), 256, 0, ix.stream>>>(ix.view(), smp_view<uint32_t>(ix), lo,
+                                                                                 count, d_out);
   HK_HIP(hipGetLastError());
 }
 
@@ -324,8 +357,12 @@ void sampled_extract(Index& ix, uint64_t i, uint64_t j, uint8_t* d_out) {
   if (j <= i) return;
   const uint64_t lanes = (j - 1) / ix.smp_rate - i / ix.smp_rate + 1;
   TimedLaunch t(ix.timer, "extract_sampled", 0.0);
-  k_extract_smp<<<grid_for(lanes, 256, 65535), 256, 0, ix.stream>>>(ix.view(), smp_view(ix), i, j,
-                                                                    ix.smp_inv.as<uint8_t>(), d_out);
+  if (ix.smp_w64)
+    k_extract_smp<uint64_t><<<grid_for(lanes, 256, 65535), 256, 0, ix.stream>>>(ix.view(), smp_view<uint64_t>(ix), i,
+                                                                                j, ix.smp_inv.as<uint8_t>(), d_out);
+  else
+    k_extract_smp<uint32_t><<<grid_for(lanes, 256, 65535), 256, 0, ix.stream>>>(ix.view(), smp_view<uint32_t>(ix), i,
+                                                                                j, ix.smp_inv.as<uint8_t>(), d_out);
   HK_HIP(hipGetLastError());
 }
 

@@ -585,8 +585,9 @@ int radix_sort_pairs(SortWork& w, KernelTimer& tm, uint64_t* k[2], V* v[2], int 
     HK_HIP(hipGetLastError());
   };
   if (src && (!d_hist0 || !vals_iota)) throw ApiError{-1, "radix_sort_pairs: text keys need hist0 and iota values"};
-  // small sorts (refinement rounds): every digit's histogram and offsets from one read of the keys
-  // and one host round trip, then the passes back to back (no per-pass readback)
+  // small sorts (refinement rounds): every digit's histogram and offsets from one read of the keys,
+  // then every pass back to back with no host round trip (no single-digit pass is skipped: a skipped
+  // small pass saves less than the readback that finds it)
   const bool upfront = small && !d_hist0;
   if (upfront) {
     HK_HIP(hipMemsetAsync(hist, 0, (uint64_t)np * 256 * 8, s));
@@ -598,8 +599,6 @@ int radix_sort_pairs(SortWork& w, KernelTimer& tm, uint64_t* k[2], V* v[2], int 
     }
     k_hist_offsets<<<np, 256, 0, s>>>(hist, w.offs.as<uint64_t>());
     HK_HIP(hipGetLastError());
-    HK_HIP(hipMemcpyAsync(w.h_hist, hist, (uint64_t)np * 256 * 8, hipMemcpyDeviceToHost, s));
-    HK_HIP(hipStreamSynchronize(s));
   } else if (d_hist0) {
     HK_HIP(hipMemcpyAsync(hist, d_hist0, 256 * 8, hipMemcpyDeviceToDevice, s));
   } else {
@@ -616,7 +615,7 @@ int radix_sort_pairs(SortWork& w, KernelTimer& tm, uint64_t* k[2], V* v[2], int 
       HK_HIP(hipStreamSynchronize(s));
     }
     bool trivial = false;
-    for (int d = 0; d < 256; ++d)
+    for (int d = 0; d < 256 && !upfront; ++d)
       if (w.h_hist[p * 256 + d] == n) trivial = true;
     const bool from_text = src && p == 0;   // builds the keys: never skipped
     if (from_text) trivial = false;
@@ -689,10 +688,11 @@ int radix_sort_pairs(SortWork& w, KernelTimer& tm, uint64_t* k[2], V* v[2], int 
     w.passes_run++;
   }
   if (iota_pending) fill_iota<V>(v[cur], n, s);
-  uint32_t herr = 0;
-  HK_HIP(hipMemcpyAsync(&herr, w.err.p, 4, hipMemcpyDeviceToHost, s));
+  w.herr.ensure(16);
+  uint32_t* const he = static_cast<uint32_t*>(w.herr.p);
+  HK_HIP(hipMemcpyAsync(he, w.err.p, 4, hipMemcpyDeviceToHost, s));
   HK_HIP(hipStreamSynchronize(s));
-  if (herr) throw ApiError{-7, "radix sort lookback exceeded its spin bound"};
+  if (*he) throw ApiError{-7, "radix sort lookback exceeded its spin bound"};
   return cur;
 }
 

@@ -15,6 +15,7 @@ struct SortWork {
   DevBuf hpart;        // 64 x 256 u64 partial histograms of the next digit, written by a pass
   DevBuf offs;         // 8 x 256 u64 exclusive digit offsets
   DevBuf err;          // u32 error flag (lookback spin bound exceeded)
+  HostBuf herr;        // its pinned landing slot
   DevBuf scan_tmp;     // scan partials (multi-level)
   uint32_t epoch = 0;  // lookback epoch of the last pass (16 bits used)
   uint64_t status_tiles = 0;

@@ -21,6 +21,7 @@
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
+#include <type_traits>
 #include <vector>
 
 #include "hk_index.hpp"
@@ -67,7 +68,14 @@ struct WtSmall {
   uint32_t lut_lo, lut_hi;   // bit of codes 0..3 / 4..7, one byte each
   uint32_t thr[7];           // code-start byte of codes 1..7, replicated to the 4 bytes
   int nthr;                  // sigma - 1 at level 0, 0 below (the input is already codes)
+  int p2sh;                  // sigma = 256 (dense code = byte, a perfect tree): the level's bit is
+                             // (byte >> p2sh) & 1, four symbols per VALU step; -1 otherwise
 };
+
+// bits of four bytes at one bit position, gathered as in small_bits4
+__device__ __forceinline__ uint32_t p2_bits4(uint32_t w, int sh) {
+  return ((((w >> sh) & 0x01010101u) * 0x01020408u) >> 24) & 15u;
+}
 
 __device__ __forceinline__ uint32_t small_codes(uint32_t x, const WtSmall& a) {
   if (!a.nthr) return x;
@@ -114,6 +122,11 @@ __global__ __launch_bounds__(256) void k_wt_bits(const uint8_t* __restrict__ S, 
         const uint32_t w4[4] = {v[it].x, v[it].y, v[it].z, v[it].w};
 #pragma unroll
         for (int k = 0; k < 4; ++k) bits |= small_bits4(small_codes(w4[k], sa), sa) << (4 * k);
+        if (j + 16 > n) bits &= j >= n ? 0u : (1u << (uint32_t)(n - j)) - 1;
+      } else if (sa.p2sh >= 0) {
+        const uint32_t w4[4] = {v[it].x, v[it].y, v[it].z, v[it].w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) bits |= p2_bits4(w4[k], sa.p2sh) << (4 * k);
         if (j + 16 > n) bits &= j >= n ? 0u : (1u << (uint32_t)(n - j)) - 1;
       } else {
 #pragma unroll
@@ -221,6 +234,9 @@ __global__ __launch_bounds__(256) void k_wt_partition(const uint8_t* __restrict_
         cw[k] = small_codes(cw[k], sa);
         bits |= small_bits4(cw[k], sa) << (4 * k);
       }
+    } else if (sa.p2sh >= 0) {   // sigma = 256: codes are the bytes, bits by shifts
+#pragma unroll
+      for (int k = 0; k < 4; ++k) bits |= p2_bits4(cw[k], sa.p2sh) << (4 * k);
     } else if (translate) {   // level 0: BWT bytes -> dense codes
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
@@ -423,22 +439,221 @@ __device__ __forceinline__ uint64_t occ_rank(const uint4* __restrict__ lines, co
   return sb[(uint64_t)c * nsb + (li >> 8)] + cnt + (uint64_t)(__popcll(m0) + __popcll(m1));
 }
 
+// Two-level 16-ary occ directory (8 < sigma <= 256).  With g = max(0, levels - 4), level 0 is the
+// BWT mapped to the WT node of each code at depth g (<= 16 nodes, each of <= 16 codes) and level 1 is
+// the WT's depth-g sequence (the BWT stably partitioned by those nodes) mapped to code - node start
+// (g = 0: the BWT's codes).  With h, v the node and value of code c, B[h] the node's start (= C of its
+// first code) and A[c] = C[c] - (values v in the nodes before h):
+//   LF(c, x) = C[c] + occ(c, x) = A[c] + rank1_v(B[h] + rank0_h(x))
+// so an LF step reads two 64-B lines (one for g = 0) where the WT reads one per level.
+// Line: 64 symbols in 64 B: the 16 values' u16 counts before the line (relative to its superblock of
+// NB_LPS lines) + 4 bit-planes of 64 bits; per superblock 16 u64 counts, [value][superblock].
+constexpr int NB_S = 64, NB_LPS = 1024;
+
+// one workgroup per superblock, 64 lines a round: 4 threads per line, 16 symbols each (one 16-B load)
+__global__ __launch_bounds__(256) void k_nib_lines(const uint8_t* __restrict__ seq, uint64_t n,
+                                                   const uint8_t* __restrict__ map, uint64_t nlines,
+                                                   uint4* __restrict__ lines, uint64_t* __restrict__ sbt) {
+  __shared__ uint8_t MP[256];
+  __shared__ uint4 img[64 * 4];
+  __shared__ uint32_t lc[64][17];
+  const uint32_t tid = threadIdx.x, ln = tid >> 2, j = tid & 3, lane = tid & 63, wv = tid >> 6;
+  MP[tid] = map[tid];
+  uint32_t carry[4] = {0, 0, 0, 0};   // this wave's values 4 wv .. 4 wv + 3 (wave-uniform)
+  __syncthreads();
+  uint16_t* const img16 = reinterpret_cast<uint16_t*>(img);
+  for (int it = 0; it < NB_LPS / 64; ++it) {
+    const uint64_t l0 = (uint64_t)blockIdx.x * NB_LPS + (uint64_t)it * 64;
+    if (l0 >= nlines) break;   // uniform
+    const uint64_t li = l0 + ln, p = li * NB_S + 16 * j;
+    // symbols past n: value 0 (after every queried position; the input holds n + 64 bytes)
+    const uint4 v = li < nlines && p < n ? *reinterpret_cast<const uint4*>(seq + p) : make_uint4(0, 0, 0, 0);
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    uint32_t pq[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const uint32_t x = p + i < n ? MP[(w[i >> 2] >> (8 * (i & 3))) & 255u] : 0u;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) pq[q] |= ((x >> q) & 1u) << i;
+    }
+    // the 16 values' counts in these 16 symbols, a byte each (<= 64 over the line's 4 threads)
+    const uint32_t nq[4] = {~pq[0] & 0xFFFFu, ~pq[1] & 0xFFFFu, ~pq[2] & 0xFFFFu, ~pq[3] & 0xFFFFu};
+    const uint32_t a01[4] = {nq[0] & nq[1], pq[0] & nq[1], nq[0] & pq[1], pq[0] & pq[1]};
+    const uint32_t a23[4] = {nq[2] & nq[3], pq[2] & nq[3], nq[2] & pq[3], pq[2] & pq[3]};
+    uint32_t cb[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int x = 0; x < 16; ++x) cb[x >> 2] |= (uint32_t)__popc(a01[x & 3] & a23[x >> 2]) << (8 * (x & 3));
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      cb[k] += __shfl_xor(cb[k], 1, 64);
+      cb[k] += __shfl_xor(cb[k], 2, 64);
+    }
+    // thread j records values 4j .. 4j + 3 of its line
+#pragma unroll
+    for (int k = 0; k < 4; ++k) lc[ln][4 * j + k] = (cb[j] >> (8 * k)) & 255u;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) img16[ln * 32 + 16 + 4 * q + j] = (uint16_t)pq[q];
+    __syncthreads();
+    // wave wv, lane = line: the counts of values 4 wv + k before each line of the superblock
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t val = 4 * wv + k, x = lc[lane][val];
+      const uint32_t inc = wave_incl_sum<uint32_t>(x);
+      img16[lane * 32 + val] = (uint16_t)(carry[k] + inc - x);
+      carry[k] += __shfl(inc, 63, 64);
+    }
+    __syncthreads();
+    if (l0 + (tid >> 2) < nlines) lines[l0 * 4 + tid] = img[tid];
+    __syncthreads();
+  }
+  if (lane < 4) sbt[(uint64_t)(4 * wv + lane) * gridDim.x + blockIdx.x] = lane == 0 ? carry[0] : lane == 1 ? carry[1]
+                                                                          : lane == 2 ? carry[2] : carry[3];
+}
+
+// per value, the exclusive prefix of its superblock totals (in place; one workgroup per value)
+__global__ __launch_bounds__(1024) void k_nib_sbscan(uint64_t* __restrict__ sbt, uint64_t nsb) {
+  __shared__ uint64_t ws[16];
+  uint64_t* const row = sbt + (uint64_t)blockIdx.x * nsb;
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  uint64_t carry = 0;
+  for (uint64_t b = 0; b < nsb; b += 1024) {
+    const uint64_t i = b + tid;
+    const uint64_t x = i < nsb ? row[i] : 0;
+    const uint64_t inc = wave_incl_sum<uint64_t>(x);
+    if (lane == 63) ws[wv] = inc;
+    __syncthreads();
+    uint64_t pre = 0, tot = 0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      pre += k < (int)wv ? ws[k] : 0;
+      tot += ws[k];
+    }
+    if (i < nsb) row[i] = carry + pre + inc - x;
+    carry += tot;
+    __syncthreads();
+  }
+}
+
+__device__ __forceinline__ uint64_t nib_rank(const uint4* __restrict__ lines, const uint64_t* __restrict__ sb,
+                                             uint64_t nsb, uint32_t v, uint64_t x) {
+  const uint64_t li = x >> 6;
+  const uint32_t off = (uint32_t)x & 63u;
+  const uint4* L = lines + li * 4;
+  const uint4 h = L[v >> 3], a = L[2], b = L[3];
+  const uint32_t hw = (v & 4) ? ((v & 2) ? h.w : h.z) : ((v & 2) ? h.y : h.x);
+  const uint32_t cnt = (hw >> (16 * (v & 1))) & 0xFFFFu;
+  const uint64_t p0 = ((uint64_t)a.y << 32) | a.x, p1 = ((uint64_t)a.w << 32) | a.z;
+  const uint64_t p2 = ((uint64_t)b.y << 32) | b.x, p3 = ((uint64_t)b.w << 32) | b.z;
+  uint64_t m = ((v & 1) ? p0 : ~p0) & ((v & 2) ? p1 : ~p1) & ((v & 4) ? p2 : ~p2) & ((v & 8) ? p3 : ~p3);
+  m &= (1ull << off) - 1ull;
+  return sb[(uint64_t)v * nsb + (li >> 10)] + cnt + (uint64_t)__popcll(m);
+}
+
+// ranks of one value at two positions: a second line (and superblock count) only for lanes whose
+// positions fall in different lines (a narrow range, as most backward-search steps past the first
+// few symbols, reads one line)
+__device__ __forceinline__ void nib_rank2(const uint4* __restrict__ lines, const uint64_t* __restrict__ sb,
+                                          uint64_t nsb, uint32_t v, uint64_t xl, uint64_t xr, uint64_t& rl,
+                                          uint64_t& rr) {
+  const uint64_t ll = xl >> 6, lr = xr >> 6;
+  const uint4* L = lines + ll * 4;
+  uint4 h = L[v >> 3], a = L[2], b = L[3];
+  uint64_t s0 = sb[(uint64_t)v * nsb + (ll >> 10)], s1 = s0;
+  auto one = [&](const uint4& hh, const uint4& aa, const uint4& bb, uint64_t sbv, uint32_t off) -> uint64_t {
+    const uint32_t hw = (v & 4) ? ((v & 2) ? hh.w : hh.z) : ((v & 2) ? hh.y : hh.x);
+    const uint32_t cnt = (hw >> (16 * (v & 1))) & 0xFFFFu;
+    const uint64_t p0 = ((uint64_t)aa.y << 32) | aa.x, p1 = ((uint64_t)aa.w << 32) | aa.z;
+    const uint64_t p2 = ((uint64_t)bb.y << 32) | bb.x, p3 = ((uint64_t)bb.w << 32) | bb.z;
+    uint64_t m = ((v & 1) ? p0 : ~p0) & ((v & 2) ? p1 : ~p1) & ((v & 4) ? p2 : ~p2) & ((v & 8) ? p3 : ~p3);
+    m &= (1ull << off) - 1ull;
+    return sbv + cnt + (uint64_t)__popcll(m);
+  };
+  rl = one(h, a, b, s0, (uint32_t)xl & 63u);
+  if (lr != ll) {
+    const uint4* R = lines + lr * 4;
+    h = R[v >> 3];
+    a = R[2];
+    b = R[3];
+    s1 = sb[(uint64_t)v * nsb + (lr >> 10)];
+  }
+  rr = one(h, a, b, s1, (uint32_t)xr & 63u);
+}
+
+struct NibView {
+  const uint4* l0 = nullptr;
+  const uint64_t* sb0 = nullptr;
+  const uint4* l1 = nullptr;
+  const uint64_t* sb1 = nullptr;
+  uint64_t nsb = 0;
+  const uint8_t* tab = nullptr;   // grp[256] | val[256] | map0[256] | map1[256] | A u64[256] | B u64[16]
+  int g = 0;
+};
+
+struct NibShared {
+  uint64_t A[256];
+  uint64_t B[16];
+  uint8_t grp[256], val[256];
+};
+
+__device__ __forceinline__ void load_nib(NibShared& s, const NibView& v) {
+  const uint32_t t = threadIdx.x;   // blockDim == 256
+  s.grp[t] = v.tab[t];
+  s.val[t] = v.tab[256 + t];
+  s.A[t] = reinterpret_cast<const uint64_t*>(v.tab + 1024)[t];
+  if (t < 16) s.B[t] = reinterpret_cast<const uint64_t*>(v.tab + 3072)[t];
+}
+
+// LF of the pair (xl, xr) for code c
+__device__ __forceinline__ void nib_lf_pair(const NibView& v, const NibShared& s, int c, uint64_t& xl, uint64_t& xr) {
+  uint64_t yl = xl, yr = xr;
+  if (v.g) {
+    const uint32_t h = s.grp[c];
+    nib_rank2(v.l0, v.sb0, v.nsb, h, xl, xr, yl, yr);
+    yl += s.B[h];
+    yr += s.B[h];
+  }
+  uint64_t rl, rr;
+  nib_rank2(v.l1, v.sb1, v.nsb, s.val[c], yl, yr, rl, rr);
+  xl = s.A[c] + rl;
+  xr = s.A[c] + rr;
+}
+
+__device__ __forceinline__ uint64_t nib_lf(const NibView& v, const NibShared& s, int c, uint64_t x) {
+  uint64_t y = x;
+  if (v.g) {
+    const uint32_t h = s.grp[c];
+    y = s.B[h] + nib_rank(v.l0, v.sb0, v.nsb, h, x);
+  }
+  return s.A[c] + nib_rank(v.l1, v.sb1, v.nsb, s.val[c], y);
+}
+
 // Batched backward search, one lane per pattern (csa/enhanced_fm_index.py:21-32): the state (xl, xr)
 // is the half-open row range, a symbol outside the alphabet or an empty range ends the search.  With
 // a k-mer table (K > 0) the last K symbols of a pattern take one lookup of the state they lead to
 // from the full range (k_kmer_table: the same LF steps, so identical results) instead of K steps.
-// FLAT (sigma <= 8): the LF steps read the flat occ directory (one line per rank) instead of the WT.
-template <int NC, bool FLAT = false>
+// MODE 1 (FLAT, sigma <= 8): the LF steps read the flat occ directory (one line per rank) instead of
+// the WT; MODE 2 (NIB, 8 < sigma): the two-level 16-ary directory (two lines per rank).
+template <int NC, int MODE = 0>
 __global__ __launch_bounds__(256) void k_count(WtView v, const uint8_t* __restrict__ pats,
                                                const uint64_t* __restrict__ offs, uint64_t P,
                                                int64_t* __restrict__ lr, uint64_t* __restrict__ cnt,
                                                const ulonglong2* __restrict__ kmer, int K,
                                                const uint4* __restrict__ ol = nullptr,
-                                               const uint64_t* __restrict__ osb = nullptr, uint64_t onsb = 0) {
-  __shared__ QSharedT<NC> q;
+                                               const uint64_t* __restrict__ osb = nullptr, uint64_t onsb = 0,
+                                               NibView nv = NibView{}) {
+  constexpr bool FLAT = MODE == 1, NIB = MODE == 2;
+  __shared__ QSharedT<NIB ? 1 : NC> q;
+  __shared__ typename std::conditional<NIB, NibShared, uint8_t>::type nsx;
+  NibShared* const ns = reinterpret_cast<NibShared*>(&nsx);
   __shared__ uint64_t CC[8];
   if (FLAT && threadIdx.x < 8) CC[threadIdx.x] = threadIdx.x < (unsigned)v.sigma ? v.Ccode[threadIdx.x] : 0;
-  load_qshared(q, v);
+  if constexpr (NIB) {
+    q.code[threadIdx.x] = v.code[threadIdx.x];
+    load_nib(ns[0], nv);
+    __syncthreads();
+  } else {
+    load_qshared(q, v);
+  }
   for (uint64_t p = (uint64_t)blockIdx.x * 256 + threadIdx.x; p < P; p += (uint64_t)gridDim.x * 256) {
     const uint64_t s = offs[p];
     uint64_t k = offs[p + 1];
@@ -463,9 +678,11 @@ __global__ __launch_bounds__(256) void k_count(WtView v, const uint8_t* __restri
       --k;
       const int c = q.code[pats[k]];
       if (c < 0) { ok = false; break; }
-      if (FLAT) {
+      if constexpr (FLAT) {
         xl = CC[c] + occ_rank(ol, osb, onsb, c, xl);
         xr = CC[c] + occ_rank(ol, osb, onsb, c, xr);
+      } else if constexpr (NIB) {
+        nib_lf_pair(nv, ns[0], c, xl, xr);
       } else {
         lf_pair(q, c, xl, xr);
       }
@@ -480,23 +697,34 @@ __global__ __launch_bounds__(256) void k_count(WtView v, const uint8_t* __restri
 // k-mer table: entry idx (the codes c_0 .. c_{K-1} of a K-symbol string, c_0 most significant in
 // radix sigma) = the state after the backward search of that string from the full range; an empty
 // state is stored as (1, 0)
-template <int NC, bool FLAT = false>
+template <int NC, int MODE = 0>
 __global__ __launch_bounds__(256) void k_kmer_table(WtView v, int K, uint64_t total, ulonglong2* __restrict__ tab,
                                                     const uint4* __restrict__ ol = nullptr,
-                                                    const uint64_t* __restrict__ osb = nullptr, uint64_t onsb = 0) {
-  __shared__ QSharedT<NC> q;
+                                                    const uint64_t* __restrict__ osb = nullptr, uint64_t onsb = 0,
+                                                    NibView nv = NibView{}) {
+  constexpr bool FLAT = MODE == 1, NIB = MODE == 2;
+  __shared__ QSharedT<NIB ? 1 : NC> q;
+  __shared__ typename std::conditional<NIB, NibShared, uint8_t>::type nsx;
+  NibShared* const ns = reinterpret_cast<NibShared*>(&nsx);
   __shared__ uint64_t CC[8];
   if (FLAT && threadIdx.x < 8) CC[threadIdx.x] = threadIdx.x < (unsigned)v.sigma ? v.Ccode[threadIdx.x] : 0;
-  load_qshared(q, v);
+  if constexpr (NIB) {
+    load_nib(ns[0], nv);
+    __syncthreads();
+  } else {
+    load_qshared(q, v);
+  }
   for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (uint64_t)gridDim.x * 256) {
     uint64_t xl = 0, xr = v.n, x = i;
     bool ok = true;
     for (int j = 0; j < K; ++j) {   // the last symbol (least significant digit) first
       const int c = (int)(x % (uint64_t)v.sigma);
       x /= (uint64_t)v.sigma;
-      if (FLAT) {
+      if constexpr (FLAT) {
         xl = CC[c] + occ_rank(ol, osb, onsb, c, xl);
         xr = CC[c] + occ_rank(ol, osb, onsb, c, xr);
+      } else if constexpr (NIB) {
+        nib_lf_pair(nv, ns[0], c, xl, xr);
       } else {
         lf_pair(q, c, xl, xr);
       }
@@ -506,17 +734,31 @@ __global__ __launch_bounds__(256) void k_kmer_table(WtView v, int K, uint64_t to
   }
 }
 
+// occ(c, i) = LF(c, i) - C[c]: the WT walk, or NIB the two-level directory (two lines)
+template <bool NIB = false>
 __global__ __launch_bounds__(256) void k_rank(WtView v, const uint8_t* __restrict__ cs,
                                               const uint64_t* __restrict__ is, uint64_t K,
-                                              uint64_t* __restrict__ out) {
-  __shared__ QShared q;
-  load_qshared(q, v);
+                                              uint64_t* __restrict__ out, NibView nv = NibView{}) {
+  __shared__ QSharedT<NIB ? 1 : 256> q;
+  __shared__ typename std::conditional<NIB, NibShared, uint8_t>::type nsx;
+  NibShared* const ns = reinterpret_cast<NibShared*>(&nsx);
+  if constexpr (NIB) {
+    q.code[threadIdx.x] = v.code[threadIdx.x];
+    load_nib(ns[0], nv);
+    __syncthreads();
+  } else {
+    load_qshared(q, v);
+  }
   for (uint64_t k = (uint64_t)blockIdx.x * 256 + threadIdx.x; k < K; k += (uint64_t)gridDim.x * 256) {
     const int c = q.code[cs[k]];
     if (c < 0) { out[k] = 0; continue; }
     uint64_t x = is[k] < v.n ? is[k] : v.n;
-    uint64_t y = x;
-    lf_pair(q, c, x, y);
+    if constexpr (NIB) {
+      x = nib_lf(nv, ns[0], c, x);
+    } else {
+      uint64_t y = x;
+      lf_pair(q, c, x, y);
+    }
     out[k] = x - v.Ccode[c];
   }
 }
@@ -564,6 +806,20 @@ inline unsigned grid_for(uint64_t n, unsigned per = 256, unsigned cap = 16384) {
   return (unsigned)(g < cap ? g : cap);
 }
 
+}  // namespace
+
+namespace {
+NibView nib_view(const Index& ix) {
+  NibView nv;
+  nv.l0 = ix.nib_lines[0].as<uint4>();
+  nv.sb0 = ix.nib_sb[0].as<uint64_t>();
+  nv.l1 = ix.nib_lines[1].as<uint4>();
+  nv.sb1 = ix.nib_sb[1].as<uint64_t>();
+  nv.nsb = ix.nib_nsb;
+  nv.tab = ix.nib_tab.as<uint8_t>();
+  nv.g = ix.nib_g;
+  return nv;
+}
 }  // namespace
 
 void build_wt(Index& ix) {
@@ -618,6 +874,62 @@ void build_wt(Index& ix) {
                         hipMemcpyHostToDevice, s));
 
   const uint64_t nlines = n / kLineBits + 1;
+  // two-level 16-ary occ directory for the batched count (8 < sigma; HKCSA_NIB=0: WT walks, for A/B):
+  // node groups at depth g, their tables, and level 0 from the BWT (level 1 follows the WT partition
+  // that writes the depth-g sequence, or the BWT itself for g = 0)
+  static const bool nib_env = !getenv("HKCSA_NIB") || atoi(getenv("HKCSA_NIB")) != 0;
+  const bool nib = nib_env && sigma > 8;
+  const int ng = nib ? std::max(0, L - 4) : 0;
+  std::vector<uint8_t> nibh(3072 + 128, 0);   // host source of the table upload (alive to the sync)
+  const uint64_t nbl = n / NB_S + 1, nbsb = ceil_div(nbl, (uint64_t)NB_LPS);
+  ix.nib_ok = false;
+  auto nib_level = [&](int lv, const uint8_t* in, const uint8_t* d_map) {
+    ix.nib_lines[lv].ensure(nbl * 64 + 64);
+    ix.nib_sb[lv].ensure(nbsb * 16 * 8 + 64);
+    TimedLaunch t(ix.timer, "fm_nib_lines", (double)n * 2);
+    k_nib_lines<<<(unsigned)nbsb, 256, 0, s>>>(in, n, d_map, nbl, ix.nib_lines[lv].as<uint4>(),
+                                               ix.nib_sb[lv].as<uint64_t>());
+    HK_HIP(hipGetLastError());
+    k_nib_sbscan<<<16, 1024, 0, s>>>(ix.nib_sb[lv].as<uint64_t>(), nbsb);
+    HK_HIP(hipGetLastError());
+  };
+  if (nib) {
+    uint8_t* grp = nibh.data();
+    uint8_t* val = grp + 256;
+    uint8_t* map0 = grp + 512;
+    uint8_t* map1 = grp + 768;
+    uint64_t* A = reinterpret_cast<uint64_t*>(grp + 1024);
+    uint64_t* B = reinterpret_cast<uint64_t*>(grp + 3072);
+    int lo[17] = {0}, nh = 0;
+    for (int c = 0; c < sigma; ++c) {
+      if (c == 0 || (ng > 0 && T.start[ng][c] != T.start[ng][c - 1])) lo[nh++] = c;
+      grp[c] = (uint8_t)(nh - 1);
+      val[c] = (uint8_t)(c - lo[nh - 1]);
+    }
+    lo[nh] = sigma;
+    if (nh > 16) throw ApiError{-6, "build_wt: more than 16 nodes at the directory depth"};
+    for (int h = 0; h < nh; ++h) {
+      if (lo[h + 1] - lo[h] > 16) throw ApiError{-6, "build_wt: a directory node of more than 16 codes"};
+      B[h] = ix.Ccode[lo[h]];
+    }
+    for (int c = 0; c < sigma; ++c) {
+      uint64_t below = 0;   // value val[c] in the nodes before c's
+      for (int h = 0; h < grp[c]; ++h)
+        if (lo[h] + val[c] < lo[h + 1]) below += ix.Ccode[lo[h] + val[c] + 1] - ix.Ccode[lo[h] + val[c]];
+      A[c] = ix.Ccode[c] - below;
+    }
+    for (int x = 0; x < 256; ++x) {
+      const int c = ix.code_of[x];
+      map0[x] = c >= 0 ? grp[c] : 0;
+      map1[x] = ng == 0 ? (c >= 0 ? (uint8_t)c : 0) : (x < sigma ? val[x] : 0);
+    }
+    ix.nib_tab.ensure(nibh.size());
+    HK_HIP(hipMemcpyAsync(ix.nib_tab.p, nibh.data(), nibh.size(), hipMemcpyHostToDevice, s));
+    ix.nib_g = ng;
+    ix.nib_nsb = nbsb;
+    if (ng > 0) nib_level(0, ix.bwt.as<uint8_t>(), ix.nib_tab.as<uint8_t>() + 512);
+    else nib_level(1, ix.bwt.as<uint8_t>(), ix.nib_tab.as<uint8_t>() + 768);
+  }
   // host sources of asynchronous copies: alive until the synchronize at the end of the build
   std::vector<uint16_t> lutv((size_t)kMaxLevels * 256, 0);
   uint16_t (*lut)[256] = reinterpret_cast<uint16_t (*)[256]>(lutv.data());
@@ -653,6 +965,9 @@ void build_wt(Index& ix) {
       }
     WtSmall sml[kMaxLevels];
     memset(sml, 0, sizeof(sml));
+    // sigma = 256: every byte present, dense code = byte, the tree perfect (HKCSA_WT_P2=0: the tables)
+    static const bool p2_env = !getenv("HKCSA_WT_P2") || atoi(getenv("HKCSA_WT_P2")) != 0;
+    for (int d = 0; d < L; ++d) sml[d].p2sh = p2_env && sigma == 256 && L == 8 ? 7 - d : -1;
     for (int d = 0; d < L && small; ++d) {
       for (int c = 0; c < sigma; ++c) {
         const uint32_t bit = T.bit[d][c];
@@ -718,6 +1033,7 @@ void build_wt(Index& ix) {
                                                    ix.wt_lut.as<uint16_t>() + d * 256,
                                                    ix.tile_d.as<uint64_t>() + d * 256, nbsp[d], d == 0 ? 1 : 0, sml[d]);
         HK_HIP(hipGetLastError());
+        if (nib && ng > 0 && d + 1 == ng) nib_level(1, outp, ix.nib_tab.as<uint8_t>() + 768);
         if (d > 0) cur ^= 1;
       }
     }
@@ -739,6 +1055,7 @@ void build_wt(Index& ix) {
     ix.occ_nsb = nsb;
     ix.occ_ok = true;
   }
+  ix.nib_ok = nib;
   // k-mer table for the batched count: K = the most symbols with sigma^K <= 2^20 entries (<= 16 MiB
   // of (l, r) pairs, MALL-resident; DNA + '$': K = 8, printable: 3, bytes: 2), at most 12
   // (HKCSA_KMER=0: no table, for A/B)
@@ -747,7 +1064,7 @@ void build_wt(Index& ix) {
   if (kmer_env && L > 0 && sigma >= 2) {
     int K = 0;
     uint64_t tot = 1;
-    const uint64_t cap = ix.occ_ok ? (1ull << 21) : (1ull << 20);   // the directory builds it cheaply
+    const uint64_t cap = ix.occ_ok || ix.nib_ok ? (1ull << 21) : (1ull << 20);   // a directory builds it cheaply
     while (K < 12 && tot * (uint64_t)sigma <= cap) {
       tot *= (uint64_t)sigma;
       ++K;
@@ -756,9 +1073,12 @@ void build_wt(Index& ix) {
       ix.kmer.ensure(tot * 16 + 16);
       TimedLaunch t(ix.timer, "fm_kmer_table", (double)tot * 16);
       if (ix.occ_ok)
-        k_kmer_table<16, true><<<grid_for(tot, 256, 8192), 256, 0, s>>>(ix.view(), K, tot, ix.kmer.as<ulonglong2>(),
-                                                                       ix.occ_lines.as<uint4>(),
-                                                                       ix.occ_sb.as<uint64_t>(), ix.occ_nsb);
+        k_kmer_table<16, 1><<<grid_for(tot, 256, 8192), 256, 0, s>>>(ix.view(), K, tot, ix.kmer.as<ulonglong2>(),
+                                                                    ix.occ_lines.as<uint4>(),
+                                                                    ix.occ_sb.as<uint64_t>(), ix.occ_nsb);
+      else if (ix.nib_ok)
+        k_kmer_table<16, 2><<<grid_for(tot, 256, 8192), 256, 0, s>>>(ix.view(), K, tot, ix.kmer.as<ulonglong2>(),
+                                                                    nullptr, nullptr, 0, nib_view(ix));
       else if (sigma <= 16)
         k_kmer_table<16><<<grid_for(tot, 256, 8192), 256, 0, s>>>(ix.view(), K, tot, ix.kmer.as<ulonglong2>());
       else
@@ -778,9 +1098,12 @@ void query_count(Index& ix, const uint8_t* d_pats, const uint64_t* d_offs, uint6
   TimedLaunch t(ix.timer, "fm_count", 0.0);
   const ulonglong2* km = ix.kmer_k ? ix.kmer.as<ulonglong2>() : nullptr;
   if (ix.occ_ok)
-    k_count<16, true><<<grid_for(P, 256, 65535), 256, 0, ix.stream>>>(ix.view(), d_pats, d_offs, P, d_lr, d_cnt, km,
-                                                                       ix.kmer_k, ix.occ_lines.as<uint4>(),
-                                                                       ix.occ_sb.as<uint64_t>(), ix.occ_nsb);
+    k_count<16, 1><<<grid_for(P, 256, 65535), 256, 0, ix.stream>>>(ix.view(), d_pats, d_offs, P, d_lr, d_cnt, km,
+                                                                    ix.kmer_k, ix.occ_lines.as<uint4>(),
+                                                                    ix.occ_sb.as<uint64_t>(), ix.occ_nsb);
+  else if (ix.nib_ok)
+    k_count<16, 2><<<grid_for(P, 256, 65535), 256, 0, ix.stream>>>(ix.view(), d_pats, d_offs, P, d_lr, d_cnt, km,
+                                                                    ix.kmer_k, nullptr, nullptr, 0, nib_view(ix));
   else if (ix.sigma <= 16)
     k_count<16><<<grid_for(P, 256, 65535), 256, 0, ix.stream>>>(ix.view(), d_pats, d_offs, P, d_lr, d_cnt, km,
                                                                  ix.kmer_k);
@@ -820,7 +1143,10 @@ void query_locate_gather(Index& ix, const int64_t* d_lr, const uint64_t* d_occ_o
 void query_rank(Index& ix, const uint8_t* d_c, const uint64_t* d_i, uint64_t k, uint64_t* d_out) {
   if (!ix.have_wt) throw ApiError{-3, "rank: wavelet tree not built"};
   if (!k) return;
-  k_rank<<<grid_for(k, 256, 65535), 256, 0, ix.stream>>>(ix.view(), d_c, d_i, k, d_out);
+  if (ix.nib_ok)
+    k_rank<true><<<grid_for(k, 256, 65535), 256, 0, ix.stream>>>(ix.view(), d_c, d_i, k, d_out, nib_view(ix));
+  else
+    k_rank<><<<grid_for(k, 256, 65535), 256, 0, ix.stream>>>(ix.view(), d_c, d_i, k, d_out);
   HK_HIP(hipGetLastError());
 }
 

@@ -205,7 +205,7 @@ int hkcsa_space(hkcsa_index* h, uint64_t out[8]) {
     out[2] = (ix.have_bwt && !ix.bwt_in_wt) ? ix.n : 0;
     out[3] = ix.have_wt ? (uint64_t)ix.wt_levels * nl * 64 : 0;
     out[4] = ix.have_samples ? nl * 64 : 0;
-    out[5] = ix.have_samples ? ix.smp_count * 8 + ix.smp_fixn * 4 : 0;
+    out[5] = ix.have_samples ? (ix.smp_count * 2 + ix.smp_fixn) * (ix.smp_w64 ? 8 : 4) : 0;
     out[6] = ix.smp_rate;
     out[7] = ix.have_samples ? 1 : 0;
   });

@@ -86,6 +86,10 @@ def _texts():
     yield "bytes_1M", oracle.synth_text((1 << 20) + 1, bytes(range(256)), seed=8)
     yield "binary_256K", oracle.synth_text((1 << 18) + 1, b"ab", seed=9)
     yield "printable_1M", oracle.synth_text((1 << 20) + 1, bytes(range(0x20, 0x7F)), seed=10)
+    # the count directory's one-level (9 <= sigma <= 16) and two-level (sigma = 17: one node a side at
+    # depth 1) shapes
+    yield "sigma12_300K", oracle.synth_text(300001, b"ABCDEFGHIJK", seed=11)
+    yield "sigma17_300K", oracle.synth_text(300001, b"ABCDEFGHIJKLMNOP", seed=12)
     base = rng.integers(0, 4, size=5000).astype(np.uint8) + ord("A")
     rep = np.tile(base, 40)                                   # long repeats: many doubling rounds
     rep[rng.integers(0, len(rep), size=50)] = ord("T")
@@ -546,6 +550,35 @@ def test_shard_replicate_queries(hk, name, flags):
     assert np.array_equal(dev.sa(), sa)
     assert np.array_equal(dev.bwt(), oracle.bwt(text, sa))
     _check_queries(dev, text, sa, seed=len(text))
+    dev.close()
+
+
+@pytest.mark.parametrize("name,rate", [("dna_300K", 6), ("repeats_200K", 3)])
+def test_sampled_replicated_u64(hk, name, rate):
+    """The epsilon contract over a replicated index whose SA is u64 (flags=1, as every rank's replica
+    of a text with >= 2^32 suffixes): 8-byte samples, then SA, BWT, text, extract, count and locate by
+    LF walks equal the full arrays and the oracle."""
+    text = oracle.synth_text(300001, b"ACGT", seed=18) if name == "dna_300K" else _repetitive(name)
+    dev = hk.DeviceIndex.from_bytes(text, device=0, flags=1)
+    dev.build_sa_sharded(hk.comm_unique_id(), 1, 0)
+    dev.shard_replicate()
+    dev.build_wt()
+    sa = oracle.suffix_array(text)
+    dev.build_samples(rate)
+    dev.compact()
+    sp = dev.space()
+    assert sp["sa"] == 0 and sp["text"] == 0 and sp["sampled"] == 1 and sp["sample_rate"] == rate
+    n = len(text)
+    assert sp["samples"] == (2 * ((n + rate - 1) // rate) + int(np.count_nonzero(text == text[-1]))) * 8
+    assert np.array_equal(dev.sa(), sa)
+    assert np.array_equal(dev.bwt(), oracle.bwt(text, sa))
+    assert np.array_equal(dev.text(), text)
+    rng = np.random.default_rng(rate)
+    for _ in range(20):
+        i = int(rng.integers(0, n))
+        j = int(rng.integers(i, min(n, i + 5000) + 1))
+        assert dev.extract(i, j) == text[i:j].tobytes()
+    _check_queries(dev, text, sa, seed=n)
     dev.close()
 
 

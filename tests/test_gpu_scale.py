@@ -57,13 +57,56 @@ def test_strong_config4_4GiB_virtual_slices(hk):
         assert dev.build_info()[7] & 4, dev.build_info()[:10]   # keyed coarse scheme
 
     bench.virtual_slices(dev, k, on_slice=grab)
-    dev.close()
     assert seen[0][0] == 0 and seen[-1][1] == n
     assert all(a[1] == b[0] for a, b in zip(seen, seen[1:]))
     assert all(abs((hi - lo) - n / k) < n / k / 50 for lo, hi in seen)   # balanced slices
     text = oracle.synth_text(n, b"ACGT", seed=2)
     assert oracle.check_sa(text, sa) == 0
     assert np.array_equal(bwt, oracle.bwt(text, sa))
+    dev.close()
+
+
+def test_replicated_4GiB_epsilon_sampled_locate(hk):
+    """The replicated 4 GiB + 1 index under the epsilon contract: the strong N = 1
+    slices adopted as the replica every rank holds (u64 SA), the WT, locate with the full SA; then
+    8-byte samples at CompressedSuffixArray's rate for epsilon = 0.5 (csa/csa.py sample_rate), compact
+    (SA, BWT and text released) and the same locate by LF walks, SA rows and an extract across 2^32:
+    identical answers.  (test_strong_config4_4GiB_virtual_slices checks these slices against the
+    oracle.)"""
+    from csa.csa import sample_rate
+    bench = _bench()
+    n = (1 << 32) + 1
+    dev = hk.DeviceIndex.synthetic(n, b"ACGT", seed=2)
+    sa = np.empty(n, dtype=np.uint64)
+    bwt = np.empty(n, dtype=np.uint8)
+
+    def grab(r):
+        lo, hi = dev.shard_range()
+        dev.shard_sa(out=sa[lo:hi])
+        dev.shard_bwt(out=bwt[lo:hi])
+
+    bench.virtual_slices(dev, bench.slices_per_gpu(n, 1), on_slice=grab)
+    dev.shard_adopt(sa, bwt)
+    del bwt
+    dev.build_wt()
+    rng = np.random.default_rng(4)
+    win = dev.text((1 << 32) - (1 << 20), (1 << 32))
+    starts = rng.integers(0, len(win) - 13, size=400)
+    pats = [win[s:s + 12].tobytes() for s in starts] + [b"ACGTACGTACGTACGTACGT", b"$", b""]
+    offs_full, pos_full = dev.locate(pats)
+    tail = dev.text((1 << 32) - 100, (1 << 32) + 1)
+    rows = rng.integers(0, n, size=64)
+    rate = sample_rate(n, 0.5)
+    dev.build_samples(rate)
+    dev.compact()
+    sp = dev.space()
+    assert sp["sa"] == 0 and sp["text"] == 0 and sp["sample_rate"] == rate
+    offs, pos = dev.locate(pats)
+    assert np.array_equal(offs, offs_full) and np.array_equal(pos, pos_full)
+    for r in rows:
+        assert int(dev.sa(int(r), int(r) + 1)[0]) == int(sa[r])
+    assert dev.extract((1 << 32) - 100, (1 << 32) + 1) == tail.tobytes()
+    dev.close()
 
 
 def test_weak_rank_geometry_2GiB_two_ranks(hk):

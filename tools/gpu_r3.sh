@@ -5,6 +5,10 @@
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
 export TMPDIR=/tmp
+# heartbeat: long host-side checks inside one test print nothing until the test ends
+( while sleep 60; do date >> gpurun_out/r3_heartbeat.log; done ) &
+HB=$!
+trap 'kill $HB 2>/dev/null' EXIT
 if [ -n "${TESTS}" ]; then
   timeout -k 10 ${TT:-600} python -u -m pytest ${TESTS} -m gpu -x -v --timeout ${PT:-150} --timeout-method thread \
     ${KEXPR:+-k "$KEXPR"} > gpurun_out/r3_tests.log 2>&1
