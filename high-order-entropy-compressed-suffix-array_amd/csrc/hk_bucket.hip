@@ -1344,9 +1344,10 @@ constexpr int BS_WSPAN = BS_I * 64;
 constexpr int BS_V = BS_W;            // per-wave digit histograms, in element order
 
 template <int T>
-struct BsSharedT {
-  uint32_t buf[T * BS_I];        // u32 plane: local key exchange; positions at the end
-  uint16_t aux[T * BS_I];        // u16 plane: original-slot exchange (prev codes packed in the key),
+struct alignas(16) BsSharedT {
+  // (+4: the fast path stages its output at final index + the SA pointer's misalignment, section 7)
+  uint32_t buf[T * BS_I + 4];    // u32 plane: local key exchange; positions at the end
+  uint16_t aux[T * BS_I + 4];    // u16 plane: original-slot exchange (prev codes packed in the key),
                                  // or the prev codes by original slot (when they do not fit the key)
   uint64_t mt[T / 64][256];      // per-wave match masks (lanes holding a digit), zero between items;
                                  // mt[0..1] double as the scan's per-group prefixes
@@ -1398,25 +1399,41 @@ __device__ __forceinline__ void bs_load_keys(const uint64_t* __restrict__ keys, 
 // Workgroups of T = 1024 (18 432-suffix items, 14-bit bins, one per CU) or 512 threads (9216-suffix
 // items of 2^17 buckets, 13-bit bins, ~80 KiB of LDS: two per CU, so one item's key loads overlap
 // the other's LDS phases).  Bins hold ~1.1 suffixes either way.
-template <int T> constexpr int bf_bits() { return T == 1024 ? 14 : 13; }
 constexpr uint32_t BF_MAXBIN = 32;
+
+// LDS of the fast path: T threads, I suffixes per thread (capacity T * I)
+template <int T, int I>
+struct alignas(16) BfShared {
+  static constexpr int CAP = T * I;
+  static constexpr int BITS = CAP <= 9216 ? 13 : 14;   // ~1.1 suffixes per bin
+  static constexpr int BINS = 1 << BITS;
+  uint32_t buf[CAP + 4];       // positions by slot, records by bin, positions by final index (+4: section 7)
+  uint16_t aux[CAP + 4];       // final index by slot, then prev codes by final index
+  uint32_t H2[BINS / 2];       // u16 bin counters / starts, two per word, zero on entry
+  uint16_t lists[BINS / 2];    // listed bins (first half), tied records (second half)
+  uint32_t wloc[2 * (T / 64)];
+  uint32_t wsum[4];
+  uint64_t red[4 * (T / 64)];
+  uint8_t inv[256];
+};
 
 // PK: xs holds the packed records (sym = record >> xsh, position = the low pbits bits) and the
 // positions come from them instead of a value plane.
-template <typename V, bool TRACE, int T, bool PK = false, bool X32 = false>
-__device__ __forceinline__ bool bucket_sort_fast(BsSharedT<T>& sh, uint2 it, const uint64_t (&xs)[BS_I],
-                                                 const uint32_t (&pvr)[BS_H], uint32_t vmask, uint32_t s0,
+template <typename V, bool TRACE, int T, int I, bool PK = false, bool X32 = false>
+__device__ __forceinline__ bool bucket_sort_fast(BfShared<T, I>& sh, uint2 it, const uint64_t (&xs)[I],
+                                                 const uint32_t (&pvr)[(I + 1) / 2], uint32_t vmask, uint32_t s0,
                                                  uint64_t xmin, int lo, int width, int pb, int xsh, int pbits,
                                                  int term, const uint32_t* __restrict__ vb,
                                                  V* __restrict__ sab, uint8_t* __restrict__ bwb,
                                                  uint64_t* __restrict__ tie_k, V* __restrict__ tie_v,
                                                  unsigned long long* __restrict__ tie_n, uint64_t (&ts)[8]) {
-  constexpr int BF_BITS = bf_bits<T>(), BF_BINS = 1 << BF_BITS;   // u16 counters, two per u32: alias mt
-  constexpr uint32_t BF_BIGCAP = 4u * T;   // bins of 3+ records (u16 bin ids in whist, first half)
-  constexpr uint32_t BF_TIECAP = 4u * T;   // tied records (u16 final index | head << 15, second half)
-  static_assert(BF_BINS * 2 == (T / 64) * 256 * 8, "bin counters alias the match-mask table");
-  static_assert((BF_BIGCAP + BF_TIECAP) * 2 == (T / 64) * 256 * 4, "bin and tie lists fill whist");
-  static_assert(BF_BINS / T == 16, "16 bin counters per thread");
+  using SH = BfShared<T, I>;
+  constexpr int BF_BITS = SH::BITS, BF_BINS = SH::BINS;   // u16 counters, two per u32
+  constexpr uint32_t BF_BIGCAP = BF_BINS / 4;   // bins of 3+ records (u16 bin ids, first half of lists)
+  constexpr uint32_t BF_TIECAP = BF_BINS / 4;   // tied records (u16 final index | head << 15, second half)
+  constexpr int NP = BF_BINS / 2 / T;           // counter words (bin pairs) per thread
+  constexpr int IH = (I + 1) / 2;
+  static_assert(NP == 4 || NP == 8, "8 or 16 bin counters per thread");
   const uint32_t start = it.x, cnt = it.y;
   const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int fb = width < BF_BITS ? width : BF_BITS;
@@ -1424,15 +1441,15 @@ __device__ __forceinline__ bool bucket_sort_fast(BsSharedT<T>& sh, uint2 it, con
   const uint32_t wmask = width >= 32 ? ~0u : ((1u << width) - 1);
   const uint32_t lowmask = (1u << kb) - 1;
   const uint32_t pmask = (1u << pb) - 1;
-  uint32_t* const H2 = reinterpret_cast<uint32_t*>(&sh.mt[0][0]);   // u16 pairs, zero on entry
+  uint32_t* const H2 = sh.H2;
   const uint16_t* const H = reinterpret_cast<const uint16_t*>(H2);
-  uint16_t* const blist = reinterpret_cast<uint16_t*>(&sh.whist[0][0]);
+  uint16_t* const blist = sh.lists;
   uint16_t* const tlist = blist + BF_BIGCAP;
-  uint32_t* const nctr = sh.wsum;   // [0] listed bins, [1] tied records
-  uint32_t lk[BS_I], r0[BS_H], vv[BS_I];
+  uint32_t* const nctr = sh.wsum;   // [0] listed three-record bins, [1] tied records, [2] larger listed bins
+  uint32_t lk[I], r0[IH], vv[I];
   // ---- 1. bin histogram; the atomic's return value is the suffix's rank inside its bin
 #pragma unroll
-  for (int k = 0; k < BS_I; ++k) {
+  for (int k = 0; k < I; ++k) {
     const bool valid = (vmask >> k) & 1u;
     if (X32)
       lk[k] = (((uint32_t)(xs[k] >> 32) >> (xsh - 32)) - (uint32_t)xmin) >> lo & wmask;
@@ -1446,19 +1463,20 @@ __device__ __forceinline__ bool bucket_sort_fast(BsSharedT<T>& sh, uint2 it, con
       const uint32_t bin = lk[k] >> kb, sh16 = 16u * (bin & 1u);
       r = (atomicAdd(&H2[bin >> 1], 1u << sh16) >> sh16) & 0xFFFFu;   // counts <= 18432: no carry
     }
-    if (k < BS_H) r0[k] = r; else r0[k - BS_H] |= r << 16;
+    if (k < IH) r0[k] = r; else r0[k - IH] |= r << 16;
   }
   __syncthreads();
   if (TRACE) ts[2] = stamp();
   // ---- 2. exclusive scan of the 16384 counters (16 per thread) and the largest bin
-  uint32_t w8[8], tsum = 0, tmax = 0;
+  uint32_t w8[NP], tsum = 0, tmax = 0;
   {
-    const uint4 a = reinterpret_cast<const uint4*>(H2)[2 * tid];
-    const uint4 b = reinterpret_cast<const uint4*>(H2)[2 * tid + 1];
-    w8[0] = a.x; w8[1] = a.y; w8[2] = a.z; w8[3] = a.w;
-    w8[4] = b.x; w8[5] = b.y; w8[6] = b.z; w8[7] = b.w;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
+    for (int q = 0; q < NP / 4; ++q) {
+      const uint4 a = reinterpret_cast<const uint4*>(H2)[(NP / 4) * tid + q];
+      w8[4 * q] = a.x; w8[4 * q + 1] = a.y; w8[4 * q + 2] = a.z; w8[4 * q + 3] = a.w;
+    }
+#pragma unroll
+    for (int i = 0; i < NP; ++i) {
       const uint32_t c0 = w8[i] & 0xFFFFu, c1 = w8[i] >> 16;
       tmax = c0 > tmax ? c0 : tmax;
       tmax = c1 > tmax ? c1 : tmax;
@@ -1486,32 +1504,34 @@ __device__ __forceinline__ bool bucket_sort_fast(BsSharedT<T>& sh, uint2 it, con
   {
     const uint32_t b0 = carry + inc - tsum;
     const uint32_t b2 = b0 | (b0 << 16);   // starts <= 18432: no carry between the halves
-    reinterpret_cast<uint4*>(H2)[2 * tid] = make_uint4(b2 + w8[0], b2 + w8[1], b2 + w8[2], b2 + w8[3]);
-    reinterpret_cast<uint4*>(H2)[2 * tid + 1] = make_uint4(b2 + w8[4], b2 + w8[5], b2 + w8[6], b2 + w8[7]);
+#pragma unroll
+    for (int q = 0; q < NP / 4; ++q)
+      reinterpret_cast<uint4*>(H2)[(NP / 4) * tid + q] =
+          make_uint4(b2 + w8[4 * q], b2 + w8[4 * q + 1], b2 + w8[4 * q + 2], b2 + w8[4 * q + 3]);
   }
-  if (tid == 0) { nctr[0] = 0; nctr[1] = 0; }
+  if (tid == 0) { nctr[0] = 0; nctr[1] = 0; nctr[2] = 0; }
   __syncthreads();
   if (TRACE) ts[3] = stamp();
   // ---- 3. positions (coalesced; in flight during the bin work) and records to their bins
   if (PK) {   // packed: from the u32 plane (phase 1), before the records overwrite it
 #pragma unroll
-    for (int k = 0; k < BS_I; ++k) vv[k] = sh.buf[s0 + 64u * k];
+    for (int k = 0; k < I; ++k) vv[k] = sh.buf[s0 + 64u * k];
     __syncthreads();
   } else {
 #pragma unroll
-    for (int k = 0; k < BS_I; ++k) vv[k] = ((vmask >> k) & 1u) ? vb[s0 + 64u * k] : 0u;
+    for (int k = 0; k < I; ++k) vv[k] = ((vmask >> k) & 1u) ? vb[s0 + 64u * k] : 0u;
   }
 #pragma unroll
-  for (int k = 0; k < BS_I; ++k) {
+  for (int k = 0; k < I; ++k) {
     if ((vmask >> k) & 1u) {
-      const uint32_t r = k < BS_H ? (r0[k] & 0xFFFFu) : (r0[k - BS_H] >> 16);
+      const uint32_t r = k < IH ? (r0[k] & 0xFFFFu) : (r0[k - IH] >> 16);
       sh.buf[H[lk[k] >> kb] + r] = ((lk[k] & lowmask) << 15) | (s0 + 64u * k);
     }
   }
   __syncthreads();
   if (TRACE) ts[4] = stamp();
   // ---- 4. bins of one or two records settle in place: final index by slot into aux; 3+ are listed
-  uint32_t bigm = 0;
+  uint32_t bigm = 0, big4 = 0;
   {
     uint32_t pr[BF_BINS / 2 / T], nx[BF_BINS / 2 / T];
 #pragma unroll
@@ -1539,31 +1559,70 @@ __device__ __forceinline__ bool bucket_sort_fast(BsSharedT<T>& sh, uint2 it, con
             tlist[t + 1] = (uint16_t)(s + 1);
           }
         }
-        bigm |= (c >= 3 ? 1u : 0u) << (2 * j + h);
+        bigm |= (c == 3 ? 1u : 0u) << (2 * j + h);
+        big4 |= (c >= 4 ? 1u : 0u) << (2 * j + h);
       }
     }
   }
-  {   // wave-aggregated append of the listed bins
-    const uint32_t nb = __popc(bigm);
-    const uint32_t binc = wave_incl_sum<uint32_t>(nb);
+  {   // wave-aggregated appends of the listed bins: three-record bins from the front of the list,
+      // larger ones from its back (so that each loop of section 5 runs one code path per wave)
+    const uint32_t nb = __popc(bigm), nb4 = __popc(big4);
+    const uint32_t binc = wave_incl_sum<uint32_t>(nb | (nb4 << 16));   // both counts <= 64 * 16
     uint32_t bbase = 0;
-    if (lane == 63 && binc) bbase = atomicAdd(&nctr[0], binc);
-    bbase = __shfl(bbase, 63, 64) + binc - nb;
+    if (lane == 63 && (binc & 0xFFFFu)) bbase = atomicAdd(&nctr[0], binc & 0xFFFFu);
+    if (lane == 63 && (binc >> 16)) bbase |= atomicAdd(&nctr[2], binc >> 16) << 16;
+    bbase = __shfl(bbase, 63, 64);
+    uint32_t b3 = (bbase & 0xFFFFu) + (binc & 0xFFFFu) - nb, b4 = (bbase >> 16) + (binc >> 16) - nb4;
     while (bigm) {
       const int q = __builtin_ctz(bigm);
       bigm &= bigm - 1;
-      if (bbase < BF_BIGCAP) blist[bbase] = (uint16_t)(2u * (tid + T * (q >> 1)) + (q & 1));
-      ++bbase;
+      if (b3 < BF_BIGCAP) blist[b3] = (uint16_t)(2u * (tid + T * (q >> 1)) + (q & 1));
+      ++b3;
+    }
+    while (big4) {
+      const int q = __builtin_ctz(big4);
+      big4 &= big4 - 1;
+      if (b4 < BF_BIGCAP) blist[BF_BIGCAP - 1 - b4] = (uint16_t)(2u * (tid + T * (q >> 1)) + (q & 1));
+      ++b4;
     }
   }
   __syncthreads();
   if (TRACE) ts[5] = stamp();
-  const uint32_t nbig = nctr[0];
-  if (nbig > BF_BIGCAP) return false;
-  // ---- 5. listed bins, one thread each: up to 8 records ranked in registers (all loads in flight
-  // together), larger bins insertion-sorted in place; final indices by slot, equal keys listed
-  for (uint32_t i = tid; i < nbig; i += T) {
-    const uint32_t bn = blist[i];
+  const uint32_t nbig3 = nctr[0], nbig4 = nctr[2];
+  if (nbig3 + nbig4 > BF_BIGCAP) return false;
+  // ---- 5. listed bins, one thread each.  Three records (3/4 of the listed bins for iid text): three
+  // compares rank them.  Then up to 8 records ranked in registers (all loads in flight together),
+  // larger bins insertion-sorted in place; final indices by slot, equal keys listed
+  for (uint32_t i = tid; i < nbig3; i += T) {
+    const uint32_t s = H[blist[i]];
+    const uint32_t x = sh.buf[s], y = sh.buf[s + 1], z = sh.buf[s + 2];   // distinct (the slots differ)
+    const uint32_t xy = x < y, xz = x < z, yz = y < z;
+    sh.aux[x & 0x7FFFu] = (uint16_t)(s + (xy ^ 1u) + (xz ^ 1u));
+    sh.aux[y & 0x7FFFu] = (uint16_t)(s + xy + (yz ^ 1u));
+    sh.aux[z & 0x7FFFu] = (uint16_t)(s + xz + yz);
+    const uint32_t kx = x >> 15, ky = y >> 15, kz = z >> 15;
+    if (kx == ky || kx == kz || ky == kz) {   // equal keys (rare): every record of a group, the smallest heads it
+      const uint32_t r[3] = {x, y, z};
+#pragma unroll
+      for (int q = 0; q < 3; ++q) {
+        uint32_t below = 0, eq = 0, eqb = 0;
+#pragma unroll
+        for (int o = 0; o < 3; ++o) {
+          if (o == q) continue;
+          const bool e15 = (r[o] >> 15) == (r[q] >> 15);
+          below += r[o] < r[q] ? 1u : 0u;
+          eq |= e15 ? 1u : 0u;
+          eqb |= (e15 && r[o] < r[q]) ? 1u : 0u;
+        }
+        if (eq) {
+          const uint32_t t = atomicAdd(&nctr[1], 1u);
+          if (t < BF_TIECAP) tlist[t] = (uint16_t)((s + below) | (eqb ? 0u : 0x8000u));
+        }
+      }
+    }
+  }
+  for (uint32_t i = tid; i < nbig4; i += T) {
+    const uint32_t bn = blist[BF_BIGCAP - 1 - i];
     const uint32_t s = H[bn], e = bn + 1 < (uint32_t)BF_BINS ? (uint32_t)H[bn + 1] : cnt;
     const uint32_t c = e - s;
     if (c <= 8) {
@@ -1622,43 +1681,100 @@ __device__ __forceinline__ bool bucket_sort_fast(BsSharedT<T>& sh, uint2 it, con
   if (TRACE) ts[6] = stamp();
   const uint32_t ntie = nctr[1];
   if (ntie > BF_TIECAP) return false;
-  // tie-list space: one global atomic per workgroup; its latency overlaps the staging
+  // tie-list space: one global atomic per workgroup, by thread 0; only wave 0 waits for it (it writes
+  // the tied records after its share of the SA and BWT)
   unsigned long long tbase = 0;
   if (tid == 0 && ntie) tbase = atomicAdd(tie_n, (unsigned long long)ntie);
-  // ---- 6. stage (position, prev code) by final index
-  uint32_t fin[BS_H];
+  // ---- 6. stage (position, prev code) by final index f, at f + al: al = the SA pointer's position
+  // inside its 4-entry group, so that every 4 staged entries are one aligned 16-B SA store (two for u64
+  // positions) and one aligned 4-B BWT store (both outputs start at the same index, so the BWT pointer
+  // shares the misalignment whenever both arrays are 16-B aligned; else the per-entry stores)
+  const uint32_t al = (uint32_t)(((uintptr_t)sab / sizeof(V)) & 3u);
+  const bool vec = al == (uint32_t)((uintptr_t)bwb & 3u);
+  const uint32_t sto = vec ? al : 0u;
+  uint32_t fin[IH];
 #pragma unroll
-  for (int k = 0; k < BS_I; ++k) {
+  for (int k = 0; k < I; ++k) {
     const uint32_t f = ((vmask >> k) & 1u) ? (uint32_t)sh.aux[s0 + 64u * k] : 0u;
-    if (k < BS_H) fin[k] = f; else fin[k - BS_H] |= f << 16;
+    if (k < IH) fin[k] = f; else fin[k - IH] |= f << 16;
   }
   __syncthreads();
 #pragma unroll
-  for (int k = 0; k < BS_I; ++k) {
+  for (int k = 0; k < I; ++k) {
     if ((vmask >> k) & 1u) {
-      const uint32_t f = k < BS_H ? (fin[k] & 0xFFFFu) : (fin[k - BS_H] >> 16);
+      const uint32_t f = (k < IH ? (fin[k] & 0xFFFFu) : (fin[k - IH] >> 16)) + sto;
       sh.buf[f] = vv[k];
-      sh.aux[f] = (uint16_t)(k < BS_H ? (pvr[k] & 0xFFFFu) : (pvr[k - BS_H] >> 16));
+      sh.aux[f] = (uint16_t)(k < IH ? (pvr[k] & 0xFFFFu) : (pvr[k - IH] >> 16));
     }
   }
-  if (tid == 0) sh.rv[1][0] = tbase;
   __syncthreads();
   // ---- 7. SA / BWT in sorted order, then the tied records
+  auto bwt_byte = [&](uint32_t pos, uint32_t pv) -> uint32_t {
+    return PK && pos == 0 && (pv >> pb) == 0 && term >= 0 ? (uint32_t)term : (uint32_t)sh.inv[pv & pmask];
+  };
+  if (vec) {
+    // groups of 4 staged entries; the BWT bytes of <= 8 codes by one v_perm_b32 from the 8-byte table
+    const uint32_t ng = (cnt + al + 3) >> 2;
+    const uint32_t tlo = reinterpret_cast<const uint32_t*>(sh.inv)[0];
+    const uint32_t thi = reinterpret_cast<const uint32_t*>(sh.inv)[1];
+    for (uint32_t q = tid; q < ng; q += T) {
+      const uint4 p4 = reinterpret_cast<const uint4*>(sh.buf)[q];
+      const uint2 a2 = reinterpret_cast<const uint2*>(sh.aux)[q];
+      const uint32_t pos[4] = {p4.x, p4.y, p4.z, p4.w};
+      const uint32_t pv[4] = {a2.x & 0xFFFFu, a2.x >> 16, a2.y & 0xFFFFu, a2.y >> 16};
+      uint32_t bw;
+      if (pb <= 3) {
+        const uint32_t sel = (pv[0] & pmask) | (pv[1] & pmask) << 8 | (pv[2] & pmask) << 16 | (pv[3] & pmask) << 24;
+        bw = __builtin_amdgcn_perm(thi, tlo, sel);
+        if (PK && term >= 0) {
 #pragma unroll
-  for (int k = 0; k < BS_I; ++k) {
-    const uint32_t r = s0 + 64u * k;
-    if (r < cnt) {
-      const uint32_t pv = sh.aux[r], pos = sh.buf[r];
-      sab[r] = (V)(((uint64_t)(pv >> pb) << 32) | pos);
-      bwb[r] = PK && pos == 0 && (pv >> pb) == 0 && term >= 0 ? (uint8_t)term : sh.inv[pv & pmask];
+          for (int j = 0; j < 4; ++j)
+            if (pos[j] == 0 && (pv[j] >> pb) == 0) bw = (bw & ~(0xFFu << (8 * j))) | ((uint32_t)term << (8 * j));
+        }
+      } else {
+        bw = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) bw |= bwt_byte(pos[j], pv[j]) << (8 * j);
+      }
+      const uint32_t g = 4u * q;
+      if (g >= al && g + 4 <= cnt + al) {   // a whole group: aligned vector stores
+        V* const dst = sab + (g - al);
+        if (sizeof(V) == 4) {
+          *reinterpret_cast<uint4*>(dst) = p4;
+        } else {
+          uint4* const d4 = reinterpret_cast<uint4*>(dst);
+          d4[0] = make_uint4(pos[0], pv[0] >> pb, pos[1], pv[1] >> pb);
+          d4[1] = make_uint4(pos[2], pv[2] >> pb, pos[3], pv[3] >> pb);
+        }
+        *reinterpret_cast<uint32_t*>(bwb + (g - al)) = bw;
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const uint32_t r = g + j;
+          if (r >= al && r < cnt + al) {
+            sab[r - al] = (V)(((uint64_t)(pv[j] >> pb) << 32) | pos[j]);
+            bwb[r - al] = (uint8_t)(bw >> (8 * j));
+          }
+        }
+      }
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < I; ++k) {
+      const uint32_t r = s0 + 64u * k;
+      if (r < cnt) {
+        const uint32_t pv = sh.aux[r], pos = sh.buf[r];
+        sab[r] = (V)(((uint64_t)(pv >> pb) << 32) | pos);
+        bwb[r] = (uint8_t)bwt_byte(pos, pv);
+      }
     }
   }
-  if (ntie) {
-    const uint64_t tb = sh.rv[1][0];
-    for (uint32_t i = tid; i < ntie; i += T) {
-      const uint32_t e = tlist[i], f = e & 0x7FFFu;
+  if (wv == 0 && ntie) {
+    const uint64_t tb = __shfl(tbase, 0, 64);
+    for (uint32_t i = lane; i < ntie; i += 64) {
+      const uint32_t e = tlist[i], f = (e & 0x7FFFu) + sto;
       const uint32_t pv = sh.aux[f];
-      tie_k[tb + i] = (((uint64_t)start + f) << 1) | (e >> 15);
+      tie_k[tb + i] = (((uint64_t)start + (f - sto)) << 1) | (e >> 15);
       tie_v[tb + i] = (V)(((uint64_t)(pv >> pb) << 32) | sh.buf[f]);
     }
   }
@@ -2022,8 +2138,8 @@ __global__ __launch_bounds__(BS_T, 1) void k_bucket_sort(const uint64_t* __restr
 // sort; items it cannot take (wide keys, a bin over BF_MAXBIN) are appended to `fb` for k_bucket_sort.
 // X32 (packed records whose sym field starts at bit >= 32): the sym is the record's high word shifted,
 // so the prologue and the local keys work in 32-bit arithmetic.
-template <typename V, bool TRACE, int T, bool PK = false, bool X32 = false>
-__global__ __launch_bounds__(T, T == 1024 ? 1 : 4) void k_bucket_sort_fast(const uint64_t* __restrict__ keys,
+template <typename V, bool TRACE, int T, int I, bool PK = false, bool X32 = false>
+__global__ __launch_bounds__(T, (T * I <= 9216 ? 2 : 1) * T / 256) void k_bucket_sort_fast(const uint64_t* __restrict__ keys,
                                                               const uint32_t* __restrict__ vals,
                                                               const uint2* __restrict__ items, int pb, int sb, int hb,
                                                               uint64_t symbias, const uint8_t* __restrict__ inv,
@@ -2032,7 +2148,7 @@ __global__ __launch_bounds__(T, T == 1024 ? 1 : 4) void k_bucket_sort_fast(const
                                                               unsigned long long* __restrict__ tie_n,
                                                               uint2* __restrict__ fb, unsigned int* __restrict__ fb_n,
                                                               uint64_t* __restrict__ trace, PkGeom pg) {
-  __shared__ BsSharedT<T> sh;
+  __shared__ BfShared<T, I> sh;
   const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   uint64_t ts[8] = {0};
   if (TRACE) ts[0] = stamp();
@@ -2043,16 +2159,18 @@ __global__ __launch_bounds__(T, T == 1024 ? 1 : 4) void k_bucket_sort_fast(const
   const int pbits = PK ? pg.pbits : 0;
   pb = PK ? pg.pb2 : pb;
   const uint2 it = items[blockIdx.x];
-  uint64_t key[BS_I];
-  bs_load_keys(keys, it, key);
-  const uint32_t s0 = wv * BS_WSPAN + lane;
+  const uint32_t s0 = wv * (I * 64) + lane;   // slot k of this thread: s0 + 64 k
+  uint64_t key[I];
   uint32_t vmask = 0;
 #pragma unroll
-  for (int k = 0; k < BS_I; ++k) vmask |= (s0 + 64u * k < it.y ? 1u : 0u) << k;
+  for (int k = 0; k < I; ++k) {
+    key[k] = s0 + 64u * k < it.y ? keys[it.x + s0 + 64u * k] : 0;
+    vmask |= (s0 + 64u * k < it.y ? 1u : 0u) << k;
+  }
 
   const uint64_t symmask = sb >= 64 ? ~0ull : ((1ull << sb) - 1);
   const int pbe = pb + hb;
-  for (uint32_t i = tid; i < (T / 64) * 256; i += T) (&sh.mt[0][0])[i] = 0;
+  for (uint32_t i = tid; i < (uint32_t)BfShared<T, I>::BINS / 2; i += T) sh.H2[i] = 0;
   // the sym fields once (key -> sym - symbias in place, the BWT code / position bits to pvr), then one
   // reduction of min, max, or, and: the low varying bit of the values is that of the values relative
   // to the minimum, and the relative width is bits((max - min) >> lo).  Branch-free over the item's
@@ -2060,10 +2178,10 @@ __global__ __launch_bounds__(T, T == 1024 ? 1 : 4) void k_bucket_sort_fast(const
   using XT = std::conditional_t<X32, uint32_t, uint64_t>;
   const int xsh = pbits + pbe;   // packed: the sym field's first bit in the record
   const uint32_t pmask = (1u << pb) - 1, himask = (1u << hb) - 1;
-  uint32_t pvr[BS_H];
+  uint32_t pvr[(I + 1) / 2];
   XT xmin = (XT)~0ull, xmax = 0, vor = 0, vand = (XT)~0ull;
 #pragma unroll
-  for (int k = 0; k < BS_I; ++k) {
+  for (int k = 0; k < I; ++k) {
     const bool valid = (vmask >> k) & 1u;
     uint32_t pv;
     XT x;
@@ -2078,7 +2196,7 @@ __global__ __launch_bounds__(T, T == 1024 ? 1 : 4) void k_bucket_sort_fast(const
       x = (XT)(((kl >> pbe) & symmask) - symbias);
       if (!PK) key[k] = x;
     }
-    if (k < BS_H) pvr[k] = pv; else pvr[k - BS_H] |= pv << 16;
+    if (k < (I + 1) / 2) pvr[k] = pv; else pvr[k - (I + 1) / 2] |= pv << 16;
     if (X32) {   // selects: no masked block (the 64-bit variants keep less live with the branch)
       xmin = valid && x < xmin ? x : xmin;
       xmax = valid && x > xmax ? x : xmax;
@@ -2099,7 +2217,7 @@ __global__ __launch_bounds__(T, T == 1024 ? 1 : 4) void k_bucket_sort_fast(const
     vor |= __shfl_xor(vor, o, 64);
     vand &= __shfl_xor(vand, o, 64);
   }
-  XT* const red = reinterpret_cast<XT*>(&sh.whist[0][0]);   // [4][(T / 64)], free until the lists
+  XT* const red = reinterpret_cast<XT*>(sh.red);   // [4][(T / 64)]
   if (lane == 0) {
     red[wv] = xmin;
     red[(T / 64) + wv] = xmax;
@@ -2119,9 +2237,8 @@ __global__ __launch_bounds__(T, T == 1024 ? 1 : 4) void k_bucket_sort_fast(const
   const uint64_t span = (uint64_t)(xmax - xmin) >> lo;
   const int width = var ? 64 - __builtin_clzll(span) : 0;
   if (TRACE) ts[1] = stamp();
-  // (every thread has read the reduction before the fast path reuses whist: its first barrier)
   const bool ok = width >= 1 && width <= 30 &&
-                  bucket_sort_fast<V, TRACE, T, PK, X32>(sh, it, key, pvr, vmask, s0, (uint64_t)xmin, lo, width, pb,
+                  bucket_sort_fast<V, TRACE, T, I, PK, X32>(sh, it, key, pvr, vmask, s0, (uint64_t)xmin, lo, width, pb,
                                                          xsh, pbits, term, vals + it.x,
                                              sa + it.x, bwt + it.x, tie_k, tie_v, tie_n, ts);
   if (!ok && tid == 0) fb[atomicAdd(fb_n, 1u)] = it;
@@ -2378,36 +2495,40 @@ uint64_t sort_bucket_items(Index& ix, const BucketPlan& plan, const uint64_t* ke
       ix.bk_fb.ensure(nn * sizeof(uint2) + 16);
       unsigned int* fbn = reinterpret_cast<unsigned int*>(ix.small.as<uint8_t>() + 4352);   // small+4352: fallback count
       HK_HIP(hipMemsetAsync(fbn, 0, 4, s));
-      auto launch = [&](auto ttag, auto trtag) {
+      auto launch = [&](auto ttag, auto itag, auto trtag) {
         constexpr int T = decltype(ttag)::value;
+        constexpr int I = decltype(itag)::value;
         constexpr bool TR = decltype(trtag)::value;
         if (pk && pk->g.pbits + pk->g.pb2 >= 32) {   // sym fields in the records' high words
-          k_bucket_sort_fast<V, TR, T, true, true><<<grid_n, T, 0, s>>>(
+          k_bucket_sort_fast<V, TR, T, I, true, true><<<grid_n, T, 0, s>>>(
               keys, pk->vfull, ix.bk_items.as<uint2>(), pb, sb, hb, symbias, d_inv, sa, bwt,
               ix.ties_k.as<uint64_t>(), ix.ties_v.as<V>(), ix.ties_n.as<unsigned long long>(), ix.bk_fb.as<uint2>(),
               fbn, TR ? tbuf.as<uint64_t>() : nullptr, pk->g);
           return;
         }
         if (pk) {
-          k_bucket_sort_fast<V, TR, T, true><<<grid_n, T, 0, s>>>(
+          k_bucket_sort_fast<V, TR, T, I, true><<<grid_n, T, 0, s>>>(
               keys, pk->vfull, ix.bk_items.as<uint2>(), pb, sb, hb, symbias, d_inv, sa, bwt,
               ix.ties_k.as<uint64_t>(), ix.ties_v.as<V>(), ix.ties_n.as<unsigned long long>(), ix.bk_fb.as<uint2>(),
               fbn, TR ? tbuf.as<uint64_t>() : nullptr, pk->g);
           return;
         }
-        k_bucket_sort_fast<V, TR, T><<<grid_n, T, 0, s>>>(
+        k_bucket_sort_fast<V, TR, T, I><<<grid_n, T, 0, s>>>(
             keys, vals, ix.bk_items.as<uint2>(), pb, sb, hb, symbias, d_inv, sa, bwt, ix.ties_k.as<uint64_t>(),
             ix.ties_v.as<V>(), ix.ties_n.as<unsigned long long>(), ix.bk_fb.as<uint2>(), fbn,
             TR ? tbuf.as<uint64_t>() : nullptr, PkGeom{});
       };
       using T512 = std::integral_constant<int, 512>;
       using T1024 = std::integral_constant<int, 1024>;
+      using I18 = std::integral_constant<int, 18>;
       using TrOn = std::integral_constant<bool, true>;
       using TrOff = std::integral_constant<bool, false>;
+      // (1024 threads of 9 suffixes for the half items, two workgroups per CU at 64 VGPRs, spilled and
+      // ran 2x slower: 10.5 vs 5.3 ms at 1 GiB)
       if (plan.cap <= (uint64_t)512 * BS_I) {
-        if (trace) launch(T512{}, TrOn{}); else launch(T512{}, TrOff{});
+        if (trace) launch(T512{}, I18{}, TrOn{}); else launch(T512{}, I18{}, TrOff{});
       } else {
-        if (trace) launch(T1024{}, TrOn{}); else launch(T1024{}, TrOff{});
+        if (trace) launch(T1024{}, I18{}, TrOn{}); else launch(T1024{}, I18{}, TrOff{});
       }
       HK_HIP(hipGetLastError());
       if (trace) {
