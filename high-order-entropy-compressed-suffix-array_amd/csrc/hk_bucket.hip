@@ -1082,21 +1082,30 @@ __global__ __launch_bounds__(CP_T, 2) void k_slice_cpart(uint64_t* __restrict__ 
   }
 }
 
-// Pass A of a slice, radix 2^2 packed records, all in registers (g <= SL_G sub-tiles per unit): every
-// text load of the unit is issued up front (three 16-B loads and the word before per thread and
-// sub-tile), the packed codes and the kept-position masks stay in registers between round 1 (bins ->
-// digit counts) and round 2, which keys only the kept positions (a bit loop: ~1/N of the 16 per
-// sub-tile) and stages them at their final slots.  Each sub-tile of a unit denser than one tile is
+// diagnostic stamps (TRACE): shader-clock time at the phase boundaries
+__device__ __forceinline__ uint64_t stamp() {
+  uint64_t t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
+
+// Pass A of a slice, radix 2^2 packed records (g <= SL_G sub-tiles per unit): the unit's text is copied
+// into LDS up front by DMA (every load in flight together, no VGPRs held), the packed codes and the
+// kept-position masks stay in registers between round 1 (bins -> digit counts) and round 2, which keys
+// only the kept positions (a bit loop: ~1/N of the 16 per sub-tile) and stages them at their final slots.  Each sub-tile of a unit denser than one tile is
 // ranked, reserved and written on its own (non-iid text), as in k_slice_cpart.
 constexpr int SL_G = 8;
 
+template <bool TRACE = false>
 __global__ __launch_bounds__(CP_T, 4) void k_slice_cpart_reg(uint64_t* __restrict__ kout, uint64_t n,
                                                              unsigned long long* __restrict__ cur, uint64_t span,
                                                              TextKeySrc src, SliceSel sl,
                                                              const unsigned long long* __restrict__ skip,
-                                                             uint64_t mcap) {
+                                                             uint64_t mcap, uint64_t* __restrict__ trace = nullptr) {
   constexpr int T = CP_T;
-  __shared__ uint64_t keys[CP_TILE];
+  __shared__ uint64_t keys[CP_TILE + 8];   // round 1: the unit's text image (<= 8 sub-tiles + 64 B)
   __shared__ uint8_t sdg[CP_TILE];
   __shared__ uint32_t tg[CP_NAM], cnt[CP_NAM], wsum[CP_NAM / 64];
   __shared__ uint16_t LP[256];
@@ -1108,47 +1117,60 @@ __global__ __launch_bounds__(CP_T, 4) void k_slice_cpart_reg(uint64_t* __restric
   const uint64_t unit = (uint64_t)(gx + 8u * (k8 / per)) * per + k8 % per;
   const uint64_t ubase = unit * U;
   if (ubase >= n) return;   // past the last span (whole workgroup, before any barrier)
+  uint64_t ts[5] = {0, 0, 0, 0, 0};
+  if (TRACE) ts[0] = stamp();
+  auto trace_out = [&]() {
+    if (TRACE && tid == 0) {
+      ts[4] = stamp();
+      for (int i = 0; i < 5; ++i) trace[(uint64_t)blockIdx.x * 8 + i] = ts[i];
+      trace[(uint64_t)blockIdx.x * 8 + 5] = 1;
+    }
+  };
   unsigned long long* const row = cur + (ubase / span) * CP_NAM;
   const uint32_t nsub = (uint32_t)((n - ubase < U ? n - ubase : U) + SL_SUB - 1) / SL_SUB;
+  // the unit's text bytes [ubase - 16, ubase + U + 48) land in LDS by DMA (global_load_lds, 1 KiB per
+  // wave-instruction, all in flight together, no VGPRs held); bytes outside [0, n + 64) are not read
+  // (T' has 64 readable pad bytes; positions past n only feed short suffixes, keyed from SK)
+  uint8_t* const img = reinterpret_cast<uint8_t*>(keys);
+  __shared__ uint32_t last_byte;   // position 0's prev byte (every global load done before the copies)
+  if (tid == 0) last_byte = src.text[n - 1];
   if (tid < 256) LP[tid] = src.lutp[tid];
   if (tid < 72) SK[tid] = src.skey[tid];
   cnt[tid] = 0;
+  // the unit's text bytes [ubase - 16, ubase + U + 48) land in LDS by DMA (1 KiB per wave-instruction,
+  // all in flight together, no VGPRs held); bytes outside [0, n + 64) are not read (T' has 64 readable
+  // pad bytes; positions past n only feed short suffixes, keyed from SK).  Issued after every other
+  // global load, waited for once.  (Per-wave copies of each sub-tile with counted waits instead were
+  // slower: 8.5 vs 7.8 ms per emulated N = 8 rank.)
+  {
+    const uint32_t nins = (uint32_t)((U + 64 + 1023) / 1024);
+    for (uint32_t i = wv; i < nins; i += T / 64) {
+      const uint64_t off = (uint64_t)i * 1024 + lane * 16u;   // image byte of this lane
+      if (ubase + off >= 16 && ubase + off <= n + 64)
+        __builtin_amdgcn_global_load_lds(src.text + (ubase + off - 16), img + (uint64_t)i * 1024, 16, 0, 0);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   const uint64_t lim = n < src.g.s_start ? n : src.g.s_start;
   const uint64_t sbase = (uint64_t)sl.base << sl.bsh;
   const int kbits = 2 * src.g.q, dsh = 32 - sl.DB;
-  // ---- round 1: packed codes, kept-position masks, digit counts.  The unit's loads go out in two
-  // batches of SL_G / 2 sub-tiles (all of them at once held ~190 VGPRs: 2 waves per SIMD)
-  constexpr int SB = SL_G / 2;
+  // ---- round 1: packed codes (from the LDS image), kept-position masks, digit counts
   uint32_t c[SL_G][3], msk[SL_G], pcs = 0;
-  uint4 q[SB][3];
-  uint32_t pw[SB];
 #pragma unroll
   for (int st = 0; st < SL_G; ++st) {
-    if (st % SB == 0) {
-#pragma unroll
-      for (int u = 0; u < SB; ++u) {
-        const uint64_t pu = ubase + (uint64_t)(st + u) * SL_SUB + 16ull * tid;
-        q[u][0] = q[u][1] = q[u][2] = make_uint4(0, 0, 0, 0);
-        pw[u] = 0;
-        if ((uint32_t)(st + u) < nsub && pu < n) {   // T' has 64 readable pad bytes
-          const uint4* q4 = reinterpret_cast<const uint4*>(src.text + pu);
-          q[u][0] = q4[0];
-          q[u][1] = q4[1];
-          q[u][2] = q4[2];
-          if (pu) pw[u] = reinterpret_cast<const uint32_t*>(src.text + pu)[-1];
-        }
-      }
-    }
     msk[st] = 0;
-    c[st][0] = pack16_2(q[st % SB][0], sl);
-    c[st][1] = pack16_2(q[st % SB][1], sl);
-    c[st][2] = pack16_2(q[st % SB][2], sl);
+    c[st][0] = c[st][1] = c[st][2] = 0;
     const uint64_t p0 = ubase + (uint64_t)st * SL_SUB + 16ull * tid;
     if ((uint32_t)st >= nsub || p0 >= n) continue;
+    const uint32_t ib = 16u + (uint32_t)st * SL_SUB + 16u * tid;
+    const uint4* q4 = reinterpret_cast<const uint4*>(img + ib);
+    c[st][0] = pack16_2(q4[0], sl);
+    c[st][1] = pack16_2(q4[1], sl);
+    c[st][2] = pack16_2(q4[2], sl);
     // prev code of p0: the records' code of T'[p0 - 1] (T'[n - 1] for p0 = 0)
-    const uint32_t pb = pw[st % SB] >> 24;
-    const uint32_t pc = p0 ? __builtin_amdgcn_perm(sl.th, sl.tl, (pb >> sl.ps) & 7u) & 3u : (uint32_t)LP[src.text[n - 1]];
+    const uint32_t pb = reinterpret_cast<const uint32_t*>(img + ib)[-1] >> 24;
+    const uint32_t pc = p0 ? __builtin_amdgcn_perm(sl.th, sl.tl, (pb >> sl.ps) & 7u) & 3u : (uint32_t)LP[last_byte];
     pcs |= pc << (2 * st);
     const bool full = p0 + 16 <= lim;
     uint32_t m = 0;
@@ -1196,6 +1218,7 @@ __global__ __launch_bounds__(CP_T, 4) void k_slice_cpart_reg(uint64_t* __restric
     rec = (((wr << (kbits - Z)) >> (64 - Z)) << pz) | ((uint64_t)prv << sl.pbits) | j;
     return (uint32_t)(wr >> (64 - kbits + Z));
   };
+  if (TRACE) ts[1] = stamp();
   __syncthreads();
   const uint32_t cu = cnt[tid];
   uint32_t total = 0;
@@ -1225,6 +1248,7 @@ __global__ __launch_bounds__(CP_T, 4) void k_slice_cpart_reg(uint64_t* __restric
   if (total <= (uint32_t)CP_TILE) {
     const unsigned long long resv = cu ? atomicAdd(&row[tid], (unsigned long long)cu) : 0ull;
     __syncthreads();
+    if (TRACE) ts[2] = stamp();
     // ---- round 2: key and stage the kept positions only
 #pragma unroll
     for (int st = 0; st < SL_G; ++st) {
@@ -1251,12 +1275,14 @@ __global__ __launch_bounds__(CP_T, 4) void k_slice_cpart_reg(uint64_t* __restric
       }
     }
     __syncthreads();
+    if (TRACE) ts[3] = stamp();
     const uint32_t hi256 = tg[256];
     const uint32_t gbv = (uint32_t)(resv - tg[tid]);
     __syncthreads();
     tg[tid] = gbv;
     __syncthreads();
     write_out(total, hi256);
+    trace_out();
     return;
   }
   // dense unit: each sub-tile counted, reserved, staged and written on its own (ranks by a second
@@ -1359,14 +1385,6 @@ struct alignas(16) BsSharedT {
 };
 using BsShared = BsSharedT<BS_T>;   // the LSD passes (k_bucket_sort) always run 1024-thread items
 
-// diagnostic stamps (TRACE): shader-clock time at the phase boundaries
-__device__ __forceinline__ uint64_t stamp() {
-  uint64_t t;
-  __builtin_amdgcn_sched_barrier(0);
-  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
-  __builtin_amdgcn_sched_barrier(0);
-  return t;
-}
 
 // One workgroup sorts items[blockIdx.x] = {start, count} of the bucket-grouped (keys, vals): LSD
 // radix passes over the key bits that vary inside the range (wave ballot ranking in two
@@ -3434,8 +3452,30 @@ static int cursor_partition_slice(Index& ix, const SlicePlan& P, const TextKeySr
     const unsigned grid = (unsigned)(8 * ceil_div(nspan, 8u) * (span / U));
     void* vo = P.packed ? nullptr : (void*)vp[outA];
     const unsigned long long* skip = D > 16 ? d_ovf : nullptr;
-    if (P.reg)
-      k_slice_cpart_reg<<<grid, CP_T, 0, s>>>(kp[outA], n, d_curA, span, tks2, sl, skip, m);
+    static const bool trace = getenv("HKCSA_SL_TRACE") != nullptr;   // diagnostic phase stamps
+    if (P.reg) {
+      if (trace) {
+        DevBuf tb;
+        tb.ensure((uint64_t)grid * 64 + 64);
+        HK_HIP(hipMemsetAsync(tb.p, 0, (uint64_t)grid * 64, s));
+        k_slice_cpart_reg<true><<<grid, CP_T, 0, s>>>(kp[outA], n, d_curA, span, tks2, sl, skip, m, tb.as<uint64_t>());
+        std::vector<uint64_t> h((uint64_t)grid * 8);
+        HK_HIP(hipMemcpyAsync(h.data(), tb.p, h.size() * 8, hipMemcpyDeviceToHost, s));
+        HK_HIP(hipStreamSynchronize(s));
+        double acc[4] = {0, 0, 0, 0};
+        uint64_t nw = 0;
+        for (uint64_t w = 0; w < grid; ++w)
+          if (h[w * 8 + 5]) {
+            ++nw;
+            for (int i = 0; i < 4; ++i) acc[i] += (double)(h[w * 8 + i + 1] - h[w * 8 + i]);
+          }
+        if (nw)
+          fprintf(stderr, "[slice_cpart_reg trace] %llu units, mean cycles: round 1 %.0f, count+reserve %.0f, "
+                  "round 2 %.0f, write %.0f\n", (unsigned long long)nw, acc[0] / nw, acc[1] / nw, acc[2] / nw, acc[3] / nw);
+      } else {
+        k_slice_cpart_reg<<<grid, CP_T, 0, s>>>(kp[outA], n, d_curA, span, tks2, sl, skip, m);
+      }
+    }
     else if (P.packed && P.lb == 2)
       k_slice_cpart<2, true><<<grid, CP_T, 0, s>>>(kp[outA], nullptr, n, d_curA, span, tks2, sl, skip, m);
     else if (P.packed && P.lb == 1)
