@@ -355,9 +355,10 @@ __global__ __launch_bounds__(BH_T, 1) void k_key_hist_spans(const uint64_t* __re
 // hist[b] = drained counts + the spans' partial counts of bucket b
 __global__ __launch_bounds__(256) void k_bucket_reduce(const uint32_t* __restrict__ part,
                                                        const unsigned long long* __restrict__ drain, uint32_t nspan,
-                                                       uint32_t stride, uint32_t nb, uint64_t* __restrict__ hist) {
+                                                       uint32_t stride, uint32_t nb, uint64_t* __restrict__ hist,
+                                                       const unsigned long long* __restrict__ only_if = nullptr) {
   const uint32_t b = blockIdx.x * 256 + threadIdx.x;
-  if (b >= nb) return;
+  if (b >= nb || (only_if && !*only_if)) return;
   uint64_t s = drain[b];
 #pragma unroll 8
   for (uint32_t w = 0; w < nspan; ++w) s += part[(uint64_t)w * stride + b];
@@ -3149,11 +3150,13 @@ __global__ __launch_bounds__(BH_T, 1) void k_coarse_hist(const uint8_t* __restri
                                                          uint64_t hi, const uint16_t* __restrict__ lutk,
                                                          const uint64_t* __restrict__ skey, KeyedArgs g, int hq,
                                                          int bsh16, uint64_t span, uint32_t* __restrict__ part,
-                                                         unsigned long long* __restrict__ drain) {
+                                                         unsigned long long* __restrict__ drain,
+                                                         const unsigned long long* __restrict__ only_if = nullptr) {
   __shared__ uint32_t H[32768];
   __shared__ uint16_t L[256];
   __shared__ uint64_t SK[72];
   const uint32_t tid = threadIdx.x;
+  if (only_if && !*only_if) return;   // the register count did not wrap: nothing to recount
   for (uint32_t i = tid; i < 32768; i += BH_T) H[i] = 0;
   if (tid < 256) L[tid] = lutk[tid];
   if (tid < 72) SK[tid] = skey[tid];
@@ -3203,6 +3206,8 @@ int shard_keyed_lb(Index& ix) {
   return coarse_lb(kg);
 }
 
+static bool reg_tables(const KeyGeom& kk, SliceSel& sl);
+
 void shard_coarse_hist(Index& ix, uint64_t lo, uint64_t hi, uint64_t* d_hist) {
   hipStream_t s = ix.stream;
   const KeyGeom kg0 = key_geometry_keyed(ix);
@@ -3216,19 +3221,58 @@ void shard_coarse_hist(Index& ix, uint64_t lo, uint64_t hi, uint64_t* d_hist) {
   HK_HIP(hipMemsetAsync(d_hist, 0, 65536 * 8, s));
   if (hi <= lo) return;
   if (lo % 16) throw ApiError{-1, "coarse histogram: block start not 16-aligned"};
-  const uint64_t span = ceil_div(ceil_div(hi - lo, (uint64_t)BH_TILE), 256) * BH_TILE;
-  const uint32_t nspan = (uint32_t)ceil_div(hi - lo, span);
-  ix.cp_part.ensure((uint64_t)nspan * 65536 * 4 + 16);
   ix.bk_hist.ensure(65536 * 8 + 16);
   unsigned long long* d_drain = ix.bk_hist.as<unsigned long long>();
   HK_HIP(hipMemsetAsync(d_drain, 0, 65536 * 8, s));
   TimedLaunch t(ix.timer, "shard_hist", (double)(hi - lo));
+  // radix 2^2 with a 3-bit byte field separating the keyed bytes: the register pre-pass of the slices
+  // (k_slice_hist_spans REG, the whole sym space as one slice of 2^16 bins: the 16-bit window's top
+  // bits) over 4 MiB spans of the block with undrained u8 counters; a wrap raises the flag and the
+  // exact u16 count below runs in its place (device-side: it returns at once when the flag is clear).
+  // HKCSA_COARSE_REG=0 keeps the u16 count only (A/B).
+  static const bool creg = !getenv("HKCSA_COARSE_REG") || atoi(getenv("HKCSA_COARSE_REG")) != 0;
+  SliceSel rs;
+  const unsigned long long* only_if = nullptr;
+  if (creg && lb == 2 && lo <= kg.s_start && reg_tables(kg, rs)) {
+    rs.base = 0;
+    rs.nb = 65536;
+    rs.DB = 16;
+    rs.bsh = kg.sym_bits - 16;
+    rs.sA = 7;
+    rs.wb = 0;
+    rs.wn1 = ~0u;
+    KeyedArgs kr = ka;
+    kr.s_start = kg.s_start - lo;   // positions relative to the block (the windows read on past its end)
+    const uint64_t rspan = (uint64_t)1 << 22;
+    const uint32_t rn = (uint32_t)ceil_div(hi - lo, rspan);
+    // (one allocation for both counts: the exact count's partials follow the flag word)
+    const uint64_t span = ceil_div(ceil_div(hi - lo, (uint64_t)BH_TILE), 256) * BH_TILE;
+    ix.cp_part.ensure(((uint64_t)rn * (65536 + CP_NAM) + 16 + ceil_div(hi - lo, span) * 65536) * 4 + 16);
+    uint32_t* d_part = ix.cp_part.as<uint32_t>();
+    unsigned long long* d_ovf = reinterpret_cast<unsigned long long*>(d_part + (uint64_t)rn * (65536 + CP_NAM));
+    HK_HIP(hipMemsetAsync(d_ovf, 0, 8, s));
+    k_slice_hist_spans<8, -1, 2, 0, true><<<rn, BH_T, 0, s>>>(
+        ix.text.as<uint8_t>() + lo, hi - lo, reinterpret_cast<const uint16_t*>(small + 2560),
+        reinterpret_cast<const uint64_t*>(small + 3584), kr, rs, 16, d_part, d_drain, d_part + (uint64_t)rn * 65536,
+        rspan, d_ovf);
+    HK_HIP(hipGetLastError());
+    k_bucket_reduce<<<65536 / 256, 256, 0, s>>>(d_part, d_drain, rn, 65536, 65536, d_hist);
+    HK_HIP(hipGetLastError());
+    HK_HIP(hipMemsetAsync(d_drain, 0, 65536 * 8, s));
+    only_if = d_ovf;
+  }
+  const uint64_t span = ceil_div(ceil_div(hi - lo, (uint64_t)BH_TILE), 256) * BH_TILE;
+  const uint32_t nspan = (uint32_t)ceil_div(hi - lo, span);
+  // (the exact count's partials after the register count's flag word)
+  const uint64_t poff = only_if ? (uint64_t)ceil_div(hi - lo, (uint64_t)1 << 22) * (65536 + CP_NAM) + 16 : 0;
+  ix.cp_part.ensure((poff + (uint64_t)nspan * 65536) * 4 + 16);
+  uint32_t* const xpart = ix.cp_part.as<uint32_t>() + poff;
   k_coarse_hist<<<nspan, BH_T, 0, s>>>(ix.text.as<uint8_t>(), ix.n, lo, hi,
                                        reinterpret_cast<const uint16_t*>(small + 2560),
                                        reinterpret_cast<const uint64_t*>(small + 3584), ka, 16 / lb, kg.sym_bits - 16,
-                                       span, ix.cp_part.as<uint32_t>(), d_drain);
+                                       span, xpart, d_drain, only_if);
   HK_HIP(hipGetLastError());
-  k_bucket_reduce<<<65536 / 256, 256, 0, s>>>(ix.cp_part.as<uint32_t>(), d_drain, nspan, 65536, 65536, d_hist);
+  k_bucket_reduce<<<65536 / 256, 256, 0, s>>>(xpart, d_drain, nspan, 65536, 65536, d_hist, only_if);
   HK_HIP(hipGetLastError());
 }
 
