@@ -198,7 +198,7 @@ __global__ __launch_bounds__(256) void k_wt_partition(const uint8_t* __restrict_
                                                       const uint64_t* __restrict__ rbase,
                                                       const uint16_t* __restrict__ lut,
                                                       const uint64_t* __restrict__ bspan, uint32_t nbspan,
-                                                      int translate, WtSmall sa) {
+                                                      int translate, WtSmall sa, int carry) {
   __shared__ uint64_t OB[256], RB[256];
   __shared__ uint16_t LU[256];
   __shared__ uint64_t BS[256];
@@ -215,19 +215,45 @@ __global__ __launch_bounds__(256) void k_wt_partition(const uint8_t* __restrict_
   WtRun run[2] = {{0, 0, 0, false}, {0, 0, 0, false}};
   uint32_t bi = 0;   // boundary spans below t
   while (bi < nbspan && BS[bi] < t0) ++bi;
-  for (uint64_t t = t0; t < t1; ++t) {
-    const uint64_t base = t * 1024, j0 = base + lane * 16u;
-    const uint4 v = j0 < n ? *reinterpret_cast<const uint4*>(S + j0) : make_uint4(0, 0, 0, 0);
-    const uint64_t li0 = base / kLineBits;
+  // ones before the wave's first span from its rank line; after that the wave carries the count
+  // (its spans are contiguous), so no span waits on a line read, and the next span's symbols are
+  // loaded while this one is partitioned (HKCSA_WT_CARRY=0: a line read per span, no prefetch)
+  uint64_t onesbase = 0;
+  if (t0 < t1) {
+    const uint64_t base = t0 * 1024, li0 = base / kLineBits;
     const uint32_t wi0 = (uint32_t)(base - li0 * kLineBits) / 64;
     uint64_t part = 0;
     if (lane < wi0) part = (uint64_t)__popcll(lines[li0 * 8 + 1 + lane]);
     else if (lane == 7) part = lines[li0 * 8];
-    const uint64_t onesbase = wave_sum<uint64_t>(part);
+    onesbase = wave_sum<uint64_t>(part);
+  }
+  // unconditional loads (a load under a runtime condition makes hipcc wait for every load in flight
+  // before it): past the text the address is clamped to readable bytes, which the valid mask drops
+  const uint64_t jmax = n & ~15ull;
+  auto load_span = [&](uint64_t t) {
+    const uint64_t j = t * 1024 + lane * 16u;
+    return *reinterpret_cast<const uint4*>(S + (j < n ? j : jmax));
+  };
+  uint4 vnext = carry && t0 < t1 ? load_span(t0) : make_uint4(0, 0, 0, 0);
+  for (uint64_t t = t0; t < t1; ++t) {
+    const uint64_t base = t * 1024, j0 = base + lane * 16u;
+    uint4 vv;
+    if (carry) {
+      vv = vnext;
+      vnext = load_span(t + 1 < t1 ? t + 1 : t);
+    } else {
+      vv = load_span(t);
+      const uint64_t li0 = base / kLineBits;
+      const uint32_t wi0 = (uint32_t)(base - li0 * kLineBits) / 64;
+      uint64_t part = 0;
+      if (lane < wi0) part = (uint64_t)__popcll(lines[li0 * 8 + 1 + lane]);
+      else if (lane == 7) part = lines[li0 * 8];
+      onesbase = wave_sum<uint64_t>(part);
+    }
     const uint32_t nv = j0 >= n ? 0u : (n - j0 >= 16 ? 16u : (uint32_t)(n - j0));
     const uint32_t valid = nv == 16 ? 0xFFFFu : (1u << nv) - 1;
     uint32_t bits = 0;
-    uint32_t cw[4] = {v.x, v.y, v.z, v.w};
+    uint32_t cw[4] = {vv.x, vv.y, vv.z, vv.w};
     if (SMALL) {
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
@@ -257,6 +283,7 @@ __global__ __launch_bounds__(256) void k_wt_partition(const uint8_t* __restrict_
     const uint32_t ones = __popc(bits), nz = nv - ones;
     const uint32_t oinc = wave_incl_sum<uint32_t>(ones), zinc = wave_incl_sum<uint32_t>(nz);
     const uint32_t opre = oinc - ones, zpre = zinc - nz;
+    const uint64_t onesnext = onesbase + (uint32_t)__shfl(oinc, 63, 64);   // the next span's ones before
     const uint32_t c0 = (uint32_t)__shfl(cw[0] & 255u, 0, 64);   // code of the span's first symbol
     const bool boundary = bi < nbspan && BS[bi] == t;
     if (boundary) ++bi;
@@ -336,6 +363,7 @@ __global__ __launch_bounds__(256) void k_wt_partition(const uint8_t* __restrict_
         }
       }
     }
+    onesbase = onesnext;
   }
   __builtin_amdgcn_wave_barrier();
   wt_run_flush(run[0], ST[wv][0], out, lane);
@@ -997,6 +1025,7 @@ void build_wt(Index& ix) {
     ix.tile_d.ensure(bsp.size() * 8);
     HK_HIP(hipMemcpyAsync(ix.tile_d.p, bsp.data(), bsp.size() * 8, hipMemcpyHostToDevice, s));
     int cur = 0;
+    static const int wt_carry = !getenv("HKCSA_WT_CARRY") || atoi(getenv("HKCSA_WT_CARRY")) != 0;
     const unsigned gb = grid_for(ceil_div(nlines, WT_V), 4, 8192), gp = grid_for(ceil_div(n, 1024), 4, 8192);
     for (int d = 0; d < L; ++d) {
       ix.wt_lines[d].ensure(nlines * 64);
@@ -1026,12 +1055,12 @@ void build_wt(Index& ix) {
           k_wt_partition<true><<<gp, 256, 0, s>>>(in, outp, n, lines, ix.wt_obn.as<uint64_t>() + d * 256,
                                                   ix.wt_rbase.as<uint64_t>() + d * 256,
                                                   ix.wt_lut.as<uint16_t>() + d * 256, ix.tile_d.as<uint64_t>() + d * 256,
-                                                  nbsp[d], d == 0 ? 1 : 0, sml[d]);
+                                                  nbsp[d], d == 0 ? 1 : 0, sml[d], wt_carry);
         else
           k_wt_partition<false><<<gp, 256, 0, s>>>(in, outp, n, lines, ix.wt_obn.as<uint64_t>() + d * 256,
                                                    ix.wt_rbase.as<uint64_t>() + d * 256,
                                                    ix.wt_lut.as<uint16_t>() + d * 256,
-                                                   ix.tile_d.as<uint64_t>() + d * 256, nbsp[d], d == 0 ? 1 : 0, sml[d]);
+                                                   ix.tile_d.as<uint64_t>() + d * 256, nbsp[d], d == 0 ? 1 : 0, sml[d], wt_carry);
         HK_HIP(hipGetLastError());
         if (nib && ng > 0 && d + 1 == ng) nib_level(1, outp, ix.nib_tab.as<uint8_t>() + 768);
         if (d > 0) cur ^= 1;
