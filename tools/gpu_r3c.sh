@@ -18,7 +18,7 @@ step trace 200 env HKCSA_BS_TRACE=1 python3 bench.py --steps 1 --warmup 0 --patt
 grep -h "trace\]" "$O/trace.err"
 [ -n "$SKIP_SHARD" ] || step sharded 300 python3 bench.py --sharded --steps 5 --warmup 1 --no-cpu-baseline --no-legs --no-eps --no-pcie
 [ -n "$SKIP_SHARD" ] || step strong 400 python3 bench.py --strong --steps 3 --warmup 1 --no-cpu-baseline --no-legs --no-eps --no-pcie
-cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/$O/prof" -o run -- \
+cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$GRAFT_REPO_ROOT/$O/prof" -o run -- \
   python3 "$GRAFT_REPO_ROOT/bench.py" --steps 5 --warmup 1 --no-cpu-baseline --no-pcie > "$GRAFT_REPO_ROOT/$O/prof.out" 2> "$GRAFT_REPO_ROOT/$O/prof.err"
 rc=$?; echo "== rocprof rc=$rc"; [ $rc -eq 0 ] || { tail -20 "$GRAFT_REPO_ROOT/$O/prof.err"; exit $rc; }
 find "$GRAFT_REPO_ROOT/$O/prof" -name "*kernel_stats.csv" | head -3
