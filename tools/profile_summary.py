@@ -40,7 +40,7 @@ TIMERS = {
     "radix_part_text": lambda k: "k_cpart<0," in k,
     "radix_part_keys": lambda k: "k_cpart<1," in k,
     "radix_part": lambda k: "k_cpart<2," in k,
-    "sa_bucket_hist": lambda k: "k_bucket_hist_spans" in k,
+    "sa_bucket_hist": lambda k: "k_bucket_hist_spans" in k or "k_slice_hist_spans" in k,
     "sa_digit_hist": lambda k: "k_bucket_hist<" in k,
     "fm_count": lambda k: "k_count" in k,
 }
