@@ -120,7 +120,9 @@ struct Index {
   uint64_t nib_nsb = 0;
   DevBuf tile_a, tile_b, tile_c, tile_d, tile_e;
   DevBuf small;                // scratch for totals etc.
-  HostBuf small_host;          // pinned staging of the geometry tables (one upload per geometry)
+  HostBuf small_host;          // pinned staging of the geometry tables (one upload per geometry), with
+                               // the byte histogram's landing slots [0, 2048) and the text tail's at 8192
+  hipEvent_t geom_ev = nullptr;   // the last geometry upload (its staging is reused by the next one)
   HostBuf items_host;          // pinned staging of the bucket-sort work items
   HostBuf rb_host;             // pinned landing slots of the build's small read-backs (counts, totals)
   uint64_t* rb(int k = 4) {    // k u64 slots

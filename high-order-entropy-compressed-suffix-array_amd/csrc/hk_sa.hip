@@ -785,8 +785,9 @@ void upload_geometry(Index& ix, const KeyGeom& kg) {
   if (kg.keyed) {   // small+2560 = lutk, +4608 = lutp (u16[256]), +3584 = skey (u64[72]), +7168 = srank (u32[72])
     // +7456 = k2d (u16[256]); the ranges in between (4096: locate / fallback counters, 5120: digit
     // histogram) are reset by their users before use.  Staged in pinned memory: one upload.
-    ix.small_host.ensure(8192);
+    ix.small_host.ensure(8192 + 128);
     uint8_t* hs = ix.small_host.as<uint8_t>();
+    if (ix.geom_ev) HK_HIP(hipEventSynchronize(ix.geom_ev));   // the previous upload has read the staging
     memcpy(hs + 2048, kg.lut, 512);
     memcpy(hs + 3072, kg.inv, 512);
     memcpy(hs + 2560, kg.lutk, 512);
@@ -797,11 +798,14 @@ void upload_geometry(Index& ix, const KeyGeom& kg) {
     static_assert(7456 + sizeof(kg.k2d) <= 8192, "geometry tables fit the small buffer");
     HK_HIP(hipMemcpyAsync(ix.small.as<uint8_t>() + 2048, hs + 2048, 7456 + sizeof(kg.k2d) - 2048,
                           hipMemcpyHostToDevice, ix.stream));
+    // no wait here: the next upload (or histogram landing) waits for this event before reusing the staging
+    if (!ix.geom_ev) HK_HIP(hipEventCreateWithFlags(&ix.geom_ev, hipEventDisableTiming));
+    HK_HIP(hipEventRecord(ix.geom_ev, ix.stream));
   } else {
     HK_HIP(hipMemcpyAsync(ix.small.as<uint8_t>() + 2048, kg.lut, 512, hipMemcpyHostToDevice, ix.stream));
     HK_HIP(hipMemcpyAsync(ix.small.as<uint8_t>() + 3072, kg.inv, 512, hipMemcpyHostToDevice, ix.stream));
+    HK_HIP(hipStreamSynchronize(ix.stream));   // kg may be a host temporary
   }
-  HK_HIP(hipStreamSynchronize(ix.stream));   // kg may be a host temporary; the staging is reused
 }
 
 template <typename V>
@@ -1066,12 +1070,18 @@ void compute_alphabet(Index& ix) {
   hipStream_t s = ix.stream;
   ix.small.ensure(8192);
   byte_hist_range(ix, 0, ix.n, ix.small.as<unsigned long long>());
-  uint64_t h[256];
-  HK_HIP(hipMemcpyAsync(h, ix.small.p, 256 * 8, hipMemcpyDeviceToHost, s));
+  // both read-backs land in pinned slots (a pageable destination costs a staged, synchronous copy each)
+  ix.small_host.ensure(8192 + 128);
+  uint8_t* const hs = ix.small_host.as<uint8_t>();
+  if (ix.geom_ev) HK_HIP(hipEventSynchronize(ix.geom_ev));   // (the staging below 2048 is not the upload's)
+  HK_HIP(hipMemcpyAsync(hs, ix.small.p, 256 * 8, hipMemcpyDeviceToHost, s));
   // the text's last bytes (the keyed geometry's short suffixes) in the same round trip
   const uint64_t nt = std::min<uint64_t>(ix.n, 70);
-  if (nt) HK_HIP(hipMemcpyAsync(ix.tail, ix.text.as<uint8_t>() + (ix.n - nt), nt, hipMemcpyDeviceToHost, s));
+  if (nt) HK_HIP(hipMemcpyAsync(hs + 8192, ix.text.as<uint8_t>() + (ix.n - nt), nt, hipMemcpyDeviceToHost, s));
   HK_HIP(hipStreamSynchronize(s));
+  if (nt) memcpy(ix.tail, hs + 8192, nt);
+  uint64_t h[256];
+  memcpy(h, hs, sizeof(h));
   ix.tail_valid = nt > 0;
   set_alphabet(ix, h);
 }

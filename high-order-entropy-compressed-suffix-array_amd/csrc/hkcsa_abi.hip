@@ -223,7 +223,9 @@ void hkcsa_free(hkcsa_index* h) {
   (void)hipStreamSynchronize(h->ix.stream);
   if (h->ix.aux_stream) (void)hipStreamSynchronize(h->ix.aux_stream);
   hipStream_t s = h->ix.stream, a = h->ix.aux_stream;
+  hipEvent_t ge = h->ix.geom_ev;
   delete h;
+  if (ge) (void)hipEventDestroy(ge);
   if (s) (void)hipStreamDestroy(s);
   if (a) (void)hipStreamDestroy(a);
 }
