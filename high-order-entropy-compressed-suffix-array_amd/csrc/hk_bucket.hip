@@ -2561,10 +2561,16 @@ uint64_t sort_bucket_items(Index& ix, const BucketPlan& plan, const uint64_t* ke
                 "scatter %.0f, small bins %.0f, listed bins %.0f, stage+out %.0f\n", (size_t)nn, acc[0] / nn, acc[1] / nn,
                 acc[2] / nn, acc[3] / nn, acc[4] / nn, acc[5] / nn, acc[6] / nn);
       }
-      unsigned int nfb = 0;
-      HK_HIP(hipMemcpyAsync(&nfb, fbn, 4, hipMemcpyDeviceToHost, s));
+      // the fallback count and the tie count in one round trip (pinned slots); the tie count is read
+      // again below only when fallback items ran
+      uint64_t* const rbh = ix.rb();
+      rbh[1] = 0;
+      HK_HIP(hipMemcpyAsync(rbh + 1, fbn, 4, hipMemcpyDeviceToHost, s));
+      HK_HIP(hipMemcpyAsync(rbh, ix.ties_n.p, 8, hipMemcpyDeviceToHost, s));
       HK_HIP(hipStreamSynchronize(s));
+      const unsigned int nfb = (unsigned int)rbh[1];
       ix.info[8] += nfb;   // items sorted by the LSD passes (a bin over BF_MAXBIN, or wide local keys)
+      if (!nfb && !nw) return rbh[0];
       if (nfb) {
         if (pk) unpack_items(ix, *pk, keys, ix.bk_fb.as<uint2>(), nfb);
         k_bucket_sort<false, false, V><<<nfb, BS_T, 0, s>>>(
