@@ -4,7 +4,7 @@ cd "$GRAFT_REPO_ROOT" && mkdir -p gpurun_out && export TMPDIR=/tmp
 ( while sleep 60; do date >> gpurun_out/heartbeat.log; done ) &
 HB=$!
 trap "kill $HB 2>/dev/null" EXIT
-timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_scale.py tests/test_gpu_dropin.py -m gpu -x -q --timeout 200 --timeout-method thread -k "${K:-shard or strong or weak or replic}" > gpurun_out/sl_tests.log 2>&1 || { tail -30 gpurun_out/sl_tests.log; exit 1; }
+timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_scale.py tests/test_gpu_dropin.py -m gpu -x -q --timeout ${PT:-200} --timeout-method thread -k "${K:-shard or strong or weak or replic}" > gpurun_out/sl_tests.log 2>&1 || { tail -30 gpurun_out/sl_tests.log; exit 1; }
 tail -2 gpurun_out/sl_tests.log
 for v in ${AB_VALS:-1 0}; do
   env $AB_VAR=$v timeout -k 10 400 python3 bench.py --strong --steps 3 --warmup 1 --no-cpu-baseline --no-legs --no-eps --no-pcie > gpurun_out/strong_$v.json 2> gpurun_out/strong_$v.err || { tail -5 gpurun_out/strong_$v.err; exit 1; }
