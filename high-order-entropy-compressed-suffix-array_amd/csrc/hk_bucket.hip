@@ -1566,8 +1566,11 @@ __device__ __forceinline__ bool bucket_sort_fast(BfShared<T, I>& sh, uint2 it, c
         const uint32_t s = h ? pr[j] >> 16 : pr[j] & 0xFFFFu;
         const uint32_t c = (h ? nx[j] : pr[j] >> 16) - s;
         const bool some = c - 1u < 2u, two = c == 2;
-        const uint32_t x = some ? sh.buf[s] : 0u;
-        const uint32_t y = two ? sh.buf[s + 1] : x;
+        // unconditional reads (s + 1 <= cnt + 1 stays inside the plane): the loads of all 16 bins issue
+        // back to back instead of one exec-masked branch each
+        const uint32_t x0 = sh.buf[s], y0 = sh.buf[s + 1];
+        const uint32_t x = some ? x0 : 0u;
+        const uint32_t y = two ? y0 : x;
         const uint32_t a = x < y ? x : y, b = x < y ? y : x;
         if (some) sh.aux[a & 0x7FFFu] = (uint16_t)s;
         if (two) sh.aux[b & 0x7FFFu] = (uint16_t)(s + 1);
@@ -1647,7 +1650,10 @@ __device__ __forceinline__ bool bucket_sort_fast(BfShared<T, I>& sh, uint2 it, c
     if (c <= 8) {
       uint32_t r[8];
 #pragma unroll
-      for (int q = 0; q < 8; ++q) r[q] = (uint32_t)q < c ? sh.buf[s + q] : ~0u;   // key bits < 2^16: pads rank last
+      for (int q = 0; q < 8; ++q) {   // unconditional reads (s + 7 <= cnt + 3 for c >= 4); pads rank last
+        const uint32_t v = sh.buf[s + q];
+        r[q] = (uint32_t)q < c ? v : ~0u;
+      }
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
         uint32_t below = 0, eq = 0, eqb = 0;
@@ -1714,7 +1720,8 @@ __device__ __forceinline__ bool bucket_sort_fast(BfShared<T, I>& sh, uint2 it, c
   uint32_t fin[IH];
 #pragma unroll
   for (int k = 0; k < I; ++k) {
-    const uint32_t f = ((vmask >> k) & 1u) ? (uint32_t)sh.aux[s0 + 64u * k] : 0u;
+    const uint32_t fa = sh.aux[s0 + 64u * k];   // (unconditional: the slot is inside the plane)
+    const uint32_t f = ((vmask >> k) & 1u) ? fa : 0u;
     if (k < IH) fin[k] = f; else fin[k - IH] |= f << 16;
   }
   __syncthreads();
