@@ -1428,7 +1428,8 @@ struct alignas(16) BfShared {
   static constexpr int BINS = 1 << BITS;
   uint32_t buf[CAP + 4];       // positions by slot, records by bin, positions by final index (+4: section 7)
   uint16_t aux[CAP + 4];       // final index by slot, then prev codes by final index
-  uint32_t H2[BINS / 2];       // u16 bin counters / starts, two per word, zero on entry
+  uint32_t H2[BINS / 2 + 1];   // u16 bin counters / starts, two per word, zero on entry (+1: the
+                               // reads of a next bin's start past the last bin stay in bounds)
   uint16_t lists[BINS / 2];    // listed bins (first half), tied records (second half)
   uint32_t wloc[2 * (T / 64)];
   uint32_t wsum[4];
@@ -1557,7 +1558,8 @@ __device__ __forceinline__ bool bucket_sort_fast(BfShared<T, I>& sh, uint2 it, c
     for (int j = 0; j < BF_BINS / 2 / T; ++j) {
       const uint32_t m = tid + T * j;   // bins 2m, 2m + 1
       pr[j] = H2[m];
-      nx[j] = m + 1 < (uint32_t)BF_BINS / 2 ? (H2[m + 1] & 0xFFFFu) : cnt;
+      const uint32_t nw = H2[m + 1];   // (unconditional; the last bin's end is the item's count)
+      nx[j] = m + 1 < (uint32_t)BF_BINS / 2 ? (nw & 0xFFFFu) : cnt;
     }
 #pragma unroll
     for (int j = 0; j < BF_BINS / 2 / T; ++j) {
@@ -1645,7 +1647,8 @@ __device__ __forceinline__ bool bucket_sort_fast(BfShared<T, I>& sh, uint2 it, c
   }
   for (uint32_t i = tid; i < nbig4; i += T) {
     const uint32_t bn = blist[BF_BIGCAP - 1 - i];
-    const uint32_t s = H[bn], e = bn + 1 < (uint32_t)BF_BINS ? (uint32_t)H[bn + 1] : cnt;
+    const uint32_t hn = H[bn + 1];   // (unconditional read, in bounds by the spare word)
+    const uint32_t s = H[bn], e = bn + 1 < (uint32_t)BF_BINS ? hn : cnt;
     const uint32_t c = e - s;
     if (c <= 8) {
       uint32_t r[8];
