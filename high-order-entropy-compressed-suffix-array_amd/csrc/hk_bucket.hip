@@ -1504,12 +1504,8 @@ __device__ __forceinline__ bool bucket_sort_fast(BfShared<T, I>& sh, uint2 it, c
       tsum += c0 + c1;
     }
   }
-  const uint32_t inc = wave_incl_sum<uint32_t>(tsum);
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    const uint32_t t = __shfl_xor(tmax, o, 64);
-    tmax = t > tmax ? t : tmax;
-  }
+  const uint32_t inc = dpp_incl_sum(tsum);
+  tmax = dpp_reduce_u32(tmax, 0u, [](uint32_t a, uint32_t b) { return a > b ? a : b; });
   uint32_t* const wtot = sh.wloc;    // per-wave totals / maxima
   if (lane == 63) wtot[wv] = inc;
   if (lane == 0) wtot[(T / 64) + wv] = tmax;
@@ -1591,7 +1587,7 @@ __device__ __forceinline__ bool bucket_sort_fast(BfShared<T, I>& sh, uint2 it, c
   {   // wave-aggregated appends of the listed bins: three-record bins from the front of the list,
       // larger ones from its back (so that each loop of section 5 runs one code path per wave)
     const uint32_t nb = __popc(bigm), nb4 = __popc(big4);
-    const uint32_t binc = wave_incl_sum<uint32_t>(nb | (nb4 << 16));   // both counts <= 64 * 16
+    const uint32_t binc = dpp_incl_sum(nb | (nb4 << 16));   // both counts <= 64 * 16
     uint32_t bbase = 0;
     if (lane == 63 && (binc & 0xFFFFu)) bbase = atomicAdd(&nctr[0], binc & 0xFFFFu);
     if (lane == 63 && (binc >> 16)) bbase |= atomicAdd(&nctr[2], binc >> 16) << 16;
@@ -2238,13 +2234,20 @@ __global__ __launch_bounds__(T, (T * I <= 9216 ? 2 : 1) * T / 256) void k_bucket
       vand &= x;
     }
   }
+  if constexpr (X32) {   // u32 fields: DPP reductions (no ds_bpermute round trips)
+    xmin = dpp_reduce_u32(xmin, ~0u, [](uint32_t a, uint32_t b) { return a < b ? a : b; });
+    xmax = dpp_reduce_u32(xmax, 0u, [](uint32_t a, uint32_t b) { return a > b ? a : b; });
+    vor = dpp_reduce_u32(vor, 0u, [](uint32_t a, uint32_t b) { return a | b; });
+    vand = dpp_reduce_u32(vand, ~0u, [](uint32_t a, uint32_t b) { return a & b; });
+  } else {
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    const XT a0 = __shfl_xor(xmin, o, 64), a1 = __shfl_xor(xmax, o, 64);
-    xmin = a0 < xmin ? a0 : xmin;
-    xmax = a1 > xmax ? a1 : xmax;
-    vor |= __shfl_xor(vor, o, 64);
-    vand &= __shfl_xor(vand, o, 64);
+    for (int o = 32; o > 0; o >>= 1) {
+      const XT a0 = __shfl_xor(xmin, o, 64), a1 = __shfl_xor(xmax, o, 64);
+      xmin = a0 < xmin ? a0 : xmin;
+      xmax = a1 > xmax ? a1 : xmax;
+      vor |= __shfl_xor(vor, o, 64);
+      vand &= __shfl_xor(vand, o, 64);
+    }
   }
   XT* const red = reinterpret_cast<XT*>(sh.red);   // [4][(T / 64)]
   if (lane == 0) {

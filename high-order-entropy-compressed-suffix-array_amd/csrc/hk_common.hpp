@@ -52,6 +52,27 @@ __device__ __forceinline__ T wave_incl_sum(T v) {
   return v;
 }
 
+// DPP forms (gfx9 row_shr / row_bcast, no LDS traffic): the inclusive wave64 prefix sum of u32, and
+// u32 all-lane reductions (the result read from lane 63, wave-uniform).  The shuffles above go through
+// ds_bpermute and queue behind the LDS traffic of a co-resident workgroup.
+template <typename Op>
+__device__ __forceinline__ uint32_t dpp_scan_u32(uint32_t v, uint32_t id, Op op) {
+  v = op(v, (uint32_t)__builtin_amdgcn_update_dpp((int)id, (int)v, 0x111, 0xf, 0xf, false));   // row_shr:1
+  v = op(v, (uint32_t)__builtin_amdgcn_update_dpp((int)id, (int)v, 0x112, 0xf, 0xf, false));   // row_shr:2
+  v = op(v, (uint32_t)__builtin_amdgcn_update_dpp((int)id, (int)v, 0x114, 0xf, 0xf, false));   // row_shr:4
+  v = op(v, (uint32_t)__builtin_amdgcn_update_dpp((int)id, (int)v, 0x118, 0xf, 0xf, false));   // row_shr:8
+  v = op(v, (uint32_t)__builtin_amdgcn_update_dpp((int)id, (int)v, 0x142, 0xa, 0xf, false));   // row_bcast:15
+  v = op(v, (uint32_t)__builtin_amdgcn_update_dpp((int)id, (int)v, 0x143, 0xc, 0xf, false));   // row_bcast:31
+  return v;
+}
+__device__ __forceinline__ uint32_t dpp_incl_sum(uint32_t v) {
+  return dpp_scan_u32(v, 0u, [](uint32_t a, uint32_t b) { return a + b; });
+}
+template <typename Op>
+__device__ __forceinline__ uint32_t dpp_reduce_u32(uint32_t v, uint32_t id, Op op) {
+  return (uint32_t)__builtin_amdgcn_readlane((int)dpp_scan_u32(v, id, op), 63);
+}
+
 template <typename T>
 __device__ __forceinline__ T wave_incl_max(T v) {
   const uint32_t l = lane_id();
