@@ -72,6 +72,11 @@ template <typename Op>
 __device__ __forceinline__ uint32_t dpp_reduce_u32(uint32_t v, uint32_t id, Op op) {
   return (uint32_t)__builtin_amdgcn_readlane((int)dpp_scan_u32(v, id, op), 63);
 }
+// every u32 wave scan takes the DPP form
+template <>
+__device__ __forceinline__ uint32_t wave_incl_sum<uint32_t>(uint32_t v) {
+  return dpp_incl_sum(v);
+}
 
 template <typename T>
 __device__ __forceinline__ T wave_incl_max(T v) {
