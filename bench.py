@@ -18,7 +18,8 @@ N > 1: one process per GPU (torchrun, or spawned here when WORLD_SIZE is unset):
   all-gather only for texts whose ties outlast the chunk refinement).
     default (weak):   N GiB of text on N GPUs (1 GiB of suffixes per GPU);
     --strong:         a fixed --strong-bytes text (default 4 GiB = configs[4]) on N GPUs; at N = 1 a text
-                      with >= 2^32 suffixes is built as several slices one after another on the one GPU.
+                      with >= 2^32 - 1 suffixes is one hkcsa_build_sa call (the library builds it as slices
+                      of ~2^30 suffixes one after another into one full u64 SA / BWT).
   value = all suffixes' MB / max-over-ranks time.  After the timed steps every rank all-gathers the
   SA slices and BWT rows (replicas), builds its wavelet tree and locates its 1/N of the patterns;
   locate_patterns_per_s = all patterns / max-over-ranks time.
@@ -323,14 +324,20 @@ def run_single(args) -> dict:
     t_wt = time_wt(dev, args.wt_reps)
     wt_roof = roofline(dev, WT_KERNELS, leg)
     dev.timing(False)
-    loc = eps = None
+    loc = eps = loc_host = None
     if args.patterns > 0:
         data, offs = pattern_batch(dev, n, args.patterns, args.plen, args.seed + 1)
         loc = time_queries(dev, data, offs, args.query_reps)
+        loc_host = locate_host_leg(dev, data, offs, args.query_reps, loc)
+        log(f"[bench] locate at the host boundary: {loc_host['locate_patterns_per_s']:.3g} patterns/s")
         if args.eps:
             eps = epsilon_leg(dev, n, data, offs, args.query_reps, loc)
     dev.close()
     pcie = pcie_inclusive(n, alpha, args.seed + 7) if args.pcie else None
+    harness = harness_leg(n, args.seed + 8) if args.harness and args.sigma == 4 else None
+    if harness:
+        log(f"[bench] harness: construction {harness['construction_s']:.3f} s, locate by length "
+            f"{harness['locate_s_by_length']}")
     res = {
         "metric": METRIC,
         "value": round(value, 2),
@@ -357,7 +364,7 @@ def run_single(args) -> dict:
         "detail": {"wt_build_ms": round(t_wt * 1e3, 3), "wt_roofline": wt_roof, "locate": loc,
                    "pattern_source": f"uniform substrings of a {PATTERN_WINDOW >> 20} MiB window of the text",
                    "stages_ms_total": stages, "build_info": info[:16], "pcie_inclusive": pcie,
-                   "epsilon": eps},
+                   "epsilon": eps, "locate_host": loc_host, "harness": harness},
     }
     return res
 
@@ -370,10 +377,17 @@ def epsilon_leg(dev, n: int, data, offs, reps: int, full: dict) -> dict:
     from csa.csa import sample_rate
     rate = sample_rate(n, 0.5)
     dev.synchronize()
+    # EnhancedFMIndex.__init__ drops the construction workspace after every build (csa/enhanced_fm_index.py);
+    # timed on its own, then the epsilon part: samples + compaction (SA, BWT array and text released)
+    t0 = time.perf_counter()
+    dev.release_workspace()
+    t_ws = time.perf_counter() - t0
     dev.timing_reset()
     dev.timing(True)
     t0 = time.perf_counter()
     dev.build_samples(rate)
+    dev.synchronize()
+    t_smp = time.perf_counter() - t0
     dev.compact()
     dev.synchronize()
     t_s = time.perf_counter() - t0
@@ -388,6 +402,8 @@ def epsilon_leg(dev, n: int, data, offs, reps: int, full: dict) -> dict:
     log(f"[bench] epsilon=0.5 (rate {rate}): samples+compact {t_s * 1e3:.2f} ms, "
         f"locate {qq['locate_patterns_per_s']:.3g} patterns/s")
     return {"epsilon": 0.5, "sample_rate": rate, "samples_compact_ms": round(t_s * 1e3, 3),
+            "samples_ms": round(t_smp * 1e3, 3), "compact_ms": round((t_s - t_smp) * 1e3, 3),
+            "workspace_release_ms": round(t_ws * 1e3, 3),
             "sample_kernels_ms": smp_ms, "space_bytes": sp,
             "locate_patterns_per_s": qq["locate_patterns_per_s"], "count_patterns_per_s": qq["count_patterns_per_s"],
             "locate_sampled_kernel_ms": round(ms / max(1, l), 4), "occurrences": qq["occurrences"],
@@ -418,6 +434,7 @@ def run_extra_legs(args, res: dict):
                             "roofline": roof, "wt_roofline": wt_roof, "stages_ms_total": stages,
                             "build_info": info[:16]}
         log(f"[bench] sigma256 leg: {legs['sigma256']['ms_per_step']} ms/step, WT {t_wt * 1e3:.2f} ms")
+    legs["english_like_200MiB"] = english_leg(args)
     n = 200 * (1 << 20) + 1
     dev, wall = build_leg(PRINTABLE, n, args.leg_steps, 1, args.seed + 20)
     dev.timing_reset()
@@ -441,6 +458,104 @@ def run_extra_legs(args, res: dict):
     res["detail"]["legs"] = legs
 
 
+def english_leg(args) -> dict:
+    """configs[2]'s shape without its corpus (english.200MB is absent offline): 200 MiB of seeded
+    natural-language-like latin-1 text (utils/textgen.py: Zipf words, punctuation, 25 % verbatim copies of
+    50 - 5000 symbols plus a few of 64 KiB - 1 MiB), generated on the host (untimed) and uploaded; SA + BWT
+    steps with the refinement / prefix-doubling stage times, the WT, 1M batched 20-symbol count()."""
+    from hkcsa import DeviceIndex
+    from utils.textgen import english_like_text
+    n = 200 * (1 << 20) + 1
+    t0 = time.perf_counter()
+    text = english_like_text(n, seed=args.seed + 30)
+    gen_s = time.perf_counter() - t0
+    dev = DeviceIndex.from_bytes(text, device=0)
+    del text
+    dev.build_sa()
+    dev.synchronize()
+    dev.timing_reset()
+    dev.timing(True)
+    t0 = time.perf_counter()
+    for _ in range(args.leg_steps):
+        dev.build_sa()
+        dev.build_bwt()
+    dev.synchronize()
+    wall = time.perf_counter() - t0
+    stages = stage_breakdown(dev, BUILD_STAGES)
+    info = dev.build_info()
+    dev.timing_reset()
+    t_wt = time_wt(dev, args.wt_reps)
+    data, offs = pattern_batch(dev, n, args.patterns or 1_000_000, 20, args.seed + 31)
+    dev.timing_reset()
+    qq = time_queries(dev, data, offs, args.query_reps)
+    l, ms, _ = dev.kernel_stats("fm_count")
+    dev.timing(False)
+    dev.close()
+    refine = ("sa_refine_stats", "sa_refine_apply", "sa_refine_keys", "sa_refine_segsort", "radix_onesweep_small",
+              "radix_hist", "radix_onesweep")
+    dbl = ("sa_isa_scatter", "sa_pair_keys", "sa_group_stats", "sa_group_apply")
+    per = lambda names: round(sum(stages.get(k, {}).get("ms", 0.0) for k in names) / args.leg_steps, 3)
+    log(f"[bench] english-like leg: {wall / args.leg_steps * 1e3:.2f} ms/step, refinement {per(refine)} ms, "
+        f"doubling {per(dbl)} ms, count {qq['count_patterns_per_s']:.3g} patterns/s")
+    return {"config": "configs[2] shape (english.200MB absent offline): 200 MiB natural-language-like latin-1 text "
+                      "(utils/textgen.py english_like, seed %d) + '$': SA + BWT steps, WT, batched 20-symbol count()"
+                      % (args.seed + 30),
+            "text_symbols": n, "generate_s": round(gen_s, 2), "steps": args.leg_steps,
+            "ms_per_step": round(wall / args.leg_steps * 1e3, 3),
+            "sa_bwt_MBps": round(args.leg_steps * n / 2**20 / wall, 2),
+            "refinement_ms_per_step": per(refine), "doubling_ms_per_step": per(dbl),
+            "chunk_rounds": info[2] & 0xFFFFFFFF, "doubling_rounds": info[2] >> 32,
+            "tied_after_round": info[9:9 + 24], "wt_build_ms": round(t_wt * 1e3, 3),
+            "full_build_MBps": round(n / 2**20 / (wall / args.leg_steps + t_wt), 2),
+            "count_patterns_per_s": qq["count_patterns_per_s"], "locate_patterns_per_s": qq["locate_patterns_per_s"],
+            "fm_count_kernel_ms": round(ms / max(1, l), 4), "patterns": qq["patterns"], "plen": 20,
+            "stages_ms_total": stages, "build_info": info[:9]}
+
+
+def locate_host_leg(dev, data, offs, reps: int, full: dict) -> dict:
+    """hkcsa_locate_batch at the host boundary: the same patterns from host buffers, CSR offsets and
+    positions back into caller-owned host arrays (tests/benchmark.py:39-52 times csa.locate(p) returning
+    a list; this is its batched C-ABI form).  PCIe copies and the allocations inside the call included."""
+    occ, pos = dev.locate_batch(data, offs)            # warm; also learns the size
+    cap = len(pos)
+    if len(pos) != full["occurrences"]:
+        raise RuntimeError("host-boundary locate disagrees with the device-resident locate")
+    dev.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        occ, pos = dev.locate_batch(data, offs, cap=cap)
+    t = (time.perf_counter() - t0) / reps
+    P = len(offs) - 1
+    return {"patterns": P, "plen": full["plen"], "occurrences": int(len(pos)), "call_s": round(t, 6),
+            "locate_patterns_per_s": round(P / t, 1),
+            "in_bytes": int(data.nbytes + offs.nbytes), "out_bytes": int(occ.nbytes + pos.nbytes),
+            "vs_device_resident": round(P / t / full["locate_patterns_per_s"], 4),
+            "note": "one hkcsa_locate_batch call per batch (cap known): H2D patterns, count, scan, SA gather, "
+                    "D2H offsets + positions into pageable numpy arrays"}
+
+
+def harness_leg(n: int, seed: int, lengths=(5, 10, 50, 100, 500, 1000), iterations: int = 3) -> dict:
+    """The reference harness (tests/benchmark.py:54-89) as utils.benchmark.run_full_benchmark on the
+    bench text (1 GiB iid ACGT, epsilon = 0.5): construction through the str API (codec, upload, SA, BWT, WT,
+    samples, compaction), then `iterations` csa.locate(p) calls per pattern length, each returning a list."""
+    from hkcsa import DeviceIndex
+    from utils.benchmark import run_full_benchmark
+    dev = DeviceIndex.synthetic(n, DNA, seed=seed, device=0)
+    text = dev.text(0, n - 1).tobytes().decode("latin-1")   # the text without the '$' the class appends
+    dev.close()
+    res = run_full_benchmark(text, lengths, iterations, epsilon=0.5, seed=seed, verbose=False)
+    del text
+    gc.collect()
+    return {"text_symbols": n, "epsilon": 0.5, "construction_s": round(res.construction_time, 4),
+            "construction_MBps": round(n / 2**20 / res.construction_time, 2),
+            "device_bytes": int(res.device_bytes),
+            "locate_s_by_length": {int(k): round(v, 6) for k, v in sorted(res.pattern_times.items())},
+            "occurrences_by_length": {int(k): int(v) for k, v in sorted(res.occurrences.items())},
+            "iterations": iterations,
+            "note": "run_full_benchmark(text) over csa.CompressedSuffixArray: per-length mean of csa.locate(p), "
+                    "host str in, Python list out"}
+
+
 # ---------------------------------------------------------------------------- sharded / multi-GPU
 def run_sharded(args, rank: int, world: int, local_rank: int) -> dict | None:
     import torch
@@ -453,18 +568,16 @@ def run_sharded(args, rank: int, world: int, local_rank: int) -> dict | None:
     uid = [comm_unique_id() if rank == 0 else None]
     dist.broadcast_object_list(uid, src=0)
     uid = uid[0]
-    # one slice per rank; a text of >= 2^32 suffixes on one GPU (strong, N = 1) is built as slices of
-    # ~1 GiB one after another (the geometry of every weak-scaling rank)
-    per_gpu = slices_per_gpu(n, world)
-    if per_gpu > 1 and world > 1:
-        raise SystemExit("more than one slice per GPU is supported at N = 1 only")
-    keyed = dev.shard_scheme() == 1 if per_gpu > 1 else None
+    # one slice per rank; at N = 1 a text of >= 2^32 - 1 suffixes is the single-GPU library build
+    # (hkcsa_build_sa: slices of ~2^30 suffixes one after another into one full u64 SA / BWT)
+    single = world == 1 and n >= (1 << 32) - 1
+    per_gpu = max(2, (n + (1 << 29)) >> 30) if single else 1   # (hk_shard.hip slices_for)
 
     def step():
-        if per_gpu == 1:
-            dev.build_sa_sharded(uid, world, rank)
+        if single:
+            dev.build_sa()
         else:
-            virtual_slices(dev, per_gpu, keyed=keyed)
+            dev.build_sa_sharded(uid, world, rank)
 
     for _ in range(args.warmup):
         step()
@@ -484,7 +597,7 @@ def run_sharded(args, rank: int, world: int, local_rank: int) -> dict | None:
     el = torch.tensor([t1 - t0], dtype=torch.float64)
     dist.all_reduce(el, op=dist.ReduceOp.MAX)
     wall = float(el.item())
-    lo, hi = dev.shard_range()
+    lo, hi = (0, n) if single else dev.shard_range()
     roof = roofline(dev, ROOF_KERNELS, "", args.traffic_gb)
     if args.traffic_gb is None:   # the PMC summaries in profiles/ are of the single-GPU launches
         roof["traffic"] = None
@@ -494,11 +607,12 @@ def run_sharded(args, rank: int, world: int, local_rank: int) -> dict | None:
     info = dev.build_info()[:16]
     # ---- replicas + batched locate (patterns split P/N over the ranks)
     loc = None
-    if args.patterns > 0 and per_gpu == 1:
+    if args.patterns > 0:
         dev.release_workspace()
         dist.barrier()
         t0 = time.perf_counter()
-        dev.shard_replicate()
+        if not single:
+            dev.shard_replicate()
         dev.synchronize()
         t_rep = time.perf_counter() - t0
         t_wt = time_wt(dev, args.wt_reps)
@@ -535,7 +649,8 @@ def run_sharded(args, rank: int, world: int, local_rank: int) -> dict | None:
             "dtype": "u8",
             "data": "synthetic",
             "config": {"workload": f"{n - 1} iid sigma=4 symbols + '$' sharded over {world} GPUs"
-                                   + (f" ({per_gpu} slices built one after another)" if per_gpu > 1 else "")
+                                   + (f" (one handle: hkcsa_build_sa builds {per_gpu} slices one after another "
+                                      "into the full u64 SA / BWT)" if single else "")
                                    + ": partition histogram + slice counts by RCCL all-reduce, per-rank slice "
                                    "selection, LSD passes over the slice's bucket bits, LDS bucket sorts, tie "
                                    "refinement, RCCL all-gather of per-rank status (ISA rank exchange only for "
@@ -549,38 +664,6 @@ def run_sharded(args, rank: int, world: int, local_rank: int) -> dict | None:
         }
     dev.close()
     return res
-
-
-def slices_per_gpu(n: int, world: int) -> int:
-    """1, or at N = 1 for a text with >= 2^32 suffixes, slices of about 2^30 suffixes."""
-    if world > 1 or n < (1 << 32) - 1:
-        return 1
-    return max(2, int(round(n / (1 << 30))))
-
-
-def virtual_slices(dev, k: int, on_slice=None, keyed=None):
-    """One GPU builds all k slices of a sharded build one after another (host-driven phases).  Only
-    used when the text has >= 2^32 suffixes on a single GPU; the bench text is iid, so no slice is left
-    tied after its chunk rounds (checked).  on_slice(r) runs after slice r is built (parity tests read
-    the slice there).  Keyed coarse scheme (keyed=True, dev.shard_scheme() == 1): the exact histogram
-    of the whole text is the global one, so the slice bounds are its prefix sums at the splitters (the
-    rule of build_sa_sharded's keyed phase 1) and no per-slice block is counted again."""
-    from hkcsa.shard import split_buckets
-    if keyed is None:
-        keyed = dev.shard_scheme() == 1
-    if keyed:
-        g = dev.shard_histogram(1, 0)
-        cum = np.concatenate(([0], np.cumsum(g, dtype=np.uint64)))
-        below = np.array([cum[b] for b in split_buckets(g, k, aligned=True)], dtype=np.uint64)
-    else:
-        g = sum(dev.shard_histogram(k, r) for r in range(k))
-        below = sum(dev.shard_counts(g, k, r) for r in range(k))
-    for r in range(k):
-        dev.shard_build(g, below, k, r)
-        if dev.shard_status()[2]:
-            raise RuntimeError("virtual slices need a text without ties left after the chunk rounds")
-        if on_slice is not None:
-            on_slice(r)
 
 
 # ---------------------------------------------------------------------------- launch
@@ -680,6 +763,8 @@ def parse_args(argv=None):
                     help="skip the epsilon=0.5 compact-mode leg (samples + LF-walk locate) at N = 1")
     ap.add_argument("--no-pcie", dest="pcie", action="store_false",
                     help="skip the host-buffer (PCIe-inclusive) build after the timed steps")
+    ap.add_argument("--no-harness", dest="harness", action="store_false",
+                    help="skip run_full_benchmark (the reference harness) on the 1 GiB text at N = 1")
     ap.add_argument("--sharded", action="store_true", help="use the sharded (multi-GPU) build even at N=1")
     ap.add_argument("--strong", action="store_true", help="fixed text of --strong-bytes over the N GPUs")
     ap.add_argument("--strong-bytes", type=int, default=1 << 32)

@@ -18,7 +18,7 @@ from collections.abc import Mapping, Sequence
 
 import numpy as np
 
-from hkcsa import DeviceIndex, TextCodec
+from hkcsa import DeviceIndex, TextCodec, pack_patterns
 
 
 class OccColumn(Sequence):
@@ -134,7 +134,8 @@ class EnhancedFMIndex:
         send_idx = [i for i, e in enumerate(enc) if e is not None]
         out = [[] for _ in enc]
         if send_idx:
-            offs, pos = self._dev.locate([enc[i] for i in send_idx])
+            data, poffs = pack_patterns([enc[i] for i in send_idx])
+            offs, pos = self._dev.locate_batch(data, poffs)   # hkcsa_locate_batch: host in, host out
             for k, i in enumerate(send_idx):
                 out[i] = [int(x) for x in pos[offs[k]:offs[k + 1]]]
         return out

@@ -2516,13 +2516,11 @@ uint64_t sort_bucket_items(Index& ix, const BucketPlan& plan, const uint64_t* ke
   }
   {
     TimedLaunch t(ix.timer, "sa_bucket_sort", (double)(m - plan.big_total) * (pk ? 8 + 4 + 1 : 8 + 4 + 4 + 1));
-    static const bool trace = getenv("HKCSA_BS_TRACE") != nullptr;   // diagnostic phase stamps
-    // HKCSA_BS_FAST=0: the three stable LSD passes everywhere (A/B diagnostic)
-    static const int fast = getenv("HKCSA_BS_FAST") ? atoi(getenv("HKCSA_BS_FAST")) : 1;
+    // HKCSA_BS_TRACE=1: the phase-stamped build of the fast sort (diagnostic; identical results, tested)
+    const bool trace = getenv("HKCSA_BS_TRACE") != nullptr;
     const unsigned grid_n = (unsigned)nn, grid_w = (unsigned)nw;
     DevBuf tbuf;
-    if (trace && nn) tbuf.ensure(nn * 64 + 64);
-    if (nn && fast) {
+    if (nn) {
       if (trace) tbuf.ensure(nn * 64 + 64);
       ix.bk_fb.ensure(nn * sizeof(uint2) + 16);
       unsigned int* fbn = reinterpret_cast<unsigned int*>(ix.small.as<uint8_t>() + 4352);   // small+4352: fallback count
@@ -2590,16 +2588,6 @@ uint64_t sort_bucket_items(Index& ix, const BucketPlan& plan, const uint64_t* ke
             lkeys, lvals, ix.bk_fb.as<uint2>(), pb, sb, lhb, symbias, d_inv, sa, bwt, ix.ties_k.as<uint64_t>(),
             ix.ties_v.as<V>(), ix.ties_n.as<unsigned long long>(), nullptr);
       }
-    } else if (nn) {
-      if (pk) unpack_items(ix, *pk, keys, ix.bk_items.as<uint2>(), (uint32_t)nn);
-      if (trace && sizeof(V) == 4)
-        k_bucket_sort<false, true, V><<<grid_n, BS_T, 0, s>>>(
-            lkeys, lvals, ix.bk_items.as<uint2>(), pb, sb, lhb, symbias, d_inv, sa, bwt, ix.ties_k.as<uint64_t>(),
-            ix.ties_v.as<V>(), ix.ties_n.as<unsigned long long>(), tbuf.as<uint64_t>());
-      else
-        k_bucket_sort<false, false, V><<<grid_n, BS_T, 0, s>>>(
-            lkeys, lvals, ix.bk_items.as<uint2>(), pb, sb, lhb, symbias, d_inv, sa, bwt, ix.ties_k.as<uint64_t>(),
-            ix.ties_v.as<V>(), ix.ties_n.as<unsigned long long>(), nullptr);
     }
     if (nw) {
       if (pk) unpack_items(ix, *pk, keys, ix.bk_items.as<uint2>() + nn, (uint32_t)nw);
@@ -2608,20 +2596,6 @@ uint64_t sort_bucket_items(Index& ix, const BucketPlan& plan, const uint64_t* ke
           ix.ties_v.as<V>(), ix.ties_n.as<unsigned long long>(), nullptr);
     }
     HK_HIP(hipGetLastError());
-    if (trace && nn && !fast && sizeof(V) == 4) {
-      std::vector<uint64_t> h(nn * 8);
-      HK_HIP(hipMemcpyAsync(h.data(), tbuf.p, h.size() * 8, hipMemcpyDeviceToHost, s));
-      HK_HIP(hipStreamSynchronize(s));
-      double acc[7] = {0, 0, 0, 0, 0, 0, 0};
-      for (size_t w = 0; w < nn; ++w) {
-        for (int i = 0; i < 5; ++i) acc[i] += (double)(h[w * 8 + i + 1] - h[w * 8 + i]);
-        acc[5] += (double)(h[w * 8 + 6] - h[w * 8 + 1]);
-        acc[6] += (double)(h[w * 8 + 7] - h[w * 8 + 6]);
-      }
-      fprintf(stderr, "[bucket_sort trace] %zu WGs, mean cycles: load %.0f, passes %.0f (pass 0: rank %.0f, "
-              "scan %.0f), ties %.0f, stage %.0f, out %.0f\n", (size_t)nn, acc[0] / nn, acc[1] / nn, acc[5] / nn,
-              acc[6] / nn, acc[2] / nn, acc[3] / nn, acc[4] / nn);
-    }
   }
   uint64_t* const h = ix.rb();
   HK_HIP(hipMemcpyAsync(h, ix.ties_n.p, 8, hipMemcpyDeviceToHost, s));
@@ -2839,11 +2813,9 @@ SliceBins slice_bins(uint64_t m, const KeyGeom& kg, int hb, uint64_t kmin, uint6
 int cursor_partition(Index& ix, uint64_t n, int D, int bitlo, uint64_t kbias, const TextKeySrc* tks, uint64_t* kp[2],
                      uint32_t* vp[2], std::vector<uint64_t>& hist, PackedRecs* pk = nullptr);
 
-// the cursor partition groups buckets wherever D <= 16 (HKCSA_CURSOR=0: the stable onesweep passes)
-static bool cursor_enabled() {
-  static const bool on = !getenv("HKCSA_CURSOR") || atoi(getenv("HKCSA_CURSOR")) != 0;
-  return on;
-}
+// the cursor partition groups buckets wherever D <= 16 (lookback-free; the stable onesweep passes
+// remain for texts without whole-symbol buckets)
+static bool cursor_enabled() { return true; }
 
 template <typename V>
 bool bucket_sort_slice(Index& ix, const KeyGeom& kg, uint64_t m, int hb, const SliceBins& bins, const uint64_t* d_h0) {
@@ -2990,9 +2962,6 @@ int cursor_partition(Index& ix, uint64_t n, int D, int bitlo, uint64_t kbias, co
   uint32_t* d_spanc = d_part + (uint64_t)nspan * stride;
   unsigned long long* d_drain = ix.bk_hist.as<unsigned long long>();
   uint64_t* d_hist = ix.bk_hist.as<uint64_t>() + nb;
-  static const bool addr_dbg = getenv("HKCSA_CP_ADDR") != nullptr;   // diagnostic: buffer placement
-  if (addr_dbg)
-    fprintf(stderr, "[cp addr] k0 %p k1 %p v0 %p v1 %p\n", (void*)kp[0], (void*)kp[1], (void*)vp[0], (void*)vp[1]);
   unsigned long long* d_curA = ix.cp_cur.as<unsigned long long>();
   unsigned long long* d_curB = d_curA + (uint64_t)nspan * CP_NAM;
   uint64_t* d_totA = reinterpret_cast<uint64_t*>(d_curB + nb);
@@ -3016,9 +2985,7 @@ int cursor_partition(Index& ix, uint64_t n, int D, int bitlo, uint64_t kbias, co
     tks2.g.pb = pk->g.pb2;
   }
   // pre-pass (exact: 2^17 buckets as two u16 runs over the bucket halves, after a u8 overflow)
-  // pre-pass with the code width and window fixed at compile time (HKCSA_HIST_FIXED=0: runtime)
-  static const bool hist_fixed = !getenv("HKCSA_HIST_FIXED") || atoi(getenv("HKCSA_HIST_FIXED")) != 0;
-  auto hist_fixed_enabled = [] { return hist_fixed; };
+  // pre-pass with the code width and window fixed at compile time where they are 2 bits x 9 / 8 bits x 3
   auto prepass = [&](bool exact) {
     HK_HIP(hipMemsetAsync(d_drain, 0, (uint64_t)nb * 8, s));
     HK_HIP(hipMemsetAsync(d_ovf, 0, 8, s));
@@ -3031,8 +2998,8 @@ int cursor_partition(Index& ix, uint64_t n, int D, int bitlo, uint64_t kbias, co
                                                                      d_ovf);
       } else {
         auto kern = k_bucket_hist_spans<8>;
-        if (hist_fixed_enabled() && lbk == 2 && tks->g.hq == 9) kern = k_bucket_hist_spans<8, -1, 2, 9>;
-        else if (hist_fixed_enabled() && lbk == 8 && tks->g.hq == 3) kern = k_bucket_hist_spans<8, -1, 8, 3>;
+        if (lbk == 2 && tks->g.hq == 9) kern = k_bucket_hist_spans<8, -1, 2, 9>;
+        else if (lbk == 8 && tks->g.hq == 3) kern = k_bucket_hist_spans<8, -1, 8, 3>;
         kern<<<nspan, BH_T, 0, s>>>(tks->text, n, tks->lutk, tks->skey, tks->g, bitlo - tks->g.pb, D, sA, d_part,
                                     d_drain, d_spanc, span, d_ovf);
       }
@@ -3068,24 +3035,10 @@ int cursor_partition(Index& ix, uint64_t n, int D, int bitlo, uint64_t kbias, co
     TimedLaunch t(ix.timer, tks ? "radix_part_text" : "radix_part_keys",
                   (double)n * (packed ? 1 + 8 : tks ? 1 + 8 + 4 : 2 * (8 + 4)));
     const unsigned grid = (unsigned)(8 * ceil_div(nspan, 8u) * (span / CP_TILE));
-    // packed: 512-thread tiles, two workgroups per CU (HKCSA_PK_A1024=1: 1024-thread tiles, one per CU)
-    static const bool a1024 = getenv("HKCSA_PK_A1024") && atoi(getenv("HKCSA_PK_A1024")) != 0;
-    // consecutive positions per thread in the packed radix-2^2 pass A (HKCSA_CONSEC=0: lane-strided)
-    static const bool consec = !getenv("HKCSA_CONSEC") || atoi(getenv("HKCSA_CONSEC")) != 0;
-    const unsigned grid_pk = (unsigned)(8 * ceil_div(nspan, 8u) * (span / (1024 * CP_I)));
-    if (packed && a1024 && tks->g.lb == 2)
-      k_cpart<0, 2, 512, 1024, true><<<grid_pk, 1024, 0, s>>>(nullptr, nullptr, kp[outA], nullptr, n, bitlo2 + sA, 0,
-                                                             d_curA, nullptr, nullptr, span, tks2, pk->g.pbits, d_ovf);
-    else if (packed && a1024)
-      k_cpart<0, 0, 512, 1024, true><<<grid_pk, 1024, 0, s>>>(nullptr, nullptr, kp[outA], nullptr, n, bitlo2 + sA, 0,
-                                                             d_curA, nullptr, nullptr, span, tks2, pk->g.pbits, d_ovf);
-    else if (packed && tks->g.lb == 2 && consec)
+    // packed: 512-thread tiles, two workgroups per CU; radix 2^2: 16 consecutive positions per thread
+    if (packed && tks->g.lb == 2)
       k_cpart<0, 2, 512, CP_T, true><<<grid, CP_T, 0, s>>>(nullptr, nullptr, kp[outA], nullptr, n, bitlo2 + sA, 0,
                                                           d_curA, nullptr, nullptr, span, tks2, pk->g.pbits, d_ovf);
-    else if (packed && tks->g.lb == 2)
-      k_cpart<0, 2, 512, CP_T, true, false><<<grid, CP_T, 0, s>>>(nullptr, nullptr, kp[outA], nullptr, n,
-                                                                 bitlo2 + sA, 0, d_curA, nullptr, nullptr, span, tks2,
-                                                                 pk->g.pbits, d_ovf);
     else if (packed)
       k_cpart<0, 0, 512, CP_T, true><<<grid, CP_T, 0, s>>>(nullptr, nullptr, kp[outA], nullptr, n, bitlo2 + sA, 0,
                                                           d_curA, nullptr, nullptr, span, tks2, pk->g.pbits, d_ovf);
@@ -3135,8 +3088,7 @@ int cursor_partition(Index& ix, uint64_t n, int D, int bitlo, uint64_t kbias, co
   if (tsum != n || hsum != n) throw ApiError{-7, "cursor partition: bucket counts do not cover the text"};
   if (D > 8) {
     // 9-bit digits: 1024-thread tiles (twice the run length per digit)
-    static const bool big_b = !getenv("HKCSA_CP_B1024") || atoi(getenv("HKCSA_CP_B1024")) != 0;
-    const uint64_t btile = sA > 8 && big_b ? 1024 * CP_I : CP_TILE;
+    const uint64_t btile = sA > 8 ? 1024 * CP_I : CP_TILE;
     const uint64_t maxl = deal_regions(ix, totA, ndA, btile, h_gtab, d_gtab);
     TimedLaunch t(ix.timer, "radix_part", (double)n * 2 * (packed ? 8 : 8 + 4));
     if (packed)
@@ -3248,11 +3200,9 @@ void shard_coarse_hist(Index& ix, uint64_t lo, uint64_t hi, uint64_t* d_hist) {
   // (k_slice_hist_spans REG, the whole sym space as one slice of 2^16 bins: the 16-bit window's top
   // bits) over 4 MiB spans of the block with undrained u8 counters; a wrap raises the flag and the
   // exact u16 count below runs in its place (device-side: it returns at once when the flag is clear).
-  // HKCSA_COARSE_REG=0 keeps the u16 count only (A/B).
-  static const bool creg = !getenv("HKCSA_COARSE_REG") || atoi(getenv("HKCSA_COARSE_REG")) != 0;
   SliceSel rs;
   const unsigned long long* only_if = nullptr;
-  if (creg && lb == 2 && lo <= kg.s_start && reg_tables(kg, rs)) {
+  if (lb == 2 && lo <= kg.s_start && reg_tables(kg, rs)) {
     rs.base = 0;
     rs.nb = 65536;
     rs.DB = 16;
@@ -3364,11 +3314,9 @@ SlicePlan plan_slice(Index& ix, uint32_t c_lo, uint32_t c_hi, bool u64pos) {
     while ((1ull << pb2) < kg0.Rk) ++pb2;
     pb2 = std::min(pb2, kg0.pb);
   }
-  // HKCSA_SLICE_PACKED=0: key / value planes (A/B)
-  static const bool pk_env = !getenv("HKCSA_SLICE_PACKED") || atoi(getenv("HKCSA_SLICE_PACKED")) != 0;
   // the fallback key planes of packed records keep >= 1 position bit below the key for a u64 SA
   const int uhb = u64pos ? std::max(1, pbits - 32) : 0;
-  bool packed = pk_env;
+  bool packed = true;
   KeyGeom kk;
   int f = 0;
   if (packed) {
@@ -3423,8 +3371,7 @@ SlicePlan plan_slice(Index& ix, uint32_t c_lo, uint32_t c_hi, bool u64pos) {
   // register kernels (radix 2^2, packed): a 3-bit field of the byte that separates the keyed bytes
   // indexes an 8-entry table of their codes (every byte the scans key is keyed: the unkeyed terminal
   // only ends short suffixes, which take their boundary keys)
-  static const bool reg_env = !getenv("HKCSA_SLICE_REG") || atoi(getenv("HKCSA_SLICE_REG")) != 0;
-  if (reg_env && packed && lb == 2) P.reg = reg_tables(kk, sl);
+  if (packed && lb == 2) P.reg = reg_tables(kk, sl);
   return P;
 }
 
@@ -3515,7 +3462,7 @@ static int cursor_partition_slice(Index& ix, const SlicePlan& P, const TextKeySr
     const unsigned grid = (unsigned)(8 * ceil_div(nspan, 8u) * (span / U));
     void* vo = P.packed ? nullptr : (void*)vp[outA];
     const unsigned long long* skip = D > 16 ? d_ovf : nullptr;
-    static const bool trace = getenv("HKCSA_SL_TRACE") != nullptr;   // diagnostic phase stamps
+    const bool trace = getenv("HKCSA_SL_TRACE") != nullptr;   // diagnostic phase stamps (identical results, tested)
     if (P.reg) {
       if (trace) {
         DevBuf tb;
@@ -3737,16 +3684,14 @@ void build_sa_bucketed(Index& ix) {
   const KeyChunks kch = key_chunks(kg.Rk, kg.q);
   KeyedArgs ka{kg.Rk, kch.Rck, kch.Rlast, kg.s_start, kg.q, kch.ck, kg.pb, 0};
   // half items: one more bucket bit and 9216-suffix items sorted by 512-thread workgroups, two per
-  // CU (the cursor pre-pass takes ceil((D + 1) / lb) symbols and drops the excess low bits);
-  // HKCSA_HALF_ITEMS=0 keeps 18 432-suffix items (A/B)
-  static const bool half_env = !getenv("HKCSA_HALF_ITEMS") || atoi(getenv("HKCSA_HALF_ITEMS")) != 0;
+  // CU (the cursor pre-pass takes ceil((D + 1) / lb) symbols and drops the excess low bits)
   int item_T = 1024;
   {
     // first hq symbols are exactly the top D bits when Rk = 2^k, k | D and no short key exceeds Rk^q - 1
     const int lb = (kg.Rk & (kg.Rk - 1)) == 0 ? __builtin_ctzll(kg.Rk) : 0;
     const bool whole = lb && sb == lb * kg.q;
     const int hq1 = lb ? (D + 1 + lb - 1) / lb : 0;
-    if (half_env && cursor_enabled() && whole && D > 0 && D + 1 <= 17 && D + 1 <= sb && hq1 * lb <= 32 && hq1 <= 16) {
+    if (cursor_enabled() && whole && D > 0 && D + 1 <= 17 && D + 1 <= sb && hq1 * lb <= 32 && hq1 <= 16) {
       D += 1;
       ka.hq = hq1;
       item_T = 512;
@@ -3807,9 +3752,7 @@ void build_sa_bucketed(Index& ix) {
   int slot = 0;
   bool sorted_by_bucket = false;
   // packed records (section 1b): one u64 per suffix through both passes and the item sorts when the
-  // key bits below pass A's 9-bit digit and the position bits fit 64 (1 GiB DNA: 33 + 31);
-  // HKCSA_PACKED=0 keeps the key and position planes (A/B)
-  static const bool pk_env = !getenv("HKCSA_PACKED") || atoi(getenv("HKCSA_PACKED")) != 0;
+  // key bits below pass A's 9-bit digit and the position bits fit 64 (1 GiB DNA: 33 + 31)
   PackedRecs pkr;
   {
     const int posb = 64 - __builtin_clzll(n - 1);
@@ -3820,7 +3763,7 @@ void build_sa_bucketed(Index& ix) {
       while ((1ull << pb2) < kg.Rk) ++pb2;
       pb2 = std::min(pb2, pb);
     }
-    if (pk_env && use_cp && D == 17 && pb2 + bsh + 8 + posb <= 64) {
+    if (use_cp && D == 17 && pb2 + bsh + 8 + posb <= 64) {
       pkr.g.pbits = posb;
       pkr.g.pb = pb;
       pkr.g.pb2 = pb2;
@@ -3829,10 +3772,9 @@ void build_sa_bucketed(Index& ix) {
         pkr.lutp2[b] = pkr.g.tcode < 0 ? kg.lutp[b] : (kg.kflag[b] ? kg.kdig[b] : 0);
       pkr.kfull = kp[1];
       pkr.vfull = vp[1];
-      // radix 2^2: the register pre-pass over all 2^17 buckets (HKCSA_HIST_REG=0: the LDS-table scan)
-      static const bool hreg = !getenv("HKCSA_HIST_REG") || atoi(getenv("HKCSA_HIST_REG")) != 0;
+      // radix 2^2: the register pre-pass over all 2^17 buckets
       SliceSel& r = pkr.rsl;
-      if (hreg && tks.g.lb == 2 && reg_tables(kg, r)) {
+      if (tks.g.lb == 2 && reg_tables(kg, r)) {
         r.base = 0;
         r.nb = 1u << 17;
         r.DB = 17;

@@ -72,7 +72,10 @@ template <typename Op>
 __device__ __forceinline__ uint32_t dpp_reduce_u32(uint32_t v, uint32_t id, Op op) {
   return (uint32_t)__builtin_amdgcn_readlane((int)dpp_scan_u32(v, id, op), 63);
 }
-// every u32 wave scan takes the DPP form
+// Every u32 wave scan takes the DPP form.  Precondition: the whole wave is active (EXEC = ~0): row_shr
+// with bound_ctrl = 0 reads an inactive source lane as the identity, which breaks the prefix chain, and
+// dpp_reduce_u32 reads lane 63.  Every call site is full-wave (the WT partition, occ lines, slice
+// pre-pass, bucket sort, cursor passes); a divergent caller needs the generic shuffle form instead.
 template <>
 __device__ __forceinline__ uint32_t wave_incl_sum<uint32_t>(uint32_t v) {
   return dpp_incl_sum(v);
@@ -107,22 +110,41 @@ __device__ __forceinline__ void st_agent(uint64_t* p, uint64_t v) {
 inline uint64_t ceil_div(uint64_t a, uint64_t b) { return (a + b - 1) / b; }
 
 // ------------------------------------------------------ device buffers
+// A DevBuf either owns its allocation or is a view into another buffer (owned = false: release() and
+// the destructor leave the memory alone, and an ensure() past the view's size drops the view for an
+// allocation of its own) - the multi-slice build points the slice's SA / BWT at the full arrays.
 struct DevBuf {
   void* p = nullptr;
   size_t bytes = 0;
+  bool owned = true;
   DevBuf() = default;
   DevBuf(const DevBuf&) = delete;
   DevBuf& operator=(const DevBuf&) = delete;
-  DevBuf(DevBuf&& o) noexcept : p(o.p), bytes(o.bytes) { o.p = nullptr; o.bytes = 0; }
+  DevBuf(DevBuf&& o) noexcept : p(o.p), bytes(o.bytes), owned(o.owned) { o.p = nullptr; o.bytes = 0; o.owned = true; }
   DevBuf& operator=(DevBuf&& o) noexcept {
-    if (this != &o) { release(); p = o.p; bytes = o.bytes; o.p = nullptr; o.bytes = 0; }
+    if (this != &o) {
+      release();
+      p = o.p;
+      bytes = o.bytes;
+      owned = o.owned;
+      o.p = nullptr;
+      o.bytes = 0;
+      o.owned = true;
+    }
     return *this;
   }
   ~DevBuf() { release(); }
   void release() {
-    if (p) (void)hipFree(p);
+    if (p && owned) (void)hipFree(p);
     p = nullptr;
     bytes = 0;
+    owned = true;
+  }
+  void view(void* ptr, size_t nbytes) {   // non-owning window [ptr, ptr + nbytes)
+    release();
+    p = ptr;
+    bytes = nbytes;
+    owned = false;
   }
   // grow-only allocation (contents not preserved)
   void ensure(size_t nbytes) {

@@ -14,6 +14,7 @@ constexpr uint32_t kFlagNoSplit = 2u; // ... and sort them as whole u64 values (
 constexpr uint32_t kFlagGlobalSort = 4u; // full LSD sort of the keys (no bucket sorts)
 constexpr uint32_t kFlagMulBins = 8u;    // sharded slices: force multiplicative bucket bins
 constexpr uint32_t kFlagMaxBuckets = 16u; // single GPU: the most bucket bits at any n (diagnostic)
+constexpr uint32_t kFlagSlices = 32u;     // single GPU: the multi-slice build at any n (4 slices; parity tests)
 constexpr int kLineBits = 448;   // 7 data words per 64-B rank line (word 0 = ones before the line)
 
 struct WtTables {                // per level, per dense code (host mirror of the device tables)
@@ -146,6 +147,7 @@ struct Index {
   // sharded construction
   bool sharded = false;
   bool sa_pos64 = false;       // sharded slices of texts with n >= 2^32 hold u64 positions
+  bool slices_local = false;   // build_sa_slices: the slices' doubling updates one local ISA (no exchange)
   uint64_t shard_lo = 0, shard_hi = 0;
   std::vector<uint64_t> shard_bounds;   // SA slice starts of every rank (+ n), from the RCCL build
 
@@ -217,6 +219,10 @@ int shard_sample();
 void shard_get_sa(Index& ix, uint64_t a, uint64_t b, uint64_t* out);
 void shard_get_bwt(Index& ix, uint64_t a, uint64_t b, uint8_t* out);
 void build_sa_sharded(Index& ix, const uint8_t id[128], int nranks, int rank);
+// one GPU, k slices of the final SA built one after another into one full SA / BWT (n >= 2^32 - 1, or
+// kFlagSlices); slices_for(): the slice count build_sa uses
+void build_sa_slices(Index& ix, int k);
+int slices_for(const Index& ix);
 void shard_replicate(Index& ix);                                          // RCCL: full SA + BWT on every rank
 void shard_adopt(Index& ix, const uint64_t* h_sa, const uint8_t* h_bwt);  // host-assembled full SA + BWT
 // host-driven rank exchange of the sharded prefix doubling (hkcsa_shard_status ... hkcsa_shard_round)

@@ -664,7 +664,7 @@ void dbl_round_t(Index& ix, uint64_t K) {
   scan_exclusive_u32_to_u64(ix.sw, ta, ao, nt, true, s);
   scan_exclusive_u32_to_u64(ix.sw, th, ho, nt, true, s);
   uint64_t* pairs = nullptr;
-  if (ix.sharded) {
+  if (ix.sharded && !ix.slices_local) {
     ix.upd.ensure(A * 16 + 16);
     pairs = ix.upd.as<uint64_t>();
   }
@@ -785,9 +785,9 @@ void upload_geometry(Index& ix, const KeyGeom& kg) {
   if (kg.keyed) {   // small+2560 = lutk, +4608 = lutp (u16[256]), +3584 = skey (u64[72]), +7168 = srank (u32[72])
     // +7456 = k2d (u16[256]); the ranges in between (4096: locate / fallback counters, 5120: digit
     // histogram) are reset by their users before use.  Staged in pinned memory: one upload.
-    ix.small_host.ensure(8192 + 128);
-    uint8_t* hs = ix.small_host.as<uint8_t>();
     if (ix.geom_ev) HK_HIP(hipEventSynchronize(ix.geom_ev));   // the previous upload has read the staging
+    ix.small_host.ensure(8192 + 128);   // (after the wait: a regrowth would free the staging in flight)
+    uint8_t* hs = ix.small_host.as<uint8_t>();
     memcpy(hs + 2048, kg.lut, 512);
     memcpy(hs + 3072, kg.inv, 512);
     memcpy(hs + 2560, kg.lutk, 512);
@@ -867,10 +867,8 @@ void refine_loop(Index& ix, const KeyGeom& kg, int cur, uint64_t A, uint64_t gro
       HK_HIP(hipGetLastError());
     }
     // groups of <= SEG_MAX members sorted in place; the global radix sort only when a group is larger
-    // (HKCSA_SEGSORT=0: always the radix sort, for A/B)
-    static const bool seg_env = !getenv("HKCSA_SEGSORT") || atoi(getenv("HKCSA_SEGSORT")) != 0;
     int sl = -1;
-    if (seg_env) {
+    {
       unsigned int* d_big = reinterpret_cast<unsigned int*>(ix.small.as<uint8_t>() + 4356);   // small+4356: flag
       unsigned int h_big = 0;
       HK_HIP(hipMemsetAsync(d_big, 0, 4, s));
@@ -907,7 +905,7 @@ void refine_loop(Index& ix, const KeyGeom& kg, int cur, uint64_t A, uint64_t gro
   ix.dbl.h = h;
   ix.dbl.pending = true;
   if (!allow_doubling) {   // sharded slice: the rank exchange drives the rounds (hk_shard.hip)
-    dbl_emit_groups(ix);
+    if (!ix.slices_local) dbl_emit_groups(ix);   // (one-GPU slices: emitted once the full ISA exists)
     return;
   }
   // single GPU: ISA of every position from the full SA, tied suffixes at their head's slot
@@ -953,7 +951,7 @@ void dbl_emit_groups(Index& ix) {
   auto& st = ix.dbl;
   const uint64_t A = st.A;
   uint64_t* pairs = nullptr;
-  if (ix.sharded) {
+  if (ix.sharded && !ix.slices_local) {
     ix.upd.ensure(A * 16 + 16);
     pairs = ix.upd.as<uint64_t>();
   }
@@ -1071,9 +1069,9 @@ void compute_alphabet(Index& ix) {
   ix.small.ensure(8192);
   byte_hist_range(ix, 0, ix.n, ix.small.as<unsigned long long>());
   // both read-backs land in pinned slots (a pageable destination costs a staged, synchronous copy each)
+  if (ix.geom_ev) HK_HIP(hipEventSynchronize(ix.geom_ev));   // (before any regrowth of the staging)
   ix.small_host.ensure(8192 + 128);
   uint8_t* const hs = ix.small_host.as<uint8_t>();
-  if (ix.geom_ev) HK_HIP(hipEventSynchronize(ix.geom_ev));   // (the staging below 2048 is not the upload's)
   HK_HIP(hipMemcpyAsync(hs, ix.small.p, 256 * 8, hipMemcpyDeviceToHost, s));
   // the text's last bytes (the keyed geometry's short suffixes) in the same round trip
   const uint64_t nt = std::min<uint64_t>(ix.n, 70);
@@ -1087,6 +1085,10 @@ void compute_alphabet(Index& ix) {
 }
 
 void build_sa(Index& ix) {
+  if (ix.n >= 0xFFFFFFFFull || (ix.flags & kFlagSlices)) {   // 64-bit positions: slices (hk_shard.hip)
+    build_sa_slices(ix, slices_for(ix));
+    return;
+  }
   if (!(ix.flags & kFlagGlobalSort)) {
     build_sa_bucketed(ix);
     return;

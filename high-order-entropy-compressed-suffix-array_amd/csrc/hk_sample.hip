@@ -22,6 +22,7 @@
 //   extract(i,j): one lane per sample interval [k·s, (k+1)·s): start at the row of (k+1)·s (the
 //                 row of 0 for the interval ending at n) and emit BWT[row] = T'[p-1] while
 //                 stepping row = LF(row).
+#include <algorithm>
 #include <type_traits>
 
 #include "hk_index.hpp"
@@ -104,6 +105,43 @@ __global__ __launch_bounds__(256) void k_fix_b(const W* __restrict__ sa, uint64_
     uint64_t p = (uint64_t)sa[j] + 1;
     if (p == n) p = 0;
     fix[tmp[p]] = (W)j;
+  }
+}
+
+// The same with few c*-rows (the usual case: c* = the '$' that ends T' occurs once), without the
+// n-entry scratch: pos[k] = SA of the c*-row of rank k, then one workgroup matches each pos[k] - 1
+// against the c* bucket's SA entries held in LDS (fix[k] = the bucket row j with SA[j] = pos[k] - 1).
+constexpr uint64_t kFixSmall = 4096;
+
+template <typename W>
+__global__ __launch_bounds__(256) void k_fix_a_rank(WtView v, const W* __restrict__ sa,
+                                                    const uint8_t* __restrict__ bwt, uint8_t cstar_byte, int cstar,
+                                                    W* __restrict__ pos) {
+  __shared__ QShared q;
+  load_qshared(q, v);
+  const uint64_t n = v.n;
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
+    if (bwt[i] != cstar_byte) continue;
+    uint64_t x = i, y = i;
+    lf_pair(q, cstar, x, y);
+    pos[x - v.Ccode[cstar]] = sa[i];
+  }
+}
+
+template <typename W>
+__global__ __launch_bounds__(1024) void k_fix_b_small(const W* __restrict__ sa, uint64_t n, uint64_t b0, uint32_t cnt,
+                                                      const W* __restrict__ pos, W* __restrict__ fix) {
+  __shared__ W B[kFixSmall];
+  for (uint32_t j = threadIdx.x; j < cnt; j += 1024) B[j] = sa[b0 + j];
+  __syncthreads();
+  for (uint32_t k = threadIdx.x; k < cnt; k += 1024) {
+    const uint64_t p = pos[k];
+    const W want = (W)(p == 0 ? n - 1 : p - 1);
+    for (uint32_t j = 0; j < cnt; ++j)
+      if (B[j] == want) {
+        fix[k] = (W)(b0 + j);
+        break;
+      }
   }
 }
 
@@ -259,18 +297,37 @@ void build_samples_t(Index& ix, uint32_t rate) {
   }
   // exact LF of the c*-rows
   uint8_t last = 0;
-  HK_HIP(hipMemcpyAsync(&last, ix.text.as<uint8_t>() + n - 1, 1, hipMemcpyDeviceToHost, s));
-  HK_HIP(hipStreamSynchronize(s));
+  if (ix.tail_valid) {   // read with the byte histogram
+    last = ix.tail[std::min<uint64_t>(n, 70) - 1];
+  } else {
+    HK_HIP(hipMemcpyAsync(&last, ix.text.as<uint8_t>() + n - 1, 1, hipMemcpyDeviceToHost, s));
+    HK_HIP(hipStreamSynchronize(s));
+  }
   const int cstar = ix.code_of[last];
   const uint64_t cnt = ix.Ccode[cstar + 1] - ix.Ccode[cstar];
   ix.smp_fix.ensure(cnt * sizeof(W) + 16);
-  ix.isa.ensure(n * sizeof(W) + 16);   // scratch: tmp[SA[i]] for the c*-rows
-  {
-    TimedLaunch t(ix.timer, "smp_fix", (double)n * (1 + sizeof(W)) + (double)cnt * 4 * sizeof(W));
-    k_fix_a<W><<<grid_for(n, 256, 8192), 256, 0, s>>>(ix.view(), sa, ix.bwt.as<uint8_t>(), last, cstar,
-                                                      ix.isa.as<W>());
+  if (cnt <= kFixSmall) {   // few c*-rows: a cnt-entry scratch
+    ix.tile_d.ensure(cnt * sizeof(W) + 16);
+    TimedLaunch t(ix.timer, "smp_fix", (double)n * 1 + (double)cnt * 4 * sizeof(W));
+    k_fix_a_rank<W><<<grid_for(n, 256, 8192), 256, 0, s>>>(ix.view(), sa, ix.bwt.as<uint8_t>(), last, cstar,
+                                                           ix.tile_d.as<W>());
     HK_HIP(hipGetLastError());
-    k_fix_b<W><<<grid_for(cnt), 256, 0, s>>>(sa, n, ix.Ccode[cstar], cnt, ix.isa.as<W>(), ix.smp_fix.as<W>());
+    k_fix_b_small<W><<<1, 1024, 0, s>>>(sa, n, ix.Ccode[cstar], (uint32_t)cnt, ix.tile_d.as<W>(), ix.smp_fix.as<W>());
+    HK_HIP(hipGetLastError());
+  } else {
+    // scratch tmp[SA[i]] for the c*-rows: an n-entry buffer of the construction workspace when one is
+    // resident (no allocation), else the ISA buffer
+    W* tmp = nullptr;
+    for (DevBuf* b : {&ix.keys[0], &ix.keys[1], &ix.vals[0], &ix.vals[1], &ix.isa})
+      if (!tmp && b->p && b->bytes >= n * sizeof(W)) tmp = b->as<W>();
+    if (!tmp) {
+      ix.isa.ensure(n * sizeof(W) + 16);
+      tmp = ix.isa.as<W>();
+    }
+    TimedLaunch t(ix.timer, "smp_fix", (double)n * (1 + sizeof(W)) + (double)cnt * 4 * sizeof(W));
+    k_fix_a<W><<<grid_for(n, 256, 8192), 256, 0, s>>>(ix.view(), sa, ix.bwt.as<uint8_t>(), last, cstar, tmp);
+    HK_HIP(hipGetLastError());
+    k_fix_b<W><<<grid_for(cnt), 256, 0, s>>>(sa, n, ix.Ccode[cstar], cnt, tmp, ix.smp_fix.as<W>());
     HK_HIP(hipGetLastError());
   }
   ix.smp_inv.ensure(256);

@@ -963,6 +963,188 @@ void shard_build(Index& ix, const uint64_t* h_global_hist, const uint64_t* h_glo
   }
 }
 
+// ---------------------------------------------------------------- one GPU, several slices
+// The suffix array of a text too long for 32-bit positions (n >= 2^32 - 1: configs[4]'s 4 GiB + 1 on
+// one MI355X; the reference's build_suffix_array has no size limit, csa/suffix_array.py:131-134), or of
+// any text under kFlagSlices: the sharded slice pipeline runs k times on this device, slice r writing
+// straight into its rows of one full SA and BWT (the slice's ix.sa / ix.bwt are views of them).  The
+// slice bounds come from one partition histogram of the whole text (keyed scheme: the exact coarse
+// histogram and balanced / equal-width splitters; else the sampled key histogram and exact counts
+// below the splitters).  Groups still tied after a slice's chunk rounds wait; once every slice is
+// placed, one ISA from the full SA drives prefix doubling over every pending slice, each round at
+// K = the smallest common-prefix length of any of them (the sharded rank exchange's rule) with the ISA
+// updated in place - on one device there is nothing to exchange.
+int slices_for(const Index& ix) {
+  if (ix.n < 0xFFFFFFFFull) return 4;   // kFlagSlices at a 32-bit size (parity tests)
+  const uint64_t k = (ix.n + (1ull << 29)) >> 30;   // ~2^30 suffixes per slice: the 1 GiB pipeline
+  return (int)std::max<uint64_t>(2, std::min<uint64_t>(64, k));
+}
+
+namespace {
+struct PendingSlice {   // a slice whose tied groups wait for the full ISA
+  uint64_t lo = 0, hi = 0;
+  Index::DblState dbl;
+  DevBuf act[2][3], head_slot;
+};
+void swap_pending(Index& ix, PendingSlice& p) {
+  std::swap(ix.dbl, p.dbl);
+  for (int i = 0; i < 2; ++i)
+    for (int j = 0; j < 3; ++j) std::swap(ix.act[i][j], p.act[i][j]);
+  std::swap(ix.head_slot, p.head_slot);
+}
+}  // namespace
+
+void build_sa_slices(Index& ix, int k) {
+  const uint64_t n = ix.n;
+  hipStream_t s = ix.stream;
+  if (k < 1 || k > SH_MAX_RANKS) throw ApiError{-1, "slices: 1 to 64 slices"};
+  ix.have_alpha = false;   // every build recomputes the byte histogram / C (utils/utils.py:16-24)
+  compute_alphabet(ix);
+  ix.have_sa = ix.have_bwt = ix.have_wt = false;
+  ix.dbl = Index::DblState{};
+  const bool w64 = n > 0xFFFFFFFEull || (ix.flags & kFlagPos64);   // shard_build's position width
+  const size_t V = w64 ? 8 : 4;
+  // the full arrays (the previous build's, when the handle holds them)
+  DevBuf full_sa, full_bwt;
+  if (ix.sa.owned) std::swap(full_sa, ix.sa);
+  if (ix.bwt.owned) std::swap(full_bwt, ix.bwt);
+  ix.sa.release();
+  ix.bwt.release();
+  full_sa.ensure(n * V + 16);
+  full_bwt.ensure(n + 64);
+  if (n <= 1) {   // (kFlagSlices on a one-symbol text)
+    HK_HIP(hipMemsetAsync(full_sa.p, 0, V, s));
+    HK_HIP(hipMemcpyAsync(full_bwt.p, ix.text.p, n, hipMemcpyDeviceToDevice, s));
+    HK_HIP(hipStreamSynchronize(s));
+    ix.sa = std::move(full_sa);
+    ix.bwt = std::move(full_bwt);
+    ix.sharded = false;
+    ix.sa_pos64 = w64;
+    ix.info.assign(9, 0);
+    ix.have_sa = ix.have_bwt = true;
+    return;
+  }
+  struct LocalGuard {   // the sharded state and the row views never outlive the call
+    Index& ix;
+    ~LocalGuard() {
+      ix.slices_local = false;
+      ix.sharded = false;
+      for (DevBuf* b : {&ix.sa, &ix.bwt, &ix.vals[0], &ix.vals[1], &ix.keys[0], &ix.keys[1]})
+        if (!b->owned) b->release();
+    }
+  } guard{ix};
+  ix.slices_local = true;
+  // ---- slice bounds
+  const bool keyed = shard_keyed(ix);
+  std::vector<uint64_t> gh(SH_KBUCKETS, 0), below(k + 1, 0);
+  {
+    DevBuf d;
+    d.ensure((SH_KBUCKETS + 1) * 8 + 64);
+    shard_histogram(ix, 1, 0, d.as<uint64_t>());
+    HK_HIP(hipMemcpyAsync(gh.data(), d.p, SH_KBUCKETS * 8, hipMemcpyDeviceToHost, s));
+    HK_HIP(hipStreamSynchronize(s));
+    if (keyed) {
+      const std::vector<uint32_t> B = splitters(gh.data(), k, SH_KBUCKETS, true);
+      uint64_t acc = 0;
+      uint32_t c = 0;
+      for (int r = 0; r <= k; ++r) {
+        while (c < B[r]) acc += gh[c++];
+        below[r] = acc;
+      }
+    } else {
+      std::vector<uint64_t> part(k + 1);
+      for (int r = 0; r < k; ++r) {   // each block's counts below every splitter, summed
+        shard_counts(ix, gh.data(), k, r, d.as<uint64_t>());
+        HK_HIP(hipMemcpyAsync(part.data(), d.p, (k + 1) * 8, hipMemcpyDeviceToHost, s));
+        HK_HIP(hipStreamSynchronize(s));
+        for (int j = 0; j <= k; ++j) below[j] += part[j];
+      }
+    }
+  }
+  if (below[0] != 0 || below[k] != n) throw ApiError{-7, "slices: the partition does not cover the text"};
+  // ---- the slices, one after another
+  std::vector<uint64_t> info(9, 0), ties;
+  std::vector<PendingSlice> pend;
+  auto point = [&](uint64_t lo, uint64_t hi) {   // the slice's SA / BWT rows of the full arrays
+    ix.sa.view(full_sa.as<uint8_t>() + lo * V, (hi - lo) * V + 16);
+    ix.bwt.view(full_bwt.as<uint8_t>() + lo, hi - lo + 64);
+    ix.shard_lo = lo;
+    ix.shard_hi = hi;
+  };
+  for (int r = 0; r < k; ++r) {
+    const uint64_t lo = below[r], hi = below[r + 1];
+    point(lo, hi);
+    void* const rows = ix.sa.p;
+    shard_build(ix, gh.data(), below.data(), k, r);
+    if (ix.shard_lo != lo || ix.shard_hi != hi) throw ApiError{-7, "slices: a slice left its bounds"};
+    if (ix.sa.p != rows) {   // a global-path slice adopted a value buffer as its SA: move the rows over
+      HK_HIP(hipMemcpyAsync(rows, ix.sa.p, (hi - lo) * V, hipMemcpyDeviceToDevice, s));
+      for (int i = 0; i < 2; ++i)
+        if (!ix.vals[i].owned) ix.vals[i] = std::move(ix.sa);
+    }
+    for (int i = 0; i < 2; ++i) {   // no view may stay behind as the next slice's scratch
+      if (!ix.vals[i].owned) ix.vals[i].release();
+      if (!ix.keys[i].owned) ix.keys[i].release();
+    }
+    for (int j : {0, 1, 4, 5, 6}) info[j] += ix.info[j];
+    info[2] = std::max(info[2], ix.info[2]);
+    info[3] = std::max(info[3], ix.info[3]);
+    info[7] |= ix.info[7];
+    info[8] += ix.info[8];
+    for (size_t j = 9; j < ix.info.size(); ++j) {
+      if (ties.size() < j - 8) ties.push_back(0);
+      ties[j - 9] += ix.info[j];
+    }
+    if (ix.dbl.pending) {
+      pend.emplace_back();
+      PendingSlice& p = pend.back();
+      p.lo = lo;
+      p.hi = hi;
+      swap_pending(ix, p);
+    }
+  }
+  // ---- prefix doubling over the slices still tied (repetitive texts)
+  if (!pend.empty()) {
+    ix.sa_pos64 = w64;
+    dbl_ensure_isa(ix);
+    dbl_isa_segment(ix, full_sa.p, n, 0);   // isa[SA[j]] = j over the full (provisional) SA
+    for (auto& p : pend) {   // tied suffixes: their group head's slot
+      swap_pending(ix, p);
+      point(p.lo, p.hi);
+      dbl_emit_groups(ix);
+      swap_pending(ix, p);
+    }
+    ix.info.assign(9, 0);
+    for (int round = 0;; ++round) {
+      if (round > 64) throw ApiError{-7, "slices: prefix doubling did not converge"};
+      uint64_t K = ~0ull;
+      for (auto& p : pend)
+        if (p.dbl.A) K = std::min(K, p.dbl.h);
+      if (K == ~0ull) break;
+      for (auto& p : pend) {
+        if (!p.dbl.A) continue;
+        swap_pending(ix, p);
+        point(p.lo, p.hi);
+        dbl_round(ix, K);
+        swap_pending(ix, p);
+      }
+      info[2] += 1ull << 32;
+    }
+  }
+  HK_HIP(hipStreamSynchronize(s));
+  ix.sa = std::move(full_sa);
+  ix.bwt = std::move(full_bwt);
+  ix.sharded = false;
+  ix.slices_local = false;
+  ix.shard_lo = 0;
+  ix.shard_hi = n;
+  ix.sa_pos64 = w64;
+  ix.dbl = Index::DblState{};
+  ix.info = info;
+  ix.info.insert(ix.info.end(), ties.begin(), ties.end());
+  ix.have_sa = ix.have_bwt = true;
+}
+
 int shard_buckets() { return SH_KBUCKETS; }
 int shard_sample() { return SH_SAMPLE; }
 
@@ -1362,7 +1544,10 @@ void shard_adopt(Index& ix, const uint64_t* h_sa, const uint8_t* h_bwt) {
     HK_HIP(hipMemcpyAsync(full_sa.p, h_sa, n * 8, hipMemcpyHostToDevice, s));
   } else {
     std::vector<uint32_t> t(n);
-    for (uint64_t i = 0; i < n; ++i) t[i] = (uint32_t)h_sa[i];
+    for (uint64_t i = 0; i < n; ++i) {   // (narrowed here: an entry >= n must not wrap into range)
+      if (h_sa[i] >= n) throw ApiError{-4, "adopt: suffix array entry out of range"};
+      t[i] = (uint32_t)h_sa[i];
+    }
     HK_HIP(hipMemcpyAsync(full_sa.p, t.data(), n * 4, hipMemcpyHostToDevice, s));
     HK_HIP(hipStreamSynchronize(s));
   }

@@ -550,11 +550,8 @@ int radix_sort_pairs(SortWork& w, KernelTimer& tm, uint64_t* k[2], V* v[2], int 
   // large sorts: 1024 (key passes) or 512 (text-keyed first pass) threads x 16 keys per tile;
   // small sorts (refinement of tied suffixes): 256 x 16, its own kernel symbol and timer name
   const bool small = n < kSmallSort;
-  // key passes over n >= 2^24 pairs: 1024 x 16 tiles (A/B: pass 2 of the 1 GiB build 6.79 -> 6.61 ms);
-  // HKCSA_OS_SMALL_TILES=1 restores 512 x 16 (diagnostic)
-  static const bool big_tiles = getenv("HKCSA_OS_SMALL_TILES") == nullptr;
-  // the text-keyed first pass keeps 512-thread tiles (its key building is heavier per tile)
-  static const bool text_big = getenv("HKCSA_OS_TEXT_T") && atoi(getenv("HKCSA_OS_TEXT_T")) == 1024;
+  // large key passes: 1024 x 16 tiles (pass 2 of the 1 GiB build 6.79 -> 6.61 ms against 512 x 16); the
+  // text-keyed first pass keeps 512-thread tiles (its key building is heavier per tile)
   const uint64_t tile_elems = small ? 256 * OS_I : OS_TILE;
   const uint64_t big_elems = 1024 * OS_I;
   const uint64_t tiles = ceil_div(n, tile_elems);
@@ -644,11 +641,6 @@ int radix_sort_pairs(SortWork& w, KernelTimer& tm, uint64_t* k[2], V* v[2], int 
               nullptr, nullptr, k[nxt], v[nxt], n, (uint32_t)(bit_lo + 8 * p), w.offs.as<uint64_t>() + p * 256,
               w.status.as<uint64_t>(), w.counters.as<uint32_t>() + p, w.epoch, w.err.as<uint32_t>(), 1,
               has_next ? bit_lo + 8 * (p + 1) : -1, w.hpart.as<unsigned long long>(), *src);
-        else if (src->g.lb == 2 && text_big)   // DNA, 1024-thread tiles (A/B: HKCSA_OS_TEXT_T=1024)
-          k_onesweep<V, 1024, OS_I, 0, 4, true, 2><<<(unsigned)ceil_div(n, big_elems), 1024, 0, s>>>(
-              nullptr, nullptr, k[nxt], v[nxt], n, (uint32_t)(bit_lo + 8 * p), w.offs.as<uint64_t>() + p * 256,
-              w.status.as<uint64_t>(), w.counters.as<uint32_t>() + p, w.epoch, w.err.as<uint32_t>(), 1,
-              has_next ? bit_lo + 8 * (p + 1) : -1, w.hpart.as<unsigned long long>(), *src);
         else if (src->g.lb == 2)   // DNA: packing fully unrolled
           k_onesweep<V, OS_T, OS_I, 0, 4, true, 2><<<(unsigned)tiles, OS_T, 0, s>>>(
               nullptr, nullptr, k[nxt], v[nxt], n, (uint32_t)(bit_lo + 8 * p), w.offs.as<uint64_t>() + p * 256,
@@ -665,14 +657,8 @@ int radix_sort_pairs(SortWork& w, KernelTimer& tm, uint64_t* k[2], V* v[2], int 
             w.offs.as<uint64_t>() + p * 256, w.status.as<uint64_t>(), w.counters.as<uint32_t>() + p, w.epoch,
             w.err.as<uint32_t>(), iota_pending ? 1 : 0, has_next ? bit_lo + 8 * (p + 1) : -1,
             w.hpart.as<unsigned long long>(), TextKeySrc{}, kbias);
-      else if (big_tiles)
-        k_onesweep<V, 1024, OS_I, 0><<<(unsigned)ceil_div(n, big_elems), 1024, 0, s>>>(
-            k[cur], iota_pending ? nullptr : v[cur], k[nxt], v[nxt], n, (uint32_t)(bit_lo + 8 * p),
-            w.offs.as<uint64_t>() + p * 256, w.status.as<uint64_t>(), w.counters.as<uint32_t>() + p, w.epoch,
-            w.err.as<uint32_t>(), iota_pending ? 1 : 0, has_next ? bit_lo + 8 * (p + 1) : -1,
-            w.hpart.as<unsigned long long>(), TextKeySrc{}, kbias);
       else
-        k_onesweep<V, OS_T, OS_I, 0><<<(unsigned)tiles, OS_T, 0, s>>>(
+        k_onesweep<V, 1024, OS_I, 0><<<(unsigned)ceil_div(n, big_elems), 1024, 0, s>>>(
             k[cur], iota_pending ? nullptr : v[cur], k[nxt], v[nxt], n, (uint32_t)(bit_lo + 8 * p),
             w.offs.as<uint64_t>() + p * 256, w.status.as<uint64_t>(), w.counters.as<uint32_t>() + p, w.epoch,
             w.err.as<uint32_t>(), iota_pending ? 1 : 0, has_next ? bit_lo + 8 * (p + 1) : -1,

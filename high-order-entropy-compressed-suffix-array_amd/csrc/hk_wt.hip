@@ -198,7 +198,7 @@ __global__ __launch_bounds__(256) void k_wt_partition(const uint8_t* __restrict_
                                                       const uint64_t* __restrict__ rbase,
                                                       const uint16_t* __restrict__ lut,
                                                       const uint64_t* __restrict__ bspan, uint32_t nbspan,
-                                                      int translate, WtSmall sa, int carry) {
+                                                      int translate, WtSmall sa) {
   __shared__ uint64_t OB[256], RB[256];
   __shared__ uint16_t LU[256];
   __shared__ uint64_t BS[256];
@@ -217,7 +217,7 @@ __global__ __launch_bounds__(256) void k_wt_partition(const uint8_t* __restrict_
   while (bi < nbspan && BS[bi] < t0) ++bi;
   // ones before the wave's first span from its rank line; after that the wave carries the count
   // (its spans are contiguous), so no span waits on a line read, and the next span's symbols are
-  // loaded while this one is partitioned (HKCSA_WT_CARRY=0: a line read per span, no prefetch)
+  // loaded while this one is partitioned (0.76 -> 0.68 ms per 1 GiB level against a line read per span)
   uint64_t onesbase = 0;
   if (t0 < t1) {
     const uint64_t base = t0 * 1024, li0 = base / kLineBits;
@@ -234,22 +234,11 @@ __global__ __launch_bounds__(256) void k_wt_partition(const uint8_t* __restrict_
     const uint64_t j = t * 1024 + lane * 16u;
     return *reinterpret_cast<const uint4*>(S + (j < n ? j : jmax));
   };
-  uint4 vnext = carry && t0 < t1 ? load_span(t0) : make_uint4(0, 0, 0, 0);
+  uint4 vnext = t0 < t1 ? load_span(t0) : make_uint4(0, 0, 0, 0);
   for (uint64_t t = t0; t < t1; ++t) {
     const uint64_t base = t * 1024, j0 = base + lane * 16u;
-    uint4 vv;
-    if (carry) {
-      vv = vnext;
-      vnext = load_span(t + 1 < t1 ? t + 1 : t);
-    } else {
-      vv = load_span(t);
-      const uint64_t li0 = base / kLineBits;
-      const uint32_t wi0 = (uint32_t)(base - li0 * kLineBits) / 64;
-      uint64_t part = 0;
-      if (lane < wi0) part = (uint64_t)__popcll(lines[li0 * 8 + 1 + lane]);
-      else if (lane == 7) part = lines[li0 * 8];
-      onesbase = wave_sum<uint64_t>(part);
-    }
+    const uint4 vv = vnext;
+    vnext = load_span(t + 1 < t1 ? t + 1 : t);
     const uint32_t nv = j0 >= n ? 0u : (n - j0 >= 16 ? 16u : (uint32_t)(n - j0));
     const uint32_t valid = nv == 16 ? 0xFFFFu : (1u << nv) - 1;
     uint32_t bits = 0;
@@ -902,11 +891,10 @@ void build_wt(Index& ix) {
                         hipMemcpyHostToDevice, s));
 
   const uint64_t nlines = n / kLineBits + 1;
-  // two-level 16-ary occ directory for the batched count (8 < sigma; HKCSA_NIB=0: WT walks, for A/B):
+  // two-level 16-ary occ directory for the batched count (8 < sigma):
   // node groups at depth g, their tables, and level 0 from the BWT (level 1 follows the WT partition
   // that writes the depth-g sequence, or the BWT itself for g = 0)
-  static const bool nib_env = !getenv("HKCSA_NIB") || atoi(getenv("HKCSA_NIB")) != 0;
-  const bool nib = nib_env && sigma > 8;
+  const bool nib = sigma > 8;
   const int ng = nib ? std::max(0, L - 4) : 0;
   std::vector<uint8_t> nibh(3072 + 128, 0);   // host source of the table upload (alive to the sync)
   const uint64_t nbl = n / NB_S + 1, nbsb = ceil_div(nbl, (uint64_t)NB_LPS);
@@ -982,9 +970,8 @@ void build_wt(Index& ix) {
     }
     ix.wt_lut.ensure(lutv.size() * 2);
     HK_HIP(hipMemcpyAsync(ix.wt_lut.p, lutv.data(), (size_t)L * 512, hipMemcpyHostToDevice, s));
-    // small alphabets: the SWAR level kernels (HKCSA_WT_SMALL=0 keeps the table path, for A/B)
-    static const bool small_env = !getenv("HKCSA_WT_SMALL") || atoi(getenv("HKCSA_WT_SMALL")) != 0;
-    bool small = small_env && sigma <= 8;
+    // small alphabets: the SWAR level kernels
+    bool small = sigma <= 8;
     int byte_of_code[8] = {0};
     for (int b = 0; b < 256; ++b)
       if (ix.code_of[b] >= 0) {
@@ -993,9 +980,8 @@ void build_wt(Index& ix) {
       }
     WtSmall sml[kMaxLevels];
     memset(sml, 0, sizeof(sml));
-    // sigma = 256: every byte present, dense code = byte, the tree perfect (HKCSA_WT_P2=0: the tables)
-    static const bool p2_env = !getenv("HKCSA_WT_P2") || atoi(getenv("HKCSA_WT_P2")) != 0;
-    for (int d = 0; d < L; ++d) sml[d].p2sh = p2_env && sigma == 256 && L == 8 ? 7 - d : -1;
+    // sigma = 256: every byte present, dense code = byte, the tree perfect: level bits by shifts
+    for (int d = 0; d < L; ++d) sml[d].p2sh = sigma == 256 && L == 8 ? 7 - d : -1;
     for (int d = 0; d < L && small; ++d) {
       for (int c = 0; c < sigma; ++c) {
         const uint32_t bit = T.bit[d][c];
@@ -1025,7 +1011,6 @@ void build_wt(Index& ix) {
     ix.tile_d.ensure(bsp.size() * 8);
     HK_HIP(hipMemcpyAsync(ix.tile_d.p, bsp.data(), bsp.size() * 8, hipMemcpyHostToDevice, s));
     int cur = 0;
-    static const int wt_carry = !getenv("HKCSA_WT_CARRY") || atoi(getenv("HKCSA_WT_CARRY")) != 0;
     const unsigned gb = grid_for(ceil_div(nlines, WT_V), 4, 8192), gp = grid_for(ceil_div(n, 1024), 4, 8192);
     for (int d = 0; d < L; ++d) {
       ix.wt_lines[d].ensure(nlines * 64);
@@ -1055,22 +1040,21 @@ void build_wt(Index& ix) {
           k_wt_partition<true><<<gp, 256, 0, s>>>(in, outp, n, lines, ix.wt_obn.as<uint64_t>() + d * 256,
                                                   ix.wt_rbase.as<uint64_t>() + d * 256,
                                                   ix.wt_lut.as<uint16_t>() + d * 256, ix.tile_d.as<uint64_t>() + d * 256,
-                                                  nbsp[d], d == 0 ? 1 : 0, sml[d], wt_carry);
+                                                  nbsp[d], d == 0 ? 1 : 0, sml[d]);
         else
           k_wt_partition<false><<<gp, 256, 0, s>>>(in, outp, n, lines, ix.wt_obn.as<uint64_t>() + d * 256,
                                                    ix.wt_rbase.as<uint64_t>() + d * 256,
                                                    ix.wt_lut.as<uint16_t>() + d * 256,
-                                                   ix.tile_d.as<uint64_t>() + d * 256, nbsp[d], d == 0 ? 1 : 0, sml[d], wt_carry);
+                                                   ix.tile_d.as<uint64_t>() + d * 256, nbsp[d], d == 0 ? 1 : 0, sml[d]);
         HK_HIP(hipGetLastError());
         if (nib && ng > 0 && d + 1 == ng) nib_level(1, outp, ix.nib_tab.as<uint8_t>() + 768);
         if (d > 0) cur ^= 1;
       }
     }
   }
-  // flat occ directory for the batched count (sigma <= 8; HKCSA_OCC=0: WT walks, for A/B)
-  static const bool occ_env = !getenv("HKCSA_OCC") || atoi(getenv("HKCSA_OCC")) != 0;
+  // flat occ directory for the batched count (sigma <= 8)
   ix.occ_ok = false;
-  if (occ_env && sigma >= 2 && sigma <= 8) {
+  if (sigma >= 2 && sigma <= 8) {
     const uint64_t nl = n / OC_S + 1, nsb = ceil_div(nl, (uint64_t)OC_LPS);
     ix.occ_lines.ensure(nl * 64 + 64);
     ix.occ_sb.ensure(nsb * 64 + 64);   // [8 codes][nsb]
@@ -1087,10 +1071,8 @@ void build_wt(Index& ix) {
   ix.nib_ok = nib;
   // k-mer table for the batched count: K = the most symbols with sigma^K <= 2^20 entries (<= 16 MiB
   // of (l, r) pairs, MALL-resident; DNA + '$': K = 8, printable: 3, bytes: 2), at most 12
-  // (HKCSA_KMER=0: no table, for A/B)
-  static const bool kmer_env = !getenv("HKCSA_KMER") || atoi(getenv("HKCSA_KMER")) != 0;
   ix.kmer_k = 0;
-  if (kmer_env && L > 0 && sigma >= 2) {
+  if (L > 0 && sigma >= 2) {
     int K = 0;
     uint64_t tot = 1;
     const uint64_t cap = ix.occ_ok || ix.nib_ok ? (1ull << 21) : (1ull << 20);   // a directory builds it cheaply

@@ -518,13 +518,32 @@ int hkcsa_count_batch(hkcsa_index* h, const uint8_t* pats, const uint64_t* offs,
   return rc;
 }
 
+// Sizes first (count + scan, no gather); the SA gather runs only when pos_out can hold every
+// position, so a caller with a large enough buffer finishes in one call and a short one gets the
+// CSR offsets with HKCSA_E_RANGE (nothing gathered) and calls again.
 int hkcsa_locate_batch(hkcsa_index* h, const uint8_t* pats, const uint64_t* offs, uint64_t P,
                        uint64_t* occ_offs, uint64_t* pos_out, uint64_t cap) {
   hkcsa_queries* q = nullptr;
   int rc = hkcsa_queries_upload(h, pats, offs, P, &q);
   if (rc) return rc;
-  rc = hkcsa_queries_locate(h, q, nullptr);
-  if (!rc) rc = hkcsa_queries_download(h, q, nullptr, occ_offs, pos_out, pos_out ? cap : 0);
+  rc = guarded([&] {
+    need(occ_offs != nullptr, HKCSA_E_INVALID, "null occ_offs");
+    need(!h->ix.sharded, HKCSA_E_STATE, "sharded index holds only a slice");
+    hipStream_t s = h->ix.stream;
+    hk::query_count(h->ix, q->pats.as<uint8_t>(), q->offs.as<uint64_t>(), q->P, q->lr.as<int64_t>(),
+                    q->cnt.as<uint64_t>());
+    hk::scan_exclusive_u64(h->ix.sw, q->cnt.as<uint64_t>(), q->occ_offs.as<uint64_t>(), q->P, true, s);
+    HK_HIP(hipMemcpyAsync(occ_offs, q->occ_offs.p, (q->P + 1) * 8, hipMemcpyDeviceToHost, s));
+    HK_HIP(hipStreamSynchronize(s));
+    const uint64_t tot = occ_offs[q->P];
+    if (!pos_out) return;
+    need(cap >= tot, HKCSA_E_RANGE, "position buffer too small (occ_offs holds the sizes)");
+    if (!tot) return;
+    q->pos.ensure(tot * 8 + 16);
+    hk::query_locate_gather(h->ix, q->lr.as<int64_t>(), q->occ_offs.as<uint64_t>(), q->P, q->pos.as<uint64_t>());
+    HK_HIP(hipMemcpyAsync(pos_out, q->pos.p, tot * 8, hipMemcpyDeviceToHost, s));
+    HK_HIP(hipStreamSynchronize(s));
+  });
   hkcsa_queries_free(q);
   return rc;
 }
@@ -555,8 +574,7 @@ int hkcsa_shard_scheme(hkcsa_index* h, int* scheme) {
     activate(h);
     need(scheme != nullptr, HKCSA_E_INVALID, "null output");
     need(h->ix.have_text, HKCSA_E_STATE, "text released by hkcsa_compact");
-    h->ix.have_alpha = false;
-    *scheme = hk::shard_keyed(h->ix) ? 1 : 0;
+    *scheme = hk::shard_keyed(h->ix) ? 1 : 0;   // (a query: the alphabet is computed once, if missing)
   });
 }
 

@@ -19,6 +19,9 @@ i64p = C.POINTER(C.c_int64)
 vp = C.c_void_p
 
 
+E_RANGE = -4   # HKCSA_E_RANGE
+
+
 class HkcsaError(RuntimeError):
     """Raised for every non-zero return code of the C-ABI."""
 

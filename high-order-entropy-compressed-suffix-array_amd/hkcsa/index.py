@@ -79,6 +79,7 @@ FLAG_POS64 = 1   # HKCSA_FLAG_POS64: 64-bit positions in sharded builds at any n
 FLAG_GLOBAL_SORT = 4   # HKCSA_FLAG_GLOBAL_SORT: build by full-width LSD sort (no bucket sorts)
 FLAG_MUL_BINS = 8      # HKCSA_FLAG_MUL_BINS: sharded slices use multiplicative bucket bins (diagnostic)
 FLAG_MAX_BUCKETS = 16  # HKCSA_FLAG_MAX_BUCKETS: single GPU, the most bucket bits at any n (diagnostic)
+FLAG_SLICES = 32       # HKCSA_FLAG_SLICES: single GPU, the multi-slice build (n >= 2^32 - 1) at any n
 
 
 class DeviceIndex:
@@ -261,6 +262,25 @@ class DeviceIndex:
             return q.positions()
         finally:
             q.close()
+
+    def locate_batch(self, data: np.ndarray, offs: np.ndarray, cap: int | None = None) -> tuple[np.ndarray, np.ndarray]:
+        """hkcsa_locate_batch from host buffers: (CSR offsets u64[P+1], positions u64) in caller-owned
+        arrays.  One call when `cap` (default 2 positions per pattern + 1024) holds every position,
+        else a second call with the exact size the first one reported."""
+        data = np.ascontiguousarray(data, dtype=np.uint8)
+        offs = np.ascontiguousarray(offs, dtype=np.uint64)
+        P = len(offs) - 1
+        occ = np.empty(P + 1, dtype=np.uint64)
+        cap = 2 * P + 1024 if cap is None else int(cap)
+        pos = np.empty(max(1, cap), dtype=np.uint64)
+        rc = self.lib.hkcsa_locate_batch(self.h, _ptr(data) if len(data) else None, _ptr(offs), P, _ptr(occ),
+                                         _ptr(pos), cap)
+        if rc == N.E_RANGE:
+            pos = np.empty(max(1, int(occ[P])), dtype=np.uint64)
+            rc = self.lib.hkcsa_locate_batch(self.h, _ptr(data) if len(data) else None, _ptr(offs), P,
+                                             _ptr(occ), _ptr(pos), len(pos))
+        N.check(rc)
+        return occ, pos[:int(occ[P])]
 
     # ------------------------------------------------------------ sharding
     def build_sa_sharded(self, uid: bytes, nranks: int, rank: int):

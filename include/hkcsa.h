@@ -53,6 +53,8 @@ typedef struct hkcsa_queries hkcsa_queries;
                                /* shift bins would do (diagnostic; chosen automatically)    */
 #define HKCSA_FLAG_MAX_BUCKETS 16u /* single GPU: 2^16 buckets (2^17 with half items) at any n, */
                                    /* so small texts take the 1 GiB pipeline (diagnostic)       */
+#define HKCSA_FLAG_SLICES 32u  /* single GPU: the multi-slice build (taken by itself when    */
+                               /* n >= 2^32 - 1) at any n, in 4 slices (parity tests)        */
 
 typedef struct hkcsa_opts {
   int32_t device;   /* HIP device ordinal (-1 = current)                 */
@@ -83,7 +85,12 @@ int hkcsa_create_synthetic(uint64_t n, const uint8_t* alphabet, int sigma, uint6
  * sorts that write SA and BWT together, chunk refinement of tied suffixes, GPU
  * prefix doubling over an ISA for texts whose ties persist);
  * HKCSA_FLAG_GLOBAL_SORT: full-width LSD sort of the keys instead of bucket sorts.
- * Recomputes the byte histogram / C array every call. */
+ * Texts of n >= 2^32 - 1 symbols (64-bit positions; the reference's SA has no size
+ * limit) are built on the one device as slices of ~2^30 suffixes of the final SA, one
+ * after another, straight into one full SA / BWT: slice bounds from one partition
+ * histogram of the whole text, ties that outlast a slice's chunk refinement finished by
+ * prefix doubling over one ISA of the full SA (HKCSA_FLAG_SLICES takes this path at
+ * any n).  Recomputes the byte histogram / C array every call. */
 int hkcsa_build_sa(hkcsa_index* ix);
 /* BWT of T' (bwt_transform, csa/bwt.py:3-13).  The SA build already writes the
  * BWT in sorted order, so this is a no-op after hkcsa_build_sa; it gathers

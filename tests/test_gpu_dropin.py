@@ -158,3 +158,34 @@ def test_run_full_benchmark_harness(capsys):
     print_benchmark_summary(res)
     out = capsys.readouterr().out
     assert "=== Benchmark Summary ===" in out and "Peak Memory" in out
+
+
+def test_locate_batch_host_boundary():
+    """hkcsa_locate_batch from host buffers (EnhancedFMIndex.find, csa/enhanced_fm_index.py:15-19):
+    one call when the caller's buffer is large enough, HKCSA_E_RANGE with the CSR sizes (nothing
+    gathered) when it is not, sizes only with a NULL position buffer."""
+    import ctypes as C
+
+    import hkcsa
+    from hkcsa import _native as N
+    from hkcsa.index import _ptr, pack_patterns
+    from oracle import oracle
+    text = oracle.synth_text(1 << 16, b"ACGT", seed=12)
+    dev = hkcsa.DeviceIndex.from_bytes(text, device=0)
+    dev.build_all()
+    fm = oracle.FM(text)
+    pats = [b"A", b"ACG", b"", b"TTTTTTTTTTTTTTTTTTTT", b"$", b"GATTACA"] + \
+        [text[s:s + 9].tobytes() for s in range(0, 60000, 997)]
+    data, offs = pack_patterns(pats)
+    want = fm.find(pats)
+    for cap in (None, 0, 5, sum(map(len, want))):
+        occ, pos = dev.locate_batch(data, offs, cap=cap)
+        assert [list(map(int, pos[occ[i]:occ[i + 1]])) for i in range(len(pats))] == want, cap
+    occ = np.zeros(len(pats) + 1, dtype=np.uint64)
+    small = np.zeros(3, dtype=np.uint64)
+    rc = dev.lib.hkcsa_locate_batch(dev.h, _ptr(data), _ptr(offs), len(pats), _ptr(occ), _ptr(small), 3)
+    assert rc == N.E_RANGE and int(occ[-1]) == sum(map(len, want)) and not small.any()
+    occ[:] = 0
+    assert dev.lib.hkcsa_locate_batch(dev.h, _ptr(data), _ptr(offs), len(pats), _ptr(occ), None, 0) == 0
+    assert [int(occ[i + 1] - occ[i]) for i in range(len(pats))] == [len(w) for w in want]
+    dev.close()

@@ -127,3 +127,24 @@ def test_generate_random_patterns_reference_semantics():
     blob = text.encode()
     for i in range(50):
         assert data[offs[i]:offs[i + 1]].tobytes() in blob
+
+
+def test_english_like_text_shape():
+    """utils.textgen (the configs[2] stand-in): deterministic, latin-1 words with long repeats, and
+    small texts whose SA the oracle's naive sort (csa/suffix_array.py:131-134) and O(n) checker agree on."""
+    from oracle import oracle
+    from utils.textgen import english_like, english_like_text
+    a = english_like(1 << 20, seed=4)
+    assert len(a) == 1 << 20 and np.array_equal(a, english_like(1 << 20, seed=4))
+    assert not np.array_equal(a[:4096], english_like(1 << 20, seed=5)[:4096])
+    assert ord("$") not in set(a.tolist()) and 60 <= len(np.unique(a)) <= 120
+    assert b" the " in a.tobytes()
+    # long repeats: some 256-byte window occurs at least twice
+    w = np.lib.stride_tricks.sliding_window_view(a[: 1 << 18], 64)[::64]
+    keys = {bytes(x) for x in w}
+    assert len(keys) < len(w)
+    t = english_like_text(20001, seed=9, copy_frac=0.5, min_copy=20, max_copy=400, vocab=200)
+    assert t[-1] == ord("$") and len(t) == 20001
+    sa = oracle.suffix_array(t)
+    assert oracle.check_sa(t, sa) == 0
+    assert english_like(0).size == 0
