@@ -2,9 +2,12 @@
 
 Same constructor, attributes and methods; construction and every query run on
 the GPU through libhkcsa.so:
-  * __init__      -> hkcsa_build_all: SA (LSD radix sort of q-symbol suffix keys + tie
-                     refinement; the BWT falls out of the sorted keys), C array
-                     and the levelwise wavelet tree (replaces the O(n*sigma) occ table)
+  * __init__      -> hkcsa_build_all: SA + BWT by the keyed bucket build (q-symbol suffix
+                     keys grouped into buckets by two lookback-free scatter passes, LDS
+                     bucket sorts that write SA and BWT together, refinement of tied
+                     suffixes, prefix doubling for long repeats; texts of >= 2^32 - 1
+                     symbols as slices of the final SA), C array and the levelwise
+                     wavelet tree (replaces the O(n*sigma) occ table)
   * find_range    -> batched backward search kernel (one lane per pattern)
   * find          -> find_range + SA gather, positions in SA order (:15-19)
   * rank          -> wavelet-tree rank kernel; occ[c][i] semantics incl. the

@@ -455,10 +455,10 @@ constexpr int CP_T = 512;
 constexpr int CP_I = 16;
 constexpr int CP_TILE = CP_T * CP_I;   // 8192 suffixes per tile
 
-template <int NB, int T = CP_T, bool SD = false, bool HS = false>
+template <int NB, int T = CP_T, bool SD = false>
 struct CpShared {
   union {
-    uint64_t keys[HS ? T * CP_I / 2 : T * CP_I];   // HS: the tile's records staged in two halves
+    uint64_t keys[T * CP_I];
     uint32_t vals[T * CP_I];
     uint16_t codes[T * CP_I + kCodePad];   // pass A: the tile's text codes ...
     struct {                               // ... or packed codes and raw bytes (radix 2^lb)
@@ -466,7 +466,7 @@ struct CpShared {
       uint8_t raw[T * CP_I + 64];
     } ft;
   } stage;
-  uint8_t sd[SD ? (HS ? T * CP_I / 2 : T * CP_I) : 4];   // packed pass A: low 8 bits of each staged slot's digit
+  uint8_t sd[SD ? T * CP_I : 4];   // packed pass A: low 8 bits of each staged slot's digit
   // destination of the digit's run minus its tile start (packed pass A: u32, single GPU n < 2^32,
   // so that 512-thread tiles fit two workgroups per CU)
   std::conditional_t<SD, uint32_t, uint64_t> gb[NB];
@@ -488,10 +488,8 @@ struct CpShared {
 // position, instead of a key and a value plane.  Pass A (NB = 512) packs after ranking and stages
 // each slot's digit (low 8 bits in sd, the 9th from the slot's side of digit 256's start); pass B
 // (NB = 256, shift counts the position bits) moves the records unchanged.
-// HS (packed records): the tile's records are staged and written in two halves (32 KiB of staging), so
-// three workgroups fit a CU instead of two.
-template <int MODE, int LB, int NB = 256, int T = CP_T, bool PK = false, bool CS = true, bool HS = false>
-__global__ __launch_bounds__(T, T == 1024 ? 1 : (HS ? 3 * T / 256 : 2)) void k_cpart(const uint64_t* __restrict__ kin, const uint32_t* __restrict__ vin,
+template <int MODE, int LB, int NB = 256, int T = CP_T, bool PK = false, bool CS = true>
+__global__ __launch_bounds__(T, T == 1024 ? 1 : 2) void k_cpart(const uint64_t* __restrict__ kin, const uint32_t* __restrict__ vin,
                                                    uint64_t* __restrict__ kout, uint32_t* __restrict__ vout,
                                                    uint64_t n, int shift, uint64_t kbias,
                                                    unsigned long long* __restrict__ cur,
@@ -504,10 +502,9 @@ __global__ __launch_bounds__(T, T == 1024 ? 1 : (HS ? 3 * T / 256 : 2)) void k_c
   constexpr bool SD = PK && MODE == 0;
   static_assert(NB == 256 || NB == 512, "digits per pass");
   static_assert(!PK || MODE == 2 || (MODE == 0 && NB == 512), "packed records: pass A over 9-bit digits");
-  static_assert(!HS || PK, "half staging: packed records only");
   constexpr uint32_t DM = NB - 1;
   constexpr int TILE = T * CP_I;
-  __shared__ CpShared<NB, T, SD, HS> sh;
+  __shared__ CpShared<NB, T, SD> sh;
   const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   if (MODE == 0 && skip && *skip) return;   // the pre-pass counts overflowed: recounted, then relaunched
   uint64_t tbase;
@@ -615,37 +612,6 @@ __global__ __launch_bounds__(T, T == 1024 ? 1 : (HS ? 3 * T / 256 : 2)) void k_c
     sh.tst[tid] = carry + inc - c;
   }
   __syncthreads();
-  if constexpr (HS) {
-    // two rounds: the records of final slots [h * TILE / 2, (h + 1) * TILE / 2) staged, then written
-    constexpr uint32_t HALF = (uint32_t)TILE / 2;
-    if (tid < NB) sh.gb[tid] = (std::remove_reference_t<decltype(sh.gb[0])>)(g - sh.tst[tid]);
-    const uint32_t hi256 = SD ? sh.tst[256] : 0u;   // final slots >= hi256 hold digits >= 256
-#pragma unroll
-    for (uint32_t h = 0; h < 2; ++h) {
-      if (h) __syncthreads();   // the first half is written out
-#pragma unroll
-      for (int k = 0; k < CP_I; ++k)
-        if (c0 + cst * k < tn) {
-          const uint32_t f = sh.tst[rk[k] >> 16] + (rk[k] & 0xFFFFu);
-          if (f - h * HALF < HALF) {
-            sh.stage.keys[f - h * HALF] = key[k];
-            if (SD) sh.sd[f - h * HALF] = (uint8_t)(rk[k] >> 16);
-          }
-        }
-      __syncthreads();
-#pragma unroll
-      for (int i = 0; i < CP_I / 2; ++i) {
-        const uint32_t s = (uint32_t)i * T + tid, fs = h * HALF + s;
-        if (fs < tn) {
-          const uint64_t kk = sh.stage.keys[s];
-          const uint32_t d = SD ? (uint32_t)sh.sd[s] | (fs >= hi256 ? 256u : 0u) : (uint32_t)((kk - kbias) >> shift) & DM;
-          if (SD) kout[(uint32_t)(sh.gb[d] + fs)] = kk;
-          else kout[sh.gb[d] + fs] = kk;
-        }
-      }
-    }
-    return;
-  }
 #pragma unroll
   for (int k = 0; k < CP_I; ++k)
     if (c0 + cst * k < tn) {
@@ -3087,9 +3053,8 @@ int cursor_partition(Index& ix, uint64_t n, int D, int bitlo, uint64_t kbias, co
     const unsigned grid = (unsigned)(8 * ceil_div(nspan, 8u) * (span / CP_TILE));
     // packed: 512-thread tiles, two workgroups per CU; radix 2^2: 16 consecutive positions per thread
     if (packed && tks->g.lb == 2)
-      k_cpart<0, 2, 512, CP_T, true, true, true><<<grid, CP_T, 0, s>>>(nullptr, nullptr, kp[outA], nullptr, n,
-                                                                      bitlo2 + sA, 0, d_curA, nullptr, nullptr, span,
-                                                                      tks2, pk->g.pbits, d_ovf);
+      k_cpart<0, 2, 512, CP_T, true><<<grid, CP_T, 0, s>>>(nullptr, nullptr, kp[outA], nullptr, n, bitlo2 + sA, 0,
+                                                          d_curA, nullptr, nullptr, span, tks2, pk->g.pbits, d_ovf);
     else if (packed)
       k_cpart<0, 0, 512, CP_T, true><<<grid, CP_T, 0, s>>>(nullptr, nullptr, kp[outA], nullptr, n, bitlo2 + sA, 0,
                                                           d_curA, nullptr, nullptr, span, tks2, pk->g.pbits, d_ovf);
@@ -3143,9 +3108,9 @@ int cursor_partition(Index& ix, uint64_t n, int D, int bitlo, uint64_t kbias, co
     const uint64_t maxl = deal_regions(ix, totA, ndA, btile, h_gtab, d_gtab);
     TimedLaunch t(ix.timer, "radix_part", (double)n * 2 * (packed ? 8 : 8 + 4));
     if (packed)
-      k_cpart<2, 0, 256, CP_T, true, true, true><<<(unsigned)(8 * maxl), CP_T, 0, s>>>(
-          kp[1], nullptr, kp[0], nullptr, n, bitlo2 + pk->g.pbits, 0, d_curB, d_gtab, d_startA, 0, TextKeySrc{},
-          pk->g.pbits);
+      k_cpart<2, 0, 256, CP_T, true><<<(unsigned)(8 * maxl), CP_T, 0, s>>>(kp[1], nullptr, kp[0], nullptr, n,
+                                                                          bitlo2 + pk->g.pbits, 0, d_curB, d_gtab,
+                                                                          d_startA, 0, TextKeySrc{}, pk->g.pbits);
     else if (sA > 8 && btile > CP_TILE)
       k_cpart<2, 0, 512, 1024><<<(unsigned)(8 * maxl), 1024, 0, s>>>(kp[1], vp[1], kp[0], vp[0], n, bitlo, kbias,
                                                                       d_curB, d_gtab, d_startA, 0, TextKeySrc{});

@@ -45,3 +45,15 @@ def test_library_is_gfx950():
     so = hkcsa.LIB_PATH
     data = open(so, "rb").read()
     assert b"gfx950" in data
+
+
+def test_flag_constants_match_header():
+    """hkcsa.index.FLAG_* and _native.E_RANGE mirror the header's #defines."""
+    from hkcsa import index
+    src = open(HEADER).read()
+    flags = {m.group(1): int(m.group(2)) for m in re.finditer(r"#define HKCSA_FLAG_([A-Z0-9_]+) (\d+)u", src)}
+    assert {"POS64", "GLOBAL_SORT", "MUL_BINS", "MAX_BUCKETS", "SLICES"} <= set(flags)
+    for name, v in flags.items():
+        if hasattr(index, "FLAG_" + name):
+            assert getattr(index, "FLAG_" + name) == v, name
+    assert int(re.search(r"#define HKCSA_E_RANGE \((-\d+)\)", src).group(1)) == _native.E_RANGE

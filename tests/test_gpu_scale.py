@@ -13,6 +13,7 @@ output, csa/suffix_array.py:131-134 — the SA is unique), the BWT against the o
 """
 import os
 import sys
+import time
 
 import numpy as np
 import pytest
@@ -20,6 +21,13 @@ import pytest
 from conftest import ROOT
 
 pytestmark = pytest.mark.gpu
+
+_T0 = [time.perf_counter()]
+
+
+def _say(msg):
+    """Progress on stdout (run with -s): the 4 GiB checks spend minutes in host-side oracle work."""
+    print(f"  [{time.perf_counter() - _T0[0]:7.1f} s] {msg}", flush=True)
 
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
@@ -43,14 +51,19 @@ def test_config4_4GiB_single_handle_build(hk):
     from csa.csa import sample_rate
     from oracle import oracle
     n = (1 << 32) + 1
+    _T0[0] = time.perf_counter()
     dev = hk.DeviceIndex.synthetic(n, b"ACGT", seed=2)
     dev.build_all()
     info = dev.build_info()
+    _say(f"built SA + BWT + WT, info {info[:10]}")
     assert info[7] & 4, info[:10]                 # keyed coarse slices
     sa = dev.sa()
+    _say("SA downloaded")
     text = oracle.synth_text(n, b"ACGT", seed=2)
     assert oracle.check_sa(text, sa) == 0
+    _say("SA checked")
     assert np.array_equal(dev.bwt(), oracle.bwt(text, sa))
+    _say("BWT checked")
     del text
     rng = np.random.default_rng(4)
     win = dev.text((1 << 32) - (1 << 20), (1 << 32))
@@ -62,6 +75,7 @@ def test_config4_4GiB_single_handle_build(hk):
     rate = sample_rate(n, 0.5)
     dev.build_samples(rate)
     dev.compact()
+    _say("samples + compact")
     sp = dev.space()
     assert sp["sa"] == 0 and sp["text"] == 0 and sp["sample_rate"] == rate
     offs, pos = dev.locate(pats)
@@ -69,6 +83,7 @@ def test_config4_4GiB_single_handle_build(hk):
     for r in rows:
         assert int(dev.sa(int(r), int(r) + 1)[0]) == int(sa[r])
     assert dev.extract((1 << 32) - 100, (1 << 32) + 1) == tail.tobytes()
+    _say("sampled locate / rows / extract checked")
     dev.close()
 
 
@@ -78,6 +93,7 @@ def test_4GiB_planted_repeats_single_handle(hk):
     the full ISA finishes them; the O(n) checker and the oracle BWT."""
     from oracle import oracle
     n = (1 << 32) + 1
+    _T0[0] = time.perf_counter()
     text = oracle.synth_text(n, b"ACGT", seed=6)
     rng = np.random.default_rng(6)
     for _ in range(48):
@@ -86,13 +102,17 @@ def test_4GiB_planted_repeats_single_handle(hk):
         dst = int(rng.integers(0, n - 1 - L))
         text[dst:dst + L] = text[src:src + L].copy()
     text[(3 << 30):(3 << 30) + (64 << 20)] = text[(1 << 30):(1 << 30) + (64 << 20)].copy()
+    _say("text planted")
     dev = hk.DeviceIndex.from_bytes(text, device=0)
     dev.build_sa()
     info = dev.build_info()
+    _say(f"built SA + BWT, info {info[:12]}")
     assert info[2] >> 32 > 0, info[:12]        # prefix-doubling rounds ran
     sa = dev.sa()
     assert oracle.check_sa(text, sa) == 0
+    _say("SA checked")
     assert np.array_equal(dev.bwt(), oracle.bwt(text, sa))
+    _say("BWT checked")
     dev.close()
 
 

@@ -115,3 +115,23 @@ def test_trace_builds_identical(hk, var, monkeypatch, capfd):
         dev.close()
     err = capfd.readouterr().err
     assert "trace]" in err
+
+
+@pytest.mark.parametrize("nranks", [2, 3, 8])
+@pytest.mark.parametrize("alpha", [b"ACGT", bytes(range(256)), b"ab"])
+def test_keyed_below_rule_matches_host(hk, nranks, alpha):
+    """the keyed scheme's slice bounds (hkcsa_build_sa_sharded's `below` from the exact coarse
+    histogram alone: splitters(..., aligned) + prefix sums, the rule build_sa_slices uses too) equal the
+    host restatement (hkcsa/shard.py split_buckets) and the summed per-block counts at N = 2, 3, 8."""
+    from hkcsa.shard import split_buckets
+    text = oracle.synth_text(3 * (1 << 20) + 1, alpha, seed=nranks)
+    devs = [hk.DeviceIndex.from_bytes(text, device=0) for _ in range(nranks)]
+    assert devs[0].shard_scheme() == 1
+    g = sum(d.shard_histogram(nranks, r) for r, d in enumerate(devs))
+    assert int(g.sum()) == len(text)
+    cum = np.concatenate(([0], np.cumsum(g, dtype=np.uint64)))
+    host = np.array([cum[b] for b in split_buckets(g, nranks, aligned=True)], dtype=np.uint64)
+    dev_below = sum(d.shard_counts(g, nranks, r) for r, d in enumerate(devs))
+    assert np.array_equal(dev_below, host)
+    for d in devs:
+        d.close()
