@@ -489,7 +489,8 @@ struct CpShared {
 // each slot's digit (low 8 bits in sd, the 9th from the slot's side of digit 256's start); pass B
 // (NB = 256, shift counts the position bits) moves the records unchanged.
 // HS (packed records): the tile's records are staged and written in two halves (32 KiB of staging), so
-// three workgroups fit a CU instead of two.
+// three workgroups fit a CU instead of two (pass B: 3.52 -> 3.42-3.47 ms at 1 GiB; pass A, whose keys
+// then have to be rebuilt or spill, gained nothing and keeps full staging)
 template <int MODE, int LB, int NB = 256, int T = CP_T, bool PK = false, bool CS = true, bool HS = false>
 __global__ __launch_bounds__(T, T == 1024 ? 1 : (HS ? 3 * T / 256 : 2)) void k_cpart(const uint64_t* __restrict__ kin, const uint32_t* __restrict__ vin,
                                                    uint64_t* __restrict__ kout, uint32_t* __restrict__ vout,
@@ -559,7 +560,7 @@ __global__ __launch_bounds__(T, T == 1024 ? 1 : (HS ? 3 * T / 256 : 2)) void k_c
   }
   if (tid < NB) sh.cnt[tid] = 0;
   const uint32_t s0 = wv * WSPAN + lane;   // item k of this thread is tile slot s0 + 64 k ...
-  // ... or, packed pass A over radix-2^2 codes (HKCSA_CONSEC=0: lane-strided), slot 16 tid + k
+  // ... or, packed pass A over radix-2^2 codes, slot 16 tid + k
   constexpr bool CONSEC = CS && MODE == 0 && PK && LB == 2 && CP_I == 16;
   const uint32_t c0 = CONSEC ? 16u * tid : s0, cst = CONSEC ? 1u : 64u;
   uint64_t key[CP_I];
@@ -1597,45 +1598,29 @@ __device__ __forceinline__ bool bucket_sort_fast(BfShared<T, I>& sh, uint2 it, c
       for (int h = 0; h < 2; ++h) {   // branch-free: the loads of all 16 bins issue together
         const uint32_t s = h ? pr[j] >> 16 : pr[j] & 0xFFFFu;
         const uint32_t c = (h ? nx[j] : pr[j] >> 16) - s;
-        // bins of one to three records settle here (three records: 7 % of the bins for iid text, ~1 per
-        // thread, so a separate listed pass over them cost more than the third read and compares)
-        const bool some = c - 1u < 3u, two = c - 2u < 2u, three = c == 3;
-        // unconditional reads (s + 2 <= cnt + 2 stays inside the plane): the loads of all 16 bins issue
+        const bool some = c - 1u < 2u, two = c == 2;
+        // unconditional reads (s + 1 <= cnt + 1 stays inside the plane): the loads of all 16 bins issue
         // back to back instead of one exec-masked branch each
-        const uint32_t x0 = sh.buf[s], y0 = sh.buf[s + 1], z0 = sh.buf[s + 2];
+        const uint32_t x0 = sh.buf[s], y0 = sh.buf[s + 1];
         const uint32_t x = some ? x0 : 0u;
         const uint32_t y = two ? y0 : x;
-        const uint32_t z = three ? z0 : y;   // (records are distinct: the slots differ)
-        const uint32_t yx = y < x, zx = z < x, zy = z < y;
-        if (some) sh.aux[x & 0x7FFFu] = (uint16_t)(s + yx + (three ? zx : 0u));
-        if (two) sh.aux[y & 0x7FFFu] = (uint16_t)(s + (yx ^ 1u) + (three ? zy : 0u));
-        if (three) sh.aux[z & 0x7FFFu] = (uint16_t)(s + (zx ^ 1u) + (zy ^ 1u));
-        const uint32_t kx = x >> 15, ky = y >> 15, kz = z >> 15;
-        if (two && (kx == ky || kx == kz || ky == kz)) {   // equal keys (rare): the group's smallest heads it
-          const uint32_t r[3] = {x, y, z};
-#pragma unroll
-          for (int q = 0; q < 3; ++q) {
-            if (q == 2 && !three) break;
-            uint32_t below = 0, eq = 0, eqb = 0;
-#pragma unroll
-            for (int o = 0; o < 3; ++o) {
-              if (o == q || (o == 2 && !three)) continue;
-              const bool e15 = (r[o] >> 15) == (r[q] >> 15);
-              below += r[o] < r[q] ? 1u : 0u;
-              eq |= e15 ? 1u : 0u;
-              eqb |= (e15 && r[o] < r[q]) ? 1u : 0u;
-            }
-            if (eq) {
-              const uint32_t t = atomicAdd(&nctr[1], 1u);
-              if (t < BF_TIECAP) tlist[t] = (uint16_t)((s + below) | (eqb ? 0u : 0x8000u));
-            }
+        const uint32_t a = x < y ? x : y, b = x < y ? y : x;
+        if (some) sh.aux[a & 0x7FFFu] = (uint16_t)s;
+        if (two) sh.aux[b & 0x7FFFu] = (uint16_t)(s + 1);
+        if (two && (x >> 15) == (y >> 15)) {   // equal keys (rare)
+          const uint32_t t = atomicAdd(&nctr[1], 2u);
+          if (t + 2 <= BF_TIECAP) {
+            tlist[t] = (uint16_t)(s | 0x8000u);
+            tlist[t + 1] = (uint16_t)(s + 1);
           }
         }
+        bigm |= (c == 3 ? 1u : 0u) << (2 * j + h);
         big4 |= (c >= 4 ? 1u : 0u) << (2 * j + h);
       }
     }
   }
-  {   // wave-aggregated appends of the listed bins (four records or more) from the back of the list
+  {   // wave-aggregated appends of the listed bins: three-record bins from the front of the list,
+      // larger ones from its back (so that each loop of section 5 runs one code path per wave)
     const uint32_t nb = __popc(bigm), nb4 = __popc(big4);
     const uint32_t binc = dpp_incl_sum(nb | (nb4 << 16));   // both counts <= 64 * 16
     uint32_t bbase = 0;
@@ -3087,9 +3072,8 @@ int cursor_partition(Index& ix, uint64_t n, int D, int bitlo, uint64_t kbias, co
     const unsigned grid = (unsigned)(8 * ceil_div(nspan, 8u) * (span / CP_TILE));
     // packed: 512-thread tiles, two workgroups per CU; radix 2^2: 16 consecutive positions per thread
     if (packed && tks->g.lb == 2)
-      k_cpart<0, 2, 512, CP_T, true, true, true><<<grid, CP_T, 0, s>>>(nullptr, nullptr, kp[outA], nullptr, n,
-                                                                      bitlo2 + sA, 0, d_curA, nullptr, nullptr, span,
-                                                                      tks2, pk->g.pbits, d_ovf);
+      k_cpart<0, 2, 512, CP_T, true><<<grid, CP_T, 0, s>>>(nullptr, nullptr, kp[outA], nullptr, n, bitlo2 + sA, 0,
+                                                          d_curA, nullptr, nullptr, span, tks2, pk->g.pbits, d_ovf);
     else if (packed)
       k_cpart<0, 0, 512, CP_T, true><<<grid, CP_T, 0, s>>>(nullptr, nullptr, kp[outA], nullptr, n, bitlo2 + sA, 0,
                                                           d_curA, nullptr, nullptr, span, tks2, pk->g.pbits, d_ovf);
@@ -3589,7 +3573,7 @@ static int cursor_partition_slice(Index& ix, const SlicePlan& P, const TextKeySr
   const uint64_t maxl = deal_regions(ix, h_totA, ndA, CP_TILE, h_gtab, d_gtab);
   TimedLaunch t(ix.timer, "radix_part", (double)m * 2 * (P.packed ? 8 : 8 + 4));
   if (P.packed)
-    k_cpart<2, 0, 256, CP_T, true><<<(unsigned)(8 * maxl), CP_T, 0, s>>>(
+    k_cpart<2, 0, 256, CP_T, true, true, true><<<(unsigned)(8 * maxl), CP_T, 0, s>>>(
         kp[1], nullptr, kp[0], nullptr, m, P.pg.pbits + P.pg.pb2 + sl.bsh, 0, d_curB, d_gtab, d_startA, 0,
         TextKeySrc{}, P.pg.pbits);
   else

@@ -341,10 +341,15 @@ __device__ __forceinline__ void text_keys(uint64_t (&key)[I], const TextKeySrc& 
 // table lookup each).  The prev field is the keyed code straight from the stream (the packed records'
 // prev code: the unique terminal, code 0 in both, precedes only position 0), LP only for the byte
 // before the tile.
+// The staging half: the tile's packed codes into pk (one 32-byte chunk per thread), then this thread's
+// three words and the word before; consec2_key turns them into item k's key.
+struct Consec2Words {
+  uint32_t a, b, c, pw;
+};
+
 template <int T>
-__device__ __forceinline__ void text_keys_consec2(uint64_t (&key)[16], const TextKeySrc& src, uint64_t n,
-                                                  uint64_t tbase, uint32_t* pk, uint32_t* prev0,
-                                                  const uint16_t* L, const uint16_t* LP, const uint64_t* SK) {
+__device__ __forceinline__ Consec2Words consec2_words(const TextKeySrc& src, uint64_t n, uint64_t tbase, uint32_t* pk,
+                                                      uint32_t* prev0, const uint16_t* L) {
   constexpr int TILE = T * 16;
   const uint32_t tid = threadIdx.x;
   if (tid == 0) *prev0 = src.text[tbase == 0 ? n - 1 : tbase - 1];
@@ -369,20 +374,38 @@ __device__ __forceinline__ void text_keys_consec2(uint64_t (&key)[16], const Tex
     }
   }
   __syncthreads();
-  const uint32_t a = pk[tid], b = pk[tid + 1], c = pk[tid + 2];
-  const uint32_t pw = tid ? pk[tid - 1] : 0u;
-  const uint64_t hi = ((uint64_t)a << 32) | b;
+  return Consec2Words{pk[tid], pk[tid + 1], pk[tid + 2], tid ? pk[tid - 1] : 0u};
+}
+
+// key of item k (position tbase + 16 tid + k) from the thread's words (k compile-time after unrolling)
+__device__ __forceinline__ uint64_t consec2_key(const Consec2Words& w, int k, const TextKeySrc& src, uint64_t n,
+                                                uint64_t tbase, const uint32_t* prev0, const uint16_t* LP,
+                                                const uint64_t* SK) {
+  const uint32_t tid = threadIdx.x;
+  const uint64_t hi = ((uint64_t)w.a << 32) | w.b;
   const int kbits = src.g.q * 2;
-  const uint64_t j0 = tbase + 16ull * tid;
+  const uint64_t j = tbase + 16ull * tid + (uint64_t)k;
+  const uint64_t win = k ? (hi << (2 * k)) | (w.c >> (32 - 2 * k)) : hi;
+  uint64_t sym = kbits >= 64 ? win : win >> (64 - kbits);
+  if (j >= src.g.s_start) sym = j < n ? SK[j - src.g.s_start] : 0;
+  const uint32_t pc = k ? (w.a >> (32 - 2 * k)) & 3u : (tid ? w.pw & 3u : LP[*prev0]);
+  return j < n ? (sym << src.g.pb) | pc : ~0ull;
+}
+
+// Pass A of the packed-record build (radix 2^2 codes, 16 items per thread): item k of thread tid is
+// position tbase + 16 tid + k, so the thread's 16 windows and prev codes all come from the three packed
+// words at its own 16 symbols (plus the word before) with compile-time shifts: 4 LDS reads per thread
+// instead of 5 per key (text_keys' lane-strided items need a fresh 3-word window, a raw byte and a
+// table lookup each).  The prev field is the keyed code straight from the stream (the packed records'
+// prev code: the unique terminal, code 0 in both, precedes only position 0), LP only for the byte
+// before the tile.
+template <int T>
+__device__ __forceinline__ void text_keys_consec2(uint64_t (&key)[16], const TextKeySrc& src, uint64_t n,
+                                                  uint64_t tbase, uint32_t* pk, uint32_t* prev0,
+                                                  const uint16_t* L, const uint16_t* LP, const uint64_t* SK) {
+  const Consec2Words w = consec2_words<T>(src, n, tbase, pk, prev0, L);
 #pragma unroll
-  for (int k = 0; k < 16; ++k) {
-    const uint64_t j = j0 + k;
-    const uint64_t win = k ? (hi << (2 * k)) | (c >> (32 - 2 * k)) : hi;
-    uint64_t sym = kbits >= 64 ? win : win >> (64 - kbits);
-    if (j >= src.g.s_start) sym = j < n ? SK[j - src.g.s_start] : 0;
-    const uint32_t pc = k ? (a >> (32 - 2 * k)) & 3u : (tid ? pw & 3u : LP[*prev0]);
-    key[k] = j < n ? (sym << src.g.pb) | pc : ~0ull;
-  }
+  for (int k = 0; k < 16; ++k) key[k] = consec2_key(w, k, src, n, tbase, prev0, LP, SK);
 }
 
 }  // namespace hk

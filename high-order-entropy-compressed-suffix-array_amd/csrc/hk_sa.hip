@@ -694,7 +694,8 @@ void dbl_round_t(Index& ix, uint64_t K) {
 template <typename V>
 std::pair<uint64_t, uint64_t> refine_step(Index& ix, const KeyGeom& kg, const uint64_t* keys, const V* P,
                                           const uint32_t* J, uint64_t A, int cs, bool from_key, bool write_sa,
-                                          V* oP, uint32_t* oJ, uint32_t* oG, uint32_t* head_slot) {
+                                          V* oP, uint32_t* oJ, uint32_t* oG, uint32_t* head_slot,
+                                          const unsigned int* d_flag = nullptr, unsigned int* h_flag = nullptr) {
   hipStream_t s = ix.stream;
   const uint64_t nt = ceil_div(A, GR_TILE);
   ix.tile_b.ensure((nt + 1) * 4);
@@ -725,7 +726,12 @@ std::pair<uint64_t, uint64_t> refine_step(Index& ix, const KeyGeom& kg, const ui
   uint64_t* const tot = ix.rb();
   HK_HIP(hipMemcpyAsync(&tot[0], ix.tile_a.as<uint64_t>() + nt, 8, hipMemcpyDeviceToHost, s));
   HK_HIP(hipMemcpyAsync(&tot[1], ix.tile_d.as<uint64_t>() + nt, 8, hipMemcpyDeviceToHost, s));
+  if (d_flag) {   // a caller's device flag rides in the same round trip
+    tot[2] = 0;
+    HK_HIP(hipMemcpyAsync(&tot[2], d_flag, 4, hipMemcpyDeviceToHost, s));
+  }
   HK_HIP(hipStreamSynchronize(s));
+  if (h_flag) *h_flag = d_flag ? (unsigned int)tot[2] : 0u;
   return {tot[0], tot[1]};
 }
 
@@ -866,29 +872,29 @@ void refine_loop(Index& ix, const KeyGeom& kg, int cur, uint64_t A, uint64_t gro
                                                    vp[0], s_start, nS, d_srank);
       HK_HIP(hipGetLastError());
     }
-    // groups of <= SEG_MAX members sorted in place; the global radix sort only when a group is larger
-    int sl = -1;
+    // groups of <= SEG_MAX members sorted in place, and the round applied at once; its group-size flag
+    // comes back with the round's totals (one round trip).  A group over SEG_MAX members (it was left
+    // unsorted) redoes the round from the same keys with the global radix sort: the redo rewrites every
+    // output of the first attempt (the same SA / BWT slots, the next list, the group heads).
+    unsigned int* d_big = reinterpret_cast<unsigned int*>(ix.small.as<uint8_t>() + 4356);   // small+4356: flag
+    unsigned int h_big = 0;
+    HK_HIP(hipMemsetAsync(d_big, 0, 4, s));
     {
-      unsigned int* d_big = reinterpret_cast<unsigned int*>(ix.small.as<uint8_t>() + 4356);   // small+4356: flag
-      unsigned int h_big = 0;
-      HK_HIP(hipMemsetAsync(d_big, 0, 4, s));
-      {
-        TimedLaunch tm(ix.timer, "sa_refine_segsort", (double)A * (2 * 8 + 2 * sizeof(V) + 4));
-        k_seg_sort16<V><<<grid_for(A), 256, 0, s>>>(kp[0], vp[0], ix.act[cur][2].as<uint32_t>(), A, d_big);
-        HK_HIP(hipGetLastError());
-      }
-      HK_HIP(hipMemcpyAsync(&h_big, d_big, 4, hipMemcpyDeviceToHost, s));
-      HK_HIP(hipStreamSynchronize(s));
-      if (!h_big) sl = 0;
+      TimedLaunch tm(ix.timer, "sa_refine_segsort", (double)A * (2 * 8 + 2 * sizeof(V) + 4));
+      k_seg_sort16<V><<<grid_for(A), 256, 0, s>>>(kp[0], vp[0], ix.act[cur][2].as<uint32_t>(), A, d_big);
+      HK_HIP(hipGetLastError());
     }
-    if (sl < 0) {
-      sl = radix_sort_pairs<V>(ix.sw, ix.timer, kp, vp, 0, A, 0, 64, false, s);
+    auto r = refine_step<V>(ix, kg, kp[0], vp[0], ix.act[cur][1].as<uint32_t>(), A, 0, false, true,
+                            ix.act[cur ^ 1][0].as<V>(), ix.act[cur ^ 1][1].as<uint32_t>(),
+                            ix.act[cur ^ 1][2].as<uint32_t>(), ix.head_slot.as<uint32_t>(), d_big, &h_big);
+    if (h_big) {
+      const int sl = radix_sort_pairs<V>(ix.sw, ix.timer, kp, vp, 0, A, 0, 64, false, s);
       ix.info[0] += ix.sw.passes_run;
       ix.info[1] += ix.sw.passes_skipped;
+      r = refine_step<V>(ix, kg, kp[sl], vp[sl], ix.act[cur][1].as<uint32_t>(), A, 0, false, true,
+                         ix.act[cur ^ 1][0].as<V>(), ix.act[cur ^ 1][1].as<uint32_t>(),
+                         ix.act[cur ^ 1][2].as<uint32_t>(), ix.head_slot.as<uint32_t>());
     }
-    auto r = refine_step<V>(ix, kg, kp[sl], vp[sl], ix.act[cur][1].as<uint32_t>(), A, 0, false, true,
-                            ix.act[cur ^ 1][0].as<V>(), ix.act[cur ^ 1][1].as<uint32_t>(),
-                            ix.act[cur ^ 1][2].as<uint32_t>(), ix.head_slot.as<uint32_t>());
     cur ^= 1;
     A = r.first;
     groups = r.second;

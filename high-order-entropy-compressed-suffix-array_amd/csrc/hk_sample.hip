@@ -179,6 +179,7 @@ __device__ __forceinline__ uint64_t sa_of_row(const QShared& q, const WtView& v,
 }
 
 constexpr uint64_t kSmallOcc = 32;
+constexpr uint64_t kHugeOcc = 1ull << 16;   // one pattern spread over every workgroup
 
 template <typename W>
 __global__ __launch_bounds__(256) void k_locate_smp_small(WtView v, SmpView<W> m, const int64_t* __restrict__ lr,
@@ -191,8 +192,9 @@ __global__ __launch_bounds__(256) void k_locate_smp_small(WtView v, SmpView<W> m
     const int64_t l = lr[2 * p];
     if (l < 0) continue;
     const uint64_t c = (uint64_t)(lr[2 * p + 1] - l + 1);
-    if (c > kSmallOcc) {
-      big[atomicAdd(nbig, 1ull)] = p;
+    if (c > kSmallOcc) {   // big: one workgroup each; huge: every workgroup (listed from the end of big)
+      if (c > kHugeOcc) big[P - 1 - atomicAdd(nbig + 1, 1ull)] = p;
+      else big[atomicAdd(nbig, 1ull)] = p;
       continue;
     }
     const uint64_t o = oo[p];
@@ -204,17 +206,25 @@ template <typename W>
 __global__ __launch_bounds__(256) void k_locate_smp_big(WtView v, SmpView<W> m, const int64_t* __restrict__ lr,
                                                         const uint64_t* __restrict__ oo,
                                                         const uint64_t* __restrict__ big,
-                                                        const unsigned long long* __restrict__ nbig,
+                                                        const unsigned long long* __restrict__ nbig, uint64_t P,
                                                         uint64_t* __restrict__ pos) {
   __shared__ QShared q;
   load_qshared(q, v);
-  const uint64_t nb = *nbig;
+  const uint64_t nb = nbig[0], nh = nbig[1];
   for (uint64_t b = blockIdx.x; b < nb; b += gridDim.x) {
     const uint64_t p = big[b];
     const uint64_t l = (uint64_t)lr[2 * p];
     const uint64_t c = (uint64_t)(lr[2 * p + 1] + 1) - l;
     const uint64_t o = oo[p];
     for (uint64_t i = threadIdx.x; i < c; i += 256) pos[o + i] = sa_of_row(q, v, m, l + i);
+  }
+  for (uint64_t h = 0; h < nh; ++h) {   // a pattern with more than kHugeOcc rows (e.g. the empty one)
+    const uint64_t p = big[P - 1 - h];
+    const uint64_t l = (uint64_t)lr[2 * p];
+    const uint64_t c = (uint64_t)(lr[2 * p + 1] + 1) - l;
+    const uint64_t o = oo[p];
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < c; i += (uint64_t)gridDim.x * 256)
+      pos[o + i] = sa_of_row(q, v, m, l + i);
   }
 }
 
@@ -373,14 +383,14 @@ void sampled_locate_gather(Index& ix, const int64_t* d_lr, const uint64_t* d_occ
   ix.tile_c.ensure((P + 2) * 8);
   ix.small.ensure(8192);
   unsigned long long* nbig = ix.small.as<unsigned long long>() + 520;
-  HK_HIP(hipMemsetAsync(nbig, 0, 8, s));
+  HK_HIP(hipMemsetAsync(nbig, 0, 16, s));   // big and huge pattern counts
   TimedLaunch t(ix.timer, "fm_locate_sampled", 0.0);
   auto run = [&](auto m) {
     using W = std::remove_const_t<std::remove_pointer_t<decltype(m.ssa)>>;
     k_locate_smp_small<W><<<grid_for(P, 256, 65535), 256, 0, s>>>(ix.view(), m, d_lr, d_occ_offs, P, d_pos,
                                                                   ix.tile_c.as<uint64_t>(), nbig);
     HK_HIP(hipGetLastError());
-    k_locate_smp_big<W><<<1024, 256, 0, s>>>(ix.view(), m, d_lr, d_occ_offs, ix.tile_c.as<uint64_t>(), nbig, d_pos);
+    k_locate_smp_big<W><<<1024, 256, 0, s>>>(ix.view(), m, d_lr, d_occ_offs, ix.tile_c.as<uint64_t>(), nbig, P, d_pos);
     HK_HIP(hipGetLastError());
   };
   if (ix.smp_w64) run(smp_view<uint64_t>(ix));

@@ -781,6 +781,7 @@ __global__ __launch_bounds__(256) void k_rank(WtView v, const uint8_t* __restric
 }
 
 constexpr uint64_t kSmallOcc = 32;
+constexpr uint64_t kHugeOcc = 1ull << 16;   // one pattern spread over every workgroup
 
 template <typename S>
 __global__ __launch_bounds__(256) void k_locate_small(const S* __restrict__ sa,
@@ -792,8 +793,9 @@ __global__ __launch_bounds__(256) void k_locate_small(const S* __restrict__ sa,
     const int64_t l = lr[2 * p];
     if (l < 0) continue;
     const uint64_t c = (uint64_t)(lr[2 * p + 1] - l + 1);
-    if (c > kSmallOcc) {
-      big[atomicAdd(nbig, 1ull)] = p;
+    if (c > kSmallOcc) {   // big: one workgroup each; huge: every workgroup (listed from the end of big)
+      if (c > kHugeOcc) big[P - 1 - atomicAdd(nbig + 1, 1ull)] = p;
+      else big[atomicAdd(nbig, 1ull)] = p;
       continue;
     }
     const uint64_t o = oo[p];
@@ -806,15 +808,23 @@ __global__ __launch_bounds__(256) void k_locate_big(const S* __restrict__ sa,
                                                     const int64_t* __restrict__ lr,
                                                     const uint64_t* __restrict__ oo,
                                                     const uint64_t* __restrict__ big,
-                                                    const unsigned long long* __restrict__ nbig,
+                                                    const unsigned long long* __restrict__ nbig, uint64_t P,
                                                     uint64_t* __restrict__ pos) {
-  const uint64_t nb = *nbig;
+  const uint64_t nb = nbig[0], nh = nbig[1];
   for (uint64_t b = blockIdx.x; b < nb; b += gridDim.x) {
     const uint64_t p = big[b];
     const uint64_t l = (uint64_t)lr[2 * p];
     const uint64_t c = (uint64_t)(lr[2 * p + 1] + 1) - l;
     const uint64_t o = oo[p];
     for (uint64_t i = threadIdx.x; i < c; i += 256) pos[o + i] = sa[l + i];
+  }
+  for (uint64_t h = 0; h < nh; ++h) {   // (e.g. the empty pattern: all n rows)
+    const uint64_t p = big[P - 1 - h];
+    const uint64_t l = (uint64_t)lr[2 * p];
+    const uint64_t c = (uint64_t)(lr[2 * p + 1] + 1) - l;
+    const uint64_t o = oo[p];
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < c; i += (uint64_t)gridDim.x * 256)
+      pos[o + i] = sa[l + i];
   }
 }
 
@@ -1133,20 +1143,20 @@ void query_locate_gather(Index& ix, const int64_t* d_lr, const uint64_t* d_occ_o
   ix.tile_c.ensure((P + 2) * 8);
   ix.small.ensure(8192);
   unsigned long long* nbig = ix.small.as<unsigned long long>() + 512;   // byte 4096: clear of the build LUTs
-  HK_HIP(hipMemsetAsync(nbig, 0, 8, s));
+  HK_HIP(hipMemsetAsync(nbig, 0, 16, s));   // big and huge pattern counts
   TimedLaunch t(ix.timer, "fm_locate", 0.0);
   if (ix.sa_pos64) {   // replicated sharded SA of a text with n >= 2^32
     k_locate_small<uint64_t><<<grid_for(P, 256, 65535), 256, 0, s>>>(ix.sa.as<uint64_t>(), d_lr, d_occ_offs, P,
                                                                      d_pos, ix.tile_c.as<uint64_t>(), nbig);
     HK_HIP(hipGetLastError());
     k_locate_big<uint64_t><<<1024, 256, 0, s>>>(ix.sa.as<uint64_t>(), d_lr, d_occ_offs, ix.tile_c.as<uint64_t>(),
-                                                nbig, d_pos);
+                                                nbig, P, d_pos);
   } else {
     k_locate_small<uint32_t><<<grid_for(P, 256, 65535), 256, 0, s>>>(ix.sa.as<uint32_t>(), d_lr, d_occ_offs, P,
                                                                      d_pos, ix.tile_c.as<uint64_t>(), nbig);
     HK_HIP(hipGetLastError());
     k_locate_big<uint32_t><<<1024, 256, 0, s>>>(ix.sa.as<uint32_t>(), d_lr, d_occ_offs, ix.tile_c.as<uint64_t>(),
-                                                nbig, d_pos);
+                                                nbig, P, d_pos);
   }
   HK_HIP(hipGetLastError());
 }

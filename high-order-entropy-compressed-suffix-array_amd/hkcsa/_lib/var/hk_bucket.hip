@@ -455,10 +455,10 @@ constexpr int CP_T = 512;
 constexpr int CP_I = 16;
 constexpr int CP_TILE = CP_T * CP_I;   // 8192 suffixes per tile
 
-template <int NB, int T = CP_T, bool SD = false>
+template <int NB, int T = CP_T, bool SD = false, bool HS = false>
 struct CpShared {
   union {
-    uint64_t keys[T * CP_I];
+    uint64_t keys[HS ? T * CP_I / 2 : T * CP_I];   // HS: the tile's records staged in two halves
     uint32_t vals[T * CP_I];
     uint16_t codes[T * CP_I + kCodePad];   // pass A: the tile's text codes ...
     struct {                               // ... or packed codes and raw bytes (radix 2^lb)
@@ -466,7 +466,7 @@ struct CpShared {
       uint8_t raw[T * CP_I + 64];
     } ft;
   } stage;
-  uint8_t sd[SD ? T * CP_I : 4];   // packed pass A: low 8 bits of each staged slot's digit
+  uint8_t sd[SD ? (HS ? T * CP_I / 2 : T * CP_I) : 4];   // packed pass A: low 8 bits of each staged slot's digit
   // destination of the digit's run minus its tile start (packed pass A: u32, single GPU n < 2^32,
   // so that 512-thread tiles fit two workgroups per CU)
   std::conditional_t<SD, uint32_t, uint64_t> gb[NB];
@@ -488,8 +488,11 @@ struct CpShared {
 // position, instead of a key and a value plane.  Pass A (NB = 512) packs after ranking and stages
 // each slot's digit (low 8 bits in sd, the 9th from the slot's side of digit 256's start); pass B
 // (NB = 256, shift counts the position bits) moves the records unchanged.
-template <int MODE, int LB, int NB = 256, int T = CP_T, bool PK = false, bool CS = true>
-__global__ __launch_bounds__(T, T == 1024 ? 1 : 2) void k_cpart(const uint64_t* __restrict__ kin, const uint32_t* __restrict__ vin,
+// HS (packed records): the tile's records are staged and written in two halves (32 KiB of staging), so
+// three workgroups fit a CU instead of two (pass B: 3.52 -> 3.42-3.47 ms at 1 GiB; pass A, whose keys
+// then have to be rebuilt or spill, gained nothing and keeps full staging)
+template <int MODE, int LB, int NB = 256, int T = CP_T, bool PK = false, bool CS = true, bool HS = false>
+__global__ __launch_bounds__(T, T == 1024 ? 1 : (HS ? 3 * T / 256 : 2)) void k_cpart(const uint64_t* __restrict__ kin, const uint32_t* __restrict__ vin,
                                                    uint64_t* __restrict__ kout, uint32_t* __restrict__ vout,
                                                    uint64_t n, int shift, uint64_t kbias,
                                                    unsigned long long* __restrict__ cur,
@@ -502,9 +505,10 @@ __global__ __launch_bounds__(T, T == 1024 ? 1 : 2) void k_cpart(const uint64_t* 
   constexpr bool SD = PK && MODE == 0;
   static_assert(NB == 256 || NB == 512, "digits per pass");
   static_assert(!PK || MODE == 2 || (MODE == 0 && NB == 512), "packed records: pass A over 9-bit digits");
+  static_assert(!HS || PK, "half staging: packed records only");
   constexpr uint32_t DM = NB - 1;
   constexpr int TILE = T * CP_I;
-  __shared__ CpShared<NB, T, SD> sh;
+  __shared__ CpShared<NB, T, SD, HS> sh;
   const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   if (MODE == 0 && skip && *skip) return;   // the pre-pass counts overflowed: recounted, then relaunched
   uint64_t tbase;
@@ -556,7 +560,7 @@ __global__ __launch_bounds__(T, T == 1024 ? 1 : 2) void k_cpart(const uint64_t* 
   }
   if (tid < NB) sh.cnt[tid] = 0;
   const uint32_t s0 = wv * WSPAN + lane;   // item k of this thread is tile slot s0 + 64 k ...
-  // ... or, packed pass A over radix-2^2 codes (HKCSA_CONSEC=0: lane-strided), slot 16 tid + k
+  // ... or, packed pass A over radix-2^2 codes, slot 16 tid + k
   constexpr bool CONSEC = CS && MODE == 0 && PK && LB == 2 && CP_I == 16;
   const uint32_t c0 = CONSEC ? 16u * tid : s0, cst = CONSEC ? 1u : 64u;
   uint64_t key[CP_I];
@@ -612,6 +616,37 @@ __global__ __launch_bounds__(T, T == 1024 ? 1 : 2) void k_cpart(const uint64_t* 
     sh.tst[tid] = carry + inc - c;
   }
   __syncthreads();
+  if constexpr (HS) {
+    // two rounds: the records of final slots [h * TILE / 2, (h + 1) * TILE / 2) staged, then written
+    constexpr uint32_t HALF = (uint32_t)TILE / 2;
+    if (tid < NB) sh.gb[tid] = (std::remove_reference_t<decltype(sh.gb[0])>)(g - sh.tst[tid]);
+    const uint32_t hi256 = SD ? sh.tst[256] : 0u;   // final slots >= hi256 hold digits >= 256
+#pragma unroll
+    for (uint32_t h = 0; h < 2; ++h) {
+      if (h) __syncthreads();   // the first half is written out
+#pragma unroll
+      for (int k = 0; k < CP_I; ++k)
+        if (c0 + cst * k < tn) {
+          const uint32_t f = sh.tst[rk[k] >> 16] + (rk[k] & 0xFFFFu);
+          if (f - h * HALF < HALF) {
+            sh.stage.keys[f - h * HALF] = key[k];
+            if (SD) sh.sd[f - h * HALF] = (uint8_t)(rk[k] >> 16);
+          }
+        }
+      __syncthreads();
+#pragma unroll
+      for (int i = 0; i < CP_I / 2; ++i) {
+        const uint32_t s = (uint32_t)i * T + tid, fs = h * HALF + s;
+        if (fs < tn) {
+          const uint64_t kk = sh.stage.keys[s];
+          const uint32_t d = SD ? (uint32_t)sh.sd[s] | (fs >= hi256 ? 256u : 0u) : (uint32_t)((kk - kbias) >> shift) & DM;
+          if (SD) kout[(uint32_t)(sh.gb[d] + fs)] = kk;
+          else kout[sh.gb[d] + fs] = kk;
+        }
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int k = 0; k < CP_I; ++k)
     if (c0 + cst * k < tn) {
@@ -1549,13 +1584,20 @@ __device__ __forceinline__ bool bucket_sort_fast(BfShared<T, I>& sh, uint2 it, c
   // ---- 4. bins of one or two records settle in place: final index by slot into aux; 3+ are listed
   uint32_t bigm = 0, big4 = 0;
   {
-    uint32_t pr[BF_BINS / 2 / T], nx[BF_BINS / 2 / T];
+    // the thread's NP consecutive counter words (bins 2 NP tid ..): NP / 4 16-B reads (the scan's own
+    // layout) and one word for the next bin's start, instead of two reads per word
+    uint32_t pr[NP], nx[NP];
 #pragma unroll
-    for (int j = 0; j < BF_BINS / 2 / T; ++j) {
-      const uint32_t m = tid + T * j;   // bins 2m, 2m + 1
-      pr[j] = H2[m];
-      const uint32_t nw = H2[m + 1];   // (unconditional; the last bin's end is the item's count)
-      nx[j] = m + 1 < (uint32_t)BF_BINS / 2 ? (nw & 0xFFFFu) : cnt;
+    for (int q = 0; q < NP / 4; ++q) {
+      const uint4 a = reinterpret_cast<const uint4*>(H2)[(NP / 4) * tid + q];
+      pr[4 * q] = a.x; pr[4 * q + 1] = a.y; pr[4 * q + 2] = a.z; pr[4 * q + 3] = a.w;
+    }
+    {
+      const uint32_t m1 = NP * tid + NP;   // (unconditional; in bounds by the spare word)
+      const uint32_t nw = H2[m1];
+#pragma unroll
+      for (int j = 0; j < NP; ++j)
+        nx[j] = j + 1 < NP ? (pr[j + 1] & 0xFFFFu) : (m1 < (uint32_t)BF_BINS / 2 ? (nw & 0xFFFFu) : cnt);
     }
 #pragma unroll
     for (int j = 0; j < BF_BINS / 2 / T; ++j) {
@@ -1563,45 +1605,29 @@ __device__ __forceinline__ bool bucket_sort_fast(BfShared<T, I>& sh, uint2 it, c
       for (int h = 0; h < 2; ++h) {   // branch-free: the loads of all 16 bins issue together
         const uint32_t s = h ? pr[j] >> 16 : pr[j] & 0xFFFFu;
         const uint32_t c = (h ? nx[j] : pr[j] >> 16) - s;
-        // bins of one to three records settle here (three records: 7 % of the bins for iid text, ~1 per
-        // thread, so a separate listed pass over them cost more than the third read and compares)
-        const bool some = c - 1u < 3u, two = c - 2u < 2u, three = c == 3;
-        // unconditional reads (s + 2 <= cnt + 2 stays inside the plane): the loads of all 16 bins issue
+        const bool some = c - 1u < 2u, two = c == 2;
+        // unconditional reads (s + 1 <= cnt + 1 stays inside the plane): the loads of all 16 bins issue
         // back to back instead of one exec-masked branch each
-        const uint32_t x0 = sh.buf[s], y0 = sh.buf[s + 1], z0 = sh.buf[s + 2];
+        const uint32_t x0 = sh.buf[s], y0 = sh.buf[s + 1];
         const uint32_t x = some ? x0 : 0u;
         const uint32_t y = two ? y0 : x;
-        const uint32_t z = three ? z0 : y;   // (records are distinct: the slots differ)
-        const uint32_t yx = y < x, zx = z < x, zy = z < y;
-        if (some) sh.aux[x & 0x7FFFu] = (uint16_t)(s + yx + (three ? zx : 0u));
-        if (two) sh.aux[y & 0x7FFFu] = (uint16_t)(s + (yx ^ 1u) + (three ? zy : 0u));
-        if (three) sh.aux[z & 0x7FFFu] = (uint16_t)(s + (zx ^ 1u) + (zy ^ 1u));
-        const uint32_t kx = x >> 15, ky = y >> 15, kz = z >> 15;
-        if (two && (kx == ky || kx == kz || ky == kz)) {   // equal keys (rare): the group's smallest heads it
-          const uint32_t r[3] = {x, y, z};
-#pragma unroll
-          for (int q = 0; q < 3; ++q) {
-            if (q == 2 && !three) break;
-            uint32_t below = 0, eq = 0, eqb = 0;
-#pragma unroll
-            for (int o = 0; o < 3; ++o) {
-              if (o == q || (o == 2 && !three)) continue;
-              const bool e15 = (r[o] >> 15) == (r[q] >> 15);
-              below += r[o] < r[q] ? 1u : 0u;
-              eq |= e15 ? 1u : 0u;
-              eqb |= (e15 && r[o] < r[q]) ? 1u : 0u;
-            }
-            if (eq) {
-              const uint32_t t = atomicAdd(&nctr[1], 1u);
-              if (t < BF_TIECAP) tlist[t] = (uint16_t)((s + below) | (eqb ? 0u : 0x8000u));
-            }
+        const uint32_t a = x < y ? x : y, b = x < y ? y : x;
+        if (some) sh.aux[a & 0x7FFFu] = (uint16_t)s;
+        if (two) sh.aux[b & 0x7FFFu] = (uint16_t)(s + 1);
+        if (two && (x >> 15) == (y >> 15)) {   // equal keys (rare)
+          const uint32_t t = atomicAdd(&nctr[1], 2u);
+          if (t + 2 <= BF_TIECAP) {
+            tlist[t] = (uint16_t)(s | 0x8000u);
+            tlist[t + 1] = (uint16_t)(s + 1);
           }
         }
+        bigm |= (c == 3 ? 1u : 0u) << (2 * j + h);
         big4 |= (c >= 4 ? 1u : 0u) << (2 * j + h);
       }
     }
   }
-  {   // wave-aggregated appends of the listed bins (four records or more) from the back of the list
+  {   // wave-aggregated appends of the listed bins: three-record bins from the front of the list,
+      // larger ones from its back (so that each loop of section 5 runs one code path per wave)
     const uint32_t nb = __popc(bigm), nb4 = __popc(big4);
     const uint32_t binc = dpp_incl_sum(nb | (nb4 << 16));   // both counts <= 64 * 16
     uint32_t bbase = 0;
@@ -1612,13 +1638,13 @@ __device__ __forceinline__ bool bucket_sort_fast(BfShared<T, I>& sh, uint2 it, c
     while (bigm) {
       const int q = __builtin_ctz(bigm);
       bigm &= bigm - 1;
-      if (b3 < BF_BIGCAP) blist[b3] = (uint16_t)(2u * (tid + T * (q >> 1)) + (q & 1));
+      if (b3 < BF_BIGCAP) blist[b3] = (uint16_t)(2u * (NP * tid + (q >> 1)) + (q & 1));
       ++b3;
     }
     while (big4) {
       const int q = __builtin_ctz(big4);
       big4 &= big4 - 1;
-      if (b4 < BF_BIGCAP) blist[BF_BIGCAP - 1 - b4] = (uint16_t)(2u * (tid + T * (q >> 1)) + (q & 1));
+      if (b4 < BF_BIGCAP) blist[BF_BIGCAP - 1 - b4] = (uint16_t)(2u * (NP * tid + (q >> 1)) + (q & 1));
       ++b4;
     }
   }
@@ -3108,9 +3134,9 @@ int cursor_partition(Index& ix, uint64_t n, int D, int bitlo, uint64_t kbias, co
     const uint64_t maxl = deal_regions(ix, totA, ndA, btile, h_gtab, d_gtab);
     TimedLaunch t(ix.timer, "radix_part", (double)n * 2 * (packed ? 8 : 8 + 4));
     if (packed)
-      k_cpart<2, 0, 256, CP_T, true><<<(unsigned)(8 * maxl), CP_T, 0, s>>>(kp[1], nullptr, kp[0], nullptr, n,
-                                                                          bitlo2 + pk->g.pbits, 0, d_curB, d_gtab,
-                                                                          d_startA, 0, TextKeySrc{}, pk->g.pbits);
+      k_cpart<2, 0, 256, CP_T, true, true, true><<<(unsigned)(8 * maxl), CP_T, 0, s>>>(
+          kp[1], nullptr, kp[0], nullptr, n, bitlo2 + pk->g.pbits, 0, d_curB, d_gtab, d_startA, 0, TextKeySrc{},
+          pk->g.pbits);
     else if (sA > 8 && btile > CP_TILE)
       k_cpart<2, 0, 512, 1024><<<(unsigned)(8 * maxl), 1024, 0, s>>>(kp[1], vp[1], kp[0], vp[0], n, bitlo, kbias,
                                                                       d_curB, d_gtab, d_startA, 0, TextKeySrc{});
@@ -3554,7 +3580,7 @@ static int cursor_partition_slice(Index& ix, const SlicePlan& P, const TextKeySr
   const uint64_t maxl = deal_regions(ix, h_totA, ndA, CP_TILE, h_gtab, d_gtab);
   TimedLaunch t(ix.timer, "radix_part", (double)m * 2 * (P.packed ? 8 : 8 + 4));
   if (P.packed)
-    k_cpart<2, 0, 256, CP_T, true><<<(unsigned)(8 * maxl), CP_T, 0, s>>>(
+    k_cpart<2, 0, 256, CP_T, true, true, true><<<(unsigned)(8 * maxl), CP_T, 0, s>>>(
         kp[1], nullptr, kp[0], nullptr, m, P.pg.pbits + P.pg.pb2 + sl.bsh, 0, d_curB, d_gtab, d_startA, 0,
         TextKeySrc{}, P.pg.pbits);
   else
