@@ -365,14 +365,55 @@ __global__ __launch_bounds__(256) void k_bucket_reduce(const uint32_t* __restric
   hist[b] = s;
 }
 
+// hist[b] (zeroed) += drain[b] + the spans' partial counts of bucket b: four buckets per thread (16-B
+// loads) and the spans split over gridDim.y groups (u64 atomics), so that ~16 MiB of loads are in
+// flight (one thread per bucket over every span kept ~4 MiB in flight: 73 us at 1 GiB).  nb % 4 == 0.
+__global__ __launch_bounds__(256) void k_bucket_reduce4(const uint32_t* __restrict__ part,
+                                                        const unsigned long long* __restrict__ drain, uint32_t nspan,
+                                                        uint32_t stride, uint32_t nb,
+                                                        unsigned long long* __restrict__ hist) {
+  const uint32_t b = (blockIdx.x * 256 + threadIdx.x) * 4;
+  if (b >= nb) return;
+  const uint32_t per = (nspan + gridDim.y - 1) / gridDim.y, w0 = blockIdx.y * per;
+  const uint32_t w1 = w0 + per < nspan ? w0 + per : nspan;
+  unsigned long long s0 = 0, s1 = 0, s2 = 0, s3 = 0;
+  if (blockIdx.y == 0) {
+    const ulonglong2 d0 = *reinterpret_cast<const ulonglong2*>(drain + b);
+    const ulonglong2 d1 = *reinterpret_cast<const ulonglong2*>(drain + b + 2);
+    s0 = d0.x, s1 = d0.y, s2 = d1.x, s3 = d1.y;
+  }
+#pragma unroll 8
+  for (uint32_t w = w0; w < w1; ++w) {
+    const uint4 v = *reinterpret_cast<const uint4*>(part + (uint64_t)w * stride + b);
+    s0 += v.x, s1 += v.y, s2 += v.z, s3 += v.w;
+  }
+  if (s0) atomicAdd(&hist[b], s0);
+  if (s1) atomicAdd(&hist[b + 1], s1);
+  if (s2) atomicAdd(&hist[b + 2], s2);
+  if (s3) atomicAdd(&hist[b + 3], s3);
+}
+
 // Cursors of both passes from the counts, in two small kernels over blocks of 64 digits x 16
 // span groups (one workgroup scanning every span of every digit took 0.25-0.5 ms of serial loads):
 // k_cp_colsum: per digit, the span groups' partial sums (exclusive over groups) and the digit total;
 // k_cp_cursors: every block scans the digit totals (digit starts; block 0 publishes them as the
 // region bounds of pass B), then each (digit, group) thread walks its spans: pass A's cursor of
-// (span, digit) = the digit's start + the earlier spans' counts.  The last block instead scans the
-// bucket counts into pass B's cursors (the bucket starts).
+// (span, digit) = the digit's start + the earlier spans' counts.  Pass B's cursors (the bucket starts)
+// come per digit: each wave scans the 2^sA buckets of four of the block's digits from the digit's start
+// (coalesced 32-B loads; one extra workgroup scanning all 2^17 buckets with strided loads took 99 us).
 constexpr uint32_t CP_DB = 64, CP_NG = 16;   // digits per block, span groups
+
+// hist = drain + the spans' partial counts (hist zeroed by the caller when nb % 4 == 0)
+static void bucket_reduce(const uint32_t* part, const unsigned long long* drain, uint32_t nspan, uint32_t stride,
+                          uint32_t nb, uint64_t* hist, hipStream_t s) {
+  if (nb % 4 == 0 && stride % 4 == 0) {
+    k_bucket_reduce4<<<dim3((nb / 4 + 255) / 256, nspan >= 64 ? 8 : 1), 256, 0, s>>>(
+        part, drain, nspan, stride, nb, reinterpret_cast<unsigned long long*>(hist));
+  } else {
+    k_bucket_reduce<<<(nb + 255) / 256, 256, 0, s>>>(part, drain, nspan, stride, nb, hist);
+  }
+  HK_HIP(hipGetLastError());
+}
 
 __global__ __launch_bounds__(1024) void k_cp_colsum(const uint32_t* __restrict__ spanc, uint32_t nspan, uint32_t ndA,
                                                     uint64_t* __restrict__ gpre, uint64_t* __restrict__ totA) {
@@ -405,25 +446,6 @@ __global__ __launch_bounds__(1024) void k_cp_cursors(const uint64_t* __restrict_
   __shared__ uint64_t ws[16];
   __shared__ uint64_t st[CP_NAM];
   const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const uint32_t nblkA = (ndA + CP_DB - 1) / CP_DB;
-  if (blockIdx.x == nblkA) {
-    // pass B: exclusive scan of the bucket counts, `per` consecutive buckets per thread
-    const uint32_t per = (nb + 1023) / 1024, b0 = tid * per;
-    uint64_t sum = 0;
-#pragma unroll 8
-    for (uint32_t b = b0; b < b0 + per && b < nb; ++b) sum += hist[b];
-    const uint64_t inc = wave_incl_sum<uint64_t>(sum);
-    if (lane == 63) ws[wv] = inc;
-    __syncthreads();
-    uint64_t run = inc - sum;
-    for (uint32_t w = 0; w < wv; ++w) run += ws[w];
-#pragma unroll 8
-    for (uint32_t b = b0; b < b0 + per && b < nb; ++b) {
-      curB[b] = run;
-      run += hist[b];
-    }
-    return;
-  }
   // digit starts (every block; ndA <= CP_NAM, one value per thread of the first CP_NAM)
   const uint64_t tot = tid < ndA ? totA[tid] : 0;
   const uint64_t inc = wave_incl_sum<uint64_t>(tot);
@@ -439,6 +461,34 @@ __global__ __launch_bounds__(1024) void k_cp_cursors(const uint64_t* __restrict_
     }
   }
   __syncthreads();
+  if (curB) {   // pass B: bucket starts, four digits per wave (wave-uniform loops: full-wave scans)
+    const uint32_t nbk = nb / ndA;   // buckets per digit (2^sA)
+    for (uint32_t j = 0; j < CP_DB / 16; ++j) {
+      const uint32_t dd = blockIdx.x * CP_DB + wv * (CP_DB / 16) + j;
+      if (dd >= ndA) break;
+      uint64_t run = st[dd];
+      for (uint32_t c = 0; c < nbk; c += 256) {
+        const uint32_t i0 = c + 4 * lane;
+        const uint64_t b0 = (uint64_t)dd * nbk + i0;
+        uint64_t h[4], sum = 0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          h[i] = i0 + i < nbk ? hist[b0 + i] : 0;
+          sum += h[i];
+        }
+        const uint64_t inc = wave_incl_sum<uint64_t>(sum);
+        uint64_t e = run + inc - sum;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          if (i0 + i < nbk) {
+            curB[b0 + i] = e;
+            e += h[i];
+          }
+        run += ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(inc >> 32), 63) << 32) |
+               (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)inc, 63);
+      }
+    }
+  }
   const uint32_t dl = tid % CP_DB, g = tid / CP_DB, d = blockIdx.x * CP_DB + dl;
   if (d >= ndA) return;
   const uint32_t per = (nspan + CP_NG - 1) / CP_NG, w0 = g * per < nspan ? g * per : nspan;
@@ -727,7 +777,9 @@ __device__ __forceinline__ uint32_t win32(uint32_t w0, uint32_t w1, int k) {
 // Pre-pass of a slice: for every text span (one workgroup), the slice's bin counts (CB-bit LDS counters
 // as k_bucket_hist_spans) and its pass A digit counts.  REG: radix 2^2 in registers; else the LDS code
 // table (LBQ / HQ compile-time when given).
-template <int CB, int HB = -1, int LBQ = 0, int HQ = 0, bool REG = false>
+// ALL (REG): the slice is the whole sym space (single-GPU build, coarse histogram): no selection test,
+// and the add count of a full thread step is its 16 positions.
+template <int CB, int HB = -1, int LBQ = 0, int HQ = 0, bool REG = false, bool ALL = false>
 __global__ __launch_bounds__(BH_T, 1) void k_slice_hist_spans(const uint8_t* __restrict__ t, uint64_t n,
                                                               const uint16_t* __restrict__ lutk,
                                                               const uint64_t* __restrict__ skey, KeyedArgs g,
@@ -761,7 +813,7 @@ __global__ __launch_bounds__(BH_T, 1) void k_slice_hist_spans(const uint8_t* __r
   auto add = [&](uint32_t b) {   // b: the slice bin, < sl.nb
     if constexpr (NODRAIN) {
       atomicAdd(&H[b >> 2], 1u << (8 * (b & 3)));
-      ++kc;
+      if constexpr (!ALL) ++kc;
       return;
     }
     if (hb >= 0 && (b >> 16) != (uint32_t)hb) return;
@@ -808,14 +860,22 @@ __global__ __launch_bounds__(BH_T, 1) void k_slice_hist_spans(const uint8_t* __r
         if (full) {   // (split so the full body carries no per-position 64-bit bound test)
 #pragma unroll
           for (int k = 0; k < BH_PER; ++k) {
-            const uint32_t w = win32(c0, c1, k) - sl.wb;
-            if (w <= sl.wn1) add(w >> dsh);
+            if constexpr (ALL) {
+              add(win32(c0, c1, k) >> dsh);
+            } else {
+              const uint32_t w = win32(c0, c1, k) - sl.wb;
+              if (w <= sl.wn1) add(w >> dsh);
+            }
           }
+          if constexpr (ALL && NODRAIN) kc += BH_PER;
         } else {
 #pragma unroll
           for (int k = 0; k < BH_PER; ++k) {
             const uint32_t w = win32(c0, c1, k) - sl.wb;
-            if (w <= sl.wn1 && p0 + k < lim2) add(w >> dsh);
+            if (w <= sl.wn1 && p0 + k < lim2) {
+              add(w >> dsh);
+              if constexpr (ALL && NODRAIN) ++kc;
+            }
           }
         }
       } else {
@@ -834,7 +894,10 @@ __global__ __launch_bounds__(BH_T, 1) void k_slice_hist_spans(const uint8_t* __r
     }
     for (uint64_t p = p0 > lim ? p0 : lim; p < p0 + BH_PER && p < hi; ++p) {
       const uint32_t bin = (uint32_t)(SK[p - g.s_start] >> sl.bsh) - sl.base;
-      if (bin < sl.nb) add(bin);
+      if (bin < sl.nb) {
+        add(bin);
+        if constexpr (ALL && NODRAIN) ++kc;
+      }
     }
   };
   for (uint64_t base = lo; base < hi; base += PF * BH_TILE) {
@@ -1362,6 +1425,240 @@ __global__ __launch_bounds__(CP_T, 4) void k_slice_cpart_reg(uint64_t* __restric
     tg[tid] = gbv;
     __syncthreads();
     write_out(tot, hi256);
+  }
+}
+
+// Fused pass A of up to FS_N slices of one single-GPU build (n >= 2^32 - 1): one scan of T' keys every
+// position once for the whole group, instead of one scan per slice (each of which keyed all of T' to keep
+// a quarter of it).  The group's slices are contiguous and each starts at a pass A digit boundary (its
+// first bin a multiple of 2^sA), so a window's group digit (w >> dA) - gd0 indexes one count array for all
+// of them (u16 pairs: a unit has < 2^16 positions) and its slice follows from the digit bounds; round 1
+// keeps each kept position's slice (2 bits) next to the packed codes.  Then, slice by slice, the reserve /
+// round 2 / write-out of k_slice_cpart_reg, into the slice's own cursor rows and output.
+constexpr int FS_N = 4;
+struct FusedSel {
+  uint64_t* kout[FS_N];
+  unsigned long long* cur[FS_N];   // [span][CP_NAM] cursor rows of each slice's pre-pass
+  uint64_t mcap[FS_N];
+  uint32_t base[FS_N];             // the slice's first bin
+  uint32_t gd[FS_N + 1];           // group digits of slice s: [gd[s], gd[s + 1]), gd[0] = 0; ~0u past ns
+  uint32_t gd0;                    // the group's first absolute digit (base[0] >> sA)
+  int ns;
+};
+
+// G: sub-tiles per unit held in registers (g <= G; groups of <= 4 of every slice of the text have g <= 3)
+template <int G>
+__global__ __launch_bounds__(CP_T, 4) void k_slice_cpart_fused(uint64_t n, uint64_t span, TextKeySrc src, SliceSel sl,
+                                                               FusedSel fs, const unsigned long long* __restrict__ skip) {
+  constexpr int T = CP_T;
+  __shared__ uint64_t keys[CP_TILE + 8];   // round 1: the unit's text image; then the staged records
+  __shared__ uint8_t sdg[CP_TILE];
+  __shared__ uint32_t cnt[FS_N * CP_NAM / 2];   // u16 digit counters, two per word
+  __shared__ uint32_t tg[CP_NAM], wsum[CP_NAM / 64];
+  __shared__ uint16_t LP[256];
+  __shared__ uint64_t SK[72];
+  __shared__ uint32_t last_byte;
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  if (skip && *skip) return;   // a pre-pass overflowed: the slices run one by one instead
+  const uint64_t U = (uint64_t)SL_SUB * sl.g;
+  const uint32_t per = (uint32_t)(span / U), gx = blockIdx.x & 7u, k8 = blockIdx.x >> 3;
+  const uint64_t unit = (uint64_t)(gx + 8u * (k8 / per)) * per + k8 % per;
+  const uint64_t ubase = unit * U;
+  if (ubase >= n) return;   // past the last span (whole workgroup, before any barrier)
+  const uint64_t rowoff = (ubase / span) * CP_NAM;
+  const uint32_t nsub = (uint32_t)((n - ubase < U ? n - ubase : U) + SL_SUB - 1) / SL_SUB;
+  uint8_t* const img = reinterpret_cast<uint8_t*>(keys);
+  if (tid == 0) last_byte = src.text[n - 1];
+  if (tid < 256) LP[tid] = src.lutp[tid];
+  if (tid < 72) SK[tid] = src.skey[tid];
+  for (uint32_t i = tid; i < FS_N * CP_NAM / 2; i += T) cnt[i] = 0;
+  {   // the unit's text bytes [ubase - 16, ubase + U + 48) by DMA, as k_slice_cpart_reg
+    const uint32_t nins = (uint32_t)((U + 64 + 1023) / 1024);
+    for (uint32_t i = wv; i < nins; i += T / 64) {
+      const uint64_t off = (uint64_t)i * 1024 + lane * 16u;
+      if (ubase + off >= 16 && ubase + off <= n + 64)
+        __builtin_amdgcn_global_load_lds(src.text + (ubase + off - 16), img + (uint64_t)i * 1024, 16, 0, 0);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  const uint64_t lim = n < src.g.s_start ? n : src.g.s_start;
+  const int kbits = 2 * src.g.q, dsh = 32 - sl.DB, dA = dsh + sl.sA;
+  const uint32_t gdn = fs.gd[fs.ns];
+  // the group digit's slice (gd[j] = ~0u past ns)
+  auto slice_of = [&](uint32_t d) -> uint32_t {
+    return (d >= fs.gd[1] ? 1u : 0u) + (d >= fs.gd[2] ? 1u : 0u) + (d >= fs.gd[3] ? 1u : 0u);
+  };
+  auto count = [&](uint32_t d) { atomicAdd(&cnt[d >> 1], 1u << (16 * (d & 1u))); };
+  // ---- round 1: packed codes, kept positions (bit 2k) and their slices (bits 2k..2k+1), digit counts
+  uint32_t c[G][3], mv[G], sid[G], pcs = 0;
+#pragma unroll
+  for (int st = 0; st < G; ++st) {
+    mv[st] = sid[st] = 0;
+    c[st][0] = c[st][1] = c[st][2] = 0;
+    const uint64_t p0 = ubase + (uint64_t)st * SL_SUB + 16ull * tid;
+    if ((uint32_t)st >= nsub || p0 >= n) continue;
+    const uint32_t ib = 16u + (uint32_t)st * SL_SUB + 16u * tid;
+    const uint4* q4 = reinterpret_cast<const uint4*>(img + ib);
+    c[st][0] = pack16_2(q4[0], sl);
+    c[st][1] = pack16_2(q4[1], sl);
+    c[st][2] = pack16_2(q4[2], sl);
+    const uint32_t pb = reinterpret_cast<const uint32_t*>(img + ib)[-1] >> 24;
+    const uint32_t pc = p0 ? __builtin_amdgcn_perm(sl.th, sl.tl, (pb >> sl.ps) & 7u) & 3u : (uint32_t)LP[last_byte];
+    pcs |= pc << (2 * st);
+    const bool full = p0 + 16 <= lim;
+    uint32_t m = 0, sd = 0;
+#pragma unroll
+    for (int k = 0; k < CP_I; ++k) {
+      const uint32_t d = (win32(c[st][0], c[st][1], k) >> dA) - fs.gd0;
+      if (d < gdn && (full || p0 + k < lim)) {
+        m |= 1u << (2 * k);
+        sd |= slice_of(d) << (2 * k);
+        count(d);
+      }
+    }
+    for (uint64_t j = p0 > lim ? p0 : lim; j < p0 + 16 && j < n; ++j) {   // short suffixes: boundary keys
+      const uint32_t d = ((uint32_t)(SK[j - src.g.s_start] >> sl.bsh) >> sl.sA) - fs.gd0;
+      if (d < gdn) {
+        m |= 1u << (2 * (uint32_t)(j - p0));
+        sd |= slice_of(d) << (2 * (uint32_t)(j - p0));
+        count(d);
+      }
+    }
+    mv[st] = m;
+    sid[st] = sd;
+  }
+  const int Z = sl.bsh + sl.sA, pz = sl.pb2 + sl.pbits;
+  // ---- per slice: scan, reserve, stage, write (k_slice_cpart_reg's fast and dense paths)
+  for (int s = 0; s < fs.ns; ++s) {   // uniform
+    const uint32_t db = fs.gd[s], nd = fs.gd[s + 1] - db;
+    const uint64_t sbase = (uint64_t)fs.base[s] << sl.bsh;
+    const uint64_t wS = sbase << (64 - kbits);
+    const uint32_t spat = (uint32_t)s * 0x55555555u;
+    unsigned long long* const row = fs.cur[s] + rowoff;
+    uint64_t* const kout = fs.kout[s];
+    const uint64_t mcap = fs.mcap[s];
+    auto kept = [&](int st) -> uint32_t {   // bit 2k: position k of sub-tile st is in slice s
+      const uint32_t x = sid[st] ^ spat;
+      return ~(x | (x >> 1)) & mv[st] & 0x55555555u;
+    };
+    auto record_at = [&](int st, int k, uint64_t& rec) -> uint32_t {
+      const uint64_t j = ubase + (uint64_t)st * SL_SUB + 16ull * tid + (uint64_t)k;
+      const int sh = 32 - 2 * k;
+      const uint64_t s01 = ((uint64_t)c[st][0] << 32) | c[st][1], s12 = ((uint64_t)c[st][1] << 32) | c[st][2];
+      uint64_t wr = (((uint64_t)(uint32_t)(s01 >> sh) << 32) | (uint32_t)(s12 >> sh)) - wS;
+      if (j >= src.g.s_start) wr = (SK[j - src.g.s_start] - sbase) << (64 - kbits);
+      const uint32_t prv = (uint32_t)(((((uint64_t)((pcs >> (2 * st)) & 3u)) << 32) | c[st][0]) >> sh) & 3u;
+      rec = (((wr << (kbits - Z)) >> (64 - Z)) << pz) | ((uint64_t)prv << sl.pbits) | j;
+      return (uint32_t)(wr >> (64 - kbits + Z));
+    };
+    auto rank = [&](uint32_t d) -> uint32_t {   // d: the slice's digit
+      const uint32_t x = db + d, sh16 = 16u * (x & 1u);
+      return (atomicAdd(&cnt[x >> 1], 1u << sh16) >> sh16) & 0xFFFFu;
+    };
+    auto clear_mine = [&]() {   // the slice's counters to zero (the other half of a pair is another slice's)
+      if (tid < nd) atomicAnd(&cnt[(db + tid) >> 1], ~(0xFFFFu << (16u * ((db + tid) & 1u))));
+    };
+    auto scan = [&](uint32_t cu, uint32_t& total) {   // tg = exclusive digit starts; total
+      const uint32_t inc = wave_incl_sum<uint32_t>(cu);
+      if (lane == 63) wsum[wv] = inc;
+      __syncthreads();
+      uint32_t carry = 0;
+      total = 0;
+#pragma unroll
+      for (uint32_t w = 0; w < T / 64; ++w) {
+        carry += w < wv ? wsum[w] : 0u;
+        total += wsum[w];
+      }
+      tg[tid] = carry + inc - cu;
+    };
+    auto write_out = [&](uint32_t cnt_tile, uint32_t hi256) {
+      for (int i = 0; i < CP_I; ++i) {
+        const uint32_t q = (uint32_t)i * T + tid;
+        if (q < cnt_tile) {
+          const uint32_t d = (uint32_t)sdg[q] | (q >= hi256 ? 256u : 0u);
+          const uint32_t o = tg[d] + q;   // u32: tg = destination - tile start (mod 2^32)
+          if (o < mcap) kout[o] = keys[q];
+        }
+      }
+    };
+    __syncthreads();   // the previous slice's write-out has read keys / sdg / tg
+    const uint32_t cu = tid < nd ? (cnt[(db + tid) >> 1] >> (16u * ((db + tid) & 1u))) & 0xFFFFu : 0u;
+    uint32_t total;
+    scan(cu, total);
+    __syncthreads();   // every count read
+    clear_mine();
+    if (total <= (uint32_t)CP_TILE) {
+      const unsigned long long resv = cu ? atomicAdd(&row[tid], (unsigned long long)cu) : 0ull;
+      __syncthreads();
+#pragma unroll
+      for (int st = 0; st < G; ++st) {
+        uint32_t m = kept(st);
+        while (m) {   // two kept positions a trip: their slot atomics in flight together
+          const int k = __builtin_ctz(m) >> 1;
+          m &= m - 1;
+          const bool two = m != 0;
+          const int k2 = two ? __builtin_ctz(m) >> 1 : k;
+          m &= m - 1;
+          uint64_t rec, rec2;
+          const uint32_t d = record_at(st, k, rec);
+          const uint32_t d2 = record_at(st, k2, rec2);
+          uint32_t f = tg[d] + rank(d);
+          uint32_t f2 = two ? tg[d2] + rank(d2) : 0u;
+          f = f < (uint32_t)CP_TILE ? f : (uint32_t)CP_TILE - 1;   // (only a count mismatch overruns)
+          keys[f] = rec;
+          sdg[f] = (uint8_t)d;
+          if (two) {
+            f2 = f2 < (uint32_t)CP_TILE ? f2 : (uint32_t)CP_TILE - 1;
+            keys[f2] = rec2;
+            sdg[f2] = (uint8_t)d2;
+          }
+        }
+      }
+      __syncthreads();
+      const uint32_t hi256 = tg[256];
+      const uint32_t gbv = (uint32_t)(resv - tg[tid]);
+      __syncthreads();
+      tg[tid] = gbv;
+      __syncthreads();
+      write_out(total, hi256);
+      continue;
+    }
+    // dense unit for this slice: each sub-tile counted, reserved, staged and written on its own
+#pragma unroll
+    for (int st = 0; st < G; ++st) {
+      if ((uint32_t)st >= nsub) break;   // uniform
+      __syncthreads();   // the previous write-out has read keys / tg; counters clear
+      for (uint32_t m = kept(st); m; m &= m - 1) {
+        uint64_t rec;
+        const uint32_t d = record_at(st, __builtin_ctz(m) >> 1, rec);
+        atomicAdd(&cnt[(db + d) >> 1], 1u << (16u * ((db + d) & 1u)));
+      }
+      __syncthreads();
+      const uint32_t cc = tid < nd ? (cnt[(db + tid) >> 1] >> (16u * ((db + tid) & 1u))) & 0xFFFFu : 0u;
+      const unsigned long long g = cc ? atomicAdd(&row[tid], (unsigned long long)cc) : 0ull;
+      uint32_t tot;
+      scan(cc, tot);
+      __syncthreads();
+      clear_mine();
+      __syncthreads();
+      for (uint32_t m = kept(st); m; m &= m - 1) {
+        uint64_t rec;
+        const uint32_t d = record_at(st, __builtin_ctz(m) >> 1, rec);
+        const uint32_t f = tg[d] + rank(d);
+        keys[f] = rec;
+        sdg[f] = (uint8_t)d;
+      }
+      __syncthreads();
+      const uint32_t hi256 = tg[256];
+      const uint32_t gbv = (uint32_t)(g - tg[tid]);
+      __syncthreads();
+      tg[tid] = gbv;
+      __syncthreads();
+      write_out(tot, hi256);
+      __syncthreads();
+      clear_mine();
+    }
   }
 }
 
@@ -3022,13 +3319,13 @@ int cursor_partition(Index& ix, uint64_t n, int D, int bitlo, uint64_t kbias, co
   // pre-pass (exact: 2^17 buckets as two u16 runs over the bucket halves, after a u8 overflow)
   // pre-pass with the code width and window fixed at compile time where they are 2 bits x 9 / 8 bits x 3
   auto prepass = [&](bool exact) {
-    HK_HIP(hipMemsetAsync(d_drain, 0, (uint64_t)nb * 8, s));
+    HK_HIP(hipMemsetAsync(d_drain, 0, (uint64_t)nb * 16, s));   // drain, then hist (bucket_reduce adds)
     HK_HIP(hipMemsetAsync(d_ovf, 0, 8, s));
     TimedLaunch t(ix.timer, "sa_bucket_hist", (double)n * (tks ? (exact ? 2 : 1) : 8));
     if (tks && D > 16 && !exact) {   // 2^17 buckets: u8 counters (drained at 128)
       const int lbk = 31 - __builtin_clz((uint32_t)tks->g.Rk);
       if (packed && pk->reg) {   // register scan, undrained u8 counters (checked; exact recount on a wrap)
-        k_slice_hist_spans<8, -1, 2, 0, true><<<nspan, BH_T, 0, s>>>(tks->text, n, tks->lutk, tks->skey, tks->g,
+        k_slice_hist_spans<8, -1, 2, 0, true, true><<<nspan, BH_T, 0, s>>>(tks->text, n, tks->lutk, tks->skey, tks->g,
                                                                      pk->rsl, D, d_part, d_drain, d_spanc, span,
                                                                      d_ovf);
       } else {
@@ -3054,12 +3351,12 @@ int cursor_partition(Index& ix, uint64_t n, int D, int bitlo, uint64_t kbias, co
       k_key_hist_spans<<<nspan, BH_T, 0, s>>>(kp[0], n, bitlo, kbias, D, sA, d_part, d_drain, d_spanc, span);
     }
     HK_HIP(hipGetLastError());
-    k_bucket_reduce<<<(nb + 255) / 256, 256, 0, s>>>(d_part, d_drain, nspan, stride, nb, d_hist);
+    bucket_reduce(d_part, d_drain, nspan, stride, nb, d_hist, s);
     HK_HIP(hipGetLastError());
     const uint32_t nblkA = (ndA + CP_DB - 1) / CP_DB;
     k_cp_colsum<<<nblkA, 1024, 0, s>>>(d_spanc, nspan, ndA, d_gpre, d_totA);
     HK_HIP(hipGetLastError());
-    k_cp_cursors<<<nblkA + (D > 8 ? 1 : 0), 1024, 0, s>>>(d_hist, d_spanc, d_gpre, nspan, nb, ndA, d_curA,
+    k_cp_cursors<<<nblkA, 1024, 0, s>>>(d_hist, d_spanc, d_gpre, nspan, nb, ndA, d_curA,
                                                           D > 8 ? d_curB : nullptr, d_totA, d_startA);
     HK_HIP(hipGetLastError());
   };
@@ -3255,7 +3552,7 @@ void shard_coarse_hist(Index& ix, uint64_t lo, uint64_t hi, uint64_t* d_hist) {
     uint32_t* d_part = ix.cp_part.as<uint32_t>();
     unsigned long long* d_ovf = reinterpret_cast<unsigned long long*>(d_part + (uint64_t)rn * (65536 + CP_NAM));
     HK_HIP(hipMemsetAsync(d_ovf, 0, 8, s));
-    k_slice_hist_spans<8, -1, 2, 0, true><<<rn, BH_T, 0, s>>>(
+    k_slice_hist_spans<8, -1, 2, 0, true, true><<<rn, BH_T, 0, s>>>(
         ix.text.as<uint8_t>() + lo, hi - lo, reinterpret_cast<const uint16_t*>(small + 2560),
         reinterpret_cast<const uint64_t*>(small + 3584), kr, rs, 16, d_part, d_drain, d_part + (uint64_t)rn * 65536,
         rspan, d_ovf);
@@ -3412,6 +3709,59 @@ SlicePlan plan_slice(Index& ix, uint32_t c_lo, uint32_t c_hi, bool u64pos) {
 
 }  // namespace
 
+// one slice's pre-pass outputs (drain and hist contiguous: one memset clears both)
+struct SliceCur {
+  unsigned long long* drain;
+  uint64_t* hist;
+  unsigned long long* curA;
+  unsigned long long* curB;   // nullptr: no pass B (sA = 0)
+  uint64_t* totA;
+  uint64_t* startA;
+  unsigned long long* ovf;
+  uint64_t* gpre;
+};
+
+// The slice's pre-pass over the whole text: its bin counts and per-span pass A digit counts (the span
+// counters and digit sums in d_part / d_spanc, consumed here), then both passes' cursors.  A u8
+// counter wrap raises *c.ovf (the caller clears it): the exact recount runs with `exact`.
+static void slice_prepass(Index& ix, const SlicePlan& P, const TextKeySrc& tks, uint64_t span, uint32_t nspan,
+                          uint32_t* d_part, uint32_t* d_spanc, const SliceCur& c, bool exact) {
+  hipStream_t s = ix.stream;
+  const uint64_t n = ix.n;
+  const SliceSel& sl = P.sl;
+  const int D = P.D, sA = sl.sA;
+  const uint32_t nb2 = 1u << D, ndA = 1u << (D - sA);
+  HK_HIP(hipMemsetAsync(c.drain, 0, (uint64_t)nb2 * 16, s));   // drain, then hist (bucket_reduce adds)
+  TimedLaunch t(ix.timer, "shard_slice_hist", (double)n * (exact ? 2 : 1));
+  const KeyedArgs& g = tks.g;
+  const bool reg = P.reg;
+  if (D > 16 && !exact) {
+    auto kern = k_slice_hist_spans<8>;
+    if (reg) kern = k_slice_hist_spans<8, -1, 2, 0, true>;
+    else if (P.lb == 2 && sl.hq == 9) kern = k_slice_hist_spans<8, -1, 2, 9>;
+    else if (P.lb == 2 && sl.hq == 10) kern = k_slice_hist_spans<8, -1, 2, 10>;
+    kern<<<nspan, BH_T, 0, s>>>(tks.text, n, tks.lutk, tks.skey, g, sl, D, d_part, c.drain, d_spanc, span, c.ovf);
+  } else if (D > 16) {
+    auto k0 = reg ? k_slice_hist_spans<16, 0, 2, 0, true> : k_slice_hist_spans<16, 0>;
+    auto k1 = reg ? k_slice_hist_spans<16, 1, 2, 0, true> : k_slice_hist_spans<16, 1>;
+    k0<<<nspan, BH_T, 0, s>>>(tks.text, n, tks.lutk, tks.skey, g, sl, D, d_part, c.drain, d_spanc, span, c.ovf);
+    k1<<<nspan, BH_T, 0, s>>>(tks.text, n, tks.lutk, tks.skey, g, sl, D, d_part, c.drain, d_spanc, span, c.ovf);
+  } else {
+    auto kern = k_slice_hist_spans<16>;
+    if (reg) kern = k_slice_hist_spans<16, -1, 2, 0, true>;
+    else if (P.lb == 2 && sl.hq == 9) kern = k_slice_hist_spans<16, -1, 2, 9>;
+    else if (P.lb == 2 && sl.hq == 10) kern = k_slice_hist_spans<16, -1, 2, 10>;
+    kern<<<nspan, BH_T, 0, s>>>(tks.text, n, tks.lutk, tks.skey, g, sl, D, d_part, c.drain, d_spanc, span, c.ovf);
+  }
+  HK_HIP(hipGetLastError());
+  bucket_reduce(d_part, c.drain, nspan, nb2, nb2, c.hist, s);
+  const uint32_t nblkA = (ndA + CP_DB - 1) / CP_DB;
+  k_cp_colsum<<<nblkA, 1024, 0, s>>>(d_spanc, nspan, ndA, c.gpre, c.totA);
+  HK_HIP(hipGetLastError());
+  k_cp_cursors<<<nblkA, 1024, 0, s>>>(c.hist, d_spanc, c.gpre, nspan, nb2, ndA, c.curA, c.curB, c.totA, c.startA);
+  HK_HIP(hipGetLastError());
+}
+
 // The slice's cursor partition (section 1c): pre-pass over the whole text counting the slice's bins
 // (and its units' pass A digits), cursors, fused pass A from the text, pass B.  Records / key planes
 // end in slot 0 (D > 8) or 1; hist gets the bin counts.
@@ -3457,39 +3807,10 @@ static int cursor_partition_slice(Index& ix, const SlicePlan& P, const TextKeySr
     pkr.ndA = ndA;
     pkr.klw = P.pb + sl.bsh + sA;
   }
+  const SliceCur cur{d_drain, d_hist, d_curA, sA ? d_curB : nullptr, d_totA, d_startA, d_ovf, d_gpre};
   auto prepass = [&](bool exact) {
-    HK_HIP(hipMemsetAsync(d_drain, 0, (uint64_t)nb2 * 8, s));
     HK_HIP(hipMemsetAsync(d_ovf, 0, 8, s));
-    TimedLaunch t(ix.timer, "shard_slice_hist", (double)n * (exact ? 2 : 1));
-    const KeyedArgs& g = tks.g;
-    const bool reg = P.reg;
-    if (D > 16 && !exact) {
-      auto kern = k_slice_hist_spans<8>;
-      if (reg) kern = k_slice_hist_spans<8, -1, 2, 0, true>;
-      else if (P.lb == 2 && sl.hq == 9) kern = k_slice_hist_spans<8, -1, 2, 9>;
-      else if (P.lb == 2 && sl.hq == 10) kern = k_slice_hist_spans<8, -1, 2, 10>;
-      kern<<<nspan, BH_T, 0, s>>>(tks.text, n, tks.lutk, tks.skey, g, sl, D, d_part, d_drain, d_spanc, span, d_ovf);
-    } else if (D > 16) {
-      auto k0 = reg ? k_slice_hist_spans<16, 0, 2, 0, true> : k_slice_hist_spans<16, 0>;
-      auto k1 = reg ? k_slice_hist_spans<16, 1, 2, 0, true> : k_slice_hist_spans<16, 1>;
-      k0<<<nspan, BH_T, 0, s>>>(tks.text, n, tks.lutk, tks.skey, g, sl, D, d_part, d_drain, d_spanc, span, d_ovf);
-      k1<<<nspan, BH_T, 0, s>>>(tks.text, n, tks.lutk, tks.skey, g, sl, D, d_part, d_drain, d_spanc, span, d_ovf);
-    } else {
-      auto kern = k_slice_hist_spans<16>;
-      if (reg) kern = k_slice_hist_spans<16, -1, 2, 0, true>;
-      else if (P.lb == 2 && sl.hq == 9) kern = k_slice_hist_spans<16, -1, 2, 9>;
-      else if (P.lb == 2 && sl.hq == 10) kern = k_slice_hist_spans<16, -1, 2, 10>;
-      kern<<<nspan, BH_T, 0, s>>>(tks.text, n, tks.lutk, tks.skey, g, sl, D, d_part, d_drain, d_spanc, span, d_ovf);
-    }
-    HK_HIP(hipGetLastError());
-    k_bucket_reduce<<<(nb2 + 255) / 256, 256, 0, s>>>(d_part, d_drain, nspan, nb2, nb2, d_hist);
-    HK_HIP(hipGetLastError());
-    const uint32_t nblkA = (ndA + CP_DB - 1) / CP_DB;
-    k_cp_colsum<<<nblkA, 1024, 0, s>>>(d_spanc, nspan, ndA, d_gpre, d_totA);
-    HK_HIP(hipGetLastError());
-    k_cp_cursors<<<nblkA + (sA ? 1 : 0), 1024, 0, s>>>(d_hist, d_spanc, d_gpre, nspan, nb2, ndA, d_curA,
-                                                       sA ? d_curB : nullptr, d_totA, d_startA);
-    HK_HIP(hipGetLastError());
+    slice_prepass(ix, P, tks, span, nspan, d_part, d_spanc, cur, exact);
   };
   const int outA = sA ? 1 : 0;
   auto passA = [&]() {
@@ -3584,12 +3905,250 @@ static int cursor_partition_slice(Index& ix, const SlicePlan& P, const TextKeySr
   return 0;
 }
 
+// ---------------------------------------------------------------- fused pass A of single-GPU slices
+// build_sa_slices runs the slices of a text one after another; each slice's pass A (k_slice_cpart_reg)
+// keys all of T' to keep ~1/k of it.  For up to FS_N slices with one geometry (same bin width, radix
+// 2^2 packed records, first bins on pass A digit boundaries) the pre-passes run first, each into its
+// own cursor set, then k_slice_cpart_fused keys T' once and scatters every suffix into its slice's
+// records; each slice later takes its pass B from them (fused_pass_b).
+struct FusedSlice {
+  uint32_t c_lo = 0, c_hi = 0;
+  uint64_t m = 0;
+  SlicePlan P;
+  uint64_t* kA = nullptr;                // pass A records, grouped by the slice's digit
+  unsigned long long* curB = nullptr;    // pass B cursors (bucket starts)
+  uint64_t* startA = nullptr;            // digit starts (pass B regions)
+  std::vector<uint64_t> hist, totA;      // bin counts, digit totals
+};
+struct FusedState {
+  std::vector<FusedSlice> sl;
+  DevBuf recs, ws;
+  HostBuf hb;
+};
+
+static TextKeySrc slice_tks(Index& ix, const KeyGeom& kk, int lb) {
+  const uint8_t* small = ix.small.as<uint8_t>();
+  const KeyChunks kch = key_chunks(kk.Rk, kk.q);
+  KeyedArgs ka{kk.Rk, kch.Rck, kch.Rlast, kk.s_start, kk.q, kch.ck, kk.pb, 0, lb};
+  return TextKeySrc{ix.text.as<uint8_t>(), ix.n, reinterpret_cast<const uint16_t*>(small + 2560),
+                    reinterpret_cast<const uint16_t*>(small + 4608), reinterpret_cast<const uint64_t*>(small + 3584),
+                    ka};
+}
+
+static void prev_code_table(const KeyGeom& kk, const PkGeom& pg, uint16_t* lutp2) {
+  for (int b = 0; b < 256; ++b) lutp2[b] = pg.tcode < 0 ? kk.lutp[b] : (kk.kflag[b] ? kk.kdig[b] : 0);
+}
+
+static FusedSlice* fused_slice(Index& ix, uint32_t c_lo, uint32_t c_hi) {
+  if (!ix.fused) return nullptr;
+  for (FusedSlice& f : static_cast<FusedState*>(ix.fused.get())->sl)
+    if (f.c_lo == c_lo && f.c_hi == c_hi) return &f;
+  return nullptr;
+}
+
+bool slices_fuse(Index& ix, const std::vector<uint32_t>& B, const std::vector<uint64_t>& below, int r0, int r1,
+                 bool u64pos) {
+  ix.fused.reset();   // (the previous group's records)
+  const int ns = r1 - r0;
+  const uint64_t n = ix.n;
+  hipStream_t s = ix.stream;
+  if (ns < 2 || ns > FS_N || getenv("HKCSA_SL_TRACE")) return false;   // (the trace stamps the per-slice kernel)
+  auto st = std::make_shared<FusedState>();
+  st->sl.resize(ns);
+  uint64_t mmax = 0, msum = 0;
+  for (int i = 0; i < ns; ++i) {
+    FusedSlice& f = st->sl[i];
+    f.c_lo = B[r0 + i];
+    f.c_hi = B[r0 + i + 1];
+    f.m = below[r0 + i + 1] - below[r0 + i];
+    if (!f.m) return false;
+    f.P = plan_slice(ix, f.c_lo, f.c_hi, u64pos);
+    const SlicePlan& P = f.P;
+    if (!P.packed || !P.reg || P.lb != 2 || P.sl.sA != 8 || P.D <= 8 || P.sl.base % 256 || P.sl.nb % 256) return false;
+    if (i) {
+      const SlicePlan& Q = st->sl[0].P;
+      const SliceSel &a = P.sl, &b = Q.sl;
+      if (P.kk.q != Q.kk.q || P.kk.sym_bits != Q.kk.sym_bits || P.kk.pb != Q.kk.pb || P.kk.s_start != Q.kk.s_start ||
+          P.kk.tcode != Q.kk.tcode || P.pb != Q.pb || P.uhb != Q.uhb || a.DB != b.DB || a.bsh != b.bsh ||
+          a.hq != b.hq || a.wdrop != b.wdrop || a.pbits != b.pbits || a.pb2 != b.pb2 || a.tl != b.tl ||
+          a.th != b.th || a.ps != b.ps || P.pg.pbits != Q.pg.pbits || P.pg.pb2 != Q.pg.pb2 ||
+          P.pg.tcode != Q.pg.tcode || P.pg.phb != Q.pg.phb)
+        return false;
+      if (a.base != st->sl[i - 1].P.sl.base + st->sl[i - 1].P.sl.nb) return false;   // contiguous
+    }
+    mmax = std::max(mmax, f.m);
+    msum += f.m;
+  }
+  // one unit size for the group (the spans, hence the cursor rows, are shared)
+  uint32_t g = (uint32_t)std::floor(0.9 * (double)n / (double)mmax);
+  g = std::max<uint32_t>(1, std::min<uint32_t>(g, (uint32_t)SL_G));
+  for (FusedSlice& f : st->sl) f.P.sl.g = g;
+  const uint64_t U = (uint64_t)SL_SUB * g;
+  const uint64_t Lq = g % 2 ? 2 * U : U;
+  const uint64_t span = ceil_div(ceil_div(n, Lq), 256) * Lq;
+  const uint32_t nspan = (uint32_t)ceil_div(n, span);
+  // cursor sets: drain, hist [nb2 each], curA [nspan][CP_NAM], curB [nb2], totA, startA [CP_NAM + 1], gpre
+  auto set_words = [&](const SlicePlan& P) -> uint64_t {
+    const uint64_t nb2 = 1ull << P.D;
+    return 3 * nb2 + (uint64_t)nspan * CP_NAM + 2 * (CP_NAM + 1) + (uint64_t)CP_NG * CP_NAM + 16;
+  };
+  uint64_t wsw = 16, hw = 16;
+  for (const FusedSlice& f : st->sl) {
+    wsw += set_words(f.P);
+    hw += (1ull << f.P.D) + 2 * (CP_NAM + 1);
+  }
+  // memory: the group's records next to one slice's workspace (keys / values planes, bucket items)
+  {
+    size_t fr = 0, tot = 0;
+    HK_HIP(hipMemGetInfo(&fr, &tot));
+    const uint64_t need = msum * 8 + wsw * 8 + mmax * 40 + (1ull << 30);
+    if ((double)need > 0.9 * (double)fr) return false;
+  }
+  const SlicePlan& P0 = st->sl[0].P;
+  upload_geometry(ix, P0.kk);
+  TextKeySrc tks = slice_tks(ix, P0.kk, P0.lb);
+  uint32_t maxnb2 = 0;
+  for (const FusedSlice& f : st->sl) maxnb2 = std::max(maxnb2, 1u << f.P.D);
+  ix.cp_part.ensure((uint64_t)nspan * maxnb2 * 4 + (uint64_t)nspan * CP_NAM * 4 + 16);
+  uint32_t* d_part = ix.cp_part.as<uint32_t>();
+  uint32_t* d_spanc = d_part + (uint64_t)nspan * maxnb2;
+  st->ws.ensure(wsw * 8);
+  st->hb.ensure(hw * 8 + 64);
+  uint64_t* w = st->ws.as<uint64_t>();
+  unsigned long long* d_ovf = reinterpret_cast<unsigned long long*>(w);
+  HK_HIP(hipMemsetAsync(d_ovf, 0, 8, s));
+  w += 16;
+  std::vector<SliceCur> cur(ns);
+  for (int i = 0; i < ns; ++i) {
+    const SlicePlan& P = st->sl[i].P;
+    const uint64_t nb2 = 1ull << P.D;
+    SliceCur& c = cur[i];
+    c.drain = reinterpret_cast<unsigned long long*>(w);
+    c.hist = w + nb2;
+    c.curA = reinterpret_cast<unsigned long long*>(w + 2 * nb2);
+    c.curB = c.curA + (uint64_t)nspan * CP_NAM;
+    c.totA = reinterpret_cast<uint64_t*>(c.curB + nb2);
+    c.startA = c.totA + (CP_NAM + 1);
+    c.gpre = c.startA + (CP_NAM + 1);
+    c.ovf = d_ovf;
+    w += set_words(P);
+    st->sl[i].curB = c.curB;
+    st->sl[i].startA = c.startA;
+    slice_prepass(ix, P, tks, span, nspan, d_part, d_spanc, c, false);
+  }
+  // counts back behind an event while pass A runs
+  uint64_t* h = st->hb.as<uint64_t>();
+  std::vector<uint64_t*> h_hist(ns), h_tot(ns);
+  hipEvent_t ev_pre, ev_cnt;
+  HK_HIP(hipEventCreateWithFlags(&ev_pre, hipEventDisableTiming));
+  HK_HIP(hipEventCreateWithFlags(&ev_cnt, hipEventDisableTiming));
+  if (!ix.aux_stream) HK_HIP(hipStreamCreateWithFlags(&ix.aux_stream, hipStreamNonBlocking));
+  HK_HIP(hipEventRecord(ev_pre, s));
+  HK_HIP(hipStreamWaitEvent(ix.aux_stream, ev_pre, 0));
+  for (int i = 0; i < ns; ++i) {
+    const uint64_t nb2 = 1ull << st->sl[i].P.D;
+    h_hist[i] = h;
+    h_tot[i] = h + nb2;
+    h += nb2 + 2 * (CP_NAM + 1);
+    HK_HIP(hipMemcpyAsync(h_hist[i], cur[i].hist, nb2 * 8, hipMemcpyDeviceToHost, ix.aux_stream));
+    HK_HIP(hipMemcpyAsync(h_tot[i], cur[i].totA, (CP_NAM + 1) * 8, hipMemcpyDeviceToHost, ix.aux_stream));
+  }
+  uint64_t* h_ovf = h;
+  HK_HIP(hipMemcpyAsync(h_ovf, d_ovf, 8, hipMemcpyDeviceToHost, ix.aux_stream));
+  HK_HIP(hipEventRecord(ev_cnt, ix.aux_stream));
+  // pass A of the group
+  st->recs.ensure(msum * 8 + 16);
+  FusedSel fs{};
+  fs.ns = ns;
+  fs.gd0 = P0.sl.base >> 8;
+  uint64_t off = 0;
+  for (int i = 0; i < ns; ++i) {
+    FusedSlice& f = st->sl[i];
+    f.kA = st->recs.as<uint64_t>() + off;
+    off += f.m;
+    fs.kout[i] = f.kA;
+    fs.cur[i] = cur[i].curA;
+    fs.mcap[i] = f.m;
+    fs.base[i] = f.P.sl.base;
+    fs.gd[i] = (f.P.sl.base >> 8) - fs.gd0;
+  }
+  fs.gd[ns] = ((st->sl[ns - 1].P.sl.base + st->sl[ns - 1].P.sl.nb) >> 8) - fs.gd0;
+  for (int i = ns + 1; i <= FS_N; ++i) fs.gd[i] = ~0u;
+  for (int i = ns; i < FS_N; ++i) {
+    fs.kout[i] = nullptr;
+    fs.cur[i] = nullptr;
+  }
+  constexpr uint64_t kLp2Off = (9 + 2 * CP_NAM + 16) * 4;   // (cursor_partition_slice's table slot)
+  ix.cp_tiles.ensure(kLp2Off + 512);
+  ix.cp_host.ensure(512 + 64);
+  uint16_t* h_lp2 = ix.cp_host.as<uint16_t>();
+  prev_code_table(P0.kk, P0.pg, h_lp2);
+  uint16_t* d_lp2 = reinterpret_cast<uint16_t*>(ix.cp_tiles.as<uint8_t>() + kLp2Off);
+  HK_HIP(hipMemcpyAsync(d_lp2, h_lp2, 512, hipMemcpyHostToDevice, s));
+  TextKeySrc tks2 = tks;
+  tks2.lutp = d_lp2;
+  tks2.g.pb = P0.pg.pb2;
+  {
+    TimedLaunch t(ix.timer, "shard_slice_part", (double)n + (double)msum * 8);
+    const unsigned grid = (unsigned)(8 * ceil_div(nspan, 8u) * (span / U));
+    if (g <= 4) k_slice_cpart_fused<4><<<grid, CP_T, 0, s>>>(n, span, tks2, P0.sl, fs, d_ovf);
+    else k_slice_cpart_fused<SL_G><<<grid, CP_T, 0, s>>>(n, span, tks2, P0.sl, fs, d_ovf);
+    HK_HIP(hipGetLastError());
+  }
+  const hipError_t we = hipEventSynchronize(ev_cnt);
+  (void)hipEventDestroy(ev_pre);
+  (void)hipEventDestroy(ev_cnt);
+  HK_HIP(we);
+  HK_HIP(hipStreamSynchronize(s));   // (h_lp2 lives in cp_host, which the slices reuse)
+  if (*h_ovf) return false;   // a u8 counter wrapped: the slices run one by one (exact recounts)
+  for (int i = 0; i < ns; ++i) {
+    FusedSlice& f = st->sl[i];
+    const uint32_t nb2 = 1u << f.P.D, ndA = 1u << (f.P.D - 8);
+    f.hist.assign(h_hist[i], h_hist[i] + nb2);
+    f.totA.assign(h_tot[i], h_tot[i] + ndA);
+    uint64_t tsum = 0, hsum = 0;
+    for (uint64_t x : f.totA) tsum += x;
+    for (uint64_t x : f.hist) hsum += x;
+    if (tsum != f.m || hsum != f.m) throw ApiError{-7, "fused slices: bin counts do not match the slice size"};
+  }
+  ix.fused = st;
+  return true;
+}
+
+// pass B of a fused slice (its pass A ran in slices_fuse): records land in kp[0]
+static int fused_pass_b(Index& ix, FusedSlice& f, uint64_t m, uint64_t* kp[2], std::vector<uint64_t>& hist,
+                        PackedRecs& pkr) {
+  hipStream_t s = ix.stream;
+  const SlicePlan& P = f.P;
+  const SliceSel& sl = P.sl;
+  const uint32_t ndA = 1u << (P.D - sl.sA);
+  pkr.startA = f.startA;
+  pkr.ndA = ndA;
+  pkr.klw = P.pb + sl.bsh + sl.sA;
+  hist = f.hist;
+  ix.info[0] += 1;
+  ix.cp_tiles.ensure((9 + 2 * CP_NAM + 16) * 4 + 512);
+  ix.cp_host.ensure((9 + 2 * CP_NAM) * 4 + 64);
+  uint32_t* d_gtab = ix.cp_tiles.as<uint32_t>();
+  uint32_t* h_gtab = ix.cp_host.as<uint32_t>();
+  const uint64_t maxl = deal_regions(ix, f.totA.data(), ndA, CP_TILE, h_gtab, d_gtab);
+  TimedLaunch t(ix.timer, "radix_part", (double)m * 2 * 8);
+  k_cpart<2, 0, 256, CP_T, true, true, true><<<(unsigned)(8 * maxl), CP_T, 0, s>>>(
+      f.kA, nullptr, kp[0], nullptr, m, P.pg.pbits + P.pg.pb2 + sl.bsh, 0, f.curB, d_gtab, f.startA, 0,
+      TextKeySrc{}, P.pg.pbits);
+  HK_HIP(hipGetLastError());
+  ix.info[0] += 1;
+  return 0;
+}
+
 // One sharded slice under the keyed coarse scheme: the coarse buckets [c_lo, c_hi), m suffixes.
 template <typename V>
 void build_slice_keyed(Index& ix, uint32_t c_lo, uint32_t c_hi, uint64_t m) {
   hipStream_t s = ix.stream;
   const uint64_t n = ix.n;
-  SlicePlan P = plan_slice(ix, c_lo, c_hi, sizeof(V) == 8);
+  FusedSlice* const fz = fused_slice(ix, c_lo, c_hi);
+  if (fz && fz->m != m) throw ApiError{-7, "fused slice: size mismatch"};
+  SlicePlan P = fz ? fz->P : plan_slice(ix, c_lo, c_hi, sizeof(V) == 8);
   const KeyGeom& kk = P.kk;
   upload_geometry(ix, kk);
   ix.info[3] = (uint64_t)kk.q;
@@ -3602,12 +4161,7 @@ void build_slice_keyed(Index& ix, uint32_t c_lo, uint32_t c_hi, uint64_t m) {
     if (g > (P.reg ? (uint32_t)SL_G : 64u)) g = P.reg ? (uint32_t)SL_G : 64u;   // register kernel: <= SL_G
     P.sl.g = g;
   }
-  const uint8_t* small = ix.small.as<uint8_t>();
-  const KeyChunks kch = key_chunks(kk.Rk, kk.q);
-  KeyedArgs ka{kk.Rk, kch.Rck, kch.Rlast, kk.s_start, kk.q, kch.ck, kk.pb, 0, P.lb};
-  const TextKeySrc tks{ix.text.as<uint8_t>(), n, reinterpret_cast<const uint16_t*>(small + 2560),
-                       reinterpret_cast<const uint16_t*>(small + 4608), reinterpret_cast<const uint64_t*>(small + 3584),
-                       ka};
+  const TextKeySrc tks = slice_tks(ix, kk, P.lb);
   for (int i = 0; i < 2; ++i) {
     ix.keys[i].ensure(m * 8 + 16);
     ix.vals[i].ensure(m * sizeof(V) + 16);   // u32 here; the tie refinement sorts V values in them
@@ -3617,13 +4171,13 @@ void build_slice_keyed(Index& ix, uint32_t c_lo, uint32_t c_hi, uint64_t m) {
   PackedRecs pkr;
   if (P.packed) {
     pkr.g = P.pg;
-    for (int b = 0; b < 256; ++b) pkr.lutp2[b] = pkr.g.tcode < 0 ? kk.lutp[b] : (kk.kflag[b] ? kk.kdig[b] : 0);
+    prev_code_table(kk, pkr.g, pkr.lutp2);
     pkr.kfull = kp[1];
     pkr.vfull = vp[1];
     pkr.uhb = P.uhb;
   }
   std::vector<uint64_t> hist;
-  const int slot = cursor_partition_slice(ix, P, tks, m, kp, vp, hist, pkr);
+  const int slot = fz ? fused_pass_b(ix, *fz, m, kp, hist, pkr) : cursor_partition_slice(ix, P, tks, m, kp, vp, hist, pkr);
   const int sbx = P.sl.bsh + P.D;   // bits of the slice-relative sym field
   const int lhb = P.packed ? P.uhb : P.hb;
   uint64_t hmax = 0;

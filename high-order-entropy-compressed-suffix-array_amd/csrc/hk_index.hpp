@@ -2,6 +2,7 @@
 #pragma once
 
 #include <cstring>
+#include <memory>
 #include <utility>
 
 #include "hk_sort.hpp"
@@ -148,6 +149,7 @@ struct Index {
   bool sharded = false;
   bool sa_pos64 = false;       // sharded slices of texts with n >= 2^32 hold u64 positions
   bool slices_local = false;   // build_sa_slices: the slices' doubling updates one local ISA (no exchange)
+  std::shared_ptr<void> fused;  // build_sa_slices: a group's fused pass A (records + cursors per slice)
   uint64_t shard_lo = 0, shard_hi = 0;
   std::vector<uint64_t> shard_bounds;   // SA slice starts of every rank (+ n), from the RCCL build
 
@@ -258,6 +260,11 @@ bool bucket_sort_slice(Index& ix, const KeyGeom& kg, uint64_t m, int hb, const S
 int shard_keyed_lb(Index& ix);                                               // lb, 0: scheme not applicable
 bool shard_keyed(Index& ix);                                                 // the keyed scheme applies
 void shard_coarse_hist(Index& ix, uint64_t lo, uint64_t hi, uint64_t* d_hist);   // exact, 65536 bins, [lo, hi)
+// build_sa_slices: one fused pass A over T' for the slices [r0, r1) (coarse splitters B, SA bounds
+// below); false (nothing kept) when the group does not qualify, else ix.fused holds the slices' records
+// and cursors until build_slice_keyed consumes them
+bool slices_fuse(Index& ix, const std::vector<uint32_t>& B, const std::vector<uint64_t>& below, int r0, int r1,
+                 bool u64pos);
 // SA + BWT of the slice of coarse buckets [c_lo, c_hi) (m suffixes): fused selection + cursor partition
 // over the whole text, LDS bucket sorts, tie refinement (ties outlasting the chunk rounds left pending)
 template <typename V>

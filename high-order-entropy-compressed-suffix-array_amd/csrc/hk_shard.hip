@@ -1031,12 +1031,14 @@ void build_sa_slices(Index& ix, int k) {
       ix.sharded = false;
       for (DevBuf* b : {&ix.sa, &ix.bwt, &ix.vals[0], &ix.vals[1], &ix.keys[0], &ix.keys[1]})
         if (!b->owned) b->release();
+      ix.fused.reset();
     }
   } guard{ix};
   ix.slices_local = true;
   // ---- slice bounds
   const bool keyed = shard_keyed(ix);
   std::vector<uint64_t> gh(SH_KBUCKETS, 0), below(k + 1, 0);
+  std::vector<uint32_t> B;   // keyed: the coarse splitters
   {
     DevBuf d;
     d.ensure((SH_KBUCKETS + 1) * 8 + 64);
@@ -1044,7 +1046,7 @@ void build_sa_slices(Index& ix, int k) {
     HK_HIP(hipMemcpyAsync(gh.data(), d.p, SH_KBUCKETS * 8, hipMemcpyDeviceToHost, s));
     HK_HIP(hipStreamSynchronize(s));
     if (keyed) {
-      const std::vector<uint32_t> B = splitters(gh.data(), k, SH_KBUCKETS, true);
+      B = splitters(gh.data(), k, SH_KBUCKETS, true);
       uint64_t acc = 0;
       uint32_t c = 0;
       for (int r = 0; r <= k; ++r) {
@@ -1071,7 +1073,9 @@ void build_sa_slices(Index& ix, int k) {
     ix.shard_lo = lo;
     ix.shard_hi = hi;
   };
+  constexpr int kFuse = 4;   // slices per fused pass A (one scan of T' for the group)
   for (int r = 0; r < k; ++r) {
+    if (keyed && r % kFuse == 0) slices_fuse(ix, B, below, r, std::min(k, r + kFuse), w64);
     const uint64_t lo = below[r], hi = below[r + 1];
     point(lo, hi);
     void* const rows = ix.sa.p;
@@ -1103,6 +1107,7 @@ void build_sa_slices(Index& ix, int k) {
       swap_pending(ix, p);
     }
   }
+  ix.fused.reset();   // (the last group's records)
   // ---- prefix doubling over the slices still tied (repetitive texts)
   if (!pend.empty()) {
     ix.sa_pos64 = w64;
