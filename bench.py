@@ -211,7 +211,7 @@ BUILD_STAGES = ["byte_hist", "sa_bucket_hist", "radix_part_text", "radix_part_ke
                 "sa_bin_starts",
                 "sa_bucket_sort", "sa_big_gather", "radix_onesweep_text", "radix_table_text", "radix_tile_hist", "radix_hist", "radix_onesweep",
                 "radix_onesweep_small", "sa_pack_keys", "sa_refine_stats", "sa_refine_apply", "sa_refine_keys", "sa_refine_segsort",
-                "sa_isa_scatter", "sa_group_stats", "sa_group_apply", "sa_pair_keys", "bwt_gather"]
+                "sa_isa_scatter", "sa_group_stats", "sa_group_apply", "sa_pair_keys", "sa_pair_segsort", "bwt_gather"]
 SHARD_STAGES = ["shard_hist", "shard_below", "shard_slice_hist", "shard_slice_part", "shard_select_count",
                 "shard_pack_select", "rccl_allreduce_bytes",
                 "rccl_allreduce_hist",
@@ -493,7 +493,7 @@ def english_leg(args) -> dict:
     dev.close()
     refine = ("sa_refine_stats", "sa_refine_apply", "sa_refine_keys", "sa_refine_segsort", "radix_onesweep_small",
               "radix_hist", "radix_onesweep")
-    dbl = ("sa_isa_scatter", "sa_pair_keys", "sa_group_stats", "sa_group_apply")
+    dbl = ("sa_isa_scatter", "sa_pair_keys", "sa_pair_segsort", "sa_group_stats", "sa_group_apply")
     per = lambda names: round(sum(stages.get(k, {}).get("ms", 0.0) for k in names) / args.leg_steps, 3)
     log(f"[bench] english-like leg: {wall / args.leg_steps * 1e3:.2f} ms/step, refinement {per(refine)} ms, "
         f"doubling {per(dbl)} ms, count {qq['count_patterns_per_s']:.3g} patterns/s")

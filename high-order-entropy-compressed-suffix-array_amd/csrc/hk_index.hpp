@@ -162,6 +162,7 @@ struct Index {
     uint64_t A = 0, groups = 0, h = 0;
     uint64_t npairs = 0;       // pairs in upd from the last step
     bool pending = false;
+    bool big = false;          // a round had a group over SEG_MAX members: the next ones sort the list at once
   } dbl;
   DevBuf upd;
 

@@ -40,37 +40,6 @@ inline unsigned grid_for(uint64_t n, unsigned per = 256, unsigned cap = 16384) {
   return (unsigned)(g < cap ? g : cap);
 }
 
-__device__ __forceinline__ uint64_t blk_excl_sum(uint64_t v, uint64_t* red, uint64_t* total) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  uint64_t inc = wave_incl_sum<uint64_t>(v);
-  if (lane == 63) red[w] = inc;
-  __syncthreads();
-  uint64_t carry = 0, tot = 0;
-#pragma unroll
-  for (int i = 0; i < GR_T / 64; ++i) {
-    if (i < w) carry += red[i];
-    tot += red[i];
-  }
-  *total = tot;
-  __syncthreads();
-  return carry + inc - v;
-}
-
-__device__ __forceinline__ uint64_t blk_excl_max(uint64_t v, uint64_t* red) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  uint64_t inc = wave_incl_max<uint64_t>(v);
-  if (lane == 63) red[w] = inc;
-  __syncthreads();
-  uint64_t carry = 0;
-#pragma unroll
-  for (int i = 0; i < GR_T / 64; ++i)
-    if (i < w) carry = carry > red[i] ? carry : red[i];
-  uint64_t exc = __shfl_up(inc, 1, 64);
-  if (lane == 0) exc = 0;
-  __syncthreads();
-  return carry > exc ? carry : exc;
-}
-
 // ------------------------------------------------------------- alphabet
 // One counter copy per lane index (64 per workgroup, shared by the 4 waves' lanes of that index), u16
 // pairs with rows 129 words apart, so the lanes adding the same byte hit 64 different banks: no
@@ -198,28 +167,6 @@ __device__ __forceinline__ void tile_masks(const uint64_t* L, uint64_t tbase, ui
   }
 }
 
-// per tile: suffixes in tied groups, and heads of tied groups (keys compared >> cs)
-__global__ __launch_bounds__(GR_T) void k_refine_stats(const uint64_t* __restrict__ keys, uint64_t A, int cs,
-                                                       uint32_t* __restrict__ tact, uint32_t* __restrict__ thead) {
-  __shared__ uint64_t L[GR_LDS];
-  __shared__ uint32_t ra[4], rh[4];
-  const uint64_t tbase = (uint64_t)blockIdx.x * GR_TILE;
-  stage_tile_keys(keys, A, tbase, L);
-  uint32_t hmask, amask;
-  tile_masks(L, tbase, A, cs, hmask, amask);
-  const uint32_t act = wave_sum<uint32_t>((uint32_t)__popc(amask));
-  const uint32_t hd = wave_sum<uint32_t>((uint32_t)__popc(hmask));
-  if ((threadIdx.x & 63) == 0) {
-    ra[threadIdx.x >> 6] = act;
-    rh[threadIdx.x >> 6] = hd;
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    tact[blockIdx.x] = ra[0] + ra[1] + ra[2] + ra[3];
-    thead[blockIdx.x] = rh[0] + rh[1] + rh[2] + rh[3];
-  }
-}
-
 // writes SA / BWT entries of every suffix and compacts tied suffixes with their group ordinal.
 // FROM_KEY (initial round, J == identity, SA already in place): the BWT symbol is the key's low
 // field and P is read only for tied suffixes; otherwise BWT symbols are gathered from T'.
@@ -290,8 +237,9 @@ __global__ __launch_bounds__(GR_T) void k_refine_apply(
     } else {
       const uint32_t jv = J ? J[j] : (uint32_t)j;
       const V p = P[j];
-      if (sa) sa[jv] = p;
-      if (bwt) bwt[jv] = t[p == 0 ? n - 1 : (uint64_t)p - 1];
+      if (sa) sa[jv] = p;   // (every slot: prefix doubling builds its ISA from this SA)
+      // the BWT of a still-tied suffix waits until it settles (a later round writes its final slot)
+      if (bwt && !(amask & (1u << i))) bwt[jv] = t[p == 0 ? n - 1 : (uint64_t)p - 1];
       if (amask & (1u << i)) {
         if (hmask & (1u << i)) {
           ++g;
@@ -454,120 +402,222 @@ __global__ __launch_bounds__(256) void k_dbl_keys(const V* __restrict__ P, const
   }
 }
 
-// per tile of sorted doubling keys: 1 + slot of the last group head (0: none), tied suffixes, tied heads
-__global__ __launch_bounds__(GR_T) void k_dbl_stats(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ J,
-                                                    uint64_t A, uint64_t* __restrict__ tile_last,
-                                                    uint32_t* __restrict__ tile_act, uint32_t* __restrict__ tile_heads) {
-  __shared__ uint64_t red[GR_T / 64];
-  __shared__ uint32_t redc[GR_T / 64], redh[GR_T / 64];
-  const uint64_t base = (uint64_t)blockIdx.x * GR_TILE + (uint64_t)threadIdx.x * GR_I;
-  uint64_t last = 0;
-  uint32_t act = 0, th = 0;
-  if (base < A) {
-    uint64_t prev = base > 0 ? keys[base - 1] : 0;
-    uint64_t cur = keys[base];
-    for (int i = 0; i < GR_I; ++i) {
-      const uint64_t j = base + i;
-      if (j >= A) break;
-      const uint64_t nxt = j + 1 < A ? keys[j + 1] : 0;
-      const bool h = (j == 0) || cur != prev;
-      const bool hn = (j + 1 >= A) || nxt != cur;
-      if (h) last = (uint64_t)J[j] + 1;
-      act += (h && hn) ? 0u : 1u;
-      th += (h && !hn) ? 1u : 0u;
-      prev = cur;
-      cur = nxt;
+// ---- row-major forms of the grouping kernels: a tile's GR_I rows of GR_T consecutive items, item
+// k * GR_T + tid of thread tid, so every load and the compacted stores are coalesced (the thread-
+// contiguous forms above touch 64 lines per wave instruction).  Order-dependent quantities (the group
+// head's slot, the compaction offsets) come from one block scan per row.
+__device__ __forceinline__ void row_neighbors(const uint64_t* __restrict__ keys, uint64_t j, uint64_t A, int cs,
+                                              bool& h, bool& hn, uint64_t& cur, uint64_t& prev) {
+  cur = keys[j];
+  prev = j ? keys[j - 1] : 0;
+  const uint64_t nxt = j + 1 < A ? keys[j + 1] : 0;
+  h = j == 0 || (cur >> cs) != (prev >> cs);
+  hn = j + 1 >= A || (nxt >> cs) != (cur >> cs);
+}
+
+// k_refine_stats, row-major
+__global__ __launch_bounds__(GR_T) void k_refine_stats_rows(const uint64_t* __restrict__ keys, uint64_t A, int cs,
+                                                            uint32_t* __restrict__ tact,
+                                                            uint32_t* __restrict__ thead) {
+  __shared__ uint32_t ra[GR_T / 64];
+  const uint64_t tbase = (uint64_t)blockIdx.x * GR_TILE;
+  uint32_t c = 0;   // tied | tied heads << 16 (<= 4096 each per tile)
+#pragma unroll 4
+  for (int k = 0; k < GR_I; ++k) {
+    const uint64_t j = tbase + (uint64_t)k * GR_T + threadIdx.x;
+    if (j >= A) break;
+    bool h, hn;
+    uint64_t cur, prev;
+    row_neighbors(keys, j, A, cs, h, hn, cur, prev);
+    if (!(h && hn)) c += h ? 0x10001u : 1u;
+  }
+  c = wave_sum<uint32_t>(c);
+  if ((threadIdx.x & 63) == 0) ra[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t t = 0;
+    for (int i = 0; i < GR_T / 64; ++i) t += ra[i];
+    tact[blockIdx.x] = t & 0xFFFFu;
+    thead[blockIdx.x] = t >> 16;
+  }
+}
+
+// k_refine_apply<V, false>, row-major: SA of every suffix, BWT of the settled ones, tied suffixes compacted
+template <typename V>
+__global__ __launch_bounds__(GR_T) void k_refine_apply_rows(
+    const uint64_t* __restrict__ keys, const V* __restrict__ P, const uint32_t* __restrict__ J, uint64_t A,
+    int cs, const uint64_t* __restrict__ act_off, const uint64_t* __restrict__ head_off, V* __restrict__ sa,
+    uint8_t* __restrict__ bwt, const uint8_t* __restrict__ t, uint64_t n, V* __restrict__ oP,
+    uint32_t* __restrict__ oJ, uint32_t* __restrict__ oG, uint32_t* __restrict__ head_slot) {
+  __shared__ uint32_t wc[2][GR_T / 64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const uint64_t tbase = (uint64_t)blockIdx.x * GR_TILE;
+  uint64_t run_o = act_off[blockIdx.x], run_g = head_off[blockIdx.x];
+  for (int k = 0; k < GR_I; ++k) {   // (uniform: every thread runs every row's scan)
+    const uint64_t j = tbase + (uint64_t)k * GR_T + threadIdx.x;
+    const bool valid = j < A;
+    uint32_t a = 0, th = 0, jv = 0;
+    V p = 0;
+    if (valid) {
+      bool h, hn;
+      uint64_t cur, prev;
+      row_neighbors(keys, j, A, cs, h, hn, cur, prev);
+      a = (h && hn) ? 0u : 1u;
+      th = a && h ? 1u : 0u;
+      jv = J ? J[j] : (uint32_t)j;
+      p = P[j];
     }
+    const uint32_t ci = dpp_incl_sum(a | th << 16);
+    if (lane == 63) wc[k & 1][w] = ci;
+    __syncthreads();
+    uint32_t pre = 0, row = 0;
+#pragma unroll
+    for (int i = 0; i < GR_T / 64; ++i) {
+      const uint32_t x = wc[k & 1][i];
+      pre += i < w ? x : 0u;
+      row += x;
+    }
+    if (valid) {
+      if (sa) sa[jv] = p;   // (every slot: prefix doubling builds its ISA from this SA)
+      if (a) {
+        const uint32_t inc = pre + ci;
+        const uint64_t o = run_o + (inc & 0xFFFFu) - 1, g = run_g + (inc >> 16);
+        if (th) head_slot[g - 1] = jv;
+        oP[o] = p;
+        oJ[o] = jv;
+        oG[o] = (uint32_t)(g - 1);
+      } else if (bwt) {
+        bwt[jv] = t[p == 0 ? n - 1 : (uint64_t)p - 1];
+      }
+    }
+    run_o += row & 0xFFFFu;
+    run_g += row >> 16;
+  }
+}
+
+// k_dbl_stats, row-major
+__global__ __launch_bounds__(GR_T) void k_dbl_stats_rows(const uint64_t* __restrict__ keys,
+                                                         const uint32_t* __restrict__ J, uint64_t A, int ib,
+                                                         uint64_t* __restrict__ tile_last,
+                                                         uint32_t* __restrict__ tile_act,
+                                                         uint32_t* __restrict__ tile_heads) {
+  __shared__ uint64_t red[GR_T / 64];
+  __shared__ uint32_t redc[GR_T / 64];
+  const uint64_t tbase = (uint64_t)blockIdx.x * GR_TILE;
+  uint64_t last = 0;
+  uint32_t c = 0;
+#pragma unroll 4
+  for (int k = 0; k < GR_I; ++k) {
+    const uint64_t j = tbase + (uint64_t)k * GR_T + threadIdx.x;
+    if (j >= A) break;
+    bool h, hn;
+    uint64_t cur, prev;
+    row_neighbors(keys, j, A, 0, h, hn, cur, prev);
+    if (h) {
+      const uint64_t v = ((uint64_t)J[j] << 1 | ((j == 0 || (cur >> ib) != (prev >> ib)) ? 1u : 0u)) + 1;
+      last = v > last ? v : last;
+    }
+    if (!(h && hn)) c += h ? 0x10001u : 1u;
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
     const uint64_t tt = __shfl_xor(last, o, 64);
     last = last > tt ? last : tt;
-    act += __shfl_xor(act, o, 64);
-    th += __shfl_xor(th, o, 64);
   }
+  c = wave_sum<uint32_t>(c);
   if ((threadIdx.x & 63) == 0) {
     red[threadIdx.x >> 6] = last;
-    redc[threadIdx.x >> 6] = act;
-    redh[threadIdx.x >> 6] = th;
+    redc[threadIdx.x >> 6] = c;
   }
   __syncthreads();
   if (threadIdx.x == 0) {
     uint64_t m = 0;
-    uint32_t c = 0, hh = 0;
+    uint32_t t = 0;
     for (int i = 0; i < GR_T / 64; ++i) {
       m = m > red[i] ? m : red[i];
-      c += redc[i];
-      hh += redh[i];
+      t += redc[i];
     }
     tile_last[blockIdx.x] = m;
-    tile_act[blockIdx.x] = c;
-    tile_heads[blockIdx.x] = hh;
+    tile_act[blockIdx.x] = t & 0xFFFFu;
+    tile_heads[blockIdx.x] = t >> 16;
   }
 }
 
-// doubling round: SA / BWT entries in the slice, the new ISA of every suffix of the round (slot of
-// its new group head) into isa or as pairs, and the still-tied suffixes compacted with dense group
-// ordinals (head_slot[g] = slot of group g's head).  J is ascending (the round's slots in order).
+// k_dbl_apply, row-major
 template <typename V>
-__global__ __launch_bounds__(GR_T) void k_dbl_apply(
-    const uint64_t* __restrict__ keys, const V* __restrict__ P, const uint32_t* __restrict__ J, uint64_t A,
-    const uint64_t* __restrict__ carry_last, const uint64_t* __restrict__ act_off,
+__global__ __launch_bounds__(GR_T) void k_dbl_apply_rows(
+    const uint64_t* __restrict__ keys, const V* __restrict__ P, const uint32_t* __restrict__ J, uint64_t A, int ib,
+    bool keep_same, const uint64_t* __restrict__ carry_last, const uint64_t* __restrict__ act_off,
     const uint64_t* __restrict__ head_off, uint64_t lo, V* __restrict__ isa, uint64_t* __restrict__ pairs,
     V* __restrict__ sa, uint8_t* __restrict__ bwt, const uint8_t* __restrict__ t, uint64_t n, V* __restrict__ oP,
     uint32_t* __restrict__ oJ, uint32_t* __restrict__ oG, uint32_t* __restrict__ head_slot) {
-  __shared__ uint64_t red[GR_T / 64];
-  const uint64_t base = (uint64_t)blockIdx.x * GR_TILE + (uint64_t)threadIdx.x * GR_I;
-  uint32_t hmask = 0, amask = 0, tmask = 0;
-  uint64_t tmax = 0;
-  if (base < A) {
-    uint64_t prev = base > 0 ? keys[base - 1] : 0;
-    uint64_t cur = keys[base];
-    for (int i = 0; i < GR_I; ++i) {
-      const uint64_t j = base + i;
-      if (j >= A) break;
-      const uint64_t nxt = j + 1 < A ? keys[j + 1] : 0;
-      const bool h = (j == 0) || cur != prev;
-      const bool hn = (j + 1 >= A) || nxt != cur;
-      if (h) {
-        hmask |= 1u << i;
-        tmax = (uint64_t)J[j] + 1;
+  __shared__ uint64_t wm[2][GR_T / 64];
+  __shared__ uint32_t wc[2][GR_T / 64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const uint64_t tbase = (uint64_t)blockIdx.x * GR_TILE;
+  // 1 + (slot << 1 | first) of the last group head so far (0: none), tied so far, tied heads so far
+  uint64_t run_h = carry_last[blockIdx.x], run_o = act_off[blockIdx.x], run_g = head_off[blockIdx.x];
+  for (int k = 0; k < GR_I; ++k) {   // (uniform: every thread runs every row's scans)
+    const uint64_t j = tbase + (uint64_t)k * GR_T + threadIdx.x;
+    const bool valid = j < A;
+    uint32_t a = 0, th = 0, jv = 0;
+    uint64_t hv = 0;
+    V p = 0;
+    if (valid) {
+      bool h, hn;
+      uint64_t cur, prev;
+      row_neighbors(keys, j, A, 0, h, hn, cur, prev);
+      jv = J[j];
+      p = P[j];
+      a = (h && hn) ? 0u : 1u;
+      th = a && h ? 1u : 0u;
+      if (h) hv = ((uint64_t)jv << 1 | ((j == 0 || (cur >> ib) != (prev >> ib)) ? 1u : 0u)) + 1;
+    }
+    const uint64_t mi = wave_incl_max<uint64_t>(hv);
+    const uint32_t ci = dpp_incl_sum(a | th << 16);
+    if (lane == 63) {
+      wm[k & 1][w] = mi;
+      wc[k & 1][w] = ci;
+    }
+    __syncthreads();
+    uint64_t hm = run_h, rowm = run_h;
+    uint32_t pre = 0, row = 0;
+#pragma unroll
+    for (int i = 0; i < GR_T / 64; ++i) {
+      const uint64_t x = wm[k & 1][i];
+      const uint32_t c = wc[k & 1][i];
+      if (i < w) {
+        hm = hm > x ? hm : x;
+        pre += c;
       }
-      if (!(h && hn)) amask |= 1u << i;
-      if (h && !hn) tmask |= 1u << i;
-      prev = cur;
-      cur = nxt;
+      rowm = rowm > x ? rowm : x;
+      row += c;
     }
-  }
-  uint64_t gpre = blk_excl_max(tmax, red);
-  const uint64_t carry = carry_last[blockIdx.x];
-  gpre = gpre > carry ? gpre : carry;
-  uint64_t tot;
-  uint64_t o = blk_excl_sum((uint64_t)__popc(amask), red, &tot) + act_off[blockIdx.x];
-  uint64_t og = blk_excl_sum((uint64_t)__popc(tmask), red, &tot) + head_off[blockIdx.x];
-  uint64_t g = gpre ? gpre - 1 : 0;   // slot of the current group head
-  for (int i = 0; i < GR_I; ++i) {
-    const uint64_t j = base + i;
-    if (j >= A) break;
-    const uint32_t jv = J[j];
-    if (hmask & (1u << i)) g = jv;
-    const V p = P[j];
-    sa[jv] = p;
-    bwt[jv] = t[p == 0 ? n - 1 : (uint64_t)p - 1];
-    const uint64_t v = lo + g;
-    if (pairs) {
-      pairs[2 * j] = (uint64_t)p;
-      pairs[2 * j + 1] = v;
-    } else {
-      isa[p] = (V)v;
+    hm = hm > mi ? hm : mi;
+    if (valid) {
+      const uint64_t g = hm - 1;   // this suffix's group head: slot << 1 | first (j's head is at or before j)
+      const uint64_t v = lo + (g >> 1);
+      if (pairs) {
+        pairs[2 * j] = (uint64_t)p;
+        pairs[2 * j + 1] = v;
+      } else if (!(keep_same && (g & 1))) {
+        isa[p] = (V)v;
+      }
+      if (a) {
+        const uint32_t inc = pre + ci;
+        const uint64_t o = run_o + (inc & 0xFFFFu) - 1, gg = run_g + (inc >> 16);
+        if (th) head_slot[gg - 1] = jv;
+        oP[o] = p;
+        oJ[o] = jv;
+        oG[o] = (uint32_t)(gg - 1);
+      } else {   // settled: its final SA / BWT entry
+        sa[jv] = p;
+        bwt[jv] = t[p == 0 ? n - 1 : (uint64_t)p - 1];
+      }
     }
-    if (amask & (1u << i)) {
-      if (tmask & (1u << i)) head_slot[og++] = jv;
-      oP[o] = p;
-      oJ[o] = jv;
-      oG[o] = (uint32_t)(og - 1);
-      ++o;
-    }
+    run_h = rowm;
+    run_o += row & 0xFFFFu;
+    run_g += row >> 16;
   }
 }
 
@@ -639,9 +689,22 @@ void dbl_round_t(Index& ix, uint64_t K) {
                                               ix.isa.as<V>(), ix.n, st.h, ib, kp[0], vp[0]);
     HK_HIP(hipGetLastError());
   }
-  const int sl = radix_sort_pairs<V>(ix.sw, ix.timer, kp, vp, 0, A, 0, gbits + ib, false, s);
-  ix.info[0] += ix.sw.passes_run;
-  ix.info[1] += ix.sw.passes_skipped;
+  // groups of < 4 members on average: each group sorted in place (k_seg_sort16) and the round applied
+  // at once, redone after the radix sort only if a group had more than SEG_MAX members (its flag rides
+  // in the round's read-back); else the radix sort of the whole list at once
+  const bool direct = st.big || A >= 4 * st.groups;
+  unsigned int* d_big = reinterpret_cast<unsigned int*>(ix.small.as<uint8_t>() + 4356);   // small+4356: flag
+  int sl = 0;
+  if (direct) {
+    sl = radix_sort_pairs<V>(ix.sw, ix.timer, kp, vp, 0, A, 0, gbits + ib, false, s);
+    ix.info[0] += ix.sw.passes_run;
+    ix.info[1] += ix.sw.passes_skipped;
+  } else {
+    HK_HIP(hipMemsetAsync(d_big, 0, 4, s));
+    TimedLaunch tm(ix.timer, "sa_pair_segsort", (double)A * (2 * 8 + 2 * sizeof(V) + 4));
+    k_seg_sort16<V><<<grid_for(A), 256, 0, s>>>(kp[0], vp[0], ix.act[cur][2].as<uint32_t>(), A, d_big);
+    HK_HIP(hipGetLastError());
+  }
   const uint64_t nt = ceil_div(A, GR_TILE);
   ix.tile_a.ensure((nt + 1) * 8);
   ix.tile_b.ensure((nt + 1) * 4);
@@ -655,32 +718,48 @@ void dbl_round_t(Index& ix, uint64_t K) {
   uint64_t* ao = ix.tile_d.as<uint64_t>();
   uint32_t* th = tb2.as<uint32_t>();
   uint64_t* ho = reinterpret_cast<uint64_t*>(tb2.as<uint8_t>() + ((nt + 2) * 4 + 7) / 8 * 8);
-  {
-    TimedLaunch tm(ix.timer, "sa_group_stats", (double)A * 8);
-    k_dbl_stats<<<(unsigned)nt, GR_T, 0, s>>>(kp[sl], ix.act[cur][1].as<uint32_t>(), A, tl, ta, th);
-    HK_HIP(hipGetLastError());
-  }
-  scan_exclusive_max_u64(ix.sw, tl, cl, nt, s);
-  scan_exclusive_u32_to_u64(ix.sw, ta, ao, nt, true, s);
-  scan_exclusive_u32_to_u64(ix.sw, th, ho, nt, true, s);
   uint64_t* pairs = nullptr;
   if (ix.sharded && !ix.slices_local) {
     ix.upd.ensure(A * 16 + 16);
     pairs = ix.upd.as<uint64_t>();
   }
-  {
-    TimedLaunch tm(ix.timer, "sa_group_apply", (double)A * (8 + 2 * sizeof(V) + 4 + 1 + 1 + (pairs ? 16 : sizeof(V))));
-    k_dbl_apply<V><<<(unsigned)nt, GR_T, 0, s>>>(
-        kp[sl], vp[sl], ix.act[cur][1].as<uint32_t>(), A, cl, ao, ho, ix.sharded ? ix.shard_lo : 0,
-        ix.isa.as<V>(), pairs, ix.sa.as<V>(), ix.bwt.as<uint8_t>(), ix.text.as<uint8_t>(), ix.n,
-        ix.act[cur ^ 1][0].as<V>(), ix.act[cur ^ 1][1].as<uint32_t>(), ix.act[cur ^ 1][2].as<uint32_t>(),
-        ix.head_slot.as<uint32_t>());
-    HK_HIP(hipGetLastError());
-  }
   uint64_t* const tot = ix.rb();   // pinned: the copies land without a staging hop
-  HK_HIP(hipMemcpyAsync(&tot[0], ao + nt, 8, hipMemcpyDeviceToHost, s));
-  HK_HIP(hipMemcpyAsync(&tot[1], ho + nt, 8, hipMemcpyDeviceToHost, s));
-  HK_HIP(hipStreamSynchronize(s));
+  // keep_same: skip the ISA entries a round leaves unchanged (not in the redo after a speculative apply,
+  // which may have rewritten some of them)
+  auto apply_round = [&](int slot, bool flag, bool keep_same) {
+    {
+      TimedLaunch tm(ix.timer, "sa_group_stats", (double)A * 8);
+      k_dbl_stats_rows<<<(unsigned)nt, GR_T, 0, s>>>(kp[slot], ix.act[cur][1].as<uint32_t>(), A, ib, tl, ta, th);
+      HK_HIP(hipGetLastError());
+    }
+    scan_exclusive_max_u64(ix.sw, tl, cl, nt, s);
+    scan_exclusive_u32_to_u64(ix.sw, ta, ao, nt, true, s);
+    scan_exclusive_u32_to_u64(ix.sw, th, ho, nt, true, s);
+    {
+      TimedLaunch tm(ix.timer, "sa_group_apply", (double)A * (8 + 2 * sizeof(V) + 4 + 1 + 1 + (pairs ? 16 : sizeof(V))));
+      k_dbl_apply_rows<V><<<(unsigned)nt, GR_T, 0, s>>>(
+          kp[slot], vp[slot], ix.act[cur][1].as<uint32_t>(), A, ib, keep_same, cl, ao, ho, ix.sharded ? ix.shard_lo : 0,
+          ix.isa.as<V>(), pairs, ix.sa.as<V>(), ix.bwt.as<uint8_t>(), ix.text.as<uint8_t>(), ix.n,
+          ix.act[cur ^ 1][0].as<V>(), ix.act[cur ^ 1][1].as<uint32_t>(), ix.act[cur ^ 1][2].as<uint32_t>(),
+          ix.head_slot.as<uint32_t>());
+      HK_HIP(hipGetLastError());
+    }
+    HK_HIP(hipMemcpyAsync(&tot[0], ao + nt, 8, hipMemcpyDeviceToHost, s));
+    HK_HIP(hipMemcpyAsync(&tot[1], ho + nt, 8, hipMemcpyDeviceToHost, s));
+    tot[2] = 0;
+    if (flag) HK_HIP(hipMemcpyAsync(&tot[2], d_big, 4, hipMemcpyDeviceToHost, s));
+    HK_HIP(hipStreamSynchronize(s));
+  };
+  apply_round(sl, !direct, true);
+  if (!direct && (uint32_t)tot[2]) {   // a group over SEG_MAX members was left unsorted: redo the round
+    st.big = true;
+    // (the redo rewrites every ISA entry, list entry and group head of the first attempt; an SA / BWT
+    // slot it wrote for a suffix it wrongly took as settled is rewritten by the slot's final owner)
+    sl = radix_sort_pairs<V>(ix.sw, ix.timer, kp, vp, 0, A, 0, gbits + ib, false, s);
+    ix.info[0] += ix.sw.passes_run;
+    ix.info[1] += ix.sw.passes_skipped;
+    apply_round(sl, false, false);
+  }
   st.npairs = pairs ? A : 0;
   st.cur ^= 1;
   st.A = tot[0];
@@ -704,7 +783,7 @@ std::pair<uint64_t, uint64_t> refine_step(Index& ix, const KeyGeom& kg, const ui
   ix.tile_d.ensure((nt + 2) * 8);
   {
     TimedLaunch tm(ix.timer, "sa_refine_stats", (double)A * 8);
-    k_refine_stats<<<(unsigned)nt, GR_T, 0, s>>>(keys, A, cs, ix.tile_b.as<uint32_t>(), ix.tile_c.as<uint32_t>());
+    k_refine_stats_rows<<<(unsigned)nt, GR_T, 0, s>>>(keys, A, cs, ix.tile_b.as<uint32_t>(), ix.tile_c.as<uint32_t>());
     HK_HIP(hipGetLastError());
   }
   scan_exclusive_u32_to_u64(ix.sw, ix.tile_b.as<uint32_t>(), ix.tile_a.as<uint64_t>(), nt, true, s);
@@ -718,9 +797,9 @@ std::pair<uint64_t, uint64_t> refine_step(Index& ix, const KeyGeom& kg, const ui
           keys, P, J, A, cs, ix.tile_a.as<uint64_t>(), ix.tile_d.as<uint64_t>(), write_sa ? ix.sa.as<V>() : nullptr,
           bwt, inv, (1ull << kg.pb) - 1, ix.text.as<uint8_t>(), ix.n, oP, oJ, oG, head_slot);
     else
-      k_refine_apply<V, false><<<(unsigned)nt, GR_T, 0, s>>>(
+      k_refine_apply_rows<V><<<(unsigned)nt, GR_T, 0, s>>>(
           keys, P, J, A, cs, ix.tile_a.as<uint64_t>(), ix.tile_d.as<uint64_t>(), write_sa ? ix.sa.as<V>() : nullptr,
-          bwt, inv, 0, ix.text.as<uint8_t>(), ix.n, oP, oJ, oG, head_slot);
+          bwt, ix.text.as<uint8_t>(), ix.n, oP, oJ, oG, head_slot);
     HK_HIP(hipGetLastError());
   }
   uint64_t* const tot = ix.rb();
@@ -851,8 +930,12 @@ void refine_loop(Index& ix, const KeyGeom& kg, int cur, uint64_t A, uint64_t gro
   V* vp[2] = {ix.vals[0].as<V>(), ix.vals[1].as<V>()};
   uint64_t h = (uint64_t)kg.q;
   int rounds = 0;
-  while (A > 0) {
-    if (++rounds > kChunkRounds) break;
+  uint64_t A_prev = 0;
+  const bool local_dbl = allow_doubling || ix.slices_local;   // doubling needs no rank exchange here
+  while (A > 0 && rounds < kChunkRounds) {
+    // a round that settled under a fifth of its tied suffixes (long repeats: natural-language text) hands
+    // over to prefix doubling, whose shared prefix doubles each round instead of growing by one chunk
+    if (local_dbl && rounds > 0 && A * 5 > A_prev * 4) break;
     int gbits = 0;
     while (gbits < 64 && (1ull << gbits) < groups) ++gbits;
     auto fits = [&](int qq) {   // G in the top gbits, chunk + nS (<= R^qq - 1 + nS) below
@@ -865,6 +948,8 @@ void refine_loop(Index& ix, const KeyGeom& kg, int cur, uint64_t A, uint64_t gro
     int qn = 0;
     while (qn < 64 && fits(qn + 1)) ++qn;
     if (qn < 1) break;   // too many groups for a chunk key: prefix doubling takes over
+    ++rounds;
+    A_prev = A;
     {
       TimedLaunch tm(ix.timer, "sa_refine_keys", (double)A * (sizeof(V) * 2 + 4 + 8));
       k_refine_keys<V><<<grid_for(A), 256, 0, s>>>(ix.act[cur][0].as<V>(), ix.act[cur][2].as<uint32_t>(), A,
@@ -876,17 +961,23 @@ void refine_loop(Index& ix, const KeyGeom& kg, int cur, uint64_t A, uint64_t gro
     // comes back with the round's totals (one round trip).  A group over SEG_MAX members (it was left
     // unsorted) redoes the round from the same keys with the global radix sort: the redo rewrites every
     // output of the first attempt (the same SA / BWT slots, the next list, the group heads).
+    // groups of four or more members on average (natural-language text): some surely exceed SEG_MAX, so
+    // the round takes the radix sort at once instead of a segmented sort and an apply it would redo
+    const bool direct = groups && A >= 4 * groups;
     unsigned int* d_big = reinterpret_cast<unsigned int*>(ix.small.as<uint8_t>() + 4356);   // small+4356: flag
-    unsigned int h_big = 0;
-    HK_HIP(hipMemsetAsync(d_big, 0, 4, s));
-    {
-      TimedLaunch tm(ix.timer, "sa_refine_segsort", (double)A * (2 * 8 + 2 * sizeof(V) + 4));
-      k_seg_sort16<V><<<grid_for(A), 256, 0, s>>>(kp[0], vp[0], ix.act[cur][2].as<uint32_t>(), A, d_big);
-      HK_HIP(hipGetLastError());
+    unsigned int h_big = direct ? 1u : 0u;
+    std::pair<uint64_t, uint64_t> r{0, 0};
+    if (!direct) {
+      HK_HIP(hipMemsetAsync(d_big, 0, 4, s));
+      {
+        TimedLaunch tm(ix.timer, "sa_refine_segsort", (double)A * (2 * 8 + 2 * sizeof(V) + 4));
+        k_seg_sort16<V><<<grid_for(A), 256, 0, s>>>(kp[0], vp[0], ix.act[cur][2].as<uint32_t>(), A, d_big);
+        HK_HIP(hipGetLastError());
+      }
+      r = refine_step<V>(ix, kg, kp[0], vp[0], ix.act[cur][1].as<uint32_t>(), A, 0, false, true,
+                         ix.act[cur ^ 1][0].as<V>(), ix.act[cur ^ 1][1].as<uint32_t>(),
+                         ix.act[cur ^ 1][2].as<uint32_t>(), ix.head_slot.as<uint32_t>(), d_big, &h_big);
     }
-    auto r = refine_step<V>(ix, kg, kp[0], vp[0], ix.act[cur][1].as<uint32_t>(), A, 0, false, true,
-                            ix.act[cur ^ 1][0].as<V>(), ix.act[cur ^ 1][1].as<uint32_t>(),
-                            ix.act[cur ^ 1][2].as<uint32_t>(), ix.head_slot.as<uint32_t>(), d_big, &h_big);
     if (h_big) {
       const int sl = radix_sort_pairs<V>(ix.sw, ix.timer, kp, vp, 0, A, 0, 64, false, s);
       ix.info[0] += ix.sw.passes_run;
@@ -901,7 +992,7 @@ void refine_loop(Index& ix, const KeyGeom& kg, int cur, uint64_t A, uint64_t gro
     ix.info.push_back(A);
     h += (uint64_t)qn;
   }
-  ix.info[2] = (uint64_t)(rounds > kChunkRounds ? kChunkRounds : rounds);
+  ix.info[2] = (uint64_t)rounds;
   ix.dbl = Index::DblState{};
   if (A == 0) return;
   // ---- prefix doubling from order h over the A tied suffixes (repetitive texts)
