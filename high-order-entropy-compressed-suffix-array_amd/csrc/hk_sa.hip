@@ -123,136 +123,7 @@ __global__ __launch_bounds__(256) void k_pack_keys(const uint8_t* __restrict__ t
 }
 
 // ------------------------------------------------------------- refinement
-// A tile of GR_TILE sorted keys (+1 halo each side) is staged in LDS with one pad slot per 16
-// elements, so thread t's 16 consecutive items are read conflict-free (stride 17 x u64).
-constexpr int GR_LDS = GR_TILE + 2 + (GR_TILE + 2) / 16 + 1;
-__device__ __forceinline__ int lpad(int e) { return e + (e >> 4); }
-
-__device__ __forceinline__ void stage_tile_keys(const uint64_t* __restrict__ keys, uint64_t A, uint64_t tbase,
-                                                uint64_t* L) {
-  // slot i holds key[tbase + i - 1]; 16 coalesced loads per thread are issued back to back
-  uint64_t v[GR_I];
-#pragma unroll
-  for (int k = 0; k < GR_I; ++k) {
-    const uint64_t j = tbase + threadIdx.x + (uint64_t)k * GR_T;
-    v[k] = j < A ? keys[j] : 0;
-  }
-  if (threadIdx.x == 0) L[lpad(0)] = tbase > 0 ? keys[tbase - 1] : 0;
-  if (threadIdx.x == 1) L[lpad(GR_TILE + 1)] = tbase + GR_TILE < A ? keys[tbase + GR_TILE] : 0;
-#pragma unroll
-  for (int k = 0; k < GR_I; ++k) L[lpad(threadIdx.x + k * GR_T + 1)] = v[k];
-  __syncthreads();
-}
-
-// head / tied masks of thread t's 16 items from the staged tile
-__device__ __forceinline__ void tile_masks(const uint64_t* L, uint64_t tbase, uint64_t A, int cs, uint32_t& hmask,
-                                           uint32_t& amask) {
-  hmask = amask = 0;
-  const int e0 = threadIdx.x * GR_I;
-  uint64_t prev = L[lpad(e0)] >> cs, cur = L[lpad(e0 + 1)] >> cs;
-#pragma unroll
-  for (int i = 0; i < GR_I; ++i) {
-    const uint64_t j = tbase + e0 + i;
-    const uint64_t nxt = L[lpad(e0 + i + 2)] >> cs;
-    if (j < A) {
-      const bool h = j == 0 || cur != prev;
-      const bool hn = j + 1 >= A || nxt != cur;
-      if (!(h && hn)) {
-        amask |= 1u << i;
-        if (h) hmask |= 1u << i;
-      }
-    }
-    prev = cur;
-    cur = nxt;
-  }
-}
-
-// writes SA / BWT entries of every suffix and compacts tied suffixes with their group ordinal.
-// FROM_KEY (initial round, J == identity, SA already in place): the BWT symbol is the key's low
-// field and P is read only for tied suffixes; otherwise BWT symbols are gathered from T'.
-template <typename V, bool FROM_KEY>
-__global__ __launch_bounds__(GR_T) void k_refine_apply(
-    const uint64_t* __restrict__ keys, const V* __restrict__ P, const uint32_t* __restrict__ J, uint64_t A,
-    int cs, const uint64_t* __restrict__ act_off, const uint64_t* __restrict__ head_off, V* __restrict__ sa,
-    uint8_t* __restrict__ bwt, const uint8_t* __restrict__ inv, uint64_t pmask, const uint8_t* __restrict__ t,
-    uint64_t n, V* __restrict__ oP, uint32_t* __restrict__ oJ, uint32_t* __restrict__ oG,
-    uint32_t* __restrict__ head_slot) {
-  __shared__ uint64_t L[GR_LDS];
-  __shared__ uint32_t ra[4], rh[4];
-  __shared__ uint8_t INV[512];
-  if (FROM_KEY) {
-    INV[threadIdx.x] = inv[threadIdx.x];
-    INV[threadIdx.x + 256] = inv[threadIdx.x + 256];
-  }
-  const uint64_t tbase = (uint64_t)blockIdx.x * GR_TILE;
-  stage_tile_keys(keys, A, tbase, L);
-  uint32_t hmask, amask;
-  tile_masks(L, tbase, A, cs, hmask, amask);
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const uint32_t ca = __popc(amask), ch = __popc(hmask);
-  const uint32_t ia = wave_incl_sum<uint32_t>(ca), ih = wave_incl_sum<uint32_t>(ch);
-  if (lane == 63) {
-    ra[w] = ia;
-    rh[w] = ih;
-  }
-  __syncthreads();
-  uint64_t oa = act_off[blockIdx.x], oh = head_off[blockIdx.x];
-  for (int i = 0; i < w; ++i) {
-    oa += ra[i];
-    oh += rh[i];
-  }
-  oa += ia - ca;
-  oh += ih - ch;
-  const uint64_t base = tbase + (uint64_t)threadIdx.x * GR_I;
-  if (FROM_KEY && bwt) {
-    // BWT symbols of the 16 items straight from the prev field of the (unshifted) keys
-    if (base + GR_I <= A) {
-      uint32_t wv[4] = {0, 0, 0, 0};
-#pragma unroll
-      for (int i = 0; i < GR_I; ++i) {
-        const uint32_t sym = INV[(uint32_t)(L[lpad(threadIdx.x * GR_I + i + 1)] & pmask)];
-        wv[i >> 2] |= sym << (8 * (i & 3));
-      }
-      *reinterpret_cast<uint4*>(bwt + base) = make_uint4(wv[0], wv[1], wv[2], wv[3]);
-    } else {
-      for (int i = 0; i < GR_I; ++i)
-        if (base + i < A) bwt[base + i] = INV[(uint32_t)(L[lpad(threadIdx.x * GR_I + i + 1)] & pmask)];
-    }
-  }
-  uint64_t g = oh;  // tied-group heads before this thread's first item
-  for (int i = 0; i < GR_I; ++i) {
-    const uint64_t j = base + i;
-    if (j >= A) break;
-    if (FROM_KEY) {
-      if (!(amask & (1u << i))) continue;
-      const V p = P[j];
-      if (hmask & (1u << i)) {
-        ++g;
-        if (head_slot) head_slot[g - 1] = (uint32_t)j;
-      }
-      oP[oa] = p;
-      oJ[oa] = (uint32_t)j;
-      oG[oa] = (uint32_t)(g - 1);
-      ++oa;
-    } else {
-      const uint32_t jv = J ? J[j] : (uint32_t)j;
-      const V p = P[j];
-      if (sa) sa[jv] = p;   // (every slot: prefix doubling builds its ISA from this SA)
-      // the BWT of a still-tied suffix waits until it settles (a later round writes its final slot)
-      if (bwt && !(amask & (1u << i))) bwt[jv] = t[p == 0 ? n - 1 : (uint64_t)p - 1];
-      if (amask & (1u << i)) {
-        if (hmask & (1u << i)) {
-          ++g;
-          if (head_slot) head_slot[g - 1] = jv;
-        }
-        oP[oa] = p;
-        oJ[oa] = jv;
-        oG[oa] = (uint32_t)(g - 1);
-        ++oa;
-      }
-    }
-  }
-}
+// (the grouping kernels of a refinement / doubling round are the row-major forms below)
 
 // chunk refinement key: (group ordinal << (64-gbits)) | next qn codes of the suffix from offset h (radix R).
 // Keyed layout: short suffixes (p >= s_start) tied with others in the first round take their exact
@@ -442,14 +313,23 @@ __global__ __launch_bounds__(GR_T) void k_refine_stats_rows(const uint64_t* __re
   }
 }
 
-// k_refine_apply<V, false>, row-major: SA of every suffix, BWT of the settled ones, tied suffixes compacted
-template <typename V>
+// Refinement grouping step, row-major: SA of every suffix, BWT of the settled ones, tied suffixes compacted
+// with their group ordinal.  FROM_KEY (initial round, J == identity, SA already in place): the BWT of
+// every suffix is the key's low field and P is read only for tied suffixes.
+template <typename V, bool FROM_KEY>
 __global__ __launch_bounds__(GR_T) void k_refine_apply_rows(
     const uint64_t* __restrict__ keys, const V* __restrict__ P, const uint32_t* __restrict__ J, uint64_t A,
     int cs, const uint64_t* __restrict__ act_off, const uint64_t* __restrict__ head_off, V* __restrict__ sa,
-    uint8_t* __restrict__ bwt, const uint8_t* __restrict__ t, uint64_t n, V* __restrict__ oP,
-    uint32_t* __restrict__ oJ, uint32_t* __restrict__ oG, uint32_t* __restrict__ head_slot) {
+    uint8_t* __restrict__ bwt, const uint8_t* __restrict__ inv, uint64_t pmask, const uint8_t* __restrict__ t,
+    uint64_t n, V* __restrict__ oP, uint32_t* __restrict__ oJ, uint32_t* __restrict__ oG,
+    uint32_t* __restrict__ head_slot) {
   __shared__ uint32_t wc[2][GR_T / 64];
+  __shared__ uint8_t INV[512];
+  if (FROM_KEY) {
+    INV[threadIdx.x] = inv[threadIdx.x];
+    INV[threadIdx.x + 256] = inv[threadIdx.x + 256];
+    __syncthreads();
+  }
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const uint64_t tbase = (uint64_t)blockIdx.x * GR_TILE;
   uint64_t run_o = act_off[blockIdx.x], run_g = head_off[blockIdx.x];
@@ -464,8 +344,9 @@ __global__ __launch_bounds__(GR_T) void k_refine_apply_rows(
       row_neighbors(keys, j, A, cs, h, hn, cur, prev);
       a = (h && hn) ? 0u : 1u;
       th = a && h ? 1u : 0u;
-      jv = J ? J[j] : (uint32_t)j;
-      p = P[j];
+      jv = FROM_KEY ? (uint32_t)j : (J ? J[j] : (uint32_t)j);
+      if (!FROM_KEY || a) p = P[j];
+      if (FROM_KEY && bwt) bwt[j] = INV[(uint32_t)(cur & pmask)];
     }
     const uint32_t ci = dpp_incl_sum(a | th << 16);
     if (lane == 63) wc[k & 1][w] = ci;
@@ -478,15 +359,15 @@ __global__ __launch_bounds__(GR_T) void k_refine_apply_rows(
       row += x;
     }
     if (valid) {
-      if (sa) sa[jv] = p;   // (every slot: prefix doubling builds its ISA from this SA)
+      if (!FROM_KEY && sa) sa[jv] = p;   // (every slot: prefix doubling builds its ISA from this SA)
       if (a) {
         const uint32_t inc = pre + ci;
         const uint64_t o = run_o + (inc & 0xFFFFu) - 1, g = run_g + (inc >> 16);
-        if (th) head_slot[g - 1] = jv;
+        if (th && head_slot) head_slot[g - 1] = jv;
         oP[o] = p;
         oJ[o] = jv;
         oG[o] = (uint32_t)(g - 1);
-      } else if (bwt) {
+      } else if (!FROM_KEY && bwt) {
         bwt[jv] = t[p == 0 ? n - 1 : (uint64_t)p - 1];
       }
     }
@@ -793,13 +674,13 @@ std::pair<uint64_t, uint64_t> refine_step(Index& ix, const KeyGeom& kg, const ui
   {
     TimedLaunch tm(ix.timer, "sa_refine_apply", (double)A * (8 + sizeof(V) + (write_sa ? sizeof(V) + 4 : 0) + 1));
     if (from_key)
-      k_refine_apply<V, true><<<(unsigned)nt, GR_T, 0, s>>>(
+      k_refine_apply_rows<V, true><<<(unsigned)nt, GR_T, 0, s>>>(
           keys, P, J, A, cs, ix.tile_a.as<uint64_t>(), ix.tile_d.as<uint64_t>(), write_sa ? ix.sa.as<V>() : nullptr,
           bwt, inv, (1ull << kg.pb) - 1, ix.text.as<uint8_t>(), ix.n, oP, oJ, oG, head_slot);
     else
-      k_refine_apply_rows<V><<<(unsigned)nt, GR_T, 0, s>>>(
+      k_refine_apply_rows<V, false><<<(unsigned)nt, GR_T, 0, s>>>(
           keys, P, J, A, cs, ix.tile_a.as<uint64_t>(), ix.tile_d.as<uint64_t>(), write_sa ? ix.sa.as<V>() : nullptr,
-          bwt, ix.text.as<uint8_t>(), ix.n, oP, oJ, oG, head_slot);
+          bwt, inv, 0, ix.text.as<uint8_t>(), ix.n, oP, oJ, oG, head_slot);
     HK_HIP(hipGetLastError());
   }
   uint64_t* const tot = ix.rb();
