@@ -211,7 +211,8 @@ BUILD_STAGES = ["byte_hist", "sa_bucket_hist", "radix_part_text", "radix_part_ke
                 "sa_bin_starts",
                 "sa_bucket_sort", "sa_big_gather", "radix_onesweep_text", "radix_table_text", "radix_tile_hist", "radix_hist", "radix_onesweep",
                 "radix_onesweep_small", "sa_pack_keys", "sa_refine_stats", "sa_refine_apply", "sa_refine_keys", "sa_refine_segsort",
-                "sa_isa_scatter", "sa_group_stats", "sa_group_apply", "sa_pair_keys", "sa_pair_segsort", "bwt_gather"]
+                "sa_isa_scatter", "sa_group_stats", "sa_group_apply", "sa_pair_keys", "sa_pair_segsort", "sa_big_groups",
+                "bwt_gather"]
 SHARD_STAGES = ["shard_hist", "shard_below", "shard_slice_hist", "shard_slice_part", "shard_select_count",
                 "shard_pack_select", "rccl_allreduce_bytes",
                 "rccl_allreduce_hist",

@@ -104,7 +104,9 @@ struct Index {
   DevBuf act[2][3];            // P, J, G of the active list (double-buffered)
   DevBuf head_slot;            // SA slot of each tied group's head (refinement -> doubling switch)
   DevBuf ties_k, ties_v, ties_n;   // unordered tie list of the bucket build (J<<1|head, P), count
-  DevBuf big_k[2], big_v[2], big_j; // big buckets of the bucket build (sorted on the global path)
+  DevBuf big_k[2], big_v[2], big_j; // big buckets of the bucket build (sorted on the global path); the
+                                    // members of large tied groups of a refinement / doubling round
+  DevBuf grp_big;                   // refinement / doubling round: u8 per group, 1 = over SEG_MAX members
   DevBuf bk_items, bk_hist, bk_fb; // bucket work items, bucket histogram, fast-path fallback items
   DevBuf cp_part, cp_cur, cp_tiles; // cursor partition: per-span counts, destination cursors, pass-B tiles
   HostBuf cp_host;                  // ... and its pinned host side (bucket counts, region table)

@@ -176,14 +176,15 @@ constexpr int SEG_MAX = 16;
 template <typename V>
 __global__ __launch_bounds__(256) void k_seg_sort16(uint64_t* __restrict__ keys, V* __restrict__ vals,
                                                     const uint32_t* __restrict__ G, uint64_t A,
-                                                    unsigned int* __restrict__ big) {
+                                                    unsigned int* __restrict__ big, uint8_t* __restrict__ gbig) {
   for (uint64_t a = (uint64_t)blockIdx.x * 256 + threadIdx.x; a < A; a += (uint64_t)gridDim.x * 256) {
     const uint32_t g = G[a];
     if (a > 0 && G[a - 1] == g) continue;   // not a head
     uint32_t sz = 1;
     while (sz <= SEG_MAX && a + sz < A && G[a + sz] == g) ++sz;
-    if (sz > SEG_MAX) {
+    if (sz > SEG_MAX) {   // left for sort_big_groups (its members gathered by the group's flag)
       atomicOr(big, 1u);
+      gbig[g] = 1;
       continue;
     }
     if (sz == 1) continue;
@@ -220,6 +221,75 @@ __global__ __launch_bounds__(256) void k_seg_sort16(uint64_t* __restrict__ keys,
         keys[a + i] = k[i];
         vals[a + i] = v[i];
       }
+  }
+}
+
+// Members of the groups k_seg_sort16 left (over SEG_MAX members, gbig[G] = 1): per-tile counts, then
+// gathered in list order (row-major tiles, one block scan per row) with their list positions, radix-sorted
+// (the key carries the group in its top bits, so groups stay apart and in order) and scattered back.
+__global__ __launch_bounds__(GR_T) void k_big_count_rows(const uint32_t* __restrict__ G,
+                                                         const uint8_t* __restrict__ gbig, uint64_t A,
+                                                         uint32_t* __restrict__ tcnt) {
+  __shared__ uint32_t ra[GR_T / 64];
+  const uint64_t tbase = (uint64_t)blockIdx.x * GR_TILE;
+  uint32_t c = 0;
+#pragma unroll 4
+  for (int k = 0; k < GR_I; ++k) {
+    const uint64_t j = tbase + (uint64_t)k * GR_T + threadIdx.x;
+    if (j >= A) break;
+    c += gbig[G[j]];
+  }
+  c = wave_sum<uint32_t>(c);
+  if ((threadIdx.x & 63) == 0) ra[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t t = 0;
+    for (int i = 0; i < GR_T / 64; ++i) t += ra[i];
+    tcnt[blockIdx.x] = t;
+  }
+}
+
+template <typename V>
+__global__ __launch_bounds__(GR_T) void k_big_compact_rows(const uint64_t* __restrict__ keys, const V* __restrict__ vals,
+                                                           const uint32_t* __restrict__ G,
+                                                           const uint8_t* __restrict__ gbig, uint64_t A,
+                                                           const uint64_t* __restrict__ toff, uint64_t* __restrict__ ok,
+                                                           V* __restrict__ ov, uint32_t* __restrict__ oj) {
+  __shared__ uint32_t wc[2][GR_T / 64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const uint64_t tbase = (uint64_t)blockIdx.x * GR_TILE;
+  uint64_t run = toff[blockIdx.x];
+  for (int k = 0; k < GR_I; ++k) {   // (uniform)
+    const uint64_t j = tbase + (uint64_t)k * GR_T + threadIdx.x;
+    const uint32_t f = j < A ? gbig[G[j]] : 0u;
+    const uint32_t ci = dpp_incl_sum(f);
+    if (lane == 63) wc[k & 1][w] = ci;
+    __syncthreads();
+    uint32_t pre = 0, row = 0;
+#pragma unroll
+    for (int i = 0; i < GR_T / 64; ++i) {
+      const uint32_t x = wc[k & 1][i];
+      pre += i < w ? x : 0u;
+      row += x;
+    }
+    if (f) {
+      const uint64_t o = run + pre + ci - 1;
+      ok[o] = keys[j];
+      ov[o] = vals[j];
+      oj[o] = (uint32_t)j;
+    }
+    run += row;
+  }
+}
+
+template <typename V>
+__global__ __launch_bounds__(256) void k_big_scatter(const uint64_t* __restrict__ k, const V* __restrict__ v,
+                                                     const uint32_t* __restrict__ pos, uint64_t B,
+                                                     uint64_t* __restrict__ keys, V* __restrict__ vals) {
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < B; i += (uint64_t)gridDim.x * 256) {
+    const uint32_t j = pos[i];
+    keys[j] = k[i];
+    vals[j] = v[i];
   }
 }
 
@@ -552,6 +622,65 @@ int bits_of_u64(uint64_t v) {
   return b;
 }
 
+// Segmented sort of a round's list (keys / vals in slot 0, grouped by the dense ordinals G): each group of
+// <= SEG_MAX members sorted in place by its head thread; a larger group is left, flagged in ix.grp_big and
+// in *d_big (sort_big_groups finishes it)
+template <typename V>
+void seg_sort_groups(Index& ix, uint64_t* k0, V* v0, const uint32_t* G, uint64_t A, uint64_t groups,
+                     unsigned int* d_big, const char* name) {
+  hipStream_t s = ix.stream;
+  ix.grp_big.ensure(groups + 16);
+  HK_HIP(hipMemsetAsync(d_big, 0, 4, s));
+  HK_HIP(hipMemsetAsync(ix.grp_big.p, 0, groups, s));
+  TimedLaunch tm(ix.timer, name, (double)A * (2 * 8 + 2 * sizeof(V) + 4));
+  k_seg_sort16<V><<<grid_for(A), 256, 0, s>>>(k0, v0, G, A, d_big, ix.grp_big.as<uint8_t>());
+  HK_HIP(hipGetLastError());
+}
+
+// The members of the groups seg_sort_groups left, gathered in list order, radix-sorted on key bits
+// [0, bits) (the group ordinal is in the top bits) and scattered back to their list positions: only the
+// large groups' members pass through the radix sort, not the whole list
+template <typename V>
+void sort_big_groups(Index& ix, uint64_t* k0, V* v0, const uint32_t* G, uint64_t A, int bits) {
+  hipStream_t s = ix.stream;
+  const uint64_t nt = ceil_div(A, GR_TILE);
+  ix.tile_b.ensure((nt + 1) * 4);
+  ix.tile_a.ensure((nt + 2) * 8);
+  const uint8_t* gbig = ix.grp_big.as<uint8_t>();
+  {
+    TimedLaunch tm(ix.timer, "sa_big_groups", (double)A * 5);
+    k_big_count_rows<<<(unsigned)nt, GR_T, 0, s>>>(G, gbig, A, ix.tile_b.as<uint32_t>());
+    HK_HIP(hipGetLastError());
+  }
+  scan_exclusive_u32_to_u64(ix.sw, ix.tile_b.as<uint32_t>(), ix.tile_a.as<uint64_t>(), nt, true, s);
+  uint64_t* const rb = ix.rb();
+  HK_HIP(hipMemcpyAsync(&rb[3], ix.tile_a.as<uint64_t>() + nt, 8, hipMemcpyDeviceToHost, s));
+  HK_HIP(hipStreamSynchronize(s));
+  const uint64_t B = rb[3];
+  if (!B) return;
+  for (int i = 0; i < 2; ++i) {
+    ix.big_k[i].ensure(B * 8 + 16);
+    ix.big_v[i].ensure(B * sizeof(V) + 16);
+  }
+  ix.big_j.ensure(B * 4 + 16);
+  uint64_t* bk[2] = {ix.big_k[0].as<uint64_t>(), ix.big_k[1].as<uint64_t>()};
+  V* bv[2] = {ix.big_v[0].as<V>(), ix.big_v[1].as<V>()};
+  {
+    TimedLaunch tm(ix.timer, "sa_big_groups", (double)A * 5 + (double)B * (8 + 2 * sizeof(V) + 4 + 8));
+    k_big_compact_rows<V><<<(unsigned)nt, GR_T, 0, s>>>(k0, v0, G, gbig, A, ix.tile_a.as<uint64_t>(), bk[0], bv[0],
+                                                        ix.big_j.as<uint32_t>());
+    HK_HIP(hipGetLastError());
+  }
+  const int sl = radix_sort_pairs<V>(ix.sw, ix.timer, bk, bv, 0, B, 0, bits, false, s);
+  ix.info[0] += ix.sw.passes_run;
+  ix.info[1] += ix.sw.passes_skipped;
+  {
+    TimedLaunch tm(ix.timer, "sa_big_groups", (double)B * (8 + sizeof(V) + 4 + 8 + sizeof(V)));
+    k_big_scatter<V><<<grid_for(B), 256, 0, s>>>(bk[sl], bv[sl], ix.big_j.as<uint32_t>(), B, k0, v0);
+    HK_HIP(hipGetLastError());
+  }
+}
+
 // one doubling round over the active list: keys, sort, regroup; see k_dbl_apply
 template <typename V>
 void dbl_round_t(Index& ix, uint64_t K) {
@@ -570,21 +699,31 @@ void dbl_round_t(Index& ix, uint64_t K) {
                                               ix.isa.as<V>(), ix.n, st.h, ib, kp[0], vp[0]);
     HK_HIP(hipGetLastError());
   }
-  // groups of < 4 members on average: each group sorted in place (k_seg_sort16) and the round applied
-  // at once, redone after the radix sort only if a group had more than SEG_MAX members (its flag rides
-  // in the round's read-back); else the radix sort of the whole list at once
-  const bool direct = st.big || A >= 4 * st.groups;
+  // groups of < 4 members on average: each group sorted in place (seg_sort_groups), the few large ones
+  // by sort_big_groups; the round is applied at once (its large-group flag rides in the read-back) and
+  // redone after sort_big_groups only if a large group was left — once one was, the next rounds read the
+  // flag first.  Larger average groups: the radix sort of the whole list.
+  const bool direct = A >= 4 * st.groups;
   unsigned int* d_big = reinterpret_cast<unsigned int*>(ix.small.as<uint8_t>() + 4356);   // small+4356: flag
+  const uint32_t* G = ix.act[cur][2].as<uint32_t>();
   int sl = 0;
+  bool spec = false;
   if (direct) {
     sl = radix_sort_pairs<V>(ix.sw, ix.timer, kp, vp, 0, A, 0, gbits + ib, false, s);
     ix.info[0] += ix.sw.passes_run;
     ix.info[1] += ix.sw.passes_skipped;
   } else {
-    HK_HIP(hipMemsetAsync(d_big, 0, 4, s));
-    TimedLaunch tm(ix.timer, "sa_pair_segsort", (double)A * (2 * 8 + 2 * sizeof(V) + 4));
-    k_seg_sort16<V><<<grid_for(A), 256, 0, s>>>(kp[0], vp[0], ix.act[cur][2].as<uint32_t>(), A, d_big);
-    HK_HIP(hipGetLastError());
+    seg_sort_groups<V>(ix, kp[0], vp[0], G, A, st.groups, d_big, "sa_pair_segsort");
+    if (st.big) {
+      uint64_t* const rb = ix.rb();
+      rb[2] = 0;
+      HK_HIP(hipMemcpyAsync(&rb[2], d_big, 4, hipMemcpyDeviceToHost, s));
+      HK_HIP(hipStreamSynchronize(s));
+      st.big = (uint32_t)rb[2] != 0;
+      if (st.big) sort_big_groups<V>(ix, kp[0], vp[0], G, A, gbits + ib);
+    } else {
+      spec = true;
+    }
   }
   const uint64_t nt = ceil_div(A, GR_TILE);
   ix.tile_a.ensure((nt + 1) * 8);
@@ -631,15 +770,13 @@ void dbl_round_t(Index& ix, uint64_t K) {
     if (flag) HK_HIP(hipMemcpyAsync(&tot[2], d_big, 4, hipMemcpyDeviceToHost, s));
     HK_HIP(hipStreamSynchronize(s));
   };
-  apply_round(sl, !direct, true);
-  if (!direct && (uint32_t)tot[2]) {   // a group over SEG_MAX members was left unsorted: redo the round
+  apply_round(sl, spec, true);
+  if (spec && (uint32_t)tot[2]) {   // a group over SEG_MAX members was left unsorted: redo the round
     st.big = true;
     // (the redo rewrites every ISA entry, list entry and group head of the first attempt; an SA / BWT
     // slot it wrote for a suffix it wrongly took as settled is rewritten by the slot's final owner)
-    sl = radix_sort_pairs<V>(ix.sw, ix.timer, kp, vp, 0, A, 0, gbits + ib, false, s);
-    ix.info[0] += ix.sw.passes_run;
-    ix.info[1] += ix.sw.passes_skipped;
-    apply_round(sl, false, false);
+    sort_big_groups<V>(ix, kp[0], vp[0], G, A, gbits + ib);
+    apply_round(0, false, false);
   }
   st.npairs = pairs ? A : 0;
   st.cur ^= 1;
@@ -812,6 +949,7 @@ void refine_loop(Index& ix, const KeyGeom& kg, int cur, uint64_t A, uint64_t gro
   uint64_t h = (uint64_t)kg.q;
   int rounds = 0;
   uint64_t A_prev = 0;
+  bool big_seen = false;   // a round had a group over SEG_MAX members
   const bool local_dbl = allow_doubling || ix.slices_local;   // doubling needs no rank exchange here
   while (A > 0 && rounds < kChunkRounds) {
     // a round that settled under a fifth of its tied suffixes (long repeats: natural-language text) hands
@@ -838,34 +976,45 @@ void refine_loop(Index& ix, const KeyGeom& kg, int cur, uint64_t A, uint64_t gro
                                                    vp[0], s_start, nS, d_srank);
       HK_HIP(hipGetLastError());
     }
-    // groups of <= SEG_MAX members sorted in place, and the round applied at once; its group-size flag
-    // comes back with the round's totals (one round trip).  A group over SEG_MAX members (it was left
-    // unsorted) redoes the round from the same keys with the global radix sort: the redo rewrites every
-    // output of the first attempt (the same SA / BWT slots, the next list, the group heads).
-    // groups of four or more members on average (natural-language text): some surely exceed SEG_MAX, so
-    // the round takes the radix sort at once instead of a segmented sort and an apply it would redo
+    // groups of four or more members on average (natural-language text): the radix sort of the whole
+    // list.  Else each group of <= SEG_MAX members sorted in place and the round applied at once, its
+    // large-group flag riding in the round's read-back; a large group left unsorted is then sorted by
+    // sort_big_groups and the round redone (every output of the first attempt rewritten), and the later
+    // rounds read the flag before applying.
     const bool direct = groups && A >= 4 * groups;
+    const uint32_t* G = ix.act[cur][2].as<uint32_t>();
     unsigned int* d_big = reinterpret_cast<unsigned int*>(ix.small.as<uint8_t>() + 4356);   // small+4356: flag
-    unsigned int h_big = direct ? 1u : 0u;
+    auto step = [&](const uint64_t* keys, const V* vals, bool flag, unsigned int* h_flag) {
+      return refine_step<V>(ix, kg, keys, vals, ix.act[cur][1].as<uint32_t>(), A, 0, false, true,
+                            ix.act[cur ^ 1][0].as<V>(), ix.act[cur ^ 1][1].as<uint32_t>(),
+                            ix.act[cur ^ 1][2].as<uint32_t>(), ix.head_slot.as<uint32_t>(), flag ? d_big : nullptr,
+                            h_flag);
+    };
     std::pair<uint64_t, uint64_t> r{0, 0};
-    if (!direct) {
-      HK_HIP(hipMemsetAsync(d_big, 0, 4, s));
-      {
-        TimedLaunch tm(ix.timer, "sa_refine_segsort", (double)A * (2 * 8 + 2 * sizeof(V) + 4));
-        k_seg_sort16<V><<<grid_for(A), 256, 0, s>>>(kp[0], vp[0], ix.act[cur][2].as<uint32_t>(), A, d_big);
-        HK_HIP(hipGetLastError());
-      }
-      r = refine_step<V>(ix, kg, kp[0], vp[0], ix.act[cur][1].as<uint32_t>(), A, 0, false, true,
-                         ix.act[cur ^ 1][0].as<V>(), ix.act[cur ^ 1][1].as<uint32_t>(),
-                         ix.act[cur ^ 1][2].as<uint32_t>(), ix.head_slot.as<uint32_t>(), d_big, &h_big);
-    }
-    if (h_big) {
+    if (direct) {
       const int sl = radix_sort_pairs<V>(ix.sw, ix.timer, kp, vp, 0, A, 0, 64, false, s);
       ix.info[0] += ix.sw.passes_run;
       ix.info[1] += ix.sw.passes_skipped;
-      r = refine_step<V>(ix, kg, kp[sl], vp[sl], ix.act[cur][1].as<uint32_t>(), A, 0, false, true,
-                         ix.act[cur ^ 1][0].as<V>(), ix.act[cur ^ 1][1].as<uint32_t>(),
-                         ix.act[cur ^ 1][2].as<uint32_t>(), ix.head_slot.as<uint32_t>());
+      r = step(kp[sl], vp[sl], false, nullptr);
+    } else {
+      seg_sort_groups<V>(ix, kp[0], vp[0], G, A, groups, d_big, "sa_refine_segsort");
+      unsigned int h_big = 0;
+      if (big_seen) {
+        uint64_t* const rb = ix.rb();
+        rb[2] = 0;
+        HK_HIP(hipMemcpyAsync(&rb[2], d_big, 4, hipMemcpyDeviceToHost, s));
+        HK_HIP(hipStreamSynchronize(s));
+        big_seen = (uint32_t)rb[2] != 0;
+        if (big_seen) sort_big_groups<V>(ix, kp[0], vp[0], G, A, 64);
+        r = step(kp[0], vp[0], false, nullptr);
+      } else {
+        r = step(kp[0], vp[0], true, &h_big);
+        if (h_big) {
+          big_seen = true;
+          sort_big_groups<V>(ix, kp[0], vp[0], G, A, 64);
+          r = step(kp[0], vp[0], false, nullptr);
+        }
+      }
     }
     cur ^= 1;
     A = r.first;
