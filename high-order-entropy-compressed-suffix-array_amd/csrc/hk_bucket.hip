@@ -3920,10 +3920,8 @@ struct FusedSlice {
   uint64_t* startA = nullptr;            // digit starts (pass B regions)
   std::vector<uint64_t> hist, totA;      // bin counts, digit totals
 };
-struct FusedState {
+struct FusedState {   // (its buffers are the handle's fused_recs / fused_ws / fused_host)
   std::vector<FusedSlice> sl;
-  DevBuf recs, ws;
-  HostBuf hb;
 };
 
 static TextKeySrc slice_tks(Index& ix, const KeyGeom& kk, int lb) {
@@ -4001,8 +3999,9 @@ bool slices_fuse(Index& ix, const std::vector<uint32_t>& B, const std::vector<ui
   {
     size_t fr = 0, tot = 0;
     HK_HIP(hipMemGetInfo(&fr, &tot));
+    const uint64_t held = ix.fused_recs.bytes + ix.fused_ws.bytes;   // (reused, or freed by a regrowth)
     const uint64_t need = msum * 8 + wsw * 8 + mmax * 40 + (1ull << 30);
-    if ((double)need > 0.9 * (double)fr) return false;
+    if ((double)need > 0.9 * (double)(fr + held)) return false;
   }
   const SlicePlan& P0 = st->sl[0].P;
   upload_geometry(ix, P0.kk);
@@ -4012,9 +4011,9 @@ bool slices_fuse(Index& ix, const std::vector<uint32_t>& B, const std::vector<ui
   ix.cp_part.ensure((uint64_t)nspan * maxnb2 * 4 + (uint64_t)nspan * CP_NAM * 4 + 16);
   uint32_t* d_part = ix.cp_part.as<uint32_t>();
   uint32_t* d_spanc = d_part + (uint64_t)nspan * maxnb2;
-  st->ws.ensure(wsw * 8);
-  st->hb.ensure(hw * 8 + 64);
-  uint64_t* w = st->ws.as<uint64_t>();
+  ix.fused_ws.ensure(wsw * 8);
+  ix.fused_host.ensure(hw * 8 + 64);
+  uint64_t* w = ix.fused_ws.as<uint64_t>();
   unsigned long long* d_ovf = reinterpret_cast<unsigned long long*>(w);
   HK_HIP(hipMemsetAsync(d_ovf, 0, 8, s));
   w += 16;
@@ -4037,7 +4036,7 @@ bool slices_fuse(Index& ix, const std::vector<uint32_t>& B, const std::vector<ui
     slice_prepass(ix, P, tks, span, nspan, d_part, d_spanc, c, false);
   }
   // counts back behind an event while pass A runs
-  uint64_t* h = st->hb.as<uint64_t>();
+  uint64_t* h = ix.fused_host.as<uint64_t>();
   std::vector<uint64_t*> h_hist(ns), h_tot(ns);
   hipEvent_t ev_pre, ev_cnt;
   HK_HIP(hipEventCreateWithFlags(&ev_pre, hipEventDisableTiming));
@@ -4057,14 +4056,14 @@ bool slices_fuse(Index& ix, const std::vector<uint32_t>& B, const std::vector<ui
   HK_HIP(hipMemcpyAsync(h_ovf, d_ovf, 8, hipMemcpyDeviceToHost, ix.aux_stream));
   HK_HIP(hipEventRecord(ev_cnt, ix.aux_stream));
   // pass A of the group
-  st->recs.ensure(msum * 8 + 16);
+  ix.fused_recs.ensure(msum * 8 + 16);
   FusedSel fs{};
   fs.ns = ns;
   fs.gd0 = P0.sl.base >> 8;
   uint64_t off = 0;
   for (int i = 0; i < ns; ++i) {
     FusedSlice& f = st->sl[i];
-    f.kA = st->recs.as<uint64_t>() + off;
+    f.kA = ix.fused_recs.as<uint64_t>() + off;
     off += f.m;
     fs.kout[i] = f.kA;
     fs.cur[i] = cur[i].curA;

@@ -152,6 +152,8 @@ struct Index {
   bool sa_pos64 = false;       // sharded slices of texts with n >= 2^32 hold u64 positions
   bool slices_local = false;   // build_sa_slices: the slices' doubling updates one local ISA (no exchange)
   std::shared_ptr<void> fused;  // build_sa_slices: a group's fused pass A (records + cursors per slice)
+  DevBuf fused_recs, fused_ws;  // ... its records and cursor sets (kept across builds: allocating and freeing
+  HostBuf fused_host;           // tens of GB per build stalled some builds by seconds)
   uint64_t shard_lo = 0, shard_hi = 0;
   std::vector<uint64_t> shard_bounds;   // SA slice starts of every rank (+ n), from the RCCL build
 

@@ -173,6 +173,44 @@ __global__ __launch_bounds__(256) void k_refine_keys(const V* __restrict__ P, co
 // Equal keys may swap (they stay tied, and their slots are reassigned by the next round).
 constexpr int SEG_MAX = 16;
 
+// bitonic network over N registers (the group's sz <= N members, padded with ~0 keys), sorted in place
+template <int N, typename V>
+__device__ __forceinline__ void seg_sort_net(uint64_t* __restrict__ keys, V* __restrict__ vals, uint32_t sz) {
+  uint64_t k[N];
+  V v[N];
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    k[i] = (uint32_t)i < sz ? keys[i] : ~0ull;
+    v[i] = (uint32_t)i < sz ? vals[i] : (V)0;
+  }
+#pragma unroll
+  for (int size = 2; size <= N; size <<= 1) {
+#pragma unroll
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+#pragma unroll
+      for (int i = 0; i < N; ++i) {
+        const int j = i ^ stride;
+        if (j > i) {
+          const bool up = (i & size) == 0;
+          const bool sw = up ? k[i] > k[j] : k[i] < k[j];
+          const uint64_t ki = k[i], kj = k[j];
+          const V vi = v[i], vj = v[j];
+          k[i] = sw ? kj : ki;
+          k[j] = sw ? ki : kj;
+          v[i] = sw ? vj : vi;
+          v[j] = sw ? vi : vj;
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < N; ++i)
+    if ((uint32_t)i < sz) {
+      keys[i] = k[i];
+      vals[i] = v[i];
+    }
+}
+
 template <typename V>
 __global__ __launch_bounds__(256) void k_seg_sort16(uint64_t* __restrict__ keys, V* __restrict__ vals,
                                                     const uint32_t* __restrict__ G, uint64_t A,
@@ -188,39 +226,19 @@ __global__ __launch_bounds__(256) void k_seg_sort16(uint64_t* __restrict__ keys,
       continue;
     }
     if (sz == 1) continue;
-    uint64_t k[SEG_MAX];
-    V v[SEG_MAX];
-#pragma unroll
-    for (int i = 0; i < SEG_MAX; ++i) {
-      k[i] = (uint32_t)i < sz ? keys[a + i] : ~0ull;
-      v[i] = (uint32_t)i < sz ? vals[a + i] : (V)0;
-    }
-#pragma unroll
-    for (int size = 2; size <= SEG_MAX; size <<= 1) {
-#pragma unroll
-      for (int stride = size >> 1; stride > 0; stride >>= 1) {
-#pragma unroll
-        for (int i = 0; i < SEG_MAX; ++i) {
-          const int j = i ^ stride;
-          if (j > i) {
-            const bool up = (i & size) == 0;
-            const bool sw = up ? k[i] > k[j] : k[i] < k[j];
-            const uint64_t ki = k[i], kj = k[j];
-            const V vi = v[i], vj = v[j];
-            k[i] = sw ? kj : ki;
-            k[j] = sw ? ki : kj;
-            v[i] = sw ? vj : vi;
-            v[j] = sw ? vi : vj;
-          }
-        }
+    if (sz == 2) {   // (pairs: most groups of a doubling round over long repeats)
+      const uint64_t k0 = keys[a], k1 = keys[a + 1];
+      if (k1 < k0) {
+        const V v0 = vals[a], v1 = vals[a + 1];
+        keys[a] = k1;
+        keys[a + 1] = k0;
+        vals[a] = v1;
+        vals[a + 1] = v0;
       }
+      continue;
     }
-#pragma unroll
-    for (int i = 0; i < SEG_MAX; ++i)
-      if ((uint32_t)i < sz) {
-        keys[a + i] = k[i];
-        vals[a + i] = v[i];
-      }
+    if (sz <= 4) seg_sort_net<4>(keys + a, vals + a, sz);
+    else seg_sort_net<SEG_MAX>(keys + a, vals + a, sz);
   }
 }
 
@@ -1310,6 +1328,16 @@ void release_workspace(Index& ix) {
   ix.sw.status.release();
   ix.sw.status_tiles = 0;
   ix.sw.scan_tmp.release();
+  for (int i = 0; i < 2; ++i) {
+    ix.big_k[i].release();
+    ix.big_v[i].release();
+  }
+  ix.big_j.release();
+  ix.grp_big.release();
+  ix.fused.reset();
+  ix.fused_recs.release();
+  ix.fused_ws.release();
+  ix.fused_host.release();
 }
 
 }  // namespace hk
