@@ -969,15 +969,13 @@ void refine_loop(Index& ix, const KeyGeom& kg, int cur, uint64_t A, uint64_t gro
   uint64_t A_prev = 0;
   bool big_seen = false;   // a round had a group over SEG_MAX members
   const bool local_dbl = allow_doubling || ix.slices_local;   // doubling needs no rank exchange here
-  // a list still holding over a quarter of the suffixes after the first sort (natural-language text:
-  // 84 %) goes straight to prefix doubling: a doubling round doubles the compared prefix for one ISA
-  // gather per suffix, a chunk round reads q more symbols of T' per suffix
   const uint64_t m_all = ix.sharded ? ix.shard_hi - ix.shard_lo : ix.n;
-  const bool straight = local_dbl && A > m_all / 4;
-  while (A > 0 && rounds < kChunkRounds && !straight) {
-    // a round that settled under a fifth of its tied suffixes (long repeats: natural-language text) hands
-    // over to prefix doubling, whose shared prefix doubles each round instead of growing by one chunk
-    if (local_dbl && rounds > 0 && A * 5 > A_prev * 4) break;
+  while (A > 0 && rounds < kChunkRounds) {
+    // after the first chunk round (it also places the short suffixes), a round that settled under a fifth
+    // of its tied suffixes, or a list still holding over a quarter of all suffixes (natural-language text:
+    // 108M of 200M), hands over to prefix doubling: a doubling round doubles the compared prefix for one
+    // ISA gather per suffix, a chunk round reads the next chunk of T' per suffix
+    if (local_dbl && rounds > 0 && (A * 5 > A_prev * 4 || A > m_all / 4)) break;
     int gbits = 0;
     while (gbits < 64 && (1ull << gbits) < groups) ++gbits;
     auto fits = [&](int qq) {   // G in the top gbits, chunk + nS (<= R^qq - 1 + nS) below
