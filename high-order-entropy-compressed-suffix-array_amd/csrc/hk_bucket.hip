@@ -1197,15 +1197,21 @@ __device__ __forceinline__ uint64_t stamp() {
 // ranked, reserved and written on its own (non-iid text), as in k_slice_cpart.
 constexpr int SL_G = 8;
 
-template <bool TRACE = false>
-__global__ __launch_bounds__(CP_T, 4) void k_slice_cpart_reg(uint64_t* __restrict__ kout, uint64_t n,
+// G: sub-tiles per unit held in registers; CAP: staging capacity (records of one write-out).  CAP =
+// CP_TILE / 2 (N >= 4: units of <= 4 sub-tiles keep ~1/N of their positions) halves the LDS to ~41 KiB,
+// so three workgroups share a CU instead of two (the kernel waits between its DMA, ranking and write
+// phases); a dense sub-tile is then staged in two halves (its positions k < 8, then k >= 8).
+template <bool TRACE = false, int G = SL_G, int CAP = CP_TILE>
+__global__ __launch_bounds__(CP_T, CAP == CP_TILE ? 4 : 6) void k_slice_cpart_reg(uint64_t* __restrict__ kout, uint64_t n,
                                                              unsigned long long* __restrict__ cur, uint64_t span,
                                                              TextKeySrc src, SliceSel sl,
                                                              const unsigned long long* __restrict__ skip,
                                                              uint64_t mcap, uint64_t* __restrict__ trace = nullptr) {
   constexpr int T = CP_T;
-  __shared__ uint64_t keys[CP_TILE + 8];   // round 1: the unit's text image (<= 8 sub-tiles + 64 B)
-  __shared__ uint8_t sdg[CP_TILE];
+  static_assert((uint64_t)G * SL_SUB + 64 <= (uint64_t)(CAP + 8) * 8, "the unit's text image fits the staging");
+  static_assert(CAP == CP_TILE || CAP == CP_TILE / 2, "full or half staging");
+  __shared__ uint64_t keys[CAP + 8];   // round 1: the unit's text image (<= G sub-tiles + 64 B)
+  __shared__ uint8_t sdg[CAP];
   __shared__ uint32_t tg[CP_NAM], cnt[CP_NAM], wsum[CP_NAM / 64];
   __shared__ uint16_t LP[256];
   __shared__ uint64_t SK[72];
@@ -1255,9 +1261,9 @@ __global__ __launch_bounds__(CP_T, 4) void k_slice_cpart_reg(uint64_t* __restric
   const uint64_t sbase = (uint64_t)sl.base << sl.bsh;
   const int kbits = 2 * src.g.q, dsh = 32 - sl.DB;
   // ---- round 1: packed codes (from the LDS image), kept-position masks, digit counts
-  uint32_t c[SL_G][3], msk[SL_G], pcs = 0;
+  uint32_t c[G][3], msk[G], pcs = 0;
 #pragma unroll
-  for (int st = 0; st < SL_G; ++st) {
+  for (int st = 0; st < G; ++st) {
     msk[st] = 0;
     c[st][0] = c[st][1] = c[st][2] = 0;
     const uint64_t p0 = ubase + (uint64_t)st * SL_SUB + 16ull * tid;
@@ -1335,7 +1341,7 @@ __global__ __launch_bounds__(CP_T, 4) void k_slice_cpart_reg(uint64_t* __restric
     cnt[tid] = 0;
   }
   auto write_out = [&](uint32_t cnt_tile, uint32_t hi256) {
-    for (int i = 0; i < CP_I; ++i) {
+    for (int i = 0; i < CAP / T; ++i) {
       const uint32_t s = (uint32_t)i * T + tid;
       if (s < cnt_tile) {
         const uint32_t d = (uint32_t)sdg[s] | (s >= hi256 ? 256u : 0u);
@@ -1344,13 +1350,13 @@ __global__ __launch_bounds__(CP_T, 4) void k_slice_cpart_reg(uint64_t* __restric
       }
     }
   };
-  if (total <= (uint32_t)CP_TILE) {
+  if (total <= (uint32_t)CAP) {
     const unsigned long long resv = cu ? atomicAdd(&row[tid], (unsigned long long)cu) : 0ull;
     __syncthreads();
     if (TRACE) ts[2] = stamp();
     // ---- round 2: key and stage the kept positions only
 #pragma unroll
-    for (int st = 0; st < SL_G; ++st) {
+    for (int st = 0; st < G; ++st) {
       uint32_t m = msk[st];
       while (m) {   // two kept positions a trip: their slot atomics in flight together
         const int k = __builtin_ctz(m);
@@ -1363,11 +1369,11 @@ __global__ __launch_bounds__(CP_T, 4) void k_slice_cpart_reg(uint64_t* __restric
         const uint32_t d2 = record_at(st, k2, rec2);
         uint32_t f = tg[d] + atomicAdd(&cnt[d], 1u);
         uint32_t f2 = two ? tg[d2] + atomicAdd(&cnt[d2], 1u) : 0u;
-        f = f < (uint32_t)CP_TILE ? f : (uint32_t)CP_TILE - 1;   // (only a count mismatch overruns)
+        f = f < (uint32_t)CAP ? f : (uint32_t)CAP - 1;   // (only a count mismatch overruns)
         keys[f] = rec;
         sdg[f] = (uint8_t)d;
         if (two) {
-          f2 = f2 < (uint32_t)CP_TILE ? f2 : (uint32_t)CP_TILE - 1;
+          f2 = f2 < (uint32_t)CAP ? f2 : (uint32_t)CAP - 1;
           keys[f2] = rec2;
           sdg[f2] = (uint8_t)d2;
         }
@@ -1384,47 +1390,52 @@ __global__ __launch_bounds__(CP_T, 4) void k_slice_cpart_reg(uint64_t* __restric
     trace_out();
     return;
   }
-  // dense unit: each sub-tile counted, reserved, staged and written on its own (ranks by a second
-  // round of atomics, as the fast path: no per-position rank registers)
+  // dense unit: each sub-tile (half staging: each half of a sub-tile) counted, reserved, staged and written on
+  // its own (ranks by a second round of atomics, as the fast path: no per-position rank registers)
+  constexpr int PARTS = CAP == CP_TILE ? 1 : 2;
 #pragma unroll
-  for (int st = 0; st < SL_G; ++st) {   // (unrolled: c[st] / msk[st] stay register-resident)
+  for (int st = 0; st < G; ++st) {   // (unrolled: c[st] / msk[st] stay register-resident)
     if ((uint32_t)st >= nsub) break;   // uniform
-    __syncthreads();   // the previous write-out has read keys / tg; counters free
-    cnt[tid] = 0;
-    __syncthreads();
-    for (uint32_t m = msk[st]; m; m &= m - 1) {
-      uint64_t rec;
-      atomicAdd(&cnt[record_at(st, __builtin_ctz(m), rec)], 1u);
-    }
-    __syncthreads();
-    const uint32_t cc = cnt[tid];
-    const unsigned long long g = cc ? atomicAdd(&row[tid], (unsigned long long)cc) : 0ull;
-    const uint32_t inc = wave_incl_sum<uint32_t>(cc);
-    if (lane == 63) wsum[wv] = inc;
-    __syncthreads();
-    uint32_t carry = 0, tot = 0;
 #pragma unroll
-    for (uint32_t w = 0; w < T / 64; ++w) {
-      carry += w < wv ? wsum[w] : 0u;
-      tot += wsum[w];
+    for (int part = 0; part < PARTS; ++part) {
+      const uint32_t pm = PARTS == 1 ? msk[st] : (msk[st] & (part ? 0xFF00u : 0x00FFu));
+      __syncthreads();   // the previous write-out has read keys / tg; counters free
+      cnt[tid] = 0;
+      __syncthreads();
+      for (uint32_t m = pm; m; m &= m - 1) {
+        uint64_t rec;
+        atomicAdd(&cnt[record_at(st, __builtin_ctz(m), rec)], 1u);
+      }
+      __syncthreads();
+      const uint32_t cc = cnt[tid];
+      const unsigned long long g = cc ? atomicAdd(&row[tid], (unsigned long long)cc) : 0ull;
+      const uint32_t inc = wave_incl_sum<uint32_t>(cc);
+      if (lane == 63) wsum[wv] = inc;
+      __syncthreads();
+      uint32_t carry = 0, tot = 0;
+#pragma unroll
+      for (uint32_t w = 0; w < T / 64; ++w) {
+        carry += w < wv ? wsum[w] : 0u;
+        tot += wsum[w];
+      }
+      tg[tid] = carry + inc - cc;
+      cnt[tid] = 0;
+      __syncthreads();
+      for (uint32_t m = pm; m; m &= m - 1) {
+        uint64_t rec;
+        const uint32_t d = record_at(st, __builtin_ctz(m), rec);
+        const uint32_t f = tg[d] + atomicAdd(&cnt[d], 1u);
+        keys[f] = rec;
+        sdg[f] = (uint8_t)d;
+      }
+      __syncthreads();
+      const uint32_t hi256 = tg[256];
+      const uint32_t gbv = (uint32_t)(g - tg[tid]);
+      __syncthreads();
+      tg[tid] = gbv;
+      __syncthreads();
+      write_out(tot, hi256);
     }
-    tg[tid] = carry + inc - cc;
-    cnt[tid] = 0;
-    __syncthreads();
-    for (uint32_t m = msk[st]; m; m &= m - 1) {
-      uint64_t rec;
-      const uint32_t d = record_at(st, __builtin_ctz(m), rec);
-      const uint32_t f = tg[d] + atomicAdd(&cnt[d], 1u);
-      keys[f] = rec;
-      sdg[f] = (uint8_t)d;
-    }
-    __syncthreads();
-    const uint32_t hi256 = tg[256];
-    const uint32_t gbv = (uint32_t)(g - tg[tid]);
-    __syncthreads();
-    tg[tid] = gbv;
-    __syncthreads();
-    write_out(tot, hi256);
   }
 }
 
@@ -3585,6 +3596,7 @@ struct SlicePlan {
   int D = 0, lb = 0, pb = 0, hb = 0;   // hb: key planes' position-high bits (u64 SA)
   bool packed = false;
   bool reg = false;   // radix 2^2 packed records with a perm-table byte field: the register kernels
+  bool half = false;  // register pass A with half staging (three workgroups per CU; slices of <= 1/6 of T')
   PkGeom pg;
   int uhb = 0;
 };
@@ -3824,7 +3836,11 @@ static int cursor_partition_slice(Index& ix, const SlicePlan& P, const TextKeySr
         DevBuf tb;
         tb.ensure((uint64_t)grid * 64 + 64);
         HK_HIP(hipMemsetAsync(tb.p, 0, (uint64_t)grid * 64, s));
-        k_slice_cpart_reg<true><<<grid, CP_T, 0, s>>>(kp[outA], n, d_curA, span, tks2, sl, skip, m, tb.as<uint64_t>());
+        if (P.half)
+          k_slice_cpart_reg<true, 4, CP_TILE / 2><<<grid, CP_T, 0, s>>>(kp[outA], n, d_curA, span, tks2, sl, skip, m,
+                                                                       tb.as<uint64_t>());
+        else
+          k_slice_cpart_reg<true><<<grid, CP_T, 0, s>>>(kp[outA], n, d_curA, span, tks2, sl, skip, m, tb.as<uint64_t>());
         std::vector<uint64_t> h((uint64_t)grid * 8);
         HK_HIP(hipMemcpyAsync(h.data(), tb.p, h.size() * 8, hipMemcpyDeviceToHost, s));
         HK_HIP(hipStreamSynchronize(s));
@@ -3839,7 +3855,10 @@ static int cursor_partition_slice(Index& ix, const SlicePlan& P, const TextKeySr
           fprintf(stderr, "[slice_cpart_reg trace] %llu units, mean cycles: round 1 %.0f, count+reserve %.0f, "
                   "round 2 %.0f, write %.0f\n", (unsigned long long)nw, acc[0] / nw, acc[1] / nw, acc[2] / nw, acc[3] / nw);
       } else {
-        k_slice_cpart_reg<<<grid, CP_T, 0, s>>>(kp[outA], n, d_curA, span, tks2, sl, skip, m);
+        if (P.half)
+          k_slice_cpart_reg<false, 4, CP_TILE / 2><<<grid, CP_T, 0, s>>>(kp[outA], n, d_curA, span, tks2, sl, skip, m);
+        else
+          k_slice_cpart_reg<<<grid, CP_T, 0, s>>>(kp[outA], n, d_curA, span, tks2, sl, skip, m);
       }
     }
     else if (P.packed && P.lb == 2)
@@ -4158,6 +4177,12 @@ void build_slice_keyed(Index& ix, uint32_t c_lo, uint32_t c_hi, uint64_t m) {
     uint32_t g = (uint32_t)std::floor(0.9 * ratio);
     if (g < 1) g = 1;
     if (g > (P.reg ? (uint32_t)SL_G : 64u)) g = P.reg ? (uint32_t)SL_G : 64u;   // register kernel: <= SL_G
+    // a slice of <= 1/6 of the text (N >= 6 ranks): half staging, units of <= 4 sub-tiles keeping ~0.45 of
+    // a full tile, so three workgroups share a CU
+    if (P.reg && ratio >= 6.0) {
+      P.half = true;
+      g = std::min<uint32_t>(4, (uint32_t)std::floor(0.45 * ratio));
+    }
     P.sl.g = g;
   }
   const TextKeySrc tks = slice_tks(ix, kk, P.lb);
