@@ -2139,11 +2139,52 @@ __device__ __forceinline__ bool bucket_sort_fast(BfShared<T, I>& sh, uint2 it, c
   }
   if (wv == 0 && ntie) {
     const uint64_t tb = __shfl(tbase, 0, 64);
+    // the tied records in slot order (the refinement takes the tie list as runs of whole groups, each
+    // group's records consecutive and its head first): wave 0 alone sets bit masks of the tied and the
+    // head final indices over the bin lists (free after section 5) and walks them in order
+    if (ntie <= 64) {   // (most items) a record per lane, ranked by its final index against the others
+      const uint32_t e = lane < ntie ? tlist[lane] : 0xFFFFu, q = e & 0x7FFFu;
+      uint32_t r = 0;
+      for (uint32_t i = 0; i < ntie; ++i) r += (tlist[i] & 0x7FFFu) < q ? 1u : 0u;
+      if (lane < ntie) {
+        const uint32_t f = q + sto;
+        const uint32_t pv = sh.aux[f];
+        tie_k[tb + r] = (((uint64_t)start + q) << 1) | (e >> 15);
+        tie_v[tb + r] = (V)(((uint64_t)(pv >> pb) << 32) | sh.buf[f]);
+      }
+      return true;
+    }
+    uint32_t* const tbits = reinterpret_cast<uint32_t*>(blist);
+    const uint32_t nwd = (cnt + 31) / 32;
+    static_assert(2 * ((SH::CAP + 31) / 32) * 4 <= BF_BIGCAP * 2, "tie bit masks fit the bin lists");
+    for (uint32_t i = lane; i < 2 * nwd; i += 64) tbits[i] = 0;
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
     for (uint32_t i = lane; i < ntie; i += 64) {
-      const uint32_t e = tlist[i], f = (e & 0x7FFFu) + sto;
-      const uint32_t pv = sh.aux[f];
-      tie_k[tb + i] = (((uint64_t)start + (f - sto)) << 1) | (e >> 15);
-      tie_v[tb + i] = (V)(((uint64_t)(pv >> pb) << 32) | sh.buf[f]);
+      const uint32_t e = tlist[i], q = e & 0x7FFFu;
+      atomicOr(&tbits[q >> 5], 1u << (q & 31));
+      if (e >> 15) atomicOr(&tbits[nwd + (q >> 5)], 1u << (q & 31));
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    uint32_t run = 0;
+    for (uint32_t w0 = 0; w0 < nwd; w0 += 64) {   // 64 mask words per step, ranked by a wave scan
+      const uint32_t w = w0 + lane;
+      uint32_t bits = w < nwd ? tbits[w] : 0u;
+      const uint32_t hw = w < nwd ? tbits[nwd + w] : 0u;
+      const uint32_t c = __popc(bits);
+      const uint32_t inc = wave_incl_sum<uint32_t>(c);
+      uint32_t r = run + inc - c;
+      while (bits) {
+        const uint32_t b = __builtin_ctz(bits);
+        bits &= bits - 1;
+        const uint32_t q = 32 * w + b, f = q + sto;
+        const uint32_t pv = sh.aux[f];
+        tie_k[tb + r] = (((uint64_t)start + q) << 1) | ((hw >> b) & 1u);
+        tie_v[tb + r] = (V)(((uint64_t)(pv >> pb) << 32) | sh.buf[f]);
+        ++r;
+      }
+      run += __shfl(inc, 63, 64);
     }
   }
   return true;
@@ -2445,7 +2486,7 @@ __device__ __forceinline__ void bucket_sort_item(BsShared& sh, uint2 it, const u
     sh.rv[1][0] = b;
   }
   __syncthreads();
-  uint64_t tpos = sh.rv[1][0] + (tinc - nt);
+  uint64_t tpos = sh.rv[1][0];   // the wave's ties follow the earlier waves' (slot order: wave-major)
   for (uint32_t w = 0; w < wv; ++w) tpos += wt[w];
   __syncthreads();
 
@@ -2469,11 +2510,16 @@ __device__ __forceinline__ void bucket_sort_item(BsShared& sh, uint2 it, const u
       sab[r] = p;
       bwb[r] = sh.inv[pv & pmask];
     }
-    if (valid && ((tmask >> k) & 1u)) {
-      tie_k[tpos] = (((uint64_t)start + r) << 1) | ((hmask >> k) & 1u);
-      tie_v[tpos] = p;
-      ++tpos;
+    // in slot order (inside a wave: k-major, lane-minor), so that each group's records are consecutive
+    // in the tie list and its head comes first
+    const bool tie = valid && ((tmask >> k) & 1u);
+    const uint64_t tb = ballot64(tie);
+    if (tie) {
+      const uint64_t at = tpos + mbcnt(tb);
+      tie_k[at] = (((uint64_t)start + r) << 1) | ((hmask >> k) & 1u);
+      tie_v[at] = p;
     }
+    tpos += (uint32_t)__popcll(tb);
   }
   if (TRACE) {
     ts[5] = stamp();
@@ -3096,18 +3142,17 @@ void refine_from_ties(Index& ix, const KeyGeom& kg, uint64_t A, bool allow_doubl
     ix.act[i][2].ensure(A * 4 + 16);
   }
   ix.head_slot.ensure(A * 4 + 16);
-  // order the list by slot: key = J << 1 | head
-  uint64_t* kp[2] = {ix.ties_k.as<uint64_t>(), ix.keys[1].as<uint64_t>()};
-  V* vp[2] = {ix.ties_v.as<V>(), ix.vals[1].as<V>()};
-  int hb = 1;
-  while (hb < 64 && ((ix.n << 1) >> hb)) ++hb;
-  const int sl = radix_sort_pairs<V>(ix.sw, ix.timer, kp, vp, 0, A, 0, hb, false, s);
+  // The list needs no sort by slot: every producer writes runs of whole groups, each group's records
+  // consecutive with its head first (the bucket sorts append one item's ties in slot order, the
+  // big-bucket path refine_step's grouped output); the groups' order in the list is free.
+  uint64_t* const tk = ix.ties_k.as<uint64_t>();
+  const V* const tv = ix.ties_v.as<V>();
   V* P = ix.act[0][0].as<V>();
   uint32_t* J = ix.act[0][1].as<uint32_t>();
   uint32_t* GH = ix.act[0][2].as<uint32_t>();
-  k_tie_split<V><<<grid_of(A), 256, 0, s>>>(kp[sl], vp[sl], A, P, J, GH);
+  k_tie_split<V><<<grid_of(A), 256, 0, s>>>(tk, tv, A, P, J, GH);
   HK_HIP(hipGetLastError());
-  uint64_t* hx = kp[sl ^ 1];   // u64 scratch (A + 1)
+  uint64_t* hx = tk;   // u64 scratch (A + 1): the list is consumed
   scan_exclusive_u32_to_u64(ix.sw, GH, hx, A, true, s);
   k_tie_groups<<<grid_of(A), 256, 0, s>>>(hx, J, A, GH, ix.head_slot.as<uint32_t>());
   HK_HIP(hipGetLastError());

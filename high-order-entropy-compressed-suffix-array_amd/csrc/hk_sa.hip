@@ -483,7 +483,7 @@ __global__ __launch_bounds__(GR_T) void k_dbl_stats_rows(const uint64_t* __restr
     uint64_t cur, prev;
     row_neighbors(keys, j, A, 0, h, hn, cur, prev);
     if (h) {
-      const uint64_t v = ((uint64_t)J[j] << 1 | ((j == 0 || (cur >> ib) != (prev >> ib)) ? 1u : 0u)) + 1;
+      const uint64_t v = (j << 1 | ((j == 0 || (cur >> ib) != (prev >> ib)) ? 1u : 0u)) + 1;
       last = v > last ? v : last;
     }
     if (!(h && hn)) c += h ? 0x10001u : 1u;
@@ -524,7 +524,9 @@ __global__ __launch_bounds__(GR_T) void k_dbl_apply_rows(
   __shared__ uint32_t wc[2][GR_T / 64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const uint64_t tbase = (uint64_t)blockIdx.x * GR_TILE;
-  // 1 + (slot << 1 | first) of the last group head so far (0: none), tied so far, tied heads so far
+  // 1 + (list index << 1 | first) of the last group head so far (0: none), tied so far, tied heads so far.
+  // (The list index, not the head's slot: the tie list holds whole groups in any order of groups.  A
+  // group's slots are contiguous and ascending along the list, so the head's slot is jv - (j - index).)
   uint64_t run_h = carry_last[blockIdx.x], run_o = act_off[blockIdx.x], run_g = head_off[blockIdx.x];
   for (int k = 0; k < GR_I; ++k) {   // (uniform: every thread runs every row's scans)
     const uint64_t j = tbase + (uint64_t)k * GR_T + threadIdx.x;
@@ -540,7 +542,7 @@ __global__ __launch_bounds__(GR_T) void k_dbl_apply_rows(
       p = P[j];
       a = (h && hn) ? 0u : 1u;
       th = a && h ? 1u : 0u;
-      if (h) hv = ((uint64_t)jv << 1 | ((j == 0 || (cur >> ib) != (prev >> ib)) ? 1u : 0u)) + 1;
+      if (h) hv = (j << 1 | ((j == 0 || (cur >> ib) != (prev >> ib)) ? 1u : 0u)) + 1;
     }
     const uint64_t mi = wave_incl_max<uint64_t>(hv);
     const uint32_t ci = dpp_incl_sum(a | th << 16);
@@ -564,8 +566,8 @@ __global__ __launch_bounds__(GR_T) void k_dbl_apply_rows(
     }
     hm = hm > mi ? hm : mi;
     if (valid) {
-      const uint64_t g = hm - 1;   // this suffix's group head: slot << 1 | first (j's head is at or before j)
-      const uint64_t v = lo + (g >> 1);
+      const uint64_t g = hm - 1;   // this suffix's group head: index << 1 | first (j's head is at or before j)
+      const uint64_t v = lo + (jv - (j - (g >> 1)));
       if (pairs) {
         pairs[2 * j] = (uint64_t)p;
         pairs[2 * j + 1] = v;
@@ -953,7 +955,8 @@ void refine_after_sort(Index& ix, const KeyGeom& kg, int slot, uint64_t m, bool 
   refine_loop<V>(ix, kg, 0, r0.first, r0.second, allow_doubling);
 }
 
-// The tied suffixes (P, J = SA slot, G = dense group ordinal in slot order) are in act[cur];
+// The tied suffixes (P, J = SA slot, G = dense group ordinal in list order: whole groups in any order,
+// each one's slots contiguous and ascending along the list) are in act[cur];
 // each round sorts them by (G, next symbols from offset h) and re-groups.
 template <typename V>
 void refine_loop(Index& ix, const KeyGeom& kg, int cur, uint64_t A, uint64_t groups, bool allow_doubling) {
