@@ -772,6 +772,8 @@ def parse_args(argv=None):
     ap.add_argument("--pos64", action="store_true", help="sharded build with 64-bit positions at any n")
     ap.add_argument("--global-sort", action="store_true",
                     help="single-GPU build by full-width LSD sort of the keys (no LDS bucket sorts)")
+    ap.add_argument("--only-leg", choices=("english",), default=None,
+                    help="run only this detail leg (profiling): english = the 200 MiB English-like leg")
     ap.add_argument("--launch-check", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--traffic-gb", type=float, default=None,
                     help="PMC-measured HBM GB per launch of the dominant kernel; default: profiles/pmc_kernels.json")
@@ -802,6 +804,8 @@ def main():
             res = run_sharded(args, rank, world, int(os.environ.get("LOCAL_RANK", "0")))
         dist.barrier()
         dist.destroy_process_group()
+    elif args.only_leg == "english":
+        res = {"leg": "english_like_200MiB", **english_leg(args)}
     else:
         res = run_single(args)
         if not args.no_legs:
