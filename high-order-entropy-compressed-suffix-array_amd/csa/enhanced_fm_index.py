@@ -74,12 +74,16 @@ class OccView(Mapping):
 
 class EnhancedFMIndex:
     def __init__(self, text):
-        self.text = text + "$"
-        self._codec = TextCodec(self.text)
-        self._dev = DeviceIndex.from_bytes(self._codec.encode_text(self.text))
+        # T' = text + "$" (:9) is uploaded as two pieces — the str's own code-point buffer and the
+        # sentinel — so no concatenated copy of a GiB-sized text is built on the host; .text
+        # materialises it on first access
+        self._raw = text
+        self._text = None
+        self._codec = TextCodec(text, "$")
+        self._dev = DeviceIndex.from_parts(self._codec.parts(text, "$"))
         self._dev.build_all()
         self._dev.release_workspace()
-        self._n = len(self.text)
+        self._n = len(text) + 1
         C = self._dev.C()
         self.count = {self._codec.decode(bytes([b])): int(C[b]) for b in self._dev.alphabet()}
         self._sa = None
@@ -87,6 +91,12 @@ class EnhancedFMIndex:
         self._occ = None
 
     # ---------------------------------------------------------- attributes
+    @property
+    def text(self) -> str:
+        if self._text is None:
+            self._text = self._raw + "$"
+        return self._text
+
     @property
     def suffix_array(self) -> list:
         if self._sa is None:

@@ -19,7 +19,7 @@ def calculate_high_order_entropy(text, k):
     if not isinstance(text, str):
         text = "".join(text)
     codec = TextCodec(text)
-    dev = DeviceIndex.from_bytes(codec.encode_text(text))
+    dev = DeviceIndex.from_parts(codec.parts(text))
     try:
         return dev.entropy(int(k))
     finally:

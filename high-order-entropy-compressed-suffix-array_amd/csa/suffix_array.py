@@ -22,7 +22,7 @@ def build_suffix_array(text) -> list:
     if not text:
         return []
     codec = TextCodec(text)
-    dev = DeviceIndex.from_bytes(codec.encode_text(text))
+    dev = DeviceIndex.from_parts(codec.parts(text))
     try:
         dev.build_sa()
         return [int(x) for x in dev.sa()]

@@ -88,8 +88,8 @@ class WaveletTree:
         if not s:
             return
         self._codec = TextCodec(s)
-        enc = np.frombuffer(self._codec.encode_text(s), dtype=np.uint8)
-        self._dev = DeviceIndex.from_bytes(enc)
+        enc = self._codec.parts(s)[0]          # (a read-only view of s when no remap is needed)
+        self._dev = DeviceIndex.from_parts([enc])
         self._dev.use_text_as_bwt()
         self._dev.build_wt()
         C = self._dev.C()

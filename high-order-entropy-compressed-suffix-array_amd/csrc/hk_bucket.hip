@@ -3446,9 +3446,7 @@ int cursor_partition(Index& ix, uint64_t n, int D, int bitlo, uint64_t kbias, co
   // copies; the host waits for them alone)
   if (!ix.aux_stream) HK_HIP(hipStreamCreateWithFlags(&ix.aux_stream, hipStreamNonBlocking));
   auto counts_then_passA = [&]() {
-    hipEvent_t ev_pre, ev_cnt;
-    HK_HIP(hipEventCreateWithFlags(&ev_pre, hipEventDisableTiming));
-    HK_HIP(hipEventCreateWithFlags(&ev_cnt, hipEventDisableTiming));
+    ScopedEvent ev_pre, ev_cnt;
     HK_HIP(hipEventRecord(ev_pre, s));
     HK_HIP(hipStreamWaitEvent(ix.aux_stream, ev_pre, 0));
     HK_HIP(hipMemcpyAsync(h_hist, d_hist, (uint64_t)nb * 8, hipMemcpyDeviceToHost, ix.aux_stream));
@@ -3456,8 +3454,6 @@ int cursor_partition(Index& ix, uint64_t n, int D, int bitlo, uint64_t kbias, co
     HK_HIP(hipEventRecord(ev_cnt, ix.aux_stream));
     passA();
     const hipError_t we = hipEventSynchronize(ev_cnt);   // the counts, not pass A
-    (void)hipEventDestroy(ev_pre);
-    (void)hipEventDestroy(ev_cnt);
     HK_HIP(we);
   };
   prepass(false);
@@ -3927,9 +3923,7 @@ static int cursor_partition_slice(Index& ix, const SlicePlan& P, const TextKeySr
   };
   if (!ix.aux_stream) HK_HIP(hipStreamCreateWithFlags(&ix.aux_stream, hipStreamNonBlocking));
   auto counts_then_passA = [&]() {
-    hipEvent_t ev_pre, ev_cnt;
-    HK_HIP(hipEventCreateWithFlags(&ev_pre, hipEventDisableTiming));
-    HK_HIP(hipEventCreateWithFlags(&ev_cnt, hipEventDisableTiming));
+    ScopedEvent ev_pre, ev_cnt;
     HK_HIP(hipEventRecord(ev_pre, s));
     HK_HIP(hipStreamWaitEvent(ix.aux_stream, ev_pre, 0));
     HK_HIP(hipMemcpyAsync(h_hist, d_hist, (uint64_t)nb2 * 8, hipMemcpyDeviceToHost, ix.aux_stream));
@@ -3937,8 +3931,6 @@ static int cursor_partition_slice(Index& ix, const SlicePlan& P, const TextKeySr
     HK_HIP(hipEventRecord(ev_cnt, ix.aux_stream));
     passA();
     const hipError_t we = hipEventSynchronize(ev_cnt);
-    (void)hipEventDestroy(ev_pre);
-    (void)hipEventDestroy(ev_cnt);
     HK_HIP(we);
   };
   prepass(false);
@@ -4102,9 +4094,7 @@ bool slices_fuse(Index& ix, const std::vector<uint32_t>& B, const std::vector<ui
   // counts back behind an event while pass A runs
   uint64_t* h = ix.fused_host.as<uint64_t>();
   std::vector<uint64_t*> h_hist(ns), h_tot(ns);
-  hipEvent_t ev_pre, ev_cnt;
-  HK_HIP(hipEventCreateWithFlags(&ev_pre, hipEventDisableTiming));
-  HK_HIP(hipEventCreateWithFlags(&ev_cnt, hipEventDisableTiming));
+  ScopedEvent ev_pre, ev_cnt;
   if (!ix.aux_stream) HK_HIP(hipStreamCreateWithFlags(&ix.aux_stream, hipStreamNonBlocking));
   HK_HIP(hipEventRecord(ev_pre, s));
   HK_HIP(hipStreamWaitEvent(ix.aux_stream, ev_pre, 0));
@@ -4159,8 +4149,6 @@ bool slices_fuse(Index& ix, const std::vector<uint32_t>& B, const std::vector<ui
     HK_HIP(hipGetLastError());
   }
   const hipError_t we = hipEventSynchronize(ev_cnt);
-  (void)hipEventDestroy(ev_pre);
-  (void)hipEventDestroy(ev_cnt);
   HK_HIP(we);
   HK_HIP(hipStreamSynchronize(s));   // (h_lp2 lives in cp_host, which the slices reuse)
   if (*h_ovf) return false;   // a u8 counter wrapped: the slices run one by one (exact recounts)

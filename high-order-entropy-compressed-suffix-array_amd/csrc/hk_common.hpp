@@ -163,6 +163,18 @@ struct DevBuf {
 };
 
 // grow-only pinned host buffer (asynchronous copies in both directions)
+// an event owned by a scope: no leak when a HIP call between its creation and its last use throws
+struct ScopedEvent {
+  hipEvent_t e = nullptr;
+  ScopedEvent() { HK_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming)); }
+  ~ScopedEvent() {
+    if (e) (void)hipEventDestroy(e);
+  }
+  ScopedEvent(const ScopedEvent&) = delete;
+  ScopedEvent& operator=(const ScopedEvent&) = delete;
+  operator hipEvent_t() const { return e; }
+};
+
 struct HostBuf {
   void* p = nullptr;
   size_t bytes = 0;

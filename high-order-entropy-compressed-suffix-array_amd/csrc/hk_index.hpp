@@ -230,6 +230,10 @@ void build_sa_sharded(Index& ix, const uint8_t id[128], int nranks, int rank);
 // kFlagSlices); slices_for(): the slice count build_sa uses
 void build_sa_slices(Index& ix, int k);
 int slices_for(const Index& ix);
+// the keyed slice bounds of an exact coarse histogram (below[0..k]); throws when a slice would hold
+// 2^32 - 1 or more suffixes (32-bit slots inside a slice)
+std::vector<uint64_t> slice_bounds(const uint64_t* hist, int nbins, int k);
+void check_slice_sizes(const uint64_t* below, int k);
 void shard_replicate(Index& ix);                                          // RCCL: full SA + BWT on every rank
 void shard_adopt(Index& ix, const uint64_t* h_sa, const uint8_t* h_bwt);  // host-assembled full SA + BWT
 // host-driven rank exchange of the sharded prefix doubling (hkcsa_shard_status ... hkcsa_shard_round)

@@ -711,6 +711,10 @@ void dbl_round_t(Index& ix, uint64_t K) {
   const int gbits = st.groups > 1 ? bits_of_u64(st.groups - 1) : 0;
   const int ib = bits_of_u64(ix.n);   // ISA + 1 <= n
   if (gbits + ib > 64) throw ApiError{-6, "prefix doubling: too many tied groups for one 64-bit key"};
+  // the output lists (a parked slice of build_sa_slices released them while it waited)
+  ix.act[cur ^ 1][0].ensure(A * sizeof(V) + 16);
+  ix.act[cur ^ 1][1].ensure(A * 4 + 16);
+  ix.act[cur ^ 1][2].ensure(A * 4 + 16);
   uint64_t* kp[2] = {ix.keys[0].as<uint64_t>(), ix.keys[1].as<uint64_t>()};
   V* vp[2] = {ix.vals[0].as<V>(), ix.vals[1].as<V>()};
   {
@@ -746,7 +750,7 @@ void dbl_round_t(Index& ix, uint64_t K) {
     }
   }
   const uint64_t nt = ceil_div(A, GR_TILE);
-  ix.tile_a.ensure((nt + 1) * 8);
+  ix.tile_a.ensure((nt + 2) * 8);   // (nt + 2): sort_big_groups in the redo below must not regrow it under tl
   ix.tile_b.ensure((nt + 1) * 4);
   ix.tile_c.ensure((nt + 1) * 8);
   ix.tile_d.ensure((nt + 2) * 8);

@@ -886,6 +886,30 @@ void shard_build_keyed(Index& ix, const uint64_t* ghist, const uint64_t* gbelow,
 
 bool shard_keyed(Index& ix) { return shard_keyed_lb(ix) > 0; }
 
+// Slot indices inside a slice are 32-bit (tie lists, refinement / doubling rows, big-bucket rows), so a
+// slice must hold fewer than 2^32 - 1 suffixes.  Slices end on coarse-bucket boundaries: one coarse
+// bucket larger than that (a run of one symbol, or a few-symbol period, in a text of n > 2^32) cannot be
+// cut, and the build refuses it instead of wrapping the slots.
+void check_slice_sizes(const uint64_t* below, int k) {
+  for (int r = 0; r < k; ++r)
+    if (below[r + 1] - below[r] >= 0xFFFFFFFFull)
+      throw ApiError{-6, "a slice would hold 2^32 - 1 or more suffixes: one coarse bucket (first 16 key bits) "
+                         "of the text is too large to split across slices"};
+}
+
+std::vector<uint64_t> slice_bounds(const uint64_t* hist, int nbins, int k) {
+  const std::vector<uint32_t> B = splitters(hist, k, nbins, true);
+  std::vector<uint64_t> below(k + 1, 0);
+  uint64_t acc = 0;
+  uint32_t c = 0;
+  for (int r = 0; r <= k; ++r) {
+    while (c < B[r]) acc += hist[c++];
+    below[r] = acc;
+  }
+  check_slice_sizes(below.data(), k);
+  return below;
+}
+
 void shard_histogram(Index& ix, int nranks, int rank, uint64_t* d_hist) {
   if (shard_keyed(ix)) {   // exact coarse histogram of the 16-aligned block
     const auto b = block_of(ix.n, nranks, rank);
@@ -953,6 +977,7 @@ void shard_counts(Index& ix, const uint64_t* h_global_hist, int nranks, int rank
 }
 
 void shard_build(Index& ix, const uint64_t* h_global_hist, const uint64_t* h_global_below, int nranks, int rank) {
+  if (h_global_below[rank + 1] >= h_global_below[rank]) check_slice_sizes(h_global_below + rank, 1);
   const bool keyed = shard_keyed(ix);
   if (ix.n > 0xFFFFFFFEull || (ix.flags & kFlagPos64)) {
     if (keyed) shard_build_keyed<uint64_t>(ix, h_global_hist, h_global_below, nranks, rank);
@@ -1047,12 +1072,7 @@ void build_sa_slices(Index& ix, int k) {
     HK_HIP(hipStreamSynchronize(s));
     if (keyed) {
       B = splitters(gh.data(), k, SH_KBUCKETS, true);
-      uint64_t acc = 0;
-      uint32_t c = 0;
-      for (int r = 0; r <= k; ++r) {
-        while (c < B[r]) acc += gh[c++];
-        below[r] = acc;
-      }
+      below = slice_bounds(gh.data(), SH_KBUCKETS, k);
     } else {
       std::vector<uint64_t> part(k + 1);
       for (int r = 0; r < k; ++r) {   // each block's counts below every splitter, summed
@@ -1064,6 +1084,7 @@ void build_sa_slices(Index& ix, int k) {
     }
   }
   if (below[0] != 0 || below[k] != n) throw ApiError{-7, "slices: the partition does not cover the text"};
+  check_slice_sizes(below.data(), k);
   // ---- the slices, one after another
   std::vector<uint64_t> info(9, 0), ties;
   std::vector<PendingSlice> pend;
@@ -1105,6 +1126,9 @@ void build_sa_slices(Index& ix, int k) {
       p.lo = lo;
       p.hi = hi;
       swap_pending(ix, p);
+      // while parked only the active lists and head slots matter: the round's output lists are
+      // re-allocated at the list's size when its doubling starts (dbl_round_t)
+      for (DevBuf& b : p.act[p.dbl.cur ^ 1]) b.release();
     }
   }
   ix.fused.reset();   // (the last group's records)

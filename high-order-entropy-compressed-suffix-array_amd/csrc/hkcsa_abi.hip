@@ -2,22 +2,28 @@
 // Each entry point catches every C++ exception and maps it to a negative error code plus a
 // thread-local message; nothing ever throws across the ABI.
 
+#include <algorithm>
 #include <cstring>
+#include <initializer_list>
+#include <memory>
+#include <vector>
 #include <new>
 #include <string>
 
 #include "../../include/hkcsa.h"
 #include "hk_index.hpp"
 
-struct hkcsa_index {
-  hk::Index ix;
-};
-
 struct hkcsa_queries {
   uint64_t P = 0;
   hk::DevBuf pats, offs, lr, cnt, occ_offs, pos;
   uint64_t total = 0;
   bool have_lr = false, have_pos = false;
+};
+
+struct hkcsa_index {
+  hk::Index ix;
+  hkcsa_queries qws;                   // device workspace of the host-boundary batch calls, kept across calls
+  hk::HostBuf stage_in, stage_out;     // their pinned staging (grown, never shrunk)
 };
 
 namespace hk {
@@ -97,6 +103,36 @@ int hkcsa_create(const uint8_t* text, uint64_t n, const hkcsa_opts* o, hkcsa_ind
     try {
       init_index(h->ix, o, n);
       HK_HIP(hipMemcpyAsync(h->ix.text.p, text, n, hipMemcpyHostToDevice, h->ix.stream));
+      HK_HIP(hipStreamSynchronize(h->ix.stream));
+    } catch (...) {
+      delete h;
+      throw;
+    }
+    *out = h;
+  });
+}
+
+int hkcsa_create_parts(const uint8_t* const* parts, const uint64_t* lens, int nparts, const hkcsa_opts* o,
+                       hkcsa_index** out) {
+  return guarded([&] {
+    need(out != nullptr, HKCSA_E_INVALID, "null output handle");
+    need(nparts >= 1 && parts != nullptr && lens != nullptr, HKCSA_E_INVALID, "no parts");
+    uint64_t n = 0;
+    for (int i = 0; i < nparts; ++i) {
+      need(lens[i] == 0 || parts[i] != nullptr, HKCSA_E_INVALID, "null part");
+      n += lens[i];
+    }
+    need(n > 0, HKCSA_E_INVALID, "text must hold at least the sentinel");
+    auto* h = new hkcsa_index();
+    try {
+      init_index(h->ix, o, n);
+      uint64_t at = 0;
+      for (int i = 0; i < nparts; ++i) {
+        if (lens[i])
+          HK_HIP(hipMemcpyAsync(h->ix.text.as<uint8_t>() + at, parts[i], lens[i], hipMemcpyHostToDevice,
+                                h->ix.stream));
+        at += lens[i];
+      }
       HK_HIP(hipStreamSynchronize(h->ix.stream));
     } catch (...) {
       delete h;
@@ -508,14 +544,102 @@ int hkcsa_queries_download(hkcsa_index* h, hkcsa_queries* q, int64_t* lr_out, ui
 
 void hkcsa_queries_free(hkcsa_queries* q) { delete q; }
 
+}  // extern "C"
+
+namespace {
+// Host <-> device copies of the batch calls through the handle's pinned staging, in chunks: the host
+// copy of one chunk overlaps the DMA of the previous one (pageable copies would be staged by the
+// runtime chunk by chunk, synchronously).
+constexpr uint64_t kStageChunk = 4ull << 20;
+struct Seg {
+  void* dst;
+  const void* src;
+  uint64_t bytes;
+};
+
+void staged_h2d(hkcsa_index* h, std::initializer_list<Seg> segs) {
+  uint64_t tot = 0;
+  for (const Seg& g : segs) tot += g.bytes;
+  if (!tot) return;
+  h->stage_in.ensure(tot);
+  uint8_t* st = h->stage_in.as<uint8_t>();
+  hipStream_t s = h->ix.stream;
+  uint64_t off = 0;
+  for (const Seg& g : segs)
+    for (uint64_t a = 0; a < g.bytes; a += kStageChunk) {
+      const uint64_t c = std::min(kStageChunk, g.bytes - a);
+      std::memcpy(st + off, static_cast<const uint8_t*>(g.src) + a, c);
+      HK_HIP(hipMemcpyAsync(static_cast<uint8_t*>(g.dst) + a, st + off, c, hipMemcpyHostToDevice, s));
+      off += c;
+    }
+}
+
+// device -> host; returns after every byte has landed in the caller's buffers
+void staged_d2h(hkcsa_index* h, std::initializer_list<Seg> segs) {
+  uint64_t tot = 0;
+  for (const Seg& g : segs) tot += g.bytes;
+  hipStream_t s = h->ix.stream;
+  if (!tot) {
+    HK_HIP(hipStreamSynchronize(s));
+    return;
+  }
+  h->stage_out.ensure(tot);
+  uint8_t* st = h->stage_out.as<uint8_t>();
+  struct Piece {
+    uint8_t* dst;
+    uint64_t off, c;
+  };
+  std::vector<Piece> pieces;
+  std::vector<std::unique_ptr<hk::ScopedEvent>> evs;
+  uint64_t off = 0;
+  for (const Seg& g : segs)
+    for (uint64_t a = 0; a < g.bytes; a += kStageChunk) {
+      const uint64_t c = std::min(kStageChunk, g.bytes - a);
+      HK_HIP(hipMemcpyAsync(st + off, static_cast<const uint8_t*>(g.src) + a, c, hipMemcpyDeviceToHost, s));
+      evs.emplace_back(new hk::ScopedEvent());
+      HK_HIP(hipEventRecord(*evs.back(), s));
+      pieces.push_back({static_cast<uint8_t*>(g.dst) + a, off, c});
+      off += c;
+    }
+  for (size_t k = 0; k < pieces.size(); ++k) {
+    HK_HIP(hipEventSynchronize(*evs[k]));
+    std::memcpy(pieces[k].dst, st + pieces[k].off, pieces[k].c);
+  }
+}
+
+// the batch calls' query set: the handle's workspace, patterns staged in
+hkcsa_queries& batch_upload(hkcsa_index* h, const uint8_t* pats, const uint64_t* offs, uint64_t P) {
+  need(offs != nullptr, HKCSA_E_INVALID, "null offsets");
+  need(offs[0] == 0, HKCSA_E_INVALID, "offs[0] must be 0");
+  for (uint64_t p = 0; p < P; ++p) need(offs[p + 1] >= offs[p], HKCSA_E_INVALID, "offsets not monotone");
+  const uint64_t bytes = offs[P];
+  need(bytes == 0 || pats != nullptr, HKCSA_E_INVALID, "null patterns");
+  hkcsa_queries& q = h->qws;
+  q.P = P;
+  q.total = 0;
+  q.have_lr = q.have_pos = false;
+  q.pats.ensure(bytes + 16);
+  q.offs.ensure((P + 1) * 8);
+  q.lr.ensure(P * 16 + 16);
+  q.cnt.ensure(P * 8 + 16);
+  q.occ_offs.ensure((P + 1) * 8 + 16);
+  staged_h2d(h, {{q.pats.p, pats, bytes}, {q.offs.p, offs, (P + 1) * 8}});
+  return q;
+}
+}  // namespace
+
+extern "C" {
+
 int hkcsa_count_batch(hkcsa_index* h, const uint8_t* pats, const uint64_t* offs, uint64_t P, int64_t* lr_out) {
-  hkcsa_queries* q = nullptr;
-  int rc = hkcsa_queries_upload(h, pats, offs, P, &q);
-  if (rc) return rc;
-  rc = hkcsa_queries_count(h, q);
-  if (!rc) rc = hkcsa_queries_download(h, q, lr_out, nullptr, nullptr, 0);
-  hkcsa_queries_free(q);
-  return rc;
+  return guarded([&] {
+    activate(h);
+    need(lr_out != nullptr || P == 0, HKCSA_E_INVALID, "null output");
+    need(!h->ix.sharded, HKCSA_E_STATE, "sharded index holds only a slice");
+    hkcsa_queries& q = batch_upload(h, pats, offs, P);
+    hk::query_count(h->ix, q.pats.as<uint8_t>(), q.offs.as<uint64_t>(), q.P, q.lr.as<int64_t>(),
+                    q.cnt.as<uint64_t>());
+    staged_d2h(h, {{lr_out, q.lr.p, P * 16}});
+  });
 }
 
 // Sizes first (count + scan, no gather); the SA gather runs only when pos_out can hold every
@@ -523,29 +647,28 @@ int hkcsa_count_batch(hkcsa_index* h, const uint8_t* pats, const uint64_t* offs,
 // CSR offsets with HKCSA_E_RANGE (nothing gathered) and calls again.
 int hkcsa_locate_batch(hkcsa_index* h, const uint8_t* pats, const uint64_t* offs, uint64_t P,
                        uint64_t* occ_offs, uint64_t* pos_out, uint64_t cap) {
-  hkcsa_queries* q = nullptr;
-  int rc = hkcsa_queries_upload(h, pats, offs, P, &q);
-  if (rc) return rc;
-  rc = guarded([&] {
+  return guarded([&] {
+    activate(h);
     need(occ_offs != nullptr, HKCSA_E_INVALID, "null occ_offs");
     need(!h->ix.sharded, HKCSA_E_STATE, "sharded index holds only a slice");
+    hkcsa_queries& q = batch_upload(h, pats, offs, P);
     hipStream_t s = h->ix.stream;
-    hk::query_count(h->ix, q->pats.as<uint8_t>(), q->offs.as<uint64_t>(), q->P, q->lr.as<int64_t>(),
-                    q->cnt.as<uint64_t>());
-    hk::scan_exclusive_u64(h->ix.sw, q->cnt.as<uint64_t>(), q->occ_offs.as<uint64_t>(), q->P, true, s);
-    HK_HIP(hipMemcpyAsync(occ_offs, q->occ_offs.p, (q->P + 1) * 8, hipMemcpyDeviceToHost, s));
+    hk::query_count(h->ix, q.pats.as<uint8_t>(), q.offs.as<uint64_t>(), q.P, q.lr.as<int64_t>(),
+                    q.cnt.as<uint64_t>());
+    hk::scan_exclusive_u64(h->ix.sw, q.cnt.as<uint64_t>(), q.occ_offs.as<uint64_t>(), q.P, true, s);
+    uint64_t* const rb = h->ix.rb();   // pinned: the total first, then gather and copies back to back
+    HK_HIP(hipMemcpyAsync(&rb[3], q.occ_offs.as<uint64_t>() + P, 8, hipMemcpyDeviceToHost, s));
     HK_HIP(hipStreamSynchronize(s));
-    const uint64_t tot = occ_offs[q->P];
-    if (!pos_out) return;
-    need(cap >= tot, HKCSA_E_RANGE, "position buffer too small (occ_offs holds the sizes)");
-    if (!tot) return;
-    q->pos.ensure(tot * 8 + 16);
-    hk::query_locate_gather(h->ix, q->lr.as<int64_t>(), q->occ_offs.as<uint64_t>(), q->P, q->pos.as<uint64_t>());
-    HK_HIP(hipMemcpyAsync(pos_out, q->pos.p, tot * 8, hipMemcpyDeviceToHost, s));
-    HK_HIP(hipStreamSynchronize(s));
+    const uint64_t tot = rb[3];
+    if (!pos_out || cap < tot || !tot) {
+      staged_d2h(h, {{occ_offs, q.occ_offs.p, (P + 1) * 8}});
+      need(!pos_out || cap >= tot, HKCSA_E_RANGE, "position buffer too small (occ_offs holds the sizes)");
+      return;
+    }
+    q.pos.ensure(tot * 8 + 16);
+    hk::query_locate_gather(h->ix, q.lr.as<int64_t>(), q.occ_offs.as<uint64_t>(), q.P, q.pos.as<uint64_t>());
+    staged_d2h(h, {{occ_offs, q.occ_offs.p, (P + 1) * 8}, {pos_out, q.pos.p, tot * 8}});
   });
-  hkcsa_queries_free(q);
-  return rc;
 }
 
 // ------------------------------------------------------------ sharded SA
@@ -575,6 +698,16 @@ int hkcsa_shard_scheme(hkcsa_index* h, int* scheme) {
     need(scheme != nullptr, HKCSA_E_INVALID, "null output");
     need(h->ix.have_text, HKCSA_E_STATE, "text released by hkcsa_compact");
     *scheme = hk::shard_keyed(h->ix) ? 1 : 0;   // (a query: the alphabet is computed once, if missing)
+  });
+}
+
+int hkcsa_slice_bounds(const uint64_t* hist, uint32_t nbins, int nslices, uint64_t* below_out) {
+  return guarded([&] {
+    need(hist != nullptr && below_out != nullptr, HKCSA_E_INVALID, "null buffer");
+    need(nbins >= 1 && nbins <= (1u << 24), HKCSA_E_INVALID, "1 to 2^24 bins");
+    need(nslices >= 1 && nslices <= 64, HKCSA_E_INVALID, "1 to 64 slices");
+    const std::vector<uint64_t> b = hk::slice_bounds(hist, (int)nbins, nslices);
+    std::copy(b.begin(), b.end(), below_out);
   });
 }
 

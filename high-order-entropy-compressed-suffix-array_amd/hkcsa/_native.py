@@ -40,6 +40,7 @@ _SIGS = [
     ("hkcsa_device_count", C.c_int, [C.POINTER(C.c_int)]),
     ("hkcsa_last_error", C.c_char_p, []),
     ("hkcsa_create", C.c_int, [vp, C.c_uint64, C.POINTER(Opts), C.POINTER(vp)]),
+    ("hkcsa_create_parts", C.c_int, [vp, vp, C.c_int, C.POINTER(Opts), C.POINTER(vp)]),
     ("hkcsa_create_synthetic", C.c_int, [C.c_uint64, vp, C.c_int, C.c_uint64, C.c_uint8, C.POINTER(Opts), C.POINTER(vp)]),
     ("hkcsa_build_sa", C.c_int, [vp]),
     ("hkcsa_build_bwt", C.c_int, [vp]),
@@ -79,6 +80,7 @@ _SIGS = [
     ("hkcsa_get_shard_sa", C.c_int, [vp, C.c_uint64, C.c_uint64, vp]),
     ("hkcsa_get_shard_bwt", C.c_int, [vp, C.c_uint64, C.c_uint64, vp]),
     ("hkcsa_shard_buckets", C.c_int, []),
+    ("hkcsa_slice_bounds", C.c_int, [vp, C.c_uint32, C.c_int, vp]),
     ("hkcsa_shard_histogram", C.c_int, [vp, C.c_int, C.c_int, vp]),
     ("hkcsa_shard_sample", C.c_int, []),
     ("hkcsa_shard_scheme", C.c_int, [vp, C.POINTER(C.c_int)]),

@@ -104,6 +104,22 @@ class DeviceIndex:
         return cls(h, len(arr))
 
     @classmethod
+    def from_parts(cls, parts: Sequence[np.ndarray], device: int = -1, flags: int = 0) -> "DeviceIndex":
+        """T' = the concatenation of `parts` (uint8 arrays, e.g. TextCodec.parts(text, "$")), uploaded
+        piece by piece (hkcsa_create_parts): no host-side concatenation."""
+        lib = N.load()
+        arrs = [np.ascontiguousarray(p).view(np.uint8) for p in parts]
+        n = sum(len(a) for a in arrs)
+        if n == 0:
+            raise ValueError("DeviceIndex needs a non-empty text (append the sentinel first)")
+        ptrs = (C.c_void_p * len(arrs))(*[a.ctypes.data if len(a) else None for a in arrs])
+        lens = (C.c_uint64 * len(arrs))(*[len(a) for a in arrs])
+        o = N.Opts(device=device, flags=flags)
+        h = C.c_void_p()
+        N.check(lib.hkcsa_create_parts(ptrs, lens, len(arrs), C.byref(o), C.byref(h)))
+        return cls(h, n)
+
+    @classmethod
     def synthetic(cls, n: int, alphabet: bytes, seed: int, terminator: int = ord("$"),
                   device: int = -1, flags: int = 0) -> "DeviceIndex":
         lib = N.load()

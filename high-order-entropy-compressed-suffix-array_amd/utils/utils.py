@@ -29,7 +29,7 @@ def build_count(text) -> dict:
     if not text:
         return {}
     codec = TextCodec(text)
-    dev = DeviceIndex.from_bytes(codec.encode_text(text))
+    dev = DeviceIndex.from_parts(codec.parts(text))
     try:
         C = dev.C()
         return {codec.decode(bytes([b])): int(C[b]) for b in dev.alphabet()}
@@ -43,7 +43,7 @@ def build_occ(bwt):
     if not bwt:
         return {}
     codec = TextCodec(bwt)
-    dev = DeviceIndex.from_bytes(codec.encode_text(bwt))
+    dev = DeviceIndex.from_parts(codec.parts(bwt))
     dev.use_text_as_bwt()
     dev.build_wt()
     return OccView(dev, codec, len(bwt))

@@ -72,6 +72,11 @@ const char* hkcsa_last_error(void);
  * Replaces the text handling of EnhancedFMIndex.__init__
  * (csa/enhanced_fm_index.py:8-9). */
 int hkcsa_create(const uint8_t* text, uint64_t n, const hkcsa_opts* o, hkcsa_index** out);
+/* The same from `nparts` host pieces uploaded back to back (T' = parts[0] + parts[1] + ...):
+ * EnhancedFMIndex's `text + "$"` (csa/enhanced_fm_index.py:9) without building the
+ * concatenation on the host — the caller passes its text buffer and the sentinel. */
+int hkcsa_create_parts(const uint8_t* const* parts, const uint64_t* lens, int nparts, const hkcsa_opts* o,
+                       hkcsa_index** out);
 /* Generate a synthetic text on the device: n-1 iid bytes drawn from the
  * `sigma` symbols `alphabet[0..sigma)` by a counter-based hash of (seed, i),
  * followed by the byte `terminator`.  Reproducible on the host with
@@ -176,8 +181,11 @@ int hkcsa_rank(hkcsa_index* ix, const uint8_t* c, const uint64_t* i, uint64_t co
 int hkcsa_count_batch(hkcsa_index* ix, const uint8_t* pats, const uint64_t* offs, uint64_t P,
                       int64_t* lr_out);
 /* locate: EnhancedFMIndex.find (csa/enhanced_fm_index.py:15-19), positions in
- * SA order.  Two-phase: with pos_out == NULL only occ_offs (P+1 entries,
- * CSR offsets) is filled; then call again with cap >= occ_offs[P]. */
+ * SA order.  occ_offs (P+1 entries, CSR offsets) is required and always filled
+ * first.  pos_out == NULL: sizes only.  Otherwise, when cap >= occ_offs[P], every
+ * position is gathered into pos_out in one call; when cap is smaller the call
+ * returns HKCSA_E_RANGE with occ_offs filled and nothing written to pos_out, so
+ * the caller can size its buffer from occ_offs[P] and call again. */
 int hkcsa_locate_batch(hkcsa_index* ix, const uint8_t* pats, const uint64_t* offs, uint64_t P,
                        uint64_t* occ_offs, uint64_t* pos_out, uint64_t cap);
 /* Device-resident query sets (bench: inputs resident in HBM before timing). */
@@ -195,10 +203,13 @@ int hkcsa_extract(hkcsa_index* ix, uint64_t i, uint64_t j, uint8_t* out);   /* T
 /* RCCL unique id (128 bytes) to be broadcast by the caller from rank 0. */
 int hkcsa_comm_unique_id(uint8_t id[128]);
 /* Each rank holds the same T' (created on its own device).  Ranks split the
- * final SA into contiguous rank ranges by a shared sampled key histogram (RCCL
- * all-reduce), fix the exact slice sizes with a second all-reduce of N+1 counts,
- * and sort their slice independently; an RCCL all-gather of per-rank status
- * records checks that the slices tile [0, n).  Slices still tied after the chunk
+ * final SA into contiguous rank ranges from one RCCL all-reduce of a partition
+ * histogram: for keyed alphabets (hkcsa_shard_scheme 1: DNA, binary, 16 or 256
+ * symbols) the EXACT coarse histogram of every suffix's first 16 key bits, which
+ * fixes the slice bounds by itself; for other alphabets a sampled key histogram
+ * plus a second all-reduce of the N+1 exact counts below the splitters.  Each rank
+ * sorts its slice independently; an RCCL all-gather of per-rank status records
+ * checks that the slices tile [0, n).  Slices still tied after the chunk
  * refinement finish by prefix doubling with an ISA replica per rank, built by an
  * RCCL all-gather of the SA slices and refreshed per round by an all-gather of the
  * re-ranked suffixes' (position, ISA) pairs.  A failure on any rank makes every
@@ -242,6 +253,13 @@ int hkcsa_get_shard_bwt(hkcsa_index* ix, uint64_t a, uint64_t b, uint8_t* out);
  *     splitter j (splitters derived from G; below_out[0] = 0);
  *   hkcsa_shard_build: builds SA[lo:hi) of this rank from G and the element-wise
  *     sum of every rank's below_out (lo, hi = its entries r and r+1). */
+/* Host-side slice planner (no device work): the SA bounds below_out[0..nslices] that
+ * hkcsa_build_sa's slice build (and the keyed sharded build) derive from an exact coarse
+ * histogram of `nbins` buckets (equal-width or balanced splitters, as above).  Slots inside a
+ * slice are 32-bit, so a slice of 2^32 - 1 or more suffixes — one coarse bucket too large to
+ * split, e.g. a long run in a text of n > 2^32 — is refused with HKCSA_E_TOOBIG (the builds
+ * refuse the same text the same way instead of wrapping). */
+int hkcsa_slice_bounds(const uint64_t* hist, uint32_t nbins, int nslices, uint64_t* below_out);
 int hkcsa_shard_buckets(void);
 int hkcsa_shard_sample(void);
 int hkcsa_shard_scheme(hkcsa_index* ix, int* scheme);   /* 1 keyed coarse, 0 partition key */

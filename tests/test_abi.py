@@ -57,3 +57,39 @@ def test_flag_constants_match_header():
         if hasattr(index, "FLAG_" + name):
             assert getattr(index, "FLAG_" + name) == v, name
     assert int(re.search(r"#define HKCSA_E_RANGE \((-\d+)\)", src).group(1)) == _native.E_RANGE
+
+
+def test_slice_bounds_planner_refuses_oversized_slice():
+    """hkcsa_slice_bounds (host only, no device): the slice bounds hkcsa_build_sa's slice build takes from
+    an exact coarse histogram equal hkcsa/shard.py's restatement of the splitter rule; a histogram with one
+    dominant coarse bucket of >= 2^32 - 1 suffixes (a long run in a text of n > 2^32) is refused with
+    HKCSA_E_TOOBIG instead of wrapping the 32-bit slots inside a slice."""
+    import ctypes as C
+
+    import numpy as np
+
+    from hkcsa import shard
+    from hkcsa.index import _ptr
+    lib = hkcsa.load()
+    nb = 65536
+    rng = np.random.default_rng(3)
+    for k in (1, 2, 3, 4, 8):
+        h = rng.integers(0, 70000, size=nb).astype(np.uint64)
+        below = np.zeros(k + 1, dtype=np.uint64)
+        assert lib.hkcsa_slice_bounds(_ptr(h), nb, k, _ptr(below)) == 0
+        B = shard.split_buckets(h, k, aligned=True)
+        cum = np.concatenate(([0], np.cumsum(h)))
+        assert [int(cum[b]) for b in B] == [int(x) for x in below], k
+    # 4 GiB + 1 text whose run of one symbol fills one coarse bucket with 2^32 - 1 suffixes
+    h = np.zeros(nb, dtype=np.uint64)
+    h[0] = (1 << 32) - 1
+    h[1:3] = 1
+    below = np.zeros(5, dtype=np.uint64)
+    assert lib.hkcsa_slice_bounds(_ptr(h), nb, 4, _ptr(below)) == -6
+    assert b"2^32" in lib.hkcsa_last_error()
+    h[0] = (1 << 32) - 2                     # one fewer: a single slice of 2^32 - 2 is still addressable
+    assert lib.hkcsa_slice_bounds(_ptr(h), nb, 4, _ptr(below)) == 0
+    assert int(below[1]) == (1 << 32) - 2
+    assert lib.hkcsa_slice_bounds(None, nb, 4, _ptr(below)) == -1
+    assert lib.hkcsa_slice_bounds(_ptr(h), nb, 0, _ptr(below)) == -1
+    del C

@@ -189,3 +189,36 @@ def test_locate_batch_host_boundary():
     assert dev.lib.hkcsa_locate_batch(dev.h, _ptr(data), _ptr(offs), len(pats), _ptr(occ), None, 0) == 0
     assert [int(occ[i + 1] - occ[i]) for i in range(len(pats))] == [len(w) for w in want]
     dev.close()
+
+
+def test_unicode_64MiB_text_remap():
+    """A 64 MiB str with code points >= 256 (Cyrillic letters in English-like text, as a UTF-8 corpus read
+    by tests/dataset_benchmark.py:22 would give) through EnhancedFMIndex (csa/enhanced_fm_index.py:8-13):
+    the vectorised dense remap, the SA (O(n) checker) and BWT against the oracle on the remapped bytes,
+    and 2,000 20-symbol find_range / 200 find calls against the oracle FM index."""
+    from csa.enhanced_fm_index import EnhancedFMIndex
+    from oracle import oracle
+    from utils.textgen import english_like
+    base = english_like(64 << 20, seed=5)
+    lut = np.arange(256, dtype=np.uint32)
+    lut[ord("a"):ord("z") + 1] = 0x430 + np.arange(26, dtype=np.uint32)
+    cps = lut[base]
+    text = cps.astype("<u4").tobytes().decode("utf-32-le")
+    del base
+    idx = EnhancedFMIndex(text)
+    syms, enc = np.unique(np.concatenate([cps, np.array([ord("$")], np.uint32)]), return_inverse=True)
+    enc = enc.astype(np.uint8)
+    dev = idx.device_index
+    sa = dev.sa()
+    assert oracle.check_sa(enc, sa) == 0
+    fm = oracle.FM(enc, sa)
+    assert np.array_equal(dev.bwt(), fm.bwt)
+    assert idx.count == {chr(int(c)): int(fm.C[i]) for i, c in enumerate(syms)}
+    rng = np.random.default_rng(6)
+    starts = rng.integers(0, len(text) - 20, size=2000)
+    pats = [text[s:s + 20] for s in starts]
+    want = fm.find_range([enc[s:s + 20].tobytes() for s in starts])
+    assert np.array_equal(idx.find_range_many(pats), want)
+    for p, s in zip(pats[:200], starts[:200]):
+        assert idx.find(p) == fm.find([enc[s:s + 20].tobytes()])[0]
+    assert idx.find_range("абz一") == (-1, -1)   # a symbol the text cannot hold

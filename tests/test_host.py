@@ -29,6 +29,35 @@ def test_codec_remap_preserves_order():
     assert c.encode_pattern("x") is None
 
 
+def test_codec_parts_zero_copy_and_remap():
+    """TextCodec.parts: T' = text + sentinel as pieces without the concatenation; the identity case is
+    a view of the str's own storage (no copy), a >= 256 code-point remap is vectorised and equals the
+    dense sorted-order remap (csa/wavelet_tree.py:68 order) of text + '$'."""
+    from hkcsa import codec
+    rng = np.random.default_rng(4)
+    for t in ["banana", "caf\xe9 cr\xe8me", "", "x" * 1000]:
+        c = TextCodec(t, "$")
+        assert c.identity
+        p = c.parts(t, "$")
+        assert b"".join(x.tobytes() for x in p) == (t + "$").encode("latin-1")
+        if len(t) > 16 and codec._LAYOUT is not None:
+            assert not p[0].flags.owndata          # a view of the str itself
+    cps = np.array([0x3B1, 0x3B2, 0x3B3, 0x20AC, 0x1F600, 0x41, 0xE9], dtype=np.uint32)
+    for kind_t in [cps[:4], cps]:                  # UCS2 and UCS4 storage
+        t = "".join(chr(int(x)) for x in kind_t[rng.integers(0, len(kind_t), size=5000)])
+        c = TextCodec(t, "$")
+        assert not c.identity
+        enc = b"".join(x.tobytes() for x in c.parts(t, "$"))
+        syms = sorted(set(t + "$"))
+        assert enc == bytes(syms.index(ch) for ch in t + "$")
+        assert c.decode(enc) == t + "$"
+        assert c.encode_text(t) == enc[:-1]
+    # lone surrogates survive the round trip
+    t = "a\ud800b\udfffa$"
+    c = TextCodec(t)
+    assert c.decode(c.encode_text(t)) == t
+
+
 def test_codec_too_many_symbols():
     with pytest.raises(ValueError):
         TextCodec("".join(chr(0x400 + i) for i in range(300)))
