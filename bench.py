@@ -161,8 +161,8 @@ WT_KERNELS = ("wt_bits", "wt_partition")
 
 def pmc_traffic_gb(name: str, leg: str = "") -> float | None:
     """HBM GB per launch of timer `name`'s kernel, measured with rocprofv3 PMC counters on this config
-    (tools/gpu_pmc.sh + tools/pmc_summary.py -> profiles/pmc_kernels.json; FETCH_SIZE x2 gfx950
-    correction for the wide streaming reads)."""
+    (tools/kprof.py --pmc-json profiles/pmc_kernels.json, separate FETCH_SIZE / WRITE_SIZE passes; FETCH_SIZE
+    x2 gfx950 correction for the wide streaming reads)."""
     p = os.path.join(ROOT, "profiles", "pmc_kernels.json")
     try:
         with open(p) as f:
@@ -212,7 +212,7 @@ BUILD_STAGES = ["byte_hist", "sa_bucket_hist", "radix_part_text", "radix_part_ke
                 "sa_bucket_sort", "sa_big_gather", "radix_onesweep_text", "radix_table_text", "radix_tile_hist", "radix_hist", "radix_onesweep",
                 "radix_onesweep_small", "sa_pack_keys", "sa_refine_stats", "sa_refine_apply", "sa_refine_keys", "sa_refine_segsort",
                 "sa_isa_scatter", "sa_group_stats", "sa_group_apply", "sa_pair_keys", "sa_pair_segsort", "sa_big_groups",
-                "bwt_gather"]
+                "sa_round_plan", "sa_round_chunk", "sa_round_dbl", "bwt_gather"]
 SHARD_STAGES = ["shard_hist", "shard_below", "shard_slice_hist", "shard_slice_part", "shard_select_count",
                 "shard_pack_select", "rccl_allreduce_bytes",
                 "rccl_allreduce_hist",
@@ -436,6 +436,7 @@ def run_extra_legs(args, res: dict):
                             "build_info": info[:16]}
         log(f"[bench] sigma256 leg: {legs['sigma256']['ms_per_step']} ms/step, WT {t_wt * 1e3:.2f} ms")
     legs["english_like_200MiB"] = english_leg(args)
+    legs["protein_like_1GiB"] = protein_leg(args)
     n = 200 * (1 << 20) + 1
     dev, wall = build_leg(PRINTABLE, n, args.leg_steps, 1, args.seed + 20)
     dev.timing_reset()
@@ -493,8 +494,9 @@ def english_leg(args) -> dict:
     dev.timing(False)
     dev.close()
     refine = ("sa_refine_stats", "sa_refine_apply", "sa_refine_keys", "sa_refine_segsort", "radix_onesweep_small",
-              "radix_hist", "radix_onesweep")
-    dbl = ("sa_isa_scatter", "sa_pair_keys", "sa_pair_segsort", "sa_group_stats", "sa_group_apply")
+              "radix_hist", "radix_onesweep", "sa_round_chunk")
+    dbl = ("sa_isa_scatter", "sa_pair_keys", "sa_pair_segsort", "sa_group_stats", "sa_group_apply", "sa_round_dbl",
+           "sa_round_plan", "sa_big_groups")
     per = lambda names: round(sum(stages.get(k, {}).get("ms", 0.0) for k in names) / args.leg_steps, 3)
     log(f"[bench] english-like leg: {wall / args.leg_steps * 1e3:.2f} ms/step, refinement {per(refine)} ms, "
         f"doubling {per(dbl)} ms, count {qq['count_patterns_per_s']:.3g} patterns/s")
@@ -511,6 +513,43 @@ def english_leg(args) -> dict:
             "count_patterns_per_s": qq["count_patterns_per_s"], "locate_patterns_per_s": qq["locate_patterns_per_s"],
             "fm_count_kernel_ms": round(ms / max(1, l), 4), "patterns": qq["patterns"], "plen": 20,
             "stages_ms_total": stages, "build_info": info[:9]}
+
+
+def protein_leg(args) -> dict:
+    """The proteins corpus shape of the reference's dataset bench (tests/dataset_benchmark.py:13), absent
+    offline: 1 GiB of seeded protein-database-like text (utils/textgen.py protein_like: 25 amino-acid letters
+    at natural frequencies + newlines, 35 % family members with 8 % substitutions, 5 % duplicates), generated
+    on the host (untimed) and uploaded; SA + BWT steps (non-power-of-two alphabet: the stable onesweep
+    pair, LDS bucket sorts, refinement)."""
+    from hkcsa import DeviceIndex
+    from utils.textgen import protein_like_text
+    n = (1 << 30) + 1
+    t0 = time.perf_counter()
+    text = protein_like_text(n, seed=args.seed + 40)
+    gen_s = time.perf_counter() - t0
+    dev = DeviceIndex.from_bytes(text, device=0)
+    del text
+    dev.build_sa()
+    dev.synchronize()
+    dev.timing_reset()
+    dev.timing(True)
+    t0 = time.perf_counter()
+    for _ in range(args.leg_steps):
+        dev.build_sa()
+        dev.build_bwt()
+    dev.synchronize()
+    wall = time.perf_counter() - t0
+    stages = stage_breakdown(dev, BUILD_STAGES)
+    info = dev.build_info()
+    dev.timing(False)
+    dev.close()
+    log(f"[bench] protein-like leg: {wall / args.leg_steps * 1e3:.2f} ms/step")
+    return {"config": "proteins corpus shape (tests/dataset_benchmark.py:13; absent offline): 1 GiB protein-like "
+                      "text (utils/textgen.py protein_like, seed %d) + '$': SA + BWT steps" % (args.seed + 40),
+            "text_symbols": n, "generate_s": round(gen_s, 2), "steps": args.leg_steps,
+            "ms_per_step": round(wall / args.leg_steps * 1e3, 3),
+            "sa_bwt_MBps": round(args.leg_steps * n / 2**20 / wall, 2),
+            "tied_after_round": info[9:9 + 24], "stages_ms_total": stages, "build_info": info[:9]}
 
 
 def locate_host_leg(dev, data, offs, reps: int, full: dict) -> dict:
@@ -772,8 +811,9 @@ def parse_args(argv=None):
     ap.add_argument("--pos64", action="store_true", help="sharded build with 64-bit positions at any n")
     ap.add_argument("--global-sort", action="store_true",
                     help="single-GPU build by full-width LSD sort of the keys (no LDS bucket sorts)")
-    ap.add_argument("--only-leg", choices=("english",), default=None,
-                    help="run only this detail leg (profiling): english = the 200 MiB English-like leg")
+    ap.add_argument("--only-leg", choices=("english", "protein"), default=None,
+                    help="run only this detail leg (profiling): english = the 200 MiB English-like leg, "
+                         "protein = the 1 GiB protein-like leg")
     ap.add_argument("--launch-check", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--traffic-gb", type=float, default=None,
                     help="PMC-measured HBM GB per launch of the dominant kernel; default: profiles/pmc_kernels.json")
@@ -806,6 +846,8 @@ def main():
         dist.destroy_process_group()
     elif args.only_leg == "english":
         res = {"leg": "english_like_200MiB", **english_leg(args)}
+    elif args.only_leg == "protein":
+        res = {"leg": "protein_like_1GiB", **protein_leg(args)}
     else:
         res = run_single(args)
         if not args.no_legs:

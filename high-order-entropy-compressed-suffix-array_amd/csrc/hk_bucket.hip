@@ -1408,7 +1408,9 @@ __global__ __launch_bounds__(CP_T, CAP == CP_TILE ? 4 : 6) void k_slice_cpart_re
       }
       __syncthreads();
       const uint32_t cc = cnt[tid];
-      const unsigned long long g = cc ? atomicAdd(&row[tid], (unsigned long long)cc) : 0ull;
+      unsigned long long* rowp = row;
+      asm volatile("" : "+s"(rowp));   // (re-derived per sub-tile: a hoisted row + tid pair spilled at 80 VGPRs)
+      const unsigned long long g = cc ? atomicAdd(&rowp[tid], (unsigned long long)cc) : 0ull;
       const uint32_t inc = wave_incl_sum<uint32_t>(cc);
       if (lane == 63) wsum[wv] = inc;
       __syncthreads();
@@ -4035,7 +4037,9 @@ bool slices_fuse(Index& ix, const std::vector<uint32_t>& B, const std::vector<ui
   }
   // one unit size for the group (the spans, hence the cursor rows, are shared)
   uint32_t g = (uint32_t)std::floor(0.9 * (double)n / (double)mmax);
-  g = std::max<uint32_t>(1, std::min<uint32_t>(g, (uint32_t)SL_G));
+  // at most 4 sub-tiles per unit: the 8-sub-tile form holds 8 x 3 code words and masks and spilled 24 B/lane
+  // at 128 VGPRs (only texts of 6+ slices reach g > 4)
+  g = std::max<uint32_t>(1, std::min<uint32_t>(g, 4u));
   for (FusedSlice& f : st->sl) f.P.sl.g = g;
   const uint64_t U = (uint64_t)SL_SUB * g;
   const uint64_t Lq = g % 2 ? 2 * U : U;
@@ -4144,8 +4148,7 @@ bool slices_fuse(Index& ix, const std::vector<uint32_t>& B, const std::vector<ui
   {
     TimedLaunch t(ix.timer, "shard_slice_part", (double)n + (double)msum * 8);
     const unsigned grid = (unsigned)(8 * ceil_div(nspan, 8u) * (span / U));
-    if (g <= 4) k_slice_cpart_fused<4><<<grid, CP_T, 0, s>>>(n, span, tks2, P0.sl, fs, d_ovf);
-    else k_slice_cpart_fused<SL_G><<<grid, CP_T, 0, s>>>(n, span, tks2, P0.sl, fs, d_ovf);
+    k_slice_cpart_fused<4><<<grid, CP_T, 0, s>>>(n, span, tks2, P0.sl, fs, d_ovf);
     HK_HIP(hipGetLastError());
   }
   const hipError_t we = hipEventSynchronize(ev_cnt);

@@ -107,6 +107,9 @@ struct Index {
   DevBuf big_k[2], big_v[2], big_j; // big buckets of the bucket build (sorted on the global path); the
                                     // members of large tied groups of a refinement / doubling round
   DevBuf grp_big;                   // refinement / doubling round: u8 per group, 1 = over SEG_MAX members
+                                    // (LDS item rounds: over SR_W members)
+  DevBuf sr_hp, sr_win, sr_items, sr_cnt;   // LDS item rounds (hk_seground.hip): group heads, window
+                                            // first / last heads, items, counters
   DevBuf bk_items, bk_hist, bk_fb; // bucket work items, bucket histogram, fast-path fallback items
   DevBuf cp_part, cp_cur, cp_tiles; // cursor partition: per-span counts, destination cursors, pass-B tiles
   HostBuf cp_host;                  // ... and its pinned host side (bucket counts, region table)
@@ -292,6 +295,7 @@ void dbl_emit_groups(Index& ix);            // upd = (P, slot of its group head)
 void dbl_apply_pairs(Index& ix, const uint64_t* d_pairs, uint64_t count);   // isa[p] = v
 void dbl_round(Index& ix, uint64_t K);      // one doubling round at offset dbl.h; dbl.h += K
 void dbl_ensure_isa(Index& ix);
+void dbl_isa_init_single(Index& ix);       // one GPU, u32 positions: ISA by bucketed scatter + tied head slots
 // SA/BWT of A sorted (keys, P) at slots J; ties (compared >> cs) compacted to (oP, oJ, oG)
 std::pair<uint64_t, uint64_t> refine_step_u32(Index& ix, const KeyGeom& kg, const uint64_t* keys,
                                               const uint32_t* P, const uint32_t* J, uint64_t A, int cs,

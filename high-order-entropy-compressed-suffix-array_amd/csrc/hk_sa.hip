@@ -26,6 +26,7 @@
 
 #include "hk_index.hpp"
 #include "hk_keys.hpp"
+#include "hk_seground.hpp"
 
 namespace hk {
 namespace {
@@ -143,10 +144,28 @@ __global__ __launch_bounds__(256) void k_refine_keys(const V* __restrict__ P, co
   for (uint64_t a = (uint64_t)blockIdx.x * 256 + threadIdx.x; a < A; a += (uint64_t)gridDim.x * 256) {
     const V p = P[a];
     uint64_t chunk = 0;
+    const uint64_t s = (uint64_t)p + h;
     if ((uint64_t)p >= s_start) {
       chunk = srank[(uint64_t)p - s_start];
+    } else if (qn <= 16 && s + (uint64_t)qn <= n) {
+      // the usual case: both aligned 16-byte loads issued at once (one line fetch, not one per dependent word
+      // load — with 10^8 random positions in flight the line is gone from L2 before a dependent second load),
+      // then a 16-byte window from s by 64-bit funnel shifts
+      const uint64_t a16 = s & ~15ull;
+      const uint4 v0 = *reinterpret_cast<const uint4*>(t + a16);
+      const uint4 v1 = *reinterpret_cast<const uint4*>(t + a16 + 16);
+      const uint64_t w0 = (uint64_t)v0.x | ((uint64_t)v0.y << 32), w1 = (uint64_t)v0.z | ((uint64_t)v0.w << 32);
+      const uint64_t w2 = (uint64_t)v1.x | ((uint64_t)v1.y << 32), w3 = (uint64_t)v1.z | ((uint64_t)v1.w << 32);
+      const uint32_t off = (uint32_t)(s & 15), r8 = (off & 7) * 8;
+      const uint64_t A0 = off >= 8 ? w1 : w0, B0 = off >= 8 ? w2 : w1, C0 = off >= 8 ? w3 : w2;
+      const uint64_t W0 = r8 ? (A0 >> r8) | (B0 << (64 - r8)) : A0;
+      const uint64_t W1 = r8 ? (B0 >> r8) | (C0 << (64 - r8)) : B0;
+      for (int j = 0; j < qn; ++j) {
+        const uint32_t b = (uint32_t)((j < 8 ? W0 >> (8 * j) : W1 >> (8 * (j - 8))) & 255u);
+        chunk = chunk * R + L[b];
+      }
+      chunk += nS;
     } else {
-      const uint64_t s = (uint64_t)p + h;
       // the qn symbols from s, read as aligned 32-bit words (the text buffer has >= 64 bytes of pad)
       const uint64_t w0 = s & ~3ull;
       uint32_t word = s < n ? *reinterpret_cast<const uint32_t*>(t + w0) : 0u;
@@ -267,12 +286,14 @@ __global__ __launch_bounds__(GR_T) void k_big_count_rows(const uint32_t* __restr
   }
 }
 
+// oj: the member's list position, or with J its SA slot (a round's big groups regrouped as their own list)
 template <typename V>
 __global__ __launch_bounds__(GR_T) void k_big_compact_rows(const uint64_t* __restrict__ keys, const V* __restrict__ vals,
                                                            const uint32_t* __restrict__ G,
                                                            const uint8_t* __restrict__ gbig, uint64_t A,
                                                            const uint64_t* __restrict__ toff, uint64_t* __restrict__ ok,
-                                                           V* __restrict__ ov, uint32_t* __restrict__ oj) {
+                                                           V* __restrict__ ov, uint32_t* __restrict__ oj,
+                                                           const uint32_t* __restrict__ J = nullptr) {
   __shared__ uint32_t wc[2][GR_T / 64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const uint64_t tbase = (uint64_t)blockIdx.x * GR_TILE;
@@ -294,7 +315,7 @@ __global__ __launch_bounds__(GR_T) void k_big_compact_rows(const uint64_t* __res
       const uint64_t o = run + pre + ci - 1;
       ok[o] = keys[j];
       ov[o] = vals[j];
-      oj[o] = (uint32_t)j;
+      oj[o] = J ? J[j] : (uint32_t)j;
     }
     run += row;
   }
@@ -345,6 +366,84 @@ __global__ __launch_bounds__(256) void k_dbl_apply_pairs(const uint64_t* __restr
                                                          V* __restrict__ isa) {
   for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < cnt; i += (uint64_t)gridDim.x * 256)
     isa[pairs[2 * i]] = (V)pairs[2 * i + 1];
+}
+
+// ---- ISA of every position at the switch to prefix doubling (single GPU, u32 positions).  ISA[p] = its SA slot,
+// or for a tied suffix its group head's slot.  A straight scatter isa[SA[j]] = v writes 4 B at a random
+// position per suffix, and every such write costs a whole line in HBM (7.2 ms and 6.7 GB of writes for a
+// 200 MiB text).  Instead: hs[j] = the value of slot j (iota, then the tied slots' head slots, near-
+// coalesced along the tie list), one pass partitions (SA[j], hs[j]) into buckets of 2^ISA_SH consecutive
+// positions (bucket b holds exactly the positions [b << ISA_SH, (b + 1) << ISA_SH): no histogram), and a
+// second pass writes each bucket's ISA range from the workgroups of one XCD, so its 2 MiB of ISA lines are
+// completed in that XCD's L2 before they are written back.
+constexpr int ISA_SH = 19;            // 512 Ki positions = 2 MiB of u32 ISA per bucket
+constexpr int ISA_TILE = 256 * 32;    // SA entries per partition tile
+constexpr int ISA_Q = 16;             // workgroups per bucket in the write pass
+
+__global__ __launch_bounds__(256) void k_hs_tied(const uint32_t* __restrict__ J, const uint32_t* __restrict__ G,
+                                                 uint64_t A, const uint32_t* __restrict__ head_slot,
+                                                 uint32_t* __restrict__ hs) {
+  for (uint64_t a = (uint64_t)blockIdx.x * 256 + threadIdx.x; a < A; a += (uint64_t)gridDim.x * 256)
+    hs[J[a]] = head_slot[G[a]];
+}
+
+__global__ __launch_bounds__(256) void k_isa_part(const uint32_t* __restrict__ sa, const uint32_t* __restrict__ hs,
+                                                  uint64_t n, uint64_t* __restrict__ cursor,
+                                                  uint64_t* __restrict__ pairs) {
+  __shared__ uint32_t cnt[4096];
+  __shared__ uint64_t base[4096];
+  const uint64_t nb = (n + (1ull << ISA_SH) - 1) >> ISA_SH;   // <= 8192 for n < 2^32
+  const uint64_t t0 = (uint64_t)blockIdx.x * ISA_TILE;
+  // LDS counters for 4096 buckets: texts of more than 2^31 positions (up to 8192 buckets) take the tile in
+  // two rounds, buckets [0, 4096) then [4096, 8192)
+  for (uint32_t hi = 0; hi < (uint32_t)((nb + 4095) / 4096); ++hi) {
+    for (uint32_t i = threadIdx.x; i < 4096; i += 256) cnt[i] = 0;
+    __syncthreads();
+    uint32_t slot[32];
+#pragma unroll
+    for (int k = 0; k < 32; ++k) {
+      const uint64_t j = t0 + (uint64_t)k * 256 + threadIdx.x;
+      slot[k] = 0xFFFFFFFFu;
+      if (j < n) {
+        const uint32_t p = sa[j];
+        const uint32_t b = p >> ISA_SH;
+        if ((b >> 12) == hi) slot[k] = atomicAdd(&cnt[b & 4095u], 1u);
+      }
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < 4096; i += 256) {
+      const uint32_t c = cnt[i];
+      if (c) base[i] = atomicAdd((unsigned long long*)&cursor[((uint64_t)hi << 12) + i], (unsigned long long)c);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 32; ++k) {
+      const uint64_t j = t0 + (uint64_t)k * 256 + threadIdx.x;
+      if (slot[k] != 0xFFFFFFFFu) {
+        const uint32_t p = sa[j];
+        pairs[base[(p >> ISA_SH) & 4095u] + slot[k]] = ((uint64_t)p << 32) | hs[j];
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// bucket b is written by the workgroups g with g % 8 == b % 8 (one XCD when workgroups are dealt round-robin
+// to the 8 XCDs — a speed assumption only)
+__global__ __launch_bounds__(256) void k_isa_write(const uint64_t* __restrict__ pairs, uint64_t n,
+                                                   uint32_t* __restrict__ isa) {
+  const uint32_t g = blockIdx.x;
+  const uint32_t x = g & 7u, slotg = g >> 3;
+  const uint64_t b = (uint64_t)x + 8ull * (slotg / ISA_Q);
+  const uint32_t part = slotg % ISA_Q;
+  const uint64_t lo = b << ISA_SH;
+  if (lo >= n) return;
+  const uint64_t len = std::min<uint64_t>(1ull << ISA_SH, n - lo);
+  const uint64_t a0 = lo + len * part / ISA_Q, a1 = lo + len * (part + 1) / ISA_Q;
+  for (uint64_t a = a0 + threadIdx.x; a < a1; a += 256) {
+    const uint64_t pr = pairs[a];
+    isa[pr >> 32] = (uint32_t)pr;
+  }
 }
 
 // doubling keys: (dense group ordinal << ib) | (ISA[p + h] + 1, or 0 past the end), value = position
@@ -701,7 +800,137 @@ void sort_big_groups(Index& ix, uint64_t* k0, V* v0, const uint32_t* G, uint64_t
   }
 }
 
-// one doubling round over the active list: keys, sort, regroup; see k_dbl_apply
+// One doubling regroup over a sorted list (row kernels: stats, scans, apply): ISA of every member (or (position,
+// ISA) pairs), SA / BWT of the settled ones, the tied ones into (oP, oJ, oG) from index 0.  d_flag (nullable): a
+// device flag read back with the totals into *h_flag.  Returns (tied, groups).
+template <typename V>
+std::pair<uint64_t, uint64_t> dbl_apply_list(Index& ix, const uint64_t* keys, const V* vals, const uint32_t* J,
+                                             uint64_t A, int ib, bool keep_same, uint64_t* pairs, V* oP, uint32_t* oJ,
+                                             uint32_t* oG, const unsigned int* d_flag = nullptr,
+                                             unsigned int* h_flag = nullptr) {
+  hipStream_t s = ix.stream;
+  const uint64_t nt = ceil_div(A, GR_TILE);
+  ix.tile_a.ensure((nt + 2) * 8);
+  ix.tile_b.ensure((nt + 1) * 4);
+  ix.tile_c.ensure((nt + 1) * 8);
+  ix.tile_d.ensure((nt + 2) * 8);
+  DevBuf& tb2 = ix.tile_e;
+  tb2.ensure((nt + 2) * 12 + 16);
+  uint64_t* tl = ix.tile_a.as<uint64_t>();
+  uint32_t* ta = ix.tile_b.as<uint32_t>();
+  uint64_t* cl = ix.tile_c.as<uint64_t>();
+  uint64_t* ao = ix.tile_d.as<uint64_t>();
+  uint32_t* th = tb2.as<uint32_t>();
+  uint64_t* ho = reinterpret_cast<uint64_t*>(tb2.as<uint8_t>() + ((nt + 2) * 4 + 7) / 8 * 8);
+  {
+    TimedLaunch tm(ix.timer, "sa_group_stats", (double)A * 8);
+    k_dbl_stats_rows<<<(unsigned)nt, GR_T, 0, s>>>(keys, J, A, ib, tl, ta, th);
+    HK_HIP(hipGetLastError());
+  }
+  scan_exclusive_max_u64(ix.sw, tl, cl, nt, s);
+  scan_exclusive_u32_to_u64(ix.sw, ta, ao, nt, true, s);
+  scan_exclusive_u32_to_u64(ix.sw, th, ho, nt, true, s);
+  {
+    TimedLaunch tm(ix.timer, "sa_group_apply", (double)A * (8 + 2 * sizeof(V) + 4 + 1 + 1 + (pairs ? 16 : sizeof(V))));
+    k_dbl_apply_rows<V><<<(unsigned)nt, GR_T, 0, s>>>(
+        keys, vals, J, A, ib, keep_same, cl, ao, ho, ix.sharded ? ix.shard_lo : 0, ix.isa.as<V>(), pairs,
+        ix.sa.as<V>(), ix.bwt.as<uint8_t>(), ix.text.as<uint8_t>(), ix.n, oP, oJ, oG, ix.head_slot.as<uint32_t>());
+    HK_HIP(hipGetLastError());
+  }
+  uint64_t* const tot = ix.rb();   // pinned: the copies land without a staging hop
+  HK_HIP(hipMemcpyAsync(&tot[0], ao + nt, 8, hipMemcpyDeviceToHost, s));
+  HK_HIP(hipMemcpyAsync(&tot[1], ho + nt, 8, hipMemcpyDeviceToHost, s));
+  tot[2] = 0;
+  if (d_flag) HK_HIP(hipMemcpyAsync(&tot[2], d_flag, 4, hipMemcpyDeviceToHost, s));
+  HK_HIP(hipStreamSynchronize(s));
+  if (h_flag) *h_flag = (unsigned int)tot[2];
+  return {tot[0], tot[1]};
+}
+
+template <typename V>
+std::pair<uint64_t, uint64_t> refine_step(Index& ix, const KeyGeom& kg, const uint64_t* keys, const V* P,
+                                          const uint32_t* J, uint64_t A, int cs, bool from_key, bool write_sa,
+                                          V* oP, uint32_t* oJ, uint32_t* oG, uint32_t* head_slot,
+                                          const unsigned int* d_flag = nullptr, unsigned int* h_flag = nullptr);
+
+// One round's sort + regroup through LDS items of whole groups (hk_seground.hip).  The round's keys (G in the
+// top bits) and positions are in keys[0] / vals[0], list act[cur]; the next list goes to act[cur ^ 1].  The
+// big groups (over SR_W members) go first: their members gathered with their SA slots, radix-sorted on key
+// bits [0, bits) and regrouped by the row kernels as a list of their own into the front of the next list;
+// the items append after them.  mode 0: chunk refinement (SA of every slot, BWT of the settled), 1: doubling
+// (ISA).  Returns the next list's (tied, groups).
+template <typename V>
+std::pair<uint64_t, uint64_t> seg_round(Index& ix, const KeyGeom& kg, int mode, int cur, uint64_t A, uint64_t groups,
+                                        int bits, int ib) {
+  hipStream_t s = ix.stream;
+  uint64_t* const k0 = ix.keys[0].as<uint64_t>();
+  V* const v0 = ix.vals[0].as<V>();
+  const uint32_t* G = ix.act[cur][2].as<uint32_t>();
+  const uint32_t* J = ix.act[cur][1].as<uint32_t>();
+  V* oP = ix.act[cur ^ 1][0].as<V>();
+  uint32_t* oJ = ix.act[cur ^ 1][1].as<uint32_t>();
+  uint32_t* oG = ix.act[cur ^ 1][2].as<uint32_t>();
+  uint64_t nbg = 0;
+  const uint64_t B = sr_plan(ix, G, A, groups, &nbg);
+  std::pair<uint64_t, uint64_t> r0{0, 0};
+  if (B) {
+    const uint64_t nt = ceil_div(A, GR_TILE);
+    ix.tile_b.ensure((nt + 1) * 4);
+    ix.tile_a.ensure((nt + 2) * 8);
+    const uint8_t* gbig = ix.grp_big.as<uint8_t>();
+    {
+      TimedLaunch tm(ix.timer, "sa_big_groups", (double)A * 5);
+      k_big_count_rows<<<(unsigned)nt, GR_T, 0, s>>>(G, gbig, A, ix.tile_b.as<uint32_t>());
+      HK_HIP(hipGetLastError());
+    }
+    scan_exclusive_u32_to_u64(ix.sw, ix.tile_b.as<uint32_t>(), ix.tile_a.as<uint64_t>(), nt, true, s);
+    for (int i = 0; i < 2; ++i) {
+      ix.big_k[i].ensure(B * 8 + 16);
+      ix.big_v[i].ensure(B * sizeof(V) + 16);
+    }
+    ix.big_j.ensure(B * 4 + 16);
+    uint64_t* bk[2] = {ix.big_k[0].as<uint64_t>(), ix.big_k[1].as<uint64_t>()};
+    V* bv[2] = {ix.big_v[0].as<V>(), ix.big_v[1].as<V>()};
+    {
+      TimedLaunch tm(ix.timer, "sa_big_groups", (double)A * 5 + (double)B * (8 + 2 * sizeof(V) + 4 + 8));
+      k_big_compact_rows<V><<<(unsigned)nt, GR_T, 0, s>>>(k0, v0, G, gbig, A, ix.tile_a.as<uint64_t>(), bk[0], bv[0],
+                                                          ix.big_j.as<uint32_t>(), J);
+      HK_HIP(hipGetLastError());
+    }
+    const int sl = radix_sort_pairs<V>(ix.sw, ix.timer, bk, bv, 0, B, 0, bits, false, s);
+    ix.info[0] += ix.sw.passes_run;
+    ix.info[1] += ix.sw.passes_skipped;
+    if (mode == 0)
+      r0 = refine_step<V>(ix, kg, bk[sl], bv[sl], ix.big_j.as<uint32_t>(), B, 0, false, true, oP, oJ, oG,
+                          ix.head_slot.as<uint32_t>());
+    else
+      r0 = dbl_apply_list<V>(ix, bk[sl], bv[sl], ix.big_j.as<uint32_t>(), B, ib, true, nullptr, oP, oJ, oG);
+  }
+  SrRoundArgs<V> a{};
+  a.keys = k0;
+  a.vals = v0;
+  a.G = G;
+  a.J = J;
+  a.oP = oP;
+  a.oJ = oJ;
+  a.oG = oG;
+  a.head_slot = ix.head_slot.as<uint32_t>();
+  a.sa = ix.sa.as<V>();
+  a.bwt = ix.bwt.as<uint8_t>();
+  a.t = ix.text.as<uint8_t>();
+  a.n = ix.n;
+  a.isa = mode ? ix.isa.as<V>() : nullptr;
+  a.lo = ix.sharded ? ix.shard_lo : 0;
+  a.keep_same = 1;
+  return sr_items_round<V>(ix, mode, a, A, r0.first, r0.second);
+}
+
+// one doubling round over the active list: keys, sort, regroup.  Single GPU and one-GPU slices: the LDS item
+// round (seg_round).  Sharded slices (the rank exchange needs every member's (position, ISA) pair in list
+// order): groups of < 4 members on average sorted in place (seg_sort_groups), the few large ones by
+// sort_big_groups, the round applied at once (its large-group flag rides in the read-back) and redone after
+// sort_big_groups only if a large group was left — once one was, the next rounds read the flag first; larger
+// average groups: the radix sort of the whole list.
 template <typename V>
 void dbl_round_t(Index& ix, uint64_t K) {
   auto& st = ix.dbl;
@@ -723,89 +952,55 @@ void dbl_round_t(Index& ix, uint64_t K) {
                                               ix.isa.as<V>(), ix.n, st.h, ib, kp[0], vp[0]);
     HK_HIP(hipGetLastError());
   }
-  // groups of < 4 members on average: each group sorted in place (seg_sort_groups), the few large ones
-  // by sort_big_groups; the round is applied at once (its large-group flag rides in the read-back) and
-  // redone after sort_big_groups only if a large group was left — once one was, the next rounds read the
-  // flag first.  Larger average groups: the radix sort of the whole list.
-  const bool direct = A >= 4 * st.groups;
-  unsigned int* d_big = reinterpret_cast<unsigned int*>(ix.small.as<uint8_t>() + 4356);   // small+4356: flag
-  const uint32_t* G = ix.act[cur][2].as<uint32_t>();
-  int sl = 0;
-  bool spec = false;
-  if (direct) {
-    sl = radix_sort_pairs<V>(ix.sw, ix.timer, kp, vp, 0, A, 0, gbits + ib, false, s);
-    ix.info[0] += ix.sw.passes_run;
-    ix.info[1] += ix.sw.passes_skipped;
+  std::pair<uint64_t, uint64_t> r{0, 0};
+  const bool exchange = ix.sharded && !ix.slices_local;
+  if (!exchange) {
+    r = seg_round<V>(ix, KeyGeom{}, 1, cur, A, st.groups, gbits + ib, ib);
+    st.npairs = 0;
   } else {
-    seg_sort_groups<V>(ix, kp[0], vp[0], G, A, st.groups, d_big, "sa_pair_segsort");
-    if (st.big) {
-      uint64_t* const rb = ix.rb();
-      rb[2] = 0;
-      HK_HIP(hipMemcpyAsync(&rb[2], d_big, 4, hipMemcpyDeviceToHost, s));
-      HK_HIP(hipStreamSynchronize(s));
-      st.big = (uint32_t)rb[2] != 0;
-      if (st.big) sort_big_groups<V>(ix, kp[0], vp[0], G, A, gbits + ib);
+    const bool direct = A >= 4 * st.groups;
+    unsigned int* d_big = reinterpret_cast<unsigned int*>(ix.small.as<uint8_t>() + 4356);   // small+4356: flag
+    const uint32_t* G = ix.act[cur][2].as<uint32_t>();
+    int sl = 0;
+    bool spec = false;
+    if (direct) {
+      sl = radix_sort_pairs<V>(ix.sw, ix.timer, kp, vp, 0, A, 0, gbits + ib, false, s);
+      ix.info[0] += ix.sw.passes_run;
+      ix.info[1] += ix.sw.passes_skipped;
     } else {
-      spec = true;
+      seg_sort_groups<V>(ix, kp[0], vp[0], G, A, st.groups, d_big, "sa_pair_segsort");
+      if (st.big) {
+        uint64_t* const rb = ix.rb();
+        rb[2] = 0;
+        HK_HIP(hipMemcpyAsync(&rb[2], d_big, 4, hipMemcpyDeviceToHost, s));
+        HK_HIP(hipStreamSynchronize(s));
+        st.big = (uint32_t)rb[2] != 0;
+        if (st.big) sort_big_groups<V>(ix, kp[0], vp[0], G, A, gbits + ib);
+      } else {
+        spec = true;
+      }
     }
-  }
-  const uint64_t nt = ceil_div(A, GR_TILE);
-  ix.tile_a.ensure((nt + 2) * 8);   // (nt + 2): sort_big_groups in the redo below must not regrow it under tl
-  ix.tile_b.ensure((nt + 1) * 4);
-  ix.tile_c.ensure((nt + 1) * 8);
-  ix.tile_d.ensure((nt + 2) * 8);
-  DevBuf& tb2 = ix.tile_e;
-  tb2.ensure((nt + 2) * 12 + 16);
-  uint64_t* tl = ix.tile_a.as<uint64_t>();
-  uint32_t* ta = ix.tile_b.as<uint32_t>();
-  uint64_t* cl = ix.tile_c.as<uint64_t>();
-  uint64_t* ao = ix.tile_d.as<uint64_t>();
-  uint32_t* th = tb2.as<uint32_t>();
-  uint64_t* ho = reinterpret_cast<uint64_t*>(tb2.as<uint8_t>() + ((nt + 2) * 4 + 7) / 8 * 8);
-  uint64_t* pairs = nullptr;
-  if (ix.sharded && !ix.slices_local) {
     ix.upd.ensure(A * 16 + 16);
-    pairs = ix.upd.as<uint64_t>();
-  }
-  uint64_t* const tot = ix.rb();   // pinned: the copies land without a staging hop
-  // keep_same: skip the ISA entries a round leaves unchanged (not in the redo after a speculative apply,
-  // which may have rewritten some of them)
-  auto apply_round = [&](int slot, bool flag, bool keep_same) {
-    {
-      TimedLaunch tm(ix.timer, "sa_group_stats", (double)A * 8);
-      k_dbl_stats_rows<<<(unsigned)nt, GR_T, 0, s>>>(kp[slot], ix.act[cur][1].as<uint32_t>(), A, ib, tl, ta, th);
-      HK_HIP(hipGetLastError());
+    uint64_t* pairs = ix.upd.as<uint64_t>();
+    V* oP = ix.act[cur ^ 1][0].as<V>();
+    uint32_t* oJ = ix.act[cur ^ 1][1].as<uint32_t>();
+    uint32_t* oG = ix.act[cur ^ 1][2].as<uint32_t>();
+    const uint32_t* J = ix.act[cur][1].as<uint32_t>();
+    unsigned int h_big = 0;
+    // keep_same: skip the ISA entries a round leaves unchanged (pairs carry every entry anyway)
+    r = dbl_apply_list<V>(ix, kp[sl], vp[sl], J, A, ib, true, pairs, oP, oJ, oG, spec ? d_big : nullptr, &h_big);
+    if (spec && h_big) {   // a group over SEG_MAX members was left unsorted: redo the round
+      st.big = true;
+      // (the redo rewrites every pair, list entry and group head of the first attempt; an SA / BWT slot it
+      // wrote for a suffix it wrongly took as settled is rewritten by the slot's final owner)
+      sort_big_groups<V>(ix, kp[0], vp[0], G, A, gbits + ib);
+      r = dbl_apply_list<V>(ix, kp[0], vp[0], J, A, ib, false, pairs, oP, oJ, oG);
     }
-    scan_exclusive_max_u64(ix.sw, tl, cl, nt, s);
-    scan_exclusive_u32_to_u64(ix.sw, ta, ao, nt, true, s);
-    scan_exclusive_u32_to_u64(ix.sw, th, ho, nt, true, s);
-    {
-      TimedLaunch tm(ix.timer, "sa_group_apply", (double)A * (8 + 2 * sizeof(V) + 4 + 1 + 1 + (pairs ? 16 : sizeof(V))));
-      k_dbl_apply_rows<V><<<(unsigned)nt, GR_T, 0, s>>>(
-          kp[slot], vp[slot], ix.act[cur][1].as<uint32_t>(), A, ib, keep_same, cl, ao, ho, ix.sharded ? ix.shard_lo : 0,
-          ix.isa.as<V>(), pairs, ix.sa.as<V>(), ix.bwt.as<uint8_t>(), ix.text.as<uint8_t>(), ix.n,
-          ix.act[cur ^ 1][0].as<V>(), ix.act[cur ^ 1][1].as<uint32_t>(), ix.act[cur ^ 1][2].as<uint32_t>(),
-          ix.head_slot.as<uint32_t>());
-      HK_HIP(hipGetLastError());
-    }
-    HK_HIP(hipMemcpyAsync(&tot[0], ao + nt, 8, hipMemcpyDeviceToHost, s));
-    HK_HIP(hipMemcpyAsync(&tot[1], ho + nt, 8, hipMemcpyDeviceToHost, s));
-    tot[2] = 0;
-    if (flag) HK_HIP(hipMemcpyAsync(&tot[2], d_big, 4, hipMemcpyDeviceToHost, s));
-    HK_HIP(hipStreamSynchronize(s));
-  };
-  apply_round(sl, spec, true);
-  if (spec && (uint32_t)tot[2]) {   // a group over SEG_MAX members was left unsorted: redo the round
-    st.big = true;
-    // (the redo rewrites every ISA entry, list entry and group head of the first attempt; an SA / BWT
-    // slot it wrote for a suffix it wrongly took as settled is rewritten by the slot's final owner)
-    sort_big_groups<V>(ix, kp[0], vp[0], G, A, gbits + ib);
-    apply_round(0, false, false);
+    st.npairs = A;
   }
-  st.npairs = pairs ? A : 0;
   st.cur ^= 1;
-  st.A = tot[0];
-  st.groups = tot[1];
+  st.A = r.first;
+  st.groups = r.second;
   st.h += K;
   ix.info.push_back(st.A);
   ix.info[2] += 1ull << 32;
@@ -816,7 +1011,7 @@ template <typename V>
 std::pair<uint64_t, uint64_t> refine_step(Index& ix, const KeyGeom& kg, const uint64_t* keys, const V* P,
                                           const uint32_t* J, uint64_t A, int cs, bool from_key, bool write_sa,
                                           V* oP, uint32_t* oJ, uint32_t* oG, uint32_t* head_slot,
-                                          const unsigned int* d_flag = nullptr, unsigned int* h_flag = nullptr) {
+                                          const unsigned int* d_flag, unsigned int* h_flag) {
   hipStream_t s = ix.stream;
   const uint64_t nt = ceil_div(A, GR_TILE);
   ix.tile_b.ensure((nt + 1) * 4);
@@ -974,7 +1169,6 @@ void refine_loop(Index& ix, const KeyGeom& kg, int cur, uint64_t A, uint64_t gro
   uint64_t h = (uint64_t)kg.q;
   int rounds = 0;
   uint64_t A_prev = 0;
-  bool big_seen = false;   // a round had a group over SEG_MAX members
   const bool local_dbl = allow_doubling || ix.slices_local;   // doubling needs no rank exchange here
   const uint64_t m_all = ix.sharded ? ix.shard_hi - ix.shard_lo : ix.n;
   while (A > 0 && rounds < kChunkRounds) {
@@ -1004,46 +1198,9 @@ void refine_loop(Index& ix, const KeyGeom& kg, int cur, uint64_t A, uint64_t gro
                                                    vp[0], s_start, nS, d_srank);
       HK_HIP(hipGetLastError());
     }
-    // groups of four or more members on average (natural-language text): the radix sort of the whole
-    // list.  Else each group of <= SEG_MAX members sorted in place and the round applied at once, its
-    // large-group flag riding in the round's read-back; a large group left unsorted is then sorted by
-    // sort_big_groups and the round redone (every output of the first attempt rewritten), and the later
-    // rounds read the flag before applying.
-    const bool direct = groups && A >= 4 * groups;
-    const uint32_t* G = ix.act[cur][2].as<uint32_t>();
-    unsigned int* d_big = reinterpret_cast<unsigned int*>(ix.small.as<uint8_t>() + 4356);   // small+4356: flag
-    auto step = [&](const uint64_t* keys, const V* vals, bool flag, unsigned int* h_flag) {
-      return refine_step<V>(ix, kg, keys, vals, ix.act[cur][1].as<uint32_t>(), A, 0, false, true,
-                            ix.act[cur ^ 1][0].as<V>(), ix.act[cur ^ 1][1].as<uint32_t>(),
-                            ix.act[cur ^ 1][2].as<uint32_t>(), ix.head_slot.as<uint32_t>(), flag ? d_big : nullptr,
-                            h_flag);
-    };
-    std::pair<uint64_t, uint64_t> r{0, 0};
-    if (direct) {
-      const int sl = radix_sort_pairs<V>(ix.sw, ix.timer, kp, vp, 0, A, 0, 64, false, s);
-      ix.info[0] += ix.sw.passes_run;
-      ix.info[1] += ix.sw.passes_skipped;
-      r = step(kp[sl], vp[sl], false, nullptr);
-    } else {
-      seg_sort_groups<V>(ix, kp[0], vp[0], G, A, groups, d_big, "sa_refine_segsort");
-      unsigned int h_big = 0;
-      if (big_seen) {
-        uint64_t* const rb = ix.rb();
-        rb[2] = 0;
-        HK_HIP(hipMemcpyAsync(&rb[2], d_big, 4, hipMemcpyDeviceToHost, s));
-        HK_HIP(hipStreamSynchronize(s));
-        big_seen = (uint32_t)rb[2] != 0;
-        if (big_seen) sort_big_groups<V>(ix, kp[0], vp[0], G, A, 64);
-        r = step(kp[0], vp[0], false, nullptr);
-      } else {
-        r = step(kp[0], vp[0], true, &h_big);
-        if (h_big) {
-          big_seen = true;
-          sort_big_groups<V>(ix, kp[0], vp[0], G, A, 64);
-          r = step(kp[0], vp[0], false, nullptr);
-        }
-      }
-    }
+    // sort inside each group + regroup: LDS items of whole groups, the groups of over SR_W members by a
+    // global radix sort first (seg_round)
+    const std::pair<uint64_t, uint64_t> r = seg_round<V>(ix, kg, 0, cur, A, groups, 64, 0);
     cur ^= 1;
     A = r.first;
     groups = r.second;
@@ -1065,8 +1222,12 @@ void refine_loop(Index& ix, const KeyGeom& kg, int cur, uint64_t A, uint64_t gro
   }
   // single GPU: ISA of every position from the full SA, tied suffixes at their head's slot
   dbl_ensure_isa(ix);
-  dbl_isa_segment(ix, ix.sa.p, ix.n, 0);
-  dbl_emit_groups(ix);
+  if (!ix.sharded && !ix.sa_pos64 && ix.n < 0xFFFFFFFFull) {
+    dbl_isa_init_single(ix);
+  } else {
+    dbl_isa_segment(ix, ix.sa.p, ix.n, 0);
+    dbl_emit_groups(ix);
+  }
   int drounds = 0;
   while (ix.dbl.A > 0) {
     if (++drounds > 64) throw ApiError{-7, "prefix doubling did not converge"};
@@ -1100,6 +1261,41 @@ void dbl_isa_segment(Index& ix, const void* d_sa, uint64_t count, uint64_t lo) {
     k_isa_from_sa<uint32_t><<<grid_for(count), 256, 0, ix.stream>>>(static_cast<const uint32_t*>(d_sa), count, lo,
                                                                      ix.isa.as<uint32_t>());
   HK_HIP(hipGetLastError());
+}
+
+// ISA at the switch to doubling on one GPU (u32 positions, not sharded): see k_isa_part
+void dbl_isa_init_single(Index& ix) {
+  const uint64_t n = ix.n;
+  hipStream_t s = ix.stream;
+  auto& st = ix.dbl;
+  const uint64_t nb = (n + (1ull << ISA_SH) - 1) >> ISA_SH;
+  uint32_t* hs = ix.vals[0].as<uint32_t>();   // (free until the first round's keys)
+  uint64_t* pairs = ix.keys[1].as<uint64_t>();
+  std::vector<uint64_t> cur(nb);
+  for (uint64_t b = 0; b < nb; ++b) cur[b] = b << ISA_SH;
+  ix.tile_c.ensure(nb * 8 + 16);
+  HK_HIP(hipMemcpyAsync(ix.tile_c.p, cur.data(), nb * 8, hipMemcpyHostToDevice, s));
+  {
+    TimedLaunch tm(ix.timer, "sa_isa_scatter", (double)n * 4 + (double)st.A * 12);
+    fill_iota<uint32_t>(hs, n, s);
+    if (st.A)
+      k_hs_tied<<<grid_for(st.A), 256, 0, s>>>(ix.act[st.cur][1].as<uint32_t>(), ix.act[st.cur][2].as<uint32_t>(), st.A,
+                                                ix.head_slot.as<uint32_t>(), hs);
+    HK_HIP(hipGetLastError());
+  }
+  {
+    TimedLaunch tm(ix.timer, "sa_isa_scatter", (double)n * (4 + 4 + 8));
+    k_isa_part<<<(unsigned)ceil_div(n, ISA_TILE), 256, 0, s>>>(ix.sa.as<uint32_t>(), hs, n, ix.tile_c.as<uint64_t>(),
+                                                               pairs);
+    HK_HIP(hipGetLastError());
+  }
+  {
+    TimedLaunch tm(ix.timer, "sa_isa_scatter", (double)n * (8 + 4));
+    const uint64_t rows = ceil_div(nb, 8);
+    k_isa_write<<<(unsigned)(rows * 8 * ISA_Q), 256, 0, s>>>(pairs, n, ix.isa.as<uint32_t>());
+    HK_HIP(hipGetLastError());
+  }
+  HK_HIP(hipStreamSynchronize(s));   // (cur)
 }
 
 void dbl_emit_groups(Index& ix) {
@@ -1344,6 +1540,7 @@ void release_workspace(Index& ix) {
   }
   ix.big_j.release();
   ix.grp_big.release();
+  for (DevBuf* b : {&ix.sr_hp, &ix.sr_win, &ix.sr_items, &ix.sr_cnt}) b->release();
   ix.fused.reset();
   ix.fused_recs.release();
   ix.fused_ws.release();

@@ -1,0 +1,457 @@
+// hk_seground.hip — the sort + regroup step of one refinement (chunk) round or prefix-doubling round over
+// the tie list: each tied group is ordered by its members' next symbols / ISA[p + h]
+// (csa/suffix_array.py:131-134 orders suffixes by their whole text; the rounds extend the compared prefix).
+//
+// The tie list holds whole groups: G = dense group ordinal, ascending along the list; the members' SA
+// slots J are contiguous and ascending along the list.  A round's keys (the caller's key kernel: G in the
+// top bits, the next chunk or ISA[p + h] + 1 below) only need ordering INSIDE each group, so instead of
+// radix-sorting the whole list over every key bit (8 global passes over ~10^8 pairs on natural-language
+// text) the list is cut into items of whole groups:
+//   * windows of SR_W list entries; item w = the groups whose head lies in window w, except a last group of
+//     more than SR_W members (a "big" group, k_sr_items) — so an item holds fewer than 2 * SR_W entries;
+//   * one workgroup per item (k_sr_round): the item's keys and positions are staged in LDS and sorted there
+//     — one thread per group when no group has more than 16 members (pairs dominate late doubling rounds),
+//     else stable LSD passes of 8 bits over only the bits that vary inside the item — then regrouped in
+//     the same workgroup: settled suffixes write their SA / BWT entries, tied ones are appended to the
+//     next list through one 64-bit atomic per item (entries | groups << 33, so both are reserved in one
+//     operation and G stays ascending along the new list), doubling rounds write ISA;
+//   * big groups: gathered, radix-sorted in global memory and regrouped by the row kernels (hk_sa.hip)
+//     into the front of the next list, before the items append.
+// The round's work is then one read and one write of the list plus LDS work, instead of a full radix
+// sort plus a grouping pass.
+
+#include "hk_index.hpp"
+#include "hk_seground.hpp"
+
+namespace hk {
+namespace {
+
+constexpr int SR_T = 256;
+constexpr int SR_E = SR_CAP / SR_T;   // 16 entries per thread
+constexpr int SR_NW = SR_T / 64;
+constexpr uint32_t SR_NONE = 0xFFFFFFFFu;
+
+// heads: hp[G[a]] = a; first / last head of every window (one atomic pair per wave)
+__global__ __launch_bounds__(256) void k_sr_heads(const uint32_t* __restrict__ G, uint64_t A, uint32_t* __restrict__ hp,
+                                                  uint32_t* __restrict__ wstart, uint32_t* __restrict__ wlast) {
+  const uint32_t lane = threadIdx.x & 63;
+  for (uint64_t b = (uint64_t)blockIdx.x * 256; b < A; b += (uint64_t)gridDim.x * 256) {   // (uniform)
+    const uint64_t a = b + threadIdx.x;
+    bool head = false;
+    if (a < A) {
+      const uint32_t g = G[a];
+      head = a == 0 || G[a - 1] != g;
+      if (head) hp[g] = (uint32_t)a;
+    }
+    const uint64_t m = ballot64(head);
+    if (m) {   // a wave's 64 entries lie in one window (SR_W is a multiple of 64)
+      const uint64_t w0 = (b + (threadIdx.x & ~63u)) / SR_W;
+      if (lane == (uint32_t)__builtin_ctzll(m)) atomicMin(wstart + w0, (uint32_t)a);
+      if (lane == 63u - (uint32_t)__builtin_clzll(m)) atomicMax(wlast + w0, (uint32_t)a);
+    }
+  }
+}
+
+// items[w] = {first entry, entries}; a window's last group of more than SR_W members is big: flagged in
+// gbig, counted (cnt[0] entries, cnt[1] groups) and left out of the item
+__global__ __launch_bounds__(256) void k_sr_items(const uint32_t* __restrict__ G, const uint32_t* __restrict__ hp,
+                                                  uint64_t groups, uint64_t A, const uint32_t* __restrict__ wstart,
+                                                  const uint32_t* __restrict__ wlast, uint64_t nw,
+                                                  uint2* __restrict__ items, uint8_t* __restrict__ gbig,
+                                                  unsigned long long* __restrict__ cnt) {
+  for (uint64_t w = (uint64_t)blockIdx.x * 256 + threadIdx.x; w < nw; w += (uint64_t)gridDim.x * 256) {
+    const uint32_t ws = wstart[w];
+    if (ws == SR_NONE) {
+      items[w] = make_uint2(0u, 0u);
+      continue;
+    }
+    const uint32_t wl = wlast[w];
+    const uint32_t g = G[wl];
+    const uint64_t end = (uint64_t)g + 1 < groups ? (uint64_t)hp[g + 1] : A;
+    uint64_t we = end;
+    if (end - wl > (uint64_t)SR_W) {
+      gbig[g] = 1;
+      atomicAdd(cnt, (unsigned long long)(end - wl));
+      atomicAdd(cnt + 1, 1ull);
+      we = wl;
+    }
+    items[w] = make_uint2(ws, (uint32_t)(we - ws));
+  }
+}
+
+template <typename V>
+struct alignas(16) SrShared {
+  uint64_t key[SR_CAP];             // the item's keys (entry order; the sort permutes idx)
+  V val[SR_CAP];                    // positions
+  union {
+    uint32_t g[SR_CAP];             // group ordinals, while the head mask is built
+    uint16_t idx[2][SR_CAP];        // the order being sorted (entry indexes)
+  } u;
+  uint64_t hmask[SR_CAP / 64];      // bit i: a group starts at entry i (set past the item's end too)
+  uint32_t whist[SR_NW][256];       // per-wave digit counts -> per-wave exclusive digit offsets
+  uint64_t mtab[SR_NW][256];        // per-wave match masks (zero between uses)
+  uint32_t tstart[256];             // item-local exclusive digit start
+  uint32_t wtot[SR_NW];
+  uint64_t wor[SR_NW], wand[SR_NW];
+  uint32_t wbig[SR_NW];
+  uint32_t wmax[SR_NW], wcnt[SR_NW];
+  uint64_t obase, gbase;
+};
+
+// bitonic network over N (key, entry) registers, the group's sz <= N members padded with ~0 keys
+template <int N>
+__device__ __forceinline__ void sr_net(const uint64_t* __restrict__ key, uint16_t* __restrict__ out, uint32_t i0,
+                                       uint32_t sz) {
+  uint64_t k[N];
+  uint32_t e[N];
+#pragma unroll
+  for (int j = 0; j < N; ++j) {
+    k[j] = (uint32_t)j < sz ? key[i0 + j] : ~0ull;
+    e[j] = i0 + (uint32_t)j;
+  }
+#pragma unroll
+  for (int size = 2; size <= N; size <<= 1) {
+#pragma unroll
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+#pragma unroll
+      for (int j = 0; j < N; ++j) {
+        const int l = j ^ stride;
+        if (l > j) {
+          const bool up = (j & size) == 0;
+          const bool sw = up ? k[j] > k[l] : k[j] < k[l];
+          const uint64_t kj = k[j], kl = k[l];
+          const uint32_t ej = e[j], el = e[l];
+          k[j] = sw ? kl : kj;
+          k[l] = sw ? kj : kl;
+          e[j] = sw ? el : ej;
+          e[l] = sw ? ej : el;
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < N; ++j)
+    if ((uint32_t)j < sz) out[i0 + j] = (uint16_t)e[j];
+}
+
+__device__ __forceinline__ bool sr_head(const uint64_t* hm, uint32_t i) { return (hm[i >> 6] >> (i & 63)) & 1ull; }
+
+// the next group head after entry i (the bits past the item's end are set)
+__device__ __forceinline__ uint32_t sr_next_head(const uint64_t* hm, uint32_t i) {
+  uint32_t w = (i + 1) >> 6;
+  uint64_t b = hm[w] & (~0ull << ((i + 1) & 63));
+  while (!b) b = hm[++w];
+  return (w << 6) + (uint32_t)__builtin_ctzll(b);
+}
+
+// MODE 0: chunk refinement round (every slot's SA entry written, settled suffixes' BWT); MODE 1: prefix
+// doubling round (ISA of every member = its new group's head slot; SA / BWT of the settled ones)
+template <typename V, int MODE>
+__global__ __launch_bounds__(SR_T, sizeof(V) == 4 ? 2 : 1) void k_sr_round(SrRoundArgs<V> a) {
+  __shared__ SrShared<V> sh;
+  const uint2 it = a.items[blockIdx.x];
+  const uint32_t m = it.y;
+  if (m == 0) return;
+  const uint64_t base = it.x;
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+
+  // ---- 1. stage (striped: entry k * SR_T + tid), the head mask, the varying key bits, group sizes
+  uint64_t kor = 0, kand = ~0ull;
+#pragma unroll
+  for (int k = 0; k < SR_E; ++k) {
+    const uint32_t i = (uint32_t)k * SR_T + tid;
+    if (i < m) {
+      const uint64_t key = a.keys[base + i];
+      sh.key[i] = key;
+      sh.val[i] = a.vals[base + i];
+      sh.u.g[i] = a.G[base + i];
+      kor |= key;
+      kand &= key;
+    }
+  }
+  __syncthreads();
+  uint32_t big = 0;
+#pragma unroll
+  for (int k = 0; k < SR_E; ++k) {
+    const uint32_t i = (uint32_t)k * SR_T + tid;
+    const bool h = i >= m || i == 0 || sh.u.g[i] != sh.u.g[i - 1];
+    const uint64_t hb = ballot64(h);
+    if (lane == 0) sh.hmask[i >> 6] = hb;
+    if (i < m && i >= 16 && sh.u.g[i] == sh.u.g[i - 16]) big = 1;   // a group of more than 16 members
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    kor |= __shfl_xor(kor, o, 64);
+    kand &= __shfl_xor(kand, o, 64);
+  }
+  big = ballot64(big != 0) ? 1u : 0u;
+  if (lane == 0) {
+    sh.wor[wv] = kor;
+    sh.wand[wv] = kand;
+    sh.wbig[wv] = big;
+  }
+  __syncthreads();   // (every read of u.g is done: idx may overwrite it)
+  kor = 0;
+  kand = ~0ull;
+  big = 0;
+#pragma unroll
+  for (int w = 0; w < SR_NW; ++w) {
+    kor |= sh.wor[w];
+    kand &= sh.wand[w];
+    big |= sh.wbig[w];
+  }
+  const uint64_t vary = kor ^ kand;
+  int cur = 0;
+
+  // ---- 2. sort the item's groups (entries stay inside their group's range: G is in the keys' top bits)
+  if (!big) {
+#pragma unroll
+    for (int k = 0; k < SR_E; ++k) {   // every entry first takes its own place
+      const uint32_t i = (uint32_t)k * SR_T + tid;
+      if (i < m) sh.u.idx[0][i] = (uint16_t)i;
+    }
+    __syncthreads();
+    for (uint32_t i = tid; i < m; i += SR_T) {
+      if (!sr_head(sh.hmask, i)) continue;
+      const uint32_t sz = sr_next_head(sh.hmask, i) - i;
+      if (sz == 2) {
+        if (sh.key[i + 1] < sh.key[i]) {
+          sh.u.idx[0][i] = (uint16_t)(i + 1);
+          sh.u.idx[0][i + 1] = (uint16_t)i;
+        }
+      } else if (sz > 2 && sz <= 4) {
+        sr_net<4>(sh.key, sh.u.idx[0], i, sz);
+      } else if (sz > 4) {
+        sr_net<16>(sh.key, sh.u.idx[0], i, sz);
+      }
+    }
+    __syncthreads();
+  } else if (vary) {
+    const int lo = __builtin_ctzll(vary), hi = 64 - __builtin_clzll(vary);
+#pragma unroll
+    for (int k = 0; k < SR_E; ++k) {
+      const uint32_t i = (uint32_t)k * SR_T + tid;
+      if (i < m) sh.u.idx[0][i] = (uint16_t)i;
+    }
+    for (uint32_t i = tid; i < (uint32_t)SR_NW * 256; i += SR_T) (&sh.mtab[0][0])[i] = 0;
+    for (int shf = lo; shf < hi; shf += 8) {
+#pragma unroll
+      for (int w = 0; w < SR_NW; ++w) sh.whist[w][tid] = 0;
+      __syncthreads();
+      // rank inside the wave (stable: wave-contiguous positions, item-major then lane), as k_onesweep
+      uint32_t rk[SR_E];
+      uint64_t* const mt = sh.mtab[wv];
+#pragma unroll
+      for (int k = 0; k < SR_E; ++k) {
+        const uint32_t pos = wv * (SR_E * 64) + (uint32_t)k * 64 + lane;
+        const bool valid = pos < m;
+        const uint32_t id = valid ? sh.u.idx[cur][pos] : 0u;
+        const uint32_t d = valid ? (uint32_t)(sh.key[id] >> shf) & 255u : 0u;
+        if (valid) __hip_atomic_fetch_or(mt + d, 1ull << lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        const uint64_t msk = __hip_atomic_load(mt + d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        const uint32_t below = mbcnt(msk);
+        const uint32_t prior = sh.whist[wv][d];
+        if (valid && below == 0) {
+          __hip_atomic_store(mt + d, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          sh.whist[wv][d] = prior + (uint32_t)__popcll(msk);
+        }
+        rk[k] = (prior + below) | (d << 11) | (id << 19);   // rank < 1024, digit, entry < 4096
+      }
+      __syncthreads();
+      {   // per digit: wave prefixes, then the item-local exclusive start (thread = digit)
+        uint32_t run = 0;
+#pragma unroll
+        for (int w = 0; w < SR_NW; ++w) {
+          const uint32_t c = sh.whist[w][tid];
+          sh.whist[w][tid] = run;
+          run += c;
+        }
+        const uint32_t inc = dpp_incl_sum(run);
+        if (lane == 63) sh.wtot[wv] = inc;
+        __syncthreads();
+        uint32_t carry = 0;
+#pragma unroll
+        for (int w = 0; w < SR_NW; ++w) carry += (uint32_t)w < wv ? sh.wtot[w] : 0u;
+        sh.tstart[tid] = carry + inc - run;
+      }
+      __syncthreads();
+#pragma unroll
+      for (int k = 0; k < SR_E; ++k) {
+        const uint32_t pos = wv * (SR_E * 64) + (uint32_t)k * 64 + lane;
+        if (pos < m) {
+          const uint32_t d = (rk[k] >> 11) & 255u;
+          sh.u.idx[cur ^ 1][sh.tstart[d] + sh.whist[wv][d] + (rk[k] & 2047u)] = (uint16_t)(rk[k] >> 19);
+        }
+      }
+      __syncthreads();
+      cur ^= 1;
+    }
+  } else {   // every key equal: one group, one tied run, order kept
+#pragma unroll
+    for (int k = 0; k < SR_E; ++k) {
+      const uint32_t i = (uint32_t)k * SR_T + tid;
+      if (i < m) sh.u.idx[0][i] = (uint16_t)i;
+    }
+    __syncthreads();
+  }
+  const uint16_t* const ord = sh.u.idx[cur];
+
+  // ---- 3. regroup (blocked: thread tid owns positions [tid * SR_E, tid * SR_E + SR_E))
+  const uint32_t p0 = tid * SR_E;
+  uint32_t flags = 0;          // bit j: run head at p0 + j; bit 16 + j: tied
+  uint32_t lmax = 0, lcnt = 0;
+  {
+    uint64_t prev = 0;
+    bool have_prev = false;
+    if (p0 > 0 && p0 < m) {
+      prev = sh.key[ord[p0 - 1]];
+      have_prev = true;
+    }
+    uint64_t kc = p0 < m ? sh.key[ord[p0]] : 0;
+#pragma unroll
+    for (int j = 0; j < SR_E; ++j) {
+      const uint32_t i = p0 + (uint32_t)j;
+      if (i < m) {
+        const uint64_t kn = i + 1 < m ? sh.key[ord[i + 1]] : 0;
+        const bool rh = !have_prev || kc != prev;
+        const bool re = i + 1 >= m || kn != kc;
+        const bool tied = !(rh && re);
+        if (rh) {
+          flags |= 1u << j;
+          lmax = i;
+        }
+        if (tied) {
+          flags |= 1u << (16 + j);
+          lcnt += rh ? 0x10001u : 1u;
+        }
+        prev = kc;
+        have_prev = true;
+        kc = kn;
+      }
+    }
+  }
+  // item-wide exclusive scans of the threads' aggregates: max of run-head positions, tied | heads << 16
+  const uint32_t imax = dpp_scan_u32(lmax, 0u, [](uint32_t x, uint32_t y) { return x > y ? x : y; });
+  const uint32_t icnt = dpp_incl_sum(lcnt);
+  if (lane == 63) {
+    sh.wmax[wv] = imax;
+    sh.wcnt[wv] = icnt;
+  }
+  __syncthreads();
+  uint32_t cmax = 0, ccnt = 0, tcnt = 0;
+#pragma unroll
+  for (int w = 0; w < SR_NW; ++w) {
+    if ((uint32_t)w < wv) {
+      cmax = cmax > sh.wmax[w] ? cmax : sh.wmax[w];
+      ccnt += sh.wcnt[w];
+    }
+    tcnt += sh.wcnt[w];
+  }
+  // exclusive within the wave: the previous lane's inclusive value
+  const uint32_t pmax_w = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)imax, 0x138, 0xf, 0xf, false);   // wave_shr:1
+  const uint32_t pcnt_w = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)icnt, 0x138, 0xf, 0xf, false);
+  uint32_t rmax = cmax > pmax_w ? cmax : pmax_w;
+  uint32_t rcnt = ccnt + pcnt_w;
+  if (tid == 0) {
+    const unsigned long long inc = (unsigned long long)(tcnt & 0xFFFFu) |
+                                   ((unsigned long long)(tcnt >> 16) << 33);
+    const unsigned long long old = atomicAdd(a.counter, inc);
+    sh.obase = old & ((1ull << 33) - 1);
+    sh.gbase = old >> 33;
+  }
+  __syncthreads();
+  const uint64_t obase = sh.obase, gbase = sh.gbase;
+#pragma unroll
+  for (int j = 0; j < SR_E; ++j) {
+    const uint32_t i = p0 + (uint32_t)j;
+    if (i >= m) break;
+    const bool rh = (flags >> j) & 1u;
+    const bool tied = (flags >> (16 + j)) & 1u;
+    if (rh) rmax = i;
+    const uint32_t id = ord[i];
+    const uint64_t p = (uint64_t)sh.val[id];
+    const uint32_t slot = a.J[base + i];
+    if (MODE == 1) {
+      if (!(a.keep_same && sr_head(sh.hmask, rmax))) a.isa[p] = (V)(a.lo + (uint64_t)a.J[base + rmax]);
+    } else if (a.sa) {
+      a.sa[slot] = (V)p;   // (every slot: prefix doubling builds its ISA from this SA)
+    }
+    if (tied) {
+      if (rh) rcnt += 0x10000u;
+      const uint64_t o = obase + (rcnt & 0xFFFFu);
+      const uint64_t g = gbase + (rcnt >> 16) - 1;
+      a.oP[o] = (V)p;
+      a.oJ[o] = slot;
+      a.oG[o] = (uint32_t)g;
+      if (rh) a.head_slot[g] = slot;
+      rcnt += 1;
+    } else {
+      if (MODE == 1) a.sa[slot] = (V)p;
+      a.bwt[slot] = a.t[p == 0 ? a.n - 1 : p - 1];
+    }
+  }
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------- host
+uint64_t sr_plan(Index& ix, const uint32_t* G, uint64_t A, uint64_t groups, uint64_t* big_groups) {
+  hipStream_t s = ix.stream;
+  const uint64_t nw = ceil_div(A, (uint64_t)SR_W);
+  ix.sr_hp.ensure((groups + 1) * 4 + 16);
+  ix.sr_win.ensure(nw * 8 + 16);
+  ix.sr_items.ensure(nw * sizeof(uint2) + 16);
+  ix.sr_cnt.ensure(64);
+  ix.grp_big.ensure(groups + 16);
+  uint32_t* wstart = ix.sr_win.as<uint32_t>();
+  uint32_t* wlast = wstart + nw;
+  HK_HIP(hipMemsetAsync(wstart, 0xFF, nw * 4, s));
+  HK_HIP(hipMemsetAsync(wlast, 0, nw * 4, s));
+  HK_HIP(hipMemsetAsync(ix.grp_big.p, 0, groups, s));
+  HK_HIP(hipMemsetAsync(ix.sr_cnt.p, 0, 32, s));
+  {
+    TimedLaunch tm(ix.timer, "sa_round_plan", (double)A * 8);
+    const unsigned g = (unsigned)std::min<uint64_t>(ceil_div(A, 256), 16384);
+    k_sr_heads<<<g, 256, 0, s>>>(G, A, ix.sr_hp.as<uint32_t>(), wstart, wlast);
+    HK_HIP(hipGetLastError());
+    const unsigned g2 = (unsigned)std::min<uint64_t>(ceil_div(nw, 256), 4096);
+    k_sr_items<<<g2, 256, 0, s>>>(G, ix.sr_hp.as<uint32_t>(), groups, A, wstart, wlast, nw, ix.sr_items.as<uint2>(),
+                                  ix.grp_big.as<uint8_t>(), ix.sr_cnt.as<unsigned long long>());
+    HK_HIP(hipGetLastError());
+  }
+  uint64_t* const rb = ix.rb();
+  HK_HIP(hipMemcpyAsync(&rb[0], ix.sr_cnt.p, 16, hipMemcpyDeviceToHost, s));
+  HK_HIP(hipStreamSynchronize(s));
+  if (big_groups) *big_groups = rb[1];
+  return rb[0];
+}
+
+template <typename V>
+std::pair<uint64_t, uint64_t> sr_items_round(Index& ix, int mode, SrRoundArgs<V> args, uint64_t A, uint64_t tied0,
+                                             uint64_t groups0) {
+  hipStream_t s = ix.stream;
+  const uint64_t nw = ceil_div(A, (uint64_t)SR_W);
+  unsigned long long* ctr = ix.sr_cnt.as<unsigned long long>() + 2;
+  uint64_t* const rb = ix.rb();
+  rb[2] = tied0 | (groups0 << 33);
+  HK_HIP(hipMemcpyAsync(ctr, &rb[2], 8, hipMemcpyHostToDevice, s));
+  args.items = ix.sr_items.as<uint2>();
+  args.counter = ctr;
+  if (nw) {
+    TimedLaunch tm(ix.timer, mode ? "sa_round_dbl" : "sa_round_chunk",
+                   (double)A * (8 + 2 * sizeof(V) + 8 + 4 + 4));
+    if (mode) k_sr_round<V, 1><<<(unsigned)nw, SR_T, 0, s>>>(args);
+    else k_sr_round<V, 0><<<(unsigned)nw, SR_T, 0, s>>>(args);
+    HK_HIP(hipGetLastError());
+  }
+  HK_HIP(hipMemcpyAsync(&rb[3], ctr, 8, hipMemcpyDeviceToHost, s));
+  HK_HIP(hipStreamSynchronize(s));
+  return {rb[3] & ((1ull << 33) - 1), rb[3] >> 33};
+}
+
+template std::pair<uint64_t, uint64_t> sr_items_round<uint32_t>(Index&, int, SrRoundArgs<uint32_t>, uint64_t, uint64_t,
+                                                                 uint64_t);
+template std::pair<uint64_t, uint64_t> sr_items_round<uint64_t>(Index&, int, SrRoundArgs<uint64_t>, uint64_t, uint64_t,
+                                                                 uint64_t);
+
+}  // namespace hk

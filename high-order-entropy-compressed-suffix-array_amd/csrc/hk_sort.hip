@@ -556,16 +556,19 @@ int radix_sort_pairs(SortWork& w, KernelTimer& tm, uint64_t* k[2], V* v[2], int 
   const uint64_t big_elems = 1024 * OS_I;
   const uint64_t tiles = ceil_div(n, tile_elems);
   if (tiles > 0xFFFFFFFFull) throw ApiError{-6, "radix_sort_pairs: too many tiles"};
+  // the lookback status holds 256 granules per tile of the smallest tile this sort launches (1024 x 8 for
+  // the key passes of u64 values)
+  const uint64_t st_tiles = small || sizeof(V) == 4 ? tiles : ceil_div(n, (uint64_t)1024 * OS_I / 2);
 
   w.hist.ensure(9 * 256 * 8);
   w.offs.ensure(8 * 256 * 8);
   w.hpart.ensure(64 * 256 * 8);
   w.counters.ensure(64 * 4);
   w.err.ensure(16);
-  if (tiles > w.status_tiles || !w.status.p) {
-    w.status.ensure(tiles * 256 * 8);
-    HK_HIP(hipMemsetAsync(w.status.p, 0, tiles * 256 * 8, s));
-    w.status_tiles = tiles;
+  if (st_tiles > w.status_tiles || !w.status.p) {
+    w.status.ensure(st_tiles * 256 * 8);
+    HK_HIP(hipMemsetAsync(w.status.p, 0, st_tiles * 256 * 8, s));
+    w.status_tiles = st_tiles;
     w.epoch = 0;
   }
   HK_HIP(hipMemsetAsync(w.counters.p, 0, 64 * 4, s));
@@ -653,6 +656,12 @@ int radix_sort_pairs(SortWork& w, KernelTimer& tm, uint64_t* k[2], V* v[2], int 
               has_next ? bit_lo + 8 * (p + 1) : -1, w.hpart.as<unsigned long long>(), *src);
       } else if (small)
         k_onesweep<V, 256, OS_I, 0><<<(unsigned)tiles, 256, 0, s>>>(
+            k[cur], iota_pending ? nullptr : v[cur], k[nxt], v[nxt], n, (uint32_t)(bit_lo + 8 * p),
+            w.offs.as<uint64_t>() + p * 256, w.status.as<uint64_t>(), w.counters.as<uint32_t>() + p, w.epoch,
+            w.err.as<uint32_t>(), iota_pending ? 1 : 0, has_next ? bit_lo + 8 * (p + 1) : -1,
+            w.hpart.as<unsigned long long>(), TextKeySrc{}, kbias);
+      else if constexpr (sizeof(V) == 8)   // u64 values: 1024 x 8 tiles (1024 x 16 spills 52 B/lane)
+        k_onesweep<V, 1024, OS_I / 2, 0><<<(unsigned)ceil_div(n, big_elems / 2), 1024, 0, s>>>(
             k[cur], iota_pending ? nullptr : v[cur], k[nxt], v[nxt], n, (uint32_t)(bit_lo + 8 * p),
             w.offs.as<uint64_t>() + p * 256, w.status.as<uint64_t>(), w.counters.as<uint32_t>() + p, w.epoch,
             w.err.as<uint32_t>(), iota_pending ? 1 : 0, has_next ? bit_lo + 8 * (p + 1) : -1,

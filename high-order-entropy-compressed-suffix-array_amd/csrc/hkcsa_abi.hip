@@ -3,7 +3,9 @@
 // thread-local message; nothing ever throws across the ABI.
 
 #include <algorithm>
+#include <atomic>
 #include <cstring>
+#include <thread>
 #include <initializer_list>
 #include <memory>
 #include <vector>
@@ -547,15 +549,29 @@ void hkcsa_queries_free(hkcsa_queries* q) { delete q; }
 }  // extern "C"
 
 namespace {
-// Host <-> device copies of the batch calls through the handle's pinned staging, in chunks: the host
-// copy of one chunk overlaps the DMA of the previous one (pageable copies would be staged by the
-// runtime chunk by chunk, synchronously).
+// Host <-> device copies of the batch calls through the handle's pinned staging, in chunks: the host copies
+// run on up to kStageThreads threads (one thread copies pageable memory at ~10 GB/s, well under PCIe), each
+// thread taking its share of every chunk, and the DMA of a chunk overlaps the host copies of the next.
 constexpr uint64_t kStageChunk = 4ull << 20;
+constexpr int kStageThreads = 8;
 struct Seg {
   void* dst;
   const void* src;
   uint64_t bytes;
 };
+struct Piece {   // one chunk: host side (caller buffer), staging offset, bytes, device side
+  uint8_t* host;
+  uint64_t off, c;
+  uint8_t* dev;
+};
+
+int stage_threads(uint64_t tot) { return (int)std::max<uint64_t>(1, std::min<uint64_t>(kStageThreads, tot >> 21)); }
+
+// thread t's share [a, b) of a piece
+inline void share(const Piece& pc, int t, int T, uint64_t& a, uint64_t& b) {
+  a = pc.c * (uint64_t)t / (uint64_t)T & ~63ull;
+  b = t + 1 == T ? pc.c : (pc.c * (uint64_t)(t + 1) / (uint64_t)T & ~63ull);
+}
 
 void staged_h2d(hkcsa_index* h, std::initializer_list<Seg> segs) {
   uint64_t tot = 0;
@@ -564,14 +580,37 @@ void staged_h2d(hkcsa_index* h, std::initializer_list<Seg> segs) {
   h->stage_in.ensure(tot);
   uint8_t* st = h->stage_in.as<uint8_t>();
   hipStream_t s = h->ix.stream;
+  std::vector<Piece> pieces;
   uint64_t off = 0;
   for (const Seg& g : segs)
     for (uint64_t a = 0; a < g.bytes; a += kStageChunk) {
       const uint64_t c = std::min(kStageChunk, g.bytes - a);
-      std::memcpy(st + off, static_cast<const uint8_t*>(g.src) + a, c);
-      HK_HIP(hipMemcpyAsync(static_cast<uint8_t*>(g.dst) + a, st + off, c, hipMemcpyHostToDevice, s));
+      pieces.push_back({const_cast<uint8_t*>(static_cast<const uint8_t*>(g.src)) + a, off, c,
+                        static_cast<uint8_t*>(g.dst) + a});
       off += c;
     }
+  const int T = stage_threads(tot);
+  std::vector<std::atomic<int>> done(pieces.size());
+  for (auto& d : done) d.store(0);
+  auto work = [&](int t) {
+    for (size_t k = 0; k < pieces.size(); ++k) {
+      uint64_t a, b;
+      share(pieces[k], t, T, a, b);
+      if (b > a) std::memcpy(st + pieces[k].off + a, pieces[k].host + a, b - a);
+      done[k].fetch_add(1, std::memory_order_release);
+    }
+  };
+  std::vector<std::thread> th;
+  for (int t = 1; t < T; ++t) th.emplace_back(work, t);
+  work(0);
+  hipError_t err = hipSuccess;
+  for (size_t k = 0; k < pieces.size(); ++k) {
+    while (done[k].load(std::memory_order_acquire) < T) std::this_thread::yield();
+    if (err == hipSuccess)
+      err = hipMemcpyAsync(pieces[k].dev, st + pieces[k].off, pieces[k].c, hipMemcpyHostToDevice, s);
+  }
+  for (auto& x : th) x.join();
+  HK_HIP(err);
 }
 
 // device -> host; returns after every byte has landed in the caller's buffers
@@ -585,26 +624,37 @@ void staged_d2h(hkcsa_index* h, std::initializer_list<Seg> segs) {
   }
   h->stage_out.ensure(tot);
   uint8_t* st = h->stage_out.as<uint8_t>();
-  struct Piece {
-    uint8_t* dst;
-    uint64_t off, c;
-  };
   std::vector<Piece> pieces;
   std::vector<std::unique_ptr<hk::ScopedEvent>> evs;
   uint64_t off = 0;
   for (const Seg& g : segs)
     for (uint64_t a = 0; a < g.bytes; a += kStageChunk) {
       const uint64_t c = std::min(kStageChunk, g.bytes - a);
-      HK_HIP(hipMemcpyAsync(st + off, static_cast<const uint8_t*>(g.src) + a, c, hipMemcpyDeviceToHost, s));
+      uint8_t* dev = const_cast<uint8_t*>(static_cast<const uint8_t*>(g.src)) + a;
+      HK_HIP(hipMemcpyAsync(st + off, dev, c, hipMemcpyDeviceToHost, s));
       evs.emplace_back(new hk::ScopedEvent());
       HK_HIP(hipEventRecord(*evs.back(), s));
-      pieces.push_back({static_cast<uint8_t*>(g.dst) + a, off, c});
+      pieces.push_back({static_cast<uint8_t*>(g.dst) + a, off, c, dev});
       off += c;
     }
-  for (size_t k = 0; k < pieces.size(); ++k) {
-    HK_HIP(hipEventSynchronize(*evs[k]));
-    std::memcpy(pieces[k].dst, st + pieces[k].off, pieces[k].c);
-  }
+  const int T = stage_threads(tot);
+  std::atomic<int> bad{0};
+  auto work = [&](int t) {
+    for (size_t k = 0; k < pieces.size(); ++k) {
+      if (hipEventSynchronize(*evs[k]) != hipSuccess) {
+        bad.store(1);
+        return;
+      }
+      uint64_t a, b;
+      share(pieces[k], t, T, a, b);
+      if (b > a) std::memcpy(pieces[k].host + a, st + pieces[k].off + a, b - a);
+    }
+  };
+  std::vector<std::thread> th;
+  for (int t = 1; t < T; ++t) th.emplace_back(work, t);
+  work(0);
+  for (auto& x : th) x.join();
+  if (bad.load()) HK_HIP(hipStreamSynchronize(s));   // (reports the stream's error)
 }
 
 // the batch calls' query set: the handle's workspace, patterns staged in

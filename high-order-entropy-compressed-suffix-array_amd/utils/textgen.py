@@ -14,6 +14,12 @@ suffixes share prefixes far longer than any fixed key).  english_like() builds s
   copies of earlier stretches (`copy_frac` of all bytes, log-uniform lengths in [min_copy,
   max_copy]), plus `long_copies` copies of 64 KiB - 1 MiB passages: LCPs of 50 symbols to a megabyte.
 
+protein_like() is the shape of the corpus' proteins file (tests/dataset_benchmark.py:13): sequences
+over the 20 amino-acid letters (plus the rare B, Z, X, U, O: sigma = 25) at their natural frequencies,
+one per line, lengths ~ Gamma(mean 350), where a share of the sequences are family members — copies of
+an earlier sequence with point substitutions — and a few are exact duplicates:
+repeats with mismatches every few dozen symbols, so ties break slowly but no prefix runs for megabytes.
+
 Everything is a pure function of (n, seed, parameters): tests and bench.py regenerate the same
 bytes on any host (numpy Generator PCG64, chunked so memory stays O(n)).
 """
@@ -141,6 +147,68 @@ def english_like(n: int, seed: int = 0, copy_frac: float = 0.25, min_copy: int =
         idx = np.where(idx < lim, idx, idx % lim)
         out[O[0]:O[0] + tot] = base[np.minimum(idx, base_n - 1)]
     return out
+
+
+_AMINO = np.frombuffer(b"LAGVESIKRDTPNQFYMHCWXBZUO", dtype=np.uint8)
+_AMINO_P = np.array([9.9, 8.3, 7.1, 6.9, 6.8, 6.6, 5.9, 5.8, 5.5, 5.5, 5.3, 4.7, 4.1, 3.9, 3.9, 2.9, 2.4, 2.3, 1.4,
+                     1.1, 0.08, 0.01, 0.01, 0.005, 0.001])
+
+
+def protein_like(n: int, seed: int = 0, family_frac: float = 0.35, dup_frac: float = 0.05,
+                 mut_rate: float = 0.08) -> np.ndarray:
+    """n bytes (uint8) of seeded protein-database-like text: newline-separated sequences (no '$').
+    Built in batches of sequences: fresh ones drawn at once, family members / duplicates gathered from
+    sequences of earlier batches (a family member then takes point substitutions at `mut_rate`)."""
+    if n <= 0:
+        return np.zeros(0, dtype=np.uint8)
+    rng = np.random.default_rng(seed)
+    # letters by a 2^16-entry table of the cumulative frequencies (every letter keeps at least one entry)
+    cnt = np.maximum(1, np.round(_AMINO_P / _AMINO_P.sum() * 65536)).astype(np.int64)
+    cnt[0] -= int(cnt.sum()) - 65536
+    table = np.repeat(_AMINO, cnt)
+    draw = lambda size: table[rng.integers(0, 65536, size=size, dtype=np.uint32)]
+    out = np.empty(n, dtype=np.uint8)
+    starts = np.zeros(0, dtype=np.int64)   # earlier batches' sequences
+    slens = np.zeros(0, dtype=np.int64)
+    pos = 0
+    while pos < n:
+        K = 1 << 15
+        kind = rng.random(K)
+        lens = np.maximum(20, rng.gamma(2.0, 175.0, size=K)).astype(np.int64)
+        copy = (kind < dup_frac + family_frac) & (len(starts) > 0)
+        src = np.full(K, -1, dtype=np.int64)
+        if len(starts):
+            pick = rng.integers(0, len(starts), size=K)
+            src = np.where(copy, starts[pick], -1)
+            lens = np.where(copy, slens[pick], lens)
+        tl = lens + 1                                        # + the newline
+        st = pos + np.concatenate(([0], np.cumsum(tl)[:-1]))
+        keep = st < n
+        lens, tl, st, src, kind = lens[keep], tl[keep], st[keep], src[keep], kind[keep]
+        tot = int(min(int(tl.sum()), n - pos))
+        seq = np.repeat(np.arange(len(lens)), tl)[:tot]
+        k = np.arange(pos, pos + tot) - st[seq]
+        buf = draw(tot)
+        is_copy = (src[seq] >= 0) & (k < lens[seq])
+        buf[is_copy] = out[src[seq][is_copy] + k[is_copy]]
+        fam = is_copy & (kind[seq] >= dup_frac)
+        mut = fam & (rng.random(tot) < mut_rate)
+        buf[mut] = draw(int(mut.sum()))
+        buf[k == lens[seq]] = 0x0A
+        out[pos:pos + tot] = buf
+        full = st + lens <= pos + tot
+        starts = np.concatenate([starts, st[full]])
+        slens = np.concatenate([slens, lens[full]])
+        pos += tot
+    return out
+
+
+def protein_like_text(n: int, seed: int = 0, **kw) -> np.ndarray:
+    """T' = protein_like(n - 1) + '$'."""
+    t = np.empty(n, dtype=np.uint8)
+    t[:-1] = protein_like(n - 1, seed, **kw)
+    t[-1] = ord("$")
+    return t
 
 
 def english_like_text(n: int, seed: int = 0, **kw) -> np.ndarray:

@@ -107,7 +107,7 @@ def summarize(tag: str) -> dict:
         if "read_gb" in row and "write_gb" in row:
             row["traffic_gb"] = round(row["read_gb"] + row["write_gb"], 4)
             if row["avg_us"]:
-                row["traffic_tbs"] = round(row["traffic_gb"] / row["avg_us"] * 1e3 / 1e3, 3)
+                row["traffic_tbs"] = round(row["traffic_gb"] / row["avg_us"] * 1e3, 3)
         wc = c.get("SQ_WAVE_CYCLES", 0.0)
         waves = c.get("SQ_WAVES", 0.0)
         if dp.get("sq1") and wc:
@@ -138,6 +138,27 @@ def summarize(tag: str) -> dict:
     return res
 
 
+# bench.py timer name -> kernel-name prefix (profiles/pmc_kernels.json feeds roofline.traffic)
+TIMERS = {"sa_bucket_sort": "hk::k_bucket_sort_fast<", "byte_hist": "hk::k_byte_hist", "wt_bits": "hk::k_wt_bits<",
+          "wt_partition": "hk::k_wt_partition<", "radix_part_text": "hk::k_cpart<0,", "radix_part": "hk::k_cpart<2,",
+          "sa_bucket_hist": "hk::k_slice_hist_spans<"}
+
+
+def pmc_json(res: dict, path: str):
+    """profiles/pmc_kernels.json: per bench timer, the HBM bytes per launch of its kernel's largest-grid row."""
+    out = {"note": f"kprof {res['tag']} (bench.py --steps 1 --warmup 0 at 1 GiB sigma=4): per launch of the largest "
+                   "grid, read = 2 x FETCH_SIZE (gfx950 wide-read calibration), write = WRITE_SIZE, KiB -> GB"}
+    for name, pre in TIMERS.items():
+        rows = [r for r in res["kernels"] if r["kernel"].startswith(pre) and "traffic_gb" in r]
+        if not rows:
+            continue
+        r = max(rows, key=lambda x: x["grid"])
+        out[name] = {"kernel": r["kernel"], "read_gb_per_launch": r["read_gb"], "write_gb_per_launch": r["write_gb"],
+                     "traffic_gb_per_launch": r["traffic_gb"], "avg_us": r["avg_us"]}
+    with open(path, "w") as f:
+        json.dump(out, f, indent=1)
+
+
 def main():
     argv = sys.argv[1:]
     cmd = []
@@ -150,6 +171,7 @@ def main():
     ap.add_argument("--filter", default=None, help="kernel regex for the counter passes")
     ap.add_argument("--limit", type=int, default=240, help="seconds per pass")
     ap.add_argument("--summarize-only", action="store_true")
+    ap.add_argument("--pmc-json", default=None, help="also write the bench timers' traffic (profiles/pmc_kernels.json)")
     a = ap.parse_args(argv)
     os.makedirs("gpurun_out", exist_ok=True)
     if not a.summarize_only:
@@ -162,6 +184,8 @@ def main():
                 summarize(a.tag)
                 sys.exit(rc)
     res = summarize(a.tag)
+    if a.pmc_json:
+        pmc_json(res, a.pmc_json)
     for r in res["kernels"][:40]:
         print(json.dumps(r))
 
