@@ -108,8 +108,9 @@ struct Index {
                                     // members of large tied groups of a refinement / doubling round
   DevBuf grp_big;                   // refinement / doubling round: u8 per group, 1 = over SEG_MAX members
                                     // (LDS item rounds: over SR_W members)
-  DevBuf sr_hp, sr_win, sr_items, sr_cnt;   // LDS item rounds (hk_seground.hip): group heads, window
-                                            // first / last heads, items, counters
+  DevBuf sr_hp[2], sr_win[2], sr_items, sr_cnt;   // LDS item rounds (hk_seground.hip): group heads and window
+                                                  // first / last heads of list act[i], items, counters
+  const void* sr_plan_g = nullptr;   // the G buffer whose plan the last round wrote (next round reuses it)
   DevBuf bk_items, bk_hist, bk_fb; // bucket work items, bucket histogram, fast-path fallback items
   DevBuf cp_part, cp_cur, cp_tiles; // cursor partition: per-span counts, destination cursors, pass-B tiles
   HostBuf cp_host;                  // ... and its pinned host side (bucket counts, region table)

@@ -370,80 +370,152 @@ __global__ __launch_bounds__(256) void k_dbl_apply_pairs(const uint64_t* __restr
 
 // ---- ISA of every position at the switch to prefix doubling (single GPU, u32 positions).  ISA[p] = its SA slot,
 // or for a tied suffix its group head's slot.  A straight scatter isa[SA[j]] = v writes 4 B at a random
-// position per suffix, and every such write costs a whole line in HBM (7.2 ms and 6.7 GB of writes for a
-// 200 MiB text).  Instead: hs[j] = the value of slot j (iota, then the tied slots' head slots, near-
-// coalesced along the tie list), one pass partitions (SA[j], hs[j]) into buckets of 2^ISA_SH consecutive
-// positions (bucket b holds exactly the positions [b << ISA_SH, (b + 1) << ISA_SH): no histogram), and a
-// second pass writes each bucket's ISA range from the workgroups of one XCD, so its 2 MiB of ISA lines are
-// completed in that XCD's L2 before they are written back.
-constexpr int ISA_SH = 19;            // 512 Ki positions = 2 MiB of u32 ISA per bucket
-constexpr int ISA_TILE = 256 * 32;    // SA entries per partition tile
-constexpr int ISA_Q = 16;             // workgroups per bucket in the write pass
+// position per suffix, and each such write costs a whole line at the memory side (7.2 ms and 6.7 GB of writes
+// for a 200 MiB text).  Instead: hs[j] = the value of slot j (iota, then the tied slots' head slots, near-
+// coalesced along the tie list); the (SA[j], hs[j]) pairs are partitioned twice by position — into 256
+// level-1 buckets of 2^S1 positions, then inside each into 2^(S1 - S2) sub-buckets of 2^S2 positions — and
+// every sub-bucket's ISA window is assembled in LDS and written whole.  SA is a permutation, so every
+// bucket's size is known without counting: bucket b holds exactly the positions [b << S, (b + 1) << S).
+// Each partition pass stages its tile of pairs in LDS by digit, so the runs it writes are contiguous.
+constexpr int PP_T = 512, PP_I = 16, PP_TILE = PP_T * PP_I;   // partition tiles: 8192 pairs
+constexpr int PW_MAX = 14;                                     // sub-buckets of <= 2^14 positions (64 KiB)
 
 __global__ __launch_bounds__(256) void k_hs_tied(const uint32_t* __restrict__ J, const uint32_t* __restrict__ G,
                                                  uint64_t A, const uint32_t* __restrict__ head_slot,
-                                                 uint32_t* __restrict__ hs) {
-  for (uint64_t a = (uint64_t)blockIdx.x * 256 + threadIdx.x; a < A; a += (uint64_t)gridDim.x * 256)
-    hs[J[a]] = head_slot[G[a]];
-}
-
-__global__ __launch_bounds__(256) void k_isa_part(const uint32_t* __restrict__ sa, const uint32_t* __restrict__ hs,
-                                                  uint64_t n, uint64_t* __restrict__ cursor,
-                                                  uint64_t* __restrict__ pairs) {
-  __shared__ uint32_t cnt[4096];
-  __shared__ uint64_t base[4096];
-  const uint64_t nb = (n + (1ull << ISA_SH) - 1) >> ISA_SH;   // <= 8192 for n < 2^32
-  const uint64_t t0 = (uint64_t)blockIdx.x * ISA_TILE;
-  // LDS counters for 4096 buckets: texts of more than 2^31 positions (up to 8192 buckets) take the tile in
-  // two rounds, buckets [0, 4096) then [4096, 8192)
-  for (uint32_t hi = 0; hi < (uint32_t)((nb + 4095) / 4096); ++hi) {
-    for (uint32_t i = threadIdx.x; i < 4096; i += 256) cnt[i] = 0;
-    __syncthreads();
-    uint32_t slot[32];
-#pragma unroll
-    for (int k = 0; k < 32; ++k) {
-      const uint64_t j = t0 + (uint64_t)k * 256 + threadIdx.x;
-      slot[k] = 0xFFFFFFFFu;
-      if (j < n) {
-        const uint32_t p = sa[j];
-        const uint32_t b = p >> ISA_SH;
-        if ((b >> 12) == hi) slot[k] = atomicAdd(&cnt[b & 4095u], 1u);
-      }
-    }
-    __syncthreads();
-    for (uint32_t i = threadIdx.x; i < 4096; i += 256) {
-      const uint32_t c = cnt[i];
-      if (c) base[i] = atomicAdd((unsigned long long*)&cursor[((uint64_t)hi << 12) + i], (unsigned long long)c);
-    }
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < 32; ++k) {
-      const uint64_t j = t0 + (uint64_t)k * 256 + threadIdx.x;
-      if (slot[k] != 0xFFFFFFFFu) {
-        const uint32_t p = sa[j];
-        pairs[base[(p >> ISA_SH) & 4095u] + slot[k]] = ((uint64_t)p << 32) | hs[j];
-      }
-    }
-    __syncthreads();
+                                                 uint32_t* __restrict__ hs, uint64_t n, uint64_t groups,
+                                                 uint32_t* __restrict__ err) {
+  for (uint64_t a = (uint64_t)blockIdx.x * 256 + threadIdx.x; a < A; a += (uint64_t)gridDim.x * 256) {
+    const uint32_t j = J[a], g = G[a];
+    if (j < n && g < groups) hs[j] = head_slot[g];
+    else atomicOr(err, 1u);
   }
 }
 
-// bucket b is written by the workgroups g with g % 8 == b % 8 (one XCD when workgroups are dealt round-robin
-// to the 8 XCDs — a speed assumption only)
-__global__ __launch_bounds__(256) void k_isa_write(const uint64_t* __restrict__ pairs, uint64_t n,
-                                                   uint32_t* __restrict__ isa) {
-  const uint32_t g = blockIdx.x;
-  const uint32_t x = g & 7u, slotg = g >> 3;
-  const uint64_t b = (uint64_t)x + 8ull * (slotg / ISA_Q);
-  const uint32_t part = slotg % ISA_Q;
-  const uint64_t lo = b << ISA_SH;
-  if (lo >= n) return;
-  const uint64_t len = std::min<uint64_t>(1ull << ISA_SH, n - lo);
-  const uint64_t a0 = lo + len * part / ISA_Q, a1 = lo + len * (part + 1) / ISA_Q;
-  for (uint64_t a = a0 + threadIdx.x; a < a1; a += 256) {
-    const uint64_t pr = pairs[a];
-    isa[pr >> 32] = (uint32_t)pr;
+// cur[i] = i << sh (the cursors of buckets whose sizes are exact powers of two)
+__global__ __launch_bounds__(256) void k_pos_cursors(uint64_t* __restrict__ cur, uint64_t nb, int sh) {
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < nb; i += (uint64_t)gridDim.x * 256)
+    cur[i] = i << sh;
+}
+
+// One partition pass: LEVEL 1 reads (SA[j], hs[j]) over tiles of [0, n) and partitions by p >> s_hi (256
+// digits); LEVEL 2 reads the level-1 pairs over tiles aligned to level-1 buckets (2^s_hi positions, so a tile
+// never straddles two) and partitions by (p >> s_lo) inside the bucket.  The digit's cursor is
+// cur[p >> s_lo] (LEVEL 2) or cur[p >> s_hi] (LEVEL 1).
+template <int LEVEL>
+__global__ __launch_bounds__(PP_T, 2) void k_pos_part(const uint32_t* __restrict__ sa, const uint32_t* __restrict__ hs,
+                                                     const uint64_t* __restrict__ pin, uint64_t n, int s_hi, int s_lo,
+                                                     unsigned long long* __restrict__ cur, uint64_t* __restrict__ pout,
+                                                     uint32_t* __restrict__ err) {
+  __shared__ uint64_t stage[PP_TILE];
+  __shared__ uint32_t cnt[1024], lst[1024];
+  __shared__ unsigned long long gb[1024];
+  __shared__ uint32_t wsum[PP_T / 64];
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int dbits = LEVEL == 1 ? 8 : s_hi - s_lo;   // <= 10
+  const uint32_t nd = 1u << dbits;
+  uint64_t t0, t1;
+  if (LEVEL == 1) {
+    t0 = (uint64_t)blockIdx.x * PP_TILE;
+    t1 = t0 + PP_TILE < n ? t0 + PP_TILE : n;
+  } else {   // tiles per level-1 bucket: 2^s_hi / PP_TILE (s_hi >= 13)
+    const uint64_t tpb = (1ull << s_hi) / PP_TILE;
+    const uint64_t b = blockIdx.x / tpb;
+    t0 = (b << s_hi) + (blockIdx.x % tpb) * PP_TILE;
+    const uint64_t be = ((b + 1) << s_hi) < n ? ((b + 1) << s_hi) : n;
+    t1 = t0 + PP_TILE < be ? t0 + PP_TILE : be;
   }
+  if (t0 >= t1) return;   // (uniform: past the text's last bucket)
+  for (uint32_t i = tid; i < nd; i += PP_T) cnt[i] = 0;
+  __syncthreads();
+  uint64_t pr[PP_I];
+  uint32_t rk[PP_I];
+#pragma unroll
+  for (int k = 0; k < PP_I; ++k) {
+    const uint64_t j = t0 + (uint64_t)k * PP_T + tid;
+    rk[k] = 0;
+    pr[k] = 0;
+    if (j < t1) {
+      pr[k] = LEVEL == 1 ? ((uint64_t)sa[j] << 32) | hs[j] : pin[j];
+      if ((pr[k] >> 32) >= n) {   // (only a corrupt SA: dropped, reported; no write past the pair array)
+        atomicOr(err, 1u);
+        pr[k] = ~0ull;
+        continue;
+      }
+      const uint32_t d = (uint32_t)((pr[k] >> 32) >> (LEVEL == 1 ? s_hi : s_lo)) & (nd - 1);
+      rk[k] = atomicAdd(&cnt[d], 1u);
+    }
+  }
+  __syncthreads();
+  // exclusive digit starts inside the tile (nd <= 1024: two per thread) and the runs' global destinations
+  {
+    uint32_t c0 = tid < nd ? cnt[tid] : 0u, c1 = tid + PP_T < nd ? cnt[tid + PP_T] : 0u;
+    const uint32_t a0 = c0, a1 = c1;
+    const uint32_t i0 = dpp_incl_sum(a0);
+    if (lane == 63) wsum[wv] = i0;
+    __syncthreads();
+    uint32_t carry = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < PP_T / 64; ++w) {
+      carry += (uint32_t)w < wv ? wsum[w] : 0u;
+      tot += wsum[w];
+    }
+    __syncthreads();
+    const uint32_t i1 = dpp_incl_sum(a1);
+    if (lane == 63) wsum[wv] = i1;
+    if (tid < nd) {
+      lst[tid] = carry + i0 - a0;
+      const uint64_t key = LEVEL == 1 ? (uint64_t)tid : (t0 >> s_lo) - ((t0 >> s_lo) & (nd - 1)) + tid;
+      gb[tid] = c0 ? atomicAdd(cur + key, (unsigned long long)c0) : 0ull;
+    }
+    __syncthreads();
+    if (tid + PP_T < nd) {
+      uint32_t carry1 = tot;
+#pragma unroll
+      for (int w = 0; w < PP_T / 64; ++w) carry1 += (uint32_t)w < wv ? wsum[w] : 0u;
+      lst[tid + PP_T] = carry1 + i1 - a1;
+      const uint64_t key = (t0 >> s_lo) - ((t0 >> s_lo) & (nd - 1)) + tid + PP_T;
+      gb[tid + PP_T] = c1 ? atomicAdd(cur + key, (unsigned long long)c1) : 0ull;
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < PP_I; ++k) {
+    const uint64_t j = t0 + (uint64_t)k * PP_T + tid;
+    if (j < t1 && pr[k] != ~0ull) {
+      const uint32_t d = (uint32_t)((pr[k] >> 32) >> (LEVEL == 1 ? s_hi : s_lo)) & (nd - 1);
+      stage[lst[d] + rk[k]] = pr[k];
+    }
+  }
+  __syncthreads();
+  const uint32_t m = lst[nd - 1] + cnt[nd - 1];   // (every kept pair is staged in [0, m))
+#pragma unroll
+  for (int k = 0; k < PP_I; ++k) {
+    const uint32_t sidx = (uint32_t)k * PP_T + tid;
+    if (sidx < m) {
+      const uint64_t q = stage[sidx];
+      const uint32_t d = (uint32_t)((q >> 32) >> (LEVEL == 1 ? s_hi : s_lo)) & (nd - 1);
+      const uint64_t dst = gb[d] + (sidx - lst[d]);
+      if (dst < n) pout[dst] = q;
+      else atomicOr(err, 1u);
+    }
+  }
+}
+
+// one sub-bucket of 2^s_lo positions per workgroup: its pairs (exactly the positions of its range) scattered
+// into an LDS window, written out whole
+__global__ __launch_bounds__(512) void k_pos_write(const uint64_t* __restrict__ pin, uint64_t n, int s_lo,
+                                                   uint32_t* __restrict__ isa, uint32_t* __restrict__ err) {
+  __shared__ uint32_t win[1u << PW_MAX];
+  const uint64_t lo = (uint64_t)blockIdx.x << s_lo;
+  const uint64_t hi = lo + (1ull << s_lo) < n ? lo + (1ull << s_lo) : n;
+  for (uint64_t a = lo + threadIdx.x; a < hi; a += 512) {
+    const uint64_t q = pin[a];
+    const uint64_t o = (q >> 32) - lo;
+    if (o < hi - lo) win[(uint32_t)o] = (uint32_t)q;
+    else atomicOr(err, 1u);
+  }
+  __syncthreads();
+  for (uint64_t a = lo + threadIdx.x; a < hi; a += 512) isa[a] = win[(uint32_t)(a - lo)];
 }
 
 // doubling keys: (dense group ordinal << ib) | (ISA[p + h] + 1, or 0 past the end), value = position
@@ -871,7 +943,11 @@ std::pair<uint64_t, uint64_t> seg_round(Index& ix, const KeyGeom& kg, int mode, 
   uint32_t* oJ = ix.act[cur ^ 1][1].as<uint32_t>();
   uint32_t* oG = ix.act[cur ^ 1][2].as<uint32_t>();
   uint64_t nbg = 0;
-  const uint64_t B = sr_plan(ix, G, A, groups, &nbg);
+  // the previous round wrote this list's group heads and window bounds when it produced this very list
+  const bool ready = ix.sr_plan_g != nullptr && ix.sr_plan_g == ix.act[cur][2].p;
+  ix.sr_plan_g = nullptr;
+  const uint64_t B = sr_plan(ix, cur, G, A, groups, ready, &nbg);
+  sr_next_prepare(ix, cur ^ 1, A);
   std::pair<uint64_t, uint64_t> r0{0, 0};
   if (B) {
     const uint64_t nt = ceil_div(A, GR_TILE);
@@ -905,6 +981,7 @@ std::pair<uint64_t, uint64_t> seg_round(Index& ix, const KeyGeom& kg, int mode, 
                           ix.head_slot.as<uint32_t>());
     else
       r0 = dbl_apply_list<V>(ix, bk[sl], bv[sl], ix.big_j.as<uint32_t>(), B, ib, true, nullptr, oP, oJ, oG);
+    sr_heads(ix, cur ^ 1, oG, 0, r0.first, A, r0.second);   // (the items kernel writes the rest of the plan)
   }
   SrRoundArgs<V> a{};
   a.keys = k0;
@@ -922,7 +999,11 @@ std::pair<uint64_t, uint64_t> seg_round(Index& ix, const KeyGeom& kg, int mode, 
   a.isa = mode ? ix.isa.as<V>() : nullptr;
   a.lo = ix.sharded ? ix.shard_lo : 0;
   a.keep_same = 1;
-  return sr_items_round<V>(ix, mode, a, A, r0.first, r0.second);
+  a.hp_next = ix.sr_hp[cur ^ 1].as<uint32_t>();
+  a.win_next = ix.sr_win[cur ^ 1].as<uint32_t>();
+  const std::pair<uint64_t, uint64_t> r = sr_items_round<V>(ix, mode, a, A, r0.first, r0.second);
+  ix.sr_plan_g = ix.act[cur ^ 1][2].p;
+  return r;
 }
 
 // one doubling round over the active list: keys, sort, regroup.  Single GPU and one-GPU slices: the LDS item
@@ -958,6 +1039,7 @@ void dbl_round_t(Index& ix, uint64_t K) {
     r = seg_round<V>(ix, KeyGeom{}, 1, cur, A, st.groups, gbits + ib, ib);
     st.npairs = 0;
   } else {
+    ix.sr_plan_g = nullptr;
     const bool direct = A >= 4 * st.groups;
     unsigned int* d_big = reinterpret_cast<unsigned int*>(ix.small.as<uint8_t>() + 4356);   // small+4356: flag
     const uint32_t* G = ix.act[cur][2].as<uint32_t>();
@@ -1160,6 +1242,7 @@ void refine_after_sort(Index& ix, const KeyGeom& kg, int slot, uint64_t m, bool 
 template <typename V>
 void refine_loop(Index& ix, const KeyGeom& kg, int cur, uint64_t A, uint64_t groups, bool allow_doubling) {
   hipStream_t s = ix.stream;
+  ix.sr_plan_g = nullptr;   // (the list in act[cur] came from another producer)
   const uint16_t* d_lut = reinterpret_cast<const uint16_t*>(ix.small.as<uint8_t>() + 2048);
   const uint32_t* d_srank = reinterpret_cast<const uint32_t*>(ix.small.as<uint8_t>() + 7168);
   const uint64_t s_start = kg.keyed ? kg.s_start : ~0ull;
@@ -1222,7 +1305,7 @@ void refine_loop(Index& ix, const KeyGeom& kg, int cur, uint64_t A, uint64_t gro
   }
   // single GPU: ISA of every position from the full SA, tied suffixes at their head's slot
   dbl_ensure_isa(ix);
-  if (!ix.sharded && !ix.sa_pos64 && ix.n < 0xFFFFFFFFull) {
+  if (!ix.sharded && !ix.sa_pos64 && ix.n < 0xFFFFFFFFull && ix.n >= (1ull << 16)) {
     dbl_isa_init_single(ix);
   } else {
     dbl_isa_segment(ix, ix.sa.p, ix.n, 0);
@@ -1263,39 +1346,58 @@ void dbl_isa_segment(Index& ix, const void* d_sa, uint64_t count, uint64_t lo) {
   HK_HIP(hipGetLastError());
 }
 
-// ISA at the switch to doubling on one GPU (u32 positions, not sharded): see k_isa_part
+// ISA at the switch to doubling on one GPU (u32 positions, not sharded): see k_pos_part
 void dbl_isa_init_single(Index& ix) {
   const uint64_t n = ix.n;
   hipStream_t s = ix.stream;
   auto& st = ix.dbl;
-  const uint64_t nb = (n + (1ull << ISA_SH) - 1) >> ISA_SH;
   uint32_t* hs = ix.vals[0].as<uint32_t>();   // (free until the first round's keys)
-  uint64_t* pairs = ix.keys[1].as<uint64_t>();
-  std::vector<uint64_t> cur(nb);
-  for (uint64_t b = 0; b < nb; ++b) cur[b] = b << ISA_SH;
-  ix.tile_c.ensure(nb * 8 + 16);
-  HK_HIP(hipMemcpyAsync(ix.tile_c.p, cur.data(), nb * 8, hipMemcpyHostToDevice, s));
+  uint64_t* p1 = ix.keys[1].as<uint64_t>();
+  uint64_t* p2 = ix.keys[0].as<uint64_t>();
+  ix.sr_cnt.ensure(64);
+  uint32_t* err = reinterpret_cast<uint32_t*>(ix.sr_cnt.as<uint8_t>() + 48);
+  HK_HIP(hipMemsetAsync(err, 0, 4, s));
   {
     TimedLaunch tm(ix.timer, "sa_isa_scatter", (double)n * 4 + (double)st.A * 12);
     fill_iota<uint32_t>(hs, n, s);
     if (st.A)
       k_hs_tied<<<grid_for(st.A), 256, 0, s>>>(ix.act[st.cur][1].as<uint32_t>(), ix.act[st.cur][2].as<uint32_t>(), st.A,
-                                                ix.head_slot.as<uint32_t>(), hs);
+                                                ix.head_slot.as<uint32_t>(), hs, n, st.groups, err);
+    HK_HIP(hipGetLastError());
+  }
+  const int lgn = bits_of_u64(n - 1);
+  const int s_hi = std::max(lgn - 8, 13);                    // level-1 buckets (<= 256), >= one tile each
+  const int s_lo = std::max(std::min(s_hi - 1, PW_MAX), s_hi - 10);   // sub-buckets: <= 2^14 positions, <= 1024 per bucket
+  if (s_lo > PW_MAX) throw ApiError{-6, "ISA init: text too long for the position scatter"};
+  const uint64_t nb1 = ceil_div(n, 1ull << s_hi), nb2 = ceil_div(n, 1ull << s_lo);
+  ix.tile_c.ensure(nb2 * 8 + 16);
+  unsigned long long* cur = ix.tile_c.as<unsigned long long>();
+  {
+    TimedLaunch tm(ix.timer, "sa_isa_scatter", (double)n * (4 + 4 + 8));
+    k_pos_cursors<<<(unsigned)std::min<uint64_t>(ceil_div(nb1, 256), 4096), 256, 0, s>>>(
+        reinterpret_cast<uint64_t*>(cur), nb1, s_hi);
+    k_pos_part<1><<<(unsigned)ceil_div(n, PP_TILE), PP_T, 0, s>>>(ix.sa.as<uint32_t>(), hs, nullptr, n, s_hi, s_lo, cur,
+                                                                   p1, err);
     HK_HIP(hipGetLastError());
   }
   {
-    TimedLaunch tm(ix.timer, "sa_isa_scatter", (double)n * (4 + 4 + 8));
-    k_isa_part<<<(unsigned)ceil_div(n, ISA_TILE), 256, 0, s>>>(ix.sa.as<uint32_t>(), hs, n, ix.tile_c.as<uint64_t>(),
-                                                               pairs);
+    TimedLaunch tm(ix.timer, "sa_isa_scatter", (double)n * 16);
+    k_pos_cursors<<<(unsigned)std::min<uint64_t>(ceil_div(nb2, 256), 4096), 256, 0, s>>>(
+        reinterpret_cast<uint64_t*>(cur), nb2, s_lo);
+    const uint64_t tpb = (1ull << s_hi) / PP_TILE;
+    k_pos_part<2><<<(unsigned)(nb1 * tpb), PP_T, 0, s>>>(nullptr, nullptr, p1, n, s_hi, s_lo, cur, p2, err);
     HK_HIP(hipGetLastError());
   }
   {
     TimedLaunch tm(ix.timer, "sa_isa_scatter", (double)n * (8 + 4));
-    const uint64_t rows = ceil_div(nb, 8);
-    k_isa_write<<<(unsigned)(rows * 8 * ISA_Q), 256, 0, s>>>(pairs, n, ix.isa.as<uint32_t>());
+    k_pos_write<<<(unsigned)nb2, 512, 0, s>>>(p2, n, s_lo, ix.isa.as<uint32_t>(), err);
     HK_HIP(hipGetLastError());
   }
-  HK_HIP(hipStreamSynchronize(s));   // (cur)
+  uint64_t* const rb = ix.rb();
+  rb[3] = 0;
+  HK_HIP(hipMemcpyAsync(&rb[3], err, 4, hipMemcpyDeviceToHost, s));
+  HK_HIP(hipStreamSynchronize(s));
+  if ((uint32_t)rb[3]) throw ApiError{-7, "prefix doubling: the SA handed to the ISA scatter is not a permutation"};
 }
 
 void dbl_emit_groups(Index& ix) {
@@ -1540,7 +1642,8 @@ void release_workspace(Index& ix) {
   }
   ix.big_j.release();
   ix.grp_big.release();
-  for (DevBuf* b : {&ix.sr_hp, &ix.sr_win, &ix.sr_items, &ix.sr_cnt}) b->release();
+  for (DevBuf* b : {&ix.sr_hp[0], &ix.sr_hp[1], &ix.sr_win[0], &ix.sr_win[1], &ix.sr_items, &ix.sr_cnt}) b->release();
+  ix.sr_plan_g = nullptr;
   ix.fused.reset();
   ix.fused_recs.release();
   ix.fused_ws.release();

@@ -26,19 +26,20 @@
 namespace hk {
 namespace {
 
-constexpr int SR_T = 256;
-constexpr int SR_E = SR_CAP / SR_T;   // 16 entries per thread
+constexpr int SR_T = 512;
+constexpr int SR_E = SR_CAP / SR_T;   // 8 entries per thread
 constexpr int SR_NW = SR_T / 64;
 constexpr uint32_t SR_NONE = 0xFFFFFFFFu;
 
-// heads: hp[G[a]] = a; first / last head of every window (one atomic pair per wave)
-__global__ __launch_bounds__(256) void k_sr_heads(const uint32_t* __restrict__ G, uint64_t A, uint32_t* __restrict__ hp,
-                                                  uint32_t* __restrict__ wstart, uint32_t* __restrict__ wlast) {
+// heads: hp[G[a]] = a; first / last head of every window w (win[2w], win[2w + 1]; one atomic pair per wave)
+// (over list entries [lo, hi), lo a multiple of 64 — the list's front, or all of it)
+__global__ __launch_bounds__(256) void k_sr_heads(const uint32_t* __restrict__ G, uint64_t lo, uint64_t hi,
+                                                  uint32_t* __restrict__ hp, uint32_t* __restrict__ win) {
   const uint32_t lane = threadIdx.x & 63;
-  for (uint64_t b = (uint64_t)blockIdx.x * 256; b < A; b += (uint64_t)gridDim.x * 256) {   // (uniform)
+  for (uint64_t b = lo + (uint64_t)blockIdx.x * 256; b < hi; b += (uint64_t)gridDim.x * 256) {   // (uniform)
     const uint64_t a = b + threadIdx.x;
     bool head = false;
-    if (a < A) {
+    if (a < hi) {
       const uint32_t g = G[a];
       head = a == 0 || G[a - 1] != g;
       if (head) hp[g] = (uint32_t)a;
@@ -46,8 +47,8 @@ __global__ __launch_bounds__(256) void k_sr_heads(const uint32_t* __restrict__ G
     const uint64_t m = ballot64(head);
     if (m) {   // a wave's 64 entries lie in one window (SR_W is a multiple of 64)
       const uint64_t w0 = (b + (threadIdx.x & ~63u)) / SR_W;
-      if (lane == (uint32_t)__builtin_ctzll(m)) atomicMin(wstart + w0, (uint32_t)a);
-      if (lane == 63u - (uint32_t)__builtin_clzll(m)) atomicMax(wlast + w0, (uint32_t)a);
+      if (lane == (uint32_t)__builtin_ctzll(m)) atomicMin(win + 2 * w0, (uint32_t)a);
+      if (lane == 63u - (uint32_t)__builtin_clzll(m)) atomicMax(win + 2 * w0 + 1, (uint32_t)a);
     }
   }
 }
@@ -55,17 +56,16 @@ __global__ __launch_bounds__(256) void k_sr_heads(const uint32_t* __restrict__ G
 // items[w] = {first entry, entries}; a window's last group of more than SR_W members is big: flagged in
 // gbig, counted (cnt[0] entries, cnt[1] groups) and left out of the item
 __global__ __launch_bounds__(256) void k_sr_items(const uint32_t* __restrict__ G, const uint32_t* __restrict__ hp,
-                                                  uint64_t groups, uint64_t A, const uint32_t* __restrict__ wstart,
-                                                  const uint32_t* __restrict__ wlast, uint64_t nw,
+                                                  uint64_t groups, uint64_t A, const uint32_t* __restrict__ win, uint64_t nw,
                                                   uint2* __restrict__ items, uint8_t* __restrict__ gbig,
                                                   unsigned long long* __restrict__ cnt) {
   for (uint64_t w = (uint64_t)blockIdx.x * 256 + threadIdx.x; w < nw; w += (uint64_t)gridDim.x * 256) {
-    const uint32_t ws = wstart[w];
+    const uint32_t ws = win[2 * w];
     if (ws == SR_NONE) {
       items[w] = make_uint2(0u, 0u);
       continue;
     }
-    const uint32_t wl = wlast[w];
+    const uint32_t wl = win[2 * w + 1];
     const uint32_t g = G[wl];
     const uint64_t end = (uint64_t)g + 1 < groups ? (uint64_t)hp[g + 1] : A;
     uint64_t we = end;
@@ -79,10 +79,9 @@ __global__ __launch_bounds__(256) void k_sr_items(const uint32_t* __restrict__ G
   }
 }
 
-template <typename V>
 struct alignas(16) SrShared {
-  uint64_t key[SR_CAP];             // the item's keys (entry order; the sort permutes idx)
-  V val[SR_CAP];                    // positions
+  uint64_t key[SR_CAP];             // the item's keys (entry order; the sort permutes idx); then per-position
+                                    // regroup records (section 3)
   union {
     uint32_t g[SR_CAP];             // group ordinals, while the head mask is built
     uint16_t idx[2][SR_CAP];        // the order being sorted (entry indexes)
@@ -95,6 +94,7 @@ struct alignas(16) SrShared {
   uint64_t wor[SR_NW], wand[SR_NW];
   uint32_t wbig[SR_NW];
   uint32_t wmax[SR_NW], wcnt[SR_NW];
+  uint32_t nwmin[4], nwmax[4];      // next list: first / last group head of each window this item's chunk touches
   uint64_t obase, gbase;
 };
 
@@ -144,11 +144,14 @@ __device__ __forceinline__ uint32_t sr_next_head(const uint64_t* hm, uint32_t i)
   return (w << 6) + (uint32_t)__builtin_ctzll(b);
 }
 
+// regroup record of a sorted position (section 3): run start, tied index, group index inside the item, flags
+constexpr int RG_TIED = 36, RG_RH = 37, RG_FIRST = 38;
+
 // MODE 0: chunk refinement round (every slot's SA entry written, settled suffixes' BWT); MODE 1: prefix
 // doubling round (ISA of every member = its new group's head slot; SA / BWT of the settled ones)
 template <typename V, int MODE>
-__global__ __launch_bounds__(SR_T, sizeof(V) == 4 ? 2 : 1) void k_sr_round(SrRoundArgs<V> a) {
-  __shared__ SrShared<V> sh;
+__global__ __launch_bounds__(SR_T, 4) void k_sr_round(SrRoundArgs<V> a) {
+  __shared__ SrShared sh;
   const uint2 it = a.items[blockIdx.x];
   const uint32_t m = it.y;
   if (m == 0) return;
@@ -163,11 +166,14 @@ __global__ __launch_bounds__(SR_T, sizeof(V) == 4 ? 2 : 1) void k_sr_round(SrRou
     if (i < m) {
       const uint64_t key = a.keys[base + i];
       sh.key[i] = key;
-      sh.val[i] = a.vals[base + i];
       sh.u.g[i] = a.G[base + i];
       kor |= key;
       kand &= key;
     }
+  }
+  if (tid < 4) {
+    sh.nwmin[tid] = SR_NONE;
+    sh.nwmax[tid] = 0;
   }
   __syncthreads();
   uint32_t big = 0;
@@ -202,14 +208,14 @@ __global__ __launch_bounds__(SR_T, sizeof(V) == 4 ? 2 : 1) void k_sr_round(SrRou
   }
   const uint64_t vary = kor ^ kand;
   int cur = 0;
+#pragma unroll
+  for (int k = 0; k < SR_E; ++k) {   // every entry first takes its own place
+    const uint32_t i = (uint32_t)k * SR_T + tid;
+    if (i < m) sh.u.idx[0][i] = (uint16_t)i;
+  }
 
   // ---- 2. sort the item's groups (entries stay inside their group's range: G is in the keys' top bits)
   if (!big) {
-#pragma unroll
-    for (int k = 0; k < SR_E; ++k) {   // every entry first takes its own place
-      const uint32_t i = (uint32_t)k * SR_T + tid;
-      if (i < m) sh.u.idx[0][i] = (uint16_t)i;
-    }
     __syncthreads();
     for (uint32_t i = tid; i < m; i += SR_T) {
       if (!sr_head(sh.hmask, i)) continue;
@@ -225,18 +231,14 @@ __global__ __launch_bounds__(SR_T, sizeof(V) == 4 ? 2 : 1) void k_sr_round(SrRou
         sr_net<16>(sh.key, sh.u.idx[0], i, sz);
       }
     }
-    __syncthreads();
   } else if (vary) {
     const int lo = __builtin_ctzll(vary), hi = 64 - __builtin_clzll(vary);
-#pragma unroll
-    for (int k = 0; k < SR_E; ++k) {
-      const uint32_t i = (uint32_t)k * SR_T + tid;
-      if (i < m) sh.u.idx[0][i] = (uint16_t)i;
-    }
     for (uint32_t i = tid; i < (uint32_t)SR_NW * 256; i += SR_T) (&sh.mtab[0][0])[i] = 0;
     for (int shf = lo; shf < hi; shf += 8) {
+      if (tid < 256) {
 #pragma unroll
-      for (int w = 0; w < SR_NW; ++w) sh.whist[w][tid] = 0;
+        for (int w = 0; w < SR_NW; ++w) sh.whist[w][tid] = 0;
+      }
       __syncthreads();
       // rank inside the wave (stable: wave-contiguous positions, item-major then lane), as k_onesweep
       uint32_t rk[SR_E];
@@ -255,10 +257,10 @@ __global__ __launch_bounds__(SR_T, sizeof(V) == 4 ? 2 : 1) void k_sr_round(SrRou
           __hip_atomic_store(mt + d, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
           sh.whist[wv][d] = prior + (uint32_t)__popcll(msk);
         }
-        rk[k] = (prior + below) | (d << 11) | (id << 19);   // rank < 1024, digit, entry < 4096
+        rk[k] = (prior + below) | (d << 10) | (id << 18);   // rank < 512, digit, entry < 4096
       }
       __syncthreads();
-      {   // per digit: wave prefixes, then the item-local exclusive start (thread = digit)
+      if (wv < 4) {   // per digit (thread = digit): wave prefixes, then the item-local exclusive start
         uint32_t run = 0;
 #pragma unroll
         for (int w = 0; w < SR_NW; ++w) {
@@ -268,45 +270,40 @@ __global__ __launch_bounds__(SR_T, sizeof(V) == 4 ? 2 : 1) void k_sr_round(SrRou
         }
         const uint32_t inc = dpp_incl_sum(run);
         if (lane == 63) sh.wtot[wv] = inc;
-        __syncthreads();
+        sh.tstart[tid] = inc - run;
+      }
+      __syncthreads();
+      if (wv < 4) {
         uint32_t carry = 0;
 #pragma unroll
-        for (int w = 0; w < SR_NW; ++w) carry += (uint32_t)w < wv ? sh.wtot[w] : 0u;
-        sh.tstart[tid] = carry + inc - run;
+        for (int w = 0; w < 4; ++w) carry += (uint32_t)w < wv ? sh.wtot[w] : 0u;
+        sh.tstart[tid] += carry;
       }
       __syncthreads();
 #pragma unroll
       for (int k = 0; k < SR_E; ++k) {
         const uint32_t pos = wv * (SR_E * 64) + (uint32_t)k * 64 + lane;
         if (pos < m) {
-          const uint32_t d = (rk[k] >> 11) & 255u;
-          sh.u.idx[cur ^ 1][sh.tstart[d] + sh.whist[wv][d] + (rk[k] & 2047u)] = (uint16_t)(rk[k] >> 19);
+          const uint32_t d = (rk[k] >> 10) & 255u;
+          sh.u.idx[cur ^ 1][sh.tstart[d] + sh.whist[wv][d] + (rk[k] & 1023u)] = (uint16_t)(rk[k] >> 18);
         }
       }
-      __syncthreads();
+      __syncthreads();   // (the next pass resets whist / tstart and reads this order)
       cur ^= 1;
     }
-  } else {   // every key equal: one group, one tied run, order kept
-#pragma unroll
-    for (int k = 0; k < SR_E; ++k) {
-      const uint32_t i = (uint32_t)k * SR_T + tid;
-      if (i < m) sh.u.idx[0][i] = (uint16_t)i;
-    }
-    __syncthreads();
   }
+  __syncthreads();
   const uint16_t* const ord = sh.u.idx[cur];
 
-  // ---- 3. regroup (blocked: thread tid owns positions [tid * SR_E, tid * SR_E + SR_E))
+  // ---- 3. regroup.  (a) blocked (thread tid owns positions [tid * SR_E, tid * SR_E + SR_E)): run heads, tied
+  // flags and the item-wide scans (max of run-head positions, tied | tied heads << 16); (b) the per-position
+  // regroup records into the key plane; (c) striped: every global access coalesced across the wave
   const uint32_t p0 = tid * SR_E;
   uint32_t flags = 0;          // bit j: run head at p0 + j; bit 16 + j: tied
   uint32_t lmax = 0, lcnt = 0;
   {
-    uint64_t prev = 0;
-    bool have_prev = false;
-    if (p0 > 0 && p0 < m) {
-      prev = sh.key[ord[p0 - 1]];
-      have_prev = true;
-    }
+    uint64_t prev = p0 > 0 && p0 < m ? sh.key[ord[p0 - 1]] : 0;
+    bool have_prev = p0 > 0 && p0 < m;
     uint64_t kc = p0 < m ? sh.key[ord[p0]] : 0;
 #pragma unroll
     for (int j = 0; j < SR_E; ++j) {
@@ -330,14 +327,13 @@ __global__ __launch_bounds__(SR_T, sizeof(V) == 4 ? 2 : 1) void k_sr_round(SrRou
       }
     }
   }
-  // item-wide exclusive scans of the threads' aggregates: max of run-head positions, tied | heads << 16
   const uint32_t imax = dpp_scan_u32(lmax, 0u, [](uint32_t x, uint32_t y) { return x > y ? x : y; });
   const uint32_t icnt = dpp_incl_sum(lcnt);
   if (lane == 63) {
     sh.wmax[wv] = imax;
     sh.wcnt[wv] = icnt;
   }
-  __syncthreads();
+  __syncthreads();   // (also: every read of the key plane is done)
   uint32_t cmax = 0, ccnt = 0, tcnt = 0;
 #pragma unroll
   for (int w = 0; w < SR_NW; ++w) {
@@ -347,11 +343,24 @@ __global__ __launch_bounds__(SR_T, sizeof(V) == 4 ? 2 : 1) void k_sr_round(SrRou
     }
     tcnt += sh.wcnt[w];
   }
-  // exclusive within the wave: the previous lane's inclusive value
-  const uint32_t pmax_w = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)imax, 0x138, 0xf, 0xf, false);   // wave_shr:1
+  // exclusive within the wave: the previous lane's inclusive value (wave_shr:1)
+  const uint32_t pmax_w = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)imax, 0x138, 0xf, 0xf, false);
   const uint32_t pcnt_w = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)icnt, 0x138, 0xf, 0xf, false);
   uint32_t rmax = cmax > pmax_w ? cmax : pmax_w;
   uint32_t rcnt = ccnt + pcnt_w;
+#pragma unroll
+  for (int j = 0; j < SR_E; ++j) {
+    const uint32_t i = p0 + (uint32_t)j;
+    if (i >= m) break;
+    const bool rh = (flags >> j) & 1u;
+    const bool tied = (flags >> (16 + j)) & 1u;
+    if (rh) rmax = i;
+    if (tied && rh) rcnt += 0x10000u;
+    // run start | tied index | group index inside the item | tied | run head | run starts its group
+    sh.key[i] = (uint64_t)rmax | ((uint64_t)(rcnt & 0xFFFFu) << 12) | ((uint64_t)((rcnt >> 16) - (tied ? 1u : 0u)) << 24) |
+                ((uint64_t)tied << RG_TIED) | ((uint64_t)rh << RG_RH) | ((uint64_t)sr_head(sh.hmask, rmax) << RG_FIRST);
+    if (tied) rcnt += 1;
+  }
   if (tid == 0) {
     const unsigned long long inc = (unsigned long long)(tcnt & 0xFFFFu) |
                                    ((unsigned long long)(tcnt >> 16) << 33);
@@ -361,33 +370,47 @@ __global__ __launch_bounds__(SR_T, sizeof(V) == 4 ? 2 : 1) void k_sr_round(SrRou
   }
   __syncthreads();
   const uint64_t obase = sh.obase, gbase = sh.gbase;
+  const uint64_t w0 = obase / SR_W;
 #pragma unroll
-  for (int j = 0; j < SR_E; ++j) {
-    const uint32_t i = p0 + (uint32_t)j;
-    if (i >= m) break;
-    const bool rh = (flags >> j) & 1u;
-    const bool tied = (flags >> (16 + j)) & 1u;
-    if (rh) rmax = i;
-    const uint32_t id = ord[i];
-    const uint64_t p = (uint64_t)sh.val[id];
-    const uint32_t slot = a.J[base + i];
-    if (MODE == 1) {
-      if (!(a.keep_same && sr_head(sh.hmask, rmax))) a.isa[p] = (V)(a.lo + (uint64_t)a.J[base + rmax]);
-    } else if (a.sa) {
-      a.sa[slot] = (V)p;   // (every slot: prefix doubling builds its ISA from this SA)
+  for (int k = 0; k < SR_E; ++k) {
+    const uint32_t i = (uint32_t)k * SR_T + tid;
+    if (i < m) {
+      const uint64_t r = sh.key[i];
+      const uint32_t rs = (uint32_t)r & 0xFFFu;
+      const bool tied = (r >> RG_TIED) & 1u, rh = (r >> RG_RH) & 1u;
+      const uint64_t p = (uint64_t)a.vals[base + ord[i]];
+      const uint32_t slot = a.J[base + i];
+      if (MODE == 1) {
+        if (!(a.keep_same && ((r >> RG_FIRST) & 1u))) a.isa[p] = (V)(a.lo + (uint64_t)a.J[base + rs]);
+      } else if (a.sa) {
+        a.sa[slot] = (V)p;   // (every slot: prefix doubling builds its ISA from this SA)
+      }
+      if (tied) {
+        const uint64_t o = obase + ((r >> 12) & 0xFFFu);
+        const uint64_t g = gbase + ((r >> 24) & 0xFFFu);
+        a.oP[o] = (V)p;
+        a.oJ[o] = slot;
+        a.oG[o] = (uint32_t)g;
+        if (rh) {
+          a.head_slot[g] = slot;
+          if (a.hp_next) {   // the next round's plan: this group's head, the windows' first / last heads
+            a.hp_next[g] = (uint32_t)o;
+            const uint32_t wl = (uint32_t)(o / SR_W - w0);
+            atomicMin(&sh.nwmin[wl], (uint32_t)o);
+            atomicMax(&sh.nwmax[wl], (uint32_t)o);
+          }
+        }
+      } else {
+        if (MODE == 1) a.sa[slot] = (V)p;
+        a.bwt[slot] = a.t[p == 0 ? a.n - 1 : p - 1];
+      }
     }
-    if (tied) {
-      if (rh) rcnt += 0x10000u;
-      const uint64_t o = obase + (rcnt & 0xFFFFu);
-      const uint64_t g = gbase + (rcnt >> 16) - 1;
-      a.oP[o] = (V)p;
-      a.oJ[o] = slot;
-      a.oG[o] = (uint32_t)g;
-      if (rh) a.head_slot[g] = slot;
-      rcnt += 1;
-    } else {
-      if (MODE == 1) a.sa[slot] = (V)p;
-      a.bwt[slot] = a.t[p == 0 ? a.n - 1 : p - 1];
+  }
+  if (a.hp_next) {
+    __syncthreads();
+    if (tid < 4 && sh.nwmin[tid] != SR_NONE) {
+      atomicMin(a.win_next + 2 * (w0 + tid), sh.nwmin[tid]);
+      atomicMax(a.win_next + 2 * (w0 + tid) + 1, sh.nwmax[tid]);
     }
   }
 }
@@ -395,28 +418,51 @@ __global__ __launch_bounds__(SR_T, sizeof(V) == 4 ? 2 : 1) void k_sr_round(SrRou
 }  // namespace
 
 // ---------------------------------------------------------------- host
-uint64_t sr_plan(Index& ix, const uint32_t* G, uint64_t A, uint64_t groups, uint64_t* big_groups) {
+namespace {
+// window bounds of a list of up to A entries: {first head (none: ~0), last head} per window
+__global__ __launch_bounds__(256) void k_sr_win_reset(uint2* __restrict__ win, uint64_t nw) {
+  for (uint64_t w = (uint64_t)blockIdx.x * 256 + threadIdx.x; w < nw; w += (uint64_t)gridDim.x * 256)
+    win[w] = make_uint2(SR_NONE, 0u);
+}
+}  // namespace
+
+static void sr_windows_reset(Index& ix, int slot, uint64_t A) {
+  const uint64_t nw = ceil_div(A, (uint64_t)SR_W);
+  ix.sr_win[slot].ensure(nw * 8 + 16);
+  if (!nw) return;
+  k_sr_win_reset<<<(unsigned)std::min<uint64_t>(ceil_div(nw, 256), 4096), 256, 0, ix.stream>>>(
+      ix.sr_win[slot].as<uint2>(), nw);
+  HK_HIP(hipGetLastError());
+}
+
+void sr_heads(Index& ix, int slot, const uint32_t* G, uint64_t lo, uint64_t hi, uint64_t A, uint64_t groups) {
+  if (hi <= lo) return;
+  ix.sr_hp[slot].ensure((groups + 1) * 4 + 16);
+  TimedLaunch tm(ix.timer, "sa_round_plan", (double)(hi - lo) * 8);
+  const unsigned g = (unsigned)std::min<uint64_t>(ceil_div(hi - lo, 256), 16384);
+  k_sr_heads<<<g, 256, 0, ix.stream>>>(G, lo, hi, ix.sr_hp[slot].as<uint32_t>(), ix.sr_win[slot].as<uint32_t>());
+  HK_HIP(hipGetLastError());
+}
+
+uint64_t sr_plan(Index& ix, int slot, const uint32_t* G, uint64_t A, uint64_t groups, bool heads_ready,
+                 uint64_t* big_groups) {
   hipStream_t s = ix.stream;
   const uint64_t nw = ceil_div(A, (uint64_t)SR_W);
-  ix.sr_hp.ensure((groups + 1) * 4 + 16);
-  ix.sr_win.ensure(nw * 8 + 16);
+  ix.sr_hp[slot].ensure((groups + 1) * 4 + 16);
   ix.sr_items.ensure(nw * sizeof(uint2) + 16);
   ix.sr_cnt.ensure(64);
   ix.grp_big.ensure(groups + 16);
-  uint32_t* wstart = ix.sr_win.as<uint32_t>();
-  uint32_t* wlast = wstart + nw;
-  HK_HIP(hipMemsetAsync(wstart, 0xFF, nw * 4, s));
-  HK_HIP(hipMemsetAsync(wlast, 0, nw * 4, s));
+  if (!heads_ready) {
+    sr_windows_reset(ix, slot, A);
+    sr_heads(ix, slot, G, 0, A, A, groups);
+  }
   HK_HIP(hipMemsetAsync(ix.grp_big.p, 0, groups, s));
   HK_HIP(hipMemsetAsync(ix.sr_cnt.p, 0, 32, s));
   {
-    TimedLaunch tm(ix.timer, "sa_round_plan", (double)A * 8);
-    const unsigned g = (unsigned)std::min<uint64_t>(ceil_div(A, 256), 16384);
-    k_sr_heads<<<g, 256, 0, s>>>(G, A, ix.sr_hp.as<uint32_t>(), wstart, wlast);
-    HK_HIP(hipGetLastError());
+    TimedLaunch tm(ix.timer, "sa_round_plan", (double)nw * 16);
     const unsigned g2 = (unsigned)std::min<uint64_t>(ceil_div(nw, 256), 4096);
-    k_sr_items<<<g2, 256, 0, s>>>(G, ix.sr_hp.as<uint32_t>(), groups, A, wstart, wlast, nw, ix.sr_items.as<uint2>(),
-                                  ix.grp_big.as<uint8_t>(), ix.sr_cnt.as<unsigned long long>());
+    k_sr_items<<<g2, 256, 0, s>>>(G, ix.sr_hp[slot].as<uint32_t>(), groups, A, ix.sr_win[slot].as<uint32_t>(), nw,
+                                  ix.sr_items.as<uint2>(), ix.grp_big.as<uint8_t>(), ix.sr_cnt.as<unsigned long long>());
     HK_HIP(hipGetLastError());
   }
   uint64_t* const rb = ix.rb();
@@ -424,6 +470,11 @@ uint64_t sr_plan(Index& ix, const uint32_t* G, uint64_t A, uint64_t groups, uint
   HK_HIP(hipStreamSynchronize(s));
   if (big_groups) *big_groups = rb[1];
   return rb[0];
+}
+
+void sr_next_prepare(Index& ix, int slot, uint64_t A) {
+  ix.sr_hp[slot].ensure((A / 2 + 8) * 4 + 16);   // (the next list has at most A / 2 groups)
+  sr_windows_reset(ix, slot, A);
 }
 
 template <typename V>

@@ -30,11 +30,19 @@ struct SrRoundArgs {
   V* isa;                  // doubling: ISA (single GPU or one-GPU slices; global slot = lo + slot)
   uint64_t lo;
   int keep_same;           // doubling: skip the ISA entries a round leaves unchanged
+  uint32_t* hp_next;       // (nullable) the next round's plan: head entry of every new group, and
+  uint32_t* win_next;      //   every window's {first, last} head entry (sr_next_prepare resets them)
 };
 
-// Windows, items and big groups of a list of A entries in `groups` groups: ix.sr_items, ix.grp_big (u8 per
-// group, 1 = big).  Returns the entries in big groups (*big_groups: their number).
-uint64_t sr_plan(Index& ix, const uint32_t* G, uint64_t A, uint64_t groups, uint64_t* big_groups);
+// Windows, items and big groups of list `slot` (A entries in `groups` groups): ix.sr_items, ix.grp_big (u8 per
+// group, 1 = big).  heads_ready: the previous round already wrote the list's group heads and window bounds
+// (ix.sr_hp[slot], ix.sr_win[slot]).  Returns the entries in big groups (*big_groups: their number).
+uint64_t sr_plan(Index& ix, int slot, const uint32_t* G, uint64_t A, uint64_t groups, bool heads_ready,
+                 uint64_t* big_groups);
+// the next list's plan buffers, reset before the round writes them (A: the current list's entries)
+void sr_next_prepare(Index& ix, int slot, uint64_t A);
+// group heads + window bounds of list entries [lo, hi) (lo a multiple of 64), into list `slot`'s plan
+void sr_heads(Index& ix, int slot, const uint32_t* G, uint64_t lo, uint64_t hi, uint64_t A, uint64_t groups);
 
 // The LDS items of the round (mode 0: chunk refinement, 1: doubling); the next list already holds tied0
 // entries in groups0 groups (the big groups').  Returns the next list's (entries, groups).
