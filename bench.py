@@ -212,7 +212,7 @@ BUILD_STAGES = ["byte_hist", "sa_bucket_hist", "radix_part_text", "radix_part_ke
                 "sa_bucket_sort", "sa_big_gather", "radix_onesweep_text", "radix_table_text", "radix_tile_hist", "radix_hist", "radix_onesweep",
                 "radix_onesweep_small", "sa_pack_keys", "sa_refine_stats", "sa_refine_apply", "sa_refine_keys", "sa_refine_segsort",
                 "sa_isa_scatter", "sa_group_stats", "sa_group_apply", "sa_pair_keys", "sa_pair_segsort", "sa_big_groups",
-                "sa_round_plan", "sa_round_chunk", "sa_round_dbl", "bwt_gather"]
+                "sa_round_plan", "sa_round_chunk", "sa_round_dbl", "sa_link", "bwt_gather"]
 SHARD_STAGES = ["shard_hist", "shard_below", "shard_slice_hist", "shard_slice_part", "shard_select_count",
                 "shard_pack_select", "rccl_allreduce_bytes",
                 "rccl_allreduce_hist",
@@ -496,7 +496,7 @@ def english_leg(args) -> dict:
     refine = ("sa_refine_stats", "sa_refine_apply", "sa_refine_keys", "sa_refine_segsort", "radix_onesweep_small",
               "radix_hist", "radix_onesweep", "sa_round_chunk")
     dbl = ("sa_isa_scatter", "sa_pair_keys", "sa_pair_segsort", "sa_group_stats", "sa_group_apply", "sa_round_dbl",
-           "sa_round_plan", "sa_big_groups")
+           "sa_round_plan", "sa_big_groups", "sa_link")
     per = lambda names: round(sum(stages.get(k, {}).get("ms", 0.0) for k in names) / args.leg_steps, 3)
     log(f"[bench] english-like leg: {wall / args.leg_steps * 1e3:.2f} ms/step, refinement {per(refine)} ms, "
         f"doubling {per(dbl)} ms, count {qq['count_patterns_per_s']:.3g} patterns/s")

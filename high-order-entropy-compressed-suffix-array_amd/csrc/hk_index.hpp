@@ -16,6 +16,8 @@ constexpr uint32_t kFlagGlobalSort = 4u; // full LSD sort of the keys (no bucket
 constexpr uint32_t kFlagMulBins = 8u;    // sharded slices: force multiplicative bucket bins
 constexpr uint32_t kFlagMaxBuckets = 16u; // single GPU: the most bucket bits at any n (diagnostic)
 constexpr uint32_t kFlagSlices = 32u;     // single GPU: the multi-slice build at any n (4 slices; parity tests)
+constexpr uint32_t kFlagLinks = 64u;      // single GPU: doubling links at any tie count (parity tests)
+constexpr uint32_t kFlagNoLinks = 128u;   // single GPU: no doubling links (diagnostic)
 constexpr int kLineBits = 448;   // 7 data words per 64-B rank line (word 0 = ones before the line)
 
 struct WtTables {                // per level, per dense code (host mirror of the device tables)
@@ -111,6 +113,9 @@ struct Index {
   DevBuf sr_hp[2], sr_win[2], sr_items, sr_cnt;   // LDS item rounds (hk_seground.hip): group heads and window
                                                   // first / last heads of list act[i], items, counters
   const void* sr_plan_g = nullptr;   // the G buffer whose plan the last round wrote (next round reuses it)
+  DevBuf lk_lnk, lk_gsz, lk_tops, lk_grec;   // doubling links (hk_seground.hip): per position {offset, slot delta},
+                                             // the size of the tied group at each head slot, the link tiles' tops,
+                                             // the linked groups {head slot, size, head position}
   DevBuf bk_items, bk_hist, bk_fb; // bucket work items, bucket histogram, fast-path fallback items
   DevBuf cp_part, cp_cur, cp_tiles; // cursor partition: per-span counts, destination cursors, pass-B tiles
   HostBuf cp_host;                  // ... and its pinned host side (bucket counts, region table)
@@ -171,6 +176,10 @@ struct Index {
     uint64_t npairs = 0;       // pairs in upd from the last step
     bool pending = false;
     bool big = false;          // a round had a group over SEG_MAX members: the next ones sort the list at once
+    bool link = false;         // one GPU, n < 2^31: groups that map whole onto one tied group are linked (hk_seground)
+    uint64_t nlinked = 0;      // linked positions
+    uint32_t ltag = 0;         // the current round's link tag
+    std::vector<uint64_t> lround;   // linked groups recorded up to each linking round
   } dbl;
   DevBuf upd;
 

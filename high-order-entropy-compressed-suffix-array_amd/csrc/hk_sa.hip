@@ -377,7 +377,8 @@ __global__ __launch_bounds__(256) void k_dbl_apply_pairs(const uint64_t* __restr
 // every sub-bucket's ISA window is assembled in LDS and written whole.  SA is a permutation, so every
 // bucket's size is known without counting: bucket b holds exactly the positions [b << S, (b + 1) << S).
 // Each partition pass stages its tile of pairs in LDS by digit, so the runs it writes are contiguous.
-constexpr int PP_T = 512, PP_I = 16, PP_TILE = PP_T * PP_I;   // partition tiles: 8192 pairs
+constexpr int PP_T = 512, PP_I = 8, PP_TILE = PP_T * PP_I;    // partition tiles: 4096 pairs (48 KiB of LDS:
+                                                               // three workgroups per CU)
 constexpr int PW_MAX = 14;                                     // sub-buckets of <= 2^14 positions (64 KiB)
 
 __global__ __launch_bounds__(256) void k_hs_tied(const uint32_t* __restrict__ J, const uint32_t* __restrict__ G,
@@ -402,7 +403,7 @@ __global__ __launch_bounds__(256) void k_pos_cursors(uint64_t* __restrict__ cur,
 // never straddles two) and partitions by (p >> s_lo) inside the bucket.  The digit's cursor is
 // cur[p >> s_lo] (LEVEL 2) or cur[p >> s_hi] (LEVEL 1).
 template <int LEVEL>
-__global__ __launch_bounds__(PP_T, 2) void k_pos_part(const uint32_t* __restrict__ sa, const uint32_t* __restrict__ hs,
+__global__ __launch_bounds__(PP_T, 3) void k_pos_part(const uint32_t* __restrict__ sa, const uint32_t* __restrict__ hs,
                                                      const uint64_t* __restrict__ pin, uint64_t n, int s_hi, int s_lo,
                                                      unsigned long long* __restrict__ cur, uint64_t* __restrict__ pout,
                                                      uint32_t* __restrict__ err) {
@@ -417,7 +418,7 @@ __global__ __launch_bounds__(PP_T, 2) void k_pos_part(const uint32_t* __restrict
   if (LEVEL == 1) {
     t0 = (uint64_t)blockIdx.x * PP_TILE;
     t1 = t0 + PP_TILE < n ? t0 + PP_TILE : n;
-  } else {   // tiles per level-1 bucket: 2^s_hi / PP_TILE (s_hi >= 13)
+  } else {   // tiles per level-1 bucket: 2^s_hi / PP_TILE (s_hi >= 13 > log2(PP_TILE))
     const uint64_t tpb = (1ull << s_hi) / PP_TILE;
     const uint64_t b = blockIdx.x / tpb;
     t0 = (b << s_hi) + (blockIdx.x % tpb) * PP_TILE;
@@ -518,15 +519,28 @@ __global__ __launch_bounds__(512) void k_pos_write(const uint64_t* __restrict__ 
   for (uint64_t a = lo + threadIdx.x; a < hi; a += 512) isa[a] = win[(uint32_t)(a - lo)];
 }
 
-// doubling keys: (dense group ordinal << ib) | (ISA[p + h] + 1, or 0 past the end), value = position
+// doubling keys: (dense group ordinal << ib) | (ISA[p + h] + 1, or 0 past the end), value = position.  A linked
+// position's ISA is that of the position its link names plus the link's slot delta (hk_seground.hpp)
 template <typename V>
 __global__ __launch_bounds__(256) void k_dbl_keys(const V* __restrict__ P, const uint32_t* __restrict__ G, uint64_t A,
                                                   const V* __restrict__ isa, uint64_t n, uint64_t h, int ib,
-                                                  uint64_t* __restrict__ keys, V* __restrict__ vals) {
+                                                  uint64_t* __restrict__ keys, V* __restrict__ vals,
+                                                  const uint64_t* __restrict__ lnk) {
   for (uint64_t a = (uint64_t)blockIdx.x * 256 + threadIdx.x; a < A; a += (uint64_t)gridDim.x * 256) {
     const V p = P[a];
     const uint64_t q = (uint64_t)p + h;
-    const uint64_t s = q < n ? (uint64_t)isa[q] + 1 : 0;
+    uint64_t s = 0;
+    if (q < n) {
+      V v = isa[q];
+      if constexpr (sizeof(V) == 4) {
+        if (lnk && (v & LK_BIT)) {
+          const uint64_t l = lnk[q];
+          const uint64_t e = q + (l >> 32);
+          v = e < n ? isa[e] + (uint32_t)l : 0;   // (e < n always: a link names a position of its target group)
+        }
+      }
+      s = (uint64_t)v + 1;
+    }
     keys[a] = ((uint64_t)G[a] << ib) | s;
     vals[a] = p;
   }
@@ -948,6 +962,10 @@ std::pair<uint64_t, uint64_t> seg_round(Index& ix, const KeyGeom& kg, int mode, 
   ix.sr_plan_g = nullptr;
   const uint64_t B = sr_plan(ix, cur, G, A, groups, ready, &nbg);
   sr_next_prepare(ix, cur ^ 1, A);
+  // links in the first doubling round only: every chain then runs through groups of that one round, so a linked
+  // group's members share their chain (the group copy of lk_resolve relies on it); later rounds link far less
+  const bool link = mode == 1 && ix.dbl.link && sizeof(V) == 4 && ix.dbl.ltag == 0;
+  if (link) lk_sizes(ix, cur, A, groups);   // (before the big groups' apply rewrites head_slot)
   std::pair<uint64_t, uint64_t> r0{0, 0};
   if (B) {
     const uint64_t nt = ceil_div(A, GR_TILE);
@@ -1001,8 +1019,17 @@ std::pair<uint64_t, uint64_t> seg_round(Index& ix, const KeyGeom& kg, int mode, 
   a.keep_same = 1;
   a.hp_next = ix.sr_hp[cur ^ 1].as<uint32_t>();
   a.win_next = ix.sr_win[cur ^ 1].as<uint32_t>();
-  const std::pair<uint64_t, uint64_t> r = sr_items_round<V>(ix, mode, a, A, r0.first, r0.second);
+  uint64_t linked = 0;
+  if (link) {
+    a.lnk = ix.lk_lnk.as<uint64_t>();
+    a.gsz = ix.lk_gsz.as<uint32_t>();
+    a.h = (uint32_t)ix.dbl.h;
+    a.ltag = ++ix.dbl.ltag;
+    a.ib = ib;
+  }
+  const std::pair<uint64_t, uint64_t> r = sr_items_round<V>(ix, mode, a, A, r0.first, r0.second, &linked);
   ix.sr_plan_g = ix.act[cur ^ 1][2].p;
+  if (link) lk_after_round(ix, linked, (uint32_t)ix.dbl.h);
   return r;
 }
 
@@ -1030,7 +1057,8 @@ void dbl_round_t(Index& ix, uint64_t K) {
   {
     TimedLaunch tm(ix.timer, "sa_pair_keys", (double)A * (2 * sizeof(V) + 4 + 8 + sizeof(V)));
     k_dbl_keys<V><<<grid_for(A), 256, 0, s>>>(ix.act[cur][0].as<V>(), ix.act[cur][2].as<uint32_t>(), A,
-                                              ix.isa.as<V>(), ix.n, st.h, ib, kp[0], vp[0]);
+                                              ix.isa.as<V>(), ix.n, st.h, ib, kp[0], vp[0],
+                                              st.link ? ix.lk_lnk.as<uint64_t>() : nullptr);
     HK_HIP(hipGetLastError());
   }
   std::pair<uint64_t, uint64_t> r{0, 0};
@@ -1255,11 +1283,12 @@ void refine_loop(Index& ix, const KeyGeom& kg, int cur, uint64_t A, uint64_t gro
   const bool local_dbl = allow_doubling || ix.slices_local;   // doubling needs no rank exchange here
   const uint64_t m_all = ix.sharded ? ix.shard_hi - ix.shard_lo : ix.n;
   while (A > 0 && rounds < kChunkRounds) {
-    // after the first chunk round (it also places the short suffixes), a round that settled under a fifth
+    // after the first chunk round (it also places the short suffixes), a round that settled under two fifths
     // of its tied suffixes, or a list still holding over a quarter of all suffixes (natural-language text:
     // 108M of 200M), hands over to prefix doubling: a doubling round doubles the compared prefix for one
-    // ISA gather per suffix, a chunk round reads the next chunk of T' per suffix
-    if (local_dbl && rounds > 0 && (A * 5 > A_prev * 4 || A > m_all / 4)) break;
+    // ISA gather per suffix, a chunk round reads the next chunk of T' per suffix (1 GiB protein-like text:
+    // handing over after one chunk round instead of four, 142.5 -> 134.1 ms per build)
+    if (local_dbl && rounds > 0 && (A * 5 > A_prev * 3 || A > m_all / 4)) break;
     int gbits = 0;
     while (gbits < 64 && (1ull << gbits) < groups) ++gbits;
     auto fits = [&](int qq) {   // G in the top gbits, chunk + nS (<= R^qq - 1 + nS) below
@@ -1307,6 +1336,12 @@ void refine_loop(Index& ix, const KeyGeom& kg, int cur, uint64_t A, uint64_t gro
   dbl_ensure_isa(ix);
   if (!ix.sharded && !ix.sa_pos64 && ix.n < 0xFFFFFFFFull && ix.n >= (1ull << 16)) {
     dbl_isa_init_single(ix);
+    // links (hk_seground.hpp; ISA values < 2^31 leave the top bit for the link mark) pay where long repeats keep
+    // suffixes tied for many rounds: English-like 200 MiB (108M of 200M reach doubling) 67.7 -> 64.8 ms; on
+    // protein-like 1 GiB (256M of 1G, shorter repeats) they cost 13 ms more than the rounds they save
+    const bool many = ix.dbl.A * 3 >= ix.n;
+    ix.dbl.link = ix.n < (1ull << 31) && !(ix.flags & kFlagNoLinks) && (many || (ix.flags & kFlagLinks));
+    if (ix.dbl.link) lk_begin(ix);
   } else {
     dbl_isa_segment(ix, ix.sa.p, ix.n, 0);
     dbl_emit_groups(ix);
@@ -1315,6 +1350,10 @@ void refine_loop(Index& ix, const KeyGeom& kg, int cur, uint64_t A, uint64_t gro
   while (ix.dbl.A > 0) {
     if (++drounds > 64) throw ApiError{-7, "prefix doubling did not converge"};
     dbl_round(ix, ix.dbl.h);
+  }
+  if (ix.dbl.link) {
+    lk_resolve(ix);
+    ix.dbl.link = false;
   }
   ix.dbl.pending = false;
 }
@@ -1642,7 +1681,9 @@ void release_workspace(Index& ix) {
   }
   ix.big_j.release();
   ix.grp_big.release();
-  for (DevBuf* b : {&ix.sr_hp[0], &ix.sr_hp[1], &ix.sr_win[0], &ix.sr_win[1], &ix.sr_items, &ix.sr_cnt}) b->release();
+  for (DevBuf* b : {&ix.sr_hp[0], &ix.sr_hp[1], &ix.sr_win[0], &ix.sr_win[1], &ix.sr_items, &ix.sr_cnt, &ix.lk_lnk,
+                    &ix.lk_gsz, &ix.lk_tops, &ix.lk_grec})
+    b->release();
   ix.sr_plan_g = nullptr;
   ix.fused.reset();
   ix.fused_recs.release();

@@ -88,7 +88,13 @@ struct alignas(16) SrShared {
   } u;
   uint64_t hmask[SR_CAP / 64];      // bit i: a group starts at entry i (set past the item's end too)
   uint32_t whist[SR_NW][256];       // per-wave digit counts -> per-wave exclusive digit offsets
-  uint64_t mtab[SR_NW][256];        // per-wave match masks (zero between uses)
+  union {
+    uint64_t mtab[SR_NW][256];      // per-wave match masks (zero between uses)
+    uint32_t pl[SR_CAP];            // after the sort: u32 positions in entry order
+  } m;
+  uint64_t lkall[SR_CAP / 64];      // doubling links: bit i = entry i's group is linked
+  uint32_t lcnt, lgc;
+  unsigned long long lgbase;
   uint32_t tstart[256];             // item-local exclusive digit start
   uint32_t wtot[SR_NW];
   uint64_t wor[SR_NW], wand[SR_NW];
@@ -144,6 +150,14 @@ __device__ __forceinline__ uint32_t sr_next_head(const uint64_t* hm, uint32_t i)
   return (w << 6) + (uint32_t)__builtin_ctzll(b);
 }
 
+// the group head at or before entry i (entry 0 is a head)
+__device__ __forceinline__ uint32_t sr_prev_head(const uint64_t* hm, uint32_t i) {
+  uint32_t w = i >> 6;
+  uint64_t b = hm[w] & ((2ull << (i & 63)) - 1ull);
+  while (!b) b = hm[--w];
+  return (w << 6) + 63u - (uint32_t)__builtin_clzll(b);
+}
+
 // regroup record of a sorted position (section 3): run start, tied index, group index inside the item, flags
 constexpr int RG_TIED = 36, RG_RH = 37, RG_FIRST = 38;
 
@@ -158,15 +172,23 @@ __global__ __launch_bounds__(SR_T, 4) void k_sr_round(SrRoundArgs<V> a) {
   const uint64_t base = it.x;
   const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
 
-  // ---- 1. stage (striped: entry k * SR_T + tid), the head mask, the varying key bits, group sizes
+  // ---- 1. stage (striped: entry k * SR_T + tid), the head mask, the varying key bits, group sizes.  The
+  // entry's SA slot (and its u32 position) stay in registers until the write-out: no dependent load there
+  constexpr bool P32 = sizeof(V) == 4;
+  const bool links = P32 && MODE == 1 && a.lnk != nullptr;
   uint64_t kor = 0, kand = ~0ull;
+  uint32_t jr[SR_E], pr[SR_E];
 #pragma unroll
   for (int k = 0; k < SR_E; ++k) {
     const uint32_t i = (uint32_t)k * SR_T + tid;
+    jr[k] = 0;
+    pr[k] = 0;
     if (i < m) {
       const uint64_t key = a.keys[base + i];
       sh.key[i] = key;
       sh.u.g[i] = a.G[base + i];
+      jr[k] = a.J[base + i];
+      if constexpr (P32) pr[k] = (uint32_t)a.vals[base + i];
       kor |= key;
       kand &= key;
     }
@@ -174,6 +196,13 @@ __global__ __launch_bounds__(SR_T, 4) void k_sr_round(SrRoundArgs<V> a) {
   if (tid < 4) {
     sh.nwmin[tid] = SR_NONE;
     sh.nwmax[tid] = 0;
+  }
+  if (links) {
+    if (tid < SR_CAP / 64) sh.lkall[tid] = 0;
+    if (tid == 0) {
+      sh.lcnt = 0;
+      sh.lgc = 0;
+    }
   }
   __syncthreads();
   uint32_t big = 0;
@@ -197,6 +226,19 @@ __global__ __launch_bounds__(SR_T, 4) void k_sr_round(SrRoundArgs<V> a) {
     sh.wbig[wv] = big;
   }
   __syncthreads();   // (every read of u.g is done: idx may overwrite it)
+  // link candidates: a group head whose key names a tied group (ISA[p + h] + 1 > 0) of the same size
+  // (gsz ^ size == 0); whether all its keys are equal is read off the sorted order below
+  uint32_t lg[SR_E];
+#pragma unroll
+  for (int k = 0; k < SR_E; ++k) {
+    const uint32_t i = (uint32_t)k * SR_T + tid;
+    lg[k] = 1;
+    if (links && i < m && sr_head(sh.hmask, i)) {
+      const uint32_t sz = sr_next_head(sh.hmask, i) - i;
+      const uint64_t kl = sh.key[i] & ((1ull << a.ib) - 1);
+      if (sz >= 2 && kl && kl <= a.n) lg[k] = a.gsz[kl - 1] ^ sz;
+    }
+  }
   kor = 0;
   kand = ~0ull;
   big = 0;
@@ -233,8 +275,9 @@ __global__ __launch_bounds__(SR_T, 4) void k_sr_round(SrRoundArgs<V> a) {
     }
   } else if (vary) {
     const int lo = __builtin_ctzll(vary), hi = 64 - __builtin_clzll(vary);
-    for (uint32_t i = tid; i < (uint32_t)SR_NW * 256; i += SR_T) (&sh.mtab[0][0])[i] = 0;
+    for (uint32_t i = tid; i < (uint32_t)SR_NW * 256; i += SR_T) (&sh.m.mtab[0][0])[i] = 0;
     for (int shf = lo; shf < hi; shf += 8) {
+      if (((vary >> shf) & 255u) == 0) continue;   // (uniform: a digit with no varying bit orders nothing)
       if (tid < 256) {
 #pragma unroll
         for (int w = 0; w < SR_NW; ++w) sh.whist[w][tid] = 0;
@@ -242,7 +285,7 @@ __global__ __launch_bounds__(SR_T, 4) void k_sr_round(SrRoundArgs<V> a) {
       __syncthreads();
       // rank inside the wave (stable: wave-contiguous positions, item-major then lane), as k_onesweep
       uint32_t rk[SR_E];
-      uint64_t* const mt = sh.mtab[wv];
+      uint64_t* const mt = sh.m.mtab[wv];
 #pragma unroll
       for (int k = 0; k < SR_E; ++k) {
         const uint32_t pos = wv * (SR_E * 64) + (uint32_t)k * 64 + lane;
@@ -294,6 +337,66 @@ __global__ __launch_bounds__(SR_T, 4) void k_sr_round(SrRoundArgs<V> a) {
   }
   __syncthreads();
   const uint16_t* const ord = sh.u.idx[cur];
+  if constexpr (P32) {   // (the match masks are done with: their space takes the positions)
+#pragma unroll
+    for (int k = 0; k < SR_E; ++k) {
+      const uint32_t i = (uint32_t)k * SR_T + tid;
+      if (i < m) sh.m.pl[i] = pr[k];
+    }
+    __syncthreads();
+  }
+  if constexpr (P32 && MODE == 1) {
+    if (links) {   // a stuck candidate (first and last sorted keys equal) is linked by its head thread
+#pragma unroll
+      for (int k = 0; k < SR_E; ++k) {
+        const uint32_t i = (uint32_t)k * SR_T + tid;
+        if (lg[k] == 0) {
+          const uint32_t sz = sr_next_head(sh.hmask, i) - i;
+          lg[k] = ~0u;
+          if (sh.key[ord[i]] == sh.key[ord[i + sz - 1]]) {
+            lg[k] = atomicAdd(&sh.lgc, 1u);   // (the group's record index inside the item)
+            for (uint32_t b = i; b < i + sz;) {
+              const uint32_t lo = b & 63u, c = min(64u - lo, i + sz - b);
+              const uint64_t msk = (c == 64u ? ~0ull : ((1ull << c) - 1ull)) << lo;
+              atomicOr(reinterpret_cast<unsigned long long*>(&sh.lkall[b >> 6]), (unsigned long long)msk);
+              b += c;
+            }
+            atomicAdd(&sh.lcnt, sz);
+          }
+        }
+      }
+      __syncthreads();
+      if (tid == 0 && sh.lcnt) {
+        atomicAdd(a.lcount, (unsigned long long)sh.lcnt);
+        sh.lgbase = atomicAdd(a.gcount, (unsigned long long)sh.lgc);
+      }
+      // every linked entry writes its own link (striped: the stores of a wave go out together): the group's
+      // head slot is this entry's slot minus its distance to the head, K = its key (all equal in the group)
+#pragma unroll
+      for (int k = 0; k < SR_E; ++k) {
+        const uint32_t i = (uint32_t)k * SR_T + tid;
+        if (i < m && ((sh.lkall[i >> 6] >> (i & 63)) & 1ull)) {
+          const uint32_t gh = sr_prev_head(sh.hmask, i);
+          const uint32_t K = (uint32_t)(sh.key[i] & ((1ull << a.ib) - 1)) - 1u;
+          const uint32_t p = sh.m.pl[i];
+          a.lnk[p] = ((uint64_t)a.h << 32) | (uint32_t)(jr[k] - (i - gh) - K);
+          a.isa[p] = LK_BIT | a.ltag;
+        }
+      }
+      __syncthreads();
+      if (sh.lcnt) {
+#pragma unroll
+        for (int k = 0; k < SR_E; ++k) {
+          const uint32_t i = (uint32_t)k * SR_T + tid;
+          // (a linked group's head: its lg[k] is the record index)
+          if (i < m && sr_head(sh.hmask, i) && ((sh.lkall[i >> 6] >> (i & 63)) & 1ull)) {
+            const uint32_t sz = sr_next_head(sh.hmask, i) - i;
+            a.grec[sh.lgbase + lg[k]] = make_uint4(jr[k], sz, sh.m.pl[i], 0u);
+          }
+        }
+      }
+    }
+  }
 
   // ---- 3. regroup.  (a) blocked (thread tid owns positions [tid * SR_E, tid * SR_E + SR_E)): run heads, tied
   // flags and the item-wide scans (max of run-head positions, tied | tied heads << 16); (b) the per-position
@@ -312,7 +415,8 @@ __global__ __launch_bounds__(SR_T, 4) void k_sr_round(SrRoundArgs<V> a) {
         const uint64_t kn = i + 1 < m ? sh.key[ord[i + 1]] : 0;
         const bool rh = !have_prev || kc != prev;
         const bool re = i + 1 >= m || kn != kc;
-        const bool tied = !(rh && re);
+        const bool lk = links && ((sh.lkall[i >> 6] >> (i & 63)) & 1ull);   // (linked: neither tied nor settled)
+        const bool tied = !lk && !(rh && re);
         if (rh) {
           flags |= 1u << j;
           lmax = i;
@@ -375,13 +479,16 @@ __global__ __launch_bounds__(SR_T, 4) void k_sr_round(SrRoundArgs<V> a) {
   for (int k = 0; k < SR_E; ++k) {
     const uint32_t i = (uint32_t)k * SR_T + tid;
     if (i < m) {
+      if (links && ((sh.lkall[i >> 6] >> (i & 63)) & 1ull)) continue;
       const uint64_t r = sh.key[i];
       const uint32_t rs = (uint32_t)r & 0xFFFu;
       const bool tied = (r >> RG_TIED) & 1u, rh = (r >> RG_RH) & 1u;
-      const uint64_t p = (uint64_t)a.vals[base + ord[i]];
-      const uint32_t slot = a.J[base + i];
+      uint64_t p;
+      if constexpr (P32) p = sh.m.pl[ord[i]];
+      else p = (uint64_t)a.vals[base + ord[i]];
+      const uint32_t slot = jr[k];   // (slots are contiguous inside a group: the run start's is slot - (i - rs))
       if (MODE == 1) {
-        if (!(a.keep_same && ((r >> RG_FIRST) & 1u))) a.isa[p] = (V)(a.lo + (uint64_t)a.J[base + rs]);
+        if (!(a.keep_same && ((r >> RG_FIRST) & 1u))) a.isa[p] = (V)(a.lo + (uint64_t)(slot - (i - rs)));
       } else if (a.sa) {
         a.sa[slot] = (V)p;   // (every slot: prefix doubling builds its ISA from this SA)
       }
@@ -413,6 +520,232 @@ __global__ __launch_bounds__(SR_T, 4) void k_sr_round(SrRoundArgs<V> a) {
       atomicMax(a.win_next + 2 * (w0 + tid) + 1, sh.nwmax[tid]);
     }
   }
+}
+
+// ---- doubling links (see SrRoundArgs): the size of every tied group at its head slot; pointer jumping in dense
+// passes until every link names an unlinked position (up to LK_STEPS hops per position and pass: ISA(p) =
+// ISA(p + off) + delta composes); the SA / BWT entries of the linked positions once every other suffix is placed
+constexpr int LK_STEPS = 8;
+
+__global__ __launch_bounds__(256) void k_lk_sizes(const uint32_t* __restrict__ head_slot, const uint32_t* __restrict__ hp,
+                                                  uint64_t groups, uint64_t A, uint64_t n, uint32_t* __restrict__ gsz) {
+  for (uint64_t g = (uint64_t)blockIdx.x * 256 + threadIdx.x; g < groups; g += (uint64_t)gridDim.x * 256) {
+    const uint64_t e = g + 1 < groups ? (uint64_t)hp[g + 1] : A;
+    const uint32_t s = head_slot[g];
+    if (s < n) gsz[s] = (uint32_t)(e - hp[g]);
+  }
+}
+
+// one dense pass over the positions, highest first (a link names a higher position, so most targets were
+// jumped earlier in the same pass): every linked position follows its link while it names a linked one
+__global__ __launch_bounds__(256) void k_lk_jump(uint64_t n, uint64_t* __restrict__ lnk, const uint32_t* __restrict__ isa,
+                                                 unsigned int* __restrict__ flag) {
+  bool any = false, bad = false;
+  for (uint64_t x = (uint64_t)blockIdx.x * 256 + threadIdx.x; x < n; x += (uint64_t)gridDim.x * 256) {
+    const uint64_t p = n - 1 - x;
+    if (!(isa[p] & LK_BIT)) continue;
+    uint64_t l = lnk[p];
+    bool ch = false;
+#pragma unroll 1
+    for (int s = 0; s < LK_STEPS; ++s) {
+      const uint64_t q = p + (l >> 32);
+      if (q >= n || q <= p) {   // (never: a link names a higher position of the text)
+        bad = true;
+        break;
+      }
+      if (!(isa[q] & LK_BIT)) break;
+      const uint64_t l2 = lnk[q];
+      l = (((l >> 32) + (l2 >> 32)) << 32) | (uint32_t)((uint32_t)l + (uint32_t)l2);
+      ch = true;
+    }
+    if (ch) {
+      lnk[p] = l;
+      any = true;
+    }
+  }
+  const uint64_t ma = ballot64(any), mb = ballot64(bad);
+  if ((threadIdx.x & 63) == 0 && (ma | mb)) atomicOr(flag, (ma ? 1u : 0u) | (mb ? 2u : 0u));
+}
+
+// The links of one round all have offset h, so their chains run down the columns of the positions laid out in
+// rows of h.  A tile of R = LT_POS / h rows resolves every chain inside it in LDS: each column is split into
+// segments, each walked bottom-up by one thread (run rows / summed delta, open when the run reaches the segment
+// bottom), then the segments' carries are chained per column.  A run that reaches the tile bottom continues at
+// the next tile's top row: those tile tops (ntiles x h entries) are pointer-jumped as a small array and added to
+// the open runs afterwards (k_lk_open_fix).  One dense pass instead of log(chain) passes over every position.
+constexpr int LT_T = 256;
+constexpr uint32_t LT_POS = 8192;
+constexpr uint32_t LT_OPEN = 0x80000000u, LT_OPEN16 = 0x8000u;   // (run rows <= LT_POS < 2^15)
+
+__device__ __forceinline__ uint64_t lk_cv(uint32_t k, uint32_t d, bool open) {
+  return ((uint64_t)(k | (open ? LT_OPEN : 0u)) << 32) | d;
+}
+
+__global__ __launch_bounds__(LT_T) void k_lk_tile(const uint32_t* __restrict__ isa, uint64_t* __restrict__ lnk,
+                                                  uint64_t n, uint32_t h, uint32_t tagv, uint32_t R,
+                                                  uint64_t* __restrict__ tops) {
+  __shared__ uint32_t Dd[LT_POS];
+  __shared__ uint16_t Kk[LT_POS];   // run rows from this row down (LT_OPEN16: reaches the segment bottom), 0: unlinked
+  __shared__ uint64_t cin[LT_T];    // carry into each (column, segment) from below
+  const uint32_t tid = threadIdx.x;
+  const uint64_t base = (uint64_t)blockIdx.x * R * h;
+  const uint32_t T = R * h;
+  for (uint32_t i = tid; i < T; i += LT_T) {
+    const uint64_t p = base + i;
+    bool f = false;
+    uint32_t d = 0;
+    if (p < n && isa[p] == tagv) {
+      f = true;
+      d = (uint32_t)lnk[p];
+    }
+    Kk[i] = f ? 1 : 0;
+    Dd[i] = d;
+  }
+  __syncthreads();
+  const uint32_t S = h < (uint32_t)LT_T ? (uint32_t)LT_T / h : 1u;   // segments per column
+  const uint32_t RS = (R + S - 1) / S;                                // rows per segment
+  for (uint32_t w = tid; w < h * S; w += LT_T) {
+    const uint32_t c = w / S, sg = w % S;
+    const uint32_t r0 = sg * RS, r1 = min(R, r0 + RS);
+    uint32_t k = 0, d = 0;
+    bool open = true;
+    for (uint32_t r = r1; r-- > r0;) {
+      const uint32_t i = r * h + c;
+      if (Kk[i]) {
+        k += 1;
+        d += Dd[i];
+        Kk[i] = (uint16_t)(k | (open ? LT_OPEN16 : 0u));
+        Dd[i] = d;
+      } else {
+        k = 0;
+        d = 0;
+        open = false;
+      }
+    }
+  }
+  __syncthreads();
+  if (S > 1) {   // (h < LT_T: h * S <= LT_T carries)
+    for (uint32_t c = tid; c < h; c += LT_T) {
+      uint64_t carry = lk_cv(0, 0, true);
+      for (uint32_t sg = S; sg-- > 0;) {
+        cin[c * S + sg] = carry;
+        const uint32_t r0 = sg * RS;
+        if (r0 >= R) continue;
+        const uint32_t i = r0 * h + c;
+        const uint32_t kv = Kk[i];
+        if (!kv) {
+          carry = lk_cv(0, 0, false);
+        } else if (kv & LT_OPEN16) {
+          const uint32_t ck = (uint32_t)(carry >> 32);
+          carry = lk_cv((kv & ~LT_OPEN16) + (ck & ~LT_OPEN), Dd[i] + (uint32_t)carry, (ck & LT_OPEN) != 0);
+        } else {
+          carry = lk_cv(kv, Dd[i], false);
+        }
+      }
+    }
+  }
+  __syncthreads();
+  for (uint32_t w = tid; w < h * S; w += LT_T) {
+    const uint32_t c = w / S, sg = w % S;
+    const uint64_t cr = S > 1 ? cin[c * S + sg] : lk_cv(0, 0, true);
+    const uint32_t crk = (uint32_t)(cr >> 32);
+    const uint32_t r0 = sg * RS, r1 = min(R, r0 + RS);
+    for (uint32_t r = r0; r < r1; ++r) {
+      const uint32_t i = r * h + c;
+      const uint32_t kv = Kk[i];
+      if (!kv) {
+        if (r == 0) tops[(uint64_t)blockIdx.x * h + c] = 0;
+        continue;
+      }
+      uint32_t k = kv & ~LT_OPEN16, d = Dd[i];
+      bool open = false;
+      if (kv & LT_OPEN16) {
+        k += crk & ~LT_OPEN;
+        d += (uint32_t)cr;
+        open = (crk & LT_OPEN) != 0;
+      }
+      lnk[base + i] = ((uint64_t)k * h << 32) | d;   // (open: names the next tile's top row of this column)
+      if (r == 0) tops[(uint64_t)blockIdx.x * h + c] = lk_cv(k, d, open);
+    }
+  }
+}
+
+// tile tops: (k | open, d) per (tile, column); an open entry continues at the entry h further.  Wyllie pointer
+// jumping with ping-pong buffers: acc (k, d) and the next entry (~0: none)
+__global__ __launch_bounds__(256) void k_lk_tops_init(const uint64_t* __restrict__ tops, uint64_t m, uint32_t h,
+                                                      uint64_t* __restrict__ acc, uint64_t* __restrict__ nxt) {
+  for (uint64_t e = (uint64_t)blockIdx.x * 256 + threadIdx.x; e < m; e += (uint64_t)gridDim.x * 256) {
+    const uint64_t v = tops[e];
+    const uint32_t k = (uint32_t)(v >> 32);
+    acc[e] = ((uint64_t)(k & ~LT_OPEN) << 32) | (uint32_t)v;
+    nxt[e] = (k & LT_OPEN) && e + h < m ? e + h : ~0ull;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_lk_tops_jump(const uint64_t* __restrict__ acc, const uint64_t* __restrict__ nxt,
+                                                      uint64_t m, uint64_t* __restrict__ acc2, uint64_t* __restrict__ nxt2,
+                                                      unsigned int* __restrict__ flag) {
+  bool any = false;
+  for (uint64_t e = (uint64_t)blockIdx.x * 256 + threadIdx.x; e < m; e += (uint64_t)gridDim.x * 256) {
+    uint64_t a = acc[e], x = nxt[e];
+    if (x != ~0ull) {
+      const uint64_t b = acc[x];
+      a = ((((a >> 32) + (b >> 32)) & 0xFFFFFFFFull) << 32) | (uint32_t)((uint32_t)a + (uint32_t)b);
+      x = nxt[x];
+      any = true;
+    }
+    acc2[e] = a;
+    nxt2[e] = x;
+  }
+  if (ballot64(any) && (threadIdx.x & 63) == 0) atomicOr(flag, 1u);
+}
+
+// runs that reached their tile's bottom: add the resolved top of the next tile in their column
+__global__ __launch_bounds__(256) void k_lk_open_fix(const uint32_t* __restrict__ isa, uint64_t* __restrict__ lnk,
+                                                     uint64_t n, uint32_t h, uint32_t tagv, uint32_t R,
+                                                     const uint64_t* __restrict__ acc, uint64_t m) {
+  const uint64_t T = (uint64_t)R * h;
+  for (uint64_t p = (uint64_t)blockIdx.x * 256 + threadIdx.x; p < n; p += (uint64_t)gridDim.x * 256) {
+    if (isa[p] != tagv) continue;
+    const uint64_t l = lnk[p];
+    const uint64_t q = p + (l >> 32);
+    const uint64_t t = p / T;
+    if (q < (t + 1) * T) continue;   // closed inside the tile
+    const uint64_t e = (t + 1) * h + (p % T) % h;
+    if (e >= m) continue;            // (never: a run cannot leave the text)
+    const uint64_t b = acc[e];
+    lnk[p] = ((((l >> 32) + (b >> 32) * h) & 0xFFFFFFFFull) << 32) | (uint32_t)((uint32_t)l + (uint32_t)b);
+  }
+}
+
+// a linked group's slice of the SA is its chain end's slice shifted by the chain's offset: the members' images
+// p + OFF are unlinked suffixes whose final slots are [s - D, s - D + size) (f(p) = ISA(p + OFF) + D maps the
+// members onto [s, s + size)), and with links from one round only every member shares the head's {OFF, D}
+__global__ __launch_bounds__(256) void k_lk_resolve(const uint4* __restrict__ grec, uint64_t g0, uint64_t g1,
+                                                    const uint64_t* __restrict__ lnk, const uint8_t* __restrict__ t,
+                                                    uint64_t n, uint32_t* __restrict__ sa, uint8_t* __restrict__ bwt,
+                                                    unsigned int* __restrict__ flag) {
+  bool bad = false;
+  for (uint64_t g = g0 + (uint64_t)blockIdx.x * 256 + threadIdx.x; g < g1; g += (uint64_t)gridDim.x * 256) {
+    const uint4 r = grec[g];
+    const uint64_t l = lnk[r.z];
+    const uint32_t off = (uint32_t)(l >> 32), ke = r.x - (uint32_t)l;
+    if ((uint64_t)ke + r.y > n || (uint64_t)r.x + r.y > n) {
+      bad = true;
+      continue;
+    }
+    for (uint32_t i = 0; i < r.y; ++i) {
+      const uint32_t q = sa[ke + i];
+      if (q < off) {
+        bad = true;
+        break;
+      }
+      const uint32_t p = q - off;
+      sa[r.x + i] = p;
+      bwt[r.x + i] = t[p == 0 ? n - 1 : p - 1];
+    }
+  }
+  if (ballot64(bad) && (threadIdx.x & 63) == 0) atomicOr(flag, 2u);
 }
 
 }  // namespace
@@ -479,15 +812,22 @@ void sr_next_prepare(Index& ix, int slot, uint64_t A) {
 
 template <typename V>
 std::pair<uint64_t, uint64_t> sr_items_round(Index& ix, int mode, SrRoundArgs<V> args, uint64_t A, uint64_t tied0,
-                                             uint64_t groups0) {
+                                             uint64_t groups0, uint64_t* linked) {
   hipStream_t s = ix.stream;
   const uint64_t nw = ceil_div(A, (uint64_t)SR_W);
   unsigned long long* ctr = ix.sr_cnt.as<unsigned long long>() + 2;
   uint64_t* const rb = ix.rb();
   rb[2] = tied0 | (groups0 << 33);
+  rb[4] = 0;
   HK_HIP(hipMemcpyAsync(ctr, &rb[2], 8, hipMemcpyHostToDevice, s));
   args.items = ix.sr_items.as<uint2>();
   args.counter = ctr;
+  if (args.lnk) {
+    args.lcount = ix.sr_cnt.as<unsigned long long>() + 4;
+    args.gcount = ix.sr_cnt.as<unsigned long long>() + 10;
+    args.grec = ix.lk_grec.as<uint4>();
+    HK_HIP(hipMemsetAsync(args.lcount, 0, 8, s));
+  }
   if (nw) {
     TimedLaunch tm(ix.timer, mode ? "sa_round_dbl" : "sa_round_chunk",
                    (double)A * (8 + 2 * sizeof(V) + 8 + 4 + 4));
@@ -496,13 +836,127 @@ std::pair<uint64_t, uint64_t> sr_items_round(Index& ix, int mode, SrRoundArgs<V>
     HK_HIP(hipGetLastError());
   }
   HK_HIP(hipMemcpyAsync(&rb[3], ctr, 8, hipMemcpyDeviceToHost, s));
+  if (args.lnk) {
+    HK_HIP(hipMemcpyAsync(&rb[4], args.lcount, 8, hipMemcpyDeviceToHost, s));
+    HK_HIP(hipMemcpyAsync(&rb[5], args.gcount, 8, hipMemcpyDeviceToHost, s));
+  }
   HK_HIP(hipStreamSynchronize(s));
+  if (linked) *linked = args.lnk ? rb[4] : 0;
+  if (args.lnk) ix.dbl.lround.push_back(rb[5]);   // (the groups linked up to this round)
   return {rb[3] & ((1ull << 33) - 1), rb[3] >> 33};
 }
 
+// ---- doubling links (host)
+void lk_begin(Index& ix) {
+  const uint64_t n = ix.n;
+  ix.lk_lnk.ensure(n * 8 + 16);
+  ix.lk_gsz.ensure(n * 4 + 16);
+  ix.sr_cnt.ensure(128);   // [4]: linked entries of a round, [9]: jump flags, [10]: linked groups
+  ix.lk_grec.ensure((ix.dbl.A / 2 + 16) * sizeof(uint4));   // (a linked group has >= 2 members)
+  HK_HIP(hipMemsetAsync(ix.lk_gsz.p, 0, n * 4, ix.stream));
+  HK_HIP(hipMemsetAsync(ix.sr_cnt.as<unsigned long long>() + 10, 0, 8, ix.stream));
+  ix.dbl.lround.clear();
+  ix.dbl.nlinked = 0;
+  ix.dbl.ltag = 0;
+}
+
+void lk_sizes(Index& ix, int slot, uint64_t A, uint64_t groups) {
+  if (!groups) return;
+  TimedLaunch tm(ix.timer, "sa_link", (double)groups * 12);
+  k_lk_sizes<<<(unsigned)std::min<uint64_t>(ceil_div(groups, 256), 16384), 256, 0, ix.stream>>>(
+      ix.head_slot.as<uint32_t>(), ix.sr_hp[slot].as<uint32_t>(), groups, A, ix.n, ix.lk_gsz.as<uint32_t>());
+  HK_HIP(hipGetLastError());
+}
+
+static unsigned int lk_flag_read(Index& ix, unsigned int* d_flag) {
+  uint64_t* const rb = ix.rb();
+  rb[5] = 0;
+  HK_HIP(hipMemcpyAsync(&rb[5], d_flag, 4, hipMemcpyDeviceToHost, ix.stream));
+  HK_HIP(hipStreamSynchronize(ix.stream));
+  return (unsigned int)rb[5];
+}
+
+void lk_after_round(Index& ix, uint64_t linked, uint32_t h) {
+  if (!linked) return;
+  hipStream_t s = ix.stream;
+  const uint64_t n = ix.n;
+  unsigned int* flag = reinterpret_cast<unsigned int*>(ix.sr_cnt.as<unsigned long long>() + 9);
+  const unsigned g = (unsigned)std::min<uint64_t>(ceil_div(n, 256), 16384);
+  const uint32_t tagv = LK_BIT | ix.dbl.ltag;
+  if (h >= 1 && h <= LT_POS) {   // this round's chains (all of offset h) in LDS tiles, then across tiles
+    const uint32_t R = LT_POS / h;
+    const uint64_t T = (uint64_t)R * h, nt = ceil_div(n, T), m = nt * h;
+    ix.lk_tops.ensure(m * 8 * 5 + 64);
+    uint64_t* tops = ix.lk_tops.as<uint64_t>();
+    uint64_t* acc[2] = {tops + m, tops + 2 * m};
+    uint64_t* nxt[2] = {tops + 3 * m, tops + 4 * m};
+    {
+      TimedLaunch tm(ix.timer, "sa_link", (double)n * 4 + (double)linked * 16);
+      k_lk_tile<<<(unsigned)nt, LT_T, 0, s>>>(ix.isa.as<uint32_t>(), ix.lk_lnk.as<uint64_t>(), n, h, tagv, R, tops);
+      HK_HIP(hipGetLastError());
+    }
+    const unsigned gm = (unsigned)std::min<uint64_t>(ceil_div(m, 256), 16384);
+    {
+      TimedLaunch tm(ix.timer, "sa_link", (double)m * 24);
+      k_lk_tops_init<<<gm, 256, 0, s>>>(tops, m, h, acc[0], nxt[0]);
+      HK_HIP(hipGetLastError());
+    }
+    int c = 0;
+    for (int pass = 0;; ++pass) {
+      if (pass > 40) throw ApiError{-7, "prefix doubling: link tiles did not converge"};
+      HK_HIP(hipMemsetAsync(flag, 0, 4, s));
+      {
+        TimedLaunch tm(ix.timer, "sa_link", (double)m * 48);
+        k_lk_tops_jump<<<gm, 256, 0, s>>>(acc[c], nxt[c], m, acc[c ^ 1], nxt[c ^ 1], flag);
+        HK_HIP(hipGetLastError());
+      }
+      c ^= 1;
+      if (!lk_flag_read(ix, flag)) break;
+    }
+    {
+      TimedLaunch tm(ix.timer, "sa_link", (double)n * 4 + (double)linked * 16);
+      k_lk_open_fix<<<g, 256, 0, s>>>(ix.isa.as<uint32_t>(), ix.lk_lnk.as<uint64_t>(), n, h, tagv, R, acc[c], m);
+      HK_HIP(hipGetLastError());
+    }
+    if (!ix.dbl.nlinked) {   // no older links: every new one names an unlinked position now
+      ix.dbl.nlinked += linked;
+      return;
+    }
+  }
+  for (int pass = 0;; ++pass) {
+    if (pass > 64) throw ApiError{-7, "prefix doubling: link chains did not converge"};
+    HK_HIP(hipMemsetAsync(flag, 0, 4, s));
+    {
+      TimedLaunch tm(ix.timer, "sa_link", (double)n * 4 + (double)(ix.dbl.nlinked + linked) * 32);
+      k_lk_jump<<<g, 256, 0, s>>>(n, ix.lk_lnk.as<uint64_t>(), ix.isa.as<uint32_t>(), flag);
+      HK_HIP(hipGetLastError());
+    }
+    const unsigned int f = lk_flag_read(ix, flag);
+    if (f & 2u) throw ApiError{-7, "prefix doubling: a link leaves the text"};
+    if (!f) break;
+  }
+  ix.dbl.nlinked += linked;
+}
+
+void lk_resolve(Index& ix) {
+  if (!ix.dbl.nlinked || ix.dbl.lround.empty()) return;
+  hipStream_t s = ix.stream;
+  const uint64_t n = ix.n, ng = ix.dbl.lround.back();
+  unsigned int* flag = reinterpret_cast<unsigned int*>(ix.sr_cnt.as<unsigned long long>() + 9);
+  HK_HIP(hipMemsetAsync(flag, 0, 4, s));
+  {
+    TimedLaunch tm(ix.timer, "sa_link", (double)ng * 24 + (double)ix.dbl.nlinked * 9);
+    k_lk_resolve<<<(unsigned)std::min<uint64_t>(ceil_div(ng, 256), 16384), 256, 0, s>>>(
+        ix.lk_grec.as<uint4>(), 0, ng, ix.lk_lnk.as<uint64_t>(), ix.text.as<uint8_t>(), n, ix.sa.as<uint32_t>(),
+        ix.bwt.as<uint8_t>(), flag);
+    HK_HIP(hipGetLastError());
+  }
+  if (lk_flag_read(ix, flag)) throw ApiError{-7, "prefix doubling: a linked group found no slots"};
+}
+
 template std::pair<uint64_t, uint64_t> sr_items_round<uint32_t>(Index&, int, SrRoundArgs<uint32_t>, uint64_t, uint64_t,
-                                                                 uint64_t);
+                                                                 uint64_t, uint64_t*);
 template std::pair<uint64_t, uint64_t> sr_items_round<uint64_t>(Index&, int, SrRoundArgs<uint64_t>, uint64_t, uint64_t,
-                                                                 uint64_t);
+                                                                 uint64_t, uint64_t*);
 
 }  // namespace hk

@@ -32,7 +32,20 @@ struct SrRoundArgs {
   int keep_same;           // doubling: skip the ISA entries a round leaves unchanged
   uint32_t* hp_next;       // (nullable) the next round's plan: head entry of every new group, and
   uint32_t* win_next;      //   every window's {first, last} head entry (sr_next_prepare resets them)
+  // doubling links (nullable lnk: off).  A group whose members' keys are all ISA[p + h] = K (one tied group) and
+  // whose size equals that group's (gsz[K]) is a shifted copy of it: its members leave the list with
+  // lnk[p] = {h, own head slot - K} and isa[p] = LK_BIT | ltag, so ISA(p) = ISA(p + h) + delta at every later
+  // precision (csa/suffix_array.py:131-134: suffix p orders as suffix p + h inside the group).
+  uint64_t* lnk;
+  const uint32_t* gsz;
+  unsigned long long* lcount;   // linked entries of the round
+  unsigned long long* gcount;   // linked groups (all rounds): records grec[] = {head slot, size, head position}
+  uint4* grec;
+  uint32_t h, ltag;
+  int ib;                  // key bits below the group ordinal
 };
+
+constexpr uint32_t LK_BIT = 0x80000000u;   // isa[p] of a linked position
 
 // Windows, items and big groups of list `slot` (A entries in `groups` groups): ix.sr_items, ix.grp_big (u8 per
 // group, 1 = big).  heads_ready: the previous round already wrote the list's group heads and window bounds
@@ -48,6 +61,14 @@ void sr_heads(Index& ix, int slot, const uint32_t* G, uint64_t lo, uint64_t hi, 
 // entries in groups0 groups (the big groups').  Returns the next list's (entries, groups).
 template <typename V>
 std::pair<uint64_t, uint64_t> sr_items_round(Index& ix, int mode, SrRoundArgs<V> args, uint64_t A, uint64_t tied0,
-                                             uint64_t groups0);
+                                             uint64_t groups0, uint64_t* linked = nullptr);
+
+// doubling links (u32 positions, n < 2^31): buffers (lk_begin); gsz of list `slot`'s groups before a round
+// (lk_sizes); after a round that linked entries: collect and jump (lk_after_round); SA / BWT of every linked
+// suffix once the list is empty (lk_resolve)
+void lk_begin(Index& ix);
+void lk_sizes(Index& ix, int slot, uint64_t A, uint64_t groups);
+void lk_after_round(Index& ix, uint64_t linked, uint32_t h);
+void lk_resolve(Index& ix);
 
 }  // namespace hk

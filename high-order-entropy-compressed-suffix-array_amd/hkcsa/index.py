@@ -80,6 +80,8 @@ FLAG_GLOBAL_SORT = 4   # HKCSA_FLAG_GLOBAL_SORT: build by full-width LSD sort (n
 FLAG_MUL_BINS = 8      # HKCSA_FLAG_MUL_BINS: sharded slices use multiplicative bucket bins (diagnostic)
 FLAG_MAX_BUCKETS = 16  # HKCSA_FLAG_MAX_BUCKETS: single GPU, the most bucket bits at any n (diagnostic)
 FLAG_SLICES = 32       # HKCSA_FLAG_SLICES: single GPU, the multi-slice build (n >= 2^32 - 1) at any n
+FLAG_LINKS = 64        # HKCSA_FLAG_LINKS: single GPU, doubling links at any tie count (parity tests)
+FLAG_NO_LINKS = 128    # HKCSA_FLAG_NO_LINKS: single GPU, no doubling links (diagnostic)
 
 
 class DeviceIndex:

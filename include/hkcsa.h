@@ -55,6 +55,10 @@ typedef struct hkcsa_queries hkcsa_queries;
                                    /* so small texts take the 1 GiB pipeline (diagnostic)       */
 #define HKCSA_FLAG_SLICES 32u  /* single GPU: the multi-slice build (taken by itself when    */
                                /* n >= 2^32 - 1) at any n, in 4 slices (parity tests)        */
+#define HKCSA_FLAG_LINKS 64u   /* single GPU: link shifted-copy groups in the first doubling  */
+                               /* round at any tie count (default: when a third or more of   */
+                               /* the suffixes reach doubling; parity tests)                 */
+#define HKCSA_FLAG_NO_LINKS 128u /* single GPU: never link (diagnostic)                       */
 
 typedef struct hkcsa_opts {
   int32_t device;   /* HIP device ordinal (-1 = current)                 */

@@ -100,3 +100,30 @@ def test_protein_like_24MiB_wt(hk):
     from utils.textgen import protein_like_text
     text = protein_like_text(24 * (1 << 20) + 1, seed=9, family_frac=0.6, mut_rate=0.02)
     _full_check(hk, text, 4000, seed=91)
+
+
+@pytest.mark.parametrize("kind,flag", [("english", "FLAG_NO_LINKS"), ("protein", "FLAG_LINKS"),
+                                       ("periodic", "FLAG_LINKS"), ("repeats", "FLAG_LINKS")])
+def test_doubling_links_both_ways(hk, kind, flag):
+    """Doubling links (a group that maps whole onto one tied group leaves the list; hk_seground.hpp) forced on
+    or off against the default rule (on when a third of the suffixes reach prefix doubling): the English-like
+    text without them, protein-like, periodic and planted-repeat texts with them.  Full checks."""
+    from utils.textgen import english_like_text, protein_like_text
+    rng = np.random.default_rng(77)
+    if kind == "english":
+        text = english_like_text(12 * (1 << 20) + 1, seed=12)
+    elif kind == "protein":
+        text = protein_like_text(16 * (1 << 20) + 1, seed=13, family_frac=0.6, mut_rate=0.02)
+    elif kind == "periodic":
+        unit = rng.integers(97, 101, size=37, dtype=np.uint8)
+        body = np.tile(unit, (3 << 20) // 37 + 1)[: 3 << 20]
+        body[1 << 20] = 120                                  # one break in the period
+        text = np.concatenate([body, np.frombuffer(b"$", np.uint8)])
+    else:
+        body = rng.integers(65, 69, size=4 << 20, dtype=np.uint8)
+        for _ in range(40):                                  # planted copies of 10K - 200K symbols
+            ln = int(rng.integers(10_000, 200_000))
+            src, dst = (int(x) for x in rng.integers(0, len(body) - ln, size=2))
+            body[dst:dst + ln] = body[src:src + ln].copy()
+        text = np.concatenate([body, np.frombuffer(b"$", np.uint8)])
+    _full_check(hk, text, 3000, seed=171, flags=getattr(hk.index, flag), wt=False)

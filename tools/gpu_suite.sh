@@ -10,6 +10,7 @@
 #   profen  the same on the English-like 200 MiB leg     -> gpurun_out/kprof_<TAG>en.json
 #   strong  the strong configs[4] line at N = 1           -> gpurun_out/<TAG>_strong.json
 #   emul8   emulated N = 8 rank 0 / 7                     -> gpurun_out/<TAG>_emul8.jsonl
+#   profemul8 / profstrong   tools/kprof.py on one emulated N = 8 rank / one strong 4 GiB step
 #   gap     one-step kernel trace with host gaps          -> gpurun_out/<TAG>_gap.txt
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
@@ -40,6 +41,14 @@ for s in ${STEPS:-tests smoke bench}; do
       timeout -k 10 900 python3 tools/kprof.py --tag ${TAG}en -- python3 bench.py --only-leg english --leg-steps 1 --patterns 1000 --wt-reps 1 --query-reps 1 \
         > gpurun_out/${TAG}en_kprof.log 2>&1
       rc=$?; head -12 gpurun_out/${TAG}en_kprof.log | cut -c1-300 ;;
+    profemul8)
+      timeout -k 10 900 python3 tools/kprof.py --tag ${TAG}e8 -- python3 tools/shard_emulate.py --nranks 8 --ranks 0 --pos64 --reps 1 \
+        > gpurun_out/${TAG}e8_kprof.log 2>&1
+      rc=$?; head -12 gpurun_out/${TAG}e8_kprof.log | cut -c1-300 ;;
+    profstrong)
+      timeout -k 10 900 python3 tools/kprof.py --tag ${TAG}st -- python3 bench.py --strong --steps 1 --warmup 0 \
+        > gpurun_out/${TAG}st_kprof.log 2>&1
+      rc=$?; head -12 gpurun_out/${TAG}st_kprof.log | cut -c1-300 ;;
     strong)
       timeout -k 10 300 python3 -u bench.py --strong --steps 3 --warmup 1 > gpurun_out/${TAG}_strong.json 2> gpurun_out/${TAG}_strong.err
       rc=$?; cut -c1-300 gpurun_out/${TAG}_strong.json ;;
