@@ -21,7 +21,7 @@ for s in ${STEPS:-tests smoke bench}; do
   echo "== $s $(date +%T)"
   case $s in
     tests)
-      timeout -k 10 900 python -u -m pytest -x -v --timeout 600 --timeout-method thread -m gpu tests \
+      timeout -k 10 900 python -u -m pytest -x -v --durations=40 --timeout 600 --timeout-method thread -m gpu tests \
         > gpurun_out/${TAG}_gpu_tests.log 2>&1
       rc=$?; tail -4 gpurun_out/${TAG}_gpu_tests.log ;;
     quick)
