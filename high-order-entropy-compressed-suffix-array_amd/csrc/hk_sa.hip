@@ -964,7 +964,7 @@ std::pair<uint64_t, uint64_t> seg_round(Index& ix, const KeyGeom& kg, int mode, 
   sr_next_prepare(ix, cur ^ 1, A);
   // links in the first doubling round only: every chain then runs through groups of that one round, so a linked
   // group's members share their chain (the group copy of lk_resolve relies on it); later rounds link far less
-  const bool link = mode == 1 && ix.dbl.link && sizeof(V) == 4 && ix.dbl.ltag == 0;
+  const bool link = mode == 1 && ix.dbl.link && sizeof(V) == 4 && ix.dbl.ltag == 0 && ix.dbl.h <= lk_max_offset();
   if (link) lk_sizes(ix, cur, A, groups);   // (before the big groups' apply rewrites head_slot)
   std::pair<uint64_t, uint64_t> r0{0, 0};
   if (B) {

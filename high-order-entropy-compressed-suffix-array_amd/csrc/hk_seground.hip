@@ -522,10 +522,8 @@ __global__ __launch_bounds__(SR_T, 4) void k_sr_round(SrRoundArgs<V> a) {
   }
 }
 
-// ---- doubling links (see SrRoundArgs): the size of every tied group at its head slot; pointer jumping in dense
-// passes until every link names an unlinked position (up to LK_STEPS hops per position and pass: ISA(p) =
-// ISA(p + off) + delta composes); the SA / BWT entries of the linked positions once every other suffix is placed
-constexpr int LK_STEPS = 8;
+// ---- doubling links (see SrRoundArgs): the size of every tied group at its head slot, the chains of one round's
+// links (ISA(p) = ISA(p + off) + delta composes), the SA / BWT entries of the linked groups at the end
 
 __global__ __launch_bounds__(256) void k_lk_sizes(const uint32_t* __restrict__ head_slot, const uint32_t* __restrict__ hp,
                                                   uint64_t groups, uint64_t A, uint64_t n, uint32_t* __restrict__ gsz) {
@@ -534,37 +532,6 @@ __global__ __launch_bounds__(256) void k_lk_sizes(const uint32_t* __restrict__ h
     const uint32_t s = head_slot[g];
     if (s < n) gsz[s] = (uint32_t)(e - hp[g]);
   }
-}
-
-// one dense pass over the positions, highest first (a link names a higher position, so most targets were
-// jumped earlier in the same pass): every linked position follows its link while it names a linked one
-__global__ __launch_bounds__(256) void k_lk_jump(uint64_t n, uint64_t* __restrict__ lnk, const uint32_t* __restrict__ isa,
-                                                 unsigned int* __restrict__ flag) {
-  bool any = false, bad = false;
-  for (uint64_t x = (uint64_t)blockIdx.x * 256 + threadIdx.x; x < n; x += (uint64_t)gridDim.x * 256) {
-    const uint64_t p = n - 1 - x;
-    if (!(isa[p] & LK_BIT)) continue;
-    uint64_t l = lnk[p];
-    bool ch = false;
-#pragma unroll 1
-    for (int s = 0; s < LK_STEPS; ++s) {
-      const uint64_t q = p + (l >> 32);
-      if (q >= n || q <= p) {   // (never: a link names a higher position of the text)
-        bad = true;
-        break;
-      }
-      if (!(isa[q] & LK_BIT)) break;
-      const uint64_t l2 = lnk[q];
-      l = (((l >> 32) + (l2 >> 32)) << 32) | (uint32_t)((uint32_t)l + (uint32_t)l2);
-      ch = true;
-    }
-    if (ch) {
-      lnk[p] = l;
-      any = true;
-    }
-  }
-  const uint64_t ma = ballot64(any), mb = ballot64(bad);
-  if ((threadIdx.x & 63) == 0 && (ma | mb)) atomicOr(flag, (ma ? 1u : 0u) | (mb ? 2u : 0u));
 }
 
 // The links of one round all have offset h, so their chains run down the columns of the positions laid out in
@@ -860,6 +827,8 @@ void lk_begin(Index& ix) {
   ix.dbl.ltag = 0;
 }
 
+uint64_t lk_max_offset() { return LT_POS; }
+
 void lk_sizes(Index& ix, int slot, uint64_t A, uint64_t groups) {
   if (!groups) return;
   TimedLaunch tm(ix.timer, "sa_link", (double)groups * 12);
@@ -878,64 +847,48 @@ static unsigned int lk_flag_read(Index& ix, unsigned int* d_flag) {
 
 void lk_after_round(Index& ix, uint64_t linked, uint32_t h) {
   if (!linked) return;
+  if (h < 1 || h > LT_POS) throw ApiError{-7, "prefix doubling: link offset beyond the link tiles"};
   hipStream_t s = ix.stream;
   const uint64_t n = ix.n;
   unsigned int* flag = reinterpret_cast<unsigned int*>(ix.sr_cnt.as<unsigned long long>() + 9);
   const unsigned g = (unsigned)std::min<uint64_t>(ceil_div(n, 256), 16384);
   const uint32_t tagv = LK_BIT | ix.dbl.ltag;
-  if (h >= 1 && h <= LT_POS) {   // this round's chains (all of offset h) in LDS tiles, then across tiles
-    const uint32_t R = LT_POS / h;
-    const uint64_t T = (uint64_t)R * h, nt = ceil_div(n, T), m = nt * h;
-    ix.lk_tops.ensure(m * 8 * 5 + 64);
-    uint64_t* tops = ix.lk_tops.as<uint64_t>();
-    uint64_t* acc[2] = {tops + m, tops + 2 * m};
-    uint64_t* nxt[2] = {tops + 3 * m, tops + 4 * m};
-    {
-      TimedLaunch tm(ix.timer, "sa_link", (double)n * 4 + (double)linked * 16);
-      k_lk_tile<<<(unsigned)nt, LT_T, 0, s>>>(ix.isa.as<uint32_t>(), ix.lk_lnk.as<uint64_t>(), n, h, tagv, R, tops);
-      HK_HIP(hipGetLastError());
-    }
-    const unsigned gm = (unsigned)std::min<uint64_t>(ceil_div(m, 256), 16384);
-    {
-      TimedLaunch tm(ix.timer, "sa_link", (double)m * 24);
-      k_lk_tops_init<<<gm, 256, 0, s>>>(tops, m, h, acc[0], nxt[0]);
-      HK_HIP(hipGetLastError());
-    }
-    int c = 0;
-    for (int pass = 0;; ++pass) {
-      if (pass > 40) throw ApiError{-7, "prefix doubling: link tiles did not converge"};
-      HK_HIP(hipMemsetAsync(flag, 0, 4, s));
-      {
-        TimedLaunch tm(ix.timer, "sa_link", (double)m * 48);
-        k_lk_tops_jump<<<gm, 256, 0, s>>>(acc[c], nxt[c], m, acc[c ^ 1], nxt[c ^ 1], flag);
-        HK_HIP(hipGetLastError());
-      }
-      c ^= 1;
-      if (!lk_flag_read(ix, flag)) break;
-    }
-    {
-      TimedLaunch tm(ix.timer, "sa_link", (double)n * 4 + (double)linked * 16);
-      k_lk_open_fix<<<g, 256, 0, s>>>(ix.isa.as<uint32_t>(), ix.lk_lnk.as<uint64_t>(), n, h, tagv, R, acc[c], m);
-      HK_HIP(hipGetLastError());
-    }
-    if (!ix.dbl.nlinked) {   // no older links: every new one names an unlinked position now
-      ix.dbl.nlinked += linked;
-      return;
-    }
+  // this round's chains (all of offset h) inside LDS tiles, then across tiles
+  const uint32_t R = LT_POS / h;
+  const uint64_t T = (uint64_t)R * h, nt = ceil_div(n, T), m = nt * h;
+  ix.lk_tops.ensure(m * 8 * 5 + 64);
+  uint64_t* tops = ix.lk_tops.as<uint64_t>();
+  uint64_t* acc[2] = {tops + m, tops + 2 * m};
+  uint64_t* nxt[2] = {tops + 3 * m, tops + 4 * m};
+  {
+    TimedLaunch tm(ix.timer, "sa_link", (double)n * 4 + (double)linked * 16);
+    k_lk_tile<<<(unsigned)nt, LT_T, 0, s>>>(ix.isa.as<uint32_t>(), ix.lk_lnk.as<uint64_t>(), n, h, tagv, R, tops);
+    HK_HIP(hipGetLastError());
   }
+  const unsigned gm = (unsigned)std::min<uint64_t>(ceil_div(m, 256), 16384);
+  {
+    TimedLaunch tm(ix.timer, "sa_link", (double)m * 24);
+    k_lk_tops_init<<<gm, 256, 0, s>>>(tops, m, h, acc[0], nxt[0]);
+    HK_HIP(hipGetLastError());
+  }
+  int c = 0;
   for (int pass = 0;; ++pass) {
-    if (pass > 64) throw ApiError{-7, "prefix doubling: link chains did not converge"};
+    if (pass > 40) throw ApiError{-7, "prefix doubling: link tiles did not converge"};
     HK_HIP(hipMemsetAsync(flag, 0, 4, s));
     {
-      TimedLaunch tm(ix.timer, "sa_link", (double)n * 4 + (double)(ix.dbl.nlinked + linked) * 32);
-      k_lk_jump<<<g, 256, 0, s>>>(n, ix.lk_lnk.as<uint64_t>(), ix.isa.as<uint32_t>(), flag);
+      TimedLaunch tm(ix.timer, "sa_link", (double)m * 48);
+      k_lk_tops_jump<<<gm, 256, 0, s>>>(acc[c], nxt[c], m, acc[c ^ 1], nxt[c ^ 1], flag);
       HK_HIP(hipGetLastError());
     }
-    const unsigned int f = lk_flag_read(ix, flag);
-    if (f & 2u) throw ApiError{-7, "prefix doubling: a link leaves the text"};
-    if (!f) break;
+    c ^= 1;
+    if (!lk_flag_read(ix, flag)) break;
   }
-  ix.dbl.nlinked += linked;
+  {
+    TimedLaunch tm(ix.timer, "sa_link", (double)n * 4 + (double)linked * 16);
+    k_lk_open_fix<<<g, 256, 0, s>>>(ix.isa.as<uint32_t>(), ix.lk_lnk.as<uint64_t>(), n, h, tagv, R, acc[c], m);
+    HK_HIP(hipGetLastError());
+  }
+  ix.dbl.nlinked += linked;   // (every link names an unlinked position now)
 }
 
 void lk_resolve(Index& ix) {

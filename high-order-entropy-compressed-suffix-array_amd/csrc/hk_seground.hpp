@@ -64,9 +64,10 @@ std::pair<uint64_t, uint64_t> sr_items_round(Index& ix, int mode, SrRoundArgs<V>
                                              uint64_t groups0, uint64_t* linked = nullptr);
 
 // doubling links (u32 positions, n < 2^31): buffers (lk_begin); gsz of list `slot`'s groups before a round
-// (lk_sizes); after a round that linked entries: collect and jump (lk_after_round); SA / BWT of every linked
-// suffix once the list is empty (lk_resolve)
+// (lk_sizes); after the round that linked entries: resolve their chains (lk_after_round); SA / BWT of every
+// linked group once the list is empty (lk_resolve)
 void lk_begin(Index& ix);
+uint64_t lk_max_offset();   // the largest doubling offset whose chains the link tiles resolve
 void lk_sizes(Index& ix, int slot, uint64_t A, uint64_t groups);
 void lk_after_round(Index& ix, uint64_t linked, uint32_t h);
 void lk_resolve(Index& ix);
