@@ -4362,6 +4362,7 @@ void build_sa_bucketed(Index& ix) {
   // passes with the late bucket histogram, for A/B)
   const bool use_cp = cursor_enabled() && D > 0 && ka.hq > 0 && D <= 17;
   const bool late_hist = D > 0 && ka.hq > 0 && !use_cp;
+  bool skip_plan = false;   // a sample of the bucket counts already says: the global path
   if (use_cp) {
     // counted with the partition below
   } else if (late_hist) {
@@ -4375,6 +4376,30 @@ void build_sa_bucketed(Index& ix) {
     HK_HIP(hipGetLastError());
   } else if (D > 0) {
     ix.bk_hist.ensure((uint64_t)nbins * 8);
+    // skewed texts at scale (natural language, proteins) end on the global path anyway: the bucket counts of the
+    // text's first sixteenth decide that before the whole text is counted (1 GiB protein-like: 4.1 ms)
+    if (n >= (1ull << 26)) {
+      HK_HIP(hipMemsetAsync(ix.bk_hist.p, 0, (uint64_t)nbins * 8, s));
+      {
+        TimedLaunch t(ix.timer, "sa_bucket_hist", (double)n / 16);
+        const uint64_t tiles = ceil_div(n / 16, (uint64_t)BH_TILE);
+        const uint64_t tpw = ceil_div(tiles, 256);
+        const unsigned grid = (unsigned)ceil_div(tiles, tpw);
+        k_bucket_hist<false><<<grid, BH_T, 0, s>>>(ix.text.as<uint8_t>(), n, d_lutk, d_skey, ka, bsh, D,
+                                                   ix.bk_hist.as<unsigned long long>(), tpw * BH_TILE);
+        HK_HIP(hipGetLastError());
+      }
+      HK_HIP(hipMemcpyAsync(hist.data(), ix.bk_hist.p, (uint64_t)nbins * 8, hipMemcpyDeviceToHost, s));
+      HK_HIP(hipStreamSynchronize(s));
+      uint64_t tot = 0, big = 0;
+      for (uint32_t b = 0; b < nbins; ++b) tot += hist[b];
+      const uint64_t cap = item_T == 512 ? (uint64_t)512 * BS_I : (uint64_t)BS_CAP;
+      for (uint32_t b = 0; b < nbins; ++b)
+        if (tot && (double)hist[b] * (double)n / (double)tot > (double)cap) big += hist[b];
+      if (tot && big * 4 > tot * 3) skip_plan = true;   // over 3/4 of the suffixes in big buckets
+    }
+  }
+  if (D > 0 && !use_cp && !late_hist && !skip_plan) {
     HK_HIP(hipMemsetAsync(ix.bk_hist.p, 0, (uint64_t)nbins * 8, s));
     {
       TimedLaunch t(ix.timer, "sa_bucket_hist", (double)n);
@@ -4387,7 +4412,7 @@ void build_sa_bucketed(Index& ix) {
     }
     HK_HIP(hipMemcpyAsync(hist.data(), ix.bk_hist.p, (uint64_t)nbins * 8, hipMemcpyDeviceToHost, s));
     HK_HIP(hipStreamSynchronize(s));
-  } else {
+  } else if (D == 0) {
     hist[0] = n;
   }
 
@@ -4461,8 +4486,9 @@ void build_sa_bucketed(Index& ix) {
   }
 
   // ---- 2. work items (whole buckets, packed while they fit) and big buckets
-  const BucketPlan plan = plan_buckets(hist, bsh, item_T == 512 ? (uint64_t)512 * BS_I : (uint64_t)BS_CAP,
-                                       packed ? 8 : 32);
+  BucketPlan plan;
+  if (skip_plan) plan.big_total = n;   // (the global path: no items)
+  else plan = plan_buckets(hist, bsh, item_T == 512 ? (uint64_t)512 * BS_I : (uint64_t)BS_CAP, packed ? 8 : 32);
   const std::vector<uint2>& items_n = plan.items_n;
   const std::vector<uint2>& items_w = plan.items_w;
   const std::vector<uint64_t>& big_start = plan.big_start;

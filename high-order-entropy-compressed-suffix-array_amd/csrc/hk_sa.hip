@@ -961,7 +961,6 @@ std::pair<uint64_t, uint64_t> seg_round(Index& ix, const KeyGeom& kg, int mode, 
   const bool ready = ix.sr_plan_g != nullptr && ix.sr_plan_g == ix.act[cur][2].p;
   ix.sr_plan_g = nullptr;
   const uint64_t B = sr_plan(ix, cur, G, A, groups, ready, &nbg);
-  sr_next_prepare(ix, cur ^ 1, A);
   // links in the first doubling round only: every chain then runs through groups of that one round, so a linked
   // group's members share their chain (the group copy of lk_resolve relies on it); later rounds link far less
   const bool link = mode == 1 && ix.dbl.link && sizeof(V) == 4 && ix.dbl.ltag == 0 && ix.dbl.h <= lk_max_offset();

@@ -58,8 +58,9 @@ __global__ __launch_bounds__(256) void k_sr_heads(const uint32_t* __restrict__ G
 __global__ __launch_bounds__(256) void k_sr_items(const uint32_t* __restrict__ G, const uint32_t* __restrict__ hp,
                                                   uint64_t groups, uint64_t A, const uint32_t* __restrict__ win, uint64_t nw,
                                                   uint2* __restrict__ items, uint8_t* __restrict__ gbig,
-                                                  unsigned long long* __restrict__ cnt) {
+                                                  unsigned long long* __restrict__ cnt, uint2* __restrict__ win_next) {
   for (uint64_t w = (uint64_t)blockIdx.x * 256 + threadIdx.x; w < nw; w += (uint64_t)gridDim.x * 256) {
+    win_next[w] = make_uint2(SR_NONE, 0u);   // (the next list has at most as many windows)
     const uint32_t ws = win[2 * w];
     if (ws == SR_NONE) {
       items[w] = make_uint2(0u, 0u);
@@ -469,8 +470,8 @@ __global__ __launch_bounds__(SR_T, 4) void k_sr_round(SrRoundArgs<V> a) {
     const unsigned long long inc = (unsigned long long)(tcnt & 0xFFFFu) |
                                    ((unsigned long long)(tcnt >> 16) << 33);
     const unsigned long long old = atomicAdd(a.counter, inc);
-    sh.obase = old & ((1ull << 33) - 1);
-    sh.gbase = old >> 33;
+    sh.obase = a.base_e + (old & ((1ull << 33) - 1));   // (after the big groups' entries / groups)
+    sh.gbase = a.base_g + (old >> 33);
   }
   __syncthreads();
   const uint64_t obase = sh.obase, gbase = sh.gbase;
@@ -752,17 +753,21 @@ uint64_t sr_plan(Index& ix, int slot, const uint32_t* G, uint64_t A, uint64_t gr
   ix.sr_items.ensure(nw * sizeof(uint2) + 16);
   ix.sr_cnt.ensure(64);
   ix.grp_big.ensure(groups + 16);
+  // the next list's plan buffers (at most A entries, A / 2 groups); k_sr_items resets its windows
+  ix.sr_hp[slot ^ 1].ensure((A / 2 + 8) * 4 + 16);
+  ix.sr_win[slot ^ 1].ensure(nw * 8 + 16);
   if (!heads_ready) {
     sr_windows_reset(ix, slot, A);
     sr_heads(ix, slot, G, 0, A, A, groups);
   }
   HK_HIP(hipMemsetAsync(ix.grp_big.p, 0, groups, s));
-  HK_HIP(hipMemsetAsync(ix.sr_cnt.p, 0, 32, s));
+  HK_HIP(hipMemsetAsync(ix.sr_cnt.p, 0, 40, s));   // big counts, the round's counter, linked entries
   {
     TimedLaunch tm(ix.timer, "sa_round_plan", (double)nw * 16);
     const unsigned g2 = (unsigned)std::min<uint64_t>(ceil_div(nw, 256), 4096);
     k_sr_items<<<g2, 256, 0, s>>>(G, ix.sr_hp[slot].as<uint32_t>(), groups, A, ix.sr_win[slot].as<uint32_t>(), nw,
-                                  ix.sr_items.as<uint2>(), ix.grp_big.as<uint8_t>(), ix.sr_cnt.as<unsigned long long>());
+                                  ix.sr_items.as<uint2>(), ix.grp_big.as<uint8_t>(), ix.sr_cnt.as<unsigned long long>(),
+                                  ix.sr_win[slot ^ 1].as<uint2>());
     HK_HIP(hipGetLastError());
   }
   uint64_t* const rb = ix.rb();
@@ -772,28 +777,22 @@ uint64_t sr_plan(Index& ix, int slot, const uint32_t* G, uint64_t A, uint64_t gr
   return rb[0];
 }
 
-void sr_next_prepare(Index& ix, int slot, uint64_t A) {
-  ix.sr_hp[slot].ensure((A / 2 + 8) * 4 + 16);   // (the next list has at most A / 2 groups)
-  sr_windows_reset(ix, slot, A);
-}
-
 template <typename V>
 std::pair<uint64_t, uint64_t> sr_items_round(Index& ix, int mode, SrRoundArgs<V> args, uint64_t A, uint64_t tied0,
                                              uint64_t groups0, uint64_t* linked) {
   hipStream_t s = ix.stream;
   const uint64_t nw = ceil_div(A, (uint64_t)SR_W);
-  unsigned long long* ctr = ix.sr_cnt.as<unsigned long long>() + 2;
+  unsigned long long* ctr = ix.sr_cnt.as<unsigned long long>() + 2;   // (zeroed by sr_plan)
   uint64_t* const rb = ix.rb();
-  rb[2] = tied0 | (groups0 << 33);
   rb[4] = 0;
-  HK_HIP(hipMemcpyAsync(ctr, &rb[2], 8, hipMemcpyHostToDevice, s));
   args.items = ix.sr_items.as<uint2>();
   args.counter = ctr;
+  args.base_e = tied0;
+  args.base_g = groups0;
   if (args.lnk) {
-    args.lcount = ix.sr_cnt.as<unsigned long long>() + 4;
+    args.lcount = ix.sr_cnt.as<unsigned long long>() + 4;   // (zeroed by sr_plan)
     args.gcount = ix.sr_cnt.as<unsigned long long>() + 10;
     args.grec = ix.lk_grec.as<uint4>();
-    HK_HIP(hipMemsetAsync(args.lcount, 0, 8, s));
   }
   if (nw) {
     TimedLaunch tm(ix.timer, mode ? "sa_round_dbl" : "sa_round_chunk",
@@ -810,7 +809,7 @@ std::pair<uint64_t, uint64_t> sr_items_round(Index& ix, int mode, SrRoundArgs<V>
   HK_HIP(hipStreamSynchronize(s));
   if (linked) *linked = args.lnk ? rb[4] : 0;
   if (args.lnk) ix.dbl.lround.push_back(rb[5]);   // (the groups linked up to this round)
-  return {rb[3] & ((1ull << 33) - 1), rb[3] >> 33};
+  return {tied0 + (rb[3] & ((1ull << 33) - 1)), groups0 + (rb[3] >> 33)};
 }
 
 // ---- doubling links (host)

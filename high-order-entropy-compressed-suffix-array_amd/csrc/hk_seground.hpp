@@ -18,7 +18,8 @@ struct SrRoundArgs {
   const uint32_t* G;       // group ordinals (ascending along the list)
   const uint32_t* J;       // SA slots (contiguous and ascending inside a group)
   const uint2* items;      // (sr_plan)
-  unsigned long long* counter;   // next list: entries | groups << 33
+  unsigned long long* counter;   // next list: entries | groups << 33 (from 0; the items' output starts at
+  uint64_t base_e, base_g;       //   entry base_e, group base_g: after the big groups')
   V* oP;
   uint32_t* oJ;
   uint32_t* oG;
@@ -31,7 +32,7 @@ struct SrRoundArgs {
   uint64_t lo;
   int keep_same;           // doubling: skip the ISA entries a round leaves unchanged
   uint32_t* hp_next;       // (nullable) the next round's plan: head entry of every new group, and
-  uint32_t* win_next;      //   every window's {first, last} head entry (sr_next_prepare resets them)
+  uint32_t* win_next;      //   every window's {first, last} head entry (reset by sr_plan)
   // doubling links (nullable lnk: off).  A group whose members' keys are all ISA[p + h] = K (one tied group) and
   // whose size equals that group's (gsz[K]) is a shifted copy of it: its members leave the list with
   // lnk[p] = {h, own head slot - K} and isa[p] = LK_BIT | ltag, so ISA(p) = ISA(p + h) + delta at every later
@@ -49,11 +50,10 @@ constexpr uint32_t LK_BIT = 0x80000000u;   // isa[p] of a linked position
 
 // Windows, items and big groups of list `slot` (A entries in `groups` groups): ix.sr_items, ix.grp_big (u8 per
 // group, 1 = big).  heads_ready: the previous round already wrote the list's group heads and window bounds
-// (ix.sr_hp[slot], ix.sr_win[slot]).  Returns the entries in big groups (*big_groups: their number).
+// (ix.sr_hp[slot], ix.sr_win[slot]).  Also readies the next list's plan buffers (slot ^ 1: windows reset).
+// Returns the entries in big groups (*big_groups: their number).
 uint64_t sr_plan(Index& ix, int slot, const uint32_t* G, uint64_t A, uint64_t groups, bool heads_ready,
                  uint64_t* big_groups);
-// the next list's plan buffers, reset before the round writes them (A: the current list's entries)
-void sr_next_prepare(Index& ix, int slot, uint64_t A);
 // group heads + window bounds of list entries [lo, hi) (lo a multiple of 64), into list `slot`'s plan
 void sr_heads(Index& ix, int slot, const uint32_t* G, uint64_t lo, uint64_t hi, uint64_t A, uint64_t groups);
 
