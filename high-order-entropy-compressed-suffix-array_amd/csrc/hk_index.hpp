@@ -178,7 +178,8 @@ struct Index {
     bool big = false;          // a round had a group over SEG_MAX members: the next ones sort the list at once
     bool link = false;         // one GPU, n < 2^31: groups that map whole onto one tied group are linked (hk_seground)
     uint64_t nlinked = 0;      // linked positions
-    uint32_t ltag = 0;         // the current round's link tag
+    uint32_t ltag = 0;         // linking rounds run (links come from the first doubling round only)
+    uint32_t lk_h = 0;         // that round's offset: a link names the position hops x lk_h further
     std::vector<uint64_t> lround;   // linked groups recorded up to each linking round
   } dbl;
   DevBuf upd;

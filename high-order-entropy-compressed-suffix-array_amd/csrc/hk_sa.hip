@@ -525,7 +525,7 @@ template <typename V>
 __global__ __launch_bounds__(256) void k_dbl_keys(const V* __restrict__ P, const uint32_t* __restrict__ G, uint64_t A,
                                                   const V* __restrict__ isa, uint64_t n, uint64_t h, int ib,
                                                   uint64_t* __restrict__ keys, V* __restrict__ vals,
-                                                  const uint64_t* __restrict__ lnk) {
+                                                  const uint32_t* __restrict__ lnk, uint64_t lh) {
   for (uint64_t a = (uint64_t)blockIdx.x * 256 + threadIdx.x; a < A; a += (uint64_t)gridDim.x * 256) {
     const V p = P[a];
     const uint64_t q = (uint64_t)p + h;
@@ -534,9 +534,8 @@ __global__ __launch_bounds__(256) void k_dbl_keys(const V* __restrict__ P, const
       V v = isa[q];
       if constexpr (sizeof(V) == 4) {
         if (lnk && (v & LK_BIT)) {
-          const uint64_t l = lnk[q];
-          const uint64_t e = q + (l >> 32);
-          v = e < n ? isa[e] + (uint32_t)l : 0;   // (e < n always: a link names a position of its target group)
+          const uint64_t e = q + (uint64_t)(v & ~LK_BIT) * lh;
+          v = e < n ? isa[e] + lnk[q] : 0;   // (e < n always: a link names a position of its target group)
         }
       }
       s = (uint64_t)v + 1;
@@ -1020,10 +1019,11 @@ std::pair<uint64_t, uint64_t> seg_round(Index& ix, const KeyGeom& kg, int mode, 
   a.win_next = ix.sr_win[cur ^ 1].as<uint32_t>();
   uint64_t linked = 0;
   if (link) {
-    a.lnk = ix.lk_lnk.as<uint64_t>();
-    a.gsz = ix.lk_gsz.as<uint32_t>();
+    a.lnk = ix.lk_lnk.as<uint32_t>();
+    a.gsz = ix.lk_gsz.as<uint8_t>();
+    ix.dbl.lk_h = (uint32_t)ix.dbl.h;
     a.h = (uint32_t)ix.dbl.h;
-    a.ltag = ++ix.dbl.ltag;
+    ++ix.dbl.ltag;
     a.ib = ib;
   }
   const std::pair<uint64_t, uint64_t> r = sr_items_round<V>(ix, mode, a, A, r0.first, r0.second, &linked);
@@ -1057,7 +1057,7 @@ void dbl_round_t(Index& ix, uint64_t K) {
     TimedLaunch tm(ix.timer, "sa_pair_keys", (double)A * (2 * sizeof(V) + 4 + 8 + sizeof(V)));
     k_dbl_keys<V><<<grid_for(A), 256, 0, s>>>(ix.act[cur][0].as<V>(), ix.act[cur][2].as<uint32_t>(), A,
                                               ix.isa.as<V>(), ix.n, st.h, ib, kp[0], vp[0],
-                                              st.link ? ix.lk_lnk.as<uint64_t>() : nullptr);
+                                              st.link ? ix.lk_lnk.as<uint32_t>() : nullptr, st.lk_h);
     HK_HIP(hipGetLastError());
   }
   std::pair<uint64_t, uint64_t> r{0, 0};

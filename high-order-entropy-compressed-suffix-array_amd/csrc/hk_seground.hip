@@ -237,7 +237,7 @@ __global__ __launch_bounds__(SR_T, 4) void k_sr_round(SrRoundArgs<V> a) {
     if (links && i < m && sr_head(sh.hmask, i)) {
       const uint32_t sz = sr_next_head(sh.hmask, i) - i;
       const uint64_t kl = sh.key[i] & ((1ull << a.ib) - 1);
-      if (sz >= 2 && kl && kl <= a.n) lg[k] = a.gsz[kl - 1] ^ sz;
+      if (sz >= 2 && sz < 255 && kl && kl <= a.n) lg[k] = (uint32_t)a.gsz[kl - 1] ^ sz;
     }
   }
   kor = 0;
@@ -380,8 +380,7 @@ __global__ __launch_bounds__(SR_T, 4) void k_sr_round(SrRoundArgs<V> a) {
           const uint32_t gh = sr_prev_head(sh.hmask, i);
           const uint32_t K = (uint32_t)(sh.key[i] & ((1ull << a.ib) - 1)) - 1u;
           const uint32_t p = sh.m.pl[i];
-          a.lnk[p] = ((uint64_t)a.h << 32) | (uint32_t)(jr[k] - (i - gh) - K);
-          a.isa[p] = LK_BIT | a.ltag;
+          a.lnk[p] = jr[k] - (i - gh) - K;   // (!= 0: another group's head; the ISA mark comes with the tiles)
         }
       }
       __syncthreads();
@@ -527,11 +526,11 @@ __global__ __launch_bounds__(SR_T, 4) void k_sr_round(SrRoundArgs<V> a) {
 // links (ISA(p) = ISA(p + off) + delta composes), the SA / BWT entries of the linked groups at the end
 
 __global__ __launch_bounds__(256) void k_lk_sizes(const uint32_t* __restrict__ head_slot, const uint32_t* __restrict__ hp,
-                                                  uint64_t groups, uint64_t A, uint64_t n, uint32_t* __restrict__ gsz) {
+                                                  uint64_t groups, uint64_t A, uint64_t n, uint8_t* __restrict__ gsz) {
   for (uint64_t g = (uint64_t)blockIdx.x * 256 + threadIdx.x; g < groups; g += (uint64_t)gridDim.x * 256) {
     const uint64_t e = g + 1 < groups ? (uint64_t)hp[g + 1] : A;
     const uint32_t s = head_slot[g];
-    if (s < n) gsz[s] = (uint32_t)(e - hp[g]);
+    if (s < n) gsz[s] = (uint8_t)(e - hp[g] < 255 ? e - hp[g] : 255);
   }
 }
 
@@ -549,8 +548,8 @@ __device__ __forceinline__ uint64_t lk_cv(uint32_t k, uint32_t d, bool open) {
   return ((uint64_t)(k | (open ? LT_OPEN : 0u)) << 32) | d;
 }
 
-__global__ __launch_bounds__(LT_T) void k_lk_tile(const uint32_t* __restrict__ isa, uint64_t* __restrict__ lnk,
-                                                  uint64_t n, uint32_t h, uint32_t tagv, uint32_t R,
+__global__ __launch_bounds__(LT_T) void k_lk_tile(uint32_t* __restrict__ isa, uint32_t* __restrict__ lnk,
+                                                  uint64_t n, uint32_t h, uint32_t R,
                                                   uint64_t* __restrict__ tops) {
   __shared__ uint32_t Dd[LT_POS];
   __shared__ uint16_t Kk[LT_POS];   // run rows from this row down (LT_OPEN16: reaches the segment bottom), 0: unlinked
@@ -562,9 +561,9 @@ __global__ __launch_bounds__(LT_T) void k_lk_tile(const uint32_t* __restrict__ i
     const uint64_t p = base + i;
     bool f = false;
     uint32_t d = 0;
-    if (p < n && isa[p] == tagv) {
-      f = true;
-      d = (uint32_t)lnk[p];
+    if (p < n) {   // (linked in this round: a nonzero slot delta; the lnk plane was zeroed)
+      d = lnk[p];
+      f = d != 0;
     }
     Kk[i] = f ? 1 : 0;
     Dd[i] = d;
@@ -632,7 +631,8 @@ __global__ __launch_bounds__(LT_T) void k_lk_tile(const uint32_t* __restrict__ i
         d += (uint32_t)cr;
         open = (crk & LT_OPEN) != 0;
       }
-      lnk[base + i] = ((uint64_t)k * h << 32) | d;   // (open: names the next tile's top row of this column)
+      isa[base + i] = LK_BIT | k;   // k hops of h (open: to the next tile's top row of this column)
+      lnk[base + i] = d;
       if (r == 0) tops[(uint64_t)blockIdx.x * h + c] = lk_cv(k, d, open);
     }
   }
@@ -669,20 +669,22 @@ __global__ __launch_bounds__(256) void k_lk_tops_jump(const uint64_t* __restrict
 }
 
 // runs that reached their tile's bottom: add the resolved top of the next tile in their column
-__global__ __launch_bounds__(256) void k_lk_open_fix(const uint32_t* __restrict__ isa, uint64_t* __restrict__ lnk,
-                                                     uint64_t n, uint32_t h, uint32_t tagv, uint32_t R,
+__global__ __launch_bounds__(256) void k_lk_open_fix(uint32_t* __restrict__ isa, uint32_t* __restrict__ lnk,
+                                                     uint64_t n, uint32_t h, uint32_t R,
                                                      const uint64_t* __restrict__ acc, uint64_t m) {
   const uint64_t T = (uint64_t)R * h;
   for (uint64_t p = (uint64_t)blockIdx.x * 256 + threadIdx.x; p < n; p += (uint64_t)gridDim.x * 256) {
-    if (isa[p] != tagv) continue;
-    const uint64_t l = lnk[p];
-    const uint64_t q = p + (l >> 32);
+    const uint32_t v = isa[p];
+    if (!(v & LK_BIT)) continue;
+    const uint64_t hops = v & ~LK_BIT;
+    const uint64_t q = p + hops * h;
     const uint64_t t = p / T;
     if (q < (t + 1) * T) continue;   // closed inside the tile
     const uint64_t e = (t + 1) * h + (p % T) % h;
     if (e >= m) continue;            // (never: a run cannot leave the text)
     const uint64_t b = acc[e];
-    lnk[p] = ((((l >> 32) + (b >> 32) * h) & 0xFFFFFFFFull) << 32) | (uint32_t)((uint32_t)l + (uint32_t)b);
+    isa[p] = LK_BIT | (uint32_t)(hops + (b >> 32));
+    lnk[p] += (uint32_t)b;
   }
 }
 
@@ -690,27 +692,37 @@ __global__ __launch_bounds__(256) void k_lk_open_fix(const uint32_t* __restrict_
 // p + OFF are unlinked suffixes whose final slots are [s - D, s - D + size) (f(p) = ISA(p + OFF) + D maps the
 // members onto [s, s + size)), and with links from one round only every member shares the head's {OFF, D}
 __global__ __launch_bounds__(256) void k_lk_resolve(const uint4* __restrict__ grec, uint64_t g0, uint64_t g1,
-                                                    const uint64_t* __restrict__ lnk, const uint8_t* __restrict__ t,
+                                                    const uint32_t* __restrict__ lnk, const uint32_t* __restrict__ isa,
+                                                    uint32_t h, const uint8_t* __restrict__ t,
                                                     uint64_t n, uint32_t* __restrict__ sa, uint8_t* __restrict__ bwt,
                                                     unsigned int* __restrict__ flag) {
   bool bad = false;
   for (uint64_t g = g0 + (uint64_t)blockIdx.x * 256 + threadIdx.x; g < g1; g += (uint64_t)gridDim.x * 256) {
     const uint4 r = grec[g];
-    const uint64_t l = lnk[r.z];
-    const uint32_t off = (uint32_t)(l >> 32), ke = r.x - (uint32_t)l;
-    if ((uint64_t)ke + r.y > n || (uint64_t)r.x + r.y > n) {
+    const uint32_t v = isa[r.z];
+    const uint64_t off64 = (uint64_t)(v & ~LK_BIT) * h;
+    const uint32_t off = (uint32_t)off64, ke = r.x - lnk[r.z];
+    if (!(v & LK_BIT) || off64 >= n || (uint64_t)ke + r.y > n || (uint64_t)r.x + r.y > n) {
       bad = true;
       continue;
     }
-    for (uint32_t i = 0; i < r.y; ++i) {
-      const uint32_t q = sa[ke + i];
-      if (q < off) {
-        bad = true;
-        break;
+    for (uint32_t i0 = 0; i0 < r.y; i0 += 4) {   // four members' loads in flight together
+      uint32_t p[4];
+      uint8_t b[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) p[j] = i0 + j < r.y ? sa[ke + i0 + j] : off;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        bad |= p[j] < off;
+        p[j] = p[j] < off ? 0u : p[j] - off;
+        b[j] = i0 + j < r.y ? t[p[j] == 0 ? n - 1 : p[j] - 1] : (uint8_t)0;
       }
-      const uint32_t p = q - off;
-      sa[r.x + i] = p;
-      bwt[r.x + i] = t[p == 0 ? n - 1 : p - 1];
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (i0 + j < r.y) {
+          sa[r.x + i0 + j] = p[j];
+          bwt[r.x + i0 + j] = b[j];
+        }
     }
   }
   if (ballot64(bad) && (threadIdx.x & 63) == 0) atomicOr(flag, 2u);
@@ -815,11 +827,12 @@ std::pair<uint64_t, uint64_t> sr_items_round(Index& ix, int mode, SrRoundArgs<V>
 // ---- doubling links (host)
 void lk_begin(Index& ix) {
   const uint64_t n = ix.n;
-  ix.lk_lnk.ensure(n * 8 + 16);
-  ix.lk_gsz.ensure(n * 4 + 16);
+  ix.lk_lnk.ensure(n * 4 + 16);
+  ix.lk_gsz.ensure(n + 16);
   ix.sr_cnt.ensure(128);   // [4]: linked entries of a round, [9]: jump flags, [10]: linked groups
   ix.lk_grec.ensure((ix.dbl.A / 2 + 16) * sizeof(uint4));   // (a linked group has >= 2 members)
-  HK_HIP(hipMemsetAsync(ix.lk_gsz.p, 0, n * 4, ix.stream));
+  HK_HIP(hipMemsetAsync(ix.lk_gsz.p, 0, n, ix.stream));
+  HK_HIP(hipMemsetAsync(ix.lk_lnk.p, 0, n * 4, ix.stream));
   HK_HIP(hipMemsetAsync(ix.sr_cnt.as<unsigned long long>() + 10, 0, 8, ix.stream));
   ix.dbl.lround.clear();
   ix.dbl.nlinked = 0;
@@ -832,7 +845,7 @@ void lk_sizes(Index& ix, int slot, uint64_t A, uint64_t groups) {
   if (!groups) return;
   TimedLaunch tm(ix.timer, "sa_link", (double)groups * 12);
   k_lk_sizes<<<(unsigned)std::min<uint64_t>(ceil_div(groups, 256), 16384), 256, 0, ix.stream>>>(
-      ix.head_slot.as<uint32_t>(), ix.sr_hp[slot].as<uint32_t>(), groups, A, ix.n, ix.lk_gsz.as<uint32_t>());
+      ix.head_slot.as<uint32_t>(), ix.sr_hp[slot].as<uint32_t>(), groups, A, ix.n, ix.lk_gsz.as<uint8_t>());
   HK_HIP(hipGetLastError());
 }
 
@@ -851,7 +864,6 @@ void lk_after_round(Index& ix, uint64_t linked, uint32_t h) {
   const uint64_t n = ix.n;
   unsigned int* flag = reinterpret_cast<unsigned int*>(ix.sr_cnt.as<unsigned long long>() + 9);
   const unsigned g = (unsigned)std::min<uint64_t>(ceil_div(n, 256), 16384);
-  const uint32_t tagv = LK_BIT | ix.dbl.ltag;
   // this round's chains (all of offset h) inside LDS tiles, then across tiles
   const uint32_t R = LT_POS / h;
   const uint64_t T = (uint64_t)R * h, nt = ceil_div(n, T), m = nt * h;
@@ -861,7 +873,7 @@ void lk_after_round(Index& ix, uint64_t linked, uint32_t h) {
   uint64_t* nxt[2] = {tops + 3 * m, tops + 4 * m};
   {
     TimedLaunch tm(ix.timer, "sa_link", (double)n * 4 + (double)linked * 16);
-    k_lk_tile<<<(unsigned)nt, LT_T, 0, s>>>(ix.isa.as<uint32_t>(), ix.lk_lnk.as<uint64_t>(), n, h, tagv, R, tops);
+    k_lk_tile<<<(unsigned)nt, LT_T, 0, s>>>(ix.isa.as<uint32_t>(), ix.lk_lnk.as<uint32_t>(), n, h, R, tops);
     HK_HIP(hipGetLastError());
   }
   const unsigned gm = (unsigned)std::min<uint64_t>(ceil_div(m, 256), 16384);
@@ -884,7 +896,7 @@ void lk_after_round(Index& ix, uint64_t linked, uint32_t h) {
   }
   {
     TimedLaunch tm(ix.timer, "sa_link", (double)n * 4 + (double)linked * 16);
-    k_lk_open_fix<<<g, 256, 0, s>>>(ix.isa.as<uint32_t>(), ix.lk_lnk.as<uint64_t>(), n, h, tagv, R, acc[c], m);
+    k_lk_open_fix<<<g, 256, 0, s>>>(ix.isa.as<uint32_t>(), ix.lk_lnk.as<uint32_t>(), n, h, R, acc[c], m);
     HK_HIP(hipGetLastError());
   }
   ix.dbl.nlinked += linked;   // (every link names an unlinked position now)
@@ -899,7 +911,8 @@ void lk_resolve(Index& ix) {
   {
     TimedLaunch tm(ix.timer, "sa_link", (double)ng * 24 + (double)ix.dbl.nlinked * 9);
     k_lk_resolve<<<(unsigned)std::min<uint64_t>(ceil_div(ng, 256), 16384), 256, 0, s>>>(
-        ix.lk_grec.as<uint4>(), 0, ng, ix.lk_lnk.as<uint64_t>(), ix.text.as<uint8_t>(), n, ix.sa.as<uint32_t>(),
+        ix.lk_grec.as<uint4>(), 0, ng, ix.lk_lnk.as<uint32_t>(), ix.isa.as<uint32_t>(), ix.dbl.lk_h,
+        ix.text.as<uint8_t>(), n, ix.sa.as<uint32_t>(),
         ix.bwt.as<uint8_t>(), flag);
     HK_HIP(hipGetLastError());
   }

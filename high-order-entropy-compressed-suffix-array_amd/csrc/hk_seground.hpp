@@ -34,15 +34,16 @@ struct SrRoundArgs {
   uint32_t* hp_next;       // (nullable) the next round's plan: head entry of every new group, and
   uint32_t* win_next;      //   every window's {first, last} head entry (reset by sr_plan)
   // doubling links (nullable lnk: off).  A group whose members' keys are all ISA[p + h] = K (one tied group) and
-  // whose size equals that group's (gsz[K]) is a shifted copy of it: its members leave the list with
-  // lnk[p] = {h, own head slot - K} and isa[p] = LK_BIT | ltag, so ISA(p) = ISA(p + h) + delta at every later
-  // precision (csa/suffix_array.py:131-134: suffix p orders as suffix p + h inside the group).
-  uint64_t* lnk;
-  const uint32_t* gsz;
+  // whose size equals that group's (gsz[K], saturated at 255) is a shifted copy of it: its members leave the
+  // list with lnk[p] = own head slot - K (never 0); the chain pass then marks isa[p] = LK_BIT | hops and
+  // composes lnk, so ISA(p) = ISA(p + hops h) + lnk[p] at every later precision (csa/suffix_array.py:131-134:
+  // suffix p orders as suffix p + h inside the group).
+  uint32_t* lnk;
+  const uint8_t* gsz;
   unsigned long long* lcount;   // linked entries of the round
   unsigned long long* gcount;   // linked groups (all rounds): records grec[] = {head slot, size, head position}
   uint4* grec;
-  uint32_t h, ltag;
+  uint32_t h;
   int ib;                  // key bits below the group ordinal
 };
 
