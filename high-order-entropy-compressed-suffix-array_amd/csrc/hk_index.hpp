@@ -203,8 +203,9 @@ void synth_text(uint8_t* d_text, uint64_t n, const uint8_t* alphabet, int sigma,
                 uint8_t terminator, hipStream_t s);
 
 // queries (device-resident inputs and outputs)
+// (a pattern whose end offset precedes its start or passes `lim` is not read; it sets *d_bad)
 void query_count(Index& ix, const uint8_t* d_pats, const uint64_t* d_offs, uint64_t P,
-                 int64_t* d_lr, uint64_t* d_cnt);
+                 int64_t* d_lr, uint64_t* d_cnt, uint64_t lim, uint32_t* d_bad);
 void query_locate_gather(Index& ix, const int64_t* d_lr, const uint64_t* d_occ_offs, uint64_t P,
                          uint64_t* d_pos);
 void query_rank(Index& ix, const uint8_t* d_c, const uint64_t* d_i, uint64_t k, uint64_t* d_out);

@@ -654,8 +654,8 @@ template <int NC, int MODE = 0>
 __global__ __launch_bounds__(256) void k_count(WtView v, const uint8_t* __restrict__ pats,
                                                const uint64_t* __restrict__ offs, uint64_t P,
                                                int64_t* __restrict__ lr, uint64_t* __restrict__ cnt,
-                                               const ulonglong2* __restrict__ kmer, int K,
-                                               const uint4* __restrict__ ol = nullptr,
+                                               const ulonglong2* __restrict__ kmer, int K, uint64_t lim,
+                                               uint32_t* __restrict__ bad, const uint4* __restrict__ ol = nullptr,
                                                const uint64_t* __restrict__ osb = nullptr, uint64_t onsb = 0,
                                                NibView nv = NibView{}) {
   constexpr bool FLAT = MODE == 1, NIB = MODE == 2;
@@ -676,6 +676,11 @@ __global__ __launch_bounds__(256) void k_count(WtView v, const uint8_t* __restri
     uint64_t k = offs[p + 1];
     uint64_t xl = 0, xr = v.n;
     bool ok = true;
+    if (k < s || k > lim) {   // offsets out of order or past the pattern bytes: no read, the call fails
+      *bad = 1u;
+      ok = false;
+      k = s;
+    }
     if (K > 0 && k - s >= (uint64_t)K) {
       uint32_t idx = 0;
       for (int j = 0; j < K; ++j) {
@@ -1113,24 +1118,25 @@ void build_wt(Index& ix) {
 }
 
 void query_count(Index& ix, const uint8_t* d_pats, const uint64_t* d_offs, uint64_t P, int64_t* d_lr,
-                 uint64_t* d_cnt) {
+                 uint64_t* d_cnt, uint64_t lim, uint32_t* d_bad) {
   if (!ix.have_wt || ix.sharded) throw ApiError{-3, "count: wavelet tree not built"};
   if (!P) return;
   TimedLaunch t(ix.timer, "fm_count", 0.0);
   const ulonglong2* km = ix.kmer_k ? ix.kmer.as<ulonglong2>() : nullptr;
+  if (!d_bad) throw ApiError{-1, "count: no offsets flag"};
   if (ix.occ_ok)
     k_count<16, 1><<<grid_for(P, 256, 65535), 256, 0, ix.stream>>>(ix.view(), d_pats, d_offs, P, d_lr, d_cnt, km,
-                                                                    ix.kmer_k, ix.occ_lines.as<uint4>(),
+                                                                    ix.kmer_k, lim, d_bad, ix.occ_lines.as<uint4>(),
                                                                     ix.occ_sb.as<uint64_t>(), ix.occ_nsb);
   else if (ix.nib_ok)
     k_count<16, 2><<<grid_for(P, 256, 65535), 256, 0, ix.stream>>>(ix.view(), d_pats, d_offs, P, d_lr, d_cnt, km,
-                                                                    ix.kmer_k, nullptr, nullptr, 0, nib_view(ix));
+                                                                    ix.kmer_k, lim, d_bad, nullptr, nullptr, 0, nib_view(ix));
   else if (ix.sigma <= 16)
     k_count<16><<<grid_for(P, 256, 65535), 256, 0, ix.stream>>>(ix.view(), d_pats, d_offs, P, d_lr, d_cnt, km,
-                                                                 ix.kmer_k);
+                                                                 ix.kmer_k, lim, d_bad);
   else
     k_count<256><<<grid_for(P, 256, 65535), 256, 0, ix.stream>>>(ix.view(), d_pats, d_offs, P, d_lr, d_cnt, km,
-                                                                  ix.kmer_k);
+                                                                  ix.kmer_k, lim, d_bad);
   HK_HIP(hipGetLastError());
 }
 

@@ -19,6 +19,7 @@ i64p = C.POINTER(C.c_int64)
 vp = C.c_void_p
 
 
+E_INVALID = -1   # HKCSA_E_INVALID
 E_RANGE = -4   # HKCSA_E_RANGE
 
 

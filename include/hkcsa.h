@@ -179,7 +179,10 @@ int hkcsa_wt_golomb(hkcsa_index* ix, int depth, uint64_t nbits, uint32_t m_overr
 int hkcsa_rank(hkcsa_index* ix, const uint8_t* c, const uint64_t* i, uint64_t count, uint64_t* out);
 
 /* ---- batched queries -------------------------------------------------- */
-/* Patterns are concatenated bytes `pats` with offsets offs[0..P] (offs[0]=0).
+/* Patterns are concatenated bytes `pats` with offsets offs[0..P] (offs[0]=0,
+ * non-decreasing).  The two batch calls copy straight from and into the caller's
+ * (pageable) buffers and check the offsets on the device: offsets out of order
+ * return HKCSA_E_INVALID before any output is written.
  * count: lr_out[2p], lr_out[2p+1] = (l, r) of EnhancedFMIndex.find_range
  * (csa/enhanced_fm_index.py:21-32), (-1,-1) on a miss. */
 int hkcsa_count_batch(hkcsa_index* ix, const uint8_t* pats, const uint64_t* offs, uint64_t P,

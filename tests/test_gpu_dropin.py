@@ -191,6 +191,53 @@ def test_locate_batch_host_boundary():
     dev.close()
 
 
+def test_batch_calls_chunked_upload_and_bad_offsets():
+    """hkcsa_count_batch / hkcsa_locate_batch over 600,000 patterns (three upload chunks of 2^18, each counted
+    while the next one uploads) equal the device-resident query set on the same patterns, and the oracle on
+    the patterns at the chunk seams; offsets out of order or past offs[P] fail with HKCSA_E_INVALID (the
+    count kernel flags them, no pattern byte outside the batch is read) and leave the handle usable."""
+    import hkcsa
+    from hkcsa import _native as N
+    from hkcsa.index import _ptr
+    from oracle import oracle
+    text = oracle.synth_text(1 << 18, b"ACGT", seed=31)
+    dev = hkcsa.DeviceIndex.from_bytes(text, device=0)
+    dev.build_all()
+    rng = np.random.default_rng(5)
+    P = 600_000
+    lens = rng.integers(0, 13, P).astype(np.uint64)
+    starts = rng.integers(0, len(text) - 16, P)
+    offs = np.zeros(P + 1, np.uint64)
+    offs[1:] = np.cumsum(lens)
+    data = np.concatenate([np.asarray(text[s:s + int(k)]) for s, k in zip(starts[:P], lens)]).astype(np.uint8)
+    lr = np.empty(2 * P, np.int64)
+    assert dev.lib.hkcsa_count_batch(dev.h, _ptr(data), _ptr(offs), P, _ptr(lr)) == 0
+    q = dev.queries(data=data, offs=offs)
+    q.count()
+    want_lr = q.ranges().reshape(-1)
+    q_offs, q_pos = q.positions()
+    q.close()
+    assert np.array_equal(lr, want_lr)
+    occ, pos = dev.locate_batch(data, offs)
+    assert np.array_equal(occ, q_offs) and np.array_equal(pos, q_pos)
+    fm = oracle.FM(text)
+    seam = [i for c in (1 << 18, 2 << 18) for i in range(c - 3, c + 3)] + [0, P - 1]
+    pats = [data[int(offs[i]):int(offs[i + 1])].tobytes() for i in seam]
+    got = [list(map(int, pos[occ[i]:occ[i + 1]])) for i in seam]
+    assert got == fm.find(pats)
+    bad = offs.copy()
+    bad[400_000] = bad[400_002]                 # pattern 400,001 ends before it starts
+    assert dev.lib.hkcsa_count_batch(dev.h, _ptr(data), _ptr(bad), P, _ptr(lr)) == N.E_INVALID
+    occ2 = np.empty(P + 1, np.uint64)
+    assert dev.lib.hkcsa_locate_batch(dev.h, _ptr(data), _ptr(bad), P, _ptr(occ2), None, 0) == N.E_INVALID
+    bad = offs.copy()
+    bad[P - 1] = bad[P] + 64                    # past the last byte (and out of order with offs[P])
+    assert dev.lib.hkcsa_count_batch(dev.h, _ptr(data), _ptr(bad), P, _ptr(lr)) == N.E_INVALID
+    assert dev.lib.hkcsa_count_batch(dev.h, _ptr(data), _ptr(offs), P, _ptr(lr)) == 0
+    assert np.array_equal(lr, want_lr)
+    dev.close()
+
+
 def test_unicode_64MiB_text_remap():
     """A 64 MiB str with code points >= 256 (Cyrillic letters in English-like text, as a UTF-8 corpus read
     by tests/dataset_benchmark.py:22 would give) through EnhancedFMIndex (csa/enhanced_fm_index.py:8-13):
