@@ -151,12 +151,15 @@ __global__ __launch_bounds__(256) void k_refine_keys(const V* __restrict__ P, co
       // the usual case: both aligned 16-byte loads issued at once (one line fetch, not one per dependent word
       // load — with 10^8 random positions in flight the line is gone from L2 before a dependent second load),
       // then a 16-byte window from s by 64-bit funnel shifts
+      // The second chunk only when the qn symbols run past the first (English-like: qn ~ 5, so about a quarter of
+      // the suffixes; a second chunk across a line boundary is a second line fetch)
       const uint64_t a16 = s & ~15ull;
+      const uint32_t off = (uint32_t)(s & 15), r8 = (off & 7) * 8;
       const uint4 v0 = *reinterpret_cast<const uint4*>(t + a16);
-      const uint4 v1 = *reinterpret_cast<const uint4*>(t + a16 + 16);
+      uint4 v1 = make_uint4(0, 0, 0, 0);
+      if (off + (uint32_t)qn > 16) v1 = *reinterpret_cast<const uint4*>(t + a16 + 16);
       const uint64_t w0 = (uint64_t)v0.x | ((uint64_t)v0.y << 32), w1 = (uint64_t)v0.z | ((uint64_t)v0.w << 32);
       const uint64_t w2 = (uint64_t)v1.x | ((uint64_t)v1.y << 32), w3 = (uint64_t)v1.z | ((uint64_t)v1.w << 32);
-      const uint32_t off = (uint32_t)(s & 15), r8 = (off & 7) * 8;
       const uint64_t A0 = off >= 8 ? w1 : w0, B0 = off >= 8 ? w2 : w1, C0 = off >= 8 ? w3 : w2;
       const uint64_t W0 = r8 ? (A0 >> r8) | (B0 << (64 - r8)) : A0;
       const uint64_t W1 = r8 ? (B0 >> r8) | (C0 << (64 - r8)) : B0;
