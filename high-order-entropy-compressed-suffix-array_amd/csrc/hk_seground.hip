@@ -31,25 +31,76 @@ constexpr int SR_E = SR_CAP / SR_T;   // 8 entries per thread
 constexpr int SR_NW = SR_T / 64;
 constexpr uint32_t SR_NONE = 0xFFFFFFFFu;
 
-// heads: hp[G[a]] = a; first / last head of every window w (win[2w], win[2w + 1]; one atomic pair per wave)
-// (over list entries [lo, hi), lo a multiple of 64 — the list's front, or all of it)
+// heads: hp[G[a]] = a; first / last head of every window w (win[2w], win[2w + 1])
+// (over list entries [lo, hi), lo a multiple of SR_HB — the list's front, or all of it).  Four entries per
+// thread (one 16-byte load), the predecessor of a thread's first entry from the lane below, and one atomic
+// pair per block of SR_HB entries (a block lies in one window): the per-wave atomics on the same two words
+// serialised at the L2
+constexpr uint32_t SR_HB = 1024;
+static_assert(SR_W % SR_HB == 0, "a heads block lies in one window");
 __global__ __launch_bounds__(256) void k_sr_heads(const uint32_t* __restrict__ G, uint64_t lo, uint64_t hi,
                                                   uint32_t* __restrict__ hp, uint32_t* __restrict__ win) {
-  const uint32_t lane = threadIdx.x & 63;
-  for (uint64_t b = lo + (uint64_t)blockIdx.x * 256; b < hi; b += (uint64_t)gridDim.x * 256) {   // (uniform)
-    const uint64_t a = b + threadIdx.x;
-    bool head = false;
-    if (a < hi) {
-      const uint32_t g = G[a];
-      head = a == 0 || G[a - 1] != g;
-      if (head) hp[g] = (uint32_t)a;
+  __shared__ uint32_t rmin[4], rmax[4];
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  for (uint64_t b = lo + (uint64_t)blockIdx.x * SR_HB; b < hi; b += (uint64_t)gridDim.x * SR_HB) {   // (uniform)
+    const uint64_t a0 = b + 4ull * threadIdx.x;
+    uint32_t g[4];
+    if (a0 + 4 <= hi) {
+      const uint4 v = *reinterpret_cast<const uint4*>(G + a0);
+      g[0] = v.x;
+      g[1] = v.y;
+      g[2] = v.z;
+      g[3] = v.w;
+    } else {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) g[k] = a0 + k < hi ? G[a0 + k] : 0u;
     }
-    const uint64_t m = ballot64(head);
-    if (m) {   // a wave's 64 entries lie in one window (SR_W is a multiple of 64)
-      const uint64_t w0 = (b + (threadIdx.x & ~63u)) / SR_W;
-      if (lane == (uint32_t)__builtin_ctzll(m)) atomicMin(win + 2 * w0, (uint32_t)a);
-      if (lane == 63u - (uint32_t)__builtin_clzll(m)) atomicMax(win + 2 * w0 + 1, (uint32_t)a);
+    // the entry before a0: the lane below's last, lane 0 from memory
+    uint32_t prev = __shfl_up(g[3], 1, 64);
+    if (lane == 0 && a0 > 0 && a0 - 1 < hi) prev = G[a0 - 1];
+    uint32_t fmin = SR_NONE, fmax = 0;
+    bool any = false;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint64_t a = a0 + k;
+      const uint32_t before = k ? g[k - 1] : prev;
+      if (a < hi && (a == 0 || before != g[k])) {
+        hp[g[k]] = (uint32_t)a;
+        fmin = fmin == SR_NONE ? (uint32_t)a : fmin;
+        fmax = (uint32_t)a;
+        any = true;
+      }
     }
+    const uint64_t m = ballot64(any);
+    if (lane == 0) {
+      rmin[wv] = SR_NONE;
+      rmax[wv] = 0;
+    }
+    if (m) {
+      const uint32_t lf = (uint32_t)__builtin_ctzll(m), ll = 63u - (uint32_t)__builtin_clzll(m);
+      const uint32_t vmin = __shfl(fmin, (int)lf, 64), vmax = __shfl(fmax, (int)ll, 64);
+      if (lane == 0) {
+        rmin[wv] = vmin;
+        rmax[wv] = vmax;
+      }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      uint32_t bmin = SR_NONE, bmax = 0;
+      bool found = false;
+      for (int w = 0; w < 4; ++w)
+        if (rmin[w] != SR_NONE) {
+          bmin = bmin == SR_NONE ? rmin[w] : bmin;
+          bmax = rmax[w];
+          found = true;
+        }
+      if (found) {
+        const uint64_t w0 = b / SR_W;
+        atomicMin(win + 2 * w0, bmin);
+        atomicMax(win + 2 * w0 + 1, bmax);
+      }
+    }
+    __syncthreads();
   }
 }
 
@@ -750,9 +801,10 @@ static void sr_windows_reset(Index& ix, int slot, uint64_t A) {
 
 void sr_heads(Index& ix, int slot, const uint32_t* G, uint64_t lo, uint64_t hi, uint64_t A, uint64_t groups) {
   if (hi <= lo) return;
+  if (lo % SR_HB) throw ApiError{-1, "sr_heads: range start not block aligned"};
   ix.sr_hp[slot].ensure((groups + 1) * 4 + 16);
   TimedLaunch tm(ix.timer, "sa_round_plan", (double)(hi - lo) * 8);
-  const unsigned g = (unsigned)std::min<uint64_t>(ceil_div(hi - lo, 256), 16384);
+  const unsigned g = (unsigned)std::min<uint64_t>(ceil_div(hi - lo, (uint64_t)SR_HB), 8192);
   k_sr_heads<<<g, 256, 0, ix.stream>>>(G, lo, hi, ix.sr_hp[slot].as<uint32_t>(), ix.sr_win[slot].as<uint32_t>());
   HK_HIP(hipGetLastError());
 }
