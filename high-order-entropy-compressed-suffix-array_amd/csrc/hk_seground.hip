@@ -724,18 +724,32 @@ __global__ __launch_bounds__(256) void k_lk_open_fix(uint32_t* __restrict__ isa,
                                                      uint64_t n, uint32_t h, uint32_t R,
                                                      const uint64_t* __restrict__ acc, uint64_t m) {
   const uint64_t T = (uint64_t)R * h;
-  for (uint64_t p = (uint64_t)blockIdx.x * 256 + threadIdx.x; p < n; p += (uint64_t)gridDim.x * 256) {
-    const uint32_t v = isa[p];
-    if (!(v & LK_BIT)) continue;
-    const uint64_t hops = v & ~LK_BIT;
-    const uint64_t q = p + hops * h;
-    const uint64_t t = p / T;
-    if (q < (t + 1) * T) continue;   // closed inside the tile
-    const uint64_t e = (t + 1) * h + (p % T) % h;
-    if (e >= m) continue;            // (never: a run cannot leave the text)
-    const uint64_t b = acc[e];
-    isa[p] = LK_BIT | (uint32_t)(hops + (b >> 32));
-    lnk[p] += (uint32_t)b;
+  // four positions per thread (one 16-byte load of the ISA marks); most positions are unlinked or closed
+  const uint64_t nq = (n + 3) / 4;
+  for (uint64_t qd = (uint64_t)blockIdx.x * 256 + threadIdx.x; qd < nq; qd += (uint64_t)gridDim.x * 256) {
+    const uint64_t p0 = 4 * qd;
+    uint32_t v[4];
+    if (p0 + 4 <= n) {
+      const uint4 w = *reinterpret_cast<const uint4*>(isa + p0);
+      v[0] = w.x; v[1] = w.y; v[2] = w.z; v[3] = w.w;
+    } else {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) v[k] = p0 + k < n ? isa[p0 + k] : 0u;
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint64_t p = p0 + k;
+      if (!(v[k] & LK_BIT)) continue;
+      const uint64_t hops = v[k] & ~LK_BIT;
+      const uint64_t q = p + hops * h;
+      const uint64_t t = p / T;
+      if (q < (t + 1) * T) continue;   // closed inside the tile
+      const uint64_t e = (t + 1) * h + (p % T) % h;
+      if (e >= m) continue;            // (never: a run cannot leave the text)
+      const uint64_t b = acc[e];
+      isa[p] = LK_BIT | (uint32_t)(hops + (b >> 32));
+      lnk[p] += (uint32_t)b;
+    }
   }
 }
 
@@ -915,7 +929,6 @@ void lk_after_round(Index& ix, uint64_t linked, uint32_t h) {
   hipStream_t s = ix.stream;
   const uint64_t n = ix.n;
   unsigned int* flag = reinterpret_cast<unsigned int*>(ix.sr_cnt.as<unsigned long long>() + 9);
-  const unsigned g = (unsigned)std::min<uint64_t>(ceil_div(n, 256), 16384);
   // this round's chains (all of offset h) inside LDS tiles, then across tiles
   const uint32_t R = LT_POS / h;
   const uint64_t T = (uint64_t)R * h, nt = ceil_div(n, T), m = nt * h;
@@ -948,7 +961,7 @@ void lk_after_round(Index& ix, uint64_t linked, uint32_t h) {
   }
   {
     TimedLaunch tm(ix.timer, "sa_link", (double)n * 4 + (double)linked * 16);
-    k_lk_open_fix<<<g, 256, 0, s>>>(ix.isa.as<uint32_t>(), ix.lk_lnk.as<uint32_t>(), n, h, R, acc[c], m);
+    k_lk_open_fix<<<(unsigned)std::min<uint64_t>(ceil_div(n, 1024), 16384), 256, 0, s>>>(ix.isa.as<uint32_t>(), ix.lk_lnk.as<uint32_t>(), n, h, R, acc[c], m);
     HK_HIP(hipGetLastError());
   }
   ix.dbl.nlinked += linked;   // (every link names an unlinked position now)
