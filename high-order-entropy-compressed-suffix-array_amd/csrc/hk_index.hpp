@@ -104,6 +104,7 @@ struct Index {
   DevBuf keys[2], vals[2];
   DevBuf isa;
   DevBuf act[2][3];            // P, J, G of the active list (double-buffered)
+  DevBuf act_b;                // BWT bytes of the first refinement round's list (global path), list order
   DevBuf head_slot;            // SA slot of each tied group's head (refinement -> doubling switch)
   DevBuf ties_k, ties_v, ties_n;   // unordered tie list of the bucket build (J<<1|head, P), count
   DevBuf big_k[2], big_v[2], big_j; // big buckets of the bucket build (sorted on the global path); the
@@ -297,7 +298,8 @@ void build_slice_keyed(Index& ix, uint32_t c_lo, uint32_t c_hi, uint64_t m);
 template <typename V>
 void refine_from_ties(Index& ix, const KeyGeom& kg, uint64_t A, bool allow_doubling);
 template <typename V>
-void refine_loop(Index& ix, const KeyGeom& kg, int cur, uint64_t A, uint64_t groups, bool allow_doubling);
+void refine_loop(Index& ix, const KeyGeom& kg, int cur, uint64_t A, uint64_t groups, bool allow_doubling,
+                 const uint8_t* B0 = nullptr);
 
 // Prefix doubling over the tied suffixes (hk_sa.hip).  allow_doubling = true above runs it locally
 // (single GPU: ISA from the full SA); with false, refine_loop stops after its chunk rounds with

@@ -597,7 +597,7 @@ __global__ __launch_bounds__(GR_T) void k_refine_apply_rows(
     int cs, const uint64_t* __restrict__ act_off, const uint64_t* __restrict__ head_off, V* __restrict__ sa,
     uint8_t* __restrict__ bwt, const uint8_t* __restrict__ inv, uint64_t pmask, const uint8_t* __restrict__ t,
     uint64_t n, V* __restrict__ oP, uint32_t* __restrict__ oJ, uint32_t* __restrict__ oG,
-    uint32_t* __restrict__ head_slot) {
+    uint32_t* __restrict__ head_slot, uint8_t* __restrict__ oB) {
   __shared__ uint32_t wc[2][GR_T / 64];
   __shared__ uint8_t INV[512];
   if (FROM_KEY) {
@@ -612,6 +612,7 @@ __global__ __launch_bounds__(GR_T) void k_refine_apply_rows(
     const uint64_t j = tbase + (uint64_t)k * GR_T + threadIdx.x;
     const bool valid = j < A;
     uint32_t a = 0, th = 0, jv = 0;
+    uint8_t bc = 0;
     V p = 0;
     if (valid) {
       bool h, hn;
@@ -621,7 +622,10 @@ __global__ __launch_bounds__(GR_T) void k_refine_apply_rows(
       th = a && h ? 1u : 0u;
       jv = FROM_KEY ? (uint32_t)j : (J ? J[j] : (uint32_t)j);
       if (!FROM_KEY || a) p = P[j];
-      if (FROM_KEY && bwt) bwt[j] = INV[(uint32_t)(cur & pmask)];
+      if (FROM_KEY) {
+        bc = INV[(uint32_t)(cur & pmask)];
+        if (bwt) bwt[j] = bc;
+      }
     }
     const uint32_t ci = dpp_incl_sum(a | th << 16);
     if (lane == 63) wc[k & 1][w] = ci;
@@ -642,6 +646,7 @@ __global__ __launch_bounds__(GR_T) void k_refine_apply_rows(
         oP[o] = p;
         oJ[o] = jv;
         oG[o] = (uint32_t)(g - 1);
+        if (FROM_KEY && oB) oB[o] = bc;   // (the tied suffix's BWT byte travels with it to the next round)
       } else if (!FROM_KEY && bwt) {
         bwt[jv] = t[p == 0 ? n - 1 : (uint64_t)p - 1];
       }
@@ -939,7 +944,8 @@ template <typename V>
 std::pair<uint64_t, uint64_t> refine_step(Index& ix, const KeyGeom& kg, const uint64_t* keys, const V* P,
                                           const uint32_t* J, uint64_t A, int cs, bool from_key, bool write_sa,
                                           V* oP, uint32_t* oJ, uint32_t* oG, uint32_t* head_slot,
-                                          const unsigned int* d_flag = nullptr, unsigned int* h_flag = nullptr);
+                                          const unsigned int* d_flag = nullptr, unsigned int* h_flag = nullptr,
+                                          uint8_t* oB = nullptr);
 
 // One round's sort + regroup through LDS items of whole groups (hk_seground.hip).  The round's keys (G in the
 // top bits) and positions are in keys[0] / vals[0], list act[cur]; the next list goes to act[cur ^ 1].  The
@@ -949,7 +955,7 @@ std::pair<uint64_t, uint64_t> refine_step(Index& ix, const KeyGeom& kg, const ui
 // (ISA).  Returns the next list's (tied, groups).
 template <typename V>
 std::pair<uint64_t, uint64_t> seg_round(Index& ix, const KeyGeom& kg, int mode, int cur, uint64_t A, uint64_t groups,
-                                        int bits, int ib) {
+                                        int bits, int ib, const uint8_t* lB = nullptr) {
   hipStream_t s = ix.stream;
   uint64_t* const k0 = ix.keys[0].as<uint64_t>();
   V* const v0 = ix.vals[0].as<V>();
@@ -1014,6 +1020,7 @@ std::pair<uint64_t, uint64_t> seg_round(Index& ix, const KeyGeom& kg, int mode, 
   a.sa = ix.sa.as<V>();
   a.bwt = ix.bwt.as<uint8_t>();
   a.t = ix.text.as<uint8_t>();
+  a.B = mode == 0 ? lB : nullptr;
   a.n = ix.n;
   a.isa = mode ? ix.isa.as<V>() : nullptr;
   a.lo = ix.sharded ? ix.shard_lo : 0;
@@ -1123,7 +1130,7 @@ template <typename V>
 std::pair<uint64_t, uint64_t> refine_step(Index& ix, const KeyGeom& kg, const uint64_t* keys, const V* P,
                                           const uint32_t* J, uint64_t A, int cs, bool from_key, bool write_sa,
                                           V* oP, uint32_t* oJ, uint32_t* oG, uint32_t* head_slot,
-                                          const unsigned int* d_flag, unsigned int* h_flag) {
+                                          const unsigned int* d_flag, unsigned int* h_flag, uint8_t* oB) {
   hipStream_t s = ix.stream;
   const uint64_t nt = ceil_div(A, GR_TILE);
   ix.tile_b.ensure((nt + 1) * 4);
@@ -1144,11 +1151,11 @@ std::pair<uint64_t, uint64_t> refine_step(Index& ix, const KeyGeom& kg, const ui
     if (from_key)
       k_refine_apply_rows<V, true><<<(unsigned)nt, GR_T, 0, s>>>(
           keys, P, J, A, cs, ix.tile_a.as<uint64_t>(), ix.tile_d.as<uint64_t>(), write_sa ? ix.sa.as<V>() : nullptr,
-          bwt, inv, (1ull << kg.pb) - 1, ix.text.as<uint8_t>(), ix.n, oP, oJ, oG, head_slot);
+          bwt, inv, (1ull << kg.pb) - 1, ix.text.as<uint8_t>(), ix.n, oP, oJ, oG, head_slot, oB);
     else
       k_refine_apply_rows<V, false><<<(unsigned)nt, GR_T, 0, s>>>(
           keys, P, J, A, cs, ix.tile_a.as<uint64_t>(), ix.tile_d.as<uint64_t>(), write_sa ? ix.sa.as<V>() : nullptr,
-          bwt, inv, 0, ix.text.as<uint8_t>(), ix.n, oP, oJ, oG, head_slot);
+          bwt, inv, 0, ix.text.as<uint8_t>(), ix.n, oP, oJ, oG, head_slot, nullptr);
     HK_HIP(hipGetLastError());
   }
   uint64_t* const tot = ix.rb();
@@ -1243,7 +1250,8 @@ void upload_geometry(Index& ix, const KeyGeom& kg) {
 }
 
 template <typename V>
-void refine_loop(Index& ix, const KeyGeom& kg, int cur, uint64_t A, uint64_t groups, bool allow_doubling);
+void refine_loop(Index& ix, const KeyGeom& kg, int cur, uint64_t A, uint64_t groups, bool allow_doubling,
+                 const uint8_t* B0);
 
 // Refinement of tied groups after the initial sort of m suffixes (their sorted keys in keys[slot],
 // positions in vals[slot] — which the caller has adopted as ix.sa).  With allow_doubling (single
@@ -1259,18 +1267,21 @@ void refine_after_sort(Index& ix, const KeyGeom& kg, int slot, uint64_t m, bool 
   ix.head_slot.ensure(m * 4 + 16);
   ix.bwt.ensure(m + 64);
   // initial round: keys compared without the prev field; SA already in place; BWT from keys
+  // (the tied suffixes' BWT bytes, from the keys' prev field, travel with the list into the first chunk round)
+  ix.act_b.ensure(m + 16);
   auto r0 = refine_step<V>(ix, kg, kp[slot], ix.sa.as<V>(), nullptr, m, kg.pb, true, false,
                            ix.act[0][0].as<V>(), ix.act[0][1].as<uint32_t>(), ix.act[0][2].as<uint32_t>(),
-                           ix.head_slot.as<uint32_t>());
+                           ix.head_slot.as<uint32_t>(), nullptr, nullptr, ix.act_b.as<uint8_t>());
   ix.info.push_back(r0.first);
-  refine_loop<V>(ix, kg, 0, r0.first, r0.second, allow_doubling);
+  refine_loop<V>(ix, kg, 0, r0.first, r0.second, allow_doubling, ix.act_b.as<uint8_t>());
 }
 
 // The tied suffixes (P, J = SA slot, G = dense group ordinal in list order: whole groups in any order,
 // each one's slots contiguous and ascending along the list) are in act[cur];
 // each round sorts them by (G, next symbols from offset h) and re-groups.
 template <typename V>
-void refine_loop(Index& ix, const KeyGeom& kg, int cur, uint64_t A, uint64_t groups, bool allow_doubling) {
+void refine_loop(Index& ix, const KeyGeom& kg, int cur, uint64_t A, uint64_t groups, bool allow_doubling,
+                 const uint8_t* B0) {
   hipStream_t s = ix.stream;
   ix.sr_plan_g = nullptr;   // (the list in act[cur] came from another producer)
   const uint16_t* d_lut = reinterpret_cast<const uint16_t*>(ix.small.as<uint8_t>() + 2048);
@@ -1314,7 +1325,8 @@ void refine_loop(Index& ix, const KeyGeom& kg, int cur, uint64_t A, uint64_t gro
     }
     // sort inside each group + regroup: LDS items of whole groups, the groups of over SR_W members by a
     // global radix sort first (seg_round)
-    const std::pair<uint64_t, uint64_t> r = seg_round<V>(ix, kg, 0, cur, A, groups, 64, 0);
+    // (B0: the BWT bytes of this list, the first round's only)
+    const std::pair<uint64_t, uint64_t> r = seg_round<V>(ix, kg, 0, cur, A, groups, 64, 0, rounds == 1 ? B0 : nullptr);
     cur ^= 1;
     A = r.first;
     groups = r.second;
@@ -1368,8 +1380,8 @@ std::pair<uint64_t, uint64_t> refine_step_u32(Index& ix, const KeyGeom& kg, cons
   return refine_step<uint32_t>(ix, kg, keys, P, J, A, cs, false, true, oP, oJ, oG, ix.head_slot.as<uint32_t>());
 }
 
-template void refine_loop<uint32_t>(Index&, const KeyGeom&, int, uint64_t, uint64_t, bool);
-template void refine_loop<uint64_t>(Index&, const KeyGeom&, int, uint64_t, uint64_t, bool);
+template void refine_loop<uint32_t>(Index&, const KeyGeom&, int, uint64_t, uint64_t, bool, const uint8_t*);
+template void refine_loop<uint64_t>(Index&, const KeyGeom&, int, uint64_t, uint64_t, bool, const uint8_t*);
 
 // ---------------------------------------------------------------- prefix doubling steps
 void dbl_ensure_isa(Index& ix) { ix.isa.ensure(ix.n * (ix.sa_pos64 ? 8 : 4) + 16); }
@@ -1661,6 +1673,7 @@ void release_workspace(Index& ix) {
     ix.vals[i].release();
     ix.seq[i].release();
     for (int k = 0; k < 3; ++k) ix.act[i][k].release();
+    if (i == 0) ix.act_b.release();
   }
   ix.isa.release();
   ix.head_slot.release();

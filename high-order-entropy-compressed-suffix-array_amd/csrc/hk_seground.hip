@@ -230,6 +230,8 @@ __global__ __launch_bounds__(SR_T, 4) void k_sr_round(SrRoundArgs<V> a) {
   const bool links = P32 && MODE == 1 && a.lnk != nullptr;
   uint64_t kor = 0, kand = ~0ull;
   uint32_t jr[SR_E], pr[SR_E];
+  const bool hasB = MODE == 0 && a.B != nullptr;
+  uint32_t bq[(SR_E + 3) / 4] = {};   // the entries' BWT bytes (hasB), four per register
 #pragma unroll
   for (int k = 0; k < SR_E; ++k) {
     const uint32_t i = (uint32_t)k * SR_T + tid;
@@ -241,6 +243,7 @@ __global__ __launch_bounds__(SR_T, 4) void k_sr_round(SrRoundArgs<V> a) {
       sh.u.g[i] = a.G[base + i];
       jr[k] = a.J[base + i];
       if constexpr (P32) pr[k] = (uint32_t)a.vals[base + i];
+      if (hasB) bq[k >> 2] |= (uint32_t)a.B[base + i] << (8 * (k & 3));
       kor |= key;
       kand &= key;
     }
@@ -389,11 +392,16 @@ __global__ __launch_bounds__(SR_T, 4) void k_sr_round(SrRoundArgs<V> a) {
   }
   __syncthreads();
   const uint16_t* const ord = sh.u.idx[cur];
-  if constexpr (P32) {   // (the match masks are done with: their space takes the positions)
+  // (the other order buffer is free now: it takes the BWT bytes in entry order)
+  uint8_t* const bst = reinterpret_cast<uint8_t*>(sh.u.idx[cur ^ 1]);
+  if (P32 || hasB) {   // (the match masks are done with: their space takes the positions)
 #pragma unroll
     for (int k = 0; k < SR_E; ++k) {
       const uint32_t i = (uint32_t)k * SR_T + tid;
-      if (i < m) sh.m.pl[i] = pr[k];
+      if (i < m) {
+        if constexpr (P32) sh.m.pl[i] = pr[k];
+        if (hasB) bst[i] = (uint8_t)(bq[k >> 2] >> (8 * (k & 3)));
+      }
     }
     __syncthreads();
   }
@@ -560,7 +568,7 @@ __global__ __launch_bounds__(SR_T, 4) void k_sr_round(SrRoundArgs<V> a) {
         }
       } else {
         if (MODE == 1) a.sa[slot] = (V)p;
-        a.bwt[slot] = a.t[p == 0 ? a.n - 1 : p - 1];
+        a.bwt[slot] = hasB ? bst[ord[i]] : a.t[p == 0 ? a.n - 1 : p - 1];
       }
     }
   }

@@ -27,6 +27,7 @@ struct SrRoundArgs {
   V* sa;
   uint8_t* bwt;
   const uint8_t* t;
+  const uint8_t* B;         // (nullable, chunk rounds) the entries' BWT bytes in list order: no text gather
   uint64_t n;
   V* isa;                  // doubling: ISA (single GPU or one-GPU slices; global slot = lo + slot)
   uint64_t lo;
