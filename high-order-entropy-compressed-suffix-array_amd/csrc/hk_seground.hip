@@ -10,7 +10,7 @@
 //   * windows of SR_W list entries; item w = the groups whose head lies in window w, except a last group of
 //     more than SR_W members (a "big" group, k_sr_items) — so an item holds fewer than 2 * SR_W entries;
 //   * one workgroup per item (k_sr_round): the item's keys and positions are staged in LDS and sorted there
-//     — one thread per group when no group has more than 16 members (pairs dominate late doubling rounds),
+//     — one thread per group when no group has more than SR_NET (8) members (pairs dominate late doubling rounds),
 //     else stable LSD passes of 8 bits over only the bits that vary inside the item — then regrouped in
 //     the same workgroup: settled suffixes write their SA / BWT entries, tied ones are appended to the
 //     next list through one 64-bit atomic per item (entries | groups << 33, so both are reserved in one
@@ -29,6 +29,9 @@ namespace {
 constexpr int SR_T = 512;
 constexpr int SR_E = SR_CAP / SR_T;   // 8 entries per thread
 constexpr int SR_NW = SR_T / 64;
+// the largest group a thread sorts in registers (bitonic network); an item with a larger group takes the LDS
+// radix passes.  8, not 16: the 16-key network needs 113-123 VGPRs, over the 80 that three workgroups per CU allow
+constexpr int SR_NET = 8;
 constexpr uint32_t SR_NONE = 0xFFFFFFFFu;
 
 // heads: hp[G[a]] = a; first / last head of every window w (win[2w], win[2w + 1])
@@ -216,7 +219,7 @@ constexpr int RG_TIED = 36, RG_RH = 37, RG_FIRST = 38;
 // MODE 0: chunk refinement round (every slot's SA entry written, settled suffixes' BWT); MODE 1: prefix
 // doubling round (ISA of every member = its new group's head slot; SA / BWT of the settled ones)
 template <typename V, int MODE>
-__global__ __launch_bounds__(SR_T, 4) void k_sr_round(SrRoundArgs<V> a) {
+__global__ __launch_bounds__(SR_T, 6) void k_sr_round(SrRoundArgs<V> a) {
   __shared__ SrShared sh;
   const uint2 it = a.items[blockIdx.x];
   const uint32_t m = it.y;
@@ -267,7 +270,7 @@ __global__ __launch_bounds__(SR_T, 4) void k_sr_round(SrRoundArgs<V> a) {
     const bool h = i >= m || i == 0 || sh.u.g[i] != sh.u.g[i - 1];
     const uint64_t hb = ballot64(h);
     if (lane == 0) sh.hmask[i >> 6] = hb;
-    if (i < m && i >= 16 && sh.u.g[i] == sh.u.g[i - 16]) big = 1;   // a group of more than 16 members
+    if (i < m && i >= SR_NET && sh.u.g[i] == sh.u.g[i - SR_NET]) big = 1;   // a group of more than SR_NET members
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
@@ -325,7 +328,7 @@ __global__ __launch_bounds__(SR_T, 4) void k_sr_round(SrRoundArgs<V> a) {
       } else if (sz > 2 && sz <= 4) {
         sr_net<4>(sh.key, sh.u.idx[0], i, sz);
       } else if (sz > 4) {
-        sr_net<16>(sh.key, sh.u.idx[0], i, sz);
+        sr_net<SR_NET>(sh.key, sh.u.idx[0], i, sz);
       }
     }
   } else if (vary) {

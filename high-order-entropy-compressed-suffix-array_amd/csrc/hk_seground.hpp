@@ -8,7 +8,11 @@
 
 namespace hk {
 
-constexpr int SR_W = 2048;          // list entries per window; an item = the groups whose head is in one window
+// list entries per window; an item = the groups whose head is in one window.  1024 (51 KB of LDS per item
+// workgroup) lets three 512-thread workgroups share a CU where 2048 (76 KB) allowed two: English-like 200 MiB
+// 57.0-57.7 -> 56.4 ms per step, protein-like 1 GiB 125.3 -> 123.3 ms (the groups of 1025-2048 members move to
+// the global big-group sort)
+constexpr int SR_W = 1024;
 constexpr int SR_CAP = 2 * SR_W;    // an item holds fewer entries than this
 
 template <typename V>
