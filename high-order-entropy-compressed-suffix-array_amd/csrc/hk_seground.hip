@@ -603,7 +603,7 @@ __global__ __launch_bounds__(256) void k_lk_sizes(const uint32_t* __restrict__ h
 // the next tile's top row: those tile tops (ntiles x h entries) are pointer-jumped as a small array and added to
 // the open runs afterwards (k_lk_open_fix).  One dense pass instead of log(chain) passes over every position.
 constexpr int LT_T = 256;
-constexpr uint32_t LT_POS = 8192;
+constexpr uint32_t LT_POS = 4096;   // (25 KB of LDS: six tile workgroups per CU; links need h <= LT_POS)
 constexpr uint32_t LT_OPEN = 0x80000000u, LT_OPEN16 = 0x8000u;   // (run rows <= LT_POS < 2^15)
 
 __device__ __forceinline__ uint64_t lk_cv(uint32_t k, uint32_t d, bool open) {

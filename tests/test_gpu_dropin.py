@@ -205,11 +205,14 @@ def test_batch_calls_chunked_upload_and_bad_offsets():
     dev.build_all()
     rng = np.random.default_rng(5)
     P = 600_000
-    lens = rng.integers(0, 13, P).astype(np.uint64)
+    lens = rng.integers(8, 17, P).astype(np.uint64)   # (short patterns would each locate a large share of all n suffixes)
     starts = rng.integers(0, len(text) - 16, P)
     offs = np.zeros(P + 1, np.uint64)
     offs[1:] = np.cumsum(lens)
-    data = np.concatenate([np.asarray(text[s:s + int(k)]) for s, k in zip(starts[:P], lens)]).astype(np.uint8)
+    tot = int(offs[-1])
+    src = np.repeat(starts, lens.astype(np.int64)) + (np.arange(tot) - np.repeat(offs[:-1].astype(np.int64),
+                                                                                lens.astype(np.int64)))
+    data = np.ascontiguousarray(np.asarray(text)[src], dtype=np.uint8)
     lr = np.empty(2 * P, np.int64)
     assert dev.lib.hkcsa_count_batch(dev.h, _ptr(data), _ptr(offs), P, _ptr(lr)) == 0
     q = dev.queries(data=data, offs=offs)
