@@ -1,8 +1,9 @@
 """Drop-in for the reference's csa/suffix_array.py.
 
 build_suffix_array(text) (:131-134) returns the suffix array of `text` in
-Python str order (no sentinel added), computed by the GPU prefix-doubling radix
-sort.  ksa(T) (:46-129) is the reference's DC3 attempt; it is only correct when
+Python str order (no sentinel added), computed on the GPU by hkcsa_build_sa (the
+keyed bucket build: cursor partition passes and LDS bucket sorts, tied suffixes
+refined in LDS items, prefix doubling for repetitive text).  ksa(T) (:46-129) is the reference's DC3 attempt; it is only correct when
 its recursion is not needed (and raises TypeError otherwise),
 and whenever it returns it equals build_suffix_array(T) — so the drop-in returns
 the suffix array for every input.  Unlike the reference, importing this module

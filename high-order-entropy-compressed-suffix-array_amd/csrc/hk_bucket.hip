@@ -52,7 +52,8 @@ __device__ __forceinline__ void bh_add(uint32_t* H, uint32_t b, unsigned long lo
   }
 }
 
-// Workgroup w covers the positions [w*span, (w+1)*span) (span a multiple of BH_TILE).
+// Workgroup w covers the positions [w*stride, w*stride + span) (span and stride multiples of BH_TILE;
+// stride = 0: span, the whole text; a larger stride samples spans spread over the text).
 // DIG (HQ only): only the low 8 bits of the bucket — the first LSD pass's digit — into per-wave
 // 256-bin LDS histograms (the bucket counts come from the sorted keys afterwards, k_bin_starts).
 template <bool HQ, bool DIG = false>
@@ -60,7 +61,7 @@ __global__ __launch_bounds__(BH_T, 1) void k_bucket_hist(const uint8_t* __restri
                                                          const uint16_t* __restrict__ lutk,
                                                          const uint64_t* __restrict__ skey, KeyedArgs g, int bsh,
                                                          int D, unsigned long long* __restrict__ hist,
-                                                         uint64_t span) {
+                                                         uint64_t span, uint64_t stride = 0) {
   __shared__ uint32_t H[DIG ? 1 : 32768];
   __shared__ uint32_t HD[DIG ? BH_T / 64 : 1][256];
   __shared__ uint16_t c[HQ ? 1 : BH_STAGE + kCodePad];
@@ -78,7 +79,7 @@ __global__ __launch_bounds__(BH_T, 1) void k_bucket_hist(const uint8_t* __restri
   if (tid < 72) SK[tid] = skey[tid];
   __syncthreads();
   const uint64_t lim = n < g.s_start ? n : g.s_start;   // positions with a text window
-  const uint64_t lo = (uint64_t)blockIdx.x * span;
+  const uint64_t lo = (uint64_t)blockIdx.x * (stride ? stride : span);
   const uint64_t hi = lo + span < n ? lo + span : n;
   if (HQ) {
     const int lb = 31 - __clz((uint32_t)g.Rk);
@@ -2672,6 +2673,432 @@ __global__ __launch_bounds__(T, (T * I <= 9216 ? 2 : 1) * T / 256) void k_bucket
   }
 }
 
+// ---- record-plane sort (k_bucket_sort_rec): the 1 GiB sigma <= 8 headline's items
+// One 512-thread workgroup per item of <= BR_CAP suffixes, packed records whose sym field lies in the high
+// word (X32), u32 positions, prev codes of <= 3 bits.  The fast path above moves a suffix through four
+// planes (u32 position by slot, u32 record by bin, u16 final index by slot, then u32 position and u16 prev
+// code by final index): five random LDS accesses and ~9 barriers per item.  Here the record itself is
+// the unit: the item's sym range fixes all but `width` key bits, the top 13 of them pick one of 8192 bins
+// (u8 counters: the atomic's return is the rank inside the bin), and the record goes to its bin as ONE u64
+// whose sym field is replaced by the key bits below the bin: (low key << xsh) | prev code << pbits |
+// position.  Each record's owner then ranks it inside its bin by plain u64 compares with the bin's
+// records (the low key decides; equal low keys are equal keys; ~2/3 of iid suffixes share their bin
+// with at most one other), moves it there if the rank changed, and the plane - now at final index + the
+// SA pointer's misalignment - is written out as aligned 16-B SA / 4-B BWT groups.  Phase cycles at 1 GiB
+// (HKCSA_BS_TRACE=1): see DESIGN.md section 4.  The u8 counters need bins of < 64 records and
+// groups of < 256 (checked by the counts' total and bit tests); items outside that, or with local keys
+// wider than 30 bits, go to the LSD passes (fb).  LDS: 81,904 B, two workgroups per CU.
+constexpr int BR_T = 512, BR_I = 18;
+constexpr uint32_t BR_CAP = 9056;                 // suffixes per item (the 512-thread items' plan cap)
+constexpr int BR_BITS = 13, BR_BINS = 1 << BR_BITS, BR_NG = BR_BINS / 16;   // 16 bins per group, a group per thread
+static_assert(BR_NG == BR_T, "one bin group per thread");
+static_assert(BR_CAP <= (uint32_t)BR_T * BR_I, "capacity within the threads' slots");
+
+struct alignas(16) BrShared {
+  uint64_t rec[BR_CAP + 4];        // records at final index + al (al < 4)
+  uint32_t cnt[BR_BINS / 4];       // u8 bin counters, then in-group exclusive prefixes
+  uint16_t base[BR_NG + 8];        // group starts (+ al); [BR_NG] = count + al; [BR_NG + 4 ..] code table
+  uint32_t scr[48];                // reductions / wave totals / failure flags / tie base
+};
+static_assert(sizeof(BrShared) <= 81920, "two workgroups per CU");
+
+template <typename V, bool TRACE = false>
+__global__ __launch_bounds__(BR_T, 4) void k_bucket_sort_rec(const uint64_t* __restrict__ keys,
+                                                          const uint2* __restrict__ items,
+                                                          const uint8_t* __restrict__ inv, V* __restrict__ sa,
+                                                          uint8_t* __restrict__ bwt, uint64_t* __restrict__ tie_k,
+                                                          V* __restrict__ tie_v,
+                                                          unsigned long long* __restrict__ tie_n,
+                                                          uint2* __restrict__ fb, unsigned int* __restrict__ fb_n,
+                                                          PkGeom pg, uint64_t* __restrict__ trace = nullptr) {
+  static_assert(sizeof(V) == 4, "u32 positions");
+  __shared__ BrShared sh;
+  uint64_t ts[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (TRACE) ts[0] = stamp();
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const uint2 it = items[blockIdx.x];
+  const uint32_t start = it.x, cnt = it.y;
+  const int pbits = pg.pbits, pb = pg.pb2, xsh = pbits + pb;   // xsh >= 32 (X32)
+  // the BWT byte of each keyed prev code (codes at or above the unique terminal's shift up by one)
+  const bool remap = pg.tcode >= 0;
+  uint8_t* const tab = reinterpret_cast<uint8_t*>(sh.base + BR_NG + 4);
+  const uint32_t s0 = wv * (BR_I * 64) + lane;   // slot k of this thread: s0 + 64 k
+  uint64_t key[BR_I];
+  uint32_t vmask = 0;
+#pragma unroll
+  for (int k = 0; k < BR_I; ++k) {
+    const bool valid = s0 + 64u * k < cnt;
+    key[k] = valid ? keys[start + s0 + 64u * k] : 0;
+    vmask |= (valid ? 1u : 0u) << k;
+  }
+  // (after the record loads: the table byte's wait then covers nothing the prologue does not need anyway)
+  const uint8_t tv = tid < 8 ? inv[remap && tid >= (uint32_t)pg.tcode ? tid + 1 : tid] : 0;
+  const int term = remap ? (int)inv[pg.tcode] : -1;
+  reinterpret_cast<uint4*>(sh.cnt)[tid] = make_uint4(0u, 0u, 0u, 0u);   // the 8192 u8 counters
+  auto symx = [&](int k) -> uint32_t { return (uint32_t)(key[k] >> 32) >> (xsh - 32); };
+  // ---- 0. the item's sym range: min, max, or, and (the varying bits are those of the values relative
+  // to the minimum)
+  uint32_t xmin = ~0u, xmax = 0, vor = 0, vand = ~0u;
+#pragma unroll
+  for (int k = 0; k < BR_I; ++k) {
+    const bool valid = (vmask >> k) & 1u;
+    const uint32_t x = symx(k);
+    xmin = valid && x < xmin ? x : xmin;
+    xmax = valid && x > xmax ? x : xmax;
+    vor |= valid ? x : 0u;
+    vand &= valid ? x : ~0u;
+  }
+  xmin = dpp_reduce_u32(xmin, ~0u, [](uint32_t a, uint32_t b) { return a < b ? a : b; });
+  xmax = dpp_reduce_u32(xmax, 0u, [](uint32_t a, uint32_t b) { return a > b ? a : b; });
+  vor = dpp_reduce_u32(vor, 0u, [](uint32_t a, uint32_t b) { return a | b; });
+  vand = dpp_reduce_u32(vand, ~0u, [](uint32_t a, uint32_t b) { return a & b; });
+  if (lane == 0) {
+    sh.scr[wv] = xmin;
+    sh.scr[8 + wv] = xmax;
+    sh.scr[16 + wv] = vor;
+    sh.scr[24 + wv] = vand;
+  }
+  if (tid < 8) tab[tid] = tv;
+  __syncthreads();
+#pragma unroll
+  for (int w = 0; w < BR_T / 64; ++w) {
+    xmin = sh.scr[w] < xmin ? sh.scr[w] : xmin;
+    xmax = sh.scr[8 + w] > xmax ? sh.scr[8 + w] : xmax;
+    vor |= sh.scr[16 + w];
+    vand &= sh.scr[24 + w];
+  }
+  if (TRACE) ts[1] = stamp();
+  const uint32_t var = vor ^ vand;
+  const int lo = var ? __builtin_ctz(var) : 0;
+  const int width = var ? 32 - __builtin_clz((xmax - xmin) >> lo) : 0;
+  auto fallback = [&]() {
+    if (tid == 0) fb[atomicAdd(fb_n, 1u)] = it;
+  };
+  if (width < 1 || width > 30) {   // (uniform) all keys equal, or wider than the records' low field
+    fallback();
+    return;
+  }
+  const int kb = width > BR_BITS ? width - BR_BITS : 0;   // key bits below the bin (<= 17)
+  const uint32_t wmask = (1u << width) - 1, lowmask = (1u << kb) - 1;
+  auto local = [&](int k) -> uint32_t { return ((symx(k) - xmin) >> lo) & wmask; };
+  // ---- 1. u8 bin counters; the atomic's return is the suffix's rank inside its bin
+  uint32_t rk[(BR_I + 3) / 4];
+#pragma unroll
+  for (int k = 0; k < (BR_I + 3) / 4; ++k) rk[k] = 0;
+#pragma unroll
+  for (int k = 0; k < BR_I; ++k) {
+    if ((vmask >> k) & 1u) {
+      const uint32_t bin = local(k) >> kb, sh8 = 8u * (bin & 3u);
+      const uint32_t r = (atomicAdd(&sh.cnt[bin >> 2], 1u << sh8) >> sh8) & 0xFFu;
+      rk[k >> 2] |= r << (8 * (k & 3));
+    }
+  }
+  __syncthreads();
+  if (TRACE) ts[2] = stamp();
+  // ---- 2. group starts: thread t owns bins 16 t .. 16 t + 15 (one 16-B word of counters)
+  const uint32_t al = (uint32_t)(((uintptr_t)(sa + start) / sizeof(V)) & 3u);
+  const bool vec = al == (uint32_t)((uintptr_t)(bwt + start) & 3u);
+  const uint32_t sto = vec ? al : 0u;   // the plane's offset: 4 staged records = one aligned SA group
+  uint32_t pre[4], gs = 0;
+  bool bad = false;
+  {
+    const uint4 c4 = reinterpret_cast<const uint4*>(sh.cnt)[tid];
+    const uint32_t w[4] = {c4.x, c4.y, c4.z, c4.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      // in-group exclusive prefix per byte: exact while no bin reaches 64 and the group stays below 256
+      pre[i] = w[i] * 0x01010101u - w[i] + gs * 0x01010101u;
+      gs += __builtin_amdgcn_udot4(w[i], 0x01010101u, 0u, false);
+      bad |= (w[i] & 0xC0C0C0C0u) != 0;
+    }
+    bad |= gs > 255;
+  }
+  const uint32_t ginc = dpp_incl_sum(gs);
+  const uint64_t badw = __ballot(bad);
+  if (lane == 63) sh.scr[32 + wv] = ginc;
+  if (lane == 0) sh.scr[40 + wv] = badw ? 1u : 0u;
+  __syncthreads();
+  uint32_t carry = 0, total = 0, fail = 0;
+#pragma unroll
+  for (int w = 0; w < BR_T / 64; ++w) {
+    const uint32_t t = sh.scr[32 + w];
+    carry += (uint32_t)w < wv ? t : 0u;
+    total += t;
+    fail |= sh.scr[40 + w];
+  }
+  // (a u8 counter that wrapped carried into its neighbour or out of the word: the total shows it)
+  if (fail || total != cnt) {
+    fallback();
+    return;
+  }
+  const uint32_t gb = sto + carry + ginc - gs;   // this group's first index in the plane
+  sh.base[tid] = (uint16_t)gb;
+  if (tid == BR_T - 1) sh.base[BR_NG] = (uint16_t)(sto + cnt);
+  reinterpret_cast<uint4*>(sh.cnt)[tid] = make_uint4(pre[0], pre[1], pre[2], pre[3]);
+  __syncthreads();
+  if (TRACE) ts[3] = stamp();
+  // ---- 3. every record to its bin: (low key << xsh) | (prev code, position).  Branch-free over the
+  // item's end (invalid slots read group 0's entries and store nothing), chunks of 6 records' loads in
+  // flight together (register pressure)
+  {
+    const uint8_t* const pre8 = reinterpret_cast<const uint8_t*>(sh.cnt);
+    const uint64_t lom = (1ull << xsh) - 1;
+#pragma unroll
+    for (int k = 0; k < BR_I; ++k) {
+      if (k % 6 == 0 && k) asm volatile("" ::: "memory");
+      const bool valid = (vmask >> k) & 1u;
+      const uint32_t lk = local(k), bin = valid ? lk >> kb : 0u;
+      const uint32_t bs = sh.base[bin >> 4] + pre8[bin];
+      const uint32_t r = (rk[k >> 2] >> (8 * (k & 3))) & 0xFFu;
+      if (valid) sh.rec[bs + r] = ((uint64_t)(lk & lowmask) << xsh) | (key[k] & lom);
+    }
+  }
+  const uint32_t ge = sh.base[tid + 1];   // (written before the last barrier)
+  if (tid == 0) {   // (phase 2's flags were read before its last barrier)
+    sh.scr[40] = 0;
+    sh.scr[41] = 0;
+    sh.scr[42] = 0;
+  }
+  __syncthreads();
+  if (TRACE) ts[4] = stamp();
+  // ---- 4. the bins in place.  Two-record bins (~18 % of the bins for iid text) by their group's thread:
+  // one compare, all 16 bins' pairs read unconditionally in two batches of 8 (branch-free: a batch's reads
+  // in flight together).  Bins of 3+ records (~8 %) go to a list in the counters' space (free now) and are
+  // ranked one per thread: up to 8 records read at once and ranked by compares in registers, more (rare)
+  // by insertion.  Equal keys (same bin, same low key) form a tie run; a thread keeps up to two runs
+  // {first index, length} for the tie list (a third sends the item to the LSD passes).
+  auto kx = [&](uint64_t r) -> uint64_t { return r >> xsh; };
+  auto bstart = [&](int i) -> uint32_t { return gb + ((pre[i >> 2] >> (8 * (i & 3))) & 0xFFu); };
+  auto bend = [&](int i) -> uint32_t { return i < 15 ? bstart(i + 1) : ge; };
+  uint32_t ltie = 0, run0 = 0, run1 = 0, nrun = 0, m3 = 0;   // (two scalars: no dynamically indexed array)
+  auto add_run = [&](uint32_t f, uint32_t len) {
+    run0 = nrun == 0 ? f | len << 16 : run0;
+    run1 = nrun == 1 ? f | len << 16 : run1;
+    ++nrun;
+    ltie += len;
+  };
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    if (h) asm volatile("" ::: "memory");
+    uint64_t px[8], py[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      // every lane reads, but lanes whose bin is not a pair all read records 0 and 1 (one broadcast
+      // address: only the pairs' reads meet in the banks)
+      const uint32_t bs = bstart(8 * h + i), c = bend(8 * h + i) - bs, a = c == 2 ? bs : 0u;
+      px[i] = sh.rec[a];
+      py[i] = sh.rec[a + 1];
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int b = 8 * h + i;
+      const uint32_t bs = bstart(b), c = bend(b) - bs;
+      m3 |= (c >= 3 ? 1u : 0u) << b;
+      if (c == 2) {
+        const uint64_t x = px[i], y = py[i];
+        if (x > y) {
+          sh.rec[bs] = y;
+          sh.rec[bs + 1] = x;
+        }
+        if (kx(x) == kx(y)) add_run(bs, 2);
+      }
+    }
+  }
+  // {start | size << 16} of the 3+ bins: three-record bins from the front of the counters' space, larger
+  // ones from its back, so that each loop below runs one code path per wave
+  uint32_t* const blist = sh.cnt;
+  constexpr uint32_t BL = BR_BINS / 4;
+  {
+    uint32_t m3only = 0;
+#pragma unroll
+    for (int b = 0; b < 16; ++b) m3only |= ((m3 >> b) & 1u) && bend(b) - bstart(b) == 3 ? 1u << b : 0u;
+    uint32_t m4 = m3 & ~m3only;
+    const uint32_t n3 = __popc(m3only), n4 = __popc(m4);
+    const uint32_t binc = dpp_incl_sum(n3 | n4 << 16);   // (both <= 64 * 16)
+    uint32_t wb = 0;
+    if (lane == 63) wb = atomicAdd(&sh.scr[40], binc & 0xFFFFu) | atomicAdd(&sh.scr[42], binc >> 16) << 16;
+    wb = (uint32_t)__builtin_amdgcn_readlane((int)wb, 63);
+    uint32_t w3 = (wb & 0xFFFFu) + (binc & 0xFFFFu) - n3, w4 = (wb >> 16) + (binc >> 16) - n4;
+    while (m3only) {
+      const int b = __builtin_ctz(m3only);
+      m3only &= m3only - 1;
+      if (w3 < BL) blist[w3] = bstart(b) | 3u << 16;
+      ++w3;
+    }
+    while (m4) {
+      const int b = __builtin_ctz(m4);
+      m4 &= m4 - 1;
+      if (w4 < BL) blist[BL - 1 - w4] = bstart(b) | (bend(b) - bstart(b)) << 16;
+      ++w4;
+    }
+  }
+  __syncthreads();
+  if (TRACE) ts[5] = stamp();
+  const uint32_t nb3 = sh.scr[40], nb4 = sh.scr[42];
+  if (nb3 + nb4 > BL) {   // (uniform) a skewed item
+    fallback();
+    return;
+  }
+  for (uint32_t i = tid; i < nb3; i += BR_T) {   // three records: a network
+    const uint32_t bs = blist[i] & 0xFFFFu;
+    uint64_t x = sh.rec[bs], y = sh.rec[bs + 1], z = sh.rec[bs + 2];
+    auto cas = [](uint64_t& a, uint64_t& c2) {
+      const uint64_t lo2 = a < c2 ? a : c2, hi2 = a < c2 ? c2 : a;
+      a = lo2;
+      c2 = hi2;
+    };
+    cas(x, y);
+    cas(y, z);
+    cas(x, y);
+    sh.rec[bs] = x;
+    sh.rec[bs + 1] = y;
+    sh.rec[bs + 2] = z;
+    const bool exy = kx(x) == kx(y), eyz = kx(y) == kx(z);
+    if (exy || eyz) add_run(exy ? bs : bs + 1, exy && eyz ? 3u : 2u);
+  }
+  for (uint32_t i = tid; i < nb4; i += BR_T) {   // four or more
+    const uint32_t e = blist[BL - 1 - i], bs = e & 0xFFFFu, c = e >> 16;
+    if (c <= 8) {
+      uint64_t r[8], kr[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {   // unconditional (past the plane's end: the lists' words); pads rank last
+        const uint64_t v = sh.rec[bs + q];
+        r[q] = (uint32_t)q < c ? v : ~0ull;
+        kr[q] = kx(v);
+      }
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        uint32_t rank = 0, eqn = 0, eqb = 0;
+#pragma unroll
+        for (int o = 0; o < 8; ++o) {
+          if (o == q) continue;
+          const bool lt = r[o] < r[q], e2 = (uint32_t)o < c && kr[o] == kr[q];
+          rank += lt ? 1u : 0u;
+          eqn += e2 ? 1u : 0u;
+          eqb += e2 && lt ? 1u : 0u;
+        }
+        if ((uint32_t)q < c) {
+          sh.rec[bs + rank] = r[q];
+          if (eqn && !eqb) add_run(bs + rank, eqn + 1);
+        }
+      }
+      continue;
+    }
+    const uint32_t be = bs + c;
+    for (uint32_t p = bs + 1; p < be; ++p) {
+      const uint64_t v = sh.rec[p];
+      uint32_t q = p;
+      while (q > bs) {
+        const uint64_t u = sh.rec[q - 1];
+        if (u < v) break;
+        sh.rec[q] = u;
+        --q;
+      }
+      sh.rec[q] = v;
+    }
+    uint32_t rs = bs;
+    uint64_t kprev = kx(sh.rec[bs]);
+    for (uint32_t p = bs + 1; p <= be; ++p) {
+      const uint64_t kp = p < be ? kx(sh.rec[p]) : ~0ull;   // (keys < 2^64 >> xsh: ~0 ends the last run)
+      if (kp != kprev) {
+        if (p - rs >= 2) add_run(rs, p - rs);
+        rs = p;
+        kprev = kp;
+      }
+    }
+  }
+  if (nrun > 2) sh.scr[41] = 1u;   // (any thread: the flag is read after the next barrier)
+  const uint32_t tinc = dpp_incl_sum(ltie);
+  if (lane == 63) sh.scr[wv] = tinc;
+  __syncthreads();
+  if (TRACE) ts[6] = stamp();
+  if (sh.scr[41]) {   // (uniform) a thread with more than two tie runs: the LSD passes list them
+    fallback();
+    return;
+  }
+  uint32_t tcar = 0, ntie = 0;
+#pragma unroll
+  for (int w = 0; w < BR_T / 64; ++w) {
+    const uint32_t t = sh.scr[w];
+    tcar += (uint32_t)w < wv ? t : 0u;
+    ntie += t;
+  }
+  unsigned long long tbase = 0;
+  if (tid == 0 && ntie) tbase = atomicAdd(tie_n, (unsigned long long)ntie);
+  // ---- 5. SA / BWT in sorted order straight from the plane
+  const uint32_t posm = pbits >= 32 ? ~0u : (1u << pbits) - 1, pmask = (1u << pb) - 1;
+  auto bwt_of = [&](uint64_t r) -> uint32_t {
+    const uint32_t pos = (uint32_t)r & posm, pv = (uint32_t)(r >> pbits) & pmask;
+    return pos == 0 && term >= 0 ? (uint32_t)term : (uint32_t)tab[pv];
+  };
+  if (vec) {
+    const uint32_t ng = (cnt + al + 3) >> 2;
+    const uint32_t tlo = reinterpret_cast<const uint32_t*>(tab)[0], thi = reinterpret_cast<const uint32_t*>(tab)[1];
+    for (uint32_t q = tid; q < ng; q += BR_T) {
+      const uint4 ra = reinterpret_cast<const uint4*>(sh.rec)[2 * q];
+      const uint4 rb = reinterpret_cast<const uint4*>(sh.rec)[2 * q + 1];
+      const uint32_t lo4[4] = {ra.x, ra.z, rb.x, rb.z}, hi4[4] = {ra.y, ra.w, rb.y, rb.w};
+      uint32_t pos[4], sel = 0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint64_t r = ((uint64_t)hi4[j] << 32) | lo4[j];
+        pos[j] = lo4[j] & posm;
+        sel |= ((uint32_t)(r >> pbits) & pmask) << (8 * j);
+      }
+      uint32_t bw = __builtin_amdgcn_perm(thi, tlo, sel);
+      if (term >= 0) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (pos[j] == 0) bw = (bw & ~(0xFFu << (8 * j))) | ((uint32_t)term << (8 * j));
+      }
+      const uint32_t g = 4u * q;
+      if (g >= al && g + 4 <= cnt + al) {   // a whole group: aligned vector stores
+        *reinterpret_cast<uint4*>(sa + start + (g - al)) = make_uint4(pos[0], pos[1], pos[2], pos[3]);
+        *reinterpret_cast<uint32_t*>(bwt + start + (g - al)) = bw;
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const uint32_t r = g + j;
+          if (r >= al && r < cnt + al) {
+            sa[start + r - al] = pos[j];
+            bwt[start + r - al] = (uint8_t)(bw >> (8 * j));
+          }
+        }
+      }
+    }
+  } else {
+    for (uint32_t r = tid; r < cnt; r += BR_T) {
+      const uint64_t x = sh.rec[r];
+      sa[start + r] = (uint32_t)x & posm;
+      bwt[start + r] = (uint8_t)bwt_of(x);
+    }
+  }
+  if (ntie) {   // (uniform) each thread's tie runs: a group's records consecutive, head first
+    if (tid == 0) {
+      sh.scr[8] = (uint32_t)tbase;
+      sh.scr[9] = (uint32_t)(tbase >> 32);
+    }
+    __syncthreads();
+    if (ltie) {
+      uint64_t tb = ((uint64_t)sh.scr[9] << 32 | sh.scr[8]) + tcar + tinc - ltie;
+      auto put = [&](uint32_t f, uint32_t len) {
+        for (uint32_t j = 0; j < len; ++j) {
+          tie_k[tb + j] = ((uint64_t)(start + f + j - sto) << 1) | (j == 0 ? 1u : 0u);
+          tie_v[tb + j] = (V)((uint32_t)sh.rec[f + j] & posm);
+        }
+        tb += len;
+      };
+      if (nrun > 0) put(run0 & 0xFFFFu, run0 >> 16);
+      if (nrun > 1) put(run1 & 0xFFFFu, run1 >> 16);
+    }
+  }
+  if (TRACE) {
+    ts[7] = stamp();
+    if (tid == 0)
+      for (int i = 0; i < 8; ++i) trace[(uint64_t)blockIdx.x * 8 + i] = ts[i];
+  }
+}
+
 // ------------------------------------------------------------ 5. big buckets
 // compacted copy of the big buckets: key top D bits replaced by the big-bucket ordinal, J = slot;
 // pbits > 0: packed records (key bits << pbits | position, section 1b), no value plane
@@ -2912,7 +3339,10 @@ uint64_t sort_bucket_items(Index& ix, const BucketPlan& plan, const uint64_t* ke
     const unsigned grid_n = (unsigned)nn, grid_w = (unsigned)nw;
     DevBuf tbuf;
     if (nn) {
-      if (trace) tbuf.ensure(nn * 64 + 64);
+      if (trace) {
+        tbuf.ensure(nn * 64 + 64);
+        HK_HIP(hipMemsetAsync(tbuf.p, 0, nn * 64, s));
+      }
       ix.bk_fb.ensure(nn * sizeof(uint2) + 16);
       unsigned int* fbn = reinterpret_cast<unsigned int*>(ix.small.as<uint8_t>() + 4352);   // small+4352: fallback count
       HK_HIP(hipMemsetAsync(fbn, 0, 4, s));
@@ -2920,6 +3350,24 @@ uint64_t sort_bucket_items(Index& ix, const BucketPlan& plan, const uint64_t* ke
         constexpr int T = decltype(ttag)::value;
         constexpr int I = decltype(itag)::value;
         constexpr bool TR = decltype(trtag)::value;
+        if constexpr (T == 512 && sizeof(V) == 4) {
+          // the record-plane sort: sigma <= 8 codes, u32 positions, sym fields in the high words, and room
+          // for (low key <= 17 bits) << xsh (HKCSA_BS_REC=0 keeps the fast path, for A/B)
+          static const bool rec_off = getenv("HKCSA_BS_REC") && getenv("HKCSA_BS_REC")[0] == '0';
+          const int xsh = pk ? pk->g.pbits + pk->g.pb2 : 0;
+          if (pk && !rec_off && xsh >= 32 && xsh + 17 <= 64 && pk->g.pb2 <= 3 && pk->g.phb == 0 &&
+              plan.cap <= (uint64_t)BR_CAP) {
+            if (trace)
+              k_bucket_sort_rec<V, true><<<grid_n, BR_T, 0, s>>>(
+                  keys, ix.bk_items.as<uint2>(), d_inv, sa, bwt, ix.ties_k.as<uint64_t>(), ix.ties_v.as<V>(),
+                  ix.ties_n.as<unsigned long long>(), ix.bk_fb.as<uint2>(), fbn, pk->g, tbuf.as<uint64_t>());
+            else
+              k_bucket_sort_rec<V><<<grid_n, BR_T, 0, s>>>(
+                  keys, ix.bk_items.as<uint2>(), d_inv, sa, bwt, ix.ties_k.as<uint64_t>(), ix.ties_v.as<V>(),
+                  ix.ties_n.as<unsigned long long>(), ix.bk_fb.as<uint2>(), fbn, pk->g);
+            return;
+          }
+        }
         if (pk && pk->g.pbits + pk->g.pb2 >= 32) {   // sym fields in the records' high words
           k_bucket_sort_fast<V, TR, T, I, true, true><<<grid_n, T, 0, s>>>(
               keys, pk->vfull, ix.bk_items.as<uint2>(), pb, sb, hb, symbias, d_inv, sa, bwt,
@@ -2959,9 +3407,10 @@ uint64_t sort_bucket_items(Index& ix, const BucketPlan& plan, const uint64_t* ke
         double acc[7] = {0, 0, 0, 0, 0, 0, 0};
         for (size_t w = 0; w < nn; ++w)
           for (int i = 0; i < 7; ++i) acc[i] += (double)(h[w * 8 + i + 1] - h[w * 8 + i]);
-        fprintf(stderr, "[bucket_sort_fast trace] %zu WGs, mean cycles: load+prologue %.0f, hist %.0f, scan %.0f, "
-                "scatter %.0f, small bins %.0f, listed bins %.0f, stage+out %.0f\n", (size_t)nn, acc[0] / nn, acc[1] / nn,
-                acc[2] / nn, acc[3] / nn, acc[4] / nn, acc[5] / nn, acc[6] / nn);
+        // (fast sort: load+prologue, hist, scan, scatter, small bins, listed bins, stage+out; record-plane
+        // sort: load+prologue, hist, scan, scatter, pairs + lists, 3+ bins, output + ties)
+        fprintf(stderr, "[bucket_sort trace] %zu WGs, mean cycles per phase: %.0f %.0f %.0f %.0f %.0f %.0f %.0f\n",
+                (size_t)nn, acc[0] / nn, acc[1] / nn, acc[2] / nn, acc[3] / nn, acc[4] / nn, acc[5] / nn, acc[6] / nn);
       }
       // the fallback count and the tie count in one round trip (pinned slots); the tie count is read
       // again below only when fallback items ran
@@ -4242,7 +4691,7 @@ void build_slice_keyed(Index& ix, uint32_t c_lo, uint32_t c_hi, uint64_t m) {
   const int lhb = P.packed ? P.uhb : P.hb;
   uint64_t hmax = 0;
   for (uint64_t c : hist) hmax = std::max(hmax, c);
-  const uint64_t cap = hmax <= (uint64_t)512 * BS_I ? (uint64_t)512 * BS_I : (uint64_t)BS_CAP;
+  const uint64_t cap = hmax <= (uint64_t)BR_CAP ? (uint64_t)BR_CAP : (uint64_t)BS_CAP;
   const BucketPlan plan = plan_buckets(hist, P.sl.bsh, cap, P.packed ? P.sl.sA : 32);
   ix.info[4] = plan.items_n.size() + plan.items_w.size();
   ix.info[5] = plan.big_start.size();
@@ -4376,8 +4825,9 @@ void build_sa_bucketed(Index& ix) {
     HK_HIP(hipGetLastError());
   } else if (D > 0) {
     ix.bk_hist.ensure((uint64_t)nbins * 8);
-    // skewed texts at scale (natural language, proteins) end on the global path anyway: the bucket counts of the
-    // text's first sixteenth decide that before the whole text is counted (1 GiB protein-like: 4.1 ms)
+    // skewed texts at scale (natural language, proteins) end on the global path anyway: the bucket counts of a
+    // sixteenth of the text - spans spread evenly over it, so a skewed head (a header, a run) does not decide
+    // alone - settle that before the whole text is counted (1 GiB protein-like: 4.1 ms)
     if (n >= (1ull << 26)) {
       HK_HIP(hipMemsetAsync(ix.bk_hist.p, 0, (uint64_t)nbins * 8, s));
       {
@@ -4385,15 +4835,16 @@ void build_sa_bucketed(Index& ix) {
         const uint64_t tiles = ceil_div(n / 16, (uint64_t)BH_TILE);
         const uint64_t tpw = ceil_div(tiles, 256);
         const unsigned grid = (unsigned)ceil_div(tiles, tpw);
+        const uint64_t stride = n / grid / BH_TILE * BH_TILE;   // >= the span: n / grid >= 16 spans
         k_bucket_hist<false><<<grid, BH_T, 0, s>>>(ix.text.as<uint8_t>(), n, d_lutk, d_skey, ka, bsh, D,
-                                                   ix.bk_hist.as<unsigned long long>(), tpw * BH_TILE);
+                                                   ix.bk_hist.as<unsigned long long>(), tpw * BH_TILE, stride);
         HK_HIP(hipGetLastError());
       }
       HK_HIP(hipMemcpyAsync(hist.data(), ix.bk_hist.p, (uint64_t)nbins * 8, hipMemcpyDeviceToHost, s));
       HK_HIP(hipStreamSynchronize(s));
       uint64_t tot = 0, big = 0;
       for (uint32_t b = 0; b < nbins; ++b) tot += hist[b];
-      const uint64_t cap = item_T == 512 ? (uint64_t)512 * BS_I : (uint64_t)BS_CAP;
+      const uint64_t cap = item_T == 512 ? (uint64_t)BR_CAP : (uint64_t)BS_CAP;
       for (uint32_t b = 0; b < nbins; ++b)
         if (tot && (double)hist[b] * (double)n / (double)tot > (double)cap) big += hist[b];
       if (tot && big * 4 > tot * 3) skip_plan = true;   // over 3/4 of the suffixes in big buckets
@@ -4488,7 +4939,7 @@ void build_sa_bucketed(Index& ix) {
   // ---- 2. work items (whole buckets, packed while they fit) and big buckets
   BucketPlan plan;
   if (skip_plan) plan.big_total = n;   // (the global path: no items)
-  else plan = plan_buckets(hist, bsh, item_T == 512 ? (uint64_t)512 * BS_I : (uint64_t)BS_CAP, packed ? 8 : 32);
+  else plan = plan_buckets(hist, bsh, item_T == 512 ? (uint64_t)BR_CAP : (uint64_t)BS_CAP, packed ? 8 : 32);
   const std::vector<uint2>& items_n = plan.items_n;
   const std::vector<uint2>& items_w = plan.items_w;
   const std::vector<uint64_t>& big_start = plan.big_start;

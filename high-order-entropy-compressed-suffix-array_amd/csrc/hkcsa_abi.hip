@@ -18,6 +18,17 @@ struct hkcsa_queries {
   hk::DevBuf pats, offs, lr, cnt, occ_offs, pos, flag;
   uint64_t total = 0;
   bool have_lr = false, have_pos = false;
+  void release() {
+    for (hk::DevBuf* b : {&pats, &offs, &lr, &cnt, &occ_offs, &pos, &flag}) b->release();
+    have_lr = have_pos = false;
+  }
+  // the per-handle batch workspace keeps what an ordinary call needs; a buffer a large call grew past
+  // kKeep is freed when that call ends, so one big locate does not pin HBM for the handle's lifetime
+  static constexpr size_t kKeep = 64ull << 20;
+  void trim() {
+    for (hk::DevBuf* b : {&pats, &offs, &lr, &cnt, &occ_offs, &pos})
+      if (b->bytes > kKeep) b->release();
+  }
 };
 
 struct hkcsa_index {
@@ -199,7 +210,9 @@ int hkcsa_release_workspace(hkcsa_index* h) {
   return guarded([&] {
     activate(h);
     HK_HIP(hipStreamSynchronize(h->ix.stream));
+    if (h->copy_stream) HK_HIP(hipStreamSynchronize(h->copy_stream));
     hk::release_workspace(h->ix);
+    h->qws.release();   // the host-boundary batch calls' workspace too
   });
 }
 int hkcsa_build_samples(hkcsa_index* h, uint32_t rate) {
@@ -588,17 +601,25 @@ hkcsa_queries& batch_count(hkcsa_index* h, const uint8_t* pats, const uint64_t* 
   HK_HIP(hipStreamWaitEvent(cs, h->copy_ev, 0));
   uint8_t* const dp = q.pats.as<uint8_t>();
   uint64_t* const dofs = q.offs.as<uint64_t>();
-  for (uint64_t p0 = 0; p0 < P || p0 == 0; p0 += kCountChunk) {
-    const uint64_t p1 = std::min(P, p0 + kCountChunk);
-    // this chunk's pattern bytes (clamped: offsets out of order only lose bytes the kernel will not read)
-    const uint64_t b0 = std::min(offs[p0], bytes), b1 = std::min(std::max(offs[p1], b0), bytes);
-    if (b1 > b0) HK_HIP(hipMemcpyAsync(dp + b0, pats + b0, b1 - b0, hipMemcpyHostToDevice, cs));
-    HK_HIP(hipMemcpyAsync(dofs + p0, offs + p0, (p1 - p0 + 1) * 8, hipMemcpyHostToDevice, cs));
-    HK_HIP(hipEventRecord(h->copy_ev, cs));
-    HK_HIP(hipStreamWaitEvent(s, h->copy_ev, 0));
-    hk::query_count(h->ix, dp, dofs + p0, p1 - p0, q.lr.as<int64_t>() + 2 * p0, q.cnt.as<uint64_t>() + p0, bytes,
-                    q.flag.as<uint32_t>());
-    if (p1 >= P) break;
+  try {
+    for (uint64_t p0 = 0; p0 < P || p0 == 0; p0 += kCountChunk) {
+      const uint64_t p1 = std::min(P, p0 + kCountChunk);
+      // this chunk's pattern bytes (clamped: offsets out of order only lose bytes the kernel will not read)
+      const uint64_t b0 = std::min(offs[p0], bytes), b1 = std::min(std::max(offs[p1], b0), bytes);
+      if (b1 > b0) HK_HIP(hipMemcpyAsync(dp + b0, pats + b0, b1 - b0, hipMemcpyHostToDevice, cs));
+      HK_HIP(hipMemcpyAsync(dofs + p0, offs + p0, (p1 - p0 + 1) * 8, hipMemcpyHostToDevice, cs));
+      HK_HIP(hipEventRecord(h->copy_ev, cs));
+      HK_HIP(hipStreamWaitEvent(s, h->copy_ev, 0));
+      hk::query_count(h->ix, dp, dofs + p0, p1 - p0, q.lr.as<int64_t>() + 2 * p0, q.cnt.as<uint64_t>() + p0, bytes,
+                      q.flag.as<uint32_t>());
+      if (p1 >= P) break;
+    }
+  } catch (...) {
+    // copies from the caller's buffers may still be queued: drain both streams before the error returns,
+    // so the caller may free them (their own errors are superseded by this one)
+    (void)hipStreamSynchronize(cs);
+    (void)hipStreamSynchronize(s);
+    throw;
   }
   return q;
 }
@@ -628,6 +649,7 @@ int hkcsa_count_batch(hkcsa_index* h, const uint8_t* pats, const uint64_t* offs,
     flag_check(h);
     if (P) HK_HIP(hipMemcpyAsync(lr_out, q.lr.p, P * 16, hipMemcpyDeviceToHost, s));
     HK_HIP(hipStreamSynchronize(s));
+    q.trim();
   });
 }
 
@@ -656,6 +678,7 @@ int hkcsa_locate_batch(hkcsa_index* h, const uint8_t* pats, const uint64_t* offs
     HK_HIP(hipMemcpyAsync(occ_offs, q.occ_offs.p, (P + 1) * 8, hipMemcpyDeviceToHost, s));
     if (pos_out && cap >= tot && tot) HK_HIP(hipMemcpyAsync(pos_out, q.pos.p, tot * 8, hipMemcpyDeviceToHost, s));
     HK_HIP(hipStreamSynchronize(s));
+    q.trim();
     need(!pos_out || cap >= tot, HKCSA_E_RANGE, "position buffer too small (occ_offs holds the sizes)");
   });
 }

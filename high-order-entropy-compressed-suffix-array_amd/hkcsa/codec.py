@@ -52,6 +52,7 @@ def _view(s: str, lay):
         return np.zeros(0, dtype=dt)
     addr = id(s) + (lay[1] if ascii_ else lay[2])
     buf = (C.c_char * (n * kind)).from_address(addr)
+    buf._src = s   # the view's base chain (view -> buf -> s) keeps the str, hence its storage, alive
     v = np.frombuffer(buf, dtype=dt)
     v.flags.writeable = False
     return v
@@ -62,7 +63,7 @@ _LAYOUT = _layout()
 
 def code_points(s: str) -> np.ndarray:
     """The code points of `s` as a uint8 / uint16 / uint32 array: a zero-copy view of the str's own
-    storage on CPython (valid while `s` lives), else an encoded copy."""
+    storage on CPython (the view holds a reference to `s`), else an encoded copy."""
     if _LAYOUT is not None:
         v = _view(s, _LAYOUT)
         if v is not None:

@@ -114,7 +114,9 @@ int hkcsa_build_bwt(hkcsa_index* ix);
 int hkcsa_build_wt(hkcsa_index* ix);
 /* SA + BWT + WT in one call (EnhancedFMIndex.__init__, csa/enhanced_fm_index.py:8-13). */
 int hkcsa_build_all(hkcsa_index* ix);
-/* Drop the construction workspace (keys, ISA, ...) kept for repeated builds. */
+/* Drop the construction workspace (keys, ISA, ...) kept for repeated builds, and the device
+ * workspace of hkcsa_count_batch / hkcsa_locate_batch (those calls keep buffers of <= 64 MiB
+ * between calls and free larger ones when the call ends). */
 int hkcsa_release_workspace(hkcsa_index* ix);
 /* SA sampling for the epsilon space/time contract of CompressedSuffixArray(text, epsilon)
  * (tests/benchmark.py:25,32; the class itself is absent from the reference, csa/csa.py:3):

@@ -130,7 +130,8 @@ def _worker(rank, world, port, n, q, kind="iid"):
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     import torch
-    from hkcsa.shard import sharded_build, torch_allgather, torch_allreduce_sum
+    from hkcsa.shard import sharded_build
+    from dist_helpers import torch_allgather, torch_allreduce_sum
     from oracle import oracle
     if kind == "iid":
         text = oracle.synth_text(n, b"ACGT", seed=21)

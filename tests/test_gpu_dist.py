@@ -44,7 +44,8 @@ def _worker(rank, world, port, kind, n, q):
     ok, msg, bounds = False, "", None
     try:
         from hkcsa import DeviceIndex
-        from hkcsa.shard import sharded_build, torch_allgather, torch_allreduce_sum
+        from hkcsa.shard import sharded_build
+        from dist_helpers import torch_allgather, torch_allreduce_sum
         from oracle import oracle
         text = _texts(kind, n)
         dev = DeviceIndex.from_bytes(text, device=0)
