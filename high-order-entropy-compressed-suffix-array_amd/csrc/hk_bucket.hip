@@ -2868,41 +2868,56 @@ __global__ __launch_bounds__(BR_T, 4) void k_bucket_sort_rec(const uint64_t* __r
   // by insertion.  Equal keys (same bin, same low key) form a tie run; a thread keeps up to two runs
   // {first index, length} for the tie list (a third sends the item to the LSD passes).
   auto kx = [&](uint64_t r) -> uint64_t { return r >> xsh; };
-  auto bstart = [&](int i) -> uint32_t { return gb + ((pre[i >> 2] >> (8 * (i & 3))) & 0xFFu); };
+  // (i may be run-time: two u64 halves and a shift, so that no register array is indexed - the compiler
+  // turns a select chain over pre[] back into a scratch array)
+  const uint64_t pre_lo = (uint64_t)pre[1] << 32 | pre[0], pre_hi = (uint64_t)pre[3] << 32 | pre[2];
+  auto bstart = [&](int i) -> uint32_t {
+    return gb + ((uint32_t)((i < 8 ? pre_lo : pre_hi) >> (8 * (i & 7))) & 0xFFu);
+  };
   auto bend = [&](int i) -> uint32_t { return i < 15 ? bstart(i + 1) : ge; };
-  uint32_t ltie = 0, run0 = 0, run1 = 0, nrun = 0, m3 = 0;   // (two scalars: no dynamically indexed array)
+  uint32_t ltie = 0, run0 = 0, run1 = 0, nrun = 0;   // (two scalars: no dynamically indexed array)
   auto add_run = [&](uint32_t f, uint32_t len) {
     run0 = nrun == 0 ? f | len << 16 : run0;
     run1 = nrun == 1 ? f | len << 16 : run1;
     ++nrun;
     ltie += len;
   };
+  // the pair bins of this group (a mask), then up to four pairs per lane with their reads in flight together,
+  // the rest (lanes with more than four, ~7 % of them) one by one
+  uint32_t m2 = 0, m3 = 0;
 #pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    if (h) asm volatile("" ::: "memory");
-    uint64_t px[8], py[8];
+  for (int b = 0; b < 16; ++b) {
+    const uint32_t c = bend(b) - bstart(b);
+    m2 |= (c == 2 ? 1u : 0u) << b;
+    m3 |= (c >= 3 ? 1u : 0u) << b;
+  }
+  auto pair = [&](uint32_t bs, uint64_t x, uint64_t y) {
+    if (x > y) {
+      sh.rec[bs] = y;
+      sh.rec[bs + 1] = x;
+    }
+    if (kx(x) == kx(y)) add_run(bs, 2);
+  };
+  {
+    uint32_t pa[4];
+    uint64_t px[4], py[4];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      // every lane reads, but lanes whose bin is not a pair all read records 0 and 1 (one broadcast
-      // address: only the pairs' reads meet in the banks)
-      const uint32_t bs = bstart(8 * h + i), c = bend(8 * h + i) - bs, a = c == 2 ? bs : 0u;
-      px[i] = sh.rec[a];
-      py[i] = sh.rec[a + 1];
+    for (int j = 0; j < 4; ++j) {   // lanes out of pairs read records 0 and 1 (one broadcast address)
+      const int b = m2 ? __builtin_ctz(m2) : 0;
+      const uint32_t a = m2 ? bstart(b) : 0u;
+      pa[j] = m2 ? a : ~0u;
+      m2 &= m2 - 1;
+      px[j] = sh.rec[a];
+      py[j] = sh.rec[a + 1];
     }
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int b = 8 * h + i;
-      const uint32_t bs = bstart(b), c = bend(b) - bs;
-      m3 |= (c >= 3 ? 1u : 0u) << b;
-      if (c == 2) {
-        const uint64_t x = px[i], y = py[i];
-        if (x > y) {
-          sh.rec[bs] = y;
-          sh.rec[bs + 1] = x;
-        }
-        if (kx(x) == kx(y)) add_run(bs, 2);
-      }
-    }
+    for (int j = 0; j < 4; ++j)
+      if (pa[j] != ~0u) pair(pa[j], px[j], py[j]);
+  }
+  while (m2) {
+    const uint32_t a = bstart(__builtin_ctz(m2));
+    m2 &= m2 - 1;
+    pair(a, sh.rec[a], sh.rec[a + 1]);
   }
   // {start | size << 16} of the 3+ bins: three-record bins from the front of the counters' space, larger
   // ones from its back, so that each loop below runs one code path per wave
