@@ -2681,13 +2681,20 @@ __global__ __launch_bounds__(T, (T * I <= 9216 ? 2 : 1) * T / 256) void k_bucket
 // the unit: the item's sym range fixes all but `width` key bits, the top 13 of them pick one of 8192 bins
 // (u8 counters: the atomic's return is the rank inside the bin), and the record goes to its bin as ONE u64
 // whose sym field is replaced by the key bits below the bin: (low key << xsh) | prev code << pbits |
-// position.  Each record's owner then ranks it inside its bin by plain u64 compares with the bin's
-// records (the low key decides; equal low keys are equal keys; ~2/3 of iid suffixes share their bin
-// with at most one other), moves it there if the rank changed, and the plane - now at final index + the
-// SA pointer's misalignment - is written out as aligned 16-B SA / 4-B BWT groups.  Phase cycles at 1 GiB
-// (HKCSA_BS_TRACE=1): see DESIGN.md section 4.  The u8 counters need bins of < 64 records and
-// groups of < 256 (checked by the counts' total and bit tests); items outside that, or with local keys
-// wider than 30 bits, go to the LSD passes (fb).  LDS: 81,904 B, two workgroups per CU.
+// position.  The plane is then ordered bin by bin in place by plain u64 compares (the low key decides;
+// equal low keys are equal keys): ~37 % of the bins of iid text hold one record (nothing to do), pairs
+// (~18 %) are settled by the thread that owns their group of 16 bins, four per lane with their reads in
+// flight together, and bins of 3+ records (~8 %) are listed and ranked one per thread.  The plane - now
+// at final index + the SA pointer's misalignment - is written out as aligned 16-B SA / 4-B BWT groups.
+// Two random LDS accesses per suffix where the fast path has five, seven barriers.  Round 6 on MI355X,
+// 1 GiB sigma = 4 items: 4.70 -> 4.13 ms per launch; per-item cycles per phase by HKCSA_BS_TRACE=1
+// in DESIGN.md section 4.  Slower variants measured and dropped: one thread per group settling all its
+// bins in loops (dependent LDS chains: 4.9-6.0 ms), every record ranking itself against its bin (more LDS
+// bytes), pairs and triples in one unconditional pass, 3+ bins by their owners, a four-record network for
+// 3- and 4-record bins, and persistent workgroups prefetching the next item (5.5 ms).  The u8 counters
+// need bins of < 64 records and groups of < 256 (checked by the counts' total and bit tests); items
+// outside that, with local keys wider than 30 bits, or with a thread holding more than two tie runs go
+// to the LSD passes (fb).  LDS: 81,904 B, two workgroups per CU.
 constexpr int BR_T = 512, BR_I = 18;
 constexpr uint32_t BR_CAP = 9056;                 // suffixes per item (the 512-thread items' plan cap)
 constexpr int BR_BITS = 13, BR_BINS = 1 << BR_BITS, BR_NG = BR_BINS / 16;   // 16 bins per group, a group per thread
