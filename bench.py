@@ -255,6 +255,55 @@ def time_queries(dev, data, offs, reps: int) -> dict:
             "locate_patterns_per_s": round(P / t_loc, 1), "count_patterns_per_s": round(P / t_cnt, 1)}
 
 
+def pmc_row(name: str) -> dict:
+    """The PMC row of timer `name` in profiles/pmc_kernels.json (tools/kprof.py --pmc-json), or {}."""
+    try:
+        with open(os.path.join(ROOT, "profiles", "pmc_kernels.json")) as f:
+            return json.load(f).get(name, {})
+    except Exception:
+        return {}
+
+
+def count_roofline(dev, data, offs, reps: int, sigma_codes: int) -> dict:
+    """The batched count kernel (k_count, one lane per pattern) against HBM: its algorithmic bytes per pattern
+    are the pattern, the k-mer table entry of its last K symbols, two 64-B occ-directory lines (+ an 8-B
+    superblock prefix each) per remaining LF step and the (l, r) + count outputs; the time is the kernel's own
+    HIP events.  L2 hit rate, HBM traffic and occupancy come from the committed rocprofv3 row (pmc_row)."""
+    P = len(offs) - 1
+    plen = int(offs[1] - offs[0]) if P else 0
+    K, tot = 0, 1
+    while K < 12 and tot * sigma_codes <= (1 << 21):   # hk_wt.hip build_wt: sigma^K <= 2^21 with a directory
+        tot *= sigma_codes
+        K += 1
+    steps = max(plen - K, 0)
+    occ = sigma_codes <= 9   # sigma <= 8 (+ '$'): the flat occ directory, one line per rank; else two (16-ary)
+    per_pat = plen + 16 + steps * 2 * ((64 if occ else 128) + 8) + 16 + 8
+    q = dev.queries(data=data, offs=offs)
+    q.count()
+    dev.synchronize()
+    dev.timing_reset()
+    dev.timing(True)
+    for _ in range(reps):
+        q.count()
+    dev.synchronize()
+    launches, ms, _ = dev.kernel_stats("fm_count")
+    dev.timing(False)
+    q.close()
+    if not launches:
+        return {}
+    avg_s = ms / launches / 1e3
+    achieved = P * per_pat / avg_s / 1e9
+    pmc = pmc_row("fm_count")
+    return {"kernel": "k_count<16,1> (occ directory + k-mer table)" if occ else "k_count<16,2> (16-ary directory)",
+            "bound": "hbm", "patterns": P, "plen": plen,
+            "kmer_k": K, "lf_steps": steps, "alg_bytes_per_pattern": per_pat, "avg_launch_ms": round(avg_s * 1e3, 4),
+            "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "traffic": pmc.get("traffic_gb_per_launch"), "l2_hit": pmc.get("l2_hit"),
+            "waves_per_cu": pmc.get("waves_per_cu"), "pmc_source": "profiles/pmc_kernels.json" if pmc else None,
+            "note": "random 64-B line reads: the line count, not the bytes used, is the HBM cost"}
+
+
 def time_wt(dev, reps: int) -> float:
     dev.build_wt()            # warm: first-call allocations happen here
     dev.synchronize()
@@ -325,10 +374,11 @@ def run_single(args) -> dict:
     t_wt = time_wt(dev, args.wt_reps)
     wt_roof = roofline(dev, WT_KERNELS, leg)
     dev.timing(False)
-    loc = eps = loc_host = None
+    loc = eps = loc_host = cnt_roof = None
     if args.patterns > 0:
         data, offs = pattern_batch(dev, n, args.patterns, args.plen, args.seed + 1)
         loc = time_queries(dev, data, offs, args.query_reps)
+        cnt_roof = count_roofline(dev, data, offs, args.query_reps, len(set(alpha)) + 1)
         loc_host = locate_host_leg(dev, data, offs, args.query_reps, loc)
         log(f"[bench] locate at the host boundary: {loc_host['locate_patterns_per_s']:.3g} patterns/s")
         if args.eps:
@@ -363,6 +413,7 @@ def run_single(args) -> dict:
         "locate_patterns_per_s": loc["locate_patterns_per_s"] if loc else None,
         "full_build_MBps": round(n / 2**20 / (wall / args.steps + t_wt), 2),
         "detail": {"wt_build_ms": round(t_wt * 1e3, 3), "wt_roofline": wt_roof, "locate": loc,
+                   "count_roofline": cnt_roof,
                    "pattern_source": f"uniform substrings of a {PATTERN_WINDOW >> 20} MiB window of the text",
                    "stages_ms_total": stages, "build_info": info[:16], "pcie_inclusive": pcie,
                    "epsilon": eps, "locate_host": loc_host, "harness": harness},

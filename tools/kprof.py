@@ -43,6 +43,7 @@ PASSES = {
             "SQ_INSTS_LDS", "SQ_INSTS_VALU", "SQ_WAIT_INST_LDS"],
     "sq2": ["--pmc", "SQ_LDS_BANK_CONFLICT", "SQ_LDS_IDX_ACTIVE", "SQ_INSTS_SALU", "SQ_INSTS_VMEM_RD",
             "SQ_INSTS_VMEM_WR", "SQ_BUSY_CYCLES", "GRBM_GUI_ACTIVE"],
+    "l2": ["--pmc", "TCC_HIT_sum", "TCC_MISS_sum"],
 }
 
 
@@ -90,7 +91,7 @@ def summarize(tag: str) -> dict:
         rows[k]["res"] = {"vgpr": int(r.get("VGPR_Count") or 0), "scratch": int(r.get("Scratch_Size") or 0),
                           "lds": int(r.get("LDS_Block_Size") or 0), "wg": int(r.get("Workgroup_Size_X") or 0)}
         rows[k]["dur_ns"] += int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
-    for p in ("fetch", "write", "sq1", "sq2"):
+    for p in ("fetch", "write", "sq1", "sq2", "l2"):
         for r in _rows(f"gpurun_out/kprof_{tag}_{p}/run_counter_collection.csv"):
             k = (kname(r["Kernel_Name"]), int(r.get("Grid_Size", 0) or 0))
             rows[k]["ctr"][r["Counter_Name"]] += float(r["Counter_Value"])
@@ -128,6 +129,8 @@ def summarize(tag: str) -> dict:
             if c.get("GRBM_GUI_ACTIVE") and wc:
                 # SQ_WAVE_CYCLES counts per SE in quad-cycles on CDNA; GRBM_GUI_ACTIVE in cycles per XCD
                 row["waves_per_cu"] = round(wc * 4 / (c["GRBM_GUI_ACTIVE"] / 8) / 256, 2)
+        if dp.get("l2") and c.get("TCC_HIT_sum", 0) + c.get("TCC_MISS_sum", 0):
+            row["l2_hit"] = round(c["TCC_HIT_sum"] / (c["TCC_HIT_sum"] + c["TCC_MISS_sum"]), 4)
         out.append(row)
     out.sort(key=lambda r: -(r["avg_us"] or 0) * r["calls"])
     res = {"tag": tag, "note": "per launch; read = 2 x FETCH_SIZE (gfx950 wide-read calibration), write = "
@@ -139,9 +142,9 @@ def summarize(tag: str) -> dict:
 
 
 # bench.py timer name -> kernel-name prefix (profiles/pmc_kernels.json feeds roofline.traffic)
-TIMERS = {"sa_bucket_sort": "hk::k_bucket_sort_fast<", "byte_hist": "hk::k_byte_hist", "wt_bits": "hk::k_wt_bits<",
+TIMERS = {"sa_bucket_sort": "hk::k_bucket_sort_rec<", "byte_hist": "hk::k_byte_hist", "wt_bits": "hk::k_wt_bits<",
           "wt_partition": "hk::k_wt_partition<", "radix_part_text": "hk::k_cpart<0,", "radix_part": "hk::k_cpart<2,",
-          "sa_bucket_hist": "hk::k_slice_hist_spans<"}
+          "sa_bucket_hist": "hk::k_slice_hist_spans<", "fm_count": "hk::k_count<"}
 
 
 def pmc_json(res: dict, path: str):
@@ -155,6 +158,9 @@ def pmc_json(res: dict, path: str):
         r = max(rows, key=lambda x: x["grid"])
         out[name] = {"kernel": r["kernel"], "read_gb_per_launch": r["read_gb"], "write_gb_per_launch": r["write_gb"],
                      "traffic_gb_per_launch": r["traffic_gb"], "avg_us": r["avg_us"]}
+        for extra in ("l2_hit", "waves_per_cu", "lds_conflict", "wait_any"):
+            if extra in r:
+                out[name][extra] = r[extra]
     with open(path, "w") as f:
         json.dump(out, f, indent=1)
 
@@ -167,7 +173,7 @@ def main():
         argv, cmd = argv[:i], argv[i + 1:]
     ap = argparse.ArgumentParser()
     ap.add_argument("--tag", required=True)
-    ap.add_argument("--passes", default="stats,fetch,write,sq1,sq2")
+    ap.add_argument("--passes", default="stats,fetch,write,sq1,sq2,l2")
     ap.add_argument("--filter", default=None, help="kernel regex for the counter passes")
     ap.add_argument("--limit", type=int, default=240, help="seconds per pass")
     ap.add_argument("--summarize-only", action="store_true")
