@@ -648,6 +648,44 @@ def harness_leg(n: int, seed: int, lengths=(5, 10, 50, 100, 500, 1000), iteratio
 
 
 # ---------------------------------------------------------------------------- sharded / multi-GPU
+def strong_leg(args, rank: int, world: int, local_rank: int, uid) -> dict:
+    """configs[4]'s fixed text (--strong-bytes, 4 GiB + '$') over the same ranks after the weak-scaling line
+    (SURVEY.md §8e's 1 -> 8 curve in both modes): one warm-up and up to three timed sharded builds,
+    barrier-bracketed, max over ranks."""
+    import torch
+    import torch.distributed as dist
+    from hkcsa import DeviceIndex
+    n = args.strong_bytes + 1
+    dev = DeviceIndex.synthetic(n, DNA, seed=args.seed, device=local_rank, flags=1 if args.pos64 else 0)
+    steps = max(1, min(args.steps, 3))
+    single = world == 1 and n >= (1 << 32) - 1   # (one rank: the library's own slices, as run_sharded)
+
+    def step():
+        if single:
+            dev.build_sa()
+        else:
+            dev.build_sa_sharded(uid, world, rank)
+
+    step()
+    dev.synchronize()
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    dev.synchronize()
+    torch.cuda.synchronize()
+    el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+    dist.barrier()
+    dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    lo, hi = (0, n) if single else dev.shard_range()
+    dev.close()
+    wall = float(el.item())
+    return {"text_symbols": n, "scaling": "strong", "n_gpus": world, "steps": steps,
+            "ms_per_step": round(wall / steps * 1e3, 3), "MBps": round(steps * n / 2**20 / wall, 2),
+            "rank0_slice": [lo, hi], "note": "configs[4]: the same 4 GiB text at every N (strong scaling)"}
+
+
 def run_sharded(args, rank: int, world: int, local_rank: int) -> dict | None:
     import torch
     import torch.distributed as dist
@@ -722,6 +760,10 @@ def run_sharded(args, rank: int, world: int, local_rank: int) -> dict | None:
                "locate_patterns_per_s": round(P / float(ts[0]), 1), "count_patterns_per_s": round(P / float(ts[1]), 1),
                "replicate_ms": round(float(ts[2]) * 1e3, 2), "wt_build_ms": round(float(ts[3]) * 1e3, 2),
                "split": f"P/{world} patterns per rank, max-over-ranks time"}
+    dev.close()
+    strong = None
+    if (world > 1 or args.sharded) and not args.strong and not single and args.strong_leg:
+        strong = strong_leg(args, rank, world, local_rank, uid)
     res = None
     if rank == 0:
         value = args.steps * n / 2**20 / wall
@@ -751,9 +793,11 @@ def run_sharded(args, rank: int, world: int, local_rank: int) -> dict | None:
             "roofline": roof,
             "locate_patterns_per_s": loc["locate_patterns_per_s"] if loc else None,
             "detail": {"rank0_slice": [lo, hi], "slices_per_gpu": per_gpu, "locate": loc,
-                       "stages_ms_total": stages, "build_info": info},
+                       "stages_ms_total": stages, "build_info": info, "strong_4GiB": strong},
         }
-    dev.close()
+        if not args.no_cpu_baseline:   # rank 0's host cores, after every timed region (the other ranks wait)
+            res["cpu_baseline"] = cpu_baseline(args.cpu_sample, args.cpu_patterns, args.cpu_config0)
+    dist.barrier()
     return res
 
 
@@ -860,6 +904,8 @@ def parse_args(argv=None):
     ap.add_argument("--strong", action="store_true", help="fixed text of --strong-bytes over the N GPUs")
     ap.add_argument("--strong-bytes", type=int, default=1 << 32)
     ap.add_argument("--pos64", action="store_true", help="sharded build with 64-bit positions at any n")
+    ap.add_argument("--no-strong-leg", dest="strong_leg", action="store_false",
+                    help="N > 1: skip configs[4]'s fixed 4 GiB (strong-scaling) leg after the weak-scaling line")
     ap.add_argument("--global-sort", action="store_true",
                     help="single-GPU build by full-width LSD sort of the keys (no LDS bucket sorts)")
     ap.add_argument("--only-leg", choices=("english", "protein"), default=None,
