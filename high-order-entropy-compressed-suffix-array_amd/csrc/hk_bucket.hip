@@ -2718,7 +2718,6 @@ __global__ __launch_bounds__(BR_T, 4) void k_bucket_sort_rec(const uint64_t* __r
                                                           unsigned long long* __restrict__ tie_n,
                                                           uint2* __restrict__ fb, unsigned int* __restrict__ fb_n,
                                                           PkGeom pg, uint64_t* __restrict__ trace = nullptr) {
-  static_assert(sizeof(V) == 4, "u32 positions");
   __shared__ BrShared sh;
   uint64_t ts[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   if (TRACE) ts[0] = stamp();
@@ -3048,10 +3047,12 @@ __global__ __launch_bounds__(BR_T, 4) void k_bucket_sort_rec(const uint64_t* __r
   unsigned long long tbase = 0;
   if (tid == 0 && ntie) tbase = atomicAdd(tie_n, (unsigned long long)ntie);
   // ---- 5. SA / BWT in sorted order straight from the plane
-  const uint32_t posm = pbits >= 32 ? ~0u : (1u << pbits) - 1, pmask = (1u << pb) - 1;
+  // u64 positions (slices of texts past 2^32): the position is the record's low pbits = 32 + phb bits
+  const uint64_t posm = (1ull << pbits) - 1;
+  const uint32_t pmask = (1u << pb) - 1;
   auto bwt_of = [&](uint64_t r) -> uint32_t {
-    const uint32_t pos = (uint32_t)r & posm, pv = (uint32_t)(r >> pbits) & pmask;
-    return pos == 0 && term >= 0 ? (uint32_t)term : (uint32_t)tab[pv];
+    const uint32_t pv = (uint32_t)(r >> pbits) & pmask;
+    return (r & posm) == 0 && term >= 0 ? (uint32_t)term : (uint32_t)tab[pv];
   };
   if (vec) {
     const uint32_t ng = (cnt + al + 3) >> 2;
@@ -3060,11 +3061,12 @@ __global__ __launch_bounds__(BR_T, 4) void k_bucket_sort_rec(const uint64_t* __r
       const uint4 ra = reinterpret_cast<const uint4*>(sh.rec)[2 * q];
       const uint4 rb = reinterpret_cast<const uint4*>(sh.rec)[2 * q + 1];
       const uint32_t lo4[4] = {ra.x, ra.z, rb.x, rb.z}, hi4[4] = {ra.y, ra.w, rb.y, rb.w};
-      uint32_t pos[4], sel = 0;
+      uint64_t pos[4];
+      uint32_t sel = 0;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const uint64_t r = ((uint64_t)hi4[j] << 32) | lo4[j];
-        pos[j] = lo4[j] & posm;
+        pos[j] = r & posm;
         sel |= ((uint32_t)(r >> pbits) & pmask) << (8 * j);
       }
       uint32_t bw = __builtin_amdgcn_perm(thi, tlo, sel);
@@ -3075,14 +3077,21 @@ __global__ __launch_bounds__(BR_T, 4) void k_bucket_sort_rec(const uint64_t* __r
       }
       const uint32_t g = 4u * q;
       if (g >= al && g + 4 <= cnt + al) {   // a whole group: aligned vector stores
-        *reinterpret_cast<uint4*>(sa + start + (g - al)) = make_uint4(pos[0], pos[1], pos[2], pos[3]);
+        if constexpr (sizeof(V) == 4) {
+          *reinterpret_cast<uint4*>(sa + start + (g - al)) =
+              make_uint4((uint32_t)pos[0], (uint32_t)pos[1], (uint32_t)pos[2], (uint32_t)pos[3]);
+        } else {
+          uint4* const d4 = reinterpret_cast<uint4*>(sa + start + (g - al));
+          d4[0] = make_uint4((uint32_t)pos[0], (uint32_t)(pos[0] >> 32), (uint32_t)pos[1], (uint32_t)(pos[1] >> 32));
+          d4[1] = make_uint4((uint32_t)pos[2], (uint32_t)(pos[2] >> 32), (uint32_t)pos[3], (uint32_t)(pos[3] >> 32));
+        }
         *reinterpret_cast<uint32_t*>(bwt + start + (g - al)) = bw;
       } else {
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const uint32_t r = g + j;
           if (r >= al && r < cnt + al) {
-            sa[start + r - al] = pos[j];
+            sa[start + r - al] = (V)pos[j];
             bwt[start + r - al] = (uint8_t)(bw >> (8 * j));
           }
         }
@@ -3091,7 +3100,7 @@ __global__ __launch_bounds__(BR_T, 4) void k_bucket_sort_rec(const uint64_t* __r
   } else {
     for (uint32_t r = tid; r < cnt; r += BR_T) {
       const uint64_t x = sh.rec[r];
-      sa[start + r] = (uint32_t)x & posm;
+      sa[start + r] = (V)(x & posm);
       bwt[start + r] = (uint8_t)bwt_of(x);
     }
   }
@@ -3106,7 +3115,7 @@ __global__ __launch_bounds__(BR_T, 4) void k_bucket_sort_rec(const uint64_t* __r
       auto put = [&](uint32_t f, uint32_t len) {
         for (uint32_t j = 0; j < len; ++j) {
           tie_k[tb + j] = ((uint64_t)(start + f + j - sto) << 1) | (j == 0 ? 1u : 0u);
-          tie_v[tb + j] = (V)((uint32_t)sh.rec[f + j] & posm);
+          tie_v[tb + j] = (V)(sh.rec[f + j] & posm);
         }
         tb += len;
       };
@@ -3372,12 +3381,14 @@ uint64_t sort_bucket_items(Index& ix, const BucketPlan& plan, const uint64_t* ke
         constexpr int T = decltype(ttag)::value;
         constexpr int I = decltype(itag)::value;
         constexpr bool TR = decltype(trtag)::value;
-        if constexpr (T == 512 && sizeof(V) == 4) {
-          // the record-plane sort: sigma <= 8 codes, u32 positions, sym fields in the high words, and room
-          // for (low key <= 17 bits) << xsh (HKCSA_BS_REC=0 keeps the fast path, for A/B)
+        if constexpr (T == 512) {
+          // the record-plane sort: sigma <= 8 codes, sym fields in the high words, and room for (low key
+          // <= 17 bits) << xsh; u64 positions as the record's low 32 + phb bits (HKCSA_BS_REC=0 keeps the
+          // fast path, for A/B)
           static const bool rec_off = getenv("HKCSA_BS_REC") && getenv("HKCSA_BS_REC")[0] == '0';
           const int xsh = pk ? pk->g.pbits + pk->g.pb2 : 0;
-          if (pk && !rec_off && xsh >= 32 && xsh + 17 <= 64 && pk->g.pb2 <= 3 && pk->g.phb == 0 &&
+          const bool pos_ok = pk && (pk->g.phb == 0 || (sizeof(V) == 8 && pk->g.pbits == 32 + pk->g.phb));
+          if (pk && !rec_off && xsh >= 32 && xsh + 17 <= 64 && pk->g.pb2 <= 3 && pos_ok &&
               plan.cap <= (uint64_t)BR_CAP) {
             if (trace)
               k_bucket_sort_rec<V, true><<<grid_n, BR_T, 0, s>>>(

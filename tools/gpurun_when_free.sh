@@ -7,6 +7,6 @@ for try in $(seq 1 12); do
   /usr/local/graft/bin/gpurun --timeout "$to" -- "$@" > "$out" 2>&1
   rc=$?
   [ $rc -ne 3 ] && exit $rc
-  sleep 200
+  sleep 60
 done
 exit 3
