@@ -3430,7 +3430,7 @@ uint64_t sort_bucket_items(Index& ix, const BucketPlan& plan, const uint64_t* ke
       if (plan.cap <= (uint64_t)512 * BS_I) {
         if (trace) launch(T512{}, I18{}, TrOn{}); else launch(T512{}, I18{}, TrOff{});
       } else {
-        if (trace) launch(T1024{}, I18{}, TrOn{}); else launch(T1024{}, I18{}, TrOff{});
+        launch(T1024{}, I18{}, TrOff{});   // (the phase stamps: 512-thread items only; the 1024-thread build spilled)
       }
       HK_HIP(hipGetLastError());
       if (trace) {

@@ -694,7 +694,7 @@ int radix_sort_pairs(SortWork& w, KernelTimer& tm, uint64_t* k[2], V* v[2], int 
 // ---------------------------------------------------------------- diagnostics
 // Times `reps` radix passes of variant (threads x items, mode) over n DNA-text keys (u32 values)
 // plus a plain pair copy of the same bytes; used to decide where a pass spends its time.
-template <int T, int I, int MODE, int LBW = 16>
+template <int T, int I, int MODE, int LBW = 4>
 static double time_variant(SortWork& w, uint64_t* k[2], uint32_t* v[2], uint64_t n, int reps, int bit_lo,
                            const uint64_t* pristine, hipStream_t s) {
   // every variant starts from the same keys: the ablations scramble the multiset, and an exact

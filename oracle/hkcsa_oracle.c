@@ -59,42 +59,59 @@ void oracle_count(const uint8_t* t, uint64_t n, uint64_t C[257]) {
 }
 
 /* ------------------------------------------------------------------- occ
- * utils/utils.py:26-32 stores occ[c][i] = #c in bwt[0:i) for every i; here a sampled table
- * (every 64 positions, all 256 symbols) answers the same query. */
+ * utils/utils.py:26-32 stores occ[c][i] = #c in bwt[0:i) for every i; here a sampled table answers the
+ * same query: for the symbols present (dense columns), u64 counts every 65536 positions and u16 counts
+ * relative to them every 64 positions, then a scan of < 64 bytes.  u64 superblocks: texts past 2^32
+ * symbols (a symbol may occur more than 2^32 times) are answered exactly. */
 typedef struct {
   const uint8_t* bwt;
   uint64_t n;
-  uint32_t* samp; /* (n/64 + 1) x 256 */
+  int sig;                 /* present symbols (columns) */
+  int16_t col[256];        /* symbol -> column, -1 if absent */
+  uint64_t* sup;           /* (n >> 16) + 1 rows x sig */
+  uint16_t* sub;           /* (n >> 6) + 1 rows x sig, relative to the row's superblock */
 } occ_t;
 
 void* oracle_occ_new(const uint8_t* bwt, uint64_t n) {
   occ_t* o = (occ_t*)malloc(sizeof(occ_t));
-  const uint64_t nb = n / 64 + 1;
   o->bwt = bwt;
   o->n = n;
-  o->samp = (uint32_t*)calloc(nb * 256, sizeof(uint32_t));
-  /* chunked over OpenMP threads: per-chunk symbol totals, their exclusive prefix, then each chunk fills
-   * its samples from its prefix */
   int T = 1;
 #ifdef _OPENMP
   T = omp_get_max_threads();
 #endif
+  const uint64_t nsup = (n >> 16) + 1, nsub = (n >> 6) + 1;
+  /* chunks of whole superblocks: per-chunk symbol totals, their exclusive prefix, then each chunk fills
+   * its rows from its prefix */
+  const uint64_t per = (nsup + T - 1) / T;
   uint64_t* tot = (uint64_t*)calloc((size_t)(T + 1) * 256, sizeof(uint64_t));
-  const uint64_t per = (nb + T - 1) / T;   /* blocks of 64 per chunk */
 #pragma omp parallel for schedule(static, 1)
   for (int c = 0; c < T; ++c) {
-    const uint64_t b0 = per * c, b1 = per * (c + 1) < nb ? per * (c + 1) : nb;
-    for (uint64_t i = b0 * 64; i < b1 * 64 && i < n; ++i) tot[(size_t)(c + 1) * 256 + bwt[i]]++;
+    const uint64_t i0 = (per * c) << 16, i1 = (per * (c + 1)) << 16;
+    for (uint64_t i = i0; i < i1 && i < n; ++i) tot[(size_t)(c + 1) * 256 + bwt[i]]++;
   }
   for (int c = 1; c <= T; ++c)
-    for (int s = 0; s < 256; ++s) tot[(size_t)c * 256 + s] += tot[(size_t)(c - 1) * 256 + s];
+    for (int s2 = 0; s2 < 256; ++s2) tot[(size_t)c * 256 + s2] += tot[(size_t)(c - 1) * 256 + s2];
+  o->sig = 0;
+  for (int s2 = 0; s2 < 256; ++s2) o->col[s2] = tot[(size_t)T * 256 + s2] ? (int16_t)o->sig++ : (int16_t)-1;
+  const int sig = o->sig ? o->sig : 1;
+  o->sup = (uint64_t*)calloc(nsup * sig, sizeof(uint64_t));
+  o->sub = (uint16_t*)calloc(nsub * sig, sizeof(uint16_t));
 #pragma omp parallel for schedule(static, 1)
   for (int c = 0; c < T; ++c) {
-    const uint64_t b0 = per * c, b1 = per * (c + 1) < nb ? per * (c + 1) : nb;
-    uint32_t cur[256];
-    for (int s = 0; s < 256; ++s) cur[s] = (uint32_t)tot[(size_t)c * 256 + s];
-    for (uint64_t i = b0 * 64; i < b1 * 64 && i <= n; ++i) {
-      if ((i & 63) == 0) memcpy(o->samp + (i >> 6) * 256, cur, sizeof(cur));
+    const uint64_t i0 = (per * c) << 16, i1 = (per * (c + 1)) << 16;
+    uint64_t cur[256], base[256];
+    for (int s2 = 0; s2 < 256; ++s2) cur[s2] = tot[(size_t)c * 256 + s2];
+    for (uint64_t i = i0; i < i1 && i <= n; ++i) {
+      if ((i & 0xFFFF) == 0) {
+        for (int s2 = 0; s2 < 256; ++s2) {
+          base[s2] = cur[s2];
+          if (o->col[s2] >= 0) o->sup[(i >> 16) * sig + o->col[s2]] = cur[s2];
+        }
+      }
+      if ((i & 63) == 0)
+        for (int s2 = 0; s2 < 256; ++s2)
+          if (o->col[s2] >= 0) o->sub[(i >> 6) * sig + o->col[s2]] = (uint16_t)(cur[s2] - base[s2]);
       if (i < n) cur[bwt[i]]++;
     }
   }
@@ -105,7 +122,8 @@ void* oracle_occ_new(const uint8_t* bwt, uint64_t n) {
 void oracle_occ_free(void* p) {
   occ_t* o = (occ_t*)p;
   if (!o) return;
-  free(o->samp);
+  free(o->sup);
+  free(o->sub);
   free(o);
 }
 
@@ -114,8 +132,10 @@ void oracle_occ_free(void* p) {
 uint64_t oracle_occ(const void* p, uint8_t c, uint64_t i) {
   const occ_t* o = (const occ_t*)p;
   if (i > o->n) i = o->n;
-  uint64_t r = o->samp[(i >> 6) * 256 + c];
-  for (uint64_t k = i & ~(uint64_t)63; k < i; ++k) r += o->bwt[k] == c;
+  const int k = o->col[c];
+  if (k < 0) return 0;
+  uint64_t r = o->sup[(i >> 16) * o->sig + k] + o->sub[(i >> 6) * o->sig + k];
+  for (uint64_t q = i & ~(uint64_t)63; q < i; ++q) r += o->bwt[q] == c;
   return r;
 }
 

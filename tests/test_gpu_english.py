@@ -42,7 +42,7 @@ def _full_check(hk, text, npat, seed, flags=0, wt=True, fm=True):
         for d in range(len(want)):
             assert np.array_equal(dev.wt_level_bits(d), want[d]), d
         del want
-    if not fm:   # (SA and BWT only: the oracle FM index of a GiB costs the suite ~25 s)
+    if not fm:
         dev.close()
         return info
     rng = np.random.default_rng(seed)
@@ -62,10 +62,11 @@ def _full_check(hk, text, npat, seed, flags=0, wt=True, fm=True):
 
 
 def test_english_like_200MiB_full_build(hk):
-    """configs[2] shape at its size: 200 MiB + '$', full build, all WT levels, 10k 20-symbol counts."""
+    """configs[2] shape at its size: 200 MiB + '$', full build, all WT levels, 1M 20-symbol counts (the
+    bench leg's batch size) and 300 locates against the oracle FM index."""
     from utils.textgen import english_like_text
     text = english_like_text(200 * (1 << 20) + 1, seed=3)
-    info = _full_check(hk, text, 10000, seed=31)
+    info = _full_check(hk, text, 1_000_000, seed=31)
     assert info[2] >> 32 > 0, info[:12]         # the prefix-doubling fallback ran (long copies)
 
 
@@ -91,11 +92,11 @@ def test_english_like_global_sort_flag(hk):
 def test_protein_like_1GiB_full_build(hk):
     """The proteins corpus shape (tests/dataset_benchmark.py:13) at 1 GiB: sigma = 25 + newline + '$' (not a
     power of two, so the stable onesweep pair instead of the cursor passes), skewed letter frequencies,
-    35 % family members (copies with 8 % substitutions) and 5 % exact duplicates.  SA by the O(n) checker and
-    BWT by the oracle's gather (counts, locate and every WT level are checked on the 24 MiB text below)."""
+    35 % family members (copies with 8 % substitutions) and 5 % exact duplicates.  SA by the O(n) checker,
+    BWT by the oracle's gather, every WT level, 100k 20-symbol counts and 300 locates against the oracle."""
     from utils.textgen import protein_like_text
     text = protein_like_text((1 << 30) + 1, seed=4)
-    _full_check(hk, text, 4000, seed=41, wt=False, fm=False)
+    _full_check(hk, text, 100_000, seed=41)
 
 
 def test_protein_like_24MiB_wt(hk):

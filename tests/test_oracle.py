@@ -182,3 +182,19 @@ def test_synth_text_deterministic():
     c = oracle.synth_text(1000, b"ACGT", seed=6)
     assert np.array_equal(a, b) and not np.array_equal(a, c)
     assert a[-1] == ord("$") and set(a[:-1].tobytes()) <= set(b"ACGT")
+
+
+def test_oracle_occ_superblocks():
+    """oracle_occ's u64 superblocks + u16 relative samples against a cumulative count, across several
+    2^16 superblock seams and 64-symbol sample seams (the table that lets oracle.FM check texts past 2^32)."""
+    from oracle import oracle
+    rng = np.random.default_rng(12)
+    t = np.frombuffer(b"ACGT", np.uint8)[rng.integers(0, 4, size=300_000)].copy()
+    t[-1] = ord("$")
+    fm = oracle.FM(t, sa=np.arange(len(t), dtype=np.uint64))   # any permutation gives a BWT-like sequence
+    b = fm.bwt
+    for c in (ord("A"), ord("T"), ord("$"), ord("Z")):
+        cum = np.concatenate([[0], np.cumsum(b == c)])
+        idx = np.concatenate([rng.integers(0, len(b) + 1, size=400), [0, 63, 64, 65535, 65536, 131072, len(b)]])
+        for i in idx:
+            assert fm.rank(c, int(i)) == int(cum[i]), (chr(c), i)
