@@ -574,7 +574,7 @@ def protein_leg(args) -> dict:
     pair, LDS bucket sorts, refinement)."""
     from hkcsa import DeviceIndex
     from utils.textgen import protein_like_text
-    n = (1 << 30) + 1
+    n = int(os.environ.get("BENCH_PROTEIN_MIB", "1024")) * (1 << 20) + 1   # (size override: experiments)
     t0 = time.perf_counter()
     text = protein_like_text(n, seed=args.seed + 40)
     gen_s = time.perf_counter() - t0
