@@ -1012,7 +1012,9 @@ struct alignas(16) BrShared {
 };
 static_assert(sizeof(BrShared) <= 81920, "two workgroups per CU");
 
-template <typename V, bool TRACE = false>
+// X32: the sym field starts at bit >= 32 (texts of 2^30 suffixes and more, slices), so the prologue works in
+// 32-bit arithmetic; else it is the record's bits >= xsh as a u64.
+template <typename V, bool TRACE = false, bool X32 = true>
 __global__ __launch_bounds__(BR_T, 4) void k_bucket_sort_rec(const uint64_t* __restrict__ keys,
                                                           const uint2* __restrict__ items,
                                                           const uint8_t* __restrict__ inv, V* __restrict__ sa,
@@ -1027,7 +1029,7 @@ __global__ __launch_bounds__(BR_T, 4) void k_bucket_sort_rec(const uint64_t* __r
   const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const uint2 it = items[blockIdx.x];
   const uint32_t start = it.x, cnt = it.y;
-  const int pbits = pg.pbits, pb = pg.pb2, xsh = pbits + pb;   // xsh >= 32 (X32)
+  const int pbits = pg.pbits, pb = pg.pb2, xsh = pbits + pb;   // (X32: xsh >= 32)
   // the BWT byte of each keyed prev code (codes at or above the unique terminal's shift up by one)
   const bool remap = pg.tcode >= 0;
   uint8_t* const tab = reinterpret_cast<uint8_t*>(sh.base + BR_NG + 4);
@@ -1044,42 +1046,60 @@ __global__ __launch_bounds__(BR_T, 4) void k_bucket_sort_rec(const uint64_t* __r
   const uint8_t tv = tid < 8 ? inv[remap && tid >= (uint32_t)pg.tcode ? tid + 1 : tid] : 0;
   const int term = remap ? (int)inv[pg.tcode] : -1;
   reinterpret_cast<uint4*>(sh.cnt)[tid] = make_uint4(0u, 0u, 0u, 0u);   // the 8192 u8 counters
-  auto symx = [&](int k) -> uint32_t { return (uint32_t)(key[k] >> 32) >> (xsh - 32); };
+  using XT = std::conditional_t<X32, uint32_t, uint64_t>;
+  auto symx = [&](int k) -> XT {
+    if constexpr (X32) return (uint32_t)(key[k] >> 32) >> (xsh - 32);
+    else return key[k] >> xsh;
+  };
   // ---- 0. the item's sym range: min, max, or, and (the varying bits are those of the values relative
   // to the minimum)
-  uint32_t xmin = ~0u, xmax = 0, vor = 0, vand = ~0u;
+  XT xmin = (XT)~0ull, xmax = 0, vor = 0, vand = (XT)~0ull;
 #pragma unroll
   for (int k = 0; k < BR_I; ++k) {
     const bool valid = (vmask >> k) & 1u;
-    const uint32_t x = symx(k);
+    const XT x = symx(k);
     xmin = valid && x < xmin ? x : xmin;
     xmax = valid && x > xmax ? x : xmax;
-    vor |= valid ? x : 0u;
-    vand &= valid ? x : ~0u;
+    vor |= valid ? x : (XT)0;
+    vand &= valid ? x : (XT)~0ull;
   }
-  xmin = dpp_reduce_u32(xmin, ~0u, [](uint32_t a, uint32_t b) { return a < b ? a : b; });
-  xmax = dpp_reduce_u32(xmax, 0u, [](uint32_t a, uint32_t b) { return a > b ? a : b; });
-  vor = dpp_reduce_u32(vor, 0u, [](uint32_t a, uint32_t b) { return a | b; });
-  vand = dpp_reduce_u32(vand, ~0u, [](uint32_t a, uint32_t b) { return a & b; });
+  // the per-wave results through LDS: u32 in scr (X32), u64 in the record plane (free until phase 3)
+  XT* const red = X32 ? reinterpret_cast<XT*>(sh.scr) : reinterpret_cast<XT*>(sh.rec);
+  if constexpr (X32) {
+    xmin = dpp_reduce_u32(xmin, ~0u, [](uint32_t a, uint32_t b) { return a < b ? a : b; });
+    xmax = dpp_reduce_u32(xmax, 0u, [](uint32_t a, uint32_t b) { return a > b ? a : b; });
+    vor = dpp_reduce_u32(vor, 0u, [](uint32_t a, uint32_t b) { return a | b; });
+    vand = dpp_reduce_u32(vand, ~0u, [](uint32_t a, uint32_t b) { return a & b; });
+  } else {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const XT a0 = __shfl_xor(xmin, o, 64), a1 = __shfl_xor(xmax, o, 64);
+      xmin = a0 < xmin ? a0 : xmin;
+      xmax = a1 > xmax ? a1 : xmax;
+      vor |= __shfl_xor(vor, o, 64);
+      vand &= __shfl_xor(vand, o, 64);
+    }
+  }
   if (lane == 0) {
-    sh.scr[wv] = xmin;
-    sh.scr[8 + wv] = xmax;
-    sh.scr[16 + wv] = vor;
-    sh.scr[24 + wv] = vand;
+    red[wv] = xmin;
+    red[8 + wv] = xmax;
+    red[16 + wv] = vor;
+    red[24 + wv] = vand;
   }
   if (tid < 8) tab[tid] = tv;
   __syncthreads();
 #pragma unroll
   for (int w = 0; w < BR_T / 64; ++w) {
-    xmin = sh.scr[w] < xmin ? sh.scr[w] : xmin;
-    xmax = sh.scr[8 + w] > xmax ? sh.scr[8 + w] : xmax;
-    vor |= sh.scr[16 + w];
-    vand &= sh.scr[24 + w];
+    xmin = red[w] < xmin ? red[w] : xmin;
+    xmax = red[8 + w] > xmax ? red[8 + w] : xmax;
+    vor |= red[16 + w];
+    vand &= red[24 + w];
   }
   if (TRACE) ts[1] = stamp();
-  const uint32_t var = vor ^ vand;
-  const int lo = var ? __builtin_ctz(var) : 0;
-  const int width = var ? 32 - __builtin_clz((xmax - xmin) >> lo) : 0;
+  const uint64_t var = (uint64_t)(vor ^ vand);
+  const int lo = var ? __builtin_ctzll(var) : 0;
+  const uint64_t spanx = (uint64_t)(xmax - xmin) >> lo;
+  const int width = var ? 64 - __builtin_clzll(spanx) : 0;
   auto fallback = [&]() {
     if (tid == 0) fb[atomicAdd(fb_n, 1u)] = it;
   };
@@ -1089,7 +1109,7 @@ __global__ __launch_bounds__(BR_T, 4) void k_bucket_sort_rec(const uint64_t* __r
   }
   const int kb = width > BR_BITS ? width - BR_BITS : 0;   // key bits below the bin (<= 17)
   const uint32_t wmask = (1u << width) - 1, lowmask = (1u << kb) - 1;
-  auto local = [&](int k) -> uint32_t { return ((symx(k) - xmin) >> lo) & wmask; };
+  auto local = [&](int k) -> uint32_t { return (uint32_t)((symx(k) - xmin) >> lo) & wmask; };
   // ---- 1. u8 bin counters; the atomic's return is the suffix's rank inside its bin
   uint32_t rk[(BR_I + 3) / 4];
 #pragma unroll
@@ -1482,27 +1502,27 @@ uint64_t sort_bucket_items(Index& ix, const BucketPlan& plan, const uint64_t* ke
       ix.bk_fb.ensure(nn * sizeof(uint2) + 16);
       unsigned int* fbn = reinterpret_cast<unsigned int*>(ix.small.as<uint8_t>() + 4352);   // small+4352: fallback count
       HK_HIP(hipMemsetAsync(fbn, 0, 4, s));
+      bool used_rec = false;
       auto launch = [&](auto ttag, auto itag, auto trtag) {
         constexpr int T = decltype(ttag)::value;
         constexpr int I = decltype(itag)::value;
         constexpr bool TR = decltype(trtag)::value;
         if constexpr (T == 512) {
-          // the record-plane sort: sigma <= 8 codes, sym fields in the high words, and room for (low key
-          // <= 17 bits) << xsh; u64 positions as the record's low 32 + phb bits (HKCSA_BS_REC=0 keeps the
-          // fast path, for A/B)
-          static const bool rec_off = getenv("HKCSA_BS_REC") && getenv("HKCSA_BS_REC")[0] == '0';
+          // the record-plane sort: sigma <= 8 codes and room for (low key <= 17 bits) << xsh; u64 positions
+          // as the record's low 32 + phb bits.  HKCSA_BS_REC=0 (read per call) keeps the fast path, for A/B.
+          const char* rec_env = getenv("HKCSA_BS_REC");
+          const bool rec_off = rec_env && rec_env[0] == '0';
           const int xsh = pk ? pk->g.pbits + pk->g.pb2 : 0;
           const bool pos_ok = pk && (pk->g.phb == 0 || (sizeof(V) == 8 && pk->g.pbits == 32 + pk->g.phb));
-          if (pk && !rec_off && xsh >= 32 && xsh + 17 <= 64 && pk->g.pb2 <= 3 && pos_ok &&
-              plan.cap <= (uint64_t)BR_CAP) {
-            if (trace)
-              k_bucket_sort_rec<V, true><<<grid_n, BR_T, 0, s>>>(
-                  keys, ix.bk_items.as<uint2>(), d_inv, sa, bwt, ix.ties_k.as<uint64_t>(), ix.ties_v.as<V>(),
-                  ix.ties_n.as<unsigned long long>(), ix.bk_fb.as<uint2>(), fbn, pk->g, tbuf.as<uint64_t>());
-            else
-              k_bucket_sort_rec<V><<<grid_n, BR_T, 0, s>>>(
-                  keys, ix.bk_items.as<uint2>(), d_inv, sa, bwt, ix.ties_k.as<uint64_t>(), ix.ties_v.as<V>(),
-                  ix.ties_n.as<unsigned long long>(), ix.bk_fb.as<uint2>(), fbn, pk->g);
+          if (pk && !rec_off && xsh + 17 <= 64 && pk->g.pb2 <= 3 && pos_ok && plan.cap <= (uint64_t)BR_CAP) {
+            auto go = [&](auto kern) {
+              kern<<<grid_n, BR_T, 0, s>>>(keys, ix.bk_items.as<uint2>(), d_inv, sa, bwt, ix.ties_k.as<uint64_t>(),
+                                           ix.ties_v.as<V>(), ix.ties_n.as<unsigned long long>(),
+                                           ix.bk_fb.as<uint2>(), fbn, pk->g, trace ? tbuf.as<uint64_t>() : nullptr);
+            };
+            if (xsh >= 32) trace ? go(k_bucket_sort_rec<V, true, true>) : go(k_bucket_sort_rec<V, false, true>);
+            else trace ? go(k_bucket_sort_rec<V, true, false>) : go(k_bucket_sort_rec<V, false, false>);
+            used_rec = true;
             return;
           }
         }
@@ -1547,8 +1567,8 @@ uint64_t sort_bucket_items(Index& ix, const BucketPlan& plan, const uint64_t* ke
           for (int i = 0; i < 7; ++i) acc[i] += (double)(h[w * 8 + i + 1] - h[w * 8 + i]);
         // (fast sort: load+prologue, hist, scan, scatter, small bins, listed bins, stage+out; record-plane
         // sort: load+prologue, hist, scan, scatter, pairs + lists, 3+ bins, output + ties)
-        fprintf(stderr, "[bucket_sort trace] %zu WGs, mean cycles per phase: %.0f %.0f %.0f %.0f %.0f %.0f %.0f\n",
-                (size_t)nn, acc[0] / nn, acc[1] / nn, acc[2] / nn, acc[3] / nn, acc[4] / nn, acc[5] / nn, acc[6] / nn);
+        fprintf(stderr, "[bucket_sort trace] %s sort, %zu WGs, mean cycles per phase: %.0f %.0f %.0f %.0f %.0f %.0f %.0f\n",
+                used_rec ? "record-plane" : "fast", (size_t)nn, acc[0] / nn, acc[1] / nn, acc[2] / nn, acc[3] / nn, acc[4] / nn, acc[5] / nn, acc[6] / nn);
       }
       // the fallback count and the tie count in one round trip (pinned slots); the tie count is read
       // again below only when fallback items ran

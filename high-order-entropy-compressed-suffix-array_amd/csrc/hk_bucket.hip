@@ -2084,8 +2084,6 @@ int cursor_partition(Index& ix, uint64_t n, int D, int bitlo, uint64_t kbias, co
 
 // the cursor partition groups buckets wherever D <= 16 (lookback-free; the stable onesweep passes
 // remain for texts without whole-symbol buckets)
-static bool cursor_enabled() { return true; }
-
 template <typename V>
 bool bucket_sort_slice(Index& ix, const KeyGeom& kg, uint64_t m, int hb, const SliceBins& bins, const uint64_t* d_h0) {
   hipStream_t s = ix.stream;
@@ -2101,7 +2099,7 @@ bool bucket_sort_slice(Index& ix, const KeyGeom& kg, uint64_t m, int hb, const S
     // (key - kmin << pbe) above bsh
     const uint64_t kbias = bins.mul ? 0 : bins.kmin << pbe;
     const int shift = bins.mul ? bins.binpos : pbe + bins.bsh;
-    if (cursor_enabled() && D <= 16) {
+    if (D <= 16) {
       // bin counts from the packed keys, then the two lookback-free cursor passes
       slot = cursor_partition(ix, m, D, shift, kbias, nullptr, kp, vp, hist);
     } else {
@@ -3219,7 +3217,7 @@ void build_sa_bucketed(Index& ix) {
     const int lb = (kg.Rk & (kg.Rk - 1)) == 0 ? __builtin_ctzll(kg.Rk) : 0;
     const bool whole = lb && sb == lb * kg.q;
     const int hq1 = lb ? (D + 1 + lb - 1) / lb : 0;
-    if (cursor_enabled() && whole && D > 0 && D + 1 <= 17 && D + 1 <= sb && hq1 * lb <= 32 && hq1 <= 16) {
+    if (whole && D > 0 && D + 1 <= 17 && D + 1 <= sb && hq1 * lb <= 32 && hq1 <= 16) {
       D += 1;
       ka.hq = hq1;
       item_T = 512;
@@ -3237,9 +3235,9 @@ void build_sa_bucketed(Index& ix) {
   const uint32_t nbins = 1u << D;
   std::vector<uint64_t> hist(nbins, 0);
   uint64_t* d_h0 = reinterpret_cast<uint64_t*>(ix.small.as<uint8_t>() + 5120);
-  // whole-symbol buckets: the lookback-free cursor partition (HKCSA_CURSOR=0: the stable onesweep
-  // passes with the late bucket histogram, for A/B)
-  const bool use_cp = cursor_enabled() && D > 0 && ka.hq > 0 && D <= 17;
+  // whole-symbol buckets: the lookback-free cursor partition; otherwise the stable onesweep passes with
+  // the late bucket histogram
+  const bool use_cp = D > 0 && ka.hq > 0 && D <= 17;
   const bool late_hist = D > 0 && ka.hq > 0 && !use_cp;
   bool skip_plan = false;   // a sample of the bucket counts already says: the global path
   if (use_cp) {

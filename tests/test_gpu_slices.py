@@ -117,6 +117,29 @@ def test_trace_builds_identical(hk, var, monkeypatch, capfd):
     assert "trace]" in err
 
 
+@pytest.mark.parametrize("rec", ["1", "0"])
+@pytest.mark.parametrize("alpha,n", [(b"ACGT", 8 << 20), (b"ab", 3 << 20), (b"ACGTNRYK", 5 << 20),
+                                     (b"ACGT", 1 << 16)])
+def test_record_sort_switch_identical(hk, rec, alpha, n, monkeypatch, capfd):
+    """HKCSA_BS_REC=0 (read per call) keeps the fast LDS sort where the record-plane sort would run; both
+    give the oracle's SA and BWT.  Small texts have the sym field below bit 32 (the u64 prologue), so this
+    covers the non-X32 record sort; the trace line names the sort that ran."""
+    text = oracle.synth_text(n + 1, alpha, seed=len(alpha) + n % 97)
+    want = oracle.suffix_array(text)
+    monkeypatch.setenv("HKCSA_BS_REC", rec)
+    monkeypatch.setenv("HKCSA_BS_TRACE", "1")
+    dev = hk.DeviceIndex.from_bytes(text, device=0, flags=16)   # 16: HKCSA_FLAG_MAX_BUCKETS
+    dev.build_sa()
+    assert np.array_equal(dev.sa(), want)
+    assert np.array_equal(dev.bwt(), oracle.bwt(text, want))
+    dev.close()
+    err = capfd.readouterr().err
+    if rec == "0":
+        assert "record-plane" not in err, err[-400:]
+    elif alpha == b"ACGT" and n >= 1 << 20:   # (sigma 2 runs 1024-thread items here: the fast sort)
+        assert "record-plane" in err, err[-400:]
+
+
 @pytest.mark.parametrize("nranks", [2, 3, 8])
 @pytest.mark.parametrize("alpha", [b"ACGT", bytes(range(256)), b"ab"])
 def test_keyed_below_rule_matches_host(hk, nranks, alpha):
