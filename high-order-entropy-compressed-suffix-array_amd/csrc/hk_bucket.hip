@@ -742,13 +742,15 @@ __global__ __launch_bounds__(T, T == 1024 ? 1 : (HS ? 3 * T / 256 : 2)) void k_c
 
 constexpr uint32_t SL_SUB = 8192;   // positions per sub-tile (= CP_TILE)
 
-// keyed codes (radix 2^2) of 16 text bytes, packed MSB-first (first byte in bits 31..30)
+// keyed codes (radix 2^2) of 16 text bytes, packed MSB-first (first byte in bits 31..30).  A word's four
+// codes (a byte each, from the table) fold into one byte by a dot product with the weights 64 / 16 / 4 / 1
+// (v_dot4_u32_u8, full rate; the multiply it replaced is a quarter-rate v_mul_lo_u32).
 __device__ __forceinline__ uint32_t pack16_2(const uint4& v, const SliceSel& sl) {
   auto p8 = [&](uint32_t w) -> uint32_t {
     const uint32_t c = __builtin_amdgcn_perm(sl.th, sl.tl, (w >> sl.ps) & 0x07070707u);   // 4 codes, a byte each
-    return (c * 0x40100401u) >> 24;   // c0 << 6 | c1 << 4 | c2 << 2 | c3 (the partial products never overlap)
+    return __builtin_amdgcn_udot4(c, 0x01041040u, 0u, false);   // c0 << 6 | c1 << 4 | c2 << 2 | c3
   };
-  return (p8(v.x) << 24) | (p8(v.y) << 16) | (p8(v.z) << 8) | p8(v.w);
+  return (((p8(v.x) << 8) | p8(v.y)) << 16) | (p8(v.z) << 8) | p8(v.w);
 }
 
 // the 32 code bits from position k of the packed stream w0:w1 (k compile-time after unrolling)
@@ -792,10 +794,11 @@ __global__ __launch_bounds__(BH_T, 1) void k_slice_hist_spans(const uint8_t* __r
   // then sum to less than the adds: the flush compares the two and raises *ovf (exact recount).
   constexpr bool NODRAIN = REG && CB == 8;
   uint32_t kc = 0;
-  auto add = [&](uint32_t b) {   // b: the slice bin, < sl.nb
+  uint32_t kcw = 0;   // (REG, not ALL: the wave's adds of whole-wave steps, from the keep ballots)
+  auto add = [&](uint32_t b, bool counted = false) {   // b: the slice bin, < sl.nb
     if constexpr (NODRAIN) {
       atomicAdd(&H[b >> 2], 1u << (8 * (b & 3)));
-      if constexpr (!ALL) ++kc;
+      if constexpr (!ALL) if (!counted) ++kc;
       return;
     }
     if (hb >= 0 && (b >> 16) != (uint32_t)hb) return;
@@ -835,6 +838,19 @@ __global__ __launch_bounds__(BH_T, 1) void k_slice_hist_spans(const uint8_t* __r
   for (int u = 0; u < PF; ++u) fetch(lo + (uint64_t)u * BH_TILE + (uint64_t)tid * BH_PER, f0[u], f1[u]);
   const uint64_t lim2 = lim < hi ? lim : hi;
   auto step = [&](uint64_t p0, const uint4 a, const uint4 b4) {
+    if constexpr (REG && NODRAIN && !ALL) {
+      if (__all(p0 + BH_PER <= lim2)) {   // (uniform) every lane's 16 positions keyed: the wave's adds
+        const uint32_t c0 = pack16_2(a, sl), c1 = pack16_2(b4, sl);   // counted from the keep ballots (SALU)
+#pragma unroll
+        for (int k = 0; k < BH_PER; ++k) {
+          const uint32_t w = win32(c0, c1, k) - sl.wb;
+          const bool keep = w <= sl.wn1;
+          kcw += (uint32_t)__popcll(__ballot(keep));
+          if (keep) add(w >> dsh, true);
+        }
+        return;
+      }
+    }
     if (p0 < lim2) {
       const bool full = p0 + BH_PER <= lim2;
       if constexpr (REG) {
@@ -894,7 +910,7 @@ __global__ __launch_bounds__(BH_T, 1) void k_slice_hist_spans(const uint8_t* __r
   }
   if (CB == 8 && bad) atomicOr(ovf, 1ull);
   if (NODRAIN) {
-    const uint32_t wk = wave_incl_sum<uint32_t>(kc);
+    const uint32_t wk = wave_incl_sum<uint32_t>(kc) + (uint32_t)__builtin_amdgcn_readfirstlane(kcw);
     if ((tid & 63) == 63 && wk) atomicAdd(&KT[0], wk);
   }
   __syncthreads();

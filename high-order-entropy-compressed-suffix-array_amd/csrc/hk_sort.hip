@@ -585,10 +585,12 @@ int radix_sort_pairs(SortWork& w, KernelTimer& tm, uint64_t* k[2], V* v[2], int 
     HK_HIP(hipGetLastError());
   };
   if (src && (!d_hist0 || !vals_iota)) throw ApiError{-1, "radix_sort_pairs: text keys need hist0 and iota values"};
-  // small sorts (refinement rounds): every digit's histogram and offsets from one read of the keys,
-  // then every pass back to back with no host round trip (no single-digit pass is skipped: a skipped
-  // small pass saves less than the readback that finds it)
-  const bool upfront = small && !d_hist0;
+  // every digit's histogram and offsets from one read of the keys, then every pass back to back: small
+  // sorts (refinement rounds) with no host round trip (no single-digit pass is skipped: a skipped small
+  // pass saves less than the readback that finds it), large sorts with one read-back of all digits.
+  // (The large passes used to count the next digit over their tile while looking back: on natural text's
+  // skewed digits that cost ~0.36 ms a pass, English-like 15.7 -> 13.1 ms of passes for +0.8 ms here.)
+  const bool upfront = !d_hist0;
   if (upfront) {
     HK_HIP(hipMemsetAsync(hist, 0, (uint64_t)np * 256 * 8, s));
     {
@@ -599,6 +601,10 @@ int radix_sort_pairs(SortWork& w, KernelTimer& tm, uint64_t* k[2], V* v[2], int 
     }
     k_hist_offsets<<<np, 256, 0, s>>>(hist, w.offs.as<uint64_t>());
     HK_HIP(hipGetLastError());
+    if (!small) {   // large sorts: one read-back finds every single-bucket (skipped) pass
+      HK_HIP(hipMemcpyAsync(w.h_hist, hist, (uint64_t)np * 256 * 8, hipMemcpyDeviceToHost, s));
+      HK_HIP(hipStreamSynchronize(s));
+    }
   } else if (d_hist0) {
     HK_HIP(hipMemcpyAsync(hist, d_hist0, 256 * 8, hipMemcpyDeviceToDevice, s));
   } else {
@@ -615,7 +621,7 @@ int radix_sort_pairs(SortWork& w, KernelTimer& tm, uint64_t* k[2], V* v[2], int 
       HK_HIP(hipStreamSynchronize(s));
     }
     bool trivial = false;
-    for (int d = 0; d < 256 && !upfront; ++d)
+    for (int d = 0; d < 256 && (!upfront || !small); ++d)
       if (w.h_hist[p * 256 + d] == n) trivial = true;
     const bool from_text = src && p == 0;   // builds the keys: never skipped
     if (from_text) trivial = false;
