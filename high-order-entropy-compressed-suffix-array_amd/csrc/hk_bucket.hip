@@ -1187,20 +1187,23 @@ __global__ __launch_bounds__(CP_T, 2) void k_slice_cpart(uint64_t* __restrict__ 
 // only the kept positions (a bit loop: ~1/N of the 16 per sub-tile) and stages them at their final slots.  Each sub-tile of a unit denser than one tile is
 // ranked, reserved and written on its own (non-iid text), as in k_slice_cpart.
 constexpr int SL_G = 8;
+// quarter staging: units of <= 3 sub-tiles keeping <= 3584 records (slices of <= 1/7.5 of T', N >= 8), 37 KiB
+// of LDS, four workgroups per CU; a dense sub-tile is staged in quarters
+constexpr int SL_CAPQ = 3584;
 
 // G: sub-tiles per unit held in registers; CAP: staging capacity (records of one write-out).  CAP =
 // CP_TILE / 2 (N >= 4: units of <= 4 sub-tiles keep ~1/N of their positions) halves the LDS to ~41 KiB,
 // so three workgroups share a CU instead of two (the kernel waits between its DMA, ranking and write
 // phases); a dense sub-tile is then staged in two halves (its positions k < 8, then k >= 8).
 template <bool TRACE = false, int G = SL_G, int CAP = CP_TILE>
-__global__ __launch_bounds__(CP_T, CAP == CP_TILE ? 4 : 6) void k_slice_cpart_reg(uint64_t* __restrict__ kout, uint64_t n,
+__global__ __launch_bounds__(CP_T, CAP == CP_TILE ? 4 : CAP == CP_TILE / 2 ? 6 : 8) void k_slice_cpart_reg(uint64_t* __restrict__ kout, uint64_t n,
                                                              unsigned long long* __restrict__ cur, uint64_t span,
                                                              TextKeySrc src, SliceSel sl,
                                                              const unsigned long long* __restrict__ skip,
                                                              uint64_t mcap, uint64_t* __restrict__ trace = nullptr) {
   constexpr int T = CP_T;
   static_assert((uint64_t)G * SL_SUB + 64 <= (uint64_t)(CAP + 8) * 8, "the unit's text image fits the staging");
-  static_assert(CAP == CP_TILE || CAP == CP_TILE / 2, "full or half staging");
+  static_assert(CAP == CP_TILE || CAP == CP_TILE / 2 || CAP == SL_CAPQ, "full, half or quarter staging");
   __shared__ uint64_t keys[CAP + 8];   // round 1: the unit's text image (<= G sub-tiles + 64 B)
   __shared__ uint8_t sdg[CAP];
   __shared__ uint32_t tg[CP_NAM], cnt[CP_NAM], wsum[CP_NAM / 64];
@@ -1383,13 +1386,13 @@ __global__ __launch_bounds__(CP_T, CAP == CP_TILE ? 4 : 6) void k_slice_cpart_re
   }
   // dense unit: each sub-tile (half staging: each half of a sub-tile) counted, reserved, staged and written on
   // its own (ranks by a second round of atomics, as the fast path: no per-position rank registers)
-  constexpr int PARTS = CAP == CP_TILE ? 1 : 2;
+  constexpr int PARTS = CAP == CP_TILE ? 1 : CAP >= CP_TILE / 2 ? 2 : 4;
 #pragma unroll
   for (int st = 0; st < G; ++st) {   // (unrolled: c[st] / msk[st] stay register-resident)
     if ((uint32_t)st >= nsub) break;   // uniform
 #pragma unroll
     for (int part = 0; part < PARTS; ++part) {
-      const uint32_t pm = PARTS == 1 ? msk[st] : (msk[st] & (part ? 0xFF00u : 0x00FFu));
+      const uint32_t pm = msk[st] & (((1u << (16 / PARTS)) - 1u) << (16 / PARTS * part));
       __syncthreads();   // the previous write-out has read keys / tg; counters free
       cnt[tid] = 0;
       __syncthreads();
@@ -1440,6 +1443,9 @@ __global__ __launch_bounds__(CP_T, CAP == CP_TILE ? 4 : 6) void k_slice_cpart_re
 // keeps each kept position's slice (2 bits) next to the packed codes.  Then, slice by slice, the reserve /
 // round 2 / write-out of k_slice_cpart_reg, into the slice's own cursor rows and output.
 constexpr int FS_N = 4;
+// staging of one slice's records of a unit: ~1/4 of <= 3 sub-tiles (6144 for iid text) + margin; 67 KiB of
+// LDS in all, two workgroups per CU (a full tile's 81 KiB allowed one); a dense unit is staged by half sub-tiles
+constexpr int FS_CAP = 6656;
 struct FusedSel {
   uint64_t* kout[FS_N];
   unsigned long long* cur[FS_N];   // [span][CP_NAM] cursor rows of each slice's pre-pass
@@ -1455,8 +1461,9 @@ template <int G>
 __global__ __launch_bounds__(CP_T, 4) void k_slice_cpart_fused(uint64_t n, uint64_t span, TextKeySrc src, SliceSel sl,
                                                                FusedSel fs, const unsigned long long* __restrict__ skip) {
   constexpr int T = CP_T;
-  __shared__ uint64_t keys[CP_TILE + 8];   // round 1: the unit's text image; then the staged records
-  __shared__ uint8_t sdg[CP_TILE];
+  static_assert((uint64_t)G * SL_SUB + 64 <= (uint64_t)(FS_CAP + 8) * 8, "the unit's text image fits the staging");
+  __shared__ uint64_t keys[FS_CAP + 8];   // round 1: the unit's text image; then the staged records
+  __shared__ uint8_t sdg[FS_CAP];
   __shared__ uint32_t cnt[FS_N * CP_NAM / 2];   // u16 digit counters, two per word
   __shared__ uint32_t tg[CP_NAM], wsum[CP_NAM / 64];
   __shared__ uint16_t LP[256];
@@ -1577,7 +1584,7 @@ __global__ __launch_bounds__(CP_T, 4) void k_slice_cpart_fused(uint64_t n, uint6
       tg[tid] = carry + inc - cu;
     };
     auto write_out = [&](uint32_t cnt_tile, uint32_t hi256) {
-      for (int i = 0; i < CP_I; ++i) {
+      for (int i = 0; i < FS_CAP / T; ++i) {
         const uint32_t q = (uint32_t)i * T + tid;
         if (q < cnt_tile) {
           const uint32_t d = (uint32_t)sdg[q] | (q >= hi256 ? 256u : 0u);
@@ -1592,7 +1599,7 @@ __global__ __launch_bounds__(CP_T, 4) void k_slice_cpart_fused(uint64_t n, uint6
     scan(cu, total);
     __syncthreads();   // every count read
     clear_mine();
-    if (total <= (uint32_t)CP_TILE) {
+    if (total <= (uint32_t)FS_CAP) {
       const unsigned long long resv = cu ? atomicAdd(&row[tid], (unsigned long long)cu) : 0ull;
       __syncthreads();
 #pragma unroll
@@ -1609,11 +1616,11 @@ __global__ __launch_bounds__(CP_T, 4) void k_slice_cpart_fused(uint64_t n, uint6
           const uint32_t d2 = record_at(st, k2, rec2);
           uint32_t f = tg[d] + rank(d);
           uint32_t f2 = two ? tg[d2] + rank(d2) : 0u;
-          f = f < (uint32_t)CP_TILE ? f : (uint32_t)CP_TILE - 1;   // (only a count mismatch overruns)
+          f = f < (uint32_t)FS_CAP ? f : (uint32_t)FS_CAP - 1;   // (only a count mismatch overruns)
           keys[f] = rec;
           sdg[f] = (uint8_t)d;
           if (two) {
-            f2 = f2 < (uint32_t)CP_TILE ? f2 : (uint32_t)CP_TILE - 1;
+            f2 = f2 < (uint32_t)FS_CAP ? f2 : (uint32_t)FS_CAP - 1;
             keys[f2] = rec2;
             sdg[f2] = (uint8_t)d2;
           }
@@ -1628,12 +1635,15 @@ __global__ __launch_bounds__(CP_T, 4) void k_slice_cpart_fused(uint64_t n, uint6
       write_out(total, hi256);
       continue;
     }
-    // dense unit for this slice: each sub-tile counted, reserved, staged and written on its own
+    // dense unit for this slice: each half sub-tile counted, reserved, staged and written on its own
 #pragma unroll
     for (int st = 0; st < G; ++st) {
       if ((uint32_t)st >= nsub) break;   // uniform
+#pragma unroll
+     for (int part = 0; part < 2; ++part) {
+      const uint32_t pm = kept(st) & (part ? 0xFFFF0000u : 0x0000FFFFu);   // positions k >= 8 / k < 8
       __syncthreads();   // the previous write-out has read keys / tg; counters clear
-      for (uint32_t m = kept(st); m; m &= m - 1) {
+      for (uint32_t m = pm; m; m &= m - 1) {
         uint64_t rec;
         const uint32_t d = record_at(st, __builtin_ctz(m) >> 1, rec);
         atomicAdd(&cnt[(db + d) >> 1], 1u << (16u * ((db + d) & 1u)));
@@ -1646,7 +1656,7 @@ __global__ __launch_bounds__(CP_T, 4) void k_slice_cpart_fused(uint64_t n, uint6
       __syncthreads();
       clear_mine();
       __syncthreads();
-      for (uint32_t m = kept(st); m; m &= m - 1) {
+      for (uint32_t m = pm; m; m &= m - 1) {
         uint64_t rec;
         const uint32_t d = record_at(st, __builtin_ctz(m) >> 1, rec);
         const uint32_t f = tg[d] + rank(d);
@@ -1662,6 +1672,7 @@ __global__ __launch_bounds__(CP_T, 4) void k_slice_cpart_fused(uint64_t n, uint6
       write_out(tot, hi256);
       __syncthreads();
       clear_mine();
+     }
     }
   }
 }
@@ -2533,6 +2544,7 @@ struct SlicePlan {
   bool packed = false;
   bool reg = false;   // radix 2^2 packed records with a perm-table byte field: the register kernels
   bool half = false;  // register pass A with half staging (three workgroups per CU; slices of <= 1/6 of T')
+  bool quarter = false;   // ... quarter staging (four per CU; slices of <= 1/7.5 of T')
   PkGeom pg;
   int uhb = 0;
 };
@@ -2772,7 +2784,10 @@ static int cursor_partition_slice(Index& ix, const SlicePlan& P, const TextKeySr
         DevBuf tb;
         tb.ensure((uint64_t)grid * 64 + 64);
         HK_HIP(hipMemsetAsync(tb.p, 0, (uint64_t)grid * 64, s));
-        if (P.half)
+        if (P.quarter)
+          k_slice_cpart_reg<true, 3, SL_CAPQ><<<grid, CP_T, 0, s>>>(kp[outA], n, d_curA, span, tks2, sl, skip, m,
+                                                                   tb.as<uint64_t>());
+        else if (P.half)
           k_slice_cpart_reg<true, 4, CP_TILE / 2><<<grid, CP_T, 0, s>>>(kp[outA], n, d_curA, span, tks2, sl, skip, m,
                                                                        tb.as<uint64_t>());
         else
@@ -2791,7 +2806,9 @@ static int cursor_partition_slice(Index& ix, const SlicePlan& P, const TextKeySr
           fprintf(stderr, "[slice_cpart_reg trace] %llu units, mean cycles: round 1 %.0f, count+reserve %.0f, "
                   "round 2 %.0f, write %.0f\n", (unsigned long long)nw, acc[0] / nw, acc[1] / nw, acc[2] / nw, acc[3] / nw);
       } else {
-        if (P.half)
+        if (P.quarter)
+          k_slice_cpart_reg<false, 3, SL_CAPQ><<<grid, CP_T, 0, s>>>(kp[outA], n, d_curA, span, tks2, sl, skip, m);
+        else if (P.half)
           k_slice_cpart_reg<false, 4, CP_TILE / 2><<<grid, CP_T, 0, s>>>(kp[outA], n, d_curA, span, tks2, sl, skip, m);
         else
           k_slice_cpart_reg<<<grid, CP_T, 0, s>>>(kp[outA], n, d_curA, span, tks2, sl, skip, m);
@@ -3108,7 +3125,10 @@ void build_slice_keyed(Index& ix, uint32_t c_lo, uint32_t c_hi, uint64_t m) {
     if (g > (P.reg ? (uint32_t)SL_G : 64u)) g = P.reg ? (uint32_t)SL_G : 64u;   // register kernel: <= SL_G
     // a slice of <= 1/6 of the text (N >= 6 ranks): half staging, units of <= 4 sub-tiles keeping ~0.45 of
     // a full tile, so three workgroups share a CU
-    if (P.reg && ratio >= 6.0) {
+    if (P.reg && ratio >= 7.5) {
+      P.quarter = true;
+      g = std::min<uint32_t>(3, (uint32_t)std::floor(0.42 * ratio));   // ~3072 of 3584 records at N = 8
+    } else if (P.reg && ratio >= 6.0) {
       P.half = true;
       g = std::min<uint32_t>(4, (uint32_t)std::floor(0.45 * ratio));
     }
