@@ -1209,7 +1209,7 @@ __global__ __launch_bounds__(CP_T, CAP == CP_TILE ? 4 : CAP == CP_TILE / 2 ? 6 :
   __shared__ uint32_t tg[CP_NAM], cnt[CP_NAM], wsum[CP_NAM / 64];
   __shared__ uint16_t LP[256];
   __shared__ uint64_t SK[72];
-  const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6);   // (wv in an SGPR)
   if (skip && *skip) return;   // the pre-pass counters overflowed: recounted, then relaunched
   const uint64_t U = (uint64_t)SL_SUB * sl.g;
   const uint32_t per = (uint32_t)(span / U), gx = blockIdx.x & 7u, k8 = blockIdx.x >> 3;
