@@ -879,8 +879,8 @@ def spawn_ranks(argv, world: int) -> dict:
 def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=3)
-    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--text-bytes", type=int, default=1 << 30, help="text symbols per GPU (before '$')")
     ap.add_argument("--sigma", type=int, default=4, choices=(4, 95, 256), help="alphabet of the headline text")
     ap.add_argument("--seed", type=int, default=2)
